@@ -1,0 +1,155 @@
+/*
+ * swimhip.h — C ABI of libswimhip, the MI355X SWIM membership engine.
+ *
+ * This header is the drop-in boundary. The reference has no SPI. Its hot path sits behind constructor-injected
+ * interfaces wired in ClusterImpl.join0 (cluster/src/main/java/io/scalecube/cluster/ClusterImpl.java:85-152):
+ *   FailureDetector    (cluster/.../fdetector/FailureDetector.java:12-25)     start/stop/listen
+ *   GossipProtocol     (cluster/.../gossip/GossipProtocol.java:12-29)        start/stop/spread/listen
+ *   MembershipProtocol (cluster/.../membership/MembershipProtocol.java:14-65)  start/stop/listen/members/member
+ *   MetadataStore      (cluster/.../metadata/MetadataStore.java:11-67)
+ *   Transport          (transport/.../Transport.java:74-135)                 send/requestResponse/listen
+ * One swim_handle simulates N members, each one a full FD + gossip + membership + metadata stack. The handle replaces
+ * those five objects for all N members at once. The MembershipEvent flux (ClusterImpl.java:287-294) becomes
+ * swim_drain_events. Configuration is the ClusterConfig field set (ClusterConfig.java:27-36,57).
+ *
+ * Conventions: every call returns 0 on success or a negative SWIM_E* code; swim_last_error() gives details.
+ * The caller owns all buffers. A handle is NOT thread-safe (one host thread per handle, mirroring the single
+ * scheduler per member, ClusterImpl.java:93). Semantics: SEMANTICS.md.
+ */
+#ifndef SWIMHIP_H
+#define SWIMHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SWIM_ABI_VERSION 1u
+
+/* error codes */
+#define SWIM_OK 0
+#define SWIM_EINVAL -1    /* bad argument / config (e.g. pingTimeout >= pingInterval, ClusterConfig.java:413-415) */
+#define SWIM_ENOMEM -2    /* device or host allocation failed */
+#define SWIM_EDEVICE -3   /* HIP / RCCL failure, or no GPU present */
+#define SWIM_ECAPACITY -4 /* a fixed-capacity structure overflowed (gossip slots, pending fetches, arenas) */
+#define SWIM_EUNSUPPORTED -5
+
+/* init_mode */
+#define SWIM_INIT_COLD_JOIN 0u    /* every member joins at tick 0 through the seeds (ClusterImpl.join0) */
+#define SWIM_INIT_PRECONVERGED 1u /* full views, ALIVE inc 0, shuffled lists (SEMANTICS.md §3) */
+
+/* mode */
+#define SWIM_MODE_FULL 0u
+
+/* event types: MembershipEvent.Type (membership/MembershipEvent.java:13-17) */
+#define SWIM_EV_ADDED 0u
+#define SWIM_EV_REMOVED 1u
+#define SWIM_EV_UPDATED 2u
+#define SWIM_META_NONE 0xFFFFFFFFu
+
+/* status codes used by swim_read_row: MemberStatus (membership/MemberStatus.java:6-15); 0 = no row */
+#define SWIM_ST_ABSENT 0u
+#define SWIM_ST_ALIVE 1u
+#define SWIM_ST_SUSPECT 2u
+
+/* flags */
+#define SWIM_FLAG_RECORD_EVENTS 1u /* keep full event records for swim_drain_events (hashes are always kept) */
+
+typedef struct swim_config {
+  uint32_t n_members;
+  uint32_t tick_ms;       /* virtual time per tick; every interval must be a multiple */
+  uint32_t latency_ticks; /* one-way message latency */
+  uint32_t init_mode;
+  uint64_t seed;
+  /* ClusterConfig (ClusterConfig.java:27-36,57) */
+  uint32_t sync_interval_ms;    /* 30000 */
+  uint32_t sync_timeout_ms;     /* 3000 */
+  uint32_t suspicion_mult;      /* 5 */
+  uint32_t ping_interval_ms;    /* 1000 */
+  uint32_t ping_timeout_ms;     /* 500 */
+  uint32_t ping_req_members;    /* 3 */
+  uint32_t gossip_interval_ms;  /* 200 */
+  uint32_t gossip_fanout;       /* 3 */
+  uint32_t gossip_repeat_mult;  /* 3 */
+  uint32_t metadata_timeout_ms; /* 3000 */
+  uint32_t mode;
+  uint32_t flags;
+  uint32_t n_seeds;
+  uint32_t seeds[16]; /* seed member ids (ClusterConfig.seedMembers) */
+  /* engine capacities (0 = default) */
+  uint32_t gossip_slot_cap;   /* concurrent gossip ids */
+  uint32_t pending_fetch_cap; /* concurrent metadata fetches per member */
+  uint32_t event_cap;         /* buffered event records */
+  uint32_t n_gpus;            /* 1 for now */
+  uint32_t device;            /* first HIP device */
+  uint32_t reserved[7];
+} swim_config;
+
+typedef struct swim_event {
+  uint32_t tick;
+  uint32_t observer;
+  uint32_t seq; /* per-observer emission sequence */
+  uint32_t type;
+  uint32_t subject;
+  uint32_t old_meta;
+  uint32_t new_meta;
+  uint32_t pad;
+} swim_event;
+
+/* deterministic op counters; identical on both backends */
+typedef struct swim_counters {
+  uint64_t tick;
+  uint64_t record_compares;   /* R */
+  uint64_t row_writes;        /* W */
+  uint64_t messages;          /* M: non-gossip messages sent */
+  uint64_t gossip_messages;   /* G: GOSSIP_REQ sent */
+  uint64_t events;            /* E */
+  uint64_t messages_lost;     /* sends failed by loss / block / dead destination */
+  uint64_t gossips_created;
+  uint64_t sync_merges;       /* SYNC + SYNC_ACK payloads merged */
+  uint64_t reserved[7];
+} swim_counters;
+
+typedef struct swim_handle swim_handle;
+
+/* fills *cfg with the reference defaults (ClusterConfig.java:27-36,57), tick 100 ms, latency 1 tick */
+void swim_default_config(swim_config* cfg);
+uint32_t swim_abi_version(void);
+
+int swim_create(const swim_config* cfg, swim_handle** out);
+int swim_destroy(swim_handle* h);
+
+/* advance the simulation */
+int swim_step(swim_handle* h, uint32_t n_ticks);
+int swim_run_periods(swim_handle* h, uint32_t n_periods); /* n * pingInterval */
+int swim_sync(swim_handle* h);                            /* wait for queued device work */
+
+/* fault injection, effective from the next tick (NetworkEmulator.java:113-192) */
+int swim_kill(swim_handle* h, uint32_t member);
+int swim_set_default_loss(swim_handle* h, uint32_t loss_percent);
+int swim_set_partition(swim_handle* h, const uint32_t* group_of_member); /* n_members entries */
+int swim_unblock_all(swim_handle* h);
+
+/* readback */
+int swim_current_tick(swim_handle* h, uint64_t* tick);
+/* row of one observer: keys[s] = inc | status<<32 | meta_present<<34 | timer_deadline<<35 (SEMANTICS.md §8) */
+int swim_read_row(swim_handle* h, uint32_t observer, uint64_t* keys_out, size_t cap);
+/* per-observer hashes: out[4*m + {0:row, 1:fd list, 2:gossip list, 3:events}] */
+int swim_state_hash(swim_handle* h, uint64_t* out, size_t cap);
+/* FD pingMembers and gossip remoteMembers lists, plus cursors */
+int swim_read_lists(swim_handle* h, uint32_t observer, uint32_t* fd_out, uint32_t* fd_len, uint32_t* gossip_out,
+                    uint32_t* gossip_len, size_t cap, int32_t* cursors_out /* [pingIdx, remoteIdx] */);
+int swim_drain_events(swim_handle* h, swim_event* out, size_t cap, size_t* n_out);
+int swim_counters_get(swim_handle* h, swim_counters* out);
+const char* swim_last_error(swim_handle* h);
+
+/* the reference's pure helpers, exported for known-answer tests */
+int swim_is_overrides(uint32_t r1_status, uint32_t r1_inc, uint32_t r0_status, uint32_t r0_inc); /* status 3 = DEAD */
+uint32_t swim_ceil_log2(uint32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,1060 @@
+// oracle/swimref.cpp — TEST INFRASTRUCTURE. CPU restatement of the reference's SWIM hot path.
+//
+// This is the oracle, not the product. Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load
+// liboracle_swimref.so, and only as the checker or the timed CPU baseline. It exports the same C ABI as
+// libswimhip (include/swimhip.h), so a parity test can drive both backends through one interface.
+//
+// Shape: one Member object per simulated member. Each holds the fields of FailureDetectorImpl,
+// GossipProtocolImpl, MembershipProtocolImpl and MetadataStoreImpl. Members talk only through explicit Msg
+// objects on an in-memory transport. Loss is applied at the sender, and a failed send errors the caller at once
+// (TransportImpl.java:205-232, NetworkEmulator.java:231-248). requestResponse is a subscription keyed by the
+// correlation id. Gossip keeps real infectedFrom sets. Concurrency and timing follow SEMANTICS.md. Every method
+// cites the Java it restates. Paths are relative to
+// /root/reference/cluster/src/main/java/io/scalecube/cluster/ unless they start with transport/.
+//
+// Parity pin: the reference is Java 8 + Reactor, with no JDK, Maven or jars in this image, so it cannot
+// run here. isOverrides is pinned by MembershipRecordTest.java:34-108 (tests/test_oracle_known_answers.py). ClusterMath
+// is pinned by its closed forms. Event ordering and timing are pinned only by SEMANTICS.md, which makes parity for
+// them "spec-pinned", not reference-pinned.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "../include/swimhip.h"
+#include "rng.h"
+
+using namespace swimref;
+
+namespace {
+
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr uint64_t NEVER = ~0ull;
+
+enum St : uint8_t { ABSENT = 0, ALIVE = 1, SUSPECT = 2, DEAD = 3 };  // MemberStatus.java:6-15 (+absent)
+enum Kind : uint8_t { K_SYNC = 1, K_SYNC_ACK, K_PING, K_PING_REQ, K_PING_ACK, K_GMD_REQ, K_GMD_RESP, K_GOSSIP };
+enum Reason { R_FD, R_GOSSIP, R_SYNC, R_INITIAL, R_TIMEOUT };  // MembershipProtocolImpl.java:54-60
+enum Stream { S_FD_SHUFFLE = 1, S_FD_INSERT = 2, S_PINGREQ = 3, S_GOSSIP_SHUFFLE = 4, S_SYNC_PICK = 5 };
+
+struct Rec {
+  uint8_t st = ABSENT;
+  uint32_t inc = 0;
+  bool operator==(const Rec& o) const { return st == o.st && inc == o.inc; }  // MembershipRecord.java:86-99
+  bool operator!=(const Rec& o) const { return !(*this == o); }
+};
+
+// MembershipRecord.isOverrides (MembershipRecord.java:66-84); r0.st == ABSENT is the `r0 == null` case.
+bool is_overrides(Rec r1, Rec r0) {
+  if (r0.st == ABSENT) return r1.st == ALIVE;
+  if (r0.st == DEAD) return false;
+  if (r1.st == DEAD) return true;
+  if (r1.inc == r0.inc) return (r1.st != r0.st) && (r1.st == SUSPECT);
+  return r1.inc > r0.inc;
+}
+
+uint32_t bitlen(uint32_t n) { return n ? 32u - (uint32_t)__builtin_clz(n) : 0u; }  // ClusterMath.java:133-135
+
+using Payload = std::vector<std::pair<uint32_t, Rec>>;
+
+struct Msg {
+  uint8_t kind = 0;
+  uint32_t src = 0, dst = 0;
+  uint32_t cid_iss = NONE, cid_cnt = 0;                  // correlation id (issuer, counter)
+  uint32_t pd_from = NONE, pd_to = NONE, pd_orig = NONE;  // PingData (fdetector/PingData.java:6-50)
+  uint32_t seq = 0;                                       // syncSeq for SYNC / SYNC_ACK
+  std::shared_ptr<Payload> payload;                       // SyncData (membership/SyncData.java:11-41)
+  uint32_t md_subject = NONE, md_meta = NONE;             // GetMetadataRequest / Response
+  uint64_t gid = 0;                                       // gossip id (origin << 32 | counter)
+  uint32_t slot = 0;                                      // target slot of a GOSSIP_REQ
+  uint32_t g_subj = 0;
+  Rec g_rec;                                              // gossip payload: MembershipRecord
+};
+
+struct Sim;
+
+struct Member {
+  Sim* sim = nullptr;
+  uint32_t id = 0;
+  bool alive = true;
+
+  // MembershipProtocolImpl state (:82-96) + MetadataStoreImpl.membersMetadata
+  std::vector<Rec> table;
+  uint32_t tsize = 0;
+  std::vector<uint32_t> meta;
+  std::map<uint32_t, uint64_t> timers;  // suspicionTimeoutTasks: subject -> deadline tick
+  std::vector<uint32_t> seeds;
+
+  // FailureDetectorImpl state (:47-49)
+  std::vector<uint32_t> ping;
+  int64_t pingIdx = 0;
+  uint64_t fdPeriod = 0;
+  struct Sub {
+    uint32_t cnt;
+    int kind;  // 0 DIRECT, 1 PINGREQ
+    uint32_t helper, target;
+    uint64_t deadline, order;
+  };
+  std::vector<Sub> subs;  // pending requestResponse subscriptions
+  uint64_t subOrder = 0;
+
+  // GossipProtocolImpl state (:47-53), GossipState.java:8-38
+  std::vector<uint32_t> remote;
+  int64_t remoteIdx = -1;
+  uint64_t gPeriod = 0;
+  uint32_t gCounter = 0;
+  struct GState {
+    uint32_t subj;
+    Rec rec;
+    uint64_t infPeriod;
+    std::set<uint32_t> infected;
+  };
+  std::map<uint64_t, GState> gossips;
+
+  // MetadataStoreImpl.fetchMetadata subscriptions (:149-186) + their updateMembership continuation
+  struct Fetch {
+    uint32_t subj;
+    Rec r1;
+    int reason;
+    bool added;
+    uint64_t deadline;
+    int group;
+  };
+  std::map<uint32_t, Fetch> fetches;
+
+  // Mono.whenDelayError over one syncMembership (:456-467); kind 0 = SYNC -> SYNC_ACK, 1 = initial sync
+  struct Group {
+    int kind;
+    uint32_t reply_to, cid_iss, cid_cnt;
+    int remaining;
+    bool error, sealed;
+  };
+  std::map<int, Group> groups;
+  int nextGroup = 0;
+
+  // start0 (:216-251)
+  bool initActive = false, initReceived = false;
+  std::set<uint32_t> initCids;
+  uint64_t initDeadline = NEVER;
+
+  uint64_t nextPing = NEVER, nextGossip = NEVER, nextSync = NEVER;
+  uint32_t cidCnt = 0, syncSeq = 0, evSeq = 0;
+  uint32_t sel[8] = {0};
+  uint64_t evHash = 0;
+
+  // ---- helpers implemented below ----
+  uint32_t draw(int stream);
+  void shuffle(std::vector<uint32_t>& v, int stream);
+  void process(uint64_t k, std::vector<Msg>& inbox);
+  void start(uint64_t k);
+  void send(Msg&& m, uint64_t k, bool gossip = false);
+  bool send_sync(uint8_t kind, uint32_t dst, uint32_t cid_iss, uint32_t cid_cnt, uint64_t k);
+  void emit_event(uint32_t type, uint32_t subj, uint32_t oldm, uint32_t newm, uint64_t k);
+  void on_member_event(uint32_t type, uint32_t subj);
+  void spread(uint32_t subj, Rec rec);
+  void update_membership(uint32_t subj, Rec r1, int reason, int group, uint64_t k);
+  void finish(int group, bool error, uint64_t k);
+  void do_finally(uint32_t subj, Rec r1, int reason);
+  void fetch(uint32_t subj, Rec r1, int reason, bool added, int group, uint64_t k);
+  void sync_membership(const Payload& p, int reason, int group, uint64_t k);
+  void complete_group(int g, uint64_t k);
+  void on_fd_event(uint32_t target, uint8_t status, uint64_t k);
+  void ping_req_step(uint32_t target, uint32_t cnt, uint64_t k);
+  void resolve_subs(uint32_t cnt, uint64_t k);
+  void do_ping(uint64_t k);
+  void do_spread_gossip(uint64_t k);
+  void do_sync(uint64_t k);
+};
+
+struct Sim {
+  swim_config cfg;
+  uint32_t N = 0;
+  uint32_t ping_t = 0, pingTimeout_t = 0, gossip_t = 0, sync_t = 0, syncTimeout_t = 0, md_t = 0, lat = 1;
+  uint32_t seed_lo = 0, seed_hi = 0;
+  uint64_t tick = 0;
+  uint32_t loss = 0;
+  bool partitioned = false;
+  std::vector<uint32_t> group;
+  std::vector<Member> members;
+  std::vector<uint32_t> md_version;  // each member's own metadata version (GET_METADATA_RESP payload)
+  std::vector<std::vector<Msg>> inflight;  // ring indexed by delivery tick % (lat+1)
+  std::vector<swim_event> events;
+  swim_counters ctr;
+  std::string err;
+
+  uint32_t suspicion_ticks(uint32_t size) const {  // ClusterMath.suspicionTimeout (ClusterMath.java:123-125)
+    return cfg.suspicion_mult * bitlen(size) * ping_t;
+  }
+  uint32_t spread_of(uint32_t cluster) const { return cfg.gossip_repeat_mult * bitlen(cluster); }  // :111-113
+  uint32_t sweep_of(uint32_t cluster) const { return 2u * (spread_of(cluster) + 1u); }            // :99-102
+
+  // NetworkEmulator.tryFail (transport/.../NetworkEmulator.java:231-248) + NetworkLinkSettings.evaluateLoss (:54-57)
+  bool blocked(uint32_t src, uint32_t dst) const {
+    if (!members[dst].alive) return true;
+    if (partitioned && group[src] != group[dst]) return true;
+    return false;
+  }
+  bool lost(uint8_t kind, uint32_t src, uint32_t dst, uint64_t k, uint32_t aux, uint32_t id) const {
+    if (blocked(src, dst)) return true;
+    if (loss == 0) return false;
+    if (loss >= 100) return true;
+    P4 r = philox4x32_10(src, dst, (uint32_t)k, id, seed_lo ^ (SALT_LOSS_BASE + kind), seed_hi ^ (aux * 0x9E3779B9u));
+    return next_int(r.v[0], 100) < loss;
+  }
+  bool lost_gossip(uint32_t src, uint32_t dst, uint64_t k, uint32_t slot, uint64_t gid) const {
+    if (blocked(src, dst)) return true;
+    if (loss == 0) return false;
+    if (loss >= 100) return true;
+    P4 r = philox4x32_10(src, (uint32_t)k ^ ((slot >> 2) << 31), (uint32_t)(gid >> 32), (uint32_t)gid,
+                         seed_lo ^ SALT_LOSS_GOSSIP, seed_hi);
+    return next_int(r.v[slot & 3], 100) < loss;
+  }
+  uint32_t init_draw(uint32_t m, uint32_t what, uint32_t i) const {
+    return philox4x32_10(m, what, i, 0, seed_lo ^ SALT_INIT, seed_hi).v[0];
+  }
+  void run_tick();
+};
+
+// ---------------------------------------------------------------------------------------------------------------
+// selector (SEMANTICS.md §2)
+uint32_t Member::draw(int stream) {
+  uint32_t c = sel[stream]++;
+  return philox4x32_10(id, (uint32_t)stream, c, 0, sim->seed_lo ^ SALT_SEL, sim->seed_hi).v[0];
+}
+// Collections.shuffle(list, rnd): for i = size..2: swap(i-1, nextInt(i))
+void Member::shuffle(std::vector<uint32_t>& v, int stream) {
+  for (size_t i = v.size(); i > 1; --i) {
+    uint32_t j = next_int(draw(stream), (uint32_t)i);
+    std::swap(v[i - 1], v[j]);
+  }
+}
+
+// transport.send (transport/.../TransportImpl.java:194-202): enqueue for delivery at k + lat
+void Member::send(Msg&& m, uint64_t k, bool gossip) {
+  (void)gossip;
+  Sim& s = *sim;
+  s.inflight[(k + s.lat) % (s.lat + 1)].push_back(std::move(m));
+}
+
+// prepareSyncDataMsg (:446-454) + transport.send; returns false when the send failed
+bool Member::send_sync(uint8_t kind, uint32_t dst, uint32_t cid_iss, uint32_t cid_cnt, uint64_t k) {
+  Sim& s = *sim;
+  uint32_t seq = syncSeq++;
+  s.ctr.messages++;
+  if (s.lost(kind, id, dst, k, id, seq)) {
+    s.ctr.messages_lost++;
+    return false;
+  }
+  Msg m;
+  m.kind = kind;
+  m.src = id;
+  m.dst = dst;
+  m.cid_iss = cid_iss;
+  m.cid_cnt = cid_cnt;
+  m.seq = seq;
+  auto p = std::make_shared<Payload>();
+  p->reserve(tsize);
+  for (uint32_t subj = 0; subj < s.N; ++subj)
+    if (table[subj].st != ABSENT) p->emplace_back(subj, table[subj]);
+  m.payload = std::move(p);
+  send(std::move(m), k);
+  return true;
+}
+
+// sink.next(MembershipEvent) (:548-584) -> user stream, FailureDetectorImpl.onMemberEvent, GossipProtocolImpl.onMemberEvent
+void Member::emit_event(uint32_t type, uint32_t subj, uint32_t oldm, uint32_t newm, uint64_t k) {
+  Sim& s = *sim;
+  uint32_t seq = evSeq++;
+  evHash = hpair(evHash, ((uint64_t)k << 32) | ((uint64_t)type << 30) | subj);
+  evHash = hpair(evHash, ((uint64_t)oldm << 32) | newm);
+  s.ctr.events++;
+  if (s.cfg.flags & SWIM_FLAG_RECORD_EVENTS) {
+    swim_event e{(uint32_t)k, id, seq, type, subj, oldm, newm, 0};
+    s.events.push_back(e);
+  }
+  on_member_event(type, subj);
+}
+
+void Member::on_member_event(uint32_t type, uint32_t subj) {
+  // FailureDetectorImpl.onMemberEvent (:321-332)
+  if (type == SWIM_EV_REMOVED) {
+    auto it = std::find(ping.begin(), ping.end(), subj);
+    if (it != ping.end()) ping.erase(it);
+  }
+  if (type == SWIM_EV_ADDED) {
+    size_t sz = ping.size();
+    size_t idx = sz > 0 ? next_int(draw(S_FD_INSERT), (uint32_t)sz) : 0;
+    ping.insert(ping.begin() + (long)idx, subj);
+  }
+  // GossipProtocolImpl.onMemberEvent (:185-193)
+  if (type == SWIM_EV_REMOVED) {
+    auto it = std::find(remote.begin(), remote.end(), subj);
+    if (it != remote.end()) remote.erase(it);
+  }
+  if (type == SWIM_EV_ADDED) remote.push_back(subj);
+}
+
+// GossipProtocolImpl.spread -> createAndPutGossip (:124-128,163-169)
+void Member::spread(uint32_t subj, Rec rec) {
+  uint64_t gid = ((uint64_t)id << 32) | gCounter++;
+  GState g;
+  g.subj = subj;
+  g.rec = rec;
+  g.infPeriod = gPeriod;
+  gossips.emplace(gid, std::move(g));
+  sim->ctr.gossips_created++;
+}
+
+// MembershipProtocolImpl.updateMembership (:475-541)
+void Member::update_membership(uint32_t subj, Rec r1, int reason, int group, uint64_t k) {
+  Sim& s = *sim;
+  Rec r0 = table[subj];
+  if (!is_overrides(r1, r0)) return;  // :483-485 (completes empty; no doFinally)
+  if (subj == id) {                   // :488-509 local member: refute with a higher incarnation
+    Rec r2{r0.st, std::max(r0.inc, r1.inc) + 1};
+    table[id] = r2;
+    s.ctr.row_writes++;
+    spread(id, r2);
+    return;
+  }
+  if (r1.st == DEAD) {  // :512-516
+    table[subj] = Rec{};
+    tsize--;
+  } else {
+    if (r0.st == ABSENT) tsize++;
+    table[subj] = r1;
+  }
+  s.ctr.row_writes++;
+  if (r1.st == SUSPECT) {  // :519-523, scheduleSuspicionTimeoutTask (:597-606) computeIfAbsent
+    if (!timers.count(subj)) timers[subj] = k + s.suspicion_ticks(tsize);
+  } else {
+    timers.erase(subj);  // cancelSuspicionTimeoutTask (:590-595)
+  }
+  // emitMembershipEvent (:543-588)
+  if (r1.st == DEAD) {
+    uint32_t oldm = meta[subj];  // metadataStore.removeMetadata (MetadataStoreImpl.java:135-146)
+    meta[subj] = NONE;
+    emit_event(SWIM_EV_REMOVED, subj, oldm, NONE, k);
+    finish(group, false, k);
+    do_finally(subj, r1, reason);
+    return;
+  }
+  if (r0.st == ABSENT && r1.st == ALIVE) {
+    fetch(subj, r1, reason, true, group, k);
+    return;
+  }
+  if (r0.st != ABSENT && r0.inc < r1.inc) {
+    fetch(subj, r1, reason, false, group, k);
+    return;
+  }
+  finish(group, false, k);
+  do_finally(subj, r1, reason);
+}
+
+// doFinally of updateMembership (:526-539): spread r1 unless it came from gossip or the initial sync
+void Member::do_finally(uint32_t subj, Rec r1, int reason) {
+  if (reason != R_GOSSIP && reason != R_INITIAL) spread(subj, r1);
+}
+
+// one inner Mono of Mono.whenDelayError terminated (synchronously or later)
+void Member::finish(int g, bool error, uint64_t k) {
+  if (g < 0) return;
+  auto it = groups.find(g);
+  if (it == groups.end()) return;
+  Group& gr = it->second;
+  if (error) gr.error = true;
+  if (gr.sealed && gr.remaining == 0) complete_group(g, k);
+}
+
+void Member::complete_group(int g, uint64_t k) {
+  Group gr = groups[g];
+  groups.erase(g);
+  if (gr.kind == 0) {
+    // onSync doOnSuccess (:351-365): SYNC_ACK with the post-merge table, only if no error
+    if (!gr.error) send_sync(K_SYNC_ACK, gr.reply_to, gr.cid_iss, gr.cid_cnt, k);
+  } else {
+    // start0 doFinally (:244-248): schedulePeriodicSync
+    initActive = false;
+    nextSync = k + sim->sync_t;
+  }
+}
+
+// MetadataStoreImpl.fetchMetadata (:149-186)
+void Member::fetch(uint32_t subj, Rec r1, int reason, bool added, int group, uint64_t k) {
+  Sim& s = *sim;
+  uint32_t cnt = cidCnt++;
+  s.ctr.messages++;
+  if (s.lost(K_GMD_REQ, id, subj, k, id, cnt)) {  // requestResponse send error -> sink.error
+    s.ctr.messages_lost++;
+    if (group >= 0) groups[group].error = true;  // error propagates to whenDelayError
+    do_finally(subj, r1, reason);
+    return;
+  }
+  Msg m;
+  m.kind = K_GMD_REQ;
+  m.src = id;
+  m.dst = subj;
+  m.cid_iss = id;
+  m.cid_cnt = cnt;
+  m.md_subject = subj;
+  send(std::move(m), k);
+  fetches[cnt] = Fetch{subj, r1, reason, added, k + s.md_t, group};
+  if (group >= 0) groups[group].remaining++;
+}
+
+// syncMembership (:456-467): eager filter of differing records, then sequential updateMembership
+void Member::sync_membership(const Payload& p, int reason, int group, uint64_t k) {
+  Sim& s = *sim;
+  s.ctr.record_compares += p.size();
+  s.ctr.sync_merges++;
+  std::vector<std::pair<uint32_t, Rec>> diff;
+  for (auto& e : p)
+    if (e.second != table[e.first]) diff.push_back(e);
+  for (auto& e : diff) update_membership(e.first, e.second, reason, group, k);
+}
+
+// onFailureDetectorEvent (:370-398)
+void Member::on_fd_event(uint32_t target, uint8_t status, uint64_t k) {
+  Rec r0 = table[target];
+  if (r0.st == ABSENT) return;
+  if (r0.st == status) return;
+  if (status == ALIVE) {
+    send_sync(K_SYNC, target, NONE, 0, k);
+  } else {
+    sim->ctr.record_compares++;
+    update_membership(target, Rec{SUSPECT, r0.inc}, R_FD, -1, k);
+  }
+}
+
+// doPing error branch (:159-175) + selectPingReqMembers (:349-361) + doPingReq (:178-213)
+void Member::ping_req_step(uint32_t target, uint32_t cnt, uint64_t k) {
+  Sim& s = *sim;
+  std::vector<uint32_t> helpers;
+  uint32_t kreq = s.cfg.ping_req_members;
+  if (kreq > 0) {
+    std::vector<uint32_t> cand(ping);
+    auto it = std::find(cand.begin(), cand.end(), target);
+    if (it != cand.end()) cand.erase(it);
+    if (!cand.empty()) {
+      uint32_t n = (uint32_t)cand.size();
+      uint32_t kk = std::min(kreq, n);
+      for (uint32_t i = 0; i < kk; ++i) {  // k forward Fisher-Yates steps (SEMANTICS.md §2)
+        uint32_t j = i + next_int(draw(S_PINGREQ), n - i);
+        std::swap(cand[i], cand[j]);
+      }
+      helpers.assign(cand.begin(), cand.begin() + kk);
+    }
+  }
+  int timeLeft = (int)s.ping_t - (int)s.pingTimeout_t;
+  if (timeLeft <= 0 || helpers.empty()) {
+    on_fd_event(target, SUSPECT, k);
+    return;
+  }
+  for (uint32_t h : helpers) {
+    s.ctr.messages++;
+    if (s.lost(K_PING_REQ, id, h, k, id, cnt)) {
+      s.ctr.messages_lost++;
+      on_fd_event(target, SUSPECT, k);
+      continue;
+    }
+    Msg m;
+    m.kind = K_PING_REQ;
+    m.src = id;
+    m.dst = h;
+    m.cid_iss = id;
+    m.cid_cnt = cnt;
+    m.pd_from = id;
+    m.pd_to = target;
+    send(std::move(m), k);
+    subs.push_back(Sub{cnt, 1, h, target, k + (uint64_t)timeLeft, subOrder++});
+  }
+}
+
+// every pending subscription on cid `cnt` takes the first matching inbound message (TransportImpl.java:205-232)
+void Member::resolve_subs(uint32_t cnt, uint64_t k) {
+  std::vector<Sub> hit;
+  std::vector<Sub> keep;
+  for (auto& sb : subs) (sb.cnt == cnt ? hit : keep).push_back(sb);
+  if (hit.empty()) return;
+  subs.swap(keep);
+  std::sort(hit.begin(), hit.end(), [](const Sub& a, const Sub& b) { return a.order < b.order; });
+  for (auto& sb : hit) on_fd_event(sb.target, ALIVE, k);  // publishPingResult(ALIVE) (:157,202)
+}
+
+// doPing (:128-176) + selectPingMember (:338-347)
+void Member::do_ping(uint64_t k) {
+  Sim& s = *sim;
+  fdPeriod++;
+  if (ping.empty()) return;
+  if (pingIdx >= (int64_t)ping.size()) {
+    pingIdx = 0;
+    shuffle(ping, S_FD_SHUFFLE);
+  }
+  uint32_t target = ping[(size_t)pingIdx++];
+  uint32_t cnt = cidCnt++;
+  s.ctr.messages++;
+  if (s.lost(K_PING, id, target, k, id, cnt)) {
+    s.ctr.messages_lost++;
+    ping_req_step(target, cnt, k);
+    return;
+  }
+  Msg m;
+  m.kind = K_PING;
+  m.src = id;
+  m.dst = target;
+  m.cid_iss = id;
+  m.cid_cnt = cnt;
+  m.pd_from = id;
+  m.pd_to = target;
+  send(std::move(m), k);
+  subs.push_back(Sub{cnt, 0, NONE, target, k + s.pingTimeout_t, subOrder++});
+}
+
+// doSpreadGossip (:139-157), selectGossipMembers (:252-273), selectGossipsToSend (:239-250), sweepGossips (:283-308)
+void Member::do_spread_gossip(uint64_t k) {
+  Sim& s = *sim;
+  uint64_t period = gPeriod++;
+  if (gossips.empty()) return;
+  std::vector<uint32_t> targets;
+  uint32_t f = s.cfg.gossip_fanout;
+  if (remote.size() < f) {
+    targets = remote;
+  } else {
+    if (remoteIdx < 0 || remoteIdx + (int64_t)f > (int64_t)remote.size()) {
+      shuffle(remote, S_GOSSIP_SHUFFLE);
+      remoteIdx = 0;
+    }
+    targets.assign(remote.begin() + remoteIdx, remote.begin() + remoteIdx + f);
+    remoteIdx += f;
+  }
+  uint32_t cluster = (uint32_t)remote.size() + 1;
+  uint64_t sp = s.spread_of(cluster);
+  for (uint32_t slot = 0; slot < targets.size(); ++slot) {
+    uint32_t t = targets[slot];
+    for (auto& kv : gossips) {
+      GState& g = kv.second;
+      if (g.infPeriod + sp < period) continue;
+      if (g.infected.count(t)) continue;
+      s.ctr.gossip_messages++;
+      if (s.lost_gossip(id, t, k, slot, kv.first)) {
+        s.ctr.messages_lost++;
+        continue;
+      }
+      Msg m;
+      m.kind = K_GOSSIP;
+      m.src = id;
+      m.dst = t;
+      m.gid = kv.first;
+      m.slot = slot;
+      m.g_subj = g.subj;
+      m.g_rec = g.rec;
+      send(std::move(m), k, true);
+    }
+  }
+  uint64_t sw = s.sweep_of(cluster);
+  for (auto it = gossips.begin(); it != gossips.end();) {
+    if (period > it->second.infPeriod + sw)
+      it = gossips.erase(it);
+    else
+      ++it;
+  }
+}
+
+// doSync (:298-314) + selectSyncAddress (:410-421)
+void Member::do_sync(uint64_t k) {
+  Sim& s = *sim;
+  std::vector<uint32_t> cand;
+  {
+    std::set<uint32_t> set(seeds.begin(), seeds.end());
+    for (uint32_t subj = 0; subj < s.N; ++subj)
+      if (subj != id && table[subj].st != ABSENT) set.insert(subj);
+    cand.assign(set.begin(), set.end());
+  }
+  if (cand.empty()) return;
+  uint32_t i = next_int(draw(S_SYNC_PICK), (uint32_t)cand.size());
+  send_sync(K_SYNC, cand[i], NONE, 0, k);
+}
+
+// ClusterImpl.join0 (:85-152) -> MembershipProtocolImpl.start0 (:216-251), COLD_JOIN only
+void Member::start(uint64_t k) {
+  Sim& s = *sim;
+  nextPing = k + s.ping_t;
+  nextGossip = k + s.gossip_t;
+  if (seeds.empty()) {
+    nextSync = k + s.sync_t;
+    return;
+  }
+  initActive = true;
+  initDeadline = k + s.syncTimeout_t;
+  uint32_t failed = 0;
+  for (uint32_t sd : seeds) {
+    uint32_t cnt = cidCnt++;
+    initCids.insert(cnt);
+    if (!send_sync(K_SYNC, sd, id, cnt, k)) failed++;
+  }
+  if (failed == seeds.size()) {  // Flux.mergeDelayError of all-failed requests errors -> doFinally
+    initActive = false;
+    nextSync = k + s.sync_t;
+  }
+}
+
+static bool fd_less(const Msg& a, const Msg& b) {
+  if (a.cid_iss != b.cid_iss) return a.cid_iss < b.cid_iss;
+  if (a.cid_cnt != b.cid_cnt) return a.cid_cnt < b.cid_cnt;
+  if (a.kind != b.kind) return a.kind < b.kind;
+  return a.src < b.src;
+}
+
+void Member::process(uint64_t k, std::vector<Msg>& inbox) {
+  Sim& s = *sim;
+  std::vector<Msg*> syncm, fdm, mdm, gm;
+  for (auto& m : inbox) {
+    switch (m.kind) {
+      case K_SYNC:
+      case K_SYNC_ACK: syncm.push_back(&m); break;
+      case K_PING:
+      case K_PING_REQ:
+      case K_PING_ACK: fdm.push_back(&m); break;
+      case K_GMD_REQ:
+      case K_GMD_RESP: mdm.push_back(&m); break;
+      default: gm.push_back(&m);
+    }
+  }
+  // ---- P1 SYNC / SYNC_ACK (onMessage :320-331, onSync :346-367, onSyncAck :337-343) ----
+  std::sort(syncm.begin(), syncm.end(), [](Msg* a, Msg* b) { return a->src != b->src ? a->src < b->src : a->seq < b->seq; });
+  for (Msg* m : syncm) {
+    if (m->kind == K_SYNC) {
+      int g = nextGroup++;
+      groups[g] = Group{0, m->src, m->cid_iss, m->cid_cnt, 0, false, false};
+      sync_membership(*m->payload, R_SYNC, g, k);
+      groups[g].sealed = true;
+      finish(g, false, k);
+    } else if (m->cid_iss == NONE) {
+      sync_membership(*m->payload, R_SYNC, -1, k);
+    } else if (m->cid_iss == id && initActive && !initReceived && initCids.count(m->cid_cnt)) {
+      initReceived = true;  // Flux.mergeDelayError(...).take(1) (:239-243)
+      int g = nextGroup++;
+      groups[g] = Group{1, NONE, NONE, 0, 0, false, false};
+      sync_membership(*m->payload, R_INITIAL, g, k);
+      groups[g].sealed = true;
+      finish(g, false, k);
+    }
+  }
+  // ---- P2 FD (onMessage :219-227) ----
+  std::sort(fdm.begin(), fdm.end(), [](Msg* a, Msg* b) { return fd_less(*a, *b); });
+  for (Msg* m : fdm) {
+    if (m->kind == K_PING) {  // onPing (:230-255)
+      if (m->pd_to != id) continue;
+      s.ctr.messages++;
+      if (s.lost(K_PING_ACK, id, m->pd_from, k, m->cid_iss, m->cid_cnt)) {
+        s.ctr.messages_lost++;
+        continue;
+      }
+      Msg a = *m;
+      a.kind = K_PING_ACK;
+      a.src = id;
+      a.dst = m->pd_from;
+      send(std::move(a), k);
+    } else if (m->kind == K_PING_REQ) {  // onPingReq (:258-284): transit ping
+      s.ctr.messages++;
+      if (s.lost(K_PING, id, m->pd_to, k, m->cid_iss, m->cid_cnt)) {
+        s.ctr.messages_lost++;
+        continue;
+      }
+      Msg p;
+      p.kind = K_PING;
+      p.src = id;
+      p.dst = m->pd_to;
+      p.cid_iss = m->cid_iss;
+      p.cid_cnt = m->cid_cnt;
+      p.pd_from = id;
+      p.pd_to = m->pd_to;
+      p.pd_orig = m->pd_from;
+      send(std::move(p), k);
+    } else if (m->pd_orig != NONE) {  // onTransitPingAck (:290-315)
+      s.ctr.messages++;
+      if (s.lost(K_PING_ACK, id, m->pd_orig, k, m->cid_iss, m->cid_cnt)) {
+        s.ctr.messages_lost++;
+        continue;
+      }
+      Msg a;
+      a.kind = K_PING_ACK;
+      a.src = id;
+      a.dst = m->pd_orig;
+      a.cid_iss = m->cid_iss;
+      a.cid_cnt = m->cid_cnt;
+      a.pd_from = m->pd_orig;
+      a.pd_to = m->pd_to;
+      send(std::move(a), k);
+    } else if (m->cid_iss == id) {  // response for a pending requestResponse
+      resolve_subs(m->cid_cnt, k);
+    }
+  }
+  // ---- P3 metadata (MetadataStoreImpl.onMessage :192-196, onMetadataRequest :202-241) ----
+  std::sort(mdm.begin(), mdm.end(), [](Msg* a, Msg* b) { return fd_less(*a, *b); });
+  for (Msg* m : mdm) {
+    if (m->kind == K_GMD_REQ) {
+      if (m->md_subject != id) continue;
+      s.ctr.messages++;
+      if (s.lost(K_GMD_RESP, id, m->src, k, m->cid_iss, m->cid_cnt)) {
+        s.ctr.messages_lost++;
+        continue;
+      }
+      Msg r;
+      r.kind = K_GMD_RESP;
+      r.src = id;
+      r.dst = m->src;
+      r.cid_iss = m->cid_iss;
+      r.cid_cnt = m->cid_cnt;
+      r.md_subject = id;
+      r.md_meta = s.md_version[id];
+      send(std::move(r), k);
+    } else if (m->cid_iss == id) {
+      auto it = fetches.find(m->cid_cnt);
+      if (it == fetches.end()) continue;  // late response after timeout: subscription gone
+      Fetch f = it->second;
+      fetches.erase(it);
+      // doOnSuccess (:563-567, :576-581): updateMetadata then sink.next
+      uint32_t oldm = meta[f.subj];
+      meta[f.subj] = m->md_meta;
+      if (f.added)
+        emit_event(SWIM_EV_ADDED, f.subj, NONE, m->md_meta, k);
+      else
+        emit_event(SWIM_EV_UPDATED, f.subj, oldm, m->md_meta, k);
+      if (f.group >= 0) groups[f.group].remaining--;
+      finish(f.group, false, k);
+      do_finally(f.subj, f.r1, f.reason);
+    }
+  }
+  // ---- P4 gossip (onGossipReq :171-183) ----
+  std::sort(gm.begin(), gm.end(), [](Msg* a, Msg* b) { return a->gid != b->gid ? a->gid < b->gid : a->src < b->src; });
+  for (Msg* m : gm) {
+    if (!gossips.count(m->gid)) {
+      GState g;
+      g.subj = m->g_subj;
+      g.rec = m->g_rec;
+      g.infPeriod = gPeriod;
+      gossips.emplace(m->gid, std::move(g));
+      s.ctr.record_compares++;
+      update_membership(m->g_subj, m->g_rec, R_GOSSIP, -1, k);  // onMembershipGossip (:401-408)
+    }
+    gossips[m->gid].infected.insert(m->src);
+  }
+  // ---- P5 timers ----
+  {
+    std::vector<Sub> due;
+    std::vector<Sub> keep;
+    for (auto& sb : subs) (sb.deadline == k ? due : keep).push_back(sb);
+    subs.swap(keep);
+    std::sort(due.begin(), due.end(), [](const Sub& a, const Sub& b) { return a.cnt != b.cnt ? a.cnt < b.cnt : a.order < b.order; });
+    for (auto& sb : due) {
+      if (sb.kind == 0)
+        ping_req_step(sb.target, sb.cnt, k);  // ping timeout -> ping-req (:159-175)
+      else
+        on_fd_event(sb.target, SUSPECT, k);  // ping-req timeout (:204-212)
+    }
+  }
+  {
+    std::vector<uint32_t> due;
+    for (auto& kv : fetches)
+      if (kv.second.deadline == k) due.push_back(kv.first);
+    for (uint32_t c : due) {  // .timeout(metadataTimeout) -> onErrorResume(TimeoutException) (:568,582)
+      Fetch f = fetches[c];
+      fetches.erase(c);
+      if (f.group >= 0) groups[f.group].remaining--;
+      finish(f.group, false, k);
+      do_finally(f.subj, f.r1, f.reason);
+    }
+  }
+  if (initActive && !initReceived && k == initDeadline) {  // .timeout(syncTimeout) (:241)
+    initActive = false;
+    nextSync = k + s.sync_t;
+  }
+  {
+    std::vector<uint32_t> due;
+    for (auto& kv : timers)
+      if (kv.second == k) due.push_back(kv.first);
+    for (uint32_t subj : due) {  // onSuspicionTimeout (:608-618)
+      auto it = timers.find(subj);
+      if (it == timers.end() || it->second != k) continue;
+      timers.erase(it);
+      Rec r = table[subj];
+      if (r.st != ABSENT) {
+        s.ctr.record_compares++;
+        update_membership(subj, Rec{DEAD, r.inc}, R_TIMEOUT, -1, k);
+      }
+    }
+  }
+  // ---- P6 periodic tasks ----
+  if (k == nextPing) {
+    nextPing += s.ping_t;
+    do_ping(k);
+  }
+  if (k == nextGossip) {
+    nextGossip += s.gossip_t;
+    do_spread_gossip(k);
+  }
+  if (k == nextSync) {
+    nextSync += s.sync_t;
+    do_sync(k);
+  }
+}
+
+void Sim::run_tick() {
+  uint64_t k = tick;
+  std::vector<Msg> arrived;
+  arrived.swap(inflight[k % (lat + 1)]);
+  std::vector<std::vector<Msg>> inbox(N);
+  for (auto& m : arrived) inbox[m.dst].push_back(std::move(m));
+  if (k == 0 && cfg.init_mode == SWIM_INIT_COLD_JOIN)
+    for (auto& m : members) m.start(0);
+  for (uint32_t i = 0; i < N; ++i)
+    if (members[i].alive) members[i].process(k, inbox[i]);
+  tick++;
+  ctr.tick = tick;
+}
+
+bool ms_to_ticks(uint32_t ms, uint32_t tick_ms, uint32_t* out) {
+  if (ms % tick_ms) return false;
+  *out = ms / tick_ms;
+  return true;
+}
+
+}  // namespace
+
+struct swim_handle {
+  Sim sim;
+};
+
+extern "C" {
+
+__attribute__((visibility("default"))) uint32_t swim_abi_version(void) { return SWIM_ABI_VERSION; }
+
+__attribute__((visibility("default"))) void swim_default_config(swim_config* c) {
+  std::memset(c, 0, sizeof(*c));
+  c->tick_ms = 100;
+  c->latency_ticks = 1;
+  c->init_mode = SWIM_INIT_PRECONVERGED;
+  c->seed = 0x5EED5EEDull;
+  c->sync_interval_ms = 30000;
+  c->sync_timeout_ms = 3000;
+  c->suspicion_mult = 5;
+  c->ping_interval_ms = 1000;
+  c->ping_timeout_ms = 500;
+  c->ping_req_members = 3;
+  c->gossip_interval_ms = 200;
+  c->gossip_fanout = 3;
+  c->gossip_repeat_mult = 3;
+  c->metadata_timeout_ms = 3000;
+  c->n_gpus = 1;
+}
+
+__attribute__((visibility("default"))) int swim_is_overrides(uint32_t r1s, uint32_t r1i, uint32_t r0s, uint32_t r0i) {
+  return is_overrides(Rec{(uint8_t)r1s, r1i}, Rec{(uint8_t)r0s, r0i}) ? 1 : 0;
+}
+__attribute__((visibility("default"))) uint32_t swim_ceil_log2(uint32_t n) { return bitlen(n); }
+
+__attribute__((visibility("default"))) int swim_create(const swim_config* cfg, swim_handle** out) {
+  if (!cfg || !out) return SWIM_EINVAL;
+  *out = nullptr;
+  const swim_config& c = *cfg;
+  if (c.n_members < 1 || c.tick_ms == 0 || c.latency_ticks == 0) return SWIM_EINVAL;
+  if (c.ping_timeout_ms >= c.ping_interval_ms) return SWIM_EINVAL;  // ClusterConfig.java:413-415
+  if (c.gossip_fanout == 0 || c.gossip_fanout > 8 || c.n_seeds > 16) return SWIM_EINVAL;
+  auto* h = new swim_handle();
+  Sim& s = h->sim;
+  s.cfg = c;
+  s.N = c.n_members;
+  uint32_t st;
+  bool ok = ms_to_ticks(c.ping_interval_ms, c.tick_ms, &s.ping_t) && ms_to_ticks(c.ping_timeout_ms, c.tick_ms, &s.pingTimeout_t) &&
+            ms_to_ticks(c.gossip_interval_ms, c.tick_ms, &s.gossip_t) && ms_to_ticks(c.sync_interval_ms, c.tick_ms, &s.sync_t) &&
+            ms_to_ticks(c.sync_timeout_ms, c.tick_ms, &s.syncTimeout_t) && ms_to_ticks(c.metadata_timeout_ms, c.tick_ms, &s.md_t);
+  (void)st;
+  if (!ok || s.ping_t == 0 || s.gossip_t == 0 || s.sync_t == 0) {
+    delete h;
+    return SWIM_EINVAL;
+  }
+  s.lat = c.latency_ticks;
+  s.seed_lo = (uint32_t)c.seed;
+  s.seed_hi = (uint32_t)(c.seed >> 32);
+  std::memset(&s.ctr, 0, sizeof(s.ctr));
+  s.inflight.assign(s.lat + 1, {});
+  s.group.assign(s.N, 0);
+  s.md_version.assign(s.N, 0);
+  s.members.resize(s.N);
+  for (uint32_t m = 0; m < s.N; ++m) {
+    Member& mb = s.members[m];
+    mb.sim = &s;
+    mb.id = m;
+    mb.table.assign(s.N, Rec{});
+    mb.meta.assign(s.N, NONE);
+    // seeds: LinkedHashSet, minus self (MembershipProtocolImpl.java:160-166)
+    for (uint32_t i = 0; i < c.n_seeds; ++i) {
+      uint32_t sd = c.seeds[i];
+      if (sd >= s.N || sd == m) continue;
+      if (std::find(mb.seeds.begin(), mb.seeds.end(), sd) == mb.seeds.end()) mb.seeds.push_back(sd);
+    }
+    mb.table[m] = Rec{ALIVE, 0};  // :133
+    mb.tsize = 1;
+    mb.meta[m] = 0;  // local metadata is always known
+    if (c.init_mode == SWIM_INIT_PRECONVERGED) {
+      for (uint32_t x = 0; x < s.N; ++x) {
+        mb.table[x] = Rec{ALIVE, 0};
+        mb.meta[x] = 0;
+      }
+      mb.tsize = s.N;
+      uint32_t n = s.N - 1;
+      for (int w = 0; w < 2; ++w) {
+        uint32_t keys[4];
+        for (int r = 0; r < 4; ++r) keys[r] = s.init_draw(m, 16 + 4 * (uint32_t)w + (uint32_t)r, 0);
+        Feistel f(n ? n : 1, keys);
+        std::vector<uint32_t>& L = w == 0 ? mb.ping : mb.remote;
+        L.resize(n);
+        for (uint32_t i = 0; i < n; ++i) {
+          uint32_t j = f(i);
+          L[i] = j < m ? j : j + 1;
+        }
+      }
+      mb.pingIdx = 0;
+      mb.remoteIdx = 0;
+      mb.nextPing = 1 + s.init_draw(m, 1, 0) % s.ping_t;
+      mb.nextGossip = 1 + s.init_draw(m, 2, 0) % s.gossip_t;
+      mb.nextSync = 1 + s.init_draw(m, 3, 0) % s.sync_t;
+    }
+  }
+  *out = h;
+  return SWIM_OK;
+}
+
+__attribute__((visibility("default"))) int swim_destroy(swim_handle* h) {
+  delete h;
+  return SWIM_OK;
+}
+
+__attribute__((visibility("default"))) int swim_step(swim_handle* h, uint32_t n) {
+  if (!h) return SWIM_EINVAL;
+  for (uint32_t i = 0; i < n; ++i) h->sim.run_tick();
+  return SWIM_OK;
+}
+__attribute__((visibility("default"))) int swim_run_periods(swim_handle* h, uint32_t n) {
+  if (!h) return SWIM_EINVAL;
+  return swim_step(h, n * h->sim.ping_t);
+}
+__attribute__((visibility("default"))) int swim_sync(swim_handle* h) { return h ? SWIM_OK : SWIM_EINVAL; }
+
+__attribute__((visibility("default"))) int swim_kill(swim_handle* h, uint32_t m) {
+  if (!h || m >= h->sim.N) return SWIM_EINVAL;
+  h->sim.members[m].alive = false;
+  return SWIM_OK;
+}
+__attribute__((visibility("default"))) int swim_set_default_loss(swim_handle* h, uint32_t pct) {
+  if (!h || pct > 100) return SWIM_EINVAL;
+  h->sim.loss = pct;
+  return SWIM_OK;
+}
+__attribute__((visibility("default"))) int swim_set_partition(swim_handle* h, const uint32_t* g) {
+  if (!h) return SWIM_EINVAL;
+  if (!g) {
+    h->sim.partitioned = false;
+    return SWIM_OK;
+  }
+  h->sim.group.assign(g, g + h->sim.N);
+  h->sim.partitioned = true;
+  return SWIM_OK;
+}
+__attribute__((visibility("default"))) int swim_unblock_all(swim_handle* h) {
+  if (!h) return SWIM_EINVAL;
+  h->sim.partitioned = false;
+  return SWIM_OK;
+}
+__attribute__((visibility("default"))) int swim_current_tick(swim_handle* h, uint64_t* t) {
+  if (!h || !t) return SWIM_EINVAL;
+  *t = h->sim.tick;
+  return SWIM_OK;
+}
+
+__attribute__((visibility("default"))) int swim_read_row(swim_handle* h, uint32_t obs, uint64_t* out, size_t cap) {
+  if (!h || obs >= h->sim.N || cap < h->sim.N) return SWIM_EINVAL;
+  const Member& mb = h->sim.members[obs];
+  for (uint32_t s = 0; s < h->sim.N; ++s) {
+    const Rec& r = mb.table[s];
+    if (r.st == ABSENT) {
+      out[s] = 0;
+      continue;
+    }
+    uint64_t v = (uint64_t)r.inc | ((uint64_t)r.st << 32) | ((uint64_t)(mb.meta[s] != NONE) << 34);
+    auto it = mb.timers.find(s);
+    if (it != mb.timers.end()) v |= (it->second & ((1ull << 29) - 1)) << 35;
+    out[s] = v;
+  }
+  return SWIM_OK;
+}
+
+__attribute__((visibility("default"))) int swim_state_hash(swim_handle* h, uint64_t* out, size_t cap) {
+  if (!h || cap < 6ull * h->sim.N) return SWIM_EINVAL;
+  Sim& s = h->sim;
+  std::vector<uint64_t> row(s.N);
+  for (uint32_t m = 0; m < s.N; ++m) {
+    const Member& mb = s.members[m];
+    swim_read_row(h, m, row.data(), s.N);
+    uint64_t hr = 0;
+    for (uint32_t x = 0; x < s.N; ++x)
+      if (row[x]) hr += hpair(x, row[x]);
+    uint64_t hf = mix64((uint64_t)mb.pingIdx ^ 0xF00Dull) + mb.ping.size();
+    for (size_t p = 0; p < mb.ping.size(); ++p) hf += hpair(p | (1ull << 40), mb.ping[p]);
+    uint64_t hg = mix64((uint64_t)mb.remoteIdx ^ 0xBEEFull) + mb.remote.size();
+    for (size_t p = 0; p < mb.remote.size(); ++p) hg += hpair(p | (2ull << 40), mb.remote[p]);
+    uint64_t hgs = 0;
+    for (auto& kv : mb.gossips) hgs += hpair(kv.first, kv.second.infPeriod);
+    uint64_t misc = hpair(hpair(hpair(mb.cidCnt, mb.syncSeq), mb.gCounter), mb.nextSync) + mix64(mb.fdPeriod * 3 + mb.gPeriod * 7);
+    out[6 * m + 0] = hr;
+    out[6 * m + 1] = hf;
+    out[6 * m + 2] = hg;
+    out[6 * m + 3] = mb.evHash;
+    out[6 * m + 4] = hgs;
+    out[6 * m + 5] = misc;
+  }
+  return SWIM_OK;
+}
+
+__attribute__((visibility("default"))) int swim_read_lists(swim_handle* h, uint32_t obs, uint32_t* fd, uint32_t* fd_len,
+                                                           uint32_t* gl, uint32_t* g_len, size_t cap, int32_t* cursors) {
+  if (!h || obs >= h->sim.N) return SWIM_EINVAL;
+  const Member& mb = h->sim.members[obs];
+  if (mb.ping.size() > cap || mb.remote.size() > cap) return SWIM_EINVAL;
+  std::copy(mb.ping.begin(), mb.ping.end(), fd);
+  std::copy(mb.remote.begin(), mb.remote.end(), gl);
+  *fd_len = (uint32_t)mb.ping.size();
+  *g_len = (uint32_t)mb.remote.size();
+  cursors[0] = (int32_t)mb.pingIdx;
+  cursors[1] = (int32_t)mb.remoteIdx;
+  return SWIM_OK;
+}
+
+__attribute__((visibility("default"))) int swim_drain_events(swim_handle* h, swim_event* out, size_t cap, size_t* n_out) {
+  if (!h || !n_out) return SWIM_EINVAL;
+  auto& ev = h->sim.events;
+  std::stable_sort(ev.begin(), ev.end(), [](const swim_event& a, const swim_event& b) {
+    if (a.tick != b.tick) return a.tick < b.tick;
+    if (a.observer != b.observer) return a.observer < b.observer;
+    return a.seq < b.seq;
+  });
+  size_t n = std::min(cap, ev.size());
+  std::copy(ev.begin(), ev.begin() + (long)n, out);
+  ev.erase(ev.begin(), ev.begin() + (long)n);
+  *n_out = n;
+  return SWIM_OK;
+}
+
+__attribute__((visibility("default"))) int swim_counters_get(swim_handle* h, swim_counters* out) {
+  if (!h || !out) return SWIM_EINVAL;
+  *out = h->sim.ctr;
+  return SWIM_OK;
+}
+
+__attribute__((visibility("default"))) const char* swim_last_error(swim_handle* h) { return h ? h->sim.err.c_str() : "null handle"; }
+
+}  // extern "C"

@@ -1,0 +1,125 @@
+"""ctypes mirror of include/swimhip.h (the C ABI of libswimhip).
+
+The same ABI is exported by the product library (libswimhip.so, gfx950) and, for tests only, by the CPU oracle
+(oracle/liboracle_swimref.so). This module only describes the ABI. Choosing a library is the caller's job.
+"""
+import ctypes as C
+
+SWIM_OK = 0
+SWIM_EINVAL = -1
+SWIM_ENOMEM = -2
+SWIM_EDEVICE = -3
+SWIM_ECAPACITY = -4
+SWIM_EUNSUPPORTED = -5
+
+INIT_COLD_JOIN = 0
+INIT_PRECONVERGED = 1
+MODE_FULL = 0
+FLAG_RECORD_EVENTS = 1
+
+EV_ADDED, EV_REMOVED, EV_UPDATED = 0, 1, 2
+META_NONE = 0xFFFFFFFF
+ST_ABSENT, ST_ALIVE, ST_SUSPECT, ST_DEAD = 0, 1, 2, 3
+HASH_WORDS = 6  # row, fd list, gossip list, events, gossips held, misc
+
+
+class SwimConfig(C.Structure):
+    _fields_ = [
+        ("n_members", C.c_uint32),
+        ("tick_ms", C.c_uint32),
+        ("latency_ticks", C.c_uint32),
+        ("init_mode", C.c_uint32),
+        ("seed", C.c_uint64),
+        ("sync_interval_ms", C.c_uint32),
+        ("sync_timeout_ms", C.c_uint32),
+        ("suspicion_mult", C.c_uint32),
+        ("ping_interval_ms", C.c_uint32),
+        ("ping_timeout_ms", C.c_uint32),
+        ("ping_req_members", C.c_uint32),
+        ("gossip_interval_ms", C.c_uint32),
+        ("gossip_fanout", C.c_uint32),
+        ("gossip_repeat_mult", C.c_uint32),
+        ("metadata_timeout_ms", C.c_uint32),
+        ("mode", C.c_uint32),
+        ("flags", C.c_uint32),
+        ("n_seeds", C.c_uint32),
+        ("seeds", C.c_uint32 * 16),
+        ("gossip_slot_cap", C.c_uint32),
+        ("pending_fetch_cap", C.c_uint32),
+        ("event_cap", C.c_uint32),
+        ("n_gpus", C.c_uint32),
+        ("device", C.c_uint32),
+        ("reserved", C.c_uint32 * 7),
+    ]
+
+
+class SwimEvent(C.Structure):
+    _fields_ = [
+        ("tick", C.c_uint32),
+        ("observer", C.c_uint32),
+        ("seq", C.c_uint32),
+        ("type", C.c_uint32),
+        ("subject", C.c_uint32),
+        ("old_meta", C.c_uint32),
+        ("new_meta", C.c_uint32),
+        ("pad", C.c_uint32),
+    ]
+
+
+class SwimCounters(C.Structure):
+    _fields_ = [
+        ("tick", C.c_uint64),
+        ("record_compares", C.c_uint64),
+        ("row_writes", C.c_uint64),
+        ("messages", C.c_uint64),
+        ("gossip_messages", C.c_uint64),
+        ("events", C.c_uint64),
+        ("messages_lost", C.c_uint64),
+        ("gossips_created", C.c_uint64),
+        ("sync_merges", C.c_uint64),
+        ("reserved", C.c_uint64 * 7),
+    ]
+
+    def as_dict(self):
+        return {k: int(getattr(self, k)) for k, _ in self._fields_ if k != "reserved"}
+
+
+# every entry point declared in include/swimhip.h: name -> (restype, argtypes)
+_H = C.c_void_p
+_U32P = C.POINTER(C.c_uint32)
+SIGNATURES = {
+    "swim_default_config": (None, [C.POINTER(SwimConfig)]),
+    "swim_abi_version": (C.c_uint32, []),
+    "swim_create": (C.c_int, [C.POINTER(SwimConfig), C.POINTER(_H)]),
+    "swim_destroy": (C.c_int, [_H]),
+    "swim_step": (C.c_int, [_H, C.c_uint32]),
+    "swim_run_periods": (C.c_int, [_H, C.c_uint32]),
+    "swim_sync": (C.c_int, [_H]),
+    "swim_kill": (C.c_int, [_H, C.c_uint32]),
+    "swim_set_default_loss": (C.c_int, [_H, C.c_uint32]),
+    "swim_set_partition": (C.c_int, [_H, _U32P]),
+    "swim_unblock_all": (C.c_int, [_H]),
+    "swim_current_tick": (C.c_int, [_H, C.POINTER(C.c_uint64)]),
+    "swim_read_row": (C.c_int, [_H, C.c_uint32, C.POINTER(C.c_uint64), C.c_size_t]),
+    "swim_state_hash": (C.c_int, [_H, C.POINTER(C.c_uint64), C.c_size_t]),
+    "swim_read_lists": (C.c_int, [_H, C.c_uint32, _U32P, _U32P, _U32P, _U32P, C.c_size_t, C.POINTER(C.c_int32)]),
+    "swim_drain_events": (C.c_int, [_H, C.POINTER(SwimEvent), C.c_size_t, C.POINTER(C.c_size_t)]),
+    "swim_counters_get": (C.c_int, [_H, C.POINTER(SwimCounters)]),
+    "swim_last_error": (C.c_char_p, [_H]),
+    "swim_is_overrides": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
+    "swim_ceil_log2": (C.c_uint32, [C.c_uint32]),
+}
+
+
+def bind(lib):
+    """Attach restype/argtypes for every ABI symbol; raises AttributeError if one is missing."""
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+def load(path):
+    # RTLD_LOCAL keeps the oracle's and the engine's identically named swim_* symbols apart in one process
+    return bind(C.CDLL(str(path), mode=C.RTLD_LOCAL))

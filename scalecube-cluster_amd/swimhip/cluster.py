@@ -1,0 +1,187 @@
+"""SimulatedCluster: N scalecube members behind one libswimhip handle.
+
+It mirrors the outward surface of the reference's per-member stack:
+  * MembershipEvent (membership/MembershipEvent.java:11-123): type ADDED/REMOVED/UPDATED, member, old/new metadata.
+  * Cluster.listenMembership / MembershipProtocol.listen (Cluster.java:247, ClusterImpl.java:287-294): here events()
+    drains them in (tick, observer, seq) order.
+  * MembershipProtocol.members / member(id) (MembershipProtocol.java:14-65): members(observer).
+  * MembershipProtocolImpl.getMembershipRecords (:678-680): records(observer).
+  * NetworkEmulator.block / unblockAll / setDefaultLinkSettings (transport/.../NetworkEmulator.java:113-192).
+The failure behaviour follows the C ABI: any negative return raises SwimError carrying swim_last_error().
+"""
+import ctypes as C
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+
+from . import _abi
+from .config import SimConfig
+
+
+class SwimError(RuntimeError):
+    pass
+
+
+@dataclass(frozen=True)
+class MembershipEvent:
+    tick: int
+    observer: int
+    seq: int
+    type: str  # "ADDED" | "REMOVED" | "UPDATED"
+    member: int
+    oldMetadata: Optional[int]
+    newMetadata: Optional[int]
+
+    def isAdded(self):
+        return self.type == "ADDED"
+
+    def isRemoved(self):
+        return self.type == "REMOVED"
+
+    def isUpdated(self):
+        return self.type == "UPDATED"
+
+
+@dataclass(frozen=True)
+class MembershipRecord:
+    member: int
+    status: str  # "ALIVE" | "SUSPECT"
+    incarnation: int
+    has_metadata: bool
+    suspicion_deadline: Optional[int]
+
+
+_TYPES = {_abi.EV_ADDED: "ADDED", _abi.EV_REMOVED: "REMOVED", _abi.EV_UPDATED: "UPDATED"}
+_STATUS = {_abi.ST_ALIVE: "ALIVE", _abi.ST_SUSPECT: "SUSPECT"}
+
+
+def _meta(v):
+    return None if v == _abi.META_NONE else int(v)
+
+
+class SimulatedCluster:
+    def __init__(self, lib, cfg: SimConfig):
+        self.lib = lib
+        self.cfg = cfg
+        self.n = cfg.n_members
+        self._h = C.c_void_p()
+        a = cfg.to_abi()
+        rc = lib.swim_create(C.byref(a), C.byref(self._h))
+        if rc != 0:
+            raise SwimError(f"swim_create failed rc={rc}")
+
+    # -- lifecycle ------------------------------------------------------------------------------------------
+    def close(self):
+        if self._h:
+            self.lib.swim_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _ck(self, rc, what):
+        if rc != 0:
+            msg = self.lib.swim_last_error(self._h)
+            raise SwimError(f"{what} failed rc={rc}: {msg.decode() if msg else ''}")
+
+    # -- driving --------------------------------------------------------------------------------------------
+    def step(self, ticks=1):
+        self._ck(self.lib.swim_step(self._h, ticks), "swim_step")
+
+    def run_periods(self, n):
+        self._ck(self.lib.swim_run_periods(self._h, n), "swim_run_periods")
+
+    def sync(self):
+        self._ck(self.lib.swim_sync(self._h), "swim_sync")
+
+    @property
+    def tick(self):
+        t = C.c_uint64()
+        self._ck(self.lib.swim_current_tick(self._h, C.byref(t)), "swim_current_tick")
+        return t.value
+
+    # -- fault injection (NetworkEmulator) ------------------------------------------------------------------
+    def kill(self, member):
+        self._ck(self.lib.swim_kill(self._h, member), "swim_kill")
+
+    def set_default_loss(self, pct):
+        self._ck(self.lib.swim_set_default_loss(self._h, pct), "swim_set_default_loss")
+
+    def partition(self, group_of_member):
+        g = np.ascontiguousarray(np.asarray(group_of_member, dtype=np.uint32))
+        assert g.shape == (self.n,)
+        self._ck(self.lib.swim_set_partition(self._h, g.ctypes.data_as(C.POINTER(C.c_uint32))), "swim_set_partition")
+
+    def unblock_all(self):
+        self._ck(self.lib.swim_unblock_all(self._h), "swim_unblock_all")
+
+    # -- readback -------------------------------------------------------------------------------------------
+    def row(self, observer) -> np.ndarray:
+        out = np.zeros(self.n, dtype=np.uint64)
+        self._ck(self.lib.swim_read_row(self._h, observer, out.ctypes.data_as(C.POINTER(C.c_uint64)), self.n),
+                 "swim_read_row")
+        return out
+
+    def records(self, observer) -> List[MembershipRecord]:
+        row = self.row(observer)
+        recs = []
+        for s in np.nonzero(row)[0]:
+            v = int(row[s])
+            st = (v >> 32) & 3
+            dl = v >> 35
+            recs.append(MembershipRecord(int(s), _STATUS[st], v & 0xFFFFFFFF, bool((v >> 34) & 1), dl or None))
+        return recs
+
+    def members(self, observer):
+        return [r.member for r in self.records(observer)]
+
+    def trusted(self, observer):
+        return [r.member for r in self.records(observer) if r.status == "ALIVE"]
+
+    def suspected(self, observer):
+        return [r.member for r in self.records(observer) if r.status == "SUSPECT"]
+
+    def lists(self, observer):
+        cap = max(self.n * 2, 16)
+        fd = np.zeros(cap, dtype=np.uint32)
+        gl = np.zeros(cap, dtype=np.uint32)
+        fl, glen = C.c_uint32(), C.c_uint32()
+        cur = (C.c_int32 * 2)()
+        P = C.POINTER(C.c_uint32)
+        self._ck(self.lib.swim_read_lists(self._h, observer, fd.ctypes.data_as(P), C.byref(fl), gl.ctypes.data_as(P),
+                                          C.byref(glen), cap, cur), "swim_read_lists")
+        return fd[: fl.value].copy(), gl[: glen.value].copy(), (cur[0], cur[1])
+
+    def state_hash(self) -> np.ndarray:
+        out = np.zeros(self.n * _abi.HASH_WORDS, dtype=np.uint64)
+        self._ck(self.lib.swim_state_hash(self._h, out.ctypes.data_as(C.POINTER(C.c_uint64)), out.size),
+                 "swim_state_hash")
+        return out.reshape(self.n, _abi.HASH_WORDS)
+
+    def counters(self):
+        c = _abi.SwimCounters()
+        self._ck(self.lib.swim_counters_get(self._h, C.byref(c)), "swim_counters_get")
+        return c.as_dict()
+
+    def events(self, cap=1 << 16) -> List[MembershipEvent]:
+        out = []
+        buf = (_abi.SwimEvent * cap)()
+        n = C.c_size_t()
+        while True:
+            self._ck(self.lib.swim_drain_events(self._h, buf, cap, C.byref(n)), "swim_drain_events")
+            for i in range(n.value):
+                e = buf[i]
+                out.append(MembershipEvent(e.tick, e.observer, e.seq, _TYPES[e.type], e.subject, _meta(e.old_meta),
+                                           _meta(e.new_meta)))
+            if n.value < cap:
+                return out
