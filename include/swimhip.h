@@ -136,11 +136,15 @@ int swim_unblock_all(swim_handle* h);
 int swim_current_tick(swim_handle* h, uint64_t* tick);
 /* row of one observer: keys[s] = inc | status<<32 | meta_present<<34 | timer_deadline<<35 (SEMANTICS.md §8) */
 int swim_read_row(swim_handle* h, uint32_t observer, uint64_t* keys_out, size_t cap);
-/* per-observer hashes: out[4*m + {0:row, 1:fd list, 2:gossip list, 3:events}] */
+/* per-observer hashes: out[6*m + {0:row, 1:fd list, 2:gossip list, 3:events, 4:gossips held, 5:counters}] */
 int swim_state_hash(swim_handle* h, uint64_t* out, size_t cap);
 /* FD pingMembers and gossip remoteMembers lists, plus cursors */
 int swim_read_lists(swim_handle* h, uint32_t observer, uint32_t* fd_out, uint32_t* fd_len, uint32_t* gossip_out,
                     uint32_t* gossip_len, size_t cap, int32_t* cursors_out /* [pingIdx, remoteIdx] */);
+/* gossips held by one observer (GossipProtocolImpl.gossips, GossipState.java:8-38): id = origin << 32 | counter,
+ * infection period; sorted by id */
+int swim_read_gossips(swim_handle* h, uint32_t observer, uint64_t* ids_out, uint32_t* inf_period_out, size_t cap,
+                      size_t* n_out);
 int swim_drain_events(swim_handle* h, swim_event* out, size_t cap, size_t* n_out);
 int swim_counters_get(swim_handle* h, swim_counters* out);
 const char* swim_last_error(swim_handle* h);

@@ -539,10 +539,7 @@ void Member::do_spread_gossip(uint64_t k) {
       if (g.infPeriod + sp < period) continue;
       if (g.infected.count(t)) continue;
       s.ctr.gossip_messages++;
-      if (s.lost_gossip(id, t, k, slot, kv.first)) {
-        s.ctr.messages_lost++;
-        continue;
-      }
+      if (s.lost_gossip(id, t, k, slot, kv.first)) continue;  // gossip losses are not counted (SEMANTICS.md §8)
       Msg m;
       m.kind = K_GOSSIP;
       m.src = id;
@@ -948,6 +945,7 @@ __attribute__((visibility("default"))) int swim_sync(swim_handle* h) { return h 
 __attribute__((visibility("default"))) int swim_kill(swim_handle* h, uint32_t m) {
   if (!h || m >= h->sim.N) return SWIM_EINVAL;
   h->sim.members[m].alive = false;
+  h->sim.members[m].gossips.clear();  // a crashed process keeps nothing it could gossip again (SEMANTICS.md §1)
   return SWIM_OK;
 }
 __attribute__((visibility("default"))) int swim_set_default_loss(swim_handle* h, uint32_t pct) {
@@ -1031,6 +1029,21 @@ __attribute__((visibility("default"))) int swim_read_lists(swim_handle* h, uint3
   *g_len = (uint32_t)mb.remote.size();
   cursors[0] = (int32_t)mb.pingIdx;
   cursors[1] = (int32_t)mb.remoteIdx;
+  return SWIM_OK;
+}
+
+__attribute__((visibility("default"))) int swim_read_gossips(swim_handle* h, uint32_t obs, uint64_t* ids, uint32_t* inf,
+                                                             size_t cap, size_t* n_out) {
+  if (!h || obs >= h->sim.N || !n_out) return SWIM_EINVAL;
+  const Member& mb = h->sim.members[obs];
+  size_t n = 0;
+  for (auto& kv : mb.gossips) {
+    if (n == cap) return SWIM_ECAPACITY;
+    ids[n] = kv.first;
+    inf[n] = (uint32_t)kv.second.infPeriod;
+    n++;
+  }
+  *n_out = n;
   return SWIM_OK;
 }
 

@@ -1,0 +1,451 @@
+// api.hip — the C ABI of libswimhip (include/swimhip.h): configuration, device allocation, fault injection, readback.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/swimhip.h"
+#include "engine.h"
+
+using namespace swim;
+
+struct swim_handle {
+  swim_config cfg;
+  Dev d;
+  hipStream_t stream = nullptr;
+  uint64_t tick = 0;
+  std::string err;
+  std::vector<void*> allocs;
+  std::vector<swim_event> host_events;
+  // settings-epoch ring mirrored on the host
+  uint32_t ep_from[MAX_EPOCHS], ep_loss[MAX_EPOCHS], ep_part[MAX_EPOCHS];
+  int cur_ep = 0;
+  uint32_t loss = 0;
+  bool partitioned = false;
+  std::vector<uint32_t> group;
+  size_t bytes = 0;
+};
+
+namespace {
+
+#define HIPCK(expr)                                                        \
+  do {                                                                     \
+    hipError_t e_ = (expr);                                                \
+    if (e_ != hipSuccess) {                                                \
+      h->err = std::string(#expr " -> ") + hipGetErrorString(e_);          \
+      return SWIM_EDEVICE;                                                 \
+    }                                                                      \
+  } while (0)
+
+template <class T>
+int dalloc(swim_handle* h, T** p, size_t count) {
+  size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
+  void* q = nullptr;
+  hipError_t e = hipMalloc(&q, bytes);
+  if (e != hipSuccess) {
+    h->err = "hipMalloc(" + std::to_string(bytes) + ") failed: " + hipGetErrorString(e);
+    return SWIM_ENOMEM;
+  }
+  h->allocs.push_back(q);
+  h->bytes += bytes;
+  *p = (T*)q;
+  return SWIM_OK;
+}
+
+bool to_ticks(uint32_t ms, uint32_t tick, uint32_t* out) {
+  if (tick == 0 || ms % tick) return false;
+  *out = ms / tick;
+  return true;
+}
+
+int check_err(swim_handle* h) {
+  hipError_t e = hipStreamSynchronize(h->stream);
+  if (e != hipSuccess) {
+    h->err = std::string("device failure: ") + hipGetErrorString(e);
+    return SWIM_EDEVICE;
+  }
+  uint32_t eb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (hipMemcpy(eb, h->d.err, sizeof(eb), hipMemcpyDeviceToHost) != hipSuccess) return SWIM_EDEVICE;
+  uint32_t bits = eb[0];
+  if (bits) {
+    char hex[160];
+    snprintf(hex, sizeof hex, "%x [info %u %u %u %u %u %u %u]", bits, eb[1], eb[2], eb[3], eb[4], eb[5], eb[6], eb[7]);
+    h->err = std::string("engine capacity/semantic error bits 0x") + hex +
+             " (see engine.h E_* ; raise the matching capacity in swim_config)";
+    return SWIM_ECAPACITY;
+  }
+  return SWIM_OK;
+}
+
+// open a new NetworkEmulator-settings epoch that starts at the next tick to run
+int push_epoch(swim_handle* h) {
+  int e = h->cur_ep;
+  if (h->ep_from[e] != (uint32_t)h->tick) e = (e + 1) % (int)MAX_EPOCHS;
+  h->cur_ep = e;
+  h->ep_from[e] = (uint32_t)h->tick;
+  h->ep_loss[e] = h->loss;
+  h->ep_part[e] = h->partitioned ? 1u : 0u;
+  HIPCK(hipMemcpy(h->d.ep_from + e, &h->ep_from[e], 4, hipMemcpyHostToDevice));
+  HIPCK(hipMemcpy(h->d.ep_loss + e, &h->ep_loss[e], 4, hipMemcpyHostToDevice));
+  HIPCK(hipMemcpy(h->d.ep_part + e, &h->ep_part[e], 4, hipMemcpyHostToDevice));
+  HIPCK(hipMemcpy(h->d.ep_group + (size_t)e * h->d.N, h->group.data(), 4ull * h->d.N, hipMemcpyHostToDevice));
+  return SWIM_OK;
+}
+
+int build(swim_handle* h) {
+  const swim_config& c = h->cfg;
+  Dev& d = h->d;
+  std::memset(&d, 0, sizeof(d));
+  d.N = c.n_members;
+  d.F = c.gossip_fanout;
+  d.kreq = c.ping_req_members;
+  if (!to_ticks(c.ping_interval_ms, c.tick_ms, &d.ping_t) || !to_ticks(c.ping_timeout_ms, c.tick_ms, &d.pingTimeout_t) ||
+      !to_ticks(c.gossip_interval_ms, c.tick_ms, &d.gossip_t) || !to_ticks(c.sync_interval_ms, c.tick_ms, &d.sync_t) ||
+      !to_ticks(c.sync_timeout_ms, c.tick_ms, &d.syncTimeout_t) || !to_ticks(c.metadata_timeout_ms, c.tick_ms, &d.md_t) ||
+      d.ping_t == 0 || d.gossip_t == 0 || d.sync_t == 0) {
+    h->err = "every interval/timeout must be a positive multiple of tick_ms";
+    return SWIM_EINVAL;
+  }
+  d.lat = c.latency_ticks;
+  d.suspMult = c.suspicion_mult;
+  d.repeatMult = c.gossip_repeat_mult;
+  d.seed_lo = (uint32_t)c.seed;
+  d.seed_hi = (uint32_t)(c.seed >> 32);
+  d.init_mode = c.init_mode;
+  d.flags = c.flags;
+  // seeds: LinkedHashSet of valid ids (MembershipProtocolImpl.java:160-166); self is skipped per member
+  for (uint32_t i = 0; i < c.n_seeds; ++i) {
+    uint32_t s = c.seeds[i];
+    if (s >= d.N) continue;
+    bool dup = false;
+    for (uint32_t j = 0; j < d.n_seeds; ++j) dup |= d.seeds[j] == s;
+    if (!dup) d.seeds[d.n_seeds++] = s;
+  }
+  const uint64_t N = d.N;
+  d.LCAP = d.N + 64;
+  d.FCAP = c.pending_fetch_cap ? c.pending_fetch_cap : 256;
+  d.GRCAP = c.init_mode == SWIM_INIT_COLD_JOIN ? std::min<uint32_t>(d.N + 16, 1024) : 32;
+  uint32_t maxSpread = d.repeatMult * (32u - (uint32_t)__builtin_clz(d.LCAP + 1));
+  d.LOGW = 8;
+  while (d.LOGW < 4 * (maxSpread + 2)) d.LOGW <<= 1;  // rounds kept for the infectedFrom replay
+  d.LOOKBACK = d.LOGW * d.gossip_t;
+  d.HCAP = 1u << 20;
+  uint64_t slots = c.gossip_slot_cap ? c.gossip_slot_cap : std::min<uint64_t>(65535, std::max<uint64_t>(1024, (1ull << 30) / (4 * N)));
+  d.SLOTS = (uint32_t)std::min<uint64_t>(slots, 65535);
+  uint64_t mc = N / d.sync_t * 4 + N / d.ping_t + 1024;
+  if (c.init_mode == SWIM_INIT_COLD_JOIN) mc = std::max<uint64_t>(mc, N + 1024);
+  d.MSGCAP = (uint32_t)mc;
+  d.NCHUNK = (uint32_t)((N + CH - 1) / CH);
+  d.POOLCAP = (uint32_t)std::min<uint64_t>(1ull << 26, std::max<uint64_t>(1ull << 20, N * 64));
+  d.EVCAP = c.event_cap ? c.event_cap : (1u << 20);
+  d.DCAP = (uint32_t)std::min<uint64_t>(1ull << 26, std::max<uint64_t>(1ull << 16, N * 512));
+  d.RCAP = d.DCAP;
+  d.ARENA_ROWS = 64;
+
+  int rc;
+#define A(p, n)                                   \
+  if ((rc = dalloc(h, &(p), (size_t)(n))) != 0) return rc;
+  A(d.dead_tick, N) A(d.ep_from, MAX_EPOCHS) A(d.ep_loss, MAX_EPOCHS) A(d.ep_part, MAX_EPOCHS)
+  A(d.ep_group, MAX_EPOCHS * N) A(d.md_version, N)
+  A(d.tsize, N) A(d.fdLen, N) A(d.gLen, N) A(d.fdPeriod, N) A(d.gPeriod, N) A(d.gCounter, N) A(d.nextPing, N)
+  A(d.nextGossip, N) A(d.nextSync, N) A(d.cidCnt, N) A(d.syncSeq, N) A(d.evSeq, N) A(d.held, N) A(d.timerMin, N)
+  A(d.initFlags, N) A(d.initDeadline, N) A(d.initCidBase, N) A(d.initN, N) A(d.firstGossip, N) A(d.nsub, N)
+  A(d.npath, N) A(d.nfetch, N) A(d.pingIdx, N) A(d.remoteIdx, N) A(d.sel, N * 8) A(d.evHash, N)
+  A(d.row, N * N) A(d.fdl, N * d.LCAP) A(d.gl, N * d.LCAP)
+  A(d.subs, N * SUBCAP * 4) A(d.paths, N * PATHCAP * 5) A(d.fetch, N * d.FCAP * FREC) A(d.groups, N * d.GRCAP * GREC)
+  A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F)
+  A(d.log_tick, N * d.LOGW) A(d.log_spread, N * d.LOGW) A(d.log_cnt, N * d.LOGW) A(d.log_tg, N * d.LOGW * d.F)
+  A(d.log_pos, N)
+  A(d.slot_gid, d.SLOTS) A(d.slot_subj, d.SLOTS) A(d.slot_ctick, d.SLOTS) A(d.slot_key, d.SLOTS) A(d.slot_holders, d.SLOTS)
+  A(d.slot_used, d.SLOTS) A(d.S, (uint64_t)d.SLOTS * N) A(d.free_list, d.SLOTS) A(d.free_top, 1)
+  A(d.deliv, d.DCAP) A(d.deliv_n, 1) A(d.rc_raw, d.RCAP) A(d.rc_n, 1) A(d.rc_cnt, N) A(d.rc_off, N) A(d.rc_fill, N)
+  A(d.rc_slot, d.RCAP) A(d.rc_key, d.RCAP) A(d.active, d.SLOTS) A(d.nactive, 1) A(d.hist, (uint64_t)d.HCAP * 6)
+  A(d.msgs[0], d.MSGCAP) A(d.msgs[1], d.MSGCAP) A(d.nmsg, 2) A(d.arena[0], (uint64_t)d.ARENA_ROWS * N)
+  A(d.arena[1], (uint64_t)d.ARENA_ROWS * N) A(d.arena_used, 2) A(d.m_cnt, N) A(d.m_off, N) A(d.m_fill, N)
+  A(d.m_idx, d.MSGCAP) A(d.m_key, d.MSGCAP) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
+  A(d.pool, d.POOLCAP) A(d.pool_used, 1)
+  A(d.ev, (uint64_t)d.EVCAP * 8) A(d.ev_n, 1) A(d.ctr, C_NCTR) A(d.err, 8)
+#undef A
+  HIPCK(hipMemset(d.S, 0, (size_t)d.SLOTS * N * 4));
+  HIPCK(hipMemset(d.ctr, 0, C_NCTR * 8));
+  HIPCK(hipMemset(d.hist, 0, (size_t)d.HCAP * 48));
+  HIPCK(hipMemset(d.err, 0, 32));
+  HIPCK(hipMemset(d.ev_n, 0, 4));
+  HIPCK(hipMemset(d.nmsg, 0, 8));
+  HIPCK(hipMemset(d.arena_used, 0, 8));
+  HIPCK(hipMemset(d.tcnt, 0, N * 4));
+  HIPCK(hipMemset(d.subs, 0, N * SUBCAP * 16));
+  int32_t top = (int32_t)d.SLOTS;
+  HIPCK(hipMemcpy(d.free_top, &top, 4, hipMemcpyHostToDevice));
+  std::vector<uint32_t> never(MAX_EPOCHS, NEVER);
+  HIPCK(hipMemcpy(d.ep_from, never.data(), 4 * MAX_EPOCHS, hipMemcpyHostToDevice));
+  h->group.assign(d.N, 0);
+  for (uint32_t e = 0; e < MAX_EPOCHS; ++e) h->ep_from[e] = NEVER;
+  h->cur_ep = 0;
+  launch_init(d, h->stream);
+  if ((rc = push_epoch(h)) != 0) return rc;
+  return check_err(h);
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t swim_abi_version(void) { return SWIM_ABI_VERSION; }
+
+void swim_default_config(swim_config* c) {
+  std::memset(c, 0, sizeof(*c));
+  c->tick_ms = 100;
+  c->latency_ticks = 1;
+  c->init_mode = SWIM_INIT_PRECONVERGED;
+  c->seed = 0x5EED5EEDull;
+  c->sync_interval_ms = 30000;
+  c->sync_timeout_ms = 3000;
+  c->suspicion_mult = 5;
+  c->ping_interval_ms = 1000;
+  c->ping_timeout_ms = 500;
+  c->ping_req_members = 3;
+  c->gossip_interval_ms = 200;
+  c->gossip_fanout = 3;
+  c->gossip_repeat_mult = 3;
+  c->metadata_timeout_ms = 3000;
+  c->n_gpus = 1;
+}
+
+int swim_is_overrides(uint32_t s1, uint32_t i1, uint32_t s0, uint32_t i0) { return overrides(s1, i1, s0, i0) ? 1 : 0; }
+uint32_t swim_ceil_log2(uint32_t n) { return bitlen(n); }
+
+int swim_create(const swim_config* cfg, swim_handle** out) {
+  if (!cfg || !out) return SWIM_EINVAL;
+  *out = nullptr;
+  const swim_config& c = *cfg;
+  if (c.n_members < 2 || c.ping_timeout_ms >= c.ping_interval_ms || c.gossip_fanout == 0 || c.gossip_fanout > 8 ||
+      c.ping_req_members > 8 || c.n_seeds > 16 || c.mode != SWIM_MODE_FULL || c.n_members > (1u << 30))
+    return SWIM_EINVAL;
+  if (c.latency_ticks != 1) return SWIM_EUNSUPPORTED;  // gossip data plane assumes one-tick hops
+  if (c.n_gpus > 1) return SWIM_EUNSUPPORTED;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= (int)c.device) return SWIM_EDEVICE;
+  auto* h = new swim_handle();
+  h->cfg = c;
+  if (hipSetDevice((int)c.device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return SWIM_EDEVICE;
+  }
+  int rc = build(h);
+  if (rc != SWIM_OK) {
+    fprintf(stderr, "swim_create: %s\n", h->err.c_str());
+    swim_destroy(h);
+    return rc;
+  }
+  *out = h;
+  return SWIM_OK;
+}
+
+int swim_destroy(swim_handle* h) {
+  if (!h) return SWIM_EINVAL;
+  hipSetDevice((int)h->cfg.device);
+  if (h->stream) hipStreamSynchronize(h->stream);
+  for (void* p : h->allocs) hipFree(p);
+  if (h->stream) hipStreamDestroy(h->stream);
+  delete h;
+  return SWIM_OK;
+}
+
+int swim_step(swim_handle* h, uint32_t n) {
+  if (!h) return SWIM_EINVAL;
+  hipSetDevice((int)h->cfg.device);
+  if (h->tick + n >= (1ull << 28)) return SWIM_ECAPACITY;  // deadlines are stored in 29 bits
+  for (uint32_t i = 0; i < n; ++i) {
+    launch_tick(h->d, (uint32_t)h->tick, h->stream);
+    h->tick++;
+  }
+  return check_err(h);
+}
+
+int swim_run_periods(swim_handle* h, uint32_t n) {
+  if (!h) return SWIM_EINVAL;
+  return swim_step(h, n * h->d.ping_t);
+}
+
+int swim_sync(swim_handle* h) { return h ? check_err(h) : SWIM_EINVAL; }
+
+int swim_kill(swim_handle* h, uint32_t m) {
+  if (!h || m >= h->d.N) return SWIM_EINVAL;
+  uint32_t t = (uint32_t)h->tick;
+  HIPCK(hipMemcpyAsync(h->d.dead_tick + m, &t, 4, hipMemcpyHostToDevice, h->stream));
+  launch_kill(h->d, m, h->stream);
+  return check_err(h);
+}
+
+int swim_set_default_loss(swim_handle* h, uint32_t pct) {
+  if (!h || pct > 100) return SWIM_EINVAL;
+  h->loss = pct;
+  return push_epoch(h);
+}
+
+int swim_set_partition(swim_handle* h, const uint32_t* g) {
+  if (!h) return SWIM_EINVAL;
+  if (g) {
+    h->group.assign(g, g + h->d.N);
+    h->partitioned = true;
+  } else {
+    h->partitioned = false;
+  }
+  return push_epoch(h);
+}
+
+int swim_unblock_all(swim_handle* h) {
+  if (!h) return SWIM_EINVAL;
+  h->partitioned = false;
+  return push_epoch(h);
+}
+
+int swim_current_tick(swim_handle* h, uint64_t* t) {
+  if (!h || !t) return SWIM_EINVAL;
+  *t = h->tick;
+  return SWIM_OK;
+}
+
+int swim_read_row(swim_handle* h, uint32_t obs, uint64_t* out, size_t cap) {
+  if (!h || obs >= h->d.N || cap < h->d.N) return SWIM_EINVAL;
+  HIPCK(hipStreamSynchronize(h->stream));
+  HIPCK(hipMemcpy(out, h->d.row + (size_t)obs * h->d.N, 8ull * h->d.N, hipMemcpyDeviceToHost));
+  for (uint32_t s = 0; s < h->d.N; ++s)
+    if (rec_status(out[s]) == ST_ABSENT) out[s] = 0;
+  return SWIM_OK;
+}
+
+int swim_state_hash(swim_handle* h, uint64_t* out, size_t cap) {
+  if (!h || cap < 6ull * h->d.N) return SWIM_EINVAL;
+  uint64_t* dout = nullptr;
+  HIPCK(hipMalloc(&dout, 48ull * h->d.N));
+  launch_hash(h->d, dout, (uint32_t)h->tick, h->stream);
+  HIPCK(hipStreamSynchronize(h->stream));
+  HIPCK(hipMemcpy(out, dout, 48ull * h->d.N, hipMemcpyDeviceToHost));
+  hipFree(dout);
+  return check_err(h);
+}
+
+int swim_read_lists(swim_handle* h, uint32_t obs, uint32_t* fd, uint32_t* fd_len, uint32_t* gl, uint32_t* g_len,
+                    size_t cap, int32_t* cursors) {
+  if (!h || obs >= h->d.N) return SWIM_EINVAL;
+  HIPCK(hipStreamSynchronize(h->stream));
+  uint32_t fl = 0, glen = 0;
+  HIPCK(hipMemcpy(&fl, h->d.fdLen + obs, 4, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(&glen, h->d.gLen + obs, 4, hipMemcpyDeviceToHost));
+  if (fl > cap || glen > cap) return SWIM_EINVAL;
+  HIPCK(hipMemcpy(fd, h->d.fdl + (size_t)obs * h->d.LCAP, 4ull * fl, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(gl, h->d.gl + (size_t)obs * h->d.LCAP, 4ull * glen, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(&cursors[0], h->d.pingIdx + obs, 4, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(&cursors[1], h->d.remoteIdx + obs, 4, hipMemcpyDeviceToHost));
+  *fd_len = fl;
+  *g_len = glen;
+  return SWIM_OK;
+}
+
+int swim_read_gossips(swim_handle* h, uint32_t obs, uint64_t* ids, uint32_t* inf, size_t cap, size_t* n_out) {
+  if (!h || obs >= h->d.N || !n_out) return SWIM_EINVAL;
+  HIPCK(hipStreamSynchronize(h->stream));
+  const Dev& d = h->d;
+  std::vector<uint32_t> used(d.SLOTS), col(d.SLOTS);
+  std::vector<uint64_t> gid(d.SLOTS);
+  HIPCK(hipMemcpy(used.data(), d.slot_used, 4ull * d.SLOTS, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(gid.data(), d.slot_gid, 8ull * d.SLOTS, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy2D(col.data(), 4, d.S + obs, 4ull * d.N, 4, d.SLOTS, hipMemcpyDeviceToHost));
+  uint32_t first = 0;
+  HIPCK(hipMemcpy(&first, d.firstGossip + obs, 4, hipMemcpyDeviceToHost));
+  std::vector<std::pair<uint64_t, uint32_t>> out;
+  for (uint32_t g = 0; g < d.SLOTS; ++g) {
+    uint32_t e = col[g];
+    if (!used[g] || (e & S_TICK_MASK) == 0 || (e & S_SWEPT)) continue;
+    uint32_t c = (e & S_TICK_MASK) - 1;
+    if (c >= h->tick) continue;  // receipt of the next tick's P4
+    uint32_t rb = (first == NEVER || c <= first) ? 0 : (c - first + d.gossip_t - 1) / d.gossip_t;
+    out.emplace_back(gid[g], rb);
+  }
+  std::sort(out.begin(), out.end());
+  if (out.size() > cap) return SWIM_ECAPACITY;
+  for (size_t i = 0; i < out.size(); ++i) {
+    ids[i] = out[i].first;
+    inf[i] = out[i].second;
+  }
+  *n_out = out.size();
+  return SWIM_OK;
+}
+
+int swim_drain_events(swim_handle* h, swim_event* out, size_t cap, size_t* n_out) {
+  if (!h || !n_out) return SWIM_EINVAL;
+  HIPCK(hipStreamSynchronize(h->stream));
+  uint32_t n = 0;
+  HIPCK(hipMemcpy(&n, h->d.ev_n, 4, hipMemcpyDeviceToHost));
+  n = std::min(n, h->d.EVCAP);
+  if (n) {
+    size_t base = h->host_events.size();
+    h->host_events.resize(base + n);
+    HIPCK(hipMemcpy(h->host_events.data() + base, h->d.ev, sizeof(swim_event) * n, hipMemcpyDeviceToHost));
+    HIPCK(hipMemset(h->d.ev_n, 0, 4));
+  }
+  auto& ev = h->host_events;
+  std::stable_sort(ev.begin(), ev.end(), [](const swim_event& a, const swim_event& b) {
+    if (a.tick != b.tick) return a.tick < b.tick;
+    if (a.observer != b.observer) return a.observer < b.observer;
+    return a.seq < b.seq;
+  });
+  size_t k = std::min(cap, ev.size());
+  std::copy(ev.begin(), ev.begin() + (long)k, out);
+  ev.erase(ev.begin(), ev.begin() + (long)k);
+  *n_out = k;
+  return SWIM_OK;
+}
+
+int swim_counters_get(swim_handle* h, swim_counters* out) {
+  if (!h || !out) return SWIM_EINVAL;
+  HIPCK(hipStreamSynchronize(h->stream));
+  unsigned long long c[C_NCTR];
+  HIPCK(hipMemcpy(c, h->d.ctr, sizeof(c), hipMemcpyDeviceToHost));
+  std::memset(out, 0, sizeof(*out));
+  out->tick = h->tick;
+  out->record_compares = c[C_R];
+  out->row_writes = c[C_W];
+  out->messages = c[C_M];
+  out->gossip_messages = c[C_G];
+  out->events = c[C_E];
+  out->messages_lost = c[C_LOST];
+  out->gossips_created = c[C_GCREATED];
+  out->sync_merges = c[C_SYNCMERGE];
+  out->reserved[0] = h->bytes;  // device bytes allocated
+  return SWIM_OK;
+}
+
+const char* swim_last_error(swim_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+// debugging aid (not part of the ABI header): one member's gossip-round ring: [tick, spread, cnt, targets...] x LOGW
+int swimdbg_read_log(swim_handle* h, uint32_t m, uint32_t* out, size_t cap, uint32_t* logw, uint32_t* fanout,
+                     uint32_t* pos) {
+  const Dev& d = h->d;
+  size_t need = (size_t)d.LOGW * (3 + d.F);
+  if (cap < need) return SWIM_EINVAL;
+  HIPCK(hipStreamSynchronize(h->stream));
+  std::vector<uint32_t> t(d.LOGW), sp(d.LOGW), c(d.LOGW), tg((size_t)d.LOGW * d.F);
+  HIPCK(hipMemcpy(t.data(), d.log_tick + (size_t)m * d.LOGW, 4ull * d.LOGW, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(sp.data(), d.log_spread + (size_t)m * d.LOGW, 4ull * d.LOGW, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(c.data(), d.log_cnt + (size_t)m * d.LOGW, 4ull * d.LOGW, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(tg.data(), d.log_tg + (size_t)m * d.LOGW * d.F, 4ull * d.LOGW * d.F, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(pos, d.log_pos + m, 4, hipMemcpyDeviceToHost));
+  for (uint32_t e = 0; e < d.LOGW; ++e) {
+    uint32_t* o = out + (size_t)e * (3 + d.F);
+    o[0] = t[e];
+    o[1] = sp[e];
+    o[2] = c[e];
+    for (uint32_t i = 0; i < d.F; ++i) o[3 + i] = tg[(size_t)e * d.F + i];
+  }
+  *logw = d.LOGW;
+  *fanout = d.F;
+  return SWIM_OK;
+}
+
+}  // extern "C"

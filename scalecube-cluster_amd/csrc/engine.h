@@ -1,0 +1,121 @@
+// engine.h — device-resident state of libswimhip and the per-tick kernel pipeline.
+//
+// Layout in HBM, one GPU, N members (all arrays are SoA; "per member" = indexed by observer id):
+//   row        u64[N][N]          membership table + metadata bit + suspicion deadline (swim_common.h)
+//   fdl, gl    u32[N][LCAP]       FailureDetectorImpl.pingMembers / GossipProtocolImpl.remoteMembers
+//   S          u32[SLOTS][N]      gossip slot x holder: creation tick | PENDING | SWEPT | REBORN
+//   logs       per member ring of the last LOGW gossip rounds: (tick, spread, targets[F])
+//   subs/paths/fetches/groups      fixed-capacity per-member request state (virtual remote hops)
+//   msgs       SYNC / SYNC_ACK records, double-buffered by tick parity; payload = the sender's live row
+//              (copy-on-write into the arena if the sender writes its row later in the same tick)
+#pragma once
+#include <stdint.h>
+
+#include "swim_common.h"
+
+namespace swim {
+
+constexpr uint32_t NEVER = 0xFFFFFFFFu;
+constexpr uint32_t MAX_EPOCHS = 8;
+constexpr uint32_t SUBCAP = 8, PATHCAP = 8, FREC = 8, GREC = 8;
+constexpr uint32_t CH = 1024;  // subjects per SYNC-diff chunk
+
+// S entry flags (gossip slot x member)
+constexpr uint32_t S_PENDING = 1u << 29, S_SWEPT = 1u << 30, S_REBORN = 1u << 31;
+constexpr uint32_t S_TICK_MASK = (1u << 29) - 1u;
+
+// device error bits
+constexpr uint32_t E_SLOTS = 1, E_FETCH = 2, E_SUBS = 4, E_PATHS = 8, E_GROUPS = 16, E_MSGS = 32, E_ARENA = 64,
+                   E_POOL = 128, E_LIST = 256, E_DELIV = 512, E_RECEIPTS = 1024, E_CONTACTS = 2048,
+                   E_REBORN = 4096, E_LOGWIN = 8192, E_EPOCH = 16384, E_EVENTS = 32768, E_SORTCAP = 65536;
+
+// counters (swim_counters order after .tick)
+enum Ctr { C_R = 0, C_W, C_M, C_G, C_E, C_LOST, C_GCREATED, C_SYNCMERGE, C_NCTR = 16 };
+
+struct SyncMsg {
+  uint32_t src, dst, kind, seq, cid_iss, cid_cnt;
+  uint32_t payload;  // NEVER = sender's live row, else arena row index
+  uint32_t psize;    // filled by the diff kernel: present records in the payload
+};
+
+struct Dev {
+  // ---- configuration ----
+  uint32_t N, F, kreq, ping_t, pingTimeout_t, gossip_t, sync_t, syncTimeout_t, md_t, lat, suspMult, repeatMult;
+  uint32_t seed_lo, seed_hi, init_mode, flags, n_seeds;
+  uint32_t seeds[16];
+  uint32_t LCAP, FCAP, GRCAP, LOGW, SLOTS, MSGCAP, NCHUNK, POOLCAP, EVCAP, DCAP, RCAP, ARENA_ROWS, LOOKBACK, HCAP;
+
+  // ---- network / fault history (NetworkEmulator settings per epoch) ----
+  uint32_t* dead_tick;  // [N] tick from which the member is dead, NEVER = alive
+  uint32_t* ep_from;    // [MAX_EPOCHS] first tick of each settings epoch (NEVER = unused)
+  uint32_t* ep_loss;    // [MAX_EPOCHS]
+  uint32_t* ep_part;    // [MAX_EPOCHS] partition active
+  uint32_t* ep_group;   // [MAX_EPOCHS][N]
+  uint32_t* md_version; // [N]
+
+  // ---- per member scalars ----
+  uint32_t *tsize, *fdLen, *gLen, *fdPeriod, *gPeriod, *gCounter, *nextPing, *nextGossip, *nextSync, *cidCnt, *syncSeq,
+      *evSeq, *held, *timerMin, *initFlags, *initDeadline, *initCidBase, *initN, *firstGossip, *nsub, *npath, *nfetch;
+  int32_t *pingIdx, *remoteIdx;
+  uint32_t* sel;  // [N][8]
+  uint64_t* evHash;
+
+  uint64_t* row;  // [N][N]
+  uint32_t *fdl, *gl;  // [N][LCAP]
+
+  uint32_t* subs;    // [N][SUBCAP][4]  cnt, kind, target, deadline
+  uint32_t* paths;   // [N][PATHCAP][5] cnt, stage, tick, a, b
+  uint32_t* fetch;   // [N][FCAP][FREC]
+  uint32_t* groups;  // [N][GRCAP][GREC]  pending Mono.whenDelayError groups (SYNC replies, initial sync)
+
+  // ---- gossip round of the current tick ----
+  uint32_t *tround, *tcnt, *tspread, *tperiod, *T, *tcontact;  // T, tcontact: [N][F]
+  uint32_t *log_tick, *log_spread, *log_cnt, *log_tg, *log_pos;  // [N][LOGW], tg [N][LOGW][F], pos [N]
+
+  // ---- gossip slots ----
+  uint64_t* slot_gid;
+  uint32_t* slot_subj;
+  uint32_t* slot_ctick;  // creation tick of the gossip (origin's spread)
+  uint64_t* slot_key;  // inc | status<<32 (status may be DEAD)
+  int32_t* slot_holders;
+  uint32_t* slot_used;
+  uint32_t* S;  // [SLOTS][N]
+  uint32_t* free_list;
+  int32_t* free_top;
+  uint64_t* deliv;  // (slot << 32) | member
+  uint32_t* deliv_n;
+  // receipts produced at tick k, consumed in P4 of tick k+1
+  uint64_t* rc_raw;  // (member << 32) | slot
+  uint32_t* rc_n;
+  uint32_t *rc_cnt, *rc_off, *rc_fill;  // [N]
+  uint32_t* rc_slot;  // [RCAP] sorted by member then gossip id
+  uint64_t* rc_key;   // [RCAP] gossip id sort key
+  uint32_t *active, *nactive;  // slots in use at the start of the gossip phase
+  uint64_t* hist;  // [HCAP][6] incarnation history: tag, gid, member | n << 32, 6 x u32 creation ticks
+
+  // ---- SYNC messages (double-buffered by tick parity) ----
+  SyncMsg* msgs[2];
+  uint32_t* nmsg;  // [2]
+  uint64_t* arena[2];
+  uint32_t* arena_used;  // [2]
+  uint32_t *m_cnt, *m_off, *m_fill, *m_idx;  // routing of the previous tick's messages
+  uint64_t* m_key;                           // (src << 32 | syncSeq) sort key
+  uint32_t* chunk_meta;                      // [MSGCAP][NCHUNK][2] (pool offset, count)
+  uint64_t* pool;                            // candidate (subject << 34 | key)
+  uint32_t* pool_used;
+
+  // ---- outputs ----
+  uint32_t* ev;  // [EVCAP][8] swim_event
+  uint32_t* ev_n;
+  unsigned long long* ctr;  // [C_NCTR]
+  uint32_t* err;            // [4] bits, info...
+};
+
+// host-side kernel launchers (one HIP stream)
+struct Launch;
+void launch_init(const Dev& d, void* stream);
+void launch_tick(const Dev& d, uint32_t k, void* stream);
+void launch_kill(const Dev& d, uint32_t member, void* stream);
+void launch_hash(const Dev& d, uint64_t* out, uint32_t now, void* stream);
+
+}  // namespace swim

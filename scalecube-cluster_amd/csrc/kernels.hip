@@ -1,0 +1,635 @@
+// kernels.hip — initialisation, message routing, the SYNC-payload diff, the gossip data plane, kill and state hashes.
+#include <hip/hip_runtime.h>
+
+#include "dev_util.h"
+
+namespace swim {
+
+__global__ void k_member_tick(Dev d, uint32_t k);  // member.hip
+
+// ------------------------------------------------------------------------------------------------------------
+// init (SEMANTICS.md §3)
+__device__ __forceinline__ uint32_t init_draw(const Dev& d, uint32_t m, uint32_t what, uint32_t i) {
+  return philox(m, what, i, 0, d.seed_lo ^ SALT_INIT, d.seed_hi).x;
+}
+
+__global__ void k_init_members(Dev d) {
+  uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= d.N) return;
+  bool pre = d.init_mode == 1;
+  d.tsize[m] = pre ? d.N : 1;
+  d.fdLen[m] = pre ? d.N - 1 : 0;
+  d.gLen[m] = pre ? d.N - 1 : 0;
+  d.fdPeriod[m] = d.gPeriod[m] = d.gCounter[m] = 0;
+  d.nextPing[m] = pre ? 1 + init_draw(d, m, 1, 0) % d.ping_t : d.ping_t;
+  uint32_t ng = pre ? 1 + init_draw(d, m, 2, 0) % d.gossip_t : d.gossip_t;
+  d.nextGossip[m] = ng;
+  d.firstGossip[m] = ng;
+  d.nextSync[m] = pre ? 1 + init_draw(d, m, 3, 0) % d.sync_t : NEVER;
+  d.cidCnt[m] = d.syncSeq[m] = d.evSeq[m] = d.held[m] = 0;
+  d.timerMin[m] = NEVER;
+  d.initFlags[m] = d.initDeadline[m] = d.initCidBase[m] = d.initN[m] = 0;
+  d.nsub[m] = d.npath[m] = d.nfetch[m] = 0;
+  d.pingIdx[m] = 0;
+  d.remoteIdx[m] = pre ? 0 : -1;
+  for (int i = 0; i < 8; ++i) d.sel[(size_t)m * 8 + i] = 0;
+  d.evHash[m] = 0;
+  d.tround[m] = 0;
+  d.log_pos[m] = 0;
+  d.dead_tick[m] = NEVER;
+  d.md_version[m] = 0;
+  d.rc_cnt[m] = 0;
+  d.rc_off[m] = 0;
+  d.m_cnt[m] = 0;
+  d.m_off[m] = 0;
+  for (uint32_t g = 0; g < d.GRCAP; ++g) d.groups[((size_t)m * d.GRCAP + g) * GREC + 5] = 0;
+  for (uint32_t e = 0; e < d.LOGW; ++e) d.log_tick[(size_t)m * d.LOGW + e] = NEVER;
+}
+
+__global__ void k_init_rows(Dev d) {
+  size_t total = (size_t)d.N * d.N;
+  uint64_t full = rec_key(ST_ALIVE, 0) | META_BIT;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t m = (uint32_t)(i / d.N), s = (uint32_t)(i % d.N);
+    d.row[i] = (d.init_mode == 1 || m == s) ? full : 0ull;
+  }
+}
+
+__global__ void k_init_lists(Dev d) {
+  if (d.init_mode != 1 || d.N < 2) return;
+  uint32_t n = d.N - 1;
+  size_t total = (size_t)d.N * n;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t m = (uint32_t)(i / n), p = (uint32_t)(i % n);
+    for (uint32_t w = 0; w < 2; ++w) {
+      FeistelPerm P = make_perm(n, init_draw(d, m, 16 + 4 * w + 0, 0), init_draw(d, m, 16 + 4 * w + 1, 0),
+                                init_draw(d, m, 16 + 4 * w + 2, 0), init_draw(d, m, 16 + 4 * w + 3, 0));
+      uint32_t j = feistel(P, p);
+      uint32_t v = j < m ? j : j + 1;
+      (w == 0 ? d.fdl : d.gl)[(size_t)m * d.LCAP + p] = v;
+    }
+  }
+}
+
+__global__ void k_init_slots(Dev d) {
+  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= d.SLOTS) return;
+  d.slot_used[g] = 0;
+  d.slot_holders[g] = 0;
+  d.free_list[g] = d.SLOTS - 1 - g;
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// routing: counting sort by destination member, then per-destination sort by a 64-bit key
+__global__ void k_count_dst(const SyncMsg* msgs, const uint32_t* nmsg, uint32_t cap, uint32_t* cnt) {
+  uint32_t n = *nmsg < cap ? *nmsg : cap;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    atomicAdd(&cnt[msgs[i].dst], 1u);
+}
+__global__ void k_scatter_dst(const SyncMsg* msgs, const uint32_t* nmsg, uint32_t cap, const uint32_t* off,
+                              uint32_t* fill, uint32_t* idx, uint64_t* key) {
+  uint32_t n = *nmsg < cap ? *nmsg : cap;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const SyncMsg& m = msgs[i];
+    uint32_t p = off[m.dst] + atomicAdd(&fill[m.dst], 1u);
+    idx[p] = i;
+    key[p] = ((uint64_t)m.src << 32) | m.seq;
+  }
+}
+__global__ void k_count_rc(const uint64_t* raw, const uint32_t* n_, uint32_t cap, uint32_t* cnt) {
+  uint32_t n = *n_ < cap ? *n_ : cap;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    atomicAdd(&cnt[(uint32_t)(raw[i] >> 32)], 1u);
+}
+__global__ void k_scatter_rc(const Dev d, const uint64_t* raw, const uint32_t* n_, uint32_t cap, const uint32_t* off,
+                             uint32_t* fill, uint32_t* idx, uint64_t* key) {
+  uint32_t n = *n_ < cap ? *n_ : cap;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    uint32_t t = (uint32_t)(raw[i] >> 32), g = (uint32_t)raw[i];
+    uint32_t p = off[t] + atomicAdd(&fill[t], 1u);
+    idx[p] = g;
+    key[p] = d.slot_gid[g];
+  }
+}
+
+// exclusive scan of n counts by one 1024-thread block (serial chunk per thread + block scan)
+__global__ void __launch_bounds__(1024) k_scan(const uint32_t* in, uint32_t* out, uint32_t n) {
+  __shared__ uint32_t part[1024];
+  uint32_t t = threadIdx.x;
+  uint32_t per = (n + 1023) / 1024;
+  uint32_t b = t * per, e = b + per < n ? b + per : n;
+  uint32_t s = 0;
+  for (uint32_t i = b; i < e; ++i) s += in[i];
+  part[t] = s;
+  __syncthreads();
+  for (uint32_t o = 1; o < 1024; o <<= 1) {
+    uint32_t v = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - s;
+  for (uint32_t i = b; i < e; ++i) {
+    uint32_t c = in[i];
+    out[i] = run;
+    run += c;
+  }
+}
+
+// per-segment sort of (key, val) by key: one block per segment, bitonic in LDS (<= 4096 entries)
+constexpr uint32_t SORT_MAX = 4096;
+__global__ void __launch_bounds__(256) k_seg_sort(uint64_t* key, uint32_t* val, const uint32_t* off, const uint32_t* cnt,
+                                                  uint32_t nseg, uint32_t* err) {
+  __shared__ uint64_t K[SORT_MAX];
+  __shared__ uint32_t V[SORT_MAX];
+  for (uint32_t sgi = blockIdx.x; sgi < nseg; sgi += gridDim.x) {
+    uint32_t n = cnt[sgi];
+    if (n <= 1) continue;
+    if (n > SORT_MAX) {
+      if (threadIdx.x == 0) atomicOr(err, E_SORTCAP);
+      continue;
+    }
+    uint32_t o = off[sgi];
+    uint32_t p2 = 1;
+    while (p2 < n) p2 <<= 1;
+    for (uint32_t i = threadIdx.x; i < p2; i += blockDim.x) {
+      K[i] = i < n ? key[o + i] : ~0ull;
+      V[i] = i < n ? val[o + i] : 0;
+    }
+    __syncthreads();
+    for (uint32_t size = 2; size <= p2; size <<= 1)
+      for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+        for (uint32_t i = threadIdx.x; i < p2; i += blockDim.x) {
+          uint32_t j = i ^ stride;
+          if (j > i) {
+            bool up = (i & size) == 0;
+            if ((K[i] > K[j]) == up) {
+              uint64_t tk = K[i];
+              K[i] = K[j];
+              K[j] = tk;
+              uint32_t tv = V[i];
+              V[i] = V[j];
+              V[j] = tv;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+      key[o + i] = K[i];
+      val[o + i] = V[i];
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// k_sync_diff: for every SYNC / SYNC_ACK sent in tick k-1, stream the payload row (the sender's live row, or its
+// copy-on-write snapshot) against the receiver's row and extract, per 1024-subject chunk and in subject order,
+// the records that differ (the eager `!r1.equals(table.get(id))` filter of syncMembership, :456-467).
+// This is the HBM-bound hot loop: 2 x 8 B read per subject per merge.
+__global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b) {
+  __shared__ uint32_t scan[256];
+  __shared__ uint32_t base;
+  uint32_t nmsg = d.nmsg[b] < d.MSGCAP ? d.nmsg[b] : d.MSGCAP;
+  uint32_t total = nmsg * d.NCHUNK;
+  for (uint32_t w = blockIdx.x; w < total; w += gridDim.x) {
+    uint32_t mi = w / d.NCHUNK, c = w % d.NCHUNK;
+    const SyncMsg& mm = d.msgs[b][mi];
+    const uint64_t* pay = mm.payload == NEVER ? d.row + (size_t)mm.src * d.N : d.arena[b] + (size_t)mm.payload * d.N;
+    const uint64_t* rcv = d.row + (size_t)mm.dst * d.N;
+    uint32_t s0 = c * CH + threadIdx.x * 4;
+    uint64_t cand[4];
+    uint32_t nc = 0, np = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint32_t s = s0 + j;
+      if (s < d.N) {
+        uint64_t r1 = pay[s] & KEY_MASK;
+        if (rec_status(r1) != ST_ABSENT) {
+          np++;
+          if (r1 != (rcv[s] & KEY_MASK)) cand[nc++] = ((uint64_t)s << 34) | r1;
+        }
+      }
+    }
+    scan[threadIdx.x] = nc | (np << 16);
+    __syncthreads();
+    for (uint32_t o = 1; o < 256; o <<= 1) {
+      uint32_t v = threadIdx.x >= o ? scan[threadIdx.x - o] : 0;
+      __syncthreads();
+      scan[threadIdx.x] += v;
+      __syncthreads();
+    }
+    uint32_t incl = scan[threadIdx.x];
+    uint32_t tot = scan[255];
+    uint32_t totc = tot & 0xFFFF, totp = tot >> 16;
+    if (threadIdx.x == 0) {
+      uint32_t bo = totc ? atomicAdd(d.pool_used, totc) : 0;
+      if (bo + totc > d.POOLCAP) {
+        atomicOr(d.err, E_POOL);
+        totc = 0;
+        bo = 0;
+      }
+      base = bo;
+      uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NCHUNK + c) * 2;
+      cm[0] = bo;
+      cm[1] = totc;
+      if (totp) atomicAdd(&d.msgs[b][mi].psize, totp);
+    }
+    __syncthreads();
+    uint32_t excl = (incl & 0xFFFF) - nc;
+    if (base + excl + nc <= d.POOLCAP)
+      for (uint32_t j = 0; j < nc; ++j) d.pool[(size_t)base + excl + j] = cand[j];
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// gossip data plane (GossipProtocolImpl.java:139-308 for all members at once)
+//
+// infectedFrom is never stored. `y ∈ infectedFrom_x(g)` at x's round at tick tau holds iff y delivered g to x by a
+// send in one of y's logged rounds t2 with c_x <= t2 + lat <= tau, where c_x is the creation tick of x's current
+// state for g. Whether such a send was delivered depends, one level down, on whether x had delivered g to y
+// earlier (then y skips x), and so on. The dependency only runs over the contact events between the pair
+// (x's rounds that targeted y, y's rounds that targeted x). Those are replayed in tick order as a small dynamic
+// program, so there is no recursion.
+struct Contact {
+  uint32_t tick, slot, spread, dir;  // dir 0: y -> x, 1: x -> y
+};
+
+// incarnation history of (gid, member): creation ticks of swept incarnations (rebirths are rare)
+__device__ __forceinline__ uint64_t hist_tag(uint64_t gid, uint32_t member) {
+  return mix64(gid ^ ((uint64_t)member * 0x9E3779B97F4A7C15ull)) | 1ull;
+}
+
+__device__ void hist_push(const Dev& d, uint64_t gid, uint32_t member, uint32_t cprev) {
+  uint64_t tag = hist_tag(gid, member);
+  uint32_t mask = d.HCAP - 1;
+  for (uint32_t p = 0; p < d.HCAP; ++p) {
+    unsigned long long* e = (unsigned long long*)(d.hist + (size_t)((tag + p) & mask) * 6);
+    unsigned long long old = atomicCAS(e, 0ull, (unsigned long long)tag);
+    if (old != 0ull && old != tag) continue;
+    if (old == 0ull) {
+      e[1] = gid;
+      e[2] = member;
+    }
+    uint32_t n = (uint32_t)(e[2] >> 32);  // total rebirths so far; the ring keeps the latest 6
+    uint32_t* c = (uint32_t*)(e + 3);
+    c[n % 6] = cprev;
+    e[2] = (uint64_t)member | ((uint64_t)(n + 1) << 32);
+    return;
+  }
+  atomicOr(d.err, E_REBORN);
+}
+
+// creation tick of member's incarnation of g that existed at tick tau (NEVER if none)
+__device__ uint32_t inc_at(const Dev& d, uint32_t member, uint32_t g, uint64_t gid, uint32_t tau) {
+  uint32_t e = d.S[(size_t)g * d.N + member];
+  if (!s_ever(e)) return NEVER;
+  uint32_t c = s_ctick(e);
+  if (c <= tau) return c;
+  if (!(e & S_REBORN)) return NEVER;
+  uint64_t tag = hist_tag(gid, member);
+  uint32_t mask = d.HCAP - 1;
+  for (uint32_t p = 0; p < d.HCAP; ++p) {
+    const uint64_t* h = d.hist + (size_t)((tag + p) & mask) * 6;
+    if (h[0] == 0) break;
+    if (h[0] != tag || h[1] != gid || (uint32_t)h[2] != member) continue;
+    uint32_t n = (uint32_t)(h[2] >> 32), best = NEVER, oldest = NEVER;
+    const uint32_t* cc = (const uint32_t*)(h + 3);
+    uint32_t kept = n < 6 ? n : 6;
+    for (uint32_t i = 0; i < kept; ++i) {
+      if (cc[i] < oldest) oldest = cc[i];
+      if (cc[i] <= tau && (best == NEVER || cc[i] > best)) best = cc[i];
+    }
+    if (best == NEVER && n > 6 && tau < oldest) atomicOr(d.err, E_REBORN);  // an incarnation the ring dropped
+    return best;
+  }
+  return NEVER;
+}
+
+__device__ __noinline__ bool blocked_pair(const Dev& d, uint32_t x, uint32_t y, uint32_t g, uint64_t gid,
+                                          uint32_t tau, uint32_t cx) {
+  const uint32_t lat = d.lat;
+  Contact ev[64];
+  uint32_t n = 0;
+  const uint32_t born = d.slot_ctick[g];  // no member could send g before it was created
+  uint32_t oldest[2] = {0, 0};  // oldest tick still in each log, 0 if the ring never wrapped
+  for (int side = 0; side < 2; ++side) {
+    uint32_t from = side == 0 ? y : x, to = side == 0 ? x : y;
+    bool wrapped = d.log_pos[from] > d.LOGW;
+    uint32_t old = NEVER;
+    for (uint32_t e = 0; e < d.LOGW; ++e) {
+      size_t li = (size_t)from * d.LOGW + e;
+      uint32_t t2 = d.log_tick[li];
+      if (t2 == NEVER) continue;
+      if (t2 < old) old = t2;
+      if (t2 + lat > tau || t2 < born) continue;
+      uint32_t cnt = d.log_cnt[li];
+      for (uint32_t s2 = 0; s2 < cnt; ++s2)
+        if (d.log_tg[li * d.F + s2] == to) {
+          if (n == 64) {
+            atomicOr(d.err, E_CONTACTS);
+            return false;
+          }
+          uint32_t j = n++;
+          while (j > 0 && ev[j - 1].tick > t2) {
+            ev[j] = ev[j - 1];
+            --j;
+          }
+          ev[j] = Contact{t2, s2, d.log_spread[li], (uint32_t)side};
+        }
+    }
+    oldest[side] = wrapped ? old : 0;
+  }
+  // oldest[0] is y's log (y -> x events), oldest[1] is x's log (x -> y events). Find which deliveries can matter:
+  // into x from cx on (the answer), and into a sender from its incarnation start for every relevant event
+  // (its isInfected check). The fixpoint runs over at most 64 events. The ring must cover those ranges.
+  uint32_t lo_in[2] = {cx, NEVER};  // [0]: deliveries into x, [1]: deliveries into y
+  uint32_t cinc[64];
+  for (uint32_t i = 0; i < n; ++i) cinc[i] = NEVER - 1;  // not computed yet
+  for (int pass = 0; pass < 8; ++pass) {
+    bool changed = false;
+    for (int i = (int)n - 1; i >= 0; --i) {
+      const Contact& c = ev[i];
+      uint32_t rin = c.dir == 0 ? 0 : 1;  // receiver index into lo_in
+      if (lo_in[rin] == NEVER || c.tick + lat < lo_in[rin]) continue;
+      if (cinc[i] == NEVER - 1) cinc[i] = inc_at(d, c.dir == 0 ? y : x, g, gid, c.tick);
+      uint32_t cs = cinc[i];
+      uint32_t snd = c.dir == 0 ? y : x;
+      if (cs == NEVER || rounds_before(d, snd, cs) + c.spread < rounds_before(d, snd, c.tick)) continue;
+      uint32_t sin = 1 - rin;
+      if (lo_in[sin] == NEVER || cs < lo_in[sin]) {
+        lo_in[sin] = cs;
+        changed = true;
+      }
+    }
+    if (!changed) break;
+  }
+  // deliveries into x come from y's log (oldest[0]); into y from x's log (oldest[1])
+  if ((lo_in[0] != NEVER && lo_in[0] < oldest[0] + lat) || (lo_in[1] != NEVER && lo_in[1] < oldest[1] + lat)) {
+    if (atomicOr(d.err, E_LOGWIN) == 0) {
+      d.err[1] = tau;
+      d.err[2] = lo_in[0];
+      d.err[3] = lo_in[1];
+      d.err[4] = oldest[0];
+      d.err[5] = oldest[1];
+    }
+  }
+  uint32_t del[2][64];
+  uint32_t nd[2] = {0, 0};
+  for (uint32_t i = 0; i < n; ++i) {
+    const Contact& c = ev[i];
+    uint32_t snd = c.dir == 0 ? y : x;
+    // the sender held g at that round (its incarnation then), inside its spread window (selectGossipsToSend :246)
+    uint32_t cs = inc_at(d, snd, g, gid, c.tick);
+    if (cs == NEVER) continue;
+    if (rounds_before(d, snd, cs) + c.spread < rounds_before(d, snd, c.tick)) continue;
+    // the receiver delivered g to the sender during that incarnation: infectedFrom (isInfected :247)
+    uint32_t od = 1 - c.dir;  // opposite direction
+    bool blocked = false;
+    for (uint32_t q = 0; q < nd[od] && !blocked; ++q) blocked = del[od][q] + lat >= cs && del[od][q] + lat <= c.tick;
+    if (blocked) continue;
+    if (lost_gossip(d, snd, c.dir == 0 ? x : y, c.tick, c.slot, gid)) continue;
+    del[c.dir][nd[c.dir]++] = c.tick;
+  }
+  for (uint32_t q = 0; q < nd[0]; ++q)
+    if (del[0][q] + lat >= cx) return true;
+  return false;
+}
+
+__global__ void k_gossip_active(Dev d, uint32_t* active, uint32_t* nactive) {
+  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < d.SLOTS && d.slot_used[g]) active[atomicAdd(nactive, 1u)] = g;
+}
+
+// contact flags: did target t = T[m][s] choose m in a logged round inside the look-back window?
+__global__ void k_gossip_contacts(Dev d, uint32_t k) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= d.N * d.F) return;
+  uint32_t m = i / d.F, s = i % d.F;
+  uint32_t flag = 0;
+  if (d.tround[m] && s < d.tcnt[m]) {
+    uint32_t t = d.T[i];
+    for (uint32_t e = 0; e < d.LOGW && !flag; ++e) {
+      size_t lo = (size_t)t * d.LOGW + e;
+      uint32_t t2 = d.log_tick[lo];
+      if (t2 == NEVER || t2 >= k) continue;
+      uint32_t n = d.log_cnt[lo];
+      for (uint32_t s2 = 0; s2 < n; ++s2)
+        if (d.log_tg[lo * d.F + s2] == m) flag = 1;
+    }
+  }
+  d.tcontact[i] = flag;
+}
+
+// one thread per (active slot, member): the member's round sends of this gossip, then its sweep
+__global__ void __launch_bounds__(256) k_gossip_send(Dev d, uint32_t k, const uint32_t* active, const uint32_t* nactive) {
+  __shared__ unsigned long long red[256];
+  uint32_t na = *nactive;
+  uint32_t mchunks = (d.N + 255) / 256;
+  unsigned long long sends = 0;
+  for (uint32_t w = blockIdx.x; w < na * mchunks; w += gridDim.x) {
+    uint32_t g = active[w / mchunks];
+    uint32_t m = (w % mchunks) * 256 + threadIdx.x;
+    if (m >= d.N || !d.tround[m]) continue;
+    uint32_t* Sg = d.S + (size_t)g * d.N;
+    uint32_t e = Sg[m];
+    if (!s_held(e)) continue;
+    uint32_t c = s_ctick(e);
+    uint32_t infP = rounds_before(d, m, c), per = d.tperiod[m], sp = d.tspread[m];
+    uint64_t gid = d.slot_gid[g];
+    if (infP + sp >= per) {  // selectGossipsToSend window (:246)
+      uint32_t n = d.tcnt[m];
+      for (uint32_t s = 0; s < n; ++s) {
+        uint32_t t = d.T[(size_t)m * d.F + s];
+        if (d.tcontact[(size_t)m * d.F + s] && blocked_pair(d, m, t, g, gid, k, c)) continue;  // isInfected (:247)
+        sends++;
+        uint32_t et = Sg[t];
+        bool potential = !s_held(et);
+        if (!potential && d.tround[t]) {  // t sweeps g in its own round this tick -> a delivery re-creates it
+          uint32_t it = rounds_before(d, t, s_ctick(et));
+          potential = d.tperiod[t] > it + 2u * (d.tspread[t] + 1u);
+        }
+        if (!potential) continue;
+        if (lost_gossip(d, m, t, k, s, gid)) continue;
+        uint32_t old = atomicOr(&Sg[t], S_PENDING);
+        if (!(old & S_PENDING)) {
+          uint32_t di = atomicAdd(d.deliv_n, 1u);
+          if (di < d.DCAP)
+            d.deliv[di] = ((uint64_t)g << 32) | t;
+          else
+            atomicOr(d.err, E_DELIV);
+        }
+      }
+    }
+    if (per > infP + 2u * (sp + 1u)) {  // sweepGossips (:283-308)
+      atomicOr(&Sg[m], S_SWEPT);
+      atomicSub(&d.held[m], 1u);
+      atomicSub(&d.slot_holders[g], 1);
+    }
+  }
+  red[threadIdx.x] = sends;
+  __syncthreads();
+  for (uint32_t o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && red[0]) atomicAdd(&d.ctr[C_G], red[0]);
+}
+
+// first receipts (onGossipReq :176-180): create the holder state at tick k + lat and queue the record for P4
+__global__ void k_gossip_apply(Dev d, uint32_t k) {
+  uint32_t n = *d.deliv_n < d.DCAP ? *d.deliv_n : d.DCAP;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    uint64_t v = d.deliv[i];
+    uint32_t g = (uint32_t)(v >> 32), t = (uint32_t)v;
+    uint32_t* p = d.S + (size_t)g * d.N + t;
+    uint32_t e = *p & ~S_PENDING;
+    if (s_held(e)) {
+      *p = e;
+      continue;
+    }
+    if (s_ever(e)) hist_push(d, d.slot_gid[g], t, s_ctick(e));  // rebirth after a sweep (:176-180)
+    uint32_t ne = ((k + d.lat + 1u) & S_TICK_MASK) | (s_ever(e) ? S_REBORN : 0u);
+    *p = ne;
+    atomicAdd(&d.held[t], 1u);
+    atomicAdd(&d.slot_holders[g], 1);
+    uint32_t ri = atomicAdd(d.rc_n, 1u);
+    if (ri < d.RCAP)
+      d.rc_raw[ri] = ((uint64_t)t << 32) | g;
+    else
+      atomicOr(d.err, E_RECEIPTS);
+  }
+}
+
+// a slot nobody holds can never be sent again: clear its holder row and recycle it
+__global__ void __launch_bounds__(256) k_gossip_free(Dev d, const uint32_t* active, const uint32_t* nactive) {
+  uint32_t na = *nactive;
+  for (uint32_t a = blockIdx.x; a < na; a += gridDim.x) {
+    uint32_t g = active[a];
+    if (d.slot_holders[g] > 0) continue;
+    uint32_t* Sg = d.S + (size_t)g * d.N;
+    for (uint32_t s = threadIdx.x; s < d.N; s += blockDim.x) Sg[s] = 0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      d.slot_used[g] = 0;
+      int pos = atomicAdd(d.free_top, 1);
+      d.free_list[pos] = g;
+    }
+  }
+}
+
+// swim_kill: the member stops holding gossips (it can never send them again)
+__global__ void k_kill(Dev d, uint32_t m) {
+  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= d.SLOTS || !d.slot_used[g]) return;
+  if (s_held(d.S[(size_t)g * d.N + m])) atomicSub(&d.slot_holders[g], 1);
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// state hashes (SEMANTICS.md §8), one block per member
+__global__ void __launch_bounds__(256) k_hash(Dev d, uint64_t* out, uint32_t now) {
+  __shared__ unsigned long long red[4][256];
+  uint32_t m = blockIdx.x;
+  if (m >= d.N) return;
+  unsigned long long hr = 0, hf = 0, hg = 0, hgs = 0;
+  const uint64_t* row = d.row + (size_t)m * d.N;
+  for (uint32_t s = threadIdx.x; s < d.N; s += blockDim.x) {
+    uint64_t v = row[s];
+    if (rec_status(v) != ST_ABSENT) hr += hpair(s, v);
+  }
+  uint32_t fl = d.fdLen[m], gl = d.gLen[m];
+  for (uint32_t p = threadIdx.x; p < fl; p += blockDim.x) hf += hpair((uint64_t)p | (1ull << 40), d.fdl[(size_t)m * d.LCAP + p]);
+  for (uint32_t p = threadIdx.x; p < gl; p += blockDim.x) hg += hpair((uint64_t)p | (2ull << 40), d.gl[(size_t)m * d.LCAP + p]);
+  for (uint32_t g = threadIdx.x; g < d.SLOTS; g += blockDim.x) {
+    if (!d.slot_used[g]) continue;
+    uint32_t e = d.S[(size_t)g * d.N + m];
+    // receipts applied at the end of tick now-1 belong to P4 of tick `now`: not yet visible
+    if (s_held(e) && s_ctick(e) < now) hgs += hpair(d.slot_gid[g], rounds_before(d, m, s_ctick(e)));
+  }
+  red[0][threadIdx.x] = hr;
+  red[1][threadIdx.x] = hf;
+  red[2][threadIdx.x] = hg;
+  red[3][threadIdx.x] = hgs;
+  __syncthreads();
+  for (uint32_t o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o)
+      for (int q = 0; q < 4; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    uint64_t* o6 = out + (size_t)m * 6;
+    o6[0] = red[0][0];
+    o6[1] = red[1][0] + mix64((uint64_t)(int64_t)d.pingIdx[m] ^ 0xF00Dull) + fl;
+    o6[2] = red[2][0] + mix64((uint64_t)(int64_t)d.remoteIdx[m] ^ 0xBEEFull) + gl;
+    o6[3] = d.evHash[m];
+    o6[4] = red[3][0];
+    uint64_t ns = d.nextSync[m] == NEVER ? ~0ull : (uint64_t)d.nextSync[m];
+    o6[5] = hpair(hpair(hpair(d.cidCnt[m], d.syncSeq[m]), d.gCounter[m]), ns) +
+            mix64((uint64_t)d.fdPeriod[m] * 3 + (uint64_t)d.gPeriod[m] * 7);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// host launchers
+static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+void launch_init(const Dev& d, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_init_members, dim3(cdiv(d.N, 256)), dim3(256), 0, st, d);
+  hipLaunchKernelGGL(k_init_rows, dim3(4096), dim3(256), 0, st, d);
+  hipLaunchKernelGGL(k_init_lists, dim3(4096), dim3(256), 0, st, d);
+  hipLaunchKernelGGL(k_init_slots, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, st, d);
+}
+
+void launch_tick(const Dev& d, uint32_t k, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  uint32_t b = k & 1, pb = (k - 1) & 1;
+  // fresh per-tick output buffers for this tick's sends
+  hipMemsetAsync(d.nmsg + b, 0, sizeof(uint32_t), st);
+  hipMemsetAsync(d.arena_used + b, 0, sizeof(uint32_t), st);
+  hipMemsetAsync(d.pool_used, 0, sizeof(uint32_t), st);
+  hipMemsetAsync(d.m_cnt, 0, sizeof(uint32_t) * d.N, st);
+  if (k > 0) {
+    // route the previous tick's SYNC / SYNC_ACK messages by destination, sorted by (src, syncSeq)
+    hipLaunchKernelGGL(k_count_dst, dim3(64), dim3(256), 0, st, d.msgs[pb], d.nmsg + pb, d.MSGCAP, d.m_cnt);
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, d.m_cnt, d.m_off, d.N);
+    hipMemsetAsync(d.m_fill, 0, sizeof(uint32_t) * d.N, st);
+    hipLaunchKernelGGL(k_scatter_dst, dim3(64), dim3(256), 0, st, d.msgs[pb], d.nmsg + pb, d.MSGCAP, d.m_off, d.m_fill,
+                       d.m_idx, d.m_key);
+    hipLaunchKernelGGL(k_seg_sort, dim3(1024), dim3(256), 0, st, d.m_key, d.m_idx, d.m_off, d.m_cnt, d.N,
+                       d.err);
+    hipLaunchKernelGGL(k_sync_diff, dim3(2048), dim3(256), 0, st, d, pb);
+  }
+  hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.N, 256)), dim3(256), 0, st, d, k);
+  // gossip data plane for the rounds that ran in this tick
+  uint32_t* active = d.active;
+  uint32_t* nactive = d.nactive;
+  hipMemsetAsync(nactive, 0, sizeof(uint32_t), st);
+  hipMemsetAsync(d.deliv_n, 0, sizeof(uint32_t), st);
+  hipMemsetAsync(d.rc_n, 0, sizeof(uint32_t), st);
+  hipLaunchKernelGGL(k_gossip_active, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, st, d, active, nactive);
+  hipLaunchKernelGGL(k_gossip_contacts, dim3(cdiv((uint64_t)d.N * d.F, 256)), dim3(256), 0, st, d, k);
+  hipLaunchKernelGGL(k_gossip_send, dim3(8192), dim3(256), 0, st, d, k, active, nactive);
+  hipLaunchKernelGGL(k_gossip_apply, dim3(1024), dim3(256), 0, st, d, k);
+  hipMemsetAsync(d.rc_cnt, 0, sizeof(uint32_t) * d.N, st);
+  hipLaunchKernelGGL(k_count_rc, dim3(256), dim3(256), 0, st, d.rc_raw, d.rc_n, d.RCAP, d.rc_cnt);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, d.rc_cnt, d.rc_off, d.N);
+  hipMemsetAsync(d.rc_fill, 0, sizeof(uint32_t) * d.N, st);
+  hipLaunchKernelGGL(k_scatter_rc, dim3(256), dim3(256), 0, st, d, d.rc_raw, d.rc_n, d.RCAP, d.rc_off, d.rc_fill,
+                     d.rc_slot, d.rc_key);
+  hipLaunchKernelGGL(k_seg_sort, dim3(1024), dim3(256), 0, st, d.rc_key, d.rc_slot, d.rc_off,
+                     d.rc_cnt, d.N, d.err);
+  hipLaunchKernelGGL(k_gossip_free, dim3(1024), dim3(256), 0, st, d, active, nactive);
+}
+
+void launch_kill(const Dev& d, uint32_t member, void* stream) {
+  hipLaunchKernelGGL(k_kill, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, (hipStream_t)stream, d, member);
+}
+
+void launch_hash(const Dev& d, uint64_t* out, uint32_t now, void* stream) {
+  hipLaunchKernelGGL(k_hash, dim3(d.N), dim3(256), 0, (hipStream_t)stream, d, out, now);
+}
+
+}  // namespace swim

@@ -1,0 +1,888 @@
+// member.hip — k_member_tick: one thread per simulated member runs phases P1..P6 of SEMANTICS.md §4.
+//
+// This kernel is the control plane of the protocol stack of every member: FailureDetectorImpl, MembershipProtocolImpl,
+// MetadataStoreImpl and the selection half of GossipProtocolImpl. Its work per member per tick is O(1) in the
+// common case. The O(N) work runs elsewhere: the SYNC-payload diff (k_sync_diff) and the gossip data plane
+// (gossip.hip). Remote hops of stateless request handlers (onPing, onPingReq, onTransitPingAck,
+// onMetadataRequest) are evaluated at the issuer, at the hop's own tick and against that tick's network
+// settings. The payload they would carry is only the correlation id, so no message is materialised.
+#include "dev_util.h"
+
+namespace swim {
+
+enum Reason : uint32_t { R_FD = 0, R_GOSSIP = 1, R_SYNC = 2, R_INITIAL = 3, R_TIMEOUT = 4 };
+enum : uint32_t { INIT_ACTIVE = 1, INIT_RECEIVED = 2 };
+enum : uint32_t { GF_USED = 1, GF_ERROR = 2, GF_SEALED = 4 };
+// path stages: 1..3 = pending hop at `tick`, 9 = ack arrives at `tick`
+enum : uint32_t { P_DIRECT = 0x10, P_REQ = 0x20, P_ARRIVE = 9 };
+
+struct ML {
+  const Dev* d;
+  uint32_t m, k, N;
+  uint32_t tsize, fdLen, gLen, fdPeriod, gPeriod, gCounter, nextPing, nextGossip, nextSync, cidCnt, syncSeq, evSeq,
+      held, timerMin, initFlags, initDeadline, initCidBase, initN, nsub, npath, nfetch;
+  int32_t pingIdx, remoteIdx;
+  uint32_t sel[8];
+  uint64_t evHash;
+  uint64_t* row;
+  uint32_t *fdl, *gl, *subs, *paths, *fetch, *groups;
+  unsigned long long c[8];
+  uint32_t pend[8];
+  uint32_t npend;
+  uint32_t tround;
+};
+
+__device__ uint32_t draw(ML& L, uint32_t stream) {
+  uint32_t c = L.sel[stream]++;
+  return philox(L.m, stream, c, 0, L.d->seed_lo ^ SALT_SEL, L.d->seed_hi).x;
+}
+
+// Collections.shuffle: for i = size..2: swap(i-1, nextInt(i))
+__device__ void shuffle_list(ML& L, uint32_t* v, uint32_t n, uint32_t stream) {
+  for (uint32_t i = n; i > 1; --i) {
+    uint32_t j = next_int(draw(L, stream), i);
+    uint32_t t = v[i - 1];
+    v[i - 1] = v[j];
+    v[j] = t;
+  }
+}
+
+// copy-on-write of the live row for SYNC payloads sent earlier in this tick
+__device__ __noinline__ void cow(ML& L) {
+  const Dev& d = *L.d;
+  uint32_t b = L.k & 1;
+  uint32_t r = atomicAdd(&d.arena_used[b], 1u);
+  if (r >= d.ARENA_ROWS) {
+    set_err(d, E_ARENA);
+    L.npend = 0;
+    return;
+  }
+  uint64_t* dst = d.arena[b] + (size_t)r * L.N;
+  for (uint32_t s = 0; s < L.N; ++s) dst[s] = L.row[s];
+  for (uint32_t i = 0; i < L.npend; ++i) d.msgs[b][L.pend[i]].payload = r;
+  L.npend = 0;
+}
+
+__device__ __forceinline__ void row_put(ML& L, uint32_t s, uint64_t v) {
+  uint64_t old = L.row[s];
+  if (L.npend && ((old ^ v) & KEY_MASK)) cow(L);
+  L.row[s] = v;
+}
+
+// prepareSyncDataMsg (MembershipProtocolImpl.java:446-454) + transport.send; false if the send failed
+__device__ bool send_sync(ML& L, uint32_t kind, uint32_t dst, uint32_t ciss, uint32_t ccnt) {
+  const Dev& d = *L.d;
+  uint32_t seq = L.syncSeq++;
+  L.c[C_M]++;
+  if (lost_msg(d, kind, L.m, dst, L.k, L.m, seq)) {
+    L.c[C_LOST]++;
+    return false;
+  }
+  uint32_t b = L.k & 1;
+  uint32_t i = atomicAdd(&d.nmsg[b], 1u);
+  if (i >= d.MSGCAP) {
+    set_err(d, E_MSGS);
+    return true;
+  }
+  SyncMsg mm;
+  mm.src = L.m;
+  mm.dst = dst;
+  mm.kind = kind;
+  mm.seq = seq;
+  mm.cid_iss = ciss;
+  mm.cid_cnt = ccnt;
+  mm.payload = NEVER;
+  mm.psize = 0;
+  d.msgs[b][i] = mm;
+  if (L.npend == 8) cow(L);
+  L.pend[L.npend++] = i;
+  return true;
+}
+
+__device__ void on_member_event(ML& L, uint32_t type, uint32_t subj) {
+  const Dev& d = *L.d;
+  if (type == 1) {  // REMOVED: FailureDetectorImpl.onMemberEvent (:321-325), GossipProtocolImpl (:187-189)
+    for (uint32_t i = 0; i < L.fdLen; ++i)
+      if (L.fdl[i] == subj) {
+        for (uint32_t j = i + 1; j < L.fdLen; ++j) L.fdl[j - 1] = L.fdl[j];
+        L.fdLen--;
+        break;
+      }
+    for (uint32_t i = 0; i < L.gLen; ++i)
+      if (L.gl[i] == subj) {
+        for (uint32_t j = i + 1; j < L.gLen; ++j) L.gl[j - 1] = L.gl[j];
+        L.gLen--;
+        break;
+      }
+  } else if (type == 0) {  // ADDED: insert at nextInt(size) (:326-331); append (:190-192)
+    if (L.fdLen >= d.LCAP || L.gLen >= d.LCAP) {
+      set_err(d, E_LIST);
+      return;
+    }
+    uint32_t idx = L.fdLen > 0 ? next_int(draw(L, S_FD_INSERT), L.fdLen) : 0;
+    for (uint32_t j = L.fdLen; j > idx; --j) L.fdl[j] = L.fdl[j - 1];
+    L.fdl[idx] = subj;
+    L.fdLen++;
+    L.gl[L.gLen++] = subj;
+  }
+}
+
+__device__ void emit_event(ML& L, uint32_t type, uint32_t subj, uint32_t oldm, uint32_t newm) {
+  const Dev& d = *L.d;
+  uint32_t seq = L.evSeq++;
+  L.evHash = hpair(L.evHash, ((uint64_t)L.k << 32) | ((uint64_t)type << 30) | subj);
+  L.evHash = hpair(L.evHash, ((uint64_t)oldm << 32) | newm);
+  L.c[C_E]++;
+  if (d.flags & 1u) {
+    uint32_t i = atomicAdd(d.ev_n, 1u);
+    if (i < d.EVCAP) {
+      uint32_t* e = d.ev + (size_t)i * 8;
+      e[0] = L.k;
+      e[1] = L.m;
+      e[2] = seq;
+      e[3] = type;
+      e[4] = subj;
+      e[5] = oldm;
+      e[6] = newm;
+      e[7] = 0;
+    } else {
+      set_err(d, E_EVENTS);
+    }
+  }
+  on_member_event(L, type, subj);
+}
+
+// GossipProtocolImpl.spread -> createAndPutGossip (:124-128,163-169): a new global gossip slot held by this member
+__device__ void spread(ML& L, uint32_t subj, uint32_t st, uint32_t inc) {
+  const Dev& d = *L.d;
+  uint64_t gid = ((uint64_t)L.m << 32) | L.gCounter++;
+  int pos = atomicSub(d.free_top, 1) - 1;
+  if (pos < 0) {
+    set_err(d, E_SLOTS);
+    return;
+  }
+  uint32_t g = d.free_list[pos];
+  d.slot_gid[g] = gid;
+  d.slot_subj[g] = subj;
+  d.slot_ctick[g] = L.k;
+  d.slot_key[g] = rec_key(st, inc);
+  d.slot_holders[g] = 1;
+  d.slot_used[g] = 1;
+  d.S[(size_t)g * L.N + L.m] = (L.k + 1u) & S_TICK_MASK;
+  L.held++;
+  L.c[C_GCREATED]++;
+}
+
+__device__ __forceinline__ uint32_t* grp(ML& L, int g) { return L.groups + (size_t)g * GREC; }
+
+__device__ void complete_group(ML& L, int g) {
+  uint32_t* G = grp(L, g);
+  uint32_t kind = G[0], flags = G[5];
+  G[5] = 0;
+  if (kind == 0) {
+    // onSync doOnSuccess (MembershipProtocolImpl.java:351-365): SYNC_ACK with the post-merge table
+    if (!(flags & GF_ERROR)) send_sync(L, K_SYNC_ACK, G[1], G[2], G[3]);
+  } else {
+    // start0 doFinally (:244-248): schedulePeriodicSync
+    L.initFlags &= ~INIT_ACTIVE;
+    L.nextSync = L.k + L.d->sync_t;
+  }
+}
+
+// one inner Mono of Mono.whenDelayError terminated
+__device__ void finish(ML& L, int g, bool error) {
+  if (g < 0) return;
+  uint32_t* G = grp(L, g);
+  if (error) G[5] |= GF_ERROR;
+  if ((G[5] & GF_SEALED) && G[4] == 0) complete_group(L, g);
+}
+
+__device__ int alloc_group(ML& L, uint32_t kind, uint32_t reply, uint32_t ciss, uint32_t ccnt) {
+  for (int g = 0; g < (int)L.d->GRCAP; ++g) {
+    uint32_t* G = grp(L, g);
+    if (!(G[5] & GF_USED)) {
+      G[0] = kind;
+      G[1] = reply;
+      G[2] = ciss;
+      G[3] = ccnt;
+      G[4] = 0;
+      G[5] = GF_USED;
+      return g;
+    }
+  }
+  set_err(*L.d, E_GROUPS);
+  return -1;
+}
+
+// doFinally of updateMembership (:526-539)
+__device__ __forceinline__ void do_finally(ML& L, uint32_t subj, uint32_t st, uint32_t inc, uint32_t reason) {
+  if (reason != R_GOSSIP && reason != R_INITIAL) spread(L, subj, st, inc);
+}
+
+// MetadataStoreImpl.fetchMetadata (:149-186); the response hop is evaluated in P3 at k + lat
+__device__ void fetch_md(ML& L, uint32_t subj, uint32_t st, uint32_t inc, uint32_t reason, uint32_t added, int g) {
+  const Dev& d = *L.d;
+  uint32_t cnt = L.cidCnt++;
+  L.c[C_M]++;
+  if (lost_msg(d, K_GMD_REQ, L.m, subj, L.k, L.m, cnt)) {
+    L.c[C_LOST]++;
+    if (g >= 0) grp(L, g)[5] |= GF_ERROR;
+    do_finally(L, subj, st, inc, reason);
+    return;
+  }
+  if (L.nfetch >= d.FCAP) {
+    set_err(d, E_FETCH);
+    return;
+  }
+  uint32_t* f = L.fetch + (size_t)(L.nfetch++) * FREC;
+  f[0] = cnt;
+  f[1] = subj;
+  f[2] = inc;
+  f[3] = st | (reason << 8) | (added << 16) | (1u << 24);  // stage 1: response hop pending
+  f[4] = (uint32_t)g;
+  f[5] = L.k + d.md_t;
+  f[6] = L.k + d.lat;
+  f[7] = NONE32;
+  if (g >= 0) grp(L, g)[4]++;
+}
+
+// MembershipProtocolImpl.updateMembership (:475-541) + emitMembershipEvent (:543-588)
+__device__ void update_membership(ML& L, uint32_t subj, uint32_t s1, uint32_t i1, uint32_t reason, int g) {
+  const Dev& d = *L.d;
+  uint64_t v0 = L.row[subj];
+  uint32_t s0 = rec_status(v0), i0 = rec_inc(v0);
+  if (!overrides(s1, i1, s0, i0)) return;
+  if (subj == L.m) {  // :488-509 refute with max(inc)+1, keep r0's status, spread, no event
+    uint32_t ni = (i0 > i1 ? i0 : i1) + 1u;
+    row_put(L, subj, (v0 & ~KEY_MASK) | rec_key(s0, ni));
+    L.c[C_W]++;
+    spread(L, subj, s0, ni);
+    return;
+  }
+  if (s1 == ST_DEAD) {
+    row_put(L, subj, 0);  // row removed; REMOVED below removes the metadata; the timer is cancelled
+    L.tsize--;
+  } else {
+    if (s0 == ST_ABSENT) L.tsize++;
+    uint64_t v = (v0 & ~KEY_MASK) | rec_key(s1, i1);
+    if (s1 == ST_SUSPECT) {  // scheduleSuspicionTimeoutTask (:597-606): computeIfAbsent
+      if (rec_timer(v) == 0) {
+        uint32_t dl = L.k + d.suspMult * bitlen(L.tsize) * d.ping_t;
+        v = rec_with_timer(v, dl);
+        if (dl < L.timerMin) L.timerMin = dl;
+      }
+    } else {
+      v = rec_with_timer(v, 0);  // cancelSuspicionTimeoutTask (:590-595)
+    }
+    row_put(L, subj, v);
+  }
+  L.c[C_W]++;
+  if (s1 == ST_DEAD) {
+    uint32_t oldm = (v0 & META_BIT) ? 0u : NONE32;  // metadataStore.removeMetadata
+    emit_event(L, 1, subj, oldm, NONE32);
+    finish(L, g, false);
+    do_finally(L, subj, s1, i1, reason);
+    return;
+  }
+  if (s0 == ST_ABSENT && s1 == ST_ALIVE) {
+    fetch_md(L, subj, s1, i1, reason, 1, g);
+    return;
+  }
+  if (s0 != ST_ABSENT && i0 < i1) {
+    fetch_md(L, subj, s1, i1, reason, 0, g);
+    return;
+  }
+  finish(L, g, false);
+  do_finally(L, subj, s1, i1, reason);
+}
+
+// onFailureDetectorEvent (:370-398)
+__device__ void on_fd_event(ML& L, uint32_t target, uint32_t status) {
+  uint64_t v0 = L.row[target];
+  uint32_t s0 = rec_status(v0);
+  if (s0 == ST_ABSENT || s0 == status) return;
+  if (status == ST_ALIVE) {
+    send_sync(L, K_SYNC, target, NONE32, 0);
+  } else {
+    L.c[C_R]++;
+    update_membership(L, target, ST_SUSPECT, rec_inc(v0), R_FD, -1);
+  }
+}
+
+__device__ void add_sub(ML& L, uint32_t cnt, uint32_t kind, uint32_t target, uint32_t deadline) {
+  if (L.nsub >= SUBCAP) {
+    set_err(*L.d, E_SUBS);
+    return;
+  }
+  uint32_t* s = L.subs + (size_t)(L.nsub++) * 4;
+  s[0] = cnt;
+  s[1] = kind;
+  s[2] = target;
+  s[3] = deadline;
+}
+__device__ void add_path(ML& L, uint32_t cnt, uint32_t stage, uint32_t tick, uint32_t a, uint32_t b) {
+  if (L.npath >= PATHCAP) {
+    set_err(*L.d, E_PATHS);
+    return;
+  }
+  uint32_t* p = L.paths + (size_t)(L.npath++) * 5;
+  p[0] = cnt;
+  p[1] = stage;
+  p[2] = tick;
+  p[3] = a;
+  p[4] = b;
+}
+
+// doPing error branch (FailureDetectorImpl.java:159-175), selectPingReqMembers (:349-361), doPingReq (:178-213)
+__device__ void ping_req_step(ML& L, uint32_t target, uint32_t cnt) {
+  const Dev& d = *L.d;
+  uint32_t helpers[8];
+  uint32_t nh = 0;
+  if (d.kreq > 0) {
+    uint32_t pos = L.fdLen;
+    for (uint32_t i = 0; i < L.fdLen; ++i)
+      if (L.fdl[i] == target) {
+        pos = i;
+        break;
+      }
+    uint32_t n = L.fdLen - (pos < L.fdLen ? 1u : 0u);
+    if (n > 0) {
+      uint32_t kk = d.kreq < n ? d.kreq : n;
+      uint32_t ovp[16], ovv[16], nov = 0;  // positions touched by the partial Fisher-Yates
+      auto get = [&](uint32_t i) -> uint32_t {
+        for (uint32_t q = 0; q < nov; ++q)
+          if (ovp[q] == i) return ovv[q];
+        return L.fdl[i < pos ? i : i + 1];
+      };
+      auto set = [&](uint32_t i, uint32_t v) {
+        for (uint32_t q = 0; q < nov; ++q)
+          if (ovp[q] == i) {
+            ovv[q] = v;
+            return;
+          }
+        ovp[nov] = i;
+        ovv[nov] = v;
+        nov++;
+      };
+      for (uint32_t i = 0; i < kk; ++i) {
+        uint32_t j = i + next_int(draw(L, S_PINGREQ), n - i);
+        uint32_t vi = get(i), vj = get(j);
+        set(i, vj);
+        set(j, vi);
+      }
+      for (uint32_t i = 0; i < kk; ++i) helpers[i] = get(i);
+      nh = kk;
+    }
+  }
+  int timeLeft = (int)d.ping_t - (int)d.pingTimeout_t;
+  if (timeLeft <= 0 || nh == 0) {
+    on_fd_event(L, target, ST_SUSPECT);
+    return;
+  }
+  for (uint32_t q = 0; q < nh; ++q) {
+    uint32_t h = helpers[q];
+    L.c[C_M]++;
+    if (lost_msg(d, K_PING_REQ, L.m, h, L.k, L.m, cnt)) {
+      L.c[C_LOST]++;
+      on_fd_event(L, target, ST_SUSPECT);
+      continue;
+    }
+    add_sub(L, cnt, 1, target, L.k + (uint32_t)timeLeft);
+    add_path(L, cnt, P_REQ | 1, L.k + d.lat, h, target);
+  }
+}
+
+// doPing (:128-176) + selectPingMember (:338-347)
+__device__ void do_ping(ML& L) {
+  const Dev& d = *L.d;
+  L.fdPeriod++;
+  if (L.fdLen == 0) return;
+  if (L.pingIdx >= (int32_t)L.fdLen) {
+    L.pingIdx = 0;
+    shuffle_list(L, L.fdl, L.fdLen, S_FD_SHUFFLE);
+  }
+  uint32_t target = L.fdl[L.pingIdx++];
+  uint32_t cnt = L.cidCnt++;
+  L.c[C_M]++;
+  if (lost_msg(d, K_PING, L.m, target, L.k, L.m, cnt)) {
+    L.c[C_LOST]++;
+    ping_req_step(L, target, cnt);
+    return;
+  }
+  add_sub(L, cnt, 0, target, L.k + d.pingTimeout_t);
+  add_path(L, cnt, P_DIRECT | 1, L.k + d.lat, target, 0);
+}
+
+// doSpreadGossip (GossipProtocolImpl.java:139-157) target selection (:252-273). The sends and the sweep run in
+// the gossip data plane (gossip.hip) from T / tspread / tperiod; the round is logged for infectedFrom replay.
+__device__ void do_spread_gossip(ML& L) {
+  const Dev& d = *L.d;
+  uint32_t period = L.gPeriod++;
+  if (L.held == 0) return;
+  uint32_t F = d.F;
+  uint32_t* T = d.T + (size_t)L.m * F;
+  uint32_t cnt;
+  if (L.gLen < F) {
+    for (uint32_t i = 0; i < L.gLen; ++i) T[i] = L.gl[i];
+    cnt = L.gLen;
+  } else {
+    if (L.remoteIdx < 0 || (uint32_t)L.remoteIdx + F > L.gLen) {
+      shuffle_list(L, L.gl, L.gLen, S_GOSSIP_SHUFFLE);
+      L.remoteIdx = 0;
+    }
+    for (uint32_t i = 0; i < F; ++i) T[i] = L.gl[L.remoteIdx + i];
+    L.remoteIdx += (int32_t)F;
+    cnt = F;
+  }
+  uint32_t sp = spread_of(d, L.gLen + 1);
+  L.tround = 1;
+  d.tcnt[L.m] = cnt;
+  d.tspread[L.m] = sp;
+  d.tperiod[L.m] = period;
+  uint32_t pos = d.log_pos[L.m] % d.LOGW;
+  size_t lo = (size_t)L.m * d.LOGW + pos;
+  d.log_tick[lo] = L.k;
+  d.log_spread[lo] = sp;
+  d.log_cnt[lo] = cnt;
+  for (uint32_t i = 0; i < cnt; ++i) d.log_tg[lo * F + i] = T[i];
+  d.log_pos[L.m]++;
+}
+
+__device__ __forceinline__ bool is_seed(const Dev& d, uint32_t m, uint32_t s) {
+  if (s == m) return false;
+  for (uint32_t i = 0; i < d.n_seeds; ++i)
+    if (d.seeds[i] == s) return true;
+  return false;
+}
+
+// doSync (MembershipProtocolImpl.java:298-314) + selectSyncAddress (:410-421)
+__device__ void do_sync(ML& L) {
+  const Dev& d = *L.d;
+  uint32_t extra = 0;
+  for (uint32_t i = 0; i < d.n_seeds; ++i) {
+    uint32_t s = d.seeds[i];
+    if (s != L.m && rec_status(L.row[s]) == ST_ABSENT) extra++;
+  }
+  uint32_t count = (L.tsize - 1u) + extra;
+  if (count == 0) return;
+  uint32_t i = next_int(draw(L, S_SYNC_PICK), count);
+  uint32_t target;
+  if (L.tsize == L.N) {
+    target = i < L.m ? i : i + 1u;
+  } else {
+    target = NONE32;
+    for (uint32_t s = 0; s < L.N; ++s) {
+      bool in = (s != L.m && rec_status(L.row[s]) != ST_ABSENT) || is_seed(d, L.m, s);
+      if (!in) continue;
+      if (i == 0) {
+        target = s;
+        break;
+      }
+      --i;
+    }
+  }
+  send_sync(L, K_SYNC, target, NONE32, 0);
+}
+
+// syncMembership (:456-467) over the candidates k_sync_diff extracted from one payload
+__device__ void merge_payload(ML& L, uint32_t mi, uint32_t reason, int g) {
+  const Dev& d = *L.d;
+  const SyncMsg& mm = d.msgs[(L.k - 1) & 1][mi];
+  L.c[C_R] += mm.psize;
+  L.c[C_SYNCMERGE]++;
+  for (uint32_t c = 0; c < d.NCHUNK; ++c) {
+    const uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NCHUNK + c) * 2;
+    uint32_t off = cm[0], n = cm[1];
+    for (uint32_t e = 0; e < n; ++e) {
+      uint64_t rec = d.pool[(size_t)off + e];
+      uint32_t subj = (uint32_t)(rec >> 34);
+      uint64_t key = rec & KEY_MASK;
+      if (key == (L.row[subj] & KEY_MASK)) continue;  // !r1.equals(table.get(id)) at processing time
+      update_membership(L, subj, rec_status(key), rec_inc(key), reason, g);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_member_tick(Dev dv, uint32_t k) {
+  uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  const Dev& d = dv;
+  if (m >= d.N) return;
+  // A dead member does nothing itself, but the remote hops of its in-flight requests still run at the live
+  // responders (their sends fail against the dead issuer), so those hops are still evaluated for the counters.
+  const bool dead = dead_at(d, m, k);
+  if (dead && d.npath[m] == 0 && d.nfetch[m] == 0) {
+    d.tround[m] = 0;
+    return;
+  }
+  ML L;
+  L.d = &d;
+  L.m = m;
+  L.k = k;
+  L.N = d.N;
+  L.tsize = d.tsize[m];
+  L.fdLen = d.fdLen[m];
+  L.gLen = d.gLen[m];
+  L.fdPeriod = d.fdPeriod[m];
+  L.gPeriod = d.gPeriod[m];
+  L.gCounter = d.gCounter[m];
+  L.nextPing = d.nextPing[m];
+  L.nextGossip = d.nextGossip[m];
+  L.nextSync = d.nextSync[m];
+  L.cidCnt = d.cidCnt[m];
+  L.syncSeq = d.syncSeq[m];
+  L.evSeq = d.evSeq[m];
+  L.held = d.held[m];
+  L.timerMin = d.timerMin[m];
+  L.initFlags = d.initFlags[m];
+  L.initDeadline = d.initDeadline[m];
+  L.initCidBase = d.initCidBase[m];
+  L.initN = d.initN[m];
+  L.nsub = d.nsub[m];
+  L.npath = d.npath[m];
+  L.nfetch = d.nfetch[m];
+  L.pingIdx = d.pingIdx[m];
+  L.remoteIdx = d.remoteIdx[m];
+  for (int i = 0; i < 8; ++i) L.sel[i] = d.sel[(size_t)m * 8 + i];
+  L.evHash = d.evHash[m];
+  L.row = d.row + (size_t)m * d.N;
+  L.fdl = d.fdl + (size_t)m * d.LCAP;
+  L.gl = d.gl + (size_t)m * d.LCAP;
+  L.subs = d.subs + (size_t)m * SUBCAP * 4;
+  L.paths = d.paths + (size_t)m * PATHCAP * 5;
+  L.fetch = d.fetch + (size_t)m * d.FCAP * FREC;
+  L.groups = d.groups + (size_t)m * d.GRCAP * GREC;
+  for (int i = 0; i < 8; ++i) L.c[i] = 0;
+  L.npend = 0;
+  L.tround = 0;
+
+  // ---- P0 start: ClusterImpl.join0 -> MembershipProtocolImpl.start0 (:216-251), COLD_JOIN at tick 0 ----
+  if (!dead && k == 0 && d.init_mode == 0) {
+    uint32_t ns = 0;
+    for (uint32_t i = 0; i < d.n_seeds; ++i)
+      if (d.seeds[i] != m) ns++;
+    if (ns == 0) {
+      L.nextSync = k + d.sync_t;
+    } else {
+      L.initFlags = INIT_ACTIVE;
+      L.initDeadline = k + d.syncTimeout_t;
+      L.initCidBase = L.cidCnt;
+      L.initN = ns;
+      uint32_t failed = 0;
+      for (uint32_t i = 0; i < d.n_seeds; ++i) {
+        if (d.seeds[i] == m) continue;
+        uint32_t cnt = L.cidCnt++;
+        if (!send_sync(L, K_SYNC, d.seeds[i], m, cnt)) failed++;
+      }
+      if (failed == ns) {
+        L.initFlags = 0;
+        L.nextSync = k + d.sync_t;
+      }
+    }
+  }
+
+  // ---- P1 SYNC / SYNC_ACK (onMessage :320-331, onSync :346-367, onSyncAck :337-343) ----
+  if (!dead && k > 0) {
+    uint32_t off = d.m_off[m], n = d.m_cnt[m];
+    for (uint32_t q = 0; q < n; ++q) {
+      uint32_t mi = d.m_idx[off + q];
+      SyncMsg mm = d.msgs[(k - 1) & 1][mi];
+      if (mm.kind == K_SYNC) {
+        int g = alloc_group(L, 0, mm.src, mm.cid_iss, mm.cid_cnt);
+        merge_payload(L, mi, R_SYNC, g);
+        if (g >= 0) {
+          grp(L, g)[5] |= GF_SEALED;
+          finish(L, g, false);
+        }
+      } else if (mm.cid_iss == NONE32) {
+        merge_payload(L, mi, R_SYNC, -1);
+      } else if (mm.cid_iss == m && (L.initFlags & INIT_ACTIVE) && !(L.initFlags & INIT_RECEIVED) &&
+                 mm.cid_cnt >= L.initCidBase && mm.cid_cnt < L.initCidBase + L.initN) {
+        L.initFlags |= INIT_RECEIVED;  // mergeDelayError(...).take(1) (:239-243)
+        int g = alloc_group(L, 1, NONE32, NONE32, 0);
+        merge_payload(L, mi, R_INITIAL, g);
+        if (g >= 0) {
+          grp(L, g)[5] |= GF_SEALED;
+          finish(L, g, false);
+        }
+      }
+    }
+  }
+
+  // ---- P2 FD: remote hops of pending pings, then PING_ACK arrivals in cid order ----
+  if (L.npath) {
+    uint32_t arr[PATHCAP];
+    uint32_t narr = 0;
+    uint32_t w = 0;
+    for (uint32_t p = 0; p < L.npath; ++p) {
+      uint32_t* P = L.paths + (size_t)p * 5;
+      uint32_t cnt = P[0], stage = P[1], tk = P[2], a = P[3], b = P[4];
+      bool keep = true;
+      if (tk == k) {
+        uint32_t kind = stage & 0xF0, st = stage & 0xF;
+        if (st == P_ARRIVE) {
+          if (!dead) arr[narr++] = cnt;
+          keep = false;
+        } else if (kind == P_DIRECT) {  // onPing at the target (:230-255): PING_ACK back to the issuer
+          if (dead_at(d, a, k)) {
+            keep = false;
+          } else {
+            L.c[C_M]++;
+            if (lost_msg(d, K_PING_ACK, a, m, k, m, cnt)) {
+              L.c[C_LOST]++;
+              keep = false;
+            } else {
+              stage = P_DIRECT | P_ARRIVE;
+              tk = k + d.lat;
+            }
+          }
+        } else {  // ping-req chain: helper a, target b
+          uint32_t who = st == 2 ? b : a;
+          if (dead_at(d, who, k)) {
+            keep = false;
+          } else {
+            L.c[C_M]++;
+            bool lost;
+            if (st == 1)  // onPingReq (:258-284): transit PING helper -> target
+              lost = lost_msg(d, K_PING, a, b, k, m, cnt);
+            else if (st == 2)  // onPing at the target: PING_ACK target -> helper
+              lost = lost_msg(d, K_PING_ACK, b, a, k, m, cnt);
+            else  // onTransitPingAck (:290-315): PING_ACK helper -> issuer
+              lost = lost_msg(d, K_PING_ACK, a, m, k, m, cnt);
+            if (lost) {
+              L.c[C_LOST]++;
+              keep = false;
+            } else {
+              stage = P_REQ | (st == 3 ? P_ARRIVE : st + 1);
+              tk = k + d.lat;
+            }
+          }
+        }
+      }
+      if (keep) {
+        uint32_t* Q = L.paths + (size_t)w * 5;
+        Q[0] = cnt;
+        Q[1] = stage;
+        Q[2] = tk;
+        Q[3] = a;
+        Q[4] = b;
+        w++;
+      }
+    }
+    L.npath = w;
+    // arrivals: every pending subscription on the cid takes the first PING_ACK (TransportImpl.java:205-232)
+    for (uint32_t i = 1; i < narr; ++i)
+      for (uint32_t j = i; j > 0 && arr[j - 1] > arr[j]; --j) {
+        uint32_t t = arr[j];
+        arr[j] = arr[j - 1];
+        arr[j - 1] = t;
+      }
+    for (uint32_t i = 0; i < narr; ++i) {
+      if (i && arr[i] == arr[i - 1]) continue;
+      uint32_t cnt = arr[i];
+      uint32_t hit[SUBCAP], nh = 0, w2 = 0;
+      for (uint32_t s = 0; s < L.nsub; ++s) {
+        uint32_t* S4 = L.subs + (size_t)s * 4;
+        if (S4[0] == cnt) {
+          hit[nh++] = S4[2];
+        } else {
+          uint32_t* D4 = L.subs + (size_t)w2 * 4;
+          D4[0] = S4[0];
+          D4[1] = S4[1];
+          D4[2] = S4[2];
+          D4[3] = S4[3];
+          w2++;
+        }
+      }
+      L.nsub = w2;
+      for (uint32_t q = 0; q < nh; ++q) on_fd_event(L, hit[q], ST_ALIVE);  // publishPingResult(ALIVE)
+    }
+  }
+
+  // ---- P3 metadata: response hops at the subject, then GET_METADATA_RESP arrivals in cid order ----
+  if (L.nfetch) {
+    for (uint32_t q = 0; q < L.nfetch; ++q) {  // onMetadataRequest at the subject (MetadataStoreImpl.java:202-241)
+      uint32_t* f = L.fetch + (size_t)q * FREC;
+      uint32_t stage = f[3] >> 24;
+      if (stage == 1 && f[6] == k) {
+        uint32_t subj = f[1];
+        if (dead_at(d, subj, k)) {
+          f[3] &= 0x00FFFFFFu;
+        } else {
+          L.c[C_M]++;
+          if (lost_msg(d, K_GMD_RESP, subj, m, k, m, f[0])) {
+            L.c[C_LOST]++;
+            f[3] &= 0x00FFFFFFu;
+          } else {
+            f[3] = (f[3] & 0x00FFFFFFu) | (2u << 24);
+            f[6] = k + d.lat;
+            f[7] = d.md_version[subj];
+          }
+        }
+      }
+    }
+    uint32_t q = 0;
+    while (!dead && q < L.nfetch) {
+      uint32_t* f = L.fetch + (size_t)q * FREC;
+      if ((f[3] >> 24) == 2 && f[6] == k) {
+        uint32_t cnt = f[0], subj = f[1], inc = f[2], w3 = f[3], meta = f[7];
+        int g = (int)f[4];
+        (void)cnt;
+        for (uint32_t r = q + 1; r < L.nfetch; ++r)
+          for (uint32_t x = 0; x < FREC; ++x) L.fetch[(size_t)(r - 1) * FREC + x] = L.fetch[(size_t)r * FREC + x];
+        L.nfetch--;
+        uint32_t st = w3 & 0xFF, reason = (w3 >> 8) & 0xFF, added = (w3 >> 16) & 0xFF;
+        // doOnSuccess (:563-567, :576-581): updateMetadata then sink.next
+        uint64_t v = L.row[subj];
+        uint32_t oldm = (v & META_BIT) ? 0u : NONE32;
+        L.row[subj] = v | META_BIT;
+        if (added)
+          emit_event(L, 0, subj, NONE32, meta);
+        else
+          emit_event(L, 2, subj, oldm, meta);
+        if (g >= 0) grp(L, g)[4]--;
+        finish(L, g, false);
+        do_finally(L, subj, st, inc, reason);
+      } else {
+        ++q;
+      }
+    }
+  }
+
+  if (dead) {
+    d.tround[m] = 0;
+    d.npath[m] = L.npath;
+    for (int i = 0; i < 8; ++i)
+      if (L.c[i]) atomicAdd(&d.ctr[i], L.c[i]);
+    return;
+  }
+
+  // ---- P4 gossip first receipts in gossip-id order -> onMembershipGossip (:401-408) ----
+  {
+    uint32_t off = d.rc_off[m], n = d.rc_cnt[m];
+    for (uint32_t q = 0; q < n; ++q) {
+      uint32_t g = d.rc_slot[off + q];
+      uint64_t key = d.slot_key[g];
+      L.c[C_R]++;
+      update_membership(L, d.slot_subj[g], rec_status(key), rec_inc(key), R_GOSSIP, -1);
+    }
+  }
+
+  // ---- P5 timers ----
+  if (L.nsub) {  // FD subscription timeouts in (cid, subscription) order
+    uint32_t dcnt[SUBCAP], dkind[SUBCAP], dtgt[SUBCAP], nd = 0, w = 0;
+    for (uint32_t s = 0; s < L.nsub; ++s) {
+      uint32_t* S4 = L.subs + (size_t)s * 4;
+      if (S4[3] == k) {
+        uint32_t j = nd++;
+        while (j > 0 && dcnt[j - 1] > S4[0]) {
+          dcnt[j] = dcnt[j - 1];
+          dkind[j] = dkind[j - 1];
+          dtgt[j] = dtgt[j - 1];
+          --j;
+        }
+        dcnt[j] = S4[0];
+        dkind[j] = S4[1];
+        dtgt[j] = S4[2];
+      } else {
+        uint32_t* D4 = L.subs + (size_t)w * 4;
+        D4[0] = S4[0];
+        D4[1] = S4[1];
+        D4[2] = S4[2];
+        D4[3] = S4[3];
+        w++;
+      }
+    }
+    L.nsub = w;
+    for (uint32_t q = 0; q < nd; ++q) {
+      if (dkind[q] == 0)
+        ping_req_step(L, dtgt[q], dcnt[q]);  // ping timeout (:159-175)
+      else
+        on_fd_event(L, dtgt[q], ST_SUSPECT);  // ping-req timeout (:204-212)
+    }
+  }
+  if (L.nfetch) {  // metadata timeouts: onErrorResume(TimeoutException) swallows the event (:568,582)
+    uint32_t q = 0;
+    while (q < L.nfetch) {
+      uint32_t* f = L.fetch + (size_t)q * FREC;
+      if (f[5] == k) {
+        uint32_t subj = f[1], inc = f[2], w3 = f[3];
+        int g = (int)f[4];
+        for (uint32_t r = q + 1; r < L.nfetch; ++r)
+          for (uint32_t x = 0; x < FREC; ++x) L.fetch[(size_t)(r - 1) * FREC + x] = L.fetch[(size_t)r * FREC + x];
+        L.nfetch--;
+        if (g >= 0) grp(L, g)[4]--;
+        finish(L, g, false);
+        do_finally(L, subj, w3 & 0xFF, inc, (w3 >> 8) & 0xFF);
+      } else {
+        ++q;
+      }
+    }
+  }
+  if ((L.initFlags & INIT_ACTIVE) && !(L.initFlags & INIT_RECEIVED) && k == L.initDeadline) {
+    L.initFlags &= ~INIT_ACTIVE;  // .timeout(syncTimeout) (:241) -> doFinally -> schedulePeriodicSync
+    L.nextSync = k + d.sync_t;
+  }
+  if (L.timerMin <= k) {  // suspicion timeouts (:608-618), ascending subject; lazy minimum
+    uint32_t nmin = NEVER;
+    for (uint32_t s = 0; s < L.N; ++s) {
+      uint64_t v = L.row[s];
+      uint32_t dl = rec_timer(v);
+      if (dl == 0) continue;
+      if (dl == k) {
+        L.row[s] = rec_with_timer(v, 0);
+        if (rec_status(v) != ST_ABSENT) {
+          L.c[C_R]++;
+          update_membership(L, s, ST_DEAD, rec_inc(v), R_TIMEOUT, -1);
+        }
+      } else if (dl < nmin) {
+        nmin = dl;
+      }
+    }
+    L.timerMin = nmin;
+  }
+
+  // ---- P6 periodic tasks (schedulePeriodically) ----
+  if (k == L.nextPing) {
+    L.nextPing += d.ping_t;
+    do_ping(L);
+  }
+  if (k == L.nextGossip) {
+    L.nextGossip += d.gossip_t;
+    do_spread_gossip(L);
+  }
+  if (k == L.nextSync) {
+    L.nextSync += d.sync_t;
+    do_sync(L);
+  }
+
+  d.tround[m] = L.tround;
+  d.tsize[m] = L.tsize;
+  d.fdLen[m] = L.fdLen;
+  d.gLen[m] = L.gLen;
+  d.fdPeriod[m] = L.fdPeriod;
+  d.gPeriod[m] = L.gPeriod;
+  d.gCounter[m] = L.gCounter;
+  d.nextPing[m] = L.nextPing;
+  d.nextGossip[m] = L.nextGossip;
+  d.nextSync[m] = L.nextSync;
+  d.cidCnt[m] = L.cidCnt;
+  d.syncSeq[m] = L.syncSeq;
+  d.evSeq[m] = L.evSeq;
+  d.held[m] = L.held;
+  d.timerMin[m] = L.timerMin;
+  d.initFlags[m] = L.initFlags;
+  d.initDeadline[m] = L.initDeadline;
+  d.initCidBase[m] = L.initCidBase;
+  d.initN[m] = L.initN;
+  d.nsub[m] = L.nsub;
+  d.npath[m] = L.npath;
+  d.nfetch[m] = L.nfetch;
+  d.pingIdx[m] = L.pingIdx;
+  d.remoteIdx[m] = L.remoteIdx;
+  for (int i = 0; i < 8; ++i) d.sel[(size_t)m * 8 + i] = L.sel[i];
+  d.evHash[m] = L.evHash;
+  for (int i = 0; i < 8; ++i)
+    if (L.c[i]) atomicAdd(&d.ctr[i], L.c[i]);
+}
+
+}  // namespace swim

@@ -103,6 +103,7 @@ SIGNATURES = {
     "swim_read_row": (C.c_int, [_H, C.c_uint32, C.POINTER(C.c_uint64), C.c_size_t]),
     "swim_state_hash": (C.c_int, [_H, C.POINTER(C.c_uint64), C.c_size_t]),
     "swim_read_lists": (C.c_int, [_H, C.c_uint32, _U32P, _U32P, _U32P, _U32P, C.c_size_t, C.POINTER(C.c_int32)]),
+    "swim_read_gossips": (C.c_int, [_H, C.c_uint32, C.POINTER(C.c_uint64), _U32P, C.c_size_t, C.POINTER(C.c_size_t)]),
     "swim_drain_events": (C.c_int, [_H, C.POINTER(SwimEvent), C.c_size_t, C.POINTER(C.c_size_t)]),
     "swim_counters_get": (C.c_int, [_H, C.POINTER(SwimCounters)]),
     "swim_last_error": (C.c_char_p, [_H]),

@@ -162,6 +162,15 @@ class SimulatedCluster:
                                           C.byref(glen), cap, cur), "swim_read_lists")
         return fd[: fl.value].copy(), gl[: glen.value].copy(), (cur[0], cur[1])
 
+    def gossips(self, observer, cap=1 << 20):
+        ids = np.zeros(cap, dtype=np.uint64)
+        inf = np.zeros(cap, dtype=np.uint32)
+        n = C.c_size_t()
+        self._ck(self.lib.swim_read_gossips(self._h, observer, ids.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                            inf.ctypes.data_as(C.POINTER(C.c_uint32)), cap, C.byref(n)),
+                 "swim_read_gossips")
+        return [(int(ids[i] >> 32), int(ids[i] & 0xFFFFFFFF), int(inf[i])) for i in range(n.value)]
+
     def state_hash(self) -> np.ndarray:
         out = np.zeros(self.n * _abi.HASH_WORDS, dtype=np.uint64)
         self._ck(self.lib.swim_state_hash(self._h, out.ctypes.data_as(C.POINTER(C.c_uint64)), out.size),

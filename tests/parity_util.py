@@ -1,0 +1,61 @@
+"""Helpers for diffing the gfx950 engine against the CPU oracle through the shared C ABI."""
+import numpy as np
+
+from swimhip import _abi
+from swimhip.cluster import SimulatedCluster
+
+WORDS = ["row", "fd_list", "gossip_list", "events", "gossips_held", "misc"]
+
+
+def pair(oracle_lib, engine_lib, cfg):
+    return SimulatedCluster(oracle_lib, cfg), SimulatedCluster(engine_lib, cfg)
+
+
+def first_diff(ho, he):
+    bad = np.argwhere(ho != he)
+    if len(bad) == 0:
+        return None
+    m, w = bad[0]
+    return int(m), WORDS[int(w)], len(bad)
+
+
+def explain(o, e, member):
+    """Readable detail for a mismatching member: differing row entries and list heads."""
+    ro, re_ = o.row(member), e.row(member)
+    diffs = [(int(s), hex(int(ro[s])), hex(int(re_[s]))) for s in np.nonzero(ro != re_)[0][:8]]
+    fo, go, co = o.lists(member)
+    fe, ge, ce = e.lists(member)
+    go_, ge_ = o.gossips(member), e.gossips(member)
+    so, se = set(go_), set(ge_)
+    gd = f"gossips oracle-only {sorted(so - se)[:6]} engine-only {sorted(se - so)[:6]} ({len(so)}/{len(se)}); "
+    return (gd + f"row diffs (subject, oracle, engine): {diffs}; fd len {len(fo)}/{len(fe)} eq={np.array_equal(fo, fe)} "
+            f"cursor {co}/{ce}; gossip len {len(go)}/{len(ge)} eq={np.array_equal(go, ge)}")
+
+
+def assert_same(o, e, where=""):
+    ho, he = o.state_hash(), e.state_hash()
+    d = first_diff(ho, he)
+    if d is not None:
+        m, w, n = d
+        raise AssertionError(f"{where}: state hash differs at member {m} word {w} ({n} words differ); "
+                             + explain(o, e, m))
+    co, ce = o.counters(), e.counters()
+    keys = ["record_compares", "row_writes", "messages", "gossip_messages", "events", "messages_lost",
+            "gossips_created", "sync_merges"]
+    for k in keys:
+        assert co[k] == ce[k], f"{where}: counter {k} oracle={co[k]} engine={ce[k]} ({co} vs {ce})"
+
+
+def run_lockstep(o, e, ticks, chunk, where="", events=True):
+    done = 0
+    while done < ticks:
+        n = min(chunk, ticks - done)
+        o.step(n)
+        e.step(n)
+        done += n
+        assert_same(o, e, f"{where} tick {o.tick}")
+    if events:
+        eo, ee = o.events(), e.events()
+        assert eo == ee, f"{where}: event streams differ (oracle {len(eo)} vs engine {len(ee)})"
+        return eo
+    return None

@@ -1,0 +1,39 @@
+"""The C-ABI boundary: both libraries load and export every entry point include/swimhip.h declares.
+
+No compute calls are made here, so the test runs without a GPU. The product library is libswimhip.so (gfx950). The
+oracle exports the same ABI for parity tests only.
+"""
+import re
+from pathlib import Path
+
+import pytest
+
+from swimhip import _abi, LIB_PATH
+
+HEADER = Path(__file__).resolve().parent.parent / "include" / "swimhip.h"
+
+
+def declared_symbols():
+    text = HEADER.read_text()
+    return sorted(set(re.findall(r"\b(swim_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_and_ctypes_agree():
+    assert set(declared_symbols()) == set(_abi.SIGNATURES), "ctypes mirror out of sync with include/swimhip.h"
+
+
+def test_oracle_exports_every_symbol(oracle):
+    for name in declared_symbols():
+        assert hasattr(oracle, name), name
+
+
+def test_engine_library_exports_every_symbol():
+    if not LIB_PATH.exists():
+        pytest.skip("libswimhip.so not built (run __graft_entry__.build())")
+    lib = _abi.load(LIB_PATH)  # loading initialises no device
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+    assert lib.swim_abi_version() == 1
+    # pure helpers run on the host side of the library
+    assert lib.swim_ceil_log2(100_000) == 17
+    assert lib.swim_is_overrides(_abi.ST_ALIVE, 1, _abi.ST_SUSPECT, 0) == 1
