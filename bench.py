@@ -1,0 +1,171 @@
+#!/usr/bin/env python3
+"""bench.py — member·periods/sec of the gfx950 SWIM engine (libswimhip) on the BASELINE.json headline config.
+
+Workload (BASELINE.json configs[2], the config the metric "member·periods/sec at 100k members" is quoted on): 100 000
+members with full membership views, PRECONVERGED (every row ALIVE inc 0, shuffled FD and gossip lists), the default
+ClusterConfig (ping 1 s / 500 ms, ping-req 3, gossip 200 ms x fanout 3 x repeat 3, SYNC every 30 s), no loss. One
+"step" = one FD period (pingInterval = 10 ticks of 100 ms) for every member. In this steady state every member pings
+one peer per period, and periodic SYNC / SYNC_ACK anti-entropy streams whole 100k-record payloads against whole
+receiver rows (N/30 syncs per period in each direction), so the dominant kernel is k_sync_diff. It is HBM-bound
+(16 B of algorithmic traffic per record compare) with no dense math, so no MFMA.
+
+With N=1, all 100k members run on one MI355X (about 165 GB of HBM). With --gpus N under torch.distributed.run,
+each rank runs an independent 100k-member replica on its own GPU. The row-sharded single cluster with RCCL inbox
+exchange is not built yet, so `parallelism` says "replicas" and scaling is weak.
+
+The JSON line also carries:
+  roofline      k_sync_diff algorithmic bytes (16 B x N per merged payload) / its HIP-event time, against 8 TB/s;
+                traffic = measured HBM bytes per launch from rocprofv3 PMC when available (profiles/), else null.
+  cpu_baseline  the CPU oracle (oracle/swimref.cpp, a port) on a bounded sample: same workload shape at 10k members,
+                one core, timed here on the host.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "scalecube-cluster_amd"))
+
+HBM_PEAK_GBPS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
+BASELINE_WORKLOAD = "C3: 100k members, full views, preconverged, default ClusterConfig, no loss"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=30, help="timed FD periods")
+    p.add_argument("--warmup", type=int, default=3, help="untimed FD periods")
+    p.add_argument("--members", type=int, default=100_000)
+    p.add_argument("--loss", type=int, default=0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-members", type=int, default=10_000)
+    p.add_argument("--cpu-periods", type=int, default=10)
+    return p.parse_args()
+
+
+def traffic_from_profiles(n_members):
+    """HBM bytes per k_sync_diff launch from a committed rocprofv3 PMC summary for this member count, if present."""
+    f = ROOT / "profiles" / "pmc_sync_diff.json"
+    if not f.exists():
+        return None
+    try:
+        d = json.loads(f.read_text())
+        if d.get("members") == n_members:
+            return d.get("bytes_per_launch")
+    except Exception:
+        pass
+    return None
+
+
+def cpu_baseline(members, periods):
+    """Bounded CPU sample: the oracle on the same workload shape at `members` members, one thread."""
+    from swimhip import SimConfig, SimulatedCluster, _abi
+    lib_path = ROOT / "oracle" / "liboracle_swimref.so"
+    if not lib_path.exists():
+        import subprocess
+        subprocess.check_call(["make", "-s", "-C", str(ROOT / "oracle")])
+    lib = _abi.load(lib_path)
+    c = SimulatedCluster(lib, SimConfig(n_members=members))
+    c.run_periods(1)
+    t0 = time.perf_counter()
+    c.run_periods(periods)
+    dt = time.perf_counter() - t0
+    c.close()
+    return {"value": members * periods / dt, "unit": "member·periods/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/swimref.cpp, {members} members (same C3 shape, 1/10 of N), {periods} periods "
+                      f"after 1 warm-up period, {dt:.1f} s; per-member work grows ~linearly with N (SYNC payloads), "
+                      f"so at 100k it is ~10x slower per member·period"}
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    import swimhip
+    from swimhip import SimConfig
+
+    cfg = SimConfig(n_members=a.members, device=local, profile=True)
+    c = swimhip.cluster(cfg)
+    if a.loss:
+        c.set_default_loss(a.loss)
+    c.run_periods(a.warmup)
+    base = c.counters()
+
+    def barrier():
+        c.sync()
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    t0 = time.perf_counter()
+    c.run_periods(a.steps)
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], device=f"cuda:{local}", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ctr = c.counters()
+    d = {k: ctr[k] - base[k] for k in ctr}
+
+    if rank == 0:
+        n = a.members
+        merges = d["sync_merges"]
+        diff_s = d["diff_ns"] * 1e-9
+        launches = max(1, d["diff_launches"])
+        bytes_per_launch = 16.0 * n * merges / launches  # payload row + receiver row, 8 B each per subject
+        achieved = (16.0 * n * merges) / diff_s / 1e9 if diff_s > 0 else 0.0
+        # whole-step algorithmic bytes, SURVEY.md §8d: B = 16R + 8W + 32M + 0.375G + 24E
+        B = 16 * d["record_compares"] + 8 * d["row_writes"] + 32 * d["messages"] + 0.375 * d["gossip_messages"] + 24 * d["events"]
+        line = {
+            "metric": "member·periods/sec at 100k members (whole node); achieved HBM GB/s",
+            "value": n * a.steps * world / dt,
+            "unit": "member·periods/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": dt * 1e3 / a.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (PRECONVERGED full views, seeded Philox selector)",
+            "config": {"workload": BASELINE_WORKLOAD if (n == 100_000 and not a.loss) else f"{n} members, loss {a.loss}%",
+                       "members": n, "periods_per_step": 1, "ticks_per_period": 10,
+                       "parallelism": "replicas" if world > 1 else "single-gpu"},
+            "roofline": {"bound": "hbm", "kernel": "k_sync_diff", "achieved": achieved, "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
+                         "algorithmic_bytes_per_launch": bytes_per_launch,
+                         "avg_launch_us": diff_s * 1e6 / launches,
+                         "traffic": traffic_from_profiles(n)},
+            "kernel_time_share": {"k_sync_diff": diff_s / dt, "k_member_tick": d["member_ns"] * 1e-9 / dt,
+                                  "k_gossip_send": d["gossip_ns"] * 1e-9 / dt},
+            "whole_step_algorithmic_GBps": B / dt / 1e9,
+            "counters": {k: d[k] for k in ("record_compares", "row_writes", "messages", "gossip_messages", "events",
+                                           "sync_merges")},
+            "device_bytes": ctr["device_bytes"],
+        }
+        if not a.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline(a.cpu_members, a.cpu_periods)
+        else:
+            line["cpu_baseline"] = None
+        print(json.dumps(line), flush=True)
+    c.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

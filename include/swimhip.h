@@ -56,6 +56,7 @@ extern "C" {
 
 /* flags */
 #define SWIM_FLAG_RECORD_EVENTS 1u /* keep full event records for swim_drain_events (hashes are always kept) */
+#define SWIM_FLAG_PROFILE 2u       /* time the main kernels with HIP events on the engine stream (swim_counters *_ns) */
 
 typedef struct swim_config {
   uint32_t n_members;
@@ -109,7 +110,13 @@ typedef struct swim_counters {
   uint64_t messages_lost;     /* sends failed by loss / block / dead destination */
   uint64_t gossips_created;
   uint64_t sync_merges;       /* SYNC + SYNC_ACK payloads merged */
-  uint64_t reserved[7];
+  /* engine-side measurements (0 on the oracle); *_ns need SWIM_FLAG_PROFILE */
+  uint64_t device_bytes;  /* HBM allocated for the simulation state */
+  uint64_t diff_ns;       /* k_sync_diff: SYNC payload x receiver-row stream */
+  uint64_t member_ns;     /* k_member_tick: per-member protocol control */
+  uint64_t gossip_ns;     /* k_gossip_send: gossip data plane */
+  uint64_t diff_launches;
+  uint64_t reserved[2];
 } swim_counters;
 
 typedef struct swim_handle swim_handle;

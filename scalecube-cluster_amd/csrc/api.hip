@@ -27,6 +27,9 @@ struct swim_handle {
   bool partitioned = false;
   std::vector<uint32_t> group;
   size_t bytes = 0;
+  std::vector<TickEvents> prof;  // SWIM_FLAG_PROFILE: one event set per tick of the current swim_step
+  double prof_ms[3] = {0, 0, 0};  // accumulated k_sync_diff, k_member_tick, k_gossip_send
+  uint64_t prof_diff_launches = 0;
 };
 
 namespace {
@@ -250,6 +253,8 @@ int swim_destroy(swim_handle* h) {
   hipSetDevice((int)h->cfg.device);
   if (h->stream) hipStreamSynchronize(h->stream);
   for (void* p : h->allocs) hipFree(p);
+  for (auto& te : h->prof)
+    for (auto& e : te.ev) hipEventDestroy((hipEvent_t)e);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
   return SWIM_OK;
@@ -259,11 +264,34 @@ int swim_step(swim_handle* h, uint32_t n) {
   if (!h) return SWIM_EINVAL;
   hipSetDevice((int)h->cfg.device);
   if (h->tick + n >= (1ull << 28)) return SWIM_ECAPACITY;  // deadlines are stored in 29 bits
+  const bool profile = (h->cfg.flags & SWIM_FLAG_PROFILE) != 0;
+  if (profile)
+    while (h->prof.size() < n) {
+      TickEvents te;
+      for (auto& e : te.ev) HIPCK(hipEventCreate((hipEvent_t*)&e));
+      h->prof.push_back(te);
+    }
+  uint64_t first = h->tick;
   for (uint32_t i = 0; i < n; ++i) {
-    launch_tick(h->d, (uint32_t)h->tick, h->stream);
+    launch_tick(h->d, (uint32_t)h->tick, h->stream, profile ? &h->prof[i] : nullptr);
     h->tick++;
   }
-  return check_err(h);
+  int rc = check_err(h);
+  if (rc == SWIM_OK && profile) {
+    for (uint32_t i = 0; i < n; ++i) {
+      float ms = 0;
+      if (first + i > 0) {
+        HIPCK(hipEventElapsedTime(&ms, (hipEvent_t)h->prof[i].ev[0], (hipEvent_t)h->prof[i].ev[1]));
+        h->prof_ms[0] += ms;
+        h->prof_diff_launches++;
+      }
+      HIPCK(hipEventElapsedTime(&ms, (hipEvent_t)h->prof[i].ev[2], (hipEvent_t)h->prof[i].ev[3]));
+      h->prof_ms[1] += ms;
+      HIPCK(hipEventElapsedTime(&ms, (hipEvent_t)h->prof[i].ev[4], (hipEvent_t)h->prof[i].ev[5]));
+      h->prof_ms[2] += ms;
+    }
+  }
+  return rc;
 }
 
 int swim_run_periods(swim_handle* h, uint32_t n) {
@@ -417,7 +445,11 @@ int swim_counters_get(swim_handle* h, swim_counters* out) {
   out->messages_lost = c[C_LOST];
   out->gossips_created = c[C_GCREATED];
   out->sync_merges = c[C_SYNCMERGE];
-  out->reserved[0] = h->bytes;  // device bytes allocated
+  out->device_bytes = h->bytes;
+  out->diff_ns = (uint64_t)(h->prof_ms[0] * 1e6);
+  out->member_ns = (uint64_t)(h->prof_ms[1] * 1e6);
+  out->gossip_ns = (uint64_t)(h->prof_ms[2] * 1e6);
+  out->diff_launches = h->prof_diff_launches;
   return SWIM_OK;
 }
 

@@ -111,10 +111,14 @@ struct Dev {
   uint32_t* err;            // [4] bits, info...
 };
 
+// optional per-tick timing of the three main kernels (HIP events on the engine's stream)
+struct TickEvents {
+  void* ev[6];  // hipEvent_t: diff start/stop, member start/stop, gossip-send start/stop
+};
+
 // host-side kernel launchers (one HIP stream)
-struct Launch;
 void launch_init(const Dev& d, void* stream);
-void launch_tick(const Dev& d, uint32_t k, void* stream);
+void launch_tick(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr);
 void launch_kill(const Dev& d, uint32_t member, void* stream);
 void launch_hash(const Dev& d, uint64_t* out, uint32_t now, void* stream);
 

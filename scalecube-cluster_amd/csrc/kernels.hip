@@ -46,27 +46,28 @@ __global__ void k_init_members(Dev d) {
   for (uint32_t e = 0; e < d.LOGW; ++e) d.log_tick[(size_t)m * d.LOGW + e] = NEVER;
 }
 
+// one block per observer row (grid-strided): rows are written with coalesced 8-B stores
 __global__ void k_init_rows(Dev d) {
-  size_t total = (size_t)d.N * d.N;
   uint64_t full = rec_key(ST_ALIVE, 0) | META_BIT;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    uint32_t m = (uint32_t)(i / d.N), s = (uint32_t)(i % d.N);
-    d.row[i] = (d.init_mode == 1 || m == s) ? full : 0ull;
+  for (uint32_t m = blockIdx.x; m < d.N; m += gridDim.x) {
+    uint64_t* row = d.row + (size_t)m * d.N;
+    for (uint32_t s = threadIdx.x; s < d.N; s += blockDim.x) row[s] = (d.init_mode == 1 || m == s) ? full : 0ull;
   }
 }
 
+// PRECONVERGED lists: position p of observer m holds the other member of rank feistel_m(p) (SEMANTICS.md §3)
 __global__ void k_init_lists(Dev d) {
   if (d.init_mode != 1 || d.N < 2) return;
   uint32_t n = d.N - 1;
-  size_t total = (size_t)d.N * n;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    uint32_t m = (uint32_t)(i / n), p = (uint32_t)(i % n);
+  for (uint32_t m = blockIdx.x; m < d.N; m += gridDim.x) {
     for (uint32_t w = 0; w < 2; ++w) {
       FeistelPerm P = make_perm(n, init_draw(d, m, 16 + 4 * w + 0, 0), init_draw(d, m, 16 + 4 * w + 1, 0),
                                 init_draw(d, m, 16 + 4 * w + 2, 0), init_draw(d, m, 16 + 4 * w + 3, 0));
-      uint32_t j = feistel(P, p);
-      uint32_t v = j < m ? j : j + 1;
-      (w == 0 ? d.fdl : d.gl)[(size_t)m * d.LCAP + p] = v;
+      uint32_t* L = (w == 0 ? d.fdl : d.gl) + (size_t)m * d.LCAP;
+      for (uint32_t p = threadIdx.x; p < n; p += blockDim.x) {
+        uint32_t j = feistel(P, p);
+        L[p] = j < m ? j : j + 1;
+      }
     }
   }
 }
@@ -583,7 +584,7 @@ void launch_init(const Dev& d, void* stream) {
   hipLaunchKernelGGL(k_init_slots, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, st, d);
 }
 
-void launch_tick(const Dev& d, uint32_t k, void* stream) {
+void launch_tick(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
   hipStream_t st = (hipStream_t)stream;
   uint32_t b = k & 1, pb = (k - 1) & 1;
   // fresh per-tick output buffers for this tick's sends
@@ -600,9 +601,13 @@ void launch_tick(const Dev& d, uint32_t k, void* stream) {
                        d.m_idx, d.m_key);
     hipLaunchKernelGGL(k_seg_sort, dim3(1024), dim3(256), 0, st, d.m_key, d.m_idx, d.m_off, d.m_cnt, d.N,
                        d.err);
+    if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
     hipLaunchKernelGGL(k_sync_diff, dim3(2048), dim3(256), 0, st, d, pb);
+    if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
   }
+  if (prof) hipEventRecord((hipEvent_t)prof->ev[2], st);
   hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.N, 256)), dim3(256), 0, st, d, k);
+  if (prof) hipEventRecord((hipEvent_t)prof->ev[3], st);
   // gossip data plane for the rounds that ran in this tick
   uint32_t* active = d.active;
   uint32_t* nactive = d.nactive;
@@ -611,7 +616,9 @@ void launch_tick(const Dev& d, uint32_t k, void* stream) {
   hipMemsetAsync(d.rc_n, 0, sizeof(uint32_t), st);
   hipLaunchKernelGGL(k_gossip_active, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, st, d, active, nactive);
   hipLaunchKernelGGL(k_gossip_contacts, dim3(cdiv((uint64_t)d.N * d.F, 256)), dim3(256), 0, st, d, k);
+  if (prof) hipEventRecord((hipEvent_t)prof->ev[4], st);
   hipLaunchKernelGGL(k_gossip_send, dim3(8192), dim3(256), 0, st, d, k, active, nactive);
+  if (prof) hipEventRecord((hipEvent_t)prof->ev[5], st);
   hipLaunchKernelGGL(k_gossip_apply, dim3(1024), dim3(256), 0, st, d, k);
   hipMemsetAsync(d.rc_cnt, 0, sizeof(uint32_t) * d.N, st);
   hipLaunchKernelGGL(k_count_rc, dim3(256), dim3(256), 0, st, d.rc_raw, d.rc_n, d.RCAP, d.rc_cnt);

@@ -16,6 +16,7 @@ INIT_COLD_JOIN = 0
 INIT_PRECONVERGED = 1
 MODE_FULL = 0
 FLAG_RECORD_EVENTS = 1
+FLAG_PROFILE = 2
 
 EV_ADDED, EV_REMOVED, EV_UPDATED = 0, 1, 2
 META_NONE = 0xFFFFFFFF
@@ -77,7 +78,12 @@ class SwimCounters(C.Structure):
         ("messages_lost", C.c_uint64),
         ("gossips_created", C.c_uint64),
         ("sync_merges", C.c_uint64),
-        ("reserved", C.c_uint64 * 7),
+        ("device_bytes", C.c_uint64),
+        ("diff_ns", C.c_uint64),
+        ("member_ns", C.c_uint64),
+        ("gossip_ns", C.c_uint64),
+        ("diff_launches", C.c_uint64),
+        ("reserved", C.c_uint64 * 2),
     ]
 
     def as_dict(self):

@@ -62,6 +62,7 @@ class SimConfig:
     tick_ms: int = 100
     latency_ticks: int = 1
     record_events: bool = False
+    profile: bool = False
     gossip_slot_cap: int = 0
     pending_fetch_cap: int = 0
     event_cap: int = 0
@@ -86,7 +87,7 @@ class SimConfig:
         a.gossip_repeat_mult = c.gossipRepeatMult
         a.metadata_timeout_ms = c.metadataTimeout
         a.mode = _abi.MODE_FULL
-        a.flags = _abi.FLAG_RECORD_EVENTS if self.record_events else 0
+        a.flags = (_abi.FLAG_RECORD_EVENTS if self.record_events else 0) | (_abi.FLAG_PROFILE if self.profile else 0)
         seeds = list(dict.fromkeys(c.seedMembers))
         if len(seeds) > 16:
             raise ValueError("at most 16 seed members")
