@@ -103,6 +103,7 @@ int build(swim_handle* h) {
   Dev& d = h->d;
   std::memset(&d, 0, sizeof(d));
   d.N = c.n_members;
+  d.NS = (c.n_members + 7u) & ~7u;
   d.F = c.gossip_fanout;
   d.kreq = c.ping_req_members;
   if (!to_ticks(c.ping_interval_ms, c.tick_ms, &d.ping_t) || !to_ticks(c.ping_timeout_ms, c.tick_ms, &d.pingTimeout_t) ||
@@ -141,7 +142,7 @@ int build(swim_handle* h) {
   uint64_t mc = N / d.sync_t * 4 + N / d.ping_t + 1024;
   if (c.init_mode == SWIM_INIT_COLD_JOIN) mc = std::max<uint64_t>(mc, N + 1024);
   d.MSGCAP = (uint32_t)mc;
-  d.NCHUNK = (uint32_t)((N + CH - 1) / CH);
+  d.NCHUNK = (uint32_t)((d.NS + CH - 1) / CH);
   d.POOLCAP = (uint32_t)std::min<uint64_t>(1ull << 26, std::max<uint64_t>(1ull << 20, N * 64));
   d.EVCAP = c.event_cap ? c.event_cap : (1u << 20);
   d.DCAP = (uint32_t)std::min<uint64_t>(1ull << 26, std::max<uint64_t>(1ull << 16, N * 512));
@@ -157,18 +158,18 @@ int build(swim_handle* h) {
   A(d.nextGossip, N) A(d.nextSync, N) A(d.cidCnt, N) A(d.syncSeq, N) A(d.evSeq, N) A(d.held, N) A(d.timerMin, N)
   A(d.initFlags, N) A(d.initDeadline, N) A(d.initCidBase, N) A(d.initN, N) A(d.firstGossip, N) A(d.nsub, N)
   A(d.npath, N) A(d.nfetch, N) A(d.pingIdx, N) A(d.remoteIdx, N) A(d.sel, N * 8) A(d.evHash, N)
-  A(d.row, N * N) A(d.fdl, N * d.LCAP) A(d.gl, N * d.LCAP)
+  A(d.row, N * d.NS) A(d.fdl, N * d.LCAP) A(d.gl, N * d.LCAP)
   A(d.subs, N * SUBCAP * 4) A(d.paths, N * PATHCAP * 5) A(d.fetch, N * d.FCAP * FREC) A(d.groups, N * d.GRCAP * GREC)
   A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F)
   A(d.log_tick, N * d.LOGW) A(d.log_spread, N * d.LOGW) A(d.log_cnt, N * d.LOGW) A(d.log_tg, N * d.LOGW * d.F)
   A(d.log_pos, N)
   A(d.slot_gid, d.SLOTS) A(d.slot_subj, d.SLOTS) A(d.slot_ctick, d.SLOTS) A(d.slot_key, d.SLOTS) A(d.slot_holders, d.SLOTS)
   A(d.slot_used, d.SLOTS) A(d.S, (uint64_t)d.SLOTS * N) A(d.free_list, d.SLOTS) A(d.free_top, 1)
-  A(d.deliv, d.DCAP) A(d.deliv_n, 1) A(d.rc_raw, d.RCAP) A(d.rc_n, 1) A(d.rc_cnt, N) A(d.rc_off, N) A(d.rc_fill, N)
+  A(d.deliv, d.DCAP) A(d.deliv_n, 1) A(d.rc_raw, d.RCAP) A(d.rc_n, 1) A(d.rc_cnt, N) A(d.rc_off, N) A(d.rc_fill, N) A(d.scan_part, 1024)
   A(d.rc_slot, d.RCAP) A(d.rc_key, d.RCAP) A(d.active, d.SLOTS) A(d.nactive, 1) A(d.hist, (uint64_t)d.HCAP * 6)
-  A(d.msgs[0], d.MSGCAP) A(d.msgs[1], d.MSGCAP) A(d.nmsg, 2) A(d.arena[0], (uint64_t)d.ARENA_ROWS * N)
-  A(d.arena[1], (uint64_t)d.ARENA_ROWS * N) A(d.arena_used, 2) A(d.m_cnt, N) A(d.m_off, N) A(d.m_fill, N)
-  A(d.m_idx, d.MSGCAP) A(d.m_key, d.MSGCAP) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
+  A(d.msgs[0], d.MSGCAP) A(d.msgs[1], d.MSGCAP) A(d.nmsg, 2) A(d.arena[0], (uint64_t)d.ARENA_ROWS * d.NS)
+  A(d.arena[1], (uint64_t)d.ARENA_ROWS * d.NS) A(d.arena_used, 2)
+  A(d.m_idx, d.MSGCAP) A(d.m_head, N) A(d.next_evt, N) A(d.m_key, d.MSGCAP) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
   A(d.pool, d.POOLCAP) A(d.pool_used, 1)
   A(d.ev, (uint64_t)d.EVCAP * 8) A(d.ev_n, 1) A(d.ctr, C_NCTR) A(d.err, 8)
 #undef A
@@ -188,6 +189,10 @@ int build(swim_handle* h) {
   h->group.assign(d.N, 0);
   for (uint32_t e = 0; e < MAX_EPOCHS; ++e) h->ep_from[e] = NEVER;
   h->cur_ep = 0;
+  Dev* dcopy = nullptr;
+  if ((rc = dalloc(h, &dcopy, 1)) != 0) return rc;
+  d.self = dcopy;
+  HIPCK(hipMemcpy(dcopy, &d, sizeof(Dev), hipMemcpyHostToDevice));
   launch_init(d, h->stream);
   if ((rc = push_epoch(h)) != 0) return rc;
   return check_err(h);
@@ -225,7 +230,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   if (!cfg || !out) return SWIM_EINVAL;
   *out = nullptr;
   const swim_config& c = *cfg;
-  if (c.n_members < 2 || c.ping_timeout_ms >= c.ping_interval_ms || c.gossip_fanout == 0 || c.gossip_fanout > 8 ||
+  if (c.n_members < 2 || c.n_members > (1u << 20) || c.ping_timeout_ms >= c.ping_interval_ms || c.gossip_fanout == 0 || c.gossip_fanout > 8 ||
       c.ping_req_members > 8 || c.n_seeds > 16 || c.mode != SWIM_MODE_FULL || c.n_members > (1u << 30))
     return SWIM_EINVAL;
   if (c.latency_ticks != 1) return SWIM_EUNSUPPORTED;  // gossip data plane assumes one-tick hops
@@ -341,7 +346,7 @@ int swim_current_tick(swim_handle* h, uint64_t* t) {
 int swim_read_row(swim_handle* h, uint32_t obs, uint64_t* out, size_t cap) {
   if (!h || obs >= h->d.N || cap < h->d.N) return SWIM_EINVAL;
   HIPCK(hipStreamSynchronize(h->stream));
-  HIPCK(hipMemcpy(out, h->d.row + (size_t)obs * h->d.N, 8ull * h->d.N, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(out, h->d.row + (size_t)obs * h->d.NS, 8ull * h->d.N, hipMemcpyDeviceToHost));
   for (uint32_t s = 0; s < h->d.N; ++s)
     if (rec_status(out[s]) == ST_ABSENT) out[s] = 0;
   return SWIM_OK;

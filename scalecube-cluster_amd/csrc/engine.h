@@ -18,7 +18,8 @@ namespace swim {
 constexpr uint32_t NEVER = 0xFFFFFFFFu;
 constexpr uint32_t MAX_EPOCHS = 8;
 constexpr uint32_t SUBCAP = 8, PATHCAP = 8, FREC = 8, GREC = 8;
-constexpr uint32_t CH = 1024;  // subjects per SYNC-diff chunk
+constexpr uint32_t CH = 2048;  // subjects per SYNC-diff work item (256 threads x 8)
+constexpr uint32_t MSG_SORT_MAX = 8192;  // SYNC / SYNC_ACK messages per tick (single-block LDS sort)
 
 // S entry flags (gossip slot x member)
 constexpr uint32_t S_PENDING = 1u << 29, S_SWEPT = 1u << 30, S_REBORN = 1u << 31;
@@ -35,12 +36,14 @@ enum Ctr { C_R = 0, C_W, C_M, C_G, C_E, C_LOST, C_GCREATED, C_SYNCMERGE, C_NCTR 
 struct SyncMsg {
   uint32_t src, dst, kind, seq, cid_iss, cid_cnt;
   uint32_t payload;  // NEVER = sender's live row, else arena row index
-  uint32_t psize;    // filled by the diff kernel: present records in the payload
+  uint32_t psize;    // records in the payload = the sender's table size when it sent
+  uint32_t ncand;    // filled by k_sync_diff: payload records that differ from the receiver's row
+  uint32_t pad;
 };
 
 struct Dev {
   // ---- configuration ----
-  uint32_t N, F, kreq, ping_t, pingTimeout_t, gossip_t, sync_t, syncTimeout_t, md_t, lat, suspMult, repeatMult;
+  uint32_t N, NS, F, kreq, ping_t, pingTimeout_t, gossip_t, sync_t, syncTimeout_t, md_t, lat, suspMult, repeatMult;
   uint32_t seed_lo, seed_hi, init_mode, flags, n_seeds;
   uint32_t seeds[16];
   uint32_t LCAP, FCAP, GRCAP, LOGW, SLOTS, MSGCAP, NCHUNK, POOLCAP, EVCAP, DCAP, RCAP, ARENA_ROWS, LOOKBACK, HCAP;
@@ -60,7 +63,7 @@ struct Dev {
   uint32_t* sel;  // [N][8]
   uint64_t* evHash;
 
-  uint64_t* row;  // [N][N]
+  uint64_t* row;  // [N][NS]: row stride NS = N rounded up to 8 (64-B aligned rows for 16-B loads)
   uint32_t *fdl, *gl;  // [N][LCAP]
 
   uint32_t* subs;    // [N][SUBCAP][4]  cnt, kind, target, deadline
@@ -88,6 +91,7 @@ struct Dev {
   uint64_t* rc_raw;  // (member << 32) | slot
   uint32_t* rc_n;
   uint32_t *rc_cnt, *rc_off, *rc_fill;  // [N]
+  uint32_t* scan_part;                  // block partial sums of the exclusive scan
   uint32_t* rc_slot;  // [RCAP] sorted by member then gossip id
   uint64_t* rc_key;   // [RCAP] gossip id sort key
   uint32_t *active, *nactive;  // slots in use at the start of the gossip phase
@@ -98,8 +102,10 @@ struct Dev {
   uint32_t* nmsg;  // [2]
   uint64_t* arena[2];
   uint32_t* arena_used;  // [2]
-  uint32_t *m_cnt, *m_off, *m_fill, *m_idx;  // routing of the previous tick's messages
-  uint64_t* m_key;                           // (src << 32 | syncSeq) sort key
+  uint32_t* m_idx;  // previous tick's messages sorted by m_key
+  uint32_t* m_head; // [N] first sorted message for each destination, NEVER if none (reset by the consumer)
+  uint32_t* next_evt; // [N] earliest tick at which a pending path / subscription / fetch needs the member
+  uint64_t* m_key;  // dst << 44 | src << 24 | (syncSeq & 0xFFFFFF)
   uint32_t* chunk_meta;                      // [MSGCAP][NCHUNK][2] (pool offset, count)
   uint64_t* pool;                            // candidate (subject << 34 | key)
   uint32_t* pool_used;
@@ -108,7 +114,8 @@ struct Dev {
   uint32_t* ev;  // [EVCAP][8] swim_event
   uint32_t* ev_n;
   unsigned long long* ctr;  // [C_NCTR]
-  uint32_t* err;            // [4] bits, info...
+  uint32_t* err;            // [8] bits, info...
+  const Dev* self;          // device-resident copy of this struct (kernels index it through a pointer)
 };
 
 // optional per-tick timing of the three main kernels (HIP events on the engine's stream)

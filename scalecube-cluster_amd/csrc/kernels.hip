@@ -5,7 +5,7 @@
 
 namespace swim {
 
-__global__ void k_member_tick(Dev d, uint32_t k);  // member.hip
+__global__ void k_member_tick(const Dev* __restrict__ dp, uint32_t k);  // member.hip
 
 // ------------------------------------------------------------------------------------------------------------
 // init (SEMANTICS.md §3)
@@ -40,8 +40,9 @@ __global__ void k_init_members(Dev d) {
   d.md_version[m] = 0;
   d.rc_cnt[m] = 0;
   d.rc_off[m] = 0;
-  d.m_cnt[m] = 0;
-  d.m_off[m] = 0;
+  d.rc_fill[m] = 0;
+  d.m_head[m] = NEVER;
+  d.next_evt[m] = NEVER;
   for (uint32_t g = 0; g < d.GRCAP; ++g) d.groups[((size_t)m * d.GRCAP + g) * GREC + 5] = 0;
   for (uint32_t e = 0; e < d.LOGW; ++e) d.log_tick[(size_t)m * d.LOGW + e] = NEVER;
 }
@@ -50,8 +51,9 @@ __global__ void k_init_members(Dev d) {
 __global__ void k_init_rows(Dev d) {
   uint64_t full = rec_key(ST_ALIVE, 0) | META_BIT;
   for (uint32_t m = blockIdx.x; m < d.N; m += gridDim.x) {
-    uint64_t* row = d.row + (size_t)m * d.N;
-    for (uint32_t s = threadIdx.x; s < d.N; s += blockDim.x) row[s] = (d.init_mode == 1 || m == s) ? full : 0ull;
+    uint64_t* row = d.row + (size_t)m * d.NS;
+    for (uint32_t s = threadIdx.x; s < d.NS; s += blockDim.x)
+      row[s] = s >= d.N ? 0ull : (d.init_mode == 1 || m == s) ? full : 0ull;
   }
 }
 
@@ -82,21 +84,54 @@ __global__ void k_init_slots(Dev d) {
 
 // ------------------------------------------------------------------------------------------------------------
 // routing: counting sort by destination member, then per-destination sort by a 64-bit key
-__global__ void k_count_dst(const SyncMsg* msgs, const uint32_t* nmsg, uint32_t cap, uint32_t* cnt) {
+// the previous tick's SYNC / SYNC_ACK messages sorted by (dst, src, syncSeq): one block, bitonic in LDS
+__global__ void __launch_bounds__(1024) k_sort_msgs(const SyncMsg* msgs, const uint32_t* nmsg, uint32_t cap,
+                                                    uint64_t* key_out, uint32_t* idx_out, uint32_t* err) {
+  __shared__ uint64_t K[MSG_SORT_MAX];
+  __shared__ uint32_t V[MSG_SORT_MAX];
   uint32_t n = *nmsg < cap ? *nmsg : cap;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-    atomicAdd(&cnt[msgs[i].dst], 1u);
-}
-__global__ void k_scatter_dst(const SyncMsg* msgs, const uint32_t* nmsg, uint32_t cap, const uint32_t* off,
-                              uint32_t* fill, uint32_t* idx, uint64_t* key) {
-  uint32_t n = *nmsg < cap ? *nmsg : cap;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const SyncMsg& m = msgs[i];
-    uint32_t p = off[m.dst] + atomicAdd(&fill[m.dst], 1u);
-    idx[p] = i;
-    key[p] = ((uint64_t)m.src << 32) | m.seq;
+  if (n == 0) return;
+  if (n > MSG_SORT_MAX) {
+    if (threadIdx.x == 0) atomicOr(err, E_SORTCAP);
+    n = MSG_SORT_MAX;
+  }
+  uint32_t p2 = 1;
+  while (p2 < n) p2 <<= 1;
+  for (uint32_t i = threadIdx.x; i < p2; i += blockDim.x) {
+    if (i < n) {
+      const SyncMsg& m = msgs[i];
+      K[i] = ((uint64_t)m.dst << 44) | ((uint64_t)m.src << 24) | (m.seq & 0xFFFFFFu);
+      V[i] = i;
+    } else {
+      K[i] = ~0ull;
+      V[i] = 0;
+    }
+  }
+  __syncthreads();
+  for (uint32_t size = 2; size <= p2; size <<= 1)
+    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+      for (uint32_t i = threadIdx.x; i < p2; i += blockDim.x) {
+        uint32_t j = i ^ stride;
+        if (j > i) {
+          bool up = (i & size) == 0;
+          if ((K[i] > K[j]) == up) {
+            uint64_t tk = K[i];
+            K[i] = K[j];
+            K[j] = tk;
+            uint32_t tv = V[i];
+            V[i] = V[j];
+            V[j] = tv;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    key_out[i] = K[i];
+    idx_out[i] = V[i];
   }
 }
+
 __global__ void k_count_rc(const uint64_t* raw, const uint32_t* n_, uint32_t cap, uint32_t* cnt) {
   uint32_t n = *n_ < cap ? *n_ : cap;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
@@ -113,36 +148,75 @@ __global__ void k_scatter_rc(const Dev d, const uint64_t* raw, const uint32_t* n
   }
 }
 
-// exclusive scan of n counts by one 1024-thread block (serial chunk per thread + block scan)
-__global__ void __launch_bounds__(1024) k_scan(const uint32_t* in, uint32_t* out, uint32_t n) {
-  __shared__ uint32_t part[1024];
+// first sorted message of every destination present this tick
+__global__ void k_msg_heads(const uint64_t* key, const uint32_t* nmsg, uint32_t cap, uint32_t* head) {
+  uint32_t n = *nmsg < cap ? *nmsg : cap;
+  n = n < MSG_SORT_MAX ? n : MSG_SORT_MAX;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    uint32_t dst = (uint32_t)(key[i] >> 44);
+    if (i == 0 || (uint32_t)(key[i - 1] >> 44) != dst) head[dst] = i;
+  }
+}
+
+// exclusive scan of n counts: per-1024 block scans, a scan of the block sums, then the add-back
+__device__ __forceinline__ uint32_t block_excl_scan_256(uint32_t v, uint32_t* sh, uint32_t* total) {
   uint32_t t = threadIdx.x;
-  uint32_t per = (n + 1023) / 1024;
-  uint32_t b = t * per, e = b + per < n ? b + per : n;
-  uint32_t s = 0;
-  for (uint32_t i = b; i < e; ++i) s += in[i];
-  part[t] = s;
+  sh[t] = v;
   __syncthreads();
-  for (uint32_t o = 1; o < 1024; o <<= 1) {
-    uint32_t v = t >= o ? part[t - o] : 0;
+  for (uint32_t o = 1; o < 256; o <<= 1) {
+    uint32_t a = t >= o ? sh[t - o] : 0;
     __syncthreads();
-    part[t] += v;
+    sh[t] += a;
     __syncthreads();
   }
-  uint32_t run = part[t] - s;
-  for (uint32_t i = b; i < e; ++i) {
-    uint32_t c = in[i];
-    out[i] = run;
-    run += c;
+  uint32_t incl = sh[t];
+  *total = sh[255];
+  __syncthreads();
+  return incl - v;
+}
+__global__ void __launch_bounds__(256) k_scan_blocks(const uint32_t* in, uint32_t* out, uint32_t* part, uint32_t n) {
+  __shared__ uint32_t sh[256];
+  uint32_t base = blockIdx.x * 1024 + threadIdx.x * 4;
+  uint32_t v[4], s = 0;
+  for (int j = 0; j < 4; ++j) {
+    v[j] = base + j < n ? in[base + j] : 0;
+    s += v[j];
   }
+  uint32_t tot;
+  uint32_t run = block_excl_scan_256(s, sh, &tot);
+  for (int j = 0; j < 4; ++j) {
+    if (base + j < n) out[base + j] = run;
+    run += v[j];
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+__global__ void __launch_bounds__(256) k_scan_top(uint32_t* part, uint32_t nb) {  // nb <= 1024
+  __shared__ uint32_t sh[256];
+  uint32_t base = threadIdx.x * 4;
+  uint32_t v[4], s = 0;
+  for (int j = 0; j < 4; ++j) {
+    v[j] = base + j < nb ? part[base + j] : 0;
+    s += v[j];
+  }
+  uint32_t tot;
+  uint32_t run = block_excl_scan_256(s, sh, &tot);
+  for (int j = 0; j < 4; ++j) {
+    if (base + j < nb) part[base + j] = run;
+    run += v[j];
+  }
+}
+__global__ void k_scan_add(uint32_t* out, const uint32_t* part, uint32_t n) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] += part[i / 1024];
 }
 
 // per-segment sort of (key, val) by key: one block per segment, bitonic in LDS (<= 4096 entries)
 constexpr uint32_t SORT_MAX = 4096;
 __global__ void __launch_bounds__(256) k_seg_sort(uint64_t* key, uint32_t* val, const uint32_t* off, const uint32_t* cnt,
-                                                  uint32_t nseg, uint32_t* err) {
+                                                  uint32_t nseg, uint32_t* err, const uint32_t* nitems) {
   __shared__ uint64_t K[SORT_MAX];
   __shared__ uint32_t V[SORT_MAX];
+  if (*nitems == 0) return;  // nothing was routed this tick
   for (uint32_t sgi = blockIdx.x; sgi < nseg; sgi += gridDim.x) {
     uint32_t n = cnt[sgi];
     if (n <= 1) continue;
@@ -197,23 +271,41 @@ __global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b) {
   for (uint32_t w = blockIdx.x; w < total; w += gridDim.x) {
     uint32_t mi = w / d.NCHUNK, c = w % d.NCHUNK;
     const SyncMsg& mm = d.msgs[b][mi];
-    const uint64_t* pay = mm.payload == NEVER ? d.row + (size_t)mm.src * d.N : d.arena[b] + (size_t)mm.payload * d.N;
-    const uint64_t* rcv = d.row + (size_t)mm.dst * d.N;
-    uint32_t s0 = c * CH + threadIdx.x * 4;
-    uint64_t cand[4];
-    uint32_t nc = 0, np = 0;
+    const uint64_t* pay = mm.payload == NEVER ? d.row + (size_t)mm.src * d.NS : d.arena[b] + (size_t)mm.payload * d.NS;
+    const uint64_t* rcv = d.row + (size_t)mm.dst * d.NS;
+    uint32_t s0 = c * CH + threadIdx.x * 8;
+    uint64_t p[8], r[8];
+    if (s0 < d.NS) {  // NS is a multiple of 8: the 64-B group is in bounds, padding entries are 0 (absent)
+      const ulonglong2* pv = (const ulonglong2*)(pay + s0);
+      const ulonglong2* rv = (const ulonglong2*)(rcv + s0);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      uint32_t s = s0 + j;
-      if (s < d.N) {
-        uint64_t r1 = pay[s] & KEY_MASK;
-        if (rec_status(r1) != ST_ABSENT) {
-          np++;
-          if (r1 != (rcv[s] & KEY_MASK)) cand[nc++] = ((uint64_t)s << 34) | r1;
-        }
+      for (int j = 0; j < 4; ++j) {
+        ulonglong2 a = pv[j], q = rv[j];
+        p[2 * j] = a.x;
+        p[2 * j + 1] = a.y;
+        r[2 * j] = q.x;
+        r[2 * j + 1] = q.y;
       }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) p[j] = r[j] = 0;
     }
-    scan[threadIdx.x] = nc | (np << 16);
+    uint32_t mask = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      uint64_t r1 = p[j] & KEY_MASK;
+      if (rec_status(r1) != ST_ABSENT && r1 != (r[j] & KEY_MASK)) mask |= 1u << j;
+    }
+    uint32_t nc = __popc(mask);
+    if (!__syncthreads_or(nc)) {  // steady state: the whole 2048-subject item matches
+      if (threadIdx.x == 0) {
+        uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NCHUNK + c) * 2;
+        cm[0] = 0;
+        cm[1] = 0;
+      }
+      continue;
+    }
+    scan[threadIdx.x] = nc;
     __syncthreads();
     for (uint32_t o = 1; o < 256; o <<= 1) {
       uint32_t v = threadIdx.x >= o ? scan[threadIdx.x - o] : 0;
@@ -222,10 +314,9 @@ __global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b) {
       __syncthreads();
     }
     uint32_t incl = scan[threadIdx.x];
-    uint32_t tot = scan[255];
-    uint32_t totc = tot & 0xFFFF, totp = tot >> 16;
+    uint32_t totc = scan[255];
     if (threadIdx.x == 0) {
-      uint32_t bo = totc ? atomicAdd(d.pool_used, totc) : 0;
+      uint32_t bo = atomicAdd(d.pool_used, totc);
       if (bo + totc > d.POOLCAP) {
         atomicOr(d.err, E_POOL);
         totc = 0;
@@ -235,12 +326,14 @@ __global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b) {
       uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NCHUNK + c) * 2;
       cm[0] = bo;
       cm[1] = totc;
-      if (totp) atomicAdd(&d.msgs[b][mi].psize, totp);
+      if (totc) atomicAdd(&d.msgs[b][mi].ncand, totc);
     }
     __syncthreads();
-    uint32_t excl = (incl & 0xFFFF) - nc;
-    if (base + excl + nc <= d.POOLCAP)
-      for (uint32_t j = 0; j < nc; ++j) d.pool[(size_t)base + excl + j] = cand[j];
+    uint32_t o = base + incl - nc;
+    if (o + nc <= d.POOLCAP)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (mask & (1u << j)) d.pool[o++] = ((uint64_t)(s0 + j) << 34) | (p[j] & KEY_MASK);
     __syncthreads();
   }
 }
@@ -425,7 +518,9 @@ __global__ void k_gossip_contacts(Dev d, uint32_t k) {
 }
 
 // one thread per (active slot, member): the member's round sends of this gossip, then its sweep
-__global__ void __launch_bounds__(256) k_gossip_send(Dev d, uint32_t k, const uint32_t* active, const uint32_t* nactive) {
+__global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp, uint32_t k, const uint32_t* active,
+                                                     const uint32_t* nactive) {
+  const Dev& d = *dp;
   __shared__ unsigned long long red[256];
   uint32_t na = *nactive;
   uint32_t mchunks = (d.N + 255) / 256;
@@ -535,7 +630,7 @@ __global__ void __launch_bounds__(256) k_hash(Dev d, uint64_t* out, uint32_t now
   uint32_t m = blockIdx.x;
   if (m >= d.N) return;
   unsigned long long hr = 0, hf = 0, hg = 0, hgs = 0;
-  const uint64_t* row = d.row + (size_t)m * d.N;
+  const uint64_t* row = d.row + (size_t)m * d.NS;
   for (uint32_t s = threadIdx.x; s < d.N; s += blockDim.x) {
     uint64_t v = row[s];
     if (rec_status(v) != ST_ABSENT) hr += hpair(s, v);
@@ -591,22 +686,16 @@ void launch_tick(const Dev& d, uint32_t k, void* stream, const TickEvents* prof)
   hipMemsetAsync(d.nmsg + b, 0, sizeof(uint32_t), st);
   hipMemsetAsync(d.arena_used + b, 0, sizeof(uint32_t), st);
   hipMemsetAsync(d.pool_used, 0, sizeof(uint32_t), st);
-  hipMemsetAsync(d.m_cnt, 0, sizeof(uint32_t) * d.N, st);
   if (k > 0) {
-    // route the previous tick's SYNC / SYNC_ACK messages by destination, sorted by (src, syncSeq)
-    hipLaunchKernelGGL(k_count_dst, dim3(64), dim3(256), 0, st, d.msgs[pb], d.nmsg + pb, d.MSGCAP, d.m_cnt);
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, d.m_cnt, d.m_off, d.N);
-    hipMemsetAsync(d.m_fill, 0, sizeof(uint32_t) * d.N, st);
-    hipLaunchKernelGGL(k_scatter_dst, dim3(64), dim3(256), 0, st, d.msgs[pb], d.nmsg + pb, d.MSGCAP, d.m_off, d.m_fill,
-                       d.m_idx, d.m_key);
-    hipLaunchKernelGGL(k_seg_sort, dim3(1024), dim3(256), 0, st, d.m_key, d.m_idx, d.m_off, d.m_cnt, d.N,
-                       d.err);
+    // the previous tick's SYNC / SYNC_ACK messages, sorted by (dst, src, syncSeq)
+    hipLaunchKernelGGL(k_sort_msgs, dim3(1), dim3(1024), 0, st, d.msgs[pb], d.nmsg + pb, d.MSGCAP, d.m_key, d.m_idx, d.err);
+    hipLaunchKernelGGL(k_msg_heads, dim3(32), dim3(256), 0, st, d.m_key, d.nmsg + pb, d.MSGCAP, d.m_head);
     if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
     hipLaunchKernelGGL(k_sync_diff, dim3(2048), dim3(256), 0, st, d, pb);
     if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
   }
   if (prof) hipEventRecord((hipEvent_t)prof->ev[2], st);
-  hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.N, 256)), dim3(256), 0, st, d, k);
+  hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.N, 256)), dim3(256), 0, st, d.self, k);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[3], st);
   // gossip data plane for the rounds that ran in this tick
   uint32_t* active = d.active;
@@ -617,17 +706,19 @@ void launch_tick(const Dev& d, uint32_t k, void* stream, const TickEvents* prof)
   hipLaunchKernelGGL(k_gossip_active, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, st, d, active, nactive);
   hipLaunchKernelGGL(k_gossip_contacts, dim3(cdiv((uint64_t)d.N * d.F, 256)), dim3(256), 0, st, d, k);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[4], st);
-  hipLaunchKernelGGL(k_gossip_send, dim3(8192), dim3(256), 0, st, d, k, active, nactive);
+  hipLaunchKernelGGL(k_gossip_send, dim3(1024), dim3(256), 0, st, d.self, k, active, nactive);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[5], st);
   hipLaunchKernelGGL(k_gossip_apply, dim3(1024), dim3(256), 0, st, d, k);
-  hipMemsetAsync(d.rc_cnt, 0, sizeof(uint32_t) * d.N, st);
+  // route this tick's first receipts by member (rc_cnt / rc_fill were zeroed by the consumers in k_member_tick)
   hipLaunchKernelGGL(k_count_rc, dim3(256), dim3(256), 0, st, d.rc_raw, d.rc_n, d.RCAP, d.rc_cnt);
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, d.rc_cnt, d.rc_off, d.N);
-  hipMemsetAsync(d.rc_fill, 0, sizeof(uint32_t) * d.N, st);
+  uint32_t nb = cdiv(d.N, 1024);
+  hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(256), 0, st, d.rc_cnt, d.rc_off, d.scan_part, d.N);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, st, d.scan_part, nb);
+  hipLaunchKernelGGL(k_scan_add, dim3(cdiv(d.N, 256)), dim3(256), 0, st, d.rc_off, d.scan_part, d.N);
   hipLaunchKernelGGL(k_scatter_rc, dim3(256), dim3(256), 0, st, d, d.rc_raw, d.rc_n, d.RCAP, d.rc_off, d.rc_fill,
                      d.rc_slot, d.rc_key);
-  hipLaunchKernelGGL(k_seg_sort, dim3(1024), dim3(256), 0, st, d.rc_key, d.rc_slot, d.rc_off,
-                     d.rc_cnt, d.N, d.err);
+  hipLaunchKernelGGL(k_seg_sort, dim3(1024), dim3(256), 0, st, d.rc_key, d.rc_slot, d.rc_off, d.rc_cnt, d.N, d.err,
+                     d.rc_n);
   hipLaunchKernelGGL(k_gossip_free, dim3(1024), dim3(256), 0, st, d, active, nactive);
 }
 

@@ -32,13 +32,13 @@ struct ML {
   uint32_t tround;
 };
 
-__device__ uint32_t draw(ML& L, uint32_t stream) {
+__device__ __forceinline__ uint32_t draw(ML& L, uint32_t stream) {
   uint32_t c = L.sel[stream]++;
   return philox(L.m, stream, c, 0, L.d->seed_lo ^ SALT_SEL, L.d->seed_hi).x;
 }
 
 // Collections.shuffle: for i = size..2: swap(i-1, nextInt(i))
-__device__ void shuffle_list(ML& L, uint32_t* v, uint32_t n, uint32_t stream) {
+__device__ __forceinline__ void shuffle_list(ML& L, uint32_t* v, uint32_t n, uint32_t stream) {
   for (uint32_t i = n; i > 1; --i) {
     uint32_t j = next_int(draw(L, stream), i);
     uint32_t t = v[i - 1];
@@ -48,7 +48,7 @@ __device__ void shuffle_list(ML& L, uint32_t* v, uint32_t n, uint32_t stream) {
 }
 
 // copy-on-write of the live row for SYNC payloads sent earlier in this tick
-__device__ __noinline__ void cow(ML& L) {
+__device__ __forceinline__ void cow(ML& L) {
   const Dev& d = *L.d;
   uint32_t b = L.k & 1;
   uint32_t r = atomicAdd(&d.arena_used[b], 1u);
@@ -57,7 +57,7 @@ __device__ __noinline__ void cow(ML& L) {
     L.npend = 0;
     return;
   }
-  uint64_t* dst = d.arena[b] + (size_t)r * L.N;
+  uint64_t* dst = d.arena[b] + (size_t)r * d.NS;
   for (uint32_t s = 0; s < L.N; ++s) dst[s] = L.row[s];
   for (uint32_t i = 0; i < L.npend; ++i) d.msgs[b][L.pend[i]].payload = r;
   L.npend = 0;
@@ -70,7 +70,7 @@ __device__ __forceinline__ void row_put(ML& L, uint32_t s, uint64_t v) {
 }
 
 // prepareSyncDataMsg (MembershipProtocolImpl.java:446-454) + transport.send; false if the send failed
-__device__ bool send_sync(ML& L, uint32_t kind, uint32_t dst, uint32_t ciss, uint32_t ccnt) {
+__device__ __forceinline__ bool send_sync(ML& L, uint32_t kind, uint32_t dst, uint32_t ciss, uint32_t ccnt) {
   const Dev& d = *L.d;
   uint32_t seq = L.syncSeq++;
   L.c[C_M]++;
@@ -92,14 +92,16 @@ __device__ bool send_sync(ML& L, uint32_t kind, uint32_t dst, uint32_t ciss, uin
   mm.cid_iss = ciss;
   mm.cid_cnt = ccnt;
   mm.payload = NEVER;
-  mm.psize = 0;
+  mm.psize = L.tsize;
+  mm.ncand = 0;
+  mm.pad = 0;
   d.msgs[b][i] = mm;
   if (L.npend == 8) cow(L);
   L.pend[L.npend++] = i;
   return true;
 }
 
-__device__ void on_member_event(ML& L, uint32_t type, uint32_t subj) {
+__device__ __forceinline__ void on_member_event(ML& L, uint32_t type, uint32_t subj) {
   const Dev& d = *L.d;
   if (type == 1) {  // REMOVED: FailureDetectorImpl.onMemberEvent (:321-325), GossipProtocolImpl (:187-189)
     for (uint32_t i = 0; i < L.fdLen; ++i)
@@ -127,7 +129,7 @@ __device__ void on_member_event(ML& L, uint32_t type, uint32_t subj) {
   }
 }
 
-__device__ void emit_event(ML& L, uint32_t type, uint32_t subj, uint32_t oldm, uint32_t newm) {
+__device__ __forceinline__ void emit_event(ML& L, uint32_t type, uint32_t subj, uint32_t oldm, uint32_t newm) {
   const Dev& d = *L.d;
   uint32_t seq = L.evSeq++;
   L.evHash = hpair(L.evHash, ((uint64_t)L.k << 32) | ((uint64_t)type << 30) | subj);
@@ -153,7 +155,7 @@ __device__ void emit_event(ML& L, uint32_t type, uint32_t subj, uint32_t oldm, u
 }
 
 // GossipProtocolImpl.spread -> createAndPutGossip (:124-128,163-169): a new global gossip slot held by this member
-__device__ void spread(ML& L, uint32_t subj, uint32_t st, uint32_t inc) {
+__device__ __forceinline__ void spread(ML& L, uint32_t subj, uint32_t st, uint32_t inc) {
   const Dev& d = *L.d;
   uint64_t gid = ((uint64_t)L.m << 32) | L.gCounter++;
   int pos = atomicSub(d.free_top, 1) - 1;
@@ -175,7 +177,7 @@ __device__ void spread(ML& L, uint32_t subj, uint32_t st, uint32_t inc) {
 
 __device__ __forceinline__ uint32_t* grp(ML& L, int g) { return L.groups + (size_t)g * GREC; }
 
-__device__ void complete_group(ML& L, int g) {
+__device__ __forceinline__ void complete_group(ML& L, int g) {
   uint32_t* G = grp(L, g);
   uint32_t kind = G[0], flags = G[5];
   G[5] = 0;
@@ -190,14 +192,14 @@ __device__ void complete_group(ML& L, int g) {
 }
 
 // one inner Mono of Mono.whenDelayError terminated
-__device__ void finish(ML& L, int g, bool error) {
+__device__ __forceinline__ void finish(ML& L, int g, bool error) {
   if (g < 0) return;
   uint32_t* G = grp(L, g);
   if (error) G[5] |= GF_ERROR;
   if ((G[5] & GF_SEALED) && G[4] == 0) complete_group(L, g);
 }
 
-__device__ int alloc_group(ML& L, uint32_t kind, uint32_t reply, uint32_t ciss, uint32_t ccnt) {
+__device__ __forceinline__ int alloc_group(ML& L, uint32_t kind, uint32_t reply, uint32_t ciss, uint32_t ccnt) {
   for (int g = 0; g < (int)L.d->GRCAP; ++g) {
     uint32_t* G = grp(L, g);
     if (!(G[5] & GF_USED)) {
@@ -220,7 +222,7 @@ __device__ __forceinline__ void do_finally(ML& L, uint32_t subj, uint32_t st, ui
 }
 
 // MetadataStoreImpl.fetchMetadata (:149-186); the response hop is evaluated in P3 at k + lat
-__device__ void fetch_md(ML& L, uint32_t subj, uint32_t st, uint32_t inc, uint32_t reason, uint32_t added, int g) {
+__device__ __forceinline__ void fetch_md(ML& L, uint32_t subj, uint32_t st, uint32_t inc, uint32_t reason, uint32_t added, int g) {
   const Dev& d = *L.d;
   uint32_t cnt = L.cidCnt++;
   L.c[C_M]++;
@@ -247,7 +249,7 @@ __device__ void fetch_md(ML& L, uint32_t subj, uint32_t st, uint32_t inc, uint32
 }
 
 // MembershipProtocolImpl.updateMembership (:475-541) + emitMembershipEvent (:543-588)
-__device__ void update_membership(ML& L, uint32_t subj, uint32_t s1, uint32_t i1, uint32_t reason, int g) {
+__device__ __forceinline__ void update_membership(ML& L, uint32_t subj, uint32_t s1, uint32_t i1, uint32_t reason, int g) {
   const Dev& d = *L.d;
   uint64_t v0 = L.row[subj];
   uint32_t s0 = rec_status(v0), i0 = rec_inc(v0);
@@ -297,7 +299,7 @@ __device__ void update_membership(ML& L, uint32_t subj, uint32_t s1, uint32_t i1
 }
 
 // onFailureDetectorEvent (:370-398)
-__device__ void on_fd_event(ML& L, uint32_t target, uint32_t status) {
+__device__ __forceinline__ void on_fd_event(ML& L, uint32_t target, uint32_t status) {
   uint64_t v0 = L.row[target];
   uint32_t s0 = rec_status(v0);
   if (s0 == ST_ABSENT || s0 == status) return;
@@ -309,7 +311,7 @@ __device__ void on_fd_event(ML& L, uint32_t target, uint32_t status) {
   }
 }
 
-__device__ void add_sub(ML& L, uint32_t cnt, uint32_t kind, uint32_t target, uint32_t deadline) {
+__device__ __forceinline__ void add_sub(ML& L, uint32_t cnt, uint32_t kind, uint32_t target, uint32_t deadline) {
   if (L.nsub >= SUBCAP) {
     set_err(*L.d, E_SUBS);
     return;
@@ -320,7 +322,7 @@ __device__ void add_sub(ML& L, uint32_t cnt, uint32_t kind, uint32_t target, uin
   s[2] = target;
   s[3] = deadline;
 }
-__device__ void add_path(ML& L, uint32_t cnt, uint32_t stage, uint32_t tick, uint32_t a, uint32_t b) {
+__device__ __forceinline__ void add_path(ML& L, uint32_t cnt, uint32_t stage, uint32_t tick, uint32_t a, uint32_t b) {
   if (L.npath >= PATHCAP) {
     set_err(*L.d, E_PATHS);
     return;
@@ -334,7 +336,7 @@ __device__ void add_path(ML& L, uint32_t cnt, uint32_t stage, uint32_t tick, uin
 }
 
 // doPing error branch (FailureDetectorImpl.java:159-175), selectPingReqMembers (:349-361), doPingReq (:178-213)
-__device__ void ping_req_step(ML& L, uint32_t target, uint32_t cnt) {
+__device__ __forceinline__ void ping_req_step(ML& L, uint32_t target, uint32_t cnt) {
   const Dev& d = *L.d;
   uint32_t helpers[8];
   uint32_t nh = 0;
@@ -393,7 +395,7 @@ __device__ void ping_req_step(ML& L, uint32_t target, uint32_t cnt) {
 }
 
 // doPing (:128-176) + selectPingMember (:338-347)
-__device__ void do_ping(ML& L) {
+__device__ __forceinline__ void do_ping(ML& L) {
   const Dev& d = *L.d;
   L.fdPeriod++;
   if (L.fdLen == 0) return;
@@ -415,7 +417,7 @@ __device__ void do_ping(ML& L) {
 
 // doSpreadGossip (GossipProtocolImpl.java:139-157) target selection (:252-273). The sends and the sweep run in
 // the gossip data plane (gossip.hip) from T / tspread / tperiod; the round is logged for infectedFrom replay.
-__device__ void do_spread_gossip(ML& L) {
+__device__ __forceinline__ void do_spread_gossip(ML& L) {
   const Dev& d = *L.d;
   uint32_t period = L.gPeriod++;
   if (L.held == 0) return;
@@ -456,7 +458,7 @@ __device__ __forceinline__ bool is_seed(const Dev& d, uint32_t m, uint32_t s) {
 }
 
 // doSync (MembershipProtocolImpl.java:298-314) + selectSyncAddress (:410-421)
-__device__ void do_sync(ML& L) {
+__device__ __forceinline__ void do_sync(ML& L) {
   const Dev& d = *L.d;
   uint32_t extra = 0;
   for (uint32_t i = 0; i < d.n_seeds; ++i) {
@@ -485,11 +487,12 @@ __device__ void do_sync(ML& L) {
 }
 
 // syncMembership (:456-467) over the candidates k_sync_diff extracted from one payload
-__device__ void merge_payload(ML& L, uint32_t mi, uint32_t reason, int g) {
+__device__ __forceinline__ void merge_payload(ML& L, uint32_t mi, uint32_t reason, int g) {
   const Dev& d = *L.d;
   const SyncMsg& mm = d.msgs[(L.k - 1) & 1][mi];
   L.c[C_R] += mm.psize;
   L.c[C_SYNCMERGE]++;
+  if (mm.ncand == 0) return;  // steady state: nothing differs, skip the chunk walk
   for (uint32_t c = 0; c < d.NCHUNK; ++c) {
     const uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NCHUNK + c) * 2;
     uint32_t off = cm[0], n = cm[1];
@@ -503,13 +506,33 @@ __device__ void merge_payload(ML& L, uint32_t mi, uint32_t reason, int g) {
   }
 }
 
-__global__ void __launch_bounds__(256) k_member_tick(Dev dv, uint32_t k) {
-  uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
-  const Dev& d = dv;
-  if (m >= d.N) return;
+__device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint32_t k, unsigned long long (&cnt)[8]) {
   // A dead member does nothing itself, but the remote hops of its in-flight requests still run at the live
   // responders (their sends fail against the dead issuer), so those hops are still evaluated for the counters.
   const bool dead = dead_at(d, m, k);
+  if (dead) {
+    d.rc_cnt[m] = 0;
+    d.rc_fill[m] = 0;
+    if (k > 0) d.m_head[m] = NEVER;
+  } else {
+    // idle fast path: most members have nothing due in most ticks (a ping every 10 ticks, a SYNC every 300)
+    uint32_t mh = k > 0 ? d.m_head[m] : NEVER;
+    bool busy = mh != NEVER || d.rc_cnt[m] != 0 || d.next_evt[m] <= k || d.timerMin[m] <= k || k == d.nextPing[m] ||
+                k == d.nextSync[m] || (d.initFlags[m] & INIT_ACTIVE) || (k == 0 && d.init_mode == 0);
+    if (!busy) {
+      uint32_t ng = d.nextGossip[m];
+      if (k != ng) {
+        d.tround[m] = 0;
+        return;
+      }
+      if (d.held[m] == 0) {  // doSpreadGossip with no gossips: period++ only (GossipProtocolImpl.java:141-146)
+        d.gPeriod[m]++;
+        d.nextGossip[m] = ng + d.gossip_t;
+        d.tround[m] = 0;
+        return;
+      }
+    }
+  }
   if (dead && d.npath[m] == 0 && d.nfetch[m] == 0) {
     d.tround[m] = 0;
     return;
@@ -544,7 +567,7 @@ __global__ void __launch_bounds__(256) k_member_tick(Dev dv, uint32_t k) {
   L.remoteIdx = d.remoteIdx[m];
   for (int i = 0; i < 8; ++i) L.sel[i] = d.sel[(size_t)m * 8 + i];
   L.evHash = d.evHash[m];
-  L.row = d.row + (size_t)m * d.N;
+  L.row = d.row + (size_t)m * d.NS;
   L.fdl = d.fdl + (size_t)m * d.LCAP;
   L.gl = d.gl + (size_t)m * d.LCAP;
   L.subs = d.subs + (size_t)m * SUBCAP * 4;
@@ -581,10 +604,15 @@ __global__ void __launch_bounds__(256) k_member_tick(Dev dv, uint32_t k) {
   }
 
   // ---- P1 SYNC / SYNC_ACK (onMessage :320-331, onSync :346-367, onSyncAck :337-343) ----
-  if (!dead && k > 0) {
-    uint32_t off = d.m_off[m], n = d.m_cnt[m];
-    for (uint32_t q = 0; q < n; ++q) {
-      uint32_t mi = d.m_idx[off + q];
+  if (!dead && k > 0 && d.m_head[m] != NEVER) {
+    // this member's segment of the (dst, src, syncSeq)-sorted message list
+    uint32_t nm = d.nmsg[(k - 1) & 1];
+    nm = nm < d.MSGCAP ? nm : d.MSGCAP;
+    nm = nm < MSG_SORT_MAX ? nm : MSG_SORT_MAX;
+    uint32_t lo = d.m_head[m];
+    d.m_head[m] = NEVER;
+    for (uint32_t q = lo; q < nm && (uint32_t)(d.m_key[q] >> 44) == m; ++q) {
+      uint32_t mi = d.m_idx[q];
       SyncMsg mm = d.msgs[(k - 1) & 1][mi];
       if (mm.kind == K_SYNC) {
         int g = alloc_group(L, 0, mm.src, mm.cid_iss, mm.cid_cnt);
@@ -751,14 +779,18 @@ __global__ void __launch_bounds__(256) k_member_tick(Dev dv, uint32_t k) {
   if (dead) {
     d.tround[m] = 0;
     d.npath[m] = L.npath;
-    for (int i = 0; i < 8; ++i)
-      if (L.c[i]) atomicAdd(&d.ctr[i], L.c[i]);
+    d.next_evt[m] = NEVER;
+    for (int i = 0; i < 8; ++i) cnt[i] += L.c[i];
     return;
   }
 
   // ---- P4 gossip first receipts in gossip-id order -> onMembershipGossip (:401-408) ----
   {
     uint32_t off = d.rc_off[m], n = d.rc_cnt[m];
+    if (n) {
+      d.rc_cnt[m] = 0;  // the next receipt routing counts from zero
+      d.rc_fill[m] = 0;
+    }
     for (uint32_t q = 0; q < n; ++q) {
       uint32_t g = d.rc_slot[off + q];
       uint64_t key = d.slot_key[g];
@@ -855,6 +887,15 @@ __global__ void __launch_bounds__(256) k_member_tick(Dev dv, uint32_t k) {
     do_sync(L);
   }
 
+  uint32_t nev = NEVER;
+  for (uint32_t q = 0; q < L.npath; ++q) nev = min(nev, L.paths[(size_t)q * 5 + 2]);
+  for (uint32_t q = 0; q < L.nsub; ++q) nev = min(nev, L.subs[(size_t)q * 4 + 3]);
+  for (uint32_t q = 0; q < L.nfetch; ++q) {
+    const uint32_t* f = L.fetch + (size_t)q * FREC;
+    nev = min(nev, f[5]);
+    if ((f[3] >> 24) != 0) nev = min(nev, f[6]);
+  }
+  d.next_evt[m] = nev;
   d.tround[m] = L.tround;
   d.tsize[m] = L.tsize;
   d.fdLen[m] = L.fdLen;
@@ -881,8 +922,26 @@ __global__ void __launch_bounds__(256) k_member_tick(Dev dv, uint32_t k) {
   d.remoteIdx[m] = L.remoteIdx;
   for (int i = 0; i < 8; ++i) d.sel[(size_t)m * 8 + i] = L.sel[i];
   d.evHash[m] = L.evHash;
-  for (int i = 0; i < 8; ++i)
-    if (L.c[i]) atomicAdd(&d.ctr[i], L.c[i]);
+  for (int i = 0; i < 8; ++i) cnt[i] += L.c[i];
+}
+
+// Counters are summed across the wave first: 10^4 pingers per tick adding to one word would serialise on that address.
+__global__ void __launch_bounds__(256) k_member_tick(const Dev* __restrict__ dp, uint32_t k) {
+  const Dev& d = *dp;  // global, not kernarg: taking its address must not copy ~1 KB into per-lane scratch
+  uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (m < d.N) member_tick_body(d, m, k, cnt);
+  const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    unsigned long long v = cnt[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      uint32_t lo = __shfl_xor((uint32_t)v, o), hi = __shfl_xor((uint32_t)(v >> 32), o);
+      v += ((unsigned long long)hi << 32) | lo;
+    }
+    if (lane == 0 && v) atomicAdd(&d.ctr[i], v);
+  }
 }
 
 }  // namespace swim
