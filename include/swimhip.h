@@ -138,6 +138,9 @@ int swim_kill(swim_handle* h, uint32_t member);
 int swim_set_default_loss(swim_handle* h, uint32_t loss_percent);
 int swim_set_partition(swim_handle* h, const uint32_t* group_of_member); /* n_members entries */
 int swim_unblock_all(swim_handle* h);
+/* MembershipProtocolImpl.updateIncarnation (:178-190): the member bumps its own incarnation and spreads it, at the
+ * start (P0) of the next tick; what ClusterImpl.updateMetadata does after storing new metadata */
+int swim_update_incarnation(swim_handle* h, uint32_t member);
 
 /* readback */
 int swim_current_tick(swim_handle* h, uint64_t* tick);

@@ -141,6 +141,7 @@ struct Member {
   uint64_t initDeadline = NEVER;
 
   uint64_t nextPing = NEVER, nextGossip = NEVER, nextSync = NEVER;
+  bool pendingInc = false;  // swim_update_incarnation, applied in P0 of the next tick
   uint32_t cidCnt = 0, syncSeq = 0, evSeq = 0;
   uint32_t sel[8] = {0};
   uint64_t evHash = 0;
@@ -607,6 +608,13 @@ static bool fd_less(const Msg& a, const Msg& b) {
 
 void Member::process(uint64_t k, std::vector<Msg>& inbox) {
   Sim& s = *sim;
+  if (pendingInc) {  // updateIncarnation (MembershipProtocolImpl.java:178-190)
+    pendingInc = false;
+    Rec r{ALIVE, table[id].inc + 1};
+    table[id] = r;
+    s.ctr.row_writes++;
+    spread(id, r);
+  }
   std::vector<Msg*> syncm, fdm, mdm, gm;
   for (auto& m : inbox) {
     switch (m.kind) {
@@ -946,6 +954,11 @@ __attribute__((visibility("default"))) int swim_kill(swim_handle* h, uint32_t m)
   if (!h || m >= h->sim.N) return SWIM_EINVAL;
   h->sim.members[m].alive = false;
   h->sim.members[m].gossips.clear();  // a crashed process keeps nothing it could gossip again (SEMANTICS.md §1)
+  return SWIM_OK;
+}
+__attribute__((visibility("default"))) int swim_update_incarnation(swim_handle* h, uint32_t m) {
+  if (!h || m >= h->sim.N || !h->sim.members[m].alive) return SWIM_EINVAL;
+  h->sim.members[m].pendingInc = true;
   return SWIM_OK;
 }
 __attribute__((visibility("default"))) int swim_set_default_loss(swim_handle* h, uint32_t pct) {

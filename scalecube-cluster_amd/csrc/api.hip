@@ -169,7 +169,7 @@ int build(swim_handle* h) {
   A(d.rc_slot, d.RCAP) A(d.rc_key, d.RCAP) A(d.active, d.SLOTS) A(d.nactive, 1) A(d.hist, (uint64_t)d.HCAP * 6)
   A(d.msgs[0], d.MSGCAP) A(d.msgs[1], d.MSGCAP) A(d.nmsg, 2) A(d.arena[0], (uint64_t)d.ARENA_ROWS * d.NS)
   A(d.arena[1], (uint64_t)d.ARENA_ROWS * d.NS) A(d.arena_used, 2)
-  A(d.m_idx, d.MSGCAP) A(d.m_head, N) A(d.next_evt, N) A(d.m_key, d.MSGCAP) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
+  A(d.m_idx, d.MSGCAP) A(d.m_head, N) A(d.next_evt, N) A(d.pending_inc, N) A(d.m_key, d.MSGCAP) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
   A(d.pool, d.POOLCAP) A(d.pool_used, 1)
   A(d.ev, (uint64_t)d.EVCAP * 8) A(d.ev_n, 1) A(d.ctr, C_NCTR) A(d.err, 8)
 #undef A
@@ -312,6 +312,16 @@ int swim_kill(swim_handle* h, uint32_t m) {
   HIPCK(hipMemcpyAsync(h->d.dead_tick + m, &t, 4, hipMemcpyHostToDevice, h->stream));
   launch_kill(h->d, m, h->stream);
   return check_err(h);
+}
+
+int swim_update_incarnation(swim_handle* h, uint32_t m) {
+  if (!h || m >= h->d.N) return SWIM_EINVAL;
+  uint32_t one = 1, dt = 0;
+  HIPCK(hipStreamSynchronize(h->stream));
+  HIPCK(hipMemcpy(&dt, h->d.dead_tick + m, 4, hipMemcpyDeviceToHost));
+  if (dt != NEVER) return SWIM_EINVAL;
+  HIPCK(hipMemcpy(h->d.pending_inc + m, &one, 4, hipMemcpyHostToDevice));
+  return SWIM_OK;
 }
 
 int swim_set_default_loss(swim_handle* h, uint32_t pct) {

@@ -104,6 +104,7 @@ struct Dev {
   uint32_t* arena_used;  // [2]
   uint32_t* m_idx;  // previous tick's messages sorted by m_key
   uint32_t* m_head; // [N] first sorted message for each destination, NEVER if none (reset by the consumer)
+  uint32_t* pending_inc; // [N] swim_update_incarnation requests for the next tick's P0
   uint32_t* next_evt; // [N] earliest tick at which a pending path / subscription / fetch needs the member
   uint64_t* m_key;  // dst << 44 | src << 24 | (syncSeq & 0xFFFFFF)
   uint32_t* chunk_meta;                      // [MSGCAP][NCHUNK][2] (pool offset, count)

@@ -43,6 +43,7 @@ __global__ void k_init_members(Dev d) {
   d.rc_fill[m] = 0;
   d.m_head[m] = NEVER;
   d.next_evt[m] = NEVER;
+  d.pending_inc[m] = 0;
   for (uint32_t g = 0; g < d.GRCAP; ++g) d.groups[((size_t)m * d.GRCAP + g) * GREC + 5] = 0;
   for (uint32_t e = 0; e < d.LOGW; ++e) d.log_tick[(size_t)m * d.LOGW + e] = NEVER;
 }

@@ -517,7 +517,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   } else {
     // idle fast path: most members have nothing due in most ticks (a ping every 10 ticks, a SYNC every 300)
     uint32_t mh = k > 0 ? d.m_head[m] : NEVER;
-    bool busy = mh != NEVER || d.rc_cnt[m] != 0 || d.next_evt[m] <= k || d.timerMin[m] <= k || k == d.nextPing[m] ||
+    bool busy = mh != NEVER || d.rc_cnt[m] != 0 || d.pending_inc[m] || d.next_evt[m] <= k || d.timerMin[m] <= k || k == d.nextPing[m] ||
                 k == d.nextSync[m] || (d.initFlags[m] & INIT_ACTIVE) || (k == 0 && d.init_mode == 0);
     if (!busy) {
       uint32_t ng = d.nextGossip[m];
@@ -577,6 +577,16 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   for (int i = 0; i < 8; ++i) L.c[i] = 0;
   L.npend = 0;
   L.tround = 0;
+
+  // ---- P0 host requests: updateIncarnation (MembershipProtocolImpl.java:178-190) ----
+  if (!dead && d.pending_inc[m]) {
+    d.pending_inc[m] = 0;
+    uint64_t v0 = L.row[m];
+    uint32_t ni = rec_inc(v0) + 1u;
+    row_put(L, m, (v0 & ~KEY_MASK) | rec_key(ST_ALIVE, ni));
+    L.c[C_W]++;
+    spread(L, m, ST_ALIVE, ni);
+  }
 
   // ---- P0 start: ClusterImpl.join0 -> MembershipProtocolImpl.start0 (:216-251), COLD_JOIN at tick 0 ----
   if (!dead && k == 0 && d.init_mode == 0) {

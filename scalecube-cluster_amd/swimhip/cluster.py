@@ -122,6 +122,9 @@ class SimulatedCluster:
         assert g.shape == (self.n,)
         self._ck(self.lib.swim_set_partition(self._h, g.ctypes.data_as(C.POINTER(C.c_uint32))), "swim_set_partition")
 
+    def update_incarnation(self, member):
+        self._ck(self.lib.swim_update_incarnation(self._h, member), "swim_update_incarnation")
+
     def unblock_all(self):
         self._ck(self.lib.swim_unblock_all(self._h), "swim_unblock_all")
 

@@ -60,3 +60,50 @@ def test_preconverged_sync_large(oracle, engine):
     cfg = SimConfig(n_members=1500)
     o, e = pair(oracle, engine, cfg)
     run_lockstep(o, e, 320, 80, "sync", events=False)
+
+
+def test_fast_config_partition_recovery(oracle, engine):
+    """MembershipProtocolTest's fast config (tick 10 ms, ping 200/100, sync 500/100, metadata 100), cold join of 5
+    with every member a seed, a three-way partition until removal, then healing."""
+    n = 5
+    cc = ClusterConfig(seedMembers=list(range(n)), syncInterval=500, syncTimeout=100, pingInterval=200,
+                       pingTimeout=100, metadataTimeout=100)
+    cfg = SimConfig(n_members=n, cluster=cc, init_mode=_abi.INIT_COLD_JOIN, tick_ms=10, record_events=True)
+    o, e = pair(oracle, engine, cfg)
+    run_lockstep(o, e, 300, 20, "joined")
+    g = np.array([0, 1, 2, 0, 1], dtype=np.uint32)
+    o.partition(g)
+    e.partition(g)
+    run_lockstep(o, e, 500, 25, "partitioned")
+    o.unblock_all()
+    e.unblock_all()
+    run_lockstep(o, e, 300, 25, "healed")
+
+
+@pytest.mark.parametrize("loss", [0, 25])
+def test_gossip_dissemination_update_incarnation(oracle, engine, loss):
+    """GossipProtocolTest shape: 50 members, one incarnation bump disseminated under loss."""
+    cfg = SimConfig(n_members=50, record_events=True)
+    o, e = pair(oracle, engine, cfg)
+    for c in (o, e):
+        c.set_default_loss(loss)
+        c.step(5)
+        c.update_incarnation(0)
+    run_lockstep(o, e, 120, 4, f"dissemination loss {loss}")
+    for c in (o, e):
+        c.update_incarnation(7)
+        c.update_incarnation(8)
+    run_lockstep(o, e, 200, 20, f"second wave loss {loss}")
+
+
+def test_kill_many_with_loss(oracle, engine):
+    """Churn under loss: several crashed members, suspicion storms and DEAD gossips with 10 % loss."""
+    cfg = SimConfig(n_members=120, record_events=True)
+    o, e = pair(oracle, engine, cfg)
+    for c in (o, e):
+        c.set_default_loss(10)
+    run_lockstep(o, e, 50, 25, "warm")
+    for victim in (3, 50, 51, 119):
+        o.kill(victim)
+        e.kill(victim)
+    run_lockstep(o, e, 500, 50, "after kills")

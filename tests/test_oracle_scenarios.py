@@ -1,0 +1,138 @@
+"""The reference's behavioural tests restated on the deterministic harness, run against the CPU oracle.
+
+The reference tests use wall-clock sleeps on loopback TCP and assert eventual state. Here the same member counts,
+configs and fault matrices run on virtual time. The eventual-state assertions are the reference's own. Reference file:line
+on every test. tick_ms = 10 for the fast test configs (ping 200 / 100 ms), so the 4-hop ping-req chain fits the
+ping-req timeout as it does on loopback.
+"""
+import numpy as np
+import pytest
+
+from swimhip import ClusterConfig, SimConfig, _abi
+from swimhip.cluster import SimulatedCluster
+
+# MembershipProtocolTest.testConfig (:545-554): sync 500 / 100, ping 200 / 100, metadata 100; seeds = every member
+def mp_config(n, **kw):
+    cc = ClusterConfig(seedMembers=list(range(n)), syncInterval=500, syncTimeout=100, pingInterval=200,
+                       pingTimeout=100, metadataTimeout=100)
+    return SimConfig(n_members=n, cluster=cc, init_mode=_abi.INIT_COLD_JOIN, tick_ms=10, record_events=True, **kw)
+
+
+def ticks_for_seconds(sec, tick_ms=10):
+    return int(sec * 1000 // tick_ms)
+
+
+def trusted(c, o):
+    return sorted(c.trusted(o))
+
+
+def suspected(c, o):
+    return sorted(c.suspected(o))
+
+
+def test_initial_phase_ok(oracle):  # MembershipProtocolTest.testInitialPhaseOk (:57-81)
+    c = SimulatedCluster(oracle, mp_config(3))
+    c.step(ticks_for_seconds(1))
+    for o in range(3):
+        assert trusted(c, o) == [0, 1, 2] and suspected(c, o) == []
+
+
+def test_network_partition_then_recovery(oracle):  # testNetworkPartitionThenRecovery (:83-129)
+    c = SimulatedCluster(oracle, mp_config(3))
+    c.step(ticks_for_seconds(3))
+    c.partition(np.arange(3, dtype=np.uint32))  # each member blocks the other two
+    susp_sec = 5 * 2 * 200 // 1000  # ClusterMath.suspicionTimeout(5, 3, 200) / 1000
+    c.step(ticks_for_seconds(susp_sec + 2))
+    for o in range(3):
+        assert trusted(c, o) == [o] and suspected(c, o) == []
+    c.unblock_all()
+    c.step(ticks_for_seconds(500 * 2 / 1000))
+    for o in range(3):
+        assert trusted(c, o) == [0, 1, 2] and suspected(c, o) == []
+
+
+def test_long_network_partition_no_recovery(oracle):  # testLongNetworkPartitionNoRecovery (:313-366)
+    c = SimulatedCluster(oracle, mp_config(4))
+    c.step(ticks_for_seconds(1))
+    for o in range(4):
+        assert trusted(c, o) == [0, 1, 2, 3]
+    c.partition(np.array([0, 0, 1, 1], dtype=np.uint32))
+    c.step(ticks_for_seconds(2))
+    assert trusted(c, 0) == [0, 1] and suspected(c, 0) == [2, 3]
+    assert trusted(c, 2) == [2, 3] and suspected(c, 2) == [0, 1]
+    susp_sec = 5 * 3 * 200 // 1000  # suspicionTimeout(5, 4, 200)
+    c.step(ticks_for_seconds(susp_sec + 1))
+    for o, mine in ((0, [0, 1]), (1, [0, 1]), (2, [2, 3]), (3, [2, 3])):
+        assert trusted(c, o) == mine and suspected(c, o) == []
+
+
+def test_member_lost_network_then_recover(oracle):  # testMemberLostNetworkThenRecover (:131-185)
+    c = SimulatedCluster(oracle, mp_config(3))
+    c.step(ticks_for_seconds(1))
+    c.partition(np.array([0, 1, 0], dtype=np.uint32))  # b loses the network: {b}, {a, c}
+    c.step(ticks_for_seconds(1))
+    assert trusted(c, 0) == [0, 2] and suspected(c, 0) == [1]
+    assert trusted(c, 1) == [1] and suspected(c, 1) == [0, 2]
+    c.unblock_all()
+    c.step(ticks_for_seconds(2))
+    for o in range(3):
+        assert trusted(c, o) == [0, 1, 2] and suspected(c, o) == []
+
+
+# FailureDetectorTest (:52-101): pingReqMembers 2, ping 200 / 100 ms, fixed membership
+def fd_config(n, **kw):
+    cc = ClusterConfig(pingInterval=200, pingTimeout=100, pingReqMembers=2, metadataTimeout=100)
+    return SimConfig(n_members=n, cluster=cc, tick_ms=10, record_events=True, **kw)
+
+
+def test_fd_all_trusted(oracle):  # FailureDetectorTest.testTrusted
+    c = SimulatedCluster(oracle, fd_config(3))
+    c.step(ticks_for_seconds(2))
+    for o in range(3):
+        assert trusted(c, o) == [0, 1, 2]
+    assert c.events() == []
+
+
+def test_fd_all_suspected(oracle):  # FailureDetectorTest.testSuspected: every link blocked
+    c = SimulatedCluster(oracle, fd_config(3))
+    c.partition(np.arange(3, dtype=np.uint32))
+    c.step(ticks_for_seconds(1))
+    for o in range(3):
+        assert suspected(c, o) == sorted(set(range(3)) - {o})
+
+
+def test_kill_yields_removed_everywhere(oracle):  # ClusterTest.testShutdownCluster... (:306-373)
+    n = 16
+    c = SimulatedCluster(oracle, SimConfig(n_members=n, record_events=True))
+    c.run_periods(3)
+    c.kill(5)
+    c.run_periods(5 * 5 + 5)  # suspicionTimeout(5, 16) = 25 periods
+    ev = [e for e in c.events() if e.member == 5]
+    removed = sorted(e.observer for e in ev if e.isRemoved())
+    assert removed == [o for o in range(n) if o != 5]
+    assert all(e.oldMetadata == 0 for e in ev if e.isRemoved())  # REMOVED carries the metadata
+
+
+@pytest.mark.parametrize("n,loss", [(10, 0), (10, 25), (50, 0), (50, 10), (50, 25)])
+def test_gossip_dissemination(oracle, n, loss):  # GossipProtocolTest.testGossipProtocol (:108-175)
+    c = SimulatedCluster(oracle, SimConfig(n_members=n, record_events=True))
+    c.set_default_loss(loss)
+    c.step(5)
+    c.update_incarnation(0)  # spreads ALIVE(inc 1) of member 0 (updateIncarnation, :178-190)
+    t0 = c.tick
+    sweep_ms = 2 * (3 * int(n).bit_length() + 1) * 200  # ClusterMath.gossipTimeoutToSweep(3, n, 200)
+    got = {}
+    while c.tick - t0 < sweep_ms // 100:
+        c.step(1)
+        for o in range(1, n):
+            if o not in got and (int(c.row(o)[0]) & 0xFFFFFFFF) >= 1:
+                got[o] = c.tick - t0
+        if len(got) == n - 1:
+            break
+    assert len(got) == n - 1, f"only {len(got)} of {n-1} received the gossip"
+    assert max(got.values()) * 100 < sweep_ms
+    ev = [e for e in c.events() if e.member == 0 and e.isUpdated()]
+    per_observer = {}
+    for e in ev:
+        per_observer[e.observer] = per_observer.get(e.observer, 0) + 1
+    assert all(v == 1 for v in per_observer.values()), "double delivery"
