@@ -399,8 +399,13 @@ int swim_read_gossips(swim_handle* h, uint32_t obs, uint64_t* ids, uint32_t* inf
   HIPCK(hipMemcpy(used.data(), d.slot_used, 4ull * d.SLOTS, hipMemcpyDeviceToHost));
   HIPCK(hipMemcpy(gid.data(), d.slot_gid, 8ull * d.SLOTS, hipMemcpyDeviceToHost));
   HIPCK(hipMemcpy2D(col.data(), 4, d.S + obs, 4ull * d.N, 4, d.SLOTS, hipMemcpyDeviceToHost));
-  uint32_t first = 0;
+  uint32_t first = 0, dt = 0;
   HIPCK(hipMemcpy(&first, d.firstGossip + obs, 4, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(&dt, d.dead_tick + obs, 4, hipMemcpyDeviceToHost));
+  if (dt != NEVER) {  // a crashed member keeps no gossips (its entries stay only for the infectedFrom replay)
+    *n_out = 0;
+    return SWIM_OK;
+  }
   std::vector<std::pair<uint64_t, uint32_t>> out;
   for (uint32_t g = 0; g < d.SLOTS; ++g) {
     uint32_t e = col[g];

@@ -639,7 +639,8 @@ __global__ void __launch_bounds__(256) k_hash(Dev d, uint64_t* out, uint32_t now
   uint32_t fl = d.fdLen[m], gl = d.gLen[m];
   for (uint32_t p = threadIdx.x; p < fl; p += blockDim.x) hf += hpair((uint64_t)p | (1ull << 40), d.fdl[(size_t)m * d.LCAP + p]);
   for (uint32_t p = threadIdx.x; p < gl; p += blockDim.x) hg += hpair((uint64_t)p | (2ull << 40), d.gl[(size_t)m * d.LCAP + p]);
-  for (uint32_t g = threadIdx.x; g < d.SLOTS; g += blockDim.x) {
+  const bool dead = d.dead_tick[m] != NEVER;  // a crashed member keeps no gossips (SEMANTICS.md §1)
+  for (uint32_t g = threadIdx.x; g < d.SLOTS && !dead; g += blockDim.x) {
     if (!d.slot_used[g]) continue;
     uint32_t e = d.S[(size_t)g * d.N + m];
     // receipts applied at the end of tick now-1 belong to P4 of tick `now`: not yet visible
