@@ -2,12 +2,16 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "../../include/swimhip.h"
+#include "../../include/swimhip_shard.h"
 #include "engine.h"
 
 using namespace swim;
@@ -30,6 +34,12 @@ struct swim_handle {
   std::vector<TickEvents> prof;  // SWIM_FLAG_PROFILE: one event set per tick of the current swim_step
   double prof_ms[3] = {0, 0, 0};  // accumulated k_sync_diff, k_member_tick, k_gossip_send
   uint64_t prof_diff_launches = 0;
+  // row sharding (swimhip_shard.h)
+  swim_shard_spec spec{};
+  ncclComm_t comm = nullptr;
+  unsigned long long* hcnt = nullptr;  // pinned [2W]: send then receive byte counts of the current exchange
+  std::vector<uint8_t> hsend, hrecv;  // SWIM_TRANSPORT_HOST staging
+  double xchg_ms = 0;                 // host time spent in the exchanges
 };
 
 namespace {
@@ -104,6 +114,11 @@ int build(swim_handle* h) {
   std::memset(&d, 0, sizeof(d));
   d.N = c.n_members;
   d.NS = (c.n_members + 7u) & ~7u;
+  d.W = h->spec.world ? h->spec.world : 1u;
+  d.rank = h->spec.rank;
+  d.lo = shard_lo(d.N, d.W, d.rank);
+  d.hi = shard_lo(d.N, d.W, d.rank + 1);
+  d.NL = d.hi - d.lo;
   d.F = c.gossip_fanout;
   d.kreq = c.ping_req_members;
   if (!to_ticks(c.ping_interval_ms, c.tick_ms, &d.ping_t) || !to_ticks(c.ping_timeout_ms, c.tick_ms, &d.pingTimeout_t) ||
@@ -138,7 +153,9 @@ int build(swim_handle* h) {
   d.LOOKBACK = d.LOGW * d.gossip_t;
   d.HCAP = 1u << 20;
   uint64_t slots = c.gossip_slot_cap ? c.gossip_slot_cap : std::min<uint64_t>(65535, std::max<uint64_t>(1024, (1ull << 30) / (4 * N)));
-  d.SLOTS = (uint32_t)std::min<uint64_t>(slots, 65535);
+  // every shard allocates new gossips from its own slot range; the slot table itself is replicated
+  d.SPR = (uint32_t)std::min<uint64_t>(slots, 65535 / d.W);
+  d.SLOTS = d.SPR * d.W;
   uint64_t mc = N / d.sync_t * 4 + N / d.ping_t + 1024;
   if (c.init_mode == SWIM_INIT_COLD_JOIN) mc = std::max<uint64_t>(mc, N + 1024);
   d.MSGCAP = (uint32_t)mc;
@@ -158,8 +175,9 @@ int build(swim_handle* h) {
   A(d.nextGossip, N) A(d.nextSync, N) A(d.cidCnt, N) A(d.syncSeq, N) A(d.evSeq, N) A(d.held, N) A(d.timerMin, N)
   A(d.initFlags, N) A(d.initDeadline, N) A(d.initCidBase, N) A(d.initN, N) A(d.firstGossip, N) A(d.nsub, N)
   A(d.npath, N) A(d.nfetch, N) A(d.pingIdx, N) A(d.remoteIdx, N) A(d.sel, N * 8) A(d.evHash, N)
-  A(d.row, N * d.NS) A(d.fdl, N * d.LCAP) A(d.gl, N * d.LCAP)
-  A(d.subs, N * SUBCAP * 4) A(d.paths, N * PATHCAP * 5) A(d.fetch, N * d.FCAP * FREC) A(d.groups, N * d.GRCAP * GREC)
+  const uint64_t NL = d.NL;  // per-observer arrays: this shard's rows only
+  A(d.row, NL * d.NS) A(d.fdl, NL * d.LCAP) A(d.gl, NL * d.LCAP)
+  A(d.subs, NL * SUBCAP * 4) A(d.paths, NL * PATHCAP * 5) A(d.fetch, NL * d.FCAP * FREC) A(d.groups, NL * d.GRCAP * GREC)
   A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F)
   A(d.log_tick, N * d.LOGW) A(d.log_spread, N * d.LOGW) A(d.log_cnt, N * d.LOGW) A(d.log_tg, N * d.LOGW * d.F)
   A(d.log_pos, N)
@@ -172,6 +190,32 @@ int build(swim_handle* h) {
   A(d.m_idx, d.MSGCAP) A(d.m_head, N) A(d.next_evt, N) A(d.pending_inc, N) A(d.m_key, d.MSGCAP) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
   A(d.pool, d.POOLCAP) A(d.pool_used, 1)
   A(d.ev, (uint64_t)d.EVCAP * 8) A(d.ev_n, 1) A(d.ctr, C_NCTR) A(d.err, 8)
+  if (d.W > 1) {
+    d.MW = (d.NCHUNK + 63) / 64;
+    d.NSCAP = 1u << 16;
+    d.RRCAP = d.NL;
+    d.SWCAP = 1u << 20;
+    d.RQCAP = d.MSGCAP;
+    d.RXCAP = d.MSGCAP;
+    d.CHCAP = h->spec.chunk_cap ? h->spec.chunk_cap : (uint32_t)std::min<uint64_t>(4096, (uint64_t)d.MSGCAP * d.NCHUNK);
+    uint64_t se = sizeof(SyncMsg) + 8 + 8ull * d.MW;
+    d.XA_PEER = ((32 + 4ull * NSW * d.NSCAP + 4ull * RRW * d.RRCAP + se * d.RQCAP + 511) & ~255ull) +
+                (uint64_t)d.CHCAP * CH * 8;
+    d.XB_PEER = 16 + 8ull * std::min<uint64_t>((uint64_t)d.DCAP + d.SWCAP, 1ull << 25);
+    A(d.base_row, d.NS) A(d.xn, 8) A(d.ns_rec, (uint64_t)d.NSCAP * NSW) A(d.rr_rec, (uint64_t)d.RRCAP * RRW)
+    A(d.sw_rec, d.SWCAP) A(d.rq_n, d.W) A(d.rq_list, (uint64_t)d.W * d.RQCAP)
+    A(d.rq_mask, (uint64_t)d.W * d.RQCAP * d.MW) A(d.rq_cnt, (uint64_t)d.W * d.RQCAP) A(d.rq_base, (uint64_t)d.W * d.RQCAP)
+    A(d.mtmp, d.MSGCAP) A(d.rx_mask, (uint64_t)d.RXCAP * d.MW) A(d.rx_off, d.RXCAP)
+    A(d.xa_send, d.W * d.XA_PEER) A(d.xa_recv, d.W * d.XA_PEER) A(d.xb_send, d.W * d.XB_PEER)
+    A(d.xb_recv, d.W * d.XB_PEER) A(d.xa_scnt, d.W) A(d.xa_rcnt, d.W) A(d.xb_scnt, d.W) A(d.xb_rcnt, d.W)
+    HIPCK(hipMemset(d.xa_rcnt, 0, 8ull * d.W));
+    HIPCK(hipMemset(d.xb_rcnt, 0, 8ull * d.W));
+    HIPCK(hipHostMalloc((void**)&h->hcnt, 16ull * d.W, hipHostMallocDefault));
+    if (h->spec.transport == SWIM_TRANSPORT_HOST) {
+      h->hsend.resize(d.W * std::max(d.XA_PEER, d.XB_PEER));
+      h->hrecv.resize(d.W * std::max(d.XA_PEER, d.XB_PEER));
+    }
+  }
 #undef A
   HIPCK(hipMemset(d.S, 0, (size_t)d.SLOTS * N * 4));
   HIPCK(hipMemset(d.ctr, 0, C_NCTR * 8));
@@ -181,8 +225,8 @@ int build(swim_handle* h) {
   HIPCK(hipMemset(d.nmsg, 0, 8));
   HIPCK(hipMemset(d.arena_used, 0, 8));
   HIPCK(hipMemset(d.tcnt, 0, N * 4));
-  HIPCK(hipMemset(d.subs, 0, N * SUBCAP * 16));
-  int32_t top = (int32_t)d.SLOTS;
+  HIPCK(hipMemset(d.subs, 0, NL * SUBCAP * 16));
+  int32_t top = (int32_t)d.SPR;
   HIPCK(hipMemcpy(d.free_top, &top, 4, hipMemcpyHostToDevice));
   std::vector<uint32_t> never(MAX_EPOCHS, NEVER);
   HIPCK(hipMemcpy(d.ep_from, never.data(), 4 * MAX_EPOCHS, hipMemcpyHostToDevice));
@@ -197,6 +241,121 @@ int build(swim_handle* h) {
   if ((rc = push_epoch(h)) != 0) return rc;
   return check_err(h);
 }
+
+// one all-to-all of per-peer byte blocks (fixed-capacity regions of `cap` bytes in send / recv, rank order).
+// The byte counts are device-resident (written by the pack kernels); the transport needs them on the host.
+int exchange(swim_handle* h, uint8_t* send, uint8_t* recv, uint64_t cap, unsigned long long* scnt,
+             unsigned long long* rcnt) {
+  const uint32_t W = h->d.W, me = h->d.rank;
+  hipStream_t st = h->stream;
+  unsigned long long* hc = h->hcnt;
+  auto t0 = std::chrono::steady_clock::now();
+  if (h->spec.transport == SWIM_TRANSPORT_RCCL) {
+    if (ncclAllToAll(scnt, rcnt, 1, ncclUint64, h->comm, st) != ncclSuccess) {
+      h->err = "ncclAllToAll (exchange byte counts) failed";
+      return SWIM_EDEVICE;
+    }
+    HIPCK(hipMemcpyAsync(hc, scnt, 8ull * W, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(hc + W, rcnt, 8ull * W, hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    for (uint32_t q = 0; q < W; ++q)
+      if (hc[q] > cap || hc[W + q] > cap) {
+        h->err = "exchange block larger than its region";
+        return SWIM_ECAPACITY;
+      }
+    bool ok = ncclGroupStart() == ncclSuccess;
+    for (uint32_t q = 0; q < W && ok; ++q) {
+      if (q == me) continue;
+      if (hc[q]) ok &= ncclSend(send + (size_t)q * cap, hc[q], ncclUint8, (int)q, h->comm, st) == ncclSuccess;
+      if (hc[W + q]) ok &= ncclRecv(recv + (size_t)q * cap, hc[W + q], ncclUint8, (int)q, h->comm, st) == ncclSuccess;
+    }
+    ok &= ncclGroupEnd() == ncclSuccess;
+    if (!ok) {
+      h->err = "RCCL send/recv group failed";
+      return SWIM_EDEVICE;
+    }
+  } else {
+    HIPCK(hipMemcpyAsync(hc, scnt, 8ull * W, hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    uint64_t off = 0;
+    for (uint32_t q = 0; q < W; ++q) {
+      if (hc[q] > cap) {
+        h->err = "exchange block larger than its region";
+        return SWIM_ECAPACITY;
+      }
+      if (hc[q]) HIPCK(hipMemcpyAsync(h->hsend.data() + off, send + (size_t)q * cap, hc[q], hipMemcpyDeviceToHost, st));
+      off += hc[q];
+    }
+    HIPCK(hipStreamSynchronize(st));
+    uint64_t sb[64], rb[64];
+    for (uint32_t q = 0; q < W; ++q) sb[q] = hc[q], rb[q] = 0;
+    if (h->spec.exchange(h->spec.ctx, h->hsend.data(), sb, h->hrecv.data(), h->hrecv.size(), rb) != 0) {
+      h->err = "host exchange callback failed";
+      return SWIM_EDEVICE;
+    }
+    off = 0;
+    for (uint32_t p = 0; p < W; ++p) {
+      if (rb[p] > cap) {
+        h->err = "received exchange block larger than its region";
+        return SWIM_ECAPACITY;
+      }
+      if (rb[p]) HIPCK(hipMemcpyAsync(recv + (size_t)p * cap, h->hrecv.data() + off, rb[p], hipMemcpyHostToDevice, st));
+      off += rb[p];
+      hc[W + p] = rb[p];
+    }
+    HIPCK(hipMemcpyAsync(rcnt, hc + W, 8ull * W, hipMemcpyHostToDevice, st));
+    HIPCK(hipStreamSynchronize(st));
+  }
+  h->xchg_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return SWIM_OK;
+}
+
+int create(const swim_config* cfg, const swim_shard_spec* spec, swim_handle** out) {
+  if (!cfg || !out) return SWIM_EINVAL;
+  *out = nullptr;
+  const swim_config& c = *cfg;
+  if (c.n_members < 2 || c.n_members > (1u << 20) || c.ping_timeout_ms >= c.ping_interval_ms || c.gossip_fanout == 0 || c.gossip_fanout > 8 ||
+      c.ping_req_members > 8 || c.n_seeds > 16 || c.mode != SWIM_MODE_FULL)
+    return SWIM_EINVAL;
+  if (c.latency_ticks != 1) return SWIM_EUNSUPPORTED;  // gossip data plane assumes one-tick hops
+  if (spec) {
+    if (spec->world < 1 || spec->world > 64 || spec->rank >= spec->world || spec->world > c.n_members / 2) return SWIM_EINVAL;
+    if (spec->world > 1 && spec->transport != SWIM_TRANSPORT_RCCL &&
+        !(spec->transport == SWIM_TRANSPORT_HOST && spec->exchange))
+      return SWIM_EINVAL;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= (int)c.device) return SWIM_EDEVICE;
+  auto* h = new swim_handle();
+  h->cfg = c;
+  if (spec) h->spec = *spec;
+  if (h->spec.world == 0) h->spec.world = 1;
+  if (hipSetDevice((int)c.device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return SWIM_EDEVICE;
+  }
+  if (h->spec.world > 1 && h->spec.transport == SWIM_TRANSPORT_RCCL) {
+    ncclUniqueId id;
+    static_assert(sizeof(id) == 128, "ncclUniqueId size");
+    std::memcpy(&id, h->spec.rccl_id, sizeof(id));
+    if (ncclCommInitRank(&h->comm, (int)h->spec.world, id, (int)h->spec.rank) != ncclSuccess) {
+      fprintf(stderr, "swim_create_sharded: ncclCommInitRank failed (rank %u of %u)\n", h->spec.rank, h->spec.world);
+      h->comm = nullptr;
+      swim_destroy(h);
+      return SWIM_EDEVICE;
+    }
+  }
+  int rc = build(h);
+  if (rc != SWIM_OK) {
+    fprintf(stderr, "swim_create: %s\n", h->err.c_str());
+    swim_destroy(h);
+    return rc;
+  }
+  *out = h;
+  return SWIM_OK;
+}
+
+bool owns(const swim_handle* h, uint32_t m) { return m >= h->d.lo && m < h->d.hi; }
 
 }  // namespace
 
@@ -227,29 +386,28 @@ int swim_is_overrides(uint32_t s1, uint32_t i1, uint32_t s0, uint32_t i0) { retu
 uint32_t swim_ceil_log2(uint32_t n) { return bitlen(n); }
 
 int swim_create(const swim_config* cfg, swim_handle** out) {
-  if (!cfg || !out) return SWIM_EINVAL;
-  *out = nullptr;
-  const swim_config& c = *cfg;
-  if (c.n_members < 2 || c.n_members > (1u << 20) || c.ping_timeout_ms >= c.ping_interval_ms || c.gossip_fanout == 0 || c.gossip_fanout > 8 ||
-      c.ping_req_members > 8 || c.n_seeds > 16 || c.mode != SWIM_MODE_FULL || c.n_members > (1u << 30))
-    return SWIM_EINVAL;
-  if (c.latency_ticks != 1) return SWIM_EUNSUPPORTED;  // gossip data plane assumes one-tick hops
-  if (c.n_gpus > 1) return SWIM_EUNSUPPORTED;
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= (int)c.device) return SWIM_EDEVICE;
-  auto* h = new swim_handle();
-  h->cfg = c;
-  if (hipSetDevice((int)c.device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
-    delete h;
-    return SWIM_EDEVICE;
-  }
-  int rc = build(h);
-  if (rc != SWIM_OK) {
-    fprintf(stderr, "swim_create: %s\n", h->err.c_str());
-    swim_destroy(h);
-    return rc;
-  }
-  *out = h;
+  // one handle for all N observers on one GPU; several GPUs shard the observers (swim_create_sharded)
+  if (cfg && cfg->n_gpus > 1) return SWIM_EUNSUPPORTED;
+  return create(cfg, nullptr, out);
+}
+
+int swim_create_sharded(const swim_config* cfg, const swim_shard_spec* spec, swim_handle** out) {
+  if (!spec) return SWIM_EINVAL;
+  return create(cfg, spec, out);
+}
+
+int swim_rccl_unique_id(uint8_t* out128) {
+  if (!out128) return SWIM_EINVAL;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return SWIM_EDEVICE;
+  std::memcpy(out128, &id, 128);
+  return SWIM_OK;
+}
+
+int swim_shard_range(swim_handle* h, uint32_t* lo, uint32_t* hi) {
+  if (!h || !lo || !hi) return SWIM_EINVAL;
+  *lo = h->d.lo;
+  *hi = h->d.hi;
   return SWIM_OK;
 }
 
@@ -260,6 +418,8 @@ int swim_destroy(swim_handle* h) {
   for (void* p : h->allocs) hipFree(p);
   for (auto& te : h->prof)
     for (auto& e : te.ev) hipEventDestroy((hipEvent_t)e);
+  if (h->comm) ncclCommDestroy(h->comm);
+  if (h->hcnt) hipHostFree(h->hcnt);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
   return SWIM_OK;
@@ -277,8 +437,19 @@ int swim_step(swim_handle* h, uint32_t n) {
       h->prof.push_back(te);
     }
   uint64_t first = h->tick;
+  const Dev& d = h->d;
   for (uint32_t i = 0; i < n; ++i) {
-    launch_tick(h->d, (uint32_t)h->tick, h->stream, profile ? &h->prof[i] : nullptr);
+    const TickEvents* te = profile ? &h->prof[i] : nullptr;
+    if (d.W == 1) {
+      launch_tick(d, (uint32_t)h->tick, h->stream, te);
+    } else {
+      int xr;
+      launch_tick_a(d, (uint32_t)h->tick, h->stream, te);
+      if ((xr = exchange(h, d.xa_send, d.xa_recv, d.XA_PEER, d.xa_scnt, d.xa_rcnt)) != SWIM_OK) return xr;
+      launch_tick_b(d, (uint32_t)h->tick, h->stream, te);
+      if ((xr = exchange(h, d.xb_send, d.xb_recv, d.XB_PEER, d.xb_scnt, d.xb_rcnt)) != SWIM_OK) return xr;
+      launch_tick_c(d, (uint32_t)h->tick, h->stream);
+    }
     h->tick++;
   }
   int rc = check_err(h);
@@ -316,6 +487,7 @@ int swim_kill(swim_handle* h, uint32_t m) {
 
 int swim_update_incarnation(swim_handle* h, uint32_t m) {
   if (!h || m >= h->d.N) return SWIM_EINVAL;
+  if (!owns(h, m)) return SWIM_OK;  // the owning shard bumps it; the others learn it from its gossip
   uint32_t one = 1, dt = 0;
   HIPCK(hipStreamSynchronize(h->stream));
   HIPCK(hipMemcpy(&dt, h->d.dead_tick + m, 4, hipMemcpyDeviceToHost));
@@ -354,9 +526,9 @@ int swim_current_tick(swim_handle* h, uint64_t* t) {
 }
 
 int swim_read_row(swim_handle* h, uint32_t obs, uint64_t* out, size_t cap) {
-  if (!h || obs >= h->d.N || cap < h->d.N) return SWIM_EINVAL;
+  if (!h || obs >= h->d.N || cap < h->d.N || !owns(h, obs)) return SWIM_EINVAL;
   HIPCK(hipStreamSynchronize(h->stream));
-  HIPCK(hipMemcpy(out, h->d.row + (size_t)obs * h->d.NS, 8ull * h->d.N, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(out, h->d.row + lidx(h->d, obs) * h->d.NS, 8ull * h->d.N, hipMemcpyDeviceToHost));
   for (uint32_t s = 0; s < h->d.N; ++s)
     if (rec_status(out[s]) == ST_ABSENT) out[s] = 0;
   return SWIM_OK;
@@ -366,6 +538,7 @@ int swim_state_hash(swim_handle* h, uint64_t* out, size_t cap) {
   if (!h || cap < 6ull * h->d.N) return SWIM_EINVAL;
   uint64_t* dout = nullptr;
   HIPCK(hipMalloc(&dout, 48ull * h->d.N));
+  HIPCK(hipMemsetAsync(dout, 0, 48ull * h->d.N, h->stream));  // other shards' observers stay zero
   launch_hash(h->d, dout, (uint32_t)h->tick, h->stream);
   HIPCK(hipStreamSynchronize(h->stream));
   HIPCK(hipMemcpy(out, dout, 48ull * h->d.N, hipMemcpyDeviceToHost));
@@ -375,14 +548,14 @@ int swim_state_hash(swim_handle* h, uint64_t* out, size_t cap) {
 
 int swim_read_lists(swim_handle* h, uint32_t obs, uint32_t* fd, uint32_t* fd_len, uint32_t* gl, uint32_t* g_len,
                     size_t cap, int32_t* cursors) {
-  if (!h || obs >= h->d.N) return SWIM_EINVAL;
+  if (!h || obs >= h->d.N || !owns(h, obs)) return SWIM_EINVAL;
   HIPCK(hipStreamSynchronize(h->stream));
   uint32_t fl = 0, glen = 0;
   HIPCK(hipMemcpy(&fl, h->d.fdLen + obs, 4, hipMemcpyDeviceToHost));
   HIPCK(hipMemcpy(&glen, h->d.gLen + obs, 4, hipMemcpyDeviceToHost));
   if (fl > cap || glen > cap) return SWIM_EINVAL;
-  HIPCK(hipMemcpy(fd, h->d.fdl + (size_t)obs * h->d.LCAP, 4ull * fl, hipMemcpyDeviceToHost));
-  HIPCK(hipMemcpy(gl, h->d.gl + (size_t)obs * h->d.LCAP, 4ull * glen, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(fd, h->d.fdl + lidx(h->d, obs) * h->d.LCAP, 4ull * fl, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(gl, h->d.gl + lidx(h->d, obs) * h->d.LCAP, 4ull * glen, hipMemcpyDeviceToHost));
   HIPCK(hipMemcpy(&cursors[0], h->d.pingIdx + obs, 4, hipMemcpyDeviceToHost));
   HIPCK(hipMemcpy(&cursors[1], h->d.remoteIdx + obs, 4, hipMemcpyDeviceToHost));
   *fd_len = fl;
@@ -391,7 +564,7 @@ int swim_read_lists(swim_handle* h, uint32_t obs, uint32_t* fd, uint32_t* fd_len
 }
 
 int swim_read_gossips(swim_handle* h, uint32_t obs, uint64_t* ids, uint32_t* inf, size_t cap, size_t* n_out) {
-  if (!h || obs >= h->d.N || !n_out) return SWIM_EINVAL;
+  if (!h || obs >= h->d.N || !n_out || !owns(h, obs)) return SWIM_EINVAL;
   HIPCK(hipStreamSynchronize(h->stream));
   const Dev& d = h->d;
   std::vector<uint32_t> used(d.SLOTS), col(d.SLOTS);

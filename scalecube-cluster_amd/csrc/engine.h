@@ -28,7 +28,13 @@ constexpr uint32_t S_TICK_MASK = (1u << 29) - 1u;
 // device error bits
 constexpr uint32_t E_SLOTS = 1, E_FETCH = 2, E_SUBS = 4, E_PATHS = 8, E_GROUPS = 16, E_MSGS = 32, E_ARENA = 64,
                    E_POOL = 128, E_LIST = 256, E_DELIV = 512, E_RECEIPTS = 1024, E_CONTACTS = 2048,
-                   E_REBORN = 4096, E_LOGWIN = 8192, E_EPOCH = 16384, E_EVENTS = 32768, E_SORTCAP = 65536;
+                   E_REBORN = 4096, E_LOGWIN = 8192, E_EPOCH = 16384, E_EVENTS = 32768, E_SORTCAP = 65536,
+                   E_XCAP = 1u << 17;
+
+// row sharding: SyncMsg.payload values
+constexpr uint32_t PAY_RX = 0x40000000u;  // received from another shard: PAY_RX | rx index (dirty chunks + baseline)
+constexpr uint32_t RRW = 12;              // words per gossip-round record: m, cnt, spread, period, targets[8]
+constexpr uint32_t NSW = 8;               // words per new-gossip-slot record
 
 // counters (swim_counters order after .tick)
 enum Ctr { C_R = 0, C_W, C_M, C_G, C_E, C_LOST, C_GCREATED, C_SYNCMERGE, C_NCTR = 16 };
@@ -117,7 +123,43 @@ struct Dev {
   unsigned long long* ctr;  // [C_NCTR]
   uint32_t* err;            // [8] bits, info...
   const Dev* self;          // device-resident copy of this struct (kernels index it through a pointer)
+
+  // ---- row sharding (W > 1) ----
+  // This shard owns observers [lo, hi): their rows, lists, subscriptions, paths, fetches and groups are stored
+  // at local index m - lo. Everything in the gossip plane (slots, S, round logs, hist) is replicated and kept
+  // identical on every shard by applying the union of every shard's gossip records each tick.
+  uint32_t W, rank, lo, hi, NL, SPR, MW;  // SPR: gossip slots owned per shard; MW: u64 words per chunk mask
+  uint32_t NSCAP, RRCAP, SWCAP, RQCAP, RXCAP, CHCAP;
+  uint64_t XA_PEER, XB_PEER;  // bytes per peer region of the two exchange buffers
+  uint64_t* base_row;  // [NS] baseline record keys: a remote SYNC payload ships only its chunks that differ
+  uint32_t* xn;        // [8] 0 new slots, 1 round records, 2 sweeps, 4 inbound msgs (mtmp), 5 rx payloads
+  uint32_t* ns_rec;    // [NSCAP][NSW] gossips created on this shard this tick
+  uint32_t* rr_rec;    // [RRCAP][RRW] gossip rounds of this shard's members this tick
+  uint64_t* sw_rec;    // [SWCAP] (slot << 32 | member) sweeps by this shard's members this tick
+  uint32_t* rq_n;      // [W] SYNC messages to each shard this tick
+  uint32_t* rq_list;   // [W][RQCAP] their indices in msgs[b]
+  uint64_t* rq_mask;   // [W * RQCAP][MW] chunks of the payload that differ from base_row
+  uint32_t* rq_cnt;    // [W * RQCAP] popcount of the mask
+  uint32_t* rq_base;   // [W * RQCAP] first chunk slot in the peer region
+  SyncMsg* mtmp;       // [MSGCAP] inbound list of the next tick while it is assembled
+  uint64_t* rx_mask;   // [RXCAP][MW]
+  uint64_t* rx_off;    // [RXCAP] byte offset (in xa_recv) of the first shipped chunk of a received payload
+  uint8_t *xa_send, *xa_recv, *xb_send, *xb_recv;  // [W][X*_PEER]
+  unsigned long long *xa_scnt, *xa_rcnt, *xb_scnt, *xb_rcnt;  // [W] bytes per peer region
 };
+
+// local index of an observer owned by this shard
+__host__ __device__ __forceinline__ size_t lidx(const Dev& d, uint32_t m) { return (size_t)(m - d.lo); }
+// first observer of shard r: contiguous ranges floor(r N / W)
+__host__ __device__ __forceinline__ uint32_t shard_lo(uint32_t N, uint32_t W, uint32_t r) {
+  return (uint32_t)((uint64_t)r * N / W);
+}
+__host__ __device__ __forceinline__ uint32_t shard_of(uint32_t N, uint32_t W, uint32_t m) {
+  uint32_t r = (uint32_t)((uint64_t)m * W / N);
+  while (r > 0 && m < shard_lo(N, W, r)) --r;
+  while (r + 1 < W && m >= shard_lo(N, W, r + 1)) ++r;
+  return r;
+}
 
 // optional per-tick timing of the three main kernels (HIP events on the engine's stream)
 struct TickEvents {
@@ -127,6 +169,11 @@ struct TickEvents {
 // host-side kernel launchers (one HIP stream)
 void launch_init(const Dev& d, void* stream);
 void launch_tick(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr);
+// sharded tick (W > 1): A = SYNC diff + member control + pack exchange A; B = unpack A, gossip sends, pack
+// exchange B; C = unpack B, apply receipts, routing, slot recycling. The host runs the exchanges in between.
+void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr);
+void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr);
+void launch_tick_c(const Dev& d, uint32_t k, void* stream);
 void launch_kill(const Dev& d, uint32_t member, void* stream);
 void launch_hash(const Dev& d, uint64_t* out, uint32_t now, void* stream);
 

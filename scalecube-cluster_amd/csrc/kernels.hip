@@ -6,6 +6,17 @@
 namespace swim {
 
 __global__ void k_member_tick(const Dev* __restrict__ dp, uint32_t k);  // member.hip
+// shard.hip
+__global__ void k_sync_route(Dev d, uint32_t b);
+__global__ void k_sync_dirty(Dev d, uint32_t b);
+__global__ void k_pack_a(Dev d, uint32_t b);
+__global__ void k_pack_a_chunks(Dev d, uint32_t b);
+__global__ void k_unpack_a(Dev d, uint32_t k);
+__global__ void k_msgs_commit(Dev d, uint32_t b);
+__global__ void k_pack_b(Dev d);
+__global__ void k_unpack_b_sweeps(Dev d);
+__global__ void k_unpack_b_deliv(Dev d);
+__global__ void k_round_reset(Dev d);
 
 // ------------------------------------------------------------------------------------------------------------
 // init (SEMANTICS.md §3)
@@ -44,15 +55,17 @@ __global__ void k_init_members(Dev d) {
   d.m_head[m] = NEVER;
   d.next_evt[m] = NEVER;
   d.pending_inc[m] = 0;
-  for (uint32_t g = 0; g < d.GRCAP; ++g) d.groups[((size_t)m * d.GRCAP + g) * GREC + 5] = 0;
+  if (m >= d.lo && m < d.hi)
+    for (uint32_t g = 0; g < d.GRCAP; ++g) d.groups[(lidx(d, m) * d.GRCAP + g) * GREC + 5] = 0;
   for (uint32_t e = 0; e < d.LOGW; ++e) d.log_tick[(size_t)m * d.LOGW + e] = NEVER;
 }
 
 // one block per observer row (grid-strided): rows are written with coalesced 8-B stores
 __global__ void k_init_rows(Dev d) {
   uint64_t full = rec_key(ST_ALIVE, 0) | META_BIT;
-  for (uint32_t m = blockIdx.x; m < d.N; m += gridDim.x) {
-    uint64_t* row = d.row + (size_t)m * d.NS;
+  for (uint32_t li = blockIdx.x; li < d.NL; li += gridDim.x) {
+    uint32_t m = d.lo + li;
+    uint64_t* row = d.row + (size_t)li * d.NS;
     for (uint32_t s = threadIdx.x; s < d.NS; s += blockDim.x)
       row[s] = s >= d.N ? 0ull : (d.init_mode == 1 || m == s) ? full : 0ull;
   }
@@ -62,11 +75,11 @@ __global__ void k_init_rows(Dev d) {
 __global__ void k_init_lists(Dev d) {
   if (d.init_mode != 1 || d.N < 2) return;
   uint32_t n = d.N - 1;
-  for (uint32_t m = blockIdx.x; m < d.N; m += gridDim.x) {
+  for (uint32_t m = d.lo + blockIdx.x; m < d.hi; m += gridDim.x) {
     for (uint32_t w = 0; w < 2; ++w) {
       FeistelPerm P = make_perm(n, init_draw(d, m, 16 + 4 * w + 0, 0), init_draw(d, m, 16 + 4 * w + 1, 0),
                                 init_draw(d, m, 16 + 4 * w + 2, 0), init_draw(d, m, 16 + 4 * w + 3, 0));
-      uint32_t* L = (w == 0 ? d.fdl : d.gl) + (size_t)m * d.LCAP;
+      uint32_t* L = (w == 0 ? d.fdl : d.gl) + lidx(d, m) * d.LCAP;
       for (uint32_t p = threadIdx.x; p < n; p += blockDim.x) {
         uint32_t j = feistel(P, p);
         L[p] = j < m ? j : j + 1;
@@ -80,7 +93,14 @@ __global__ void k_init_slots(Dev d) {
   if (g >= d.SLOTS) return;
   d.slot_used[g] = 0;
   d.slot_holders[g] = 0;
-  d.free_list[g] = d.SLOTS - 1 - g;
+  // each shard allocates only from its own slot range [rank SPR, (rank+1) SPR), so slot ids are global
+  if (g < d.SPR) d.free_list[g] = d.rank * d.SPR + d.SPR - 1 - g;
+}
+
+// the SYNC baseline row (record keys): what a PRECONVERGED row starts as, an empty row for a cold join
+__global__ void k_init_base(Dev d) {
+  uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < d.NS) d.base_row[s] = (s < d.N && d.init_mode == 1) ? rec_key(ST_ALIVE, 0) : 0ull;
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -272,12 +292,29 @@ __global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b) {
   for (uint32_t w = blockIdx.x; w < total; w += gridDim.x) {
     uint32_t mi = w / d.NCHUNK, c = w % d.NCHUNK;
     const SyncMsg& mm = d.msgs[b][mi];
-    const uint64_t* pay = mm.payload == NEVER ? d.row + (size_t)mm.src * d.NS : d.arena[b] + (size_t)mm.payload * d.NS;
-    const uint64_t* rcv = d.row + (size_t)mm.dst * d.NS;
-    uint32_t s0 = c * CH + threadIdx.x * 8;
+    const uint32_t s0 = c * CH + threadIdx.x * 8;
+    // this lane's 8 payload records: the sender's live row or its copy-on-write snapshot; for a payload
+    // received from another shard, the shipped chunk if it differs from the baseline, else the baseline
+    const uint64_t* p8;
+    if (mm.payload == NEVER) {
+      p8 = d.row + lidx(d, mm.src) * d.NS + s0;
+    } else if (mm.payload & PAY_RX) {
+      const uint32_t ri = mm.payload & ~PAY_RX;
+      const uint64_t* mk = d.rx_mask + (size_t)ri * d.MW;
+      if ((mk[c >> 6] >> (c & 63)) & 1ull) {
+        uint32_t rank = __popcll(mk[c >> 6] & ((1ull << (c & 63)) - 1ull));
+        for (uint32_t q = 0; q < (c >> 6); ++q) rank += __popcll(mk[q]);
+        p8 = (const uint64_t*)(d.xa_recv + d.rx_off[ri]) + (size_t)rank * CH + threadIdx.x * 8;
+      } else {
+        p8 = d.base_row + s0;
+      }
+    } else {
+      p8 = d.arena[b] + (size_t)mm.payload * d.NS + s0;
+    }
+    const uint64_t* rcv = d.row + lidx(d, mm.dst) * d.NS;
     uint64_t p[8], r[8];
     if (s0 < d.NS) {  // NS is a multiple of 8: the 64-B group is in bounds, padding entries are 0 (absent)
-      const ulonglong2* pv = (const ulonglong2*)(pay + s0);
+      const ulonglong2* pv = (const ulonglong2*)p8;
       const ulonglong2* rv = (const ulonglong2*)(rcv + s0);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -500,8 +537,8 @@ __global__ void k_gossip_active(Dev d, uint32_t* active, uint32_t* nactive) {
 
 // contact flags: did target t = T[m][s] choose m in a logged round inside the look-back window?
 __global__ void k_gossip_contacts(Dev d, uint32_t k) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= d.N * d.F) return;
+  uint32_t i = d.lo * d.F + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= d.hi * d.F) return;
   uint32_t m = i / d.F, s = i % d.F;
   uint32_t flag = 0;
   if (d.tround[m] && s < d.tcnt[m]) {
@@ -524,12 +561,12 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
   const Dev& d = *dp;
   __shared__ unsigned long long red[256];
   uint32_t na = *nactive;
-  uint32_t mchunks = (d.N + 255) / 256;
+  uint32_t mchunks = (d.NL + 255) / 256;  // this shard's senders
   unsigned long long sends = 0;
   for (uint32_t w = blockIdx.x; w < na * mchunks; w += gridDim.x) {
     uint32_t g = active[w / mchunks];
-    uint32_t m = (w % mchunks) * 256 + threadIdx.x;
-    if (m >= d.N || !d.tround[m]) continue;
+    uint32_t m = d.lo + (w % mchunks) * 256 + threadIdx.x;
+    if (m >= d.hi || !d.tround[m]) continue;
     uint32_t* Sg = d.S + (size_t)g * d.N;
     uint32_t e = Sg[m];
     if (!s_held(e)) continue;
@@ -564,6 +601,13 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
       atomicOr(&Sg[m], S_SWEPT);
       atomicSub(&d.held[m], 1u);
       atomicSub(&d.slot_holders[g], 1);
+      if (d.W > 1) {  // applied on the other shards from exchange B
+        uint32_t i = atomicAdd(&d.xn[2], 1u);
+        if (i < d.SWCAP)
+          d.sw_rec[i] = ((uint64_t)g << 32) | m;
+        else
+          atomicOr(d.err, E_XCAP);
+      }
     }
   }
   red[threadIdx.x] = sends;
@@ -592,6 +636,7 @@ __global__ void k_gossip_apply(Dev d, uint32_t k) {
     *p = ne;
     atomicAdd(&d.held[t], 1u);
     atomicAdd(&d.slot_holders[g], 1);
+    if (t < d.lo || t >= d.hi) continue;  // P4 of another shard's member
     uint32_t ri = atomicAdd(d.rc_n, 1u);
     if (ri < d.RCAP)
       d.rc_raw[ri] = ((uint64_t)t << 32) | g;
@@ -611,8 +656,10 @@ __global__ void __launch_bounds__(256) k_gossip_free(Dev d, const uint32_t* acti
     __syncthreads();
     if (threadIdx.x == 0) {
       d.slot_used[g] = 0;
-      int pos = atomicAdd(d.free_top, 1);
-      d.free_list[pos] = g;
+      if (g / d.SPR == d.rank) {  // back to the owning shard's free list
+        int pos = atomicAdd(d.free_top, 1);
+        d.free_list[pos] = g;
+      }
     }
   }
 }
@@ -628,17 +675,17 @@ __global__ void k_kill(Dev d, uint32_t m) {
 // state hashes (SEMANTICS.md §8), one block per member
 __global__ void __launch_bounds__(256) k_hash(Dev d, uint64_t* out, uint32_t now) {
   __shared__ unsigned long long red[4][256];
-  uint32_t m = blockIdx.x;
-  if (m >= d.N) return;
+  uint32_t m = d.lo + blockIdx.x;
+  if (m >= d.hi) return;
   unsigned long long hr = 0, hf = 0, hg = 0, hgs = 0;
-  const uint64_t* row = d.row + (size_t)m * d.NS;
+  const uint64_t* row = d.row + lidx(d, m) * d.NS;
   for (uint32_t s = threadIdx.x; s < d.N; s += blockDim.x) {
     uint64_t v = row[s];
     if (rec_status(v) != ST_ABSENT) hr += hpair(s, v);
   }
   uint32_t fl = d.fdLen[m], gl = d.gLen[m];
-  for (uint32_t p = threadIdx.x; p < fl; p += blockDim.x) hf += hpair((uint64_t)p | (1ull << 40), d.fdl[(size_t)m * d.LCAP + p]);
-  for (uint32_t p = threadIdx.x; p < gl; p += blockDim.x) hg += hpair((uint64_t)p | (2ull << 40), d.gl[(size_t)m * d.LCAP + p]);
+  for (uint32_t p = threadIdx.x; p < fl; p += blockDim.x) hf += hpair((uint64_t)p | (1ull << 40), d.fdl[lidx(d, m) * d.LCAP + p]);
+  for (uint32_t p = threadIdx.x; p < gl; p += blockDim.x) hg += hpair((uint64_t)p | (2ull << 40), d.gl[lidx(d, m) * d.LCAP + p]);
   const bool dead = d.dead_tick[m] != NEVER;  // a crashed member keeps no gossips (SEMANTICS.md §1)
   for (uint32_t g = threadIdx.x; g < d.SLOTS && !dead; g += blockDim.x) {
     if (!d.slot_used[g]) continue;
@@ -679,6 +726,7 @@ void launch_init(const Dev& d, void* stream) {
   hipLaunchKernelGGL(k_init_rows, dim3(4096), dim3(256), 0, st, d);
   hipLaunchKernelGGL(k_init_lists, dim3(4096), dim3(256), 0, st, d);
   hipLaunchKernelGGL(k_init_slots, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, st, d);
+  if (d.W > 1) hipLaunchKernelGGL(k_init_base, dim3(cdiv(d.NS, 256)), dim3(256), 0, st, d);
 }
 
 void launch_tick(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
@@ -697,7 +745,7 @@ void launch_tick(const Dev& d, uint32_t k, void* stream, const TickEvents* prof)
     if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
   }
   if (prof) hipEventRecord((hipEvent_t)prof->ev[2], st);
-  hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.N, 256)), dim3(256), 0, st, d.self, k);
+  hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[3], st);
   // gossip data plane for the rounds that ran in this tick
   uint32_t* active = d.active;
@@ -706,7 +754,7 @@ void launch_tick(const Dev& d, uint32_t k, void* stream, const TickEvents* prof)
   hipMemsetAsync(d.deliv_n, 0, sizeof(uint32_t), st);
   hipMemsetAsync(d.rc_n, 0, sizeof(uint32_t), st);
   hipLaunchKernelGGL(k_gossip_active, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, st, d, active, nactive);
-  hipLaunchKernelGGL(k_gossip_contacts, dim3(cdiv((uint64_t)d.N * d.F, 256)), dim3(256), 0, st, d, k);
+  hipLaunchKernelGGL(k_gossip_contacts, dim3(cdiv((uint64_t)d.NL * d.F, 256)), dim3(256), 0, st, d, k);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[4], st);
   hipLaunchKernelGGL(k_gossip_send, dim3(1024), dim3(256), 0, st, d.self, k, active, nactive);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[5], st);
@@ -724,12 +772,77 @@ void launch_tick(const Dev& d, uint32_t k, void* stream, const TickEvents* prof)
   hipLaunchKernelGGL(k_gossip_free, dim3(1024), dim3(256), 0, st, d, active, nactive);
 }
 
+// ---- sharded tick (W > 1): the same kernel sequence as launch_tick, cut at the two exchange points ----
+static void launch_receipt_routing(const Dev& d, hipStream_t st) {
+  hipLaunchKernelGGL(k_count_rc, dim3(256), dim3(256), 0, st, d.rc_raw, d.rc_n, d.RCAP, d.rc_cnt);
+  uint32_t nb = cdiv(d.N, 1024);
+  hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(256), 0, st, d.rc_cnt, d.rc_off, d.scan_part, d.N);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, st, d.scan_part, nb);
+  hipLaunchKernelGGL(k_scan_add, dim3(cdiv(d.N, 256)), dim3(256), 0, st, d.rc_off, d.scan_part, d.N);
+  hipLaunchKernelGGL(k_scatter_rc, dim3(256), dim3(256), 0, st, d, d.rc_raw, d.rc_n, d.RCAP, d.rc_off, d.rc_fill,
+                     d.rc_slot, d.rc_key);
+  hipLaunchKernelGGL(k_seg_sort, dim3(1024), dim3(256), 0, st, d.rc_key, d.rc_slot, d.rc_off, d.rc_cnt, d.N, d.err,
+                     d.rc_n);
+}
+
+void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
+  hipStream_t st = (hipStream_t)stream;
+  uint32_t b = k & 1, pb = (k - 1) & 1;
+  hipMemsetAsync(d.nmsg + b, 0, sizeof(uint32_t), st);
+  hipMemsetAsync(d.arena_used + b, 0, sizeof(uint32_t), st);
+  hipMemsetAsync(d.pool_used, 0, sizeof(uint32_t), st);
+  hipMemsetAsync(d.xn, 0, 8 * sizeof(uint32_t), st);
+  hipMemsetAsync(d.rq_n, 0, d.W * sizeof(uint32_t), st);
+  hipMemsetAsync(d.xa_scnt, 0, d.W * sizeof(unsigned long long), st);
+  if (k > 0) {
+    hipLaunchKernelGGL(k_sort_msgs, dim3(1), dim3(1024), 0, st, d.msgs[pb], d.nmsg + pb, d.MSGCAP, d.m_key, d.m_idx, d.err);
+    hipLaunchKernelGGL(k_msg_heads, dim3(32), dim3(256), 0, st, d.m_key, d.nmsg + pb, d.MSGCAP, d.m_head);
+    if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
+    hipLaunchKernelGGL(k_sync_diff, dim3(2048), dim3(256), 0, st, d, pb);
+    if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
+  }
+  if (prof) hipEventRecord((hipEvent_t)prof->ev[2], st);
+  hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k);
+  if (prof) hipEventRecord((hipEvent_t)prof->ev[3], st);
+  hipLaunchKernelGGL(k_sync_route, dim3(cdiv(d.MSGCAP, 256)), dim3(256), 0, st, d, b);
+  hipLaunchKernelGGL(k_sync_dirty, dim3(512, d.W), dim3(256), 0, st, d, b);
+  hipLaunchKernelGGL(k_pack_a, dim3(d.W), dim3(256), 0, st, d, b);
+  hipLaunchKernelGGL(k_pack_a_chunks, dim3(512, d.W), dim3(256), 0, st, d, b);
+}
+
+void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
+  hipStream_t st = (hipStream_t)stream;
+  uint32_t b = k & 1;
+  hipLaunchKernelGGL(k_unpack_a, dim3(64, d.W), dim3(256), 0, st, d, k);
+  hipLaunchKernelGGL(k_msgs_commit, dim3(64), dim3(256), 0, st, d, b);
+  hipMemsetAsync(d.nactive, 0, sizeof(uint32_t), st);
+  hipMemsetAsync(d.deliv_n, 0, sizeof(uint32_t), st);
+  hipMemsetAsync(d.rc_n, 0, sizeof(uint32_t), st);
+  hipMemsetAsync(d.xb_scnt, 0, d.W * sizeof(unsigned long long), st);
+  hipLaunchKernelGGL(k_gossip_active, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, st, d, d.active, d.nactive);
+  hipLaunchKernelGGL(k_gossip_contacts, dim3(cdiv((uint64_t)d.NL * d.F, 256)), dim3(256), 0, st, d, k);
+  if (prof) hipEventRecord((hipEvent_t)prof->ev[4], st);
+  hipLaunchKernelGGL(k_gossip_send, dim3(1024), dim3(256), 0, st, d.self, k, d.active, d.nactive);
+  if (prof) hipEventRecord((hipEvent_t)prof->ev[5], st);
+  hipLaunchKernelGGL(k_pack_b, dim3(64, d.W), dim3(256), 0, st, d);
+}
+
+void launch_tick_c(const Dev& d, uint32_t k, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_unpack_b_sweeps, dim3(64, d.W), dim3(256), 0, st, d);
+  hipLaunchKernelGGL(k_unpack_b_deliv, dim3(64, d.W), dim3(256), 0, st, d);
+  hipLaunchKernelGGL(k_gossip_apply, dim3(1024), dim3(256), 0, st, d, k);
+  launch_receipt_routing(d, st);
+  hipLaunchKernelGGL(k_gossip_free, dim3(1024), dim3(256), 0, st, d, d.active, d.nactive);
+  hipLaunchKernelGGL(k_round_reset, dim3(16, d.W), dim3(256), 0, st, d);
+}
+
 void launch_kill(const Dev& d, uint32_t member, void* stream) {
   hipLaunchKernelGGL(k_kill, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, (hipStream_t)stream, d, member);
 }
 
 void launch_hash(const Dev& d, uint64_t* out, uint32_t now, void* stream) {
-  hipLaunchKernelGGL(k_hash, dim3(d.N), dim3(256), 0, (hipStream_t)stream, d, out, now);
+  hipLaunchKernelGGL(k_hash, dim3(d.NL), dim3(256), 0, (hipStream_t)stream, d, out, now);
 }
 
 }  // namespace swim

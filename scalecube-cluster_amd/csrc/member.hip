@@ -173,6 +173,23 @@ __device__ __forceinline__ void spread(ML& L, uint32_t subj, uint32_t st, uint32
   d.S[(size_t)g * L.N + L.m] = (L.k + 1u) & S_TICK_MASK;
   L.held++;
   L.c[C_GCREATED]++;
+  if (d.W > 1) {  // replicated on the other shards from exchange A
+    uint32_t i = atomicAdd(&d.xn[0], 1u);
+    if (i >= d.NSCAP) {
+      set_err(d, E_XCAP);
+      return;
+    }
+    uint32_t* r = d.ns_rec + (size_t)i * NSW;
+    uint64_t key = d.slot_key[g];
+    r[0] = g;
+    r[1] = (uint32_t)gid;
+    r[2] = (uint32_t)(gid >> 32);
+    r[3] = subj;
+    r[4] = L.k;
+    r[5] = (uint32_t)key;
+    r[6] = (uint32_t)(key >> 32);
+    r[7] = L.m;
+  }
 }
 
 __device__ __forceinline__ uint32_t* grp(ML& L, int g) { return L.groups + (size_t)g * GREC; }
@@ -448,6 +465,19 @@ __device__ __forceinline__ void do_spread_gossip(ML& L) {
   d.log_cnt[lo] = cnt;
   for (uint32_t i = 0; i < cnt; ++i) d.log_tg[lo * F + i] = T[i];
   d.log_pos[L.m]++;
+  if (d.W > 1) {  // the round is replayed into the other shards' replicated logs from exchange A
+    uint32_t i = atomicAdd(&d.xn[1], 1u);
+    if (i >= d.RRCAP) {
+      set_err(d, E_XCAP);
+      return;
+    }
+    uint32_t* r = d.rr_rec + (size_t)i * RRW;
+    r[0] = L.m;
+    r[1] = cnt;
+    r[2] = sp;
+    r[3] = period;
+    for (uint32_t j = 0; j < cnt; ++j) r[4 + j] = T[j];
+  }
 }
 
 __device__ __forceinline__ bool is_seed(const Dev& d, uint32_t m, uint32_t s) {
@@ -567,13 +597,14 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   L.remoteIdx = d.remoteIdx[m];
   for (int i = 0; i < 8; ++i) L.sel[i] = d.sel[(size_t)m * 8 + i];
   L.evHash = d.evHash[m];
-  L.row = d.row + (size_t)m * d.NS;
-  L.fdl = d.fdl + (size_t)m * d.LCAP;
-  L.gl = d.gl + (size_t)m * d.LCAP;
-  L.subs = d.subs + (size_t)m * SUBCAP * 4;
-  L.paths = d.paths + (size_t)m * PATHCAP * 5;
-  L.fetch = d.fetch + (size_t)m * d.FCAP * FREC;
-  L.groups = d.groups + (size_t)m * d.GRCAP * GREC;
+  const size_t li = lidx(d, m);  // per-observer arrays hold only this shard's rows
+  L.row = d.row + li * d.NS;
+  L.fdl = d.fdl + li * d.LCAP;
+  L.gl = d.gl + li * d.LCAP;
+  L.subs = d.subs + li * SUBCAP * 4;
+  L.paths = d.paths + li * PATHCAP * 5;
+  L.fetch = d.fetch + li * d.FCAP * FREC;
+  L.groups = d.groups + li * d.GRCAP * GREC;
   for (int i = 0; i < 8; ++i) L.c[i] = 0;
   L.npend = 0;
   L.tround = 0;
@@ -938,9 +969,9 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
 // Counters are summed across the wave first: 10^4 pingers per tick adding to one word would serialise on that address.
 __global__ void __launch_bounds__(256) k_member_tick(const Dev* __restrict__ dp, uint32_t k) {
   const Dev& d = *dp;  // global, not kernarg: taking its address must not copy ~1 KB into per-lane scratch
-  uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t m = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (m < d.N) member_tick_body(d, m, k, cnt);
+  if (m < d.hi) member_tick_body(d, m, k, cnt);
   const uint32_t lane = threadIdx.x & 63;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {

@@ -1,0 +1,291 @@
+// shard.hip — row-sharded observers: packing and unpacking of the two per-tick exchanges.
+//
+// Each shard owns the observers [lo, hi) and runs their protocol control (k_member_tick) and their SYNC merges.
+// The gossip plane stays replicated: every shard keeps the whole slot table, S, the round logs and the
+// incarnation history, and applies the union of every shard's gossip records, so the data-plane kernels read
+// any member's gossip state locally.
+//
+//   exchange A (after k_member_tick): gossips created this tick, gossip rounds this tick (targets, spread, period),
+//     and the SYNC / SYNC_ACK messages addressed to the peer's observers. A SYNC payload (the sender's row at send
+//     time, MembershipProtocolImpl.prepareSyncDataMsg :446-454) ships as a 2048-record chunk mask against the
+//     replicated baseline row plus the chunks that differ, so a converged row costs a few bytes on xGMI.
+//   exchange B (after k_gossip_send): first receipts (slot, target) and sweeps (slot, member) of this shard's senders.
+//
+// Peer regions have a fixed capacity; a region that would overflow raises E_XCAP instead of being truncated.
+// Region A: u32 hdr[8] = {nslot, nround, nsync, nchunk, data_off, 0, 0, 0}; slot records; round records;
+//           sync entries {SyncMsg, u32 chunk base, u32 pad, u64 mask[MW]}; chunk data at data_off (256-B aligned).
+// Region B: u32 hdr[4] = {ndeliv, nsweep, 0, 0}; u64 deliveries; u64 sweeps.
+#include "dev_util.h"
+
+namespace swim {
+
+__device__ __forceinline__ uint64_t sync_entry_bytes(const Dev& d) { return sizeof(SyncMsg) + 8 + 8ull * d.MW; }
+
+__device__ __forceinline__ const uint64_t* payload_row(const Dev& d, const SyncMsg& mm, uint32_t b) {
+  return mm.payload == NEVER ? d.row + lidx(d, mm.src) * d.NS : d.arena[b] + (size_t)mm.payload * d.NS;
+}
+
+// this tick's sends: local destinations go straight to the next tick's inbound list, the rest are queued per shard
+__global__ void k_sync_route(Dev d, uint32_t b) {
+  uint32_t n = d.nmsg[b] < d.MSGCAP ? d.nmsg[b] : d.MSGCAP;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const SyncMsg& mm = d.msgs[b][i];
+    uint32_t q = shard_of(d.N, d.W, mm.dst);
+    if (q == d.rank) {
+      uint32_t j = atomicAdd(&d.xn[4], 1u);
+      if (j < d.MSGCAP) d.mtmp[j] = mm;
+      continue;
+    }
+    uint32_t j = atomicAdd(&d.rq_n[q], 1u);
+    if (j >= d.RQCAP) {
+      atomicOr(d.err, E_XCAP);
+      continue;
+    }
+    size_t e = (size_t)q * d.RQCAP + j;
+    d.rq_list[e] = i;
+    d.rq_cnt[e] = 0;
+    for (uint32_t w = 0; w < d.MW; ++w) d.rq_mask[e * d.MW + w] = 0;
+  }
+}
+
+// chunk masks: which 2048-record chunks of each outbound payload differ (in record key) from the baseline row
+__global__ void __launch_bounds__(256) k_sync_dirty(Dev d, uint32_t b) {
+  const uint32_t q = blockIdx.y;
+  if (q == d.rank) return;
+  const uint32_t nq = min(d.rq_n[q], d.RQCAP);
+  for (uint32_t w = blockIdx.x; w < nq * d.NCHUNK; w += gridDim.x) {
+    const uint32_t j = w / d.NCHUNK, c = w % d.NCHUNK;
+    const size_t e = (size_t)q * d.RQCAP + j;
+    const SyncMsg& mm = d.msgs[b][d.rq_list[e]];
+    const uint32_t s0 = c * CH + threadIdx.x * 8;
+    bool diff = false;
+    if (s0 < d.NS) {
+      const ulonglong2* pv = (const ulonglong2*)(payload_row(d, mm, b) + s0);
+      const ulonglong2* bv = (const ulonglong2*)(d.base_row + s0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        ulonglong2 a = pv[k], z = bv[k];
+        diff |= ((a.x ^ z.x) & KEY_MASK) != 0 || ((a.y ^ z.y) & KEY_MASK) != 0;
+      }
+    }
+    if (__syncthreads_or(diff) && threadIdx.x == 0) {
+      atomicOr((unsigned long long*)&d.rq_mask[e * d.MW + (c >> 6)], 1ull << (c & 63));
+      atomicAdd(&d.rq_cnt[e], 1u);
+    }
+  }
+}
+
+// region layout, records and SYNC headers for peer q (one block per peer)
+__global__ void __launch_bounds__(256) k_pack_a(Dev d, uint32_t b) {
+  const uint32_t q = blockIdx.x;
+  if (q == d.rank) return;
+  __shared__ uint32_t sh[8];
+  uint8_t* R = d.xa_send + (size_t)q * d.XA_PEER;
+  const uint64_t SE = sync_entry_bytes(d);
+  if (threadIdx.x == 0) {
+    uint32_t nslot = min(d.xn[0], d.NSCAP), nround = min(d.xn[1], d.RRCAP), nsync = min(d.rq_n[q], d.RQCAP);
+    uint32_t nchunk = 0;
+    for (uint32_t j = 0; j < nsync; ++j) {
+      size_t e = (size_t)q * d.RQCAP + j;
+      d.rq_base[e] = nchunk;
+      nchunk += d.rq_cnt[e];
+    }
+    uint64_t off_sync = 32 + 4ull * NSW * nslot + 4ull * RRW * nround;
+    uint64_t data_off = (off_sync + SE * nsync + 255) & ~255ull;
+    uint64_t total = data_off + (uint64_t)nchunk * CH * 8;
+    if (total > d.XA_PEER || nchunk > d.CHCAP) {
+      atomicOr(d.err, E_XCAP);
+      nslot = nround = nsync = nchunk = 0;
+      data_off = 256;
+      total = 32;
+    }
+    uint32_t* H = (uint32_t*)R;
+    H[0] = nslot;
+    H[1] = nround;
+    H[2] = nsync;
+    H[3] = nchunk;
+    H[4] = (uint32_t)data_off;
+    H[5] = H[6] = H[7] = 0;
+    d.xa_scnt[q] = total;
+    sh[0] = nslot;
+    sh[1] = nround;
+    sh[2] = nsync;
+  }
+  __syncthreads();
+  const uint32_t nslot = sh[0], nround = sh[1], nsync = sh[2];
+  uint32_t* S = (uint32_t*)(R + 32);
+  for (uint32_t i = threadIdx.x; i < nslot * NSW; i += blockDim.x) S[i] = d.ns_rec[i];
+  uint32_t* RR = S + (size_t)nslot * NSW;
+  for (uint32_t i = threadIdx.x; i < nround * RRW; i += blockDim.x) RR[i] = d.rr_rec[i];
+  uint8_t* E = (uint8_t*)(RR + (size_t)nround * RRW);
+  for (uint32_t j = threadIdx.x; j < nsync; j += blockDim.x) {
+    size_t e = (size_t)q * d.RQCAP + j;
+    uint8_t* p = E + SE * j;
+    *(SyncMsg*)p = d.msgs[b][d.rq_list[e]];
+    ((uint32_t*)(p + sizeof(SyncMsg)))[0] = d.rq_base[e];
+    ((uint32_t*)(p + sizeof(SyncMsg)))[1] = 0;
+    uint64_t* mk = (uint64_t*)(p + sizeof(SyncMsg) + 8);
+    for (uint32_t w = 0; w < d.MW; ++w) mk[w] = d.rq_mask[e * d.MW + w];
+  }
+}
+
+// copy the differing payload chunks into peer q's region (16-B loads and stores, 8 records per lane)
+__global__ void __launch_bounds__(256) k_pack_a_chunks(Dev d, uint32_t b) {
+  const uint32_t q = blockIdx.y;
+  if (q == d.rank) return;
+  uint8_t* R = d.xa_send + (size_t)q * d.XA_PEER;
+  const uint32_t* H = (const uint32_t*)R;
+  const uint32_t nsync = H[2], data_off = H[4];
+  if (H[3] == 0) return;
+  uint64_t* dst0 = (uint64_t*)(R + data_off);
+  for (uint32_t w = blockIdx.x; w < nsync * d.NCHUNK; w += gridDim.x) {
+    const uint32_t j = w / d.NCHUNK, c = w % d.NCHUNK;
+    const size_t e = (size_t)q * d.RQCAP + j;
+    const uint64_t* mk = d.rq_mask + e * d.MW;
+    if (!((mk[c >> 6] >> (c & 63)) & 1ull)) continue;
+    uint32_t rank = __popcll(mk[c >> 6] & ((1ull << (c & 63)) - 1ull));
+    for (uint32_t x = 0; x < (c >> 6); ++x) rank += __popcll(mk[x]);
+    const uint32_t s0 = c * CH + threadIdx.x * 8;
+    if (s0 >= d.NS) continue;
+    const SyncMsg& mm = d.msgs[b][d.rq_list[e]];
+    const ulonglong2* src = (const ulonglong2*)(payload_row(d, mm, b) + s0);
+    ulonglong2* dst = (ulonglong2*)(dst0 + (size_t)(d.rq_base[e] + rank) * CH + threadIdx.x * 8);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dst[k] = src[k];
+  }
+}
+
+// replay peer p's gossip creations and rounds into the replicated gossip plane; queue its SYNC messages
+__global__ void __launch_bounds__(256) k_unpack_a(Dev d, uint32_t k) {
+  const uint32_t p = blockIdx.y;
+  if (p == d.rank || d.xa_rcnt[p] < 32) return;
+  const uint8_t* R = d.xa_recv + (size_t)p * d.XA_PEER;
+  const uint32_t* H = (const uint32_t*)R;
+  const uint32_t nslot = H[0], nround = H[1], nsync = H[2], data_off = H[4];
+  const uint32_t* S = (const uint32_t*)(R + 32);
+  const uint32_t* RR = S + (size_t)nslot * NSW;
+  const uint8_t* E = (const uint8_t*)(RR + (size_t)nround * RRW);
+  const uint64_t SE = sync_entry_bytes(d);
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+  for (uint32_t i = tid; i < nslot; i += nth) {  // spread -> createAndPutGossip at the origin (member.hip)
+    const uint32_t* r = S + (size_t)i * NSW;
+    uint32_t g = r[0], origin = r[7];
+    d.slot_gid[g] = (uint64_t)r[1] | ((uint64_t)r[2] << 32);
+    d.slot_subj[g] = r[3];
+    d.slot_ctick[g] = r[4];
+    d.slot_key[g] = (uint64_t)r[5] | ((uint64_t)r[6] << 32);
+    d.slot_holders[g] = 1;
+    d.slot_used[g] = 1;
+    d.S[(size_t)g * d.N + origin] = (r[4] + 1u) & S_TICK_MASK;
+    atomicAdd(&d.held[origin], 1u);
+  }
+  for (uint32_t i = tid; i < nround; i += nth) {  // do_spread_gossip at the sender (member.hip)
+    const uint32_t* r = RR + (size_t)i * RRW;
+    uint32_t m = r[0], cnt = r[1];
+    d.tround[m] = 1;
+    d.tcnt[m] = cnt;
+    d.tspread[m] = r[2];
+    d.tperiod[m] = r[3];
+    uint32_t pos = d.log_pos[m] % d.LOGW;
+    size_t lo = (size_t)m * d.LOGW + pos;
+    d.log_tick[lo] = k;
+    d.log_spread[lo] = r[2];
+    d.log_cnt[lo] = cnt;
+    for (uint32_t j = 0; j < cnt; ++j) {
+      d.T[(size_t)m * d.F + j] = r[4 + j];
+      d.log_tg[lo * d.F + j] = r[4 + j];
+    }
+    d.log_pos[m]++;
+  }
+  for (uint32_t i = tid; i < nsync; i += nth) {
+    const uint8_t* e = E + SE * i;
+    SyncMsg mm = *(const SyncMsg*)e;
+    uint32_t base = ((const uint32_t*)(e + sizeof(SyncMsg)))[0];
+    const uint64_t* mk = (const uint64_t*)(e + sizeof(SyncMsg) + 8);
+    uint32_t ri = atomicAdd(&d.xn[5], 1u);
+    uint32_t j = atomicAdd(&d.xn[4], 1u);
+    if (ri >= d.RXCAP || j >= d.MSGCAP) {
+      atomicOr(d.err, E_XCAP);
+      continue;
+    }
+    for (uint32_t w = 0; w < d.MW; ++w) d.rx_mask[(size_t)ri * d.MW + w] = mk[w];
+    d.rx_off[ri] = (uint64_t)p * d.XA_PEER + data_off + (uint64_t)base * CH * 8;
+    mm.payload = PAY_RX | ri;
+    mm.ncand = 0;
+    d.mtmp[j] = mm;
+  }
+}
+
+// the assembled inbound list becomes msgs[b], which the next tick sorts and merges
+__global__ void k_msgs_commit(Dev d, uint32_t b) {
+  uint32_t n = min(d.xn[4], d.MSGCAP);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) d.msgs[b][i] = d.mtmp[i];
+  if (blockIdx.x == 0 && threadIdx.x == 0) d.nmsg[b] = n;
+}
+
+__global__ void __launch_bounds__(256) k_pack_b(Dev d) {
+  const uint32_t q = blockIdx.y;
+  if (q == d.rank) return;
+  uint8_t* R = d.xb_send + (size_t)q * d.XB_PEER;
+  uint32_t nd = min(*d.deliv_n, d.DCAP), ns = min(d.xn[2], d.SWCAP);
+  if (16 + 8ull * (nd + ns) > d.XB_PEER) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(d.err, E_XCAP);
+    nd = ns = 0;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    uint32_t* H = (uint32_t*)R;
+    H[0] = nd;
+    H[1] = ns;
+    H[2] = H[3] = 0;
+    d.xb_scnt[q] = 16 + 8ull * (nd + ns);
+  }
+  uint64_t* V = (uint64_t*)(R + 16);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nd + ns; i += gridDim.x * blockDim.x)
+    V[i] = i < nd ? d.deliv[i] : d.sw_rec[i - nd];
+}
+
+// peers' sweeps first (sweepGossips :283-308), so that a delivery to a member that swept g this tick re-creates it
+__global__ void k_unpack_b_sweeps(Dev d) {
+  const uint32_t p = blockIdx.y;
+  if (p == d.rank || d.xb_rcnt[p] < 16) return;
+  const uint8_t* R = d.xb_recv + (size_t)p * d.XB_PEER;
+  const uint32_t nd = ((const uint32_t*)R)[0], ns = ((const uint32_t*)R)[1];
+  const uint64_t* V = (const uint64_t*)(R + 16) + nd;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += gridDim.x * blockDim.x) {
+    uint32_t g = (uint32_t)(V[i] >> 32), m = (uint32_t)V[i];
+    atomicOr(&d.S[(size_t)g * d.N + m], S_SWEPT);
+    atomicSub(&d.held[m], 1u);
+    atomicSub(&d.slot_holders[g], 1);
+  }
+}
+
+// peers' first receipts join this shard's delivery list, deduplicated by the PENDING bit like local ones
+__global__ void k_unpack_b_deliv(Dev d) {
+  const uint32_t p = blockIdx.y;
+  if (p == d.rank || d.xb_rcnt[p] < 16) return;
+  const uint8_t* R = d.xb_recv + (size_t)p * d.XB_PEER;
+  const uint32_t nd = ((const uint32_t*)R)[0];
+  const uint64_t* V = (const uint64_t*)(R + 16);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nd; i += gridDim.x * blockDim.x) {
+    uint64_t v = V[i];
+    uint32_t old = atomicOr(&d.S[(size_t)(v >> 32) * d.N + (uint32_t)v], S_PENDING);
+    if (old & S_PENDING) continue;
+    uint32_t di = atomicAdd(d.deliv_n, 1u);
+    if (di < d.DCAP)
+      d.deliv[di] = v;
+    else
+      atomicOr(d.err, E_DELIV);
+  }
+}
+
+// the peers' members are out of their gossip round again
+__global__ void k_round_reset(Dev d) {
+  const uint32_t p = blockIdx.y;
+  if (p == d.rank || d.xa_rcnt[p] < 32) return;
+  const uint8_t* R = d.xa_recv + (size_t)p * d.XA_PEER;
+  const uint32_t* H = (const uint32_t*)R;
+  const uint32_t* RR = (const uint32_t*)(R + 32) + (size_t)H[0] * NSW;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < H[1]; i += gridDim.x * blockDim.x) d.tround[RR[(size_t)i * RRW]] = 0;
+}
+
+}  // namespace swim

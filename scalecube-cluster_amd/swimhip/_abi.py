@@ -119,6 +119,42 @@ SIGNATURES = {
 }
 
 
+# include/swimhip_shard.h (row-sharded multi-GPU handles; exported by libswimhip only, not by the oracle)
+TRANSPORT_RCCL = 1
+TRANSPORT_HOST = 2
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_void_p, C.c_uint64,
+                          C.POINTER(C.c_uint64))
+
+
+class SwimShardSpec(C.Structure):
+    _fields_ = [
+        ("rank", C.c_uint32),
+        ("world", C.c_uint32),
+        ("transport", C.c_uint32),
+        ("chunk_cap", C.c_uint32),
+        ("rccl_id", C.c_uint8 * 128),
+        ("exchange", EXCHANGE_FN),
+        ("ctx", C.c_void_p),
+        ("reserved", C.c_uint32 * 8),
+    ]
+
+
+SHARD_SIGNATURES = {
+    "swim_rccl_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
+    "swim_create_sharded": (C.c_int, [C.POINTER(SwimConfig), C.POINTER(SwimShardSpec), C.POINTER(_H)]),
+    "swim_shard_range": (C.c_int, [_H, _U32P, _U32P]),
+}
+
+
+def bind_shard(lib):
+    """Attach the sharding entry points (engine library only)."""
+    for name, (res, args) in SHARD_SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
 def bind(lib):
     """Attach restype/argtypes for every ABI symbol; raises AttributeError if one is missing."""
     for name, (res, args) in SIGNATURES.items():

@@ -1,0 +1,102 @@
+"""Row-sharded engine (include/swimhip_shard.h) against the CPU oracle: the same scenarios as test_gpu_parity.py,
+with the observers split over 2 or 3 shards on one GPU that exchange gossip records and SYNC payloads through the
+host transport every tick. Bit-exact: the summed per-observer hashes, the summed op counters and the merged
+MembershipEvent streams must equal the unsharded oracle's."""
+import numpy as np
+import pytest
+
+from swimhip import ClusterConfig, SimConfig, _abi
+from swimhip.cluster import SimulatedCluster
+from swimhip.shard import ThreadShardGroup, shard_range
+
+from parity_util import run_lockstep
+
+pytestmark = pytest.mark.gpu
+
+
+def group(oracle, engine, cfg, world, **kw):
+    return SimulatedCluster(oracle, cfg), ThreadShardGroup(engine, cfg, world, **kw)
+
+
+def test_shard_ranges_cover():
+    for n, w in [(64, 2), (300, 3), (100_000, 8), (50, 7)]:
+        r = [shard_range(n, w, i) for i in range(w)]
+        assert r[0][0] == 0 and r[-1][1] == n and all(r[i][1] == r[i + 1][0] for i in range(w - 1))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_c1_cold_join_kill(oracle, engine, world):
+    cfg = SimConfig(n_members=64, cluster=ClusterConfig(seedMembers=[0]), init_mode=_abi.INIT_COLD_JOIN,
+                    record_events=True)
+    o, e = group(oracle, engine, cfg, world)
+    run_lockstep(o, e, 100, 10, f"C1 join W={world}")
+    o.kill(63)
+    e.kill(63)
+    ev = run_lockstep(o, e, 400, 50, f"C1 kill W={world}")
+    assert sorted(x.observer for x in ev if x.isRemoved() and x.member == 63) == list(range(63))
+    e.close()
+
+
+def test_sharded_loss(oracle, engine):
+    cfg = SimConfig(n_members=300, record_events=True)
+    o, e = group(oracle, engine, cfg, 2)
+    o.set_default_loss(5)
+    e.set_default_loss(5)
+    ev = run_lockstep(o, e, 200, 20, "loss5 W=2")
+    assert any(x.isUpdated() for x in ev)
+    e.close()
+
+
+def test_sharded_partition_heal(oracle, engine):
+    n = 48
+    cfg = SimConfig(n_members=n, cluster=ClusterConfig(seedMembers=[0, n - 1]), record_events=True)
+    o, e = group(oracle, engine, cfg, 2)
+    g = np.array([0] * (n // 2) + [1] * (n // 2), dtype=np.uint32)
+    o.partition(g)
+    e.partition(g)
+    run_lockstep(o, e, 350, 50, "partitioned W=2")
+    o.unblock_all()
+    e.unblock_all()
+    run_lockstep(o, e, 650, 50, "healed W=2")
+    e.close()
+
+
+def test_sharded_sync_multichunk(oracle, engine):
+    """5000 members: 3 payload chunks per row, so clean and dirty chunks of one SYNC payload mix after the kill."""
+    cfg = SimConfig(n_members=5000, record_events=True)
+    o, e = group(oracle, engine, cfg, 2)
+    run_lockstep(o, e, 100, 50, "multichunk warm", events=False)
+    for c in (o, e):
+        c.kill(4100)
+        c.update_incarnation(10)
+    run_lockstep(o, e, 300, 100, "multichunk W=2")
+    e.close()
+
+
+@pytest.mark.parametrize("loss", [0, 25])
+def test_sharded_dissemination(oracle, engine, loss):
+    cfg = SimConfig(n_members=50, record_events=True)
+    o, e = group(oracle, engine, cfg, 3)
+    for c in (o, e):
+        c.set_default_loss(loss)
+        c.step(5)
+        c.update_incarnation(0)
+    run_lockstep(o, e, 120, 8, f"dissemination W=3 loss {loss}")
+    for c in (o, e):
+        c.update_incarnation(7)
+        c.update_incarnation(40)
+    run_lockstep(o, e, 200, 40, f"second wave W=3 loss {loss}")
+    e.close()
+
+
+def test_sharded_kill_many_with_loss(oracle, engine):
+    cfg = SimConfig(n_members=120, record_events=True)
+    o, e = group(oracle, engine, cfg, 2)
+    for c in (o, e):
+        c.set_default_loss(10)
+    run_lockstep(o, e, 50, 25, "warm W=2")
+    for victim in (3, 50, 51, 119):
+        o.kill(victim)
+        e.kill(victim)
+    run_lockstep(o, e, 500, 100, "after kills W=2")
+    e.close()
