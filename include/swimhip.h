@@ -116,7 +116,8 @@ typedef struct swim_counters {
   uint64_t member_ns;     /* k_member_tick: per-member protocol control */
   uint64_t gossip_ns;     /* k_gossip_send: gossip data plane */
   uint64_t diff_launches;
-  uint64_t reserved[2];
+  uint64_t exchange_ns; /* sharded handles: host time spent in the per-tick shard exchanges */
+  uint64_t reserved[1];
 } swim_counters;
 
 typedef struct swim_handle swim_handle;

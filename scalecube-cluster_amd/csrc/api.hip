@@ -643,6 +643,7 @@ int swim_counters_get(swim_handle* h, swim_counters* out) {
   out->member_ns = (uint64_t)(h->prof_ms[1] * 1e6);
   out->gossip_ns = (uint64_t)(h->prof_ms[2] * 1e6);
   out->diff_launches = h->prof_diff_launches;
+  out->exchange_ns = (uint64_t)(h->xchg_ms * 1e6);
   return SWIM_OK;
 }
 

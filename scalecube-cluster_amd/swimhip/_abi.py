@@ -83,7 +83,8 @@ class SwimCounters(C.Structure):
         ("member_ns", C.c_uint64),
         ("gossip_ns", C.c_uint64),
         ("diff_launches", C.c_uint64),
-        ("reserved", C.c_uint64 * 2),
+        ("exchange_ns", C.c_uint64),
+        ("reserved", C.c_uint64 * 1),
     ]
 
     def as_dict(self):

@@ -11,15 +11,20 @@ import pytest
 from swimhip import _abi, LIB_PATH
 
 HEADER = Path(__file__).resolve().parent.parent / "include" / "swimhip.h"
+SHARD_HEADER = Path(__file__).resolve().parent.parent / "include" / "swimhip_shard.h"
 
 
-def declared_symbols():
-    text = HEADER.read_text()
-    return sorted(set(re.findall(r"\b(swim_[a-z0-9_]+)\s*\(", text)))
+def declared_symbols(header=HEADER):
+    text = header.read_text()
+    return sorted(set(re.findall(r"\b(swim_[a-z0-9_]+)\s*\(", text)) - {"swim_exchange_fn"})
 
 
 def test_header_and_ctypes_agree():
     assert set(declared_symbols()) == set(_abi.SIGNATURES), "ctypes mirror out of sync with include/swimhip.h"
+
+
+def test_shard_header_and_ctypes_agree():
+    assert set(declared_symbols(SHARD_HEADER)) == set(_abi.SHARD_SIGNATURES)
 
 
 def test_oracle_exports_every_symbol(oracle):
@@ -31,7 +36,7 @@ def test_engine_library_exports_every_symbol():
     if not LIB_PATH.exists():
         pytest.skip("libswimhip.so not built (run __graft_entry__.build())")
     lib = _abi.load(LIB_PATH)  # loading initialises no device
-    for name in declared_symbols():
+    for name in declared_symbols() + declared_symbols(SHARD_HEADER):
         assert hasattr(lib, name), name
     assert lib.swim_abi_version() == 1
     # pure helpers run on the host side of the library
