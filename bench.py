@@ -47,6 +47,9 @@ def parse():
     p.add_argument("--cpu-members", type=int, default=10_000)
     p.add_argument("--cpu-periods", type=int, default=10)
     p.add_argument("--transport", choices=["rccl", "host"], default="rccl", help="N>1 shard exchange")
+    p.add_argument("--rehearse-one-gpu", action="store_true",
+                   help="N>1 on a single GPU (functional rehearsal only): every rank uses device 0 and gets its own "
+                        "NCCL_HOSTID, so RCCL connects the ranks through its socket transport")
     return p.parse_args()
 
 
@@ -89,6 +92,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.rehearse_one_gpu:
+        local = 0
+        os.environ["NCCL_HOSTID"] = f"swim-rehearsal-{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
     import torch
 
     dist = None

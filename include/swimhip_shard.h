@@ -30,9 +30,11 @@ extern "C" {
 #define SWIM_TRANSPORT_HOST 2u
 
 /* Host exchange: an all-to-all of one byte block per peer. `send` holds the blocks for ranks 0..world-1 back to
- * back (send_bytes[q] bytes for rank q; the caller's own block is empty). The callee writes the blocks received
- * from ranks 0..world-1 back to back into `recv` (at most recv_cap bytes) and their sizes into recv_bytes.
- * Returns 0 on success. Called from inside swim_step on the stepping thread. */
+ * back; send_bytes[q] describes the block for rank q: its size in bytes in bits 0..47 and flags in bits 48..63
+ * (the caller's own block is empty). The callee writes the blocks received from ranks 0..world-1 back to back
+ * into `recv` (at most recv_cap bytes) and sets recv_bytes[p] to the word rank p sent for it (size and flags
+ * unchanged). Returns 0 on success. Called from inside swim_step on the stepping thread. */
+#define SWIM_XCOUNT_MASK ((1ull << 48) - 1)
 typedef int (*swim_exchange_fn)(void* ctx, const void* send, const uint64_t* send_bytes, void* recv, uint64_t recv_cap,
                                 uint64_t* recv_bytes);
 

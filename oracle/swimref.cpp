@@ -1031,6 +1031,19 @@ __attribute__((visibility("default"))) int swim_state_hash(swim_handle* h, uint6
   return SWIM_OK;
 }
 
+// debugging aid (not in the ABI header): the scalar fields folded into the "misc" state-hash word
+__attribute__((visibility("default"))) int swimdbg_scalars(swim_handle* h, uint32_t m, uint64_t* out) {
+  if (!h || m >= h->sim.N) return SWIM_EINVAL;
+  const Member& mb = h->sim.members[m];
+  out[0] = mb.cidCnt;
+  out[1] = mb.syncSeq;
+  out[2] = mb.gCounter;
+  out[3] = (uint64_t)mb.nextSync;
+  out[4] = mb.fdPeriod;
+  out[5] = mb.gPeriod;
+  return SWIM_OK;
+}
+
 __attribute__((visibility("default"))) int swim_read_lists(swim_handle* h, uint32_t obs, uint32_t* fd, uint32_t* fd_len,
                                                            uint32_t* gl, uint32_t* g_len, size_t cap, int32_t* cursors) {
   if (!h || obs >= h->sim.N) return SWIM_EINVAL;

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -40,6 +41,11 @@ struct swim_handle {
   unsigned long long* hcnt = nullptr;  // pinned [2W]: send then receive byte counts of the current exchange
   std::vector<uint8_t> hsend, hrecv;  // SWIM_TRANSPORT_HOST staging
   double xchg_ms = 0;                 // host time spent in the exchanges
+  bool xflag = false;                 // last exchange: some shard has a gossip slot in use
+  volatile uint32_t* hflag = nullptr; // host-mapped flag word written by k_tick_flag (W == 1)
+  hipEvent_t ev_member = nullptr;
+  bool no_skip = getenv("SWIM_NO_GOSSIP_SKIP") != nullptr;  // debugging aid: always run the gossip data plane
+  bool no_pipe = getenv("SWIM_NO_PIPELINE") != nullptr;    // debugging aid: no early SYNC diff of the next tick
 };
 
 namespace {
@@ -64,6 +70,9 @@ int dalloc(swim_handle* h, T** p, size_t count) {
   }
   h->allocs.push_back(q);
   h->bytes += bytes;
+  // debugging aids: poison fresh allocations (all, or only allocation #SWIM_POISON_ONLY) to catch never-written state
+  const char* po = getenv("SWIM_POISON_ONLY");
+  if (getenv("SWIM_POISON") || (po && atoi(po) == (int)h->allocs.size() - 1)) hipMemsetAsync(q, 0xA5, bytes, h->stream);
   *p = (T*)q;
   return SWIM_OK;
 }
@@ -187,7 +196,7 @@ int build(swim_handle* h) {
   A(d.rc_slot, d.RCAP) A(d.rc_key, d.RCAP) A(d.active, d.SLOTS) A(d.nactive, 1) A(d.hist, (uint64_t)d.HCAP * 6)
   A(d.msgs[0], d.MSGCAP) A(d.msgs[1], d.MSGCAP) A(d.nmsg, 2) A(d.arena[0], (uint64_t)d.ARENA_ROWS * d.NS)
   A(d.arena[1], (uint64_t)d.ARENA_ROWS * d.NS) A(d.arena_used, 2)
-  A(d.m_idx, d.MSGCAP) A(d.m_head, N) A(d.next_evt, N) A(d.pending_inc, N) A(d.m_key, d.MSGCAP) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
+  A(d.m_next, d.MSGCAP) A(d.m_head, N) A(d.next_evt, N) A(d.pending_inc, N) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
   A(d.pool, d.POOLCAP) A(d.pool_used, 1)
   A(d.ev, (uint64_t)d.EVCAP * 8) A(d.ev_n, 1) A(d.ctr, C_NCTR) A(d.err, 8)
   if (d.W > 1) {
@@ -208,8 +217,8 @@ int build(swim_handle* h) {
     A(d.mtmp, d.MSGCAP) A(d.rx_mask, (uint64_t)d.RXCAP * d.MW) A(d.rx_off, d.RXCAP)
     A(d.xa_send, d.W * d.XA_PEER) A(d.xa_recv, d.W * d.XA_PEER) A(d.xb_send, d.W * d.XB_PEER)
     A(d.xb_recv, d.W * d.XB_PEER) A(d.xa_scnt, d.W) A(d.xa_rcnt, d.W) A(d.xb_scnt, d.W) A(d.xb_rcnt, d.W)
-    HIPCK(hipMemset(d.xa_rcnt, 0, 8ull * d.W));
-    HIPCK(hipMemset(d.xb_rcnt, 0, 8ull * d.W));
+    HIPCK(hipMemsetAsync(d.xa_rcnt, 0, 8ull * d.W, h->stream));
+    HIPCK(hipMemsetAsync(d.xb_rcnt, 0, 8ull * d.W, h->stream));
     HIPCK(hipHostMalloc((void**)&h->hcnt, 16ull * d.W, hipHostMallocDefault));
     if (h->spec.transport == SWIM_TRANSPORT_HOST) {
       h->hsend.resize(d.W * std::max(d.XA_PEER, d.XB_PEER));
@@ -217,26 +226,45 @@ int build(swim_handle* h) {
     }
   }
 #undef A
-  HIPCK(hipMemset(d.S, 0, (size_t)d.SLOTS * N * 4));
-  HIPCK(hipMemset(d.ctr, 0, C_NCTR * 8));
-  HIPCK(hipMemset(d.hist, 0, (size_t)d.HCAP * 48));
-  HIPCK(hipMemset(d.err, 0, 32));
-  HIPCK(hipMemset(d.ev_n, 0, 4));
-  HIPCK(hipMemset(d.nmsg, 0, 8));
-  HIPCK(hipMemset(d.arena_used, 0, 8));
-  HIPCK(hipMemset(d.tcnt, 0, N * 4));
-  HIPCK(hipMemset(d.subs, 0, NL * SUBCAP * 16));
+  HIPCK(hipMemsetAsync(d.S, 0, (size_t)d.SLOTS * N * 4, h->stream));
+  HIPCK(hipMemsetAsync(d.ctr, 0, C_NCTR * 8, h->stream));
+  HIPCK(hipMemsetAsync(d.hist, 0, (size_t)d.HCAP * 48, h->stream));
+  HIPCK(hipMemsetAsync(d.err, 0, 32, h->stream));
+  HIPCK(hipMemsetAsync(d.ev_n, 0, 4, h->stream));
+  HIPCK(hipMemsetAsync(d.nmsg, 0, 8, h->stream));
+  HIPCK(hipMemsetAsync(d.arena_used, 0, 8, h->stream));
+  HIPCK(hipMemsetAsync(d.tcnt, 0, N * 4, h->stream));
+  HIPCK(hipMemsetAsync(d.pool_used, 0, 4, h->stream));
+  HIPCK(hipMemsetAsync(d.nactive, 0, 4, h->stream));
+  HIPCK(hipMemsetAsync(d.deliv_n, 0, 4, h->stream));
+  HIPCK(hipMemsetAsync(d.rc_n, 0, 4, h->stream));
+  HIPCK(hipMemsetAsync(d.m_head, 0xFF, N * 4, h->stream));
+  if (d.W > 1) {
+    HIPCK(hipMemsetAsync(d.xn, 0, 32, h->stream));
+    HIPCK(hipMemsetAsync(d.rq_n, 0, 4ull * d.W, h->stream));
+    HIPCK(hipMemsetAsync(d.xa_scnt, 0, 8ull * d.W, h->stream));
+    HIPCK(hipMemsetAsync(d.xb_scnt, 0, 8ull * d.W, h->stream));
+  }
+  HIPCK(hipHostMalloc((void**)&h->hflag, 64, hipHostMallocMapped | hipHostMallocCoherent));
+  h->hflag[0] = 0;
+  HIPCK(hipHostGetDevicePointer((void**)&d.hflag, (void*)h->hflag, 0));
+  HIPCK(hipEventCreateWithFlags(&h->ev_member, hipEventDisableTiming));
+  HIPCK(hipMemsetAsync(d.subs, 0, NL * SUBCAP * 16, h->stream));
   int32_t top = (int32_t)d.SPR;
-  HIPCK(hipMemcpy(d.free_top, &top, 4, hipMemcpyHostToDevice));
+  HIPCK(hipMemcpyAsync(d.free_top, &top, 4, hipMemcpyHostToDevice, h->stream));
   std::vector<uint32_t> never(MAX_EPOCHS, NEVER);
-  HIPCK(hipMemcpy(d.ep_from, never.data(), 4 * MAX_EPOCHS, hipMemcpyHostToDevice));
+  HIPCK(hipMemcpyAsync(d.ep_from, never.data(), 4 * MAX_EPOCHS, hipMemcpyHostToDevice, h->stream));
+  HIPCK(hipStreamSynchronize(h->stream));  // `top` and `never` live on this stack frame
   h->group.assign(d.N, 0);
   for (uint32_t e = 0; e < MAX_EPOCHS; ++e) h->ep_from[e] = NEVER;
   h->cur_ep = 0;
+  // every initialisation above is ordered on the engine stream (a non-blocking stream does not wait for the
+  // legacy null stream, so a plain hipMemset could still be running when the first tick starts)
   Dev* dcopy = nullptr;
   if ((rc = dalloc(h, &dcopy, 1)) != 0) return rc;
   d.self = dcopy;
-  HIPCK(hipMemcpy(dcopy, &d, sizeof(Dev), hipMemcpyHostToDevice));
+  HIPCK(hipMemcpyAsync(dcopy, &d, sizeof(Dev), hipMemcpyHostToDevice, h->stream));
+  HIPCK(hipStreamSynchronize(h->stream));
   launch_init(d, h->stream);
   if ((rc = push_epoch(h)) != 0) return rc;
   return check_err(h);
@@ -258,16 +286,19 @@ int exchange(swim_handle* h, uint8_t* send, uint8_t* recv, uint64_t cap, unsigne
     HIPCK(hipMemcpyAsync(hc, scnt, 8ull * W, hipMemcpyDeviceToHost, st));
     HIPCK(hipMemcpyAsync(hc + W, rcnt, 8ull * W, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
+    h->xflag = false;
+    for (uint32_t q = 0; q < 2 * W; ++q) h->xflag |= (hc[q] & XFLAG_GOSSIP) != 0;
     for (uint32_t q = 0; q < W; ++q)
-      if (hc[q] > cap || hc[W + q] > cap) {
+      if ((hc[q] & XCNT_MASK) > cap || (hc[W + q] & XCNT_MASK) > cap) {
         h->err = "exchange block larger than its region";
         return SWIM_ECAPACITY;
       }
     bool ok = ncclGroupStart() == ncclSuccess;
     for (uint32_t q = 0; q < W && ok; ++q) {
       if (q == me) continue;
-      if (hc[q]) ok &= ncclSend(send + (size_t)q * cap, hc[q], ncclUint8, (int)q, h->comm, st) == ncclSuccess;
-      if (hc[W + q]) ok &= ncclRecv(recv + (size_t)q * cap, hc[W + q], ncclUint8, (int)q, h->comm, st) == ncclSuccess;
+      const uint64_t sb = hc[q] & XCNT_MASK, rb = hc[W + q] & XCNT_MASK;
+      if (sb) ok &= ncclSend(send + (size_t)q * cap, sb, ncclUint8, (int)q, h->comm, st) == ncclSuccess;
+      if (rb) ok &= ncclRecv(recv + (size_t)q * cap, rb, ncclUint8, (int)q, h->comm, st) == ncclSuccess;
     }
     ok &= ncclGroupEnd() == ncclSuccess;
     if (!ok) {
@@ -279,12 +310,13 @@ int exchange(swim_handle* h, uint8_t* send, uint8_t* recv, uint64_t cap, unsigne
     HIPCK(hipStreamSynchronize(st));
     uint64_t off = 0;
     for (uint32_t q = 0; q < W; ++q) {
-      if (hc[q] > cap) {
+      const uint64_t sb = hc[q] & XCNT_MASK;
+      if (sb > cap) {
         h->err = "exchange block larger than its region";
         return SWIM_ECAPACITY;
       }
-      if (hc[q]) HIPCK(hipMemcpyAsync(h->hsend.data() + off, send + (size_t)q * cap, hc[q], hipMemcpyDeviceToHost, st));
-      off += hc[q];
+      if (sb) HIPCK(hipMemcpyAsync(h->hsend.data() + off, send + (size_t)q * cap, sb, hipMemcpyDeviceToHost, st));
+      off += sb;
     }
     HIPCK(hipStreamSynchronize(st));
     uint64_t sb[64], rb[64];
@@ -294,14 +326,17 @@ int exchange(swim_handle* h, uint8_t* send, uint8_t* recv, uint64_t cap, unsigne
       return SWIM_EDEVICE;
     }
     off = 0;
+    h->xflag = false;
     for (uint32_t p = 0; p < W; ++p) {
-      if (rb[p] > cap) {
+      const uint64_t n = rb[p] & XCNT_MASK;
+      if (n > cap) {
         h->err = "received exchange block larger than its region";
         return SWIM_ECAPACITY;
       }
-      if (rb[p]) HIPCK(hipMemcpyAsync(recv + (size_t)p * cap, h->hrecv.data() + off, rb[p], hipMemcpyHostToDevice, st));
-      off += rb[p];
+      if (n) HIPCK(hipMemcpyAsync(recv + (size_t)p * cap, h->hrecv.data() + off, n, hipMemcpyHostToDevice, st));
+      off += n;
       hc[W + p] = rb[p];
+      h->xflag |= ((rb[p] | sb[p]) & XFLAG_GOSSIP) != 0;
     }
     HIPCK(hipMemcpyAsync(rcnt, hc + W, 8ull * W, hipMemcpyHostToDevice, st));
     HIPCK(hipStreamSynchronize(st));
@@ -420,6 +455,8 @@ int swim_destroy(swim_handle* h) {
     for (auto& e : te.ev) hipEventDestroy((hipEvent_t)e);
   if (h->comm) ncclCommDestroy(h->comm);
   if (h->hcnt) hipHostFree(h->hcnt);
+  if (h->hflag) hipHostFree((void*)h->hflag);
+  if (h->ev_member) hipEventDestroy(h->ev_member);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
   return SWIM_OK;
@@ -440,15 +477,29 @@ int swim_step(swim_handle* h, uint32_t n) {
   const Dev& d = h->d;
   for (uint32_t i = 0; i < n; ++i) {
     const TickEvents* te = profile ? &h->prof[i] : nullptr;
+    const uint32_t k = (uint32_t)h->tick;
     if (d.W == 1) {
-      launch_tick(d, (uint32_t)h->tick, h->stream, te);
+      // SYNC diff(k) was queued in the previous iteration, except for the first tick of this call
+      if (i == 0 || h->no_pipe) launch_diff(d, k, h->stream, te);
+      launch_member(d, k, h->stream, te);
+      HIPCK(hipEventRecord(h->ev_member, h->stream));
+      const bool pipe = i + 1 < n && !h->no_pipe;
+      if (pipe) launch_diff(d, k + 1, h->stream, profile ? &h->prof[i + 1] : nullptr);  // overlaps the wait
+      HIPCK(hipEventSynchronize(h->ev_member));
+      if (h->hflag[0] != 0 || h->no_skip) {
+        launch_gossip(d, k, h->stream, te);
+      } else if (te) {
+        HIPCK(hipEventRecord((hipEvent_t)te->ev[4], h->stream));
+        HIPCK(hipEventRecord((hipEvent_t)te->ev[5], h->stream));
+      }
     } else {
       int xr;
-      launch_tick_a(d, (uint32_t)h->tick, h->stream, te);
+      launch_tick_a(d, k, h->stream, te);
       if ((xr = exchange(h, d.xa_send, d.xa_recv, d.XA_PEER, d.xa_scnt, d.xa_rcnt)) != SWIM_OK) return xr;
-      launch_tick_b(d, (uint32_t)h->tick, h->stream, te);
-      if ((xr = exchange(h, d.xb_send, d.xb_recv, d.XB_PEER, d.xb_scnt, d.xb_rcnt)) != SWIM_OK) return xr;
-      launch_tick_c(d, (uint32_t)h->tick, h->stream);
+      const bool gossip = h->xflag;
+      launch_tick_b(d, k, h->stream, te, gossip);
+      if (gossip && (xr = exchange(h, d.xb_send, d.xb_recv, d.XB_PEER, d.xb_scnt, d.xb_rcnt)) != SWIM_OK) return xr;
+      launch_tick_c(d, k, h->stream, gossip);
     }
     h->tick++;
   }
@@ -608,7 +659,7 @@ int swim_drain_events(swim_handle* h, swim_event* out, size_t cap, size_t* n_out
     size_t base = h->host_events.size();
     h->host_events.resize(base + n);
     HIPCK(hipMemcpy(h->host_events.data() + base, h->d.ev, sizeof(swim_event) * n, hipMemcpyDeviceToHost));
-    HIPCK(hipMemset(h->d.ev_n, 0, 4));
+    HIPCK(hipMemsetAsync(h->d.ev_n, 0, 4, h->stream));
   }
   auto& ev = h->host_events;
   std::stable_sort(ev.begin(), ev.end(), [](const swim_event& a, const swim_event& b) {
@@ -648,6 +699,19 @@ int swim_counters_get(swim_handle* h, swim_counters* out) {
 }
 
 const char* swim_last_error(swim_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+// debugging aid (not part of the ABI header): the scalar fields folded into the "misc" state-hash word
+int swimdbg_scalars(swim_handle* h, uint32_t m, uint64_t* out) {
+  if (!h || !owns(h, m)) return SWIM_EINVAL;
+  HIPCK(hipStreamSynchronize(h->stream));
+  uint32_t* src[6] = {h->d.cidCnt, h->d.syncSeq, h->d.gCounter, h->d.nextSync, h->d.fdPeriod, h->d.gPeriod};
+  for (int i = 0; i < 6; ++i) {
+    uint32_t v = 0;
+    HIPCK(hipMemcpy(&v, src[i] + m, 4, hipMemcpyDeviceToHost));
+    out[i] = (i == 3 && v == NEVER) ? ~0ull : v;
+  }
+  return SWIM_OK;
+}
 
 // debugging aid (not part of the ABI header): one member's gossip-round ring: [tick, spread, cnt, targets...] x LOGW
 int swimdbg_read_log(swim_handle* h, uint32_t m, uint32_t* out, size_t cap, uint32_t* logw, uint32_t* fanout,

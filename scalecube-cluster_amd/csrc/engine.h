@@ -19,7 +19,6 @@ constexpr uint32_t NEVER = 0xFFFFFFFFu;
 constexpr uint32_t MAX_EPOCHS = 8;
 constexpr uint32_t SUBCAP = 8, PATHCAP = 8, FREC = 8, GREC = 8;
 constexpr uint32_t CH = 2048;  // subjects per SYNC-diff work item (256 threads x 8)
-constexpr uint32_t MSG_SORT_MAX = 8192;  // SYNC / SYNC_ACK messages per tick (single-block LDS sort)
 
 // S entry flags (gossip slot x member)
 constexpr uint32_t S_PENDING = 1u << 29, S_SWEPT = 1u << 30, S_REBORN = 1u << 31;
@@ -35,6 +34,8 @@ constexpr uint32_t E_SLOTS = 1, E_FETCH = 2, E_SUBS = 4, E_PATHS = 8, E_GROUPS =
 constexpr uint32_t PAY_RX = 0x40000000u;  // received from another shard: PAY_RX | rx index (dirty chunks + baseline)
 constexpr uint32_t RRW = 12;              // words per gossip-round record: m, cnt, spread, period, targets[8]
 constexpr uint32_t NSW = 8;               // words per new-gossip-slot record
+// exchange byte-count words: low 48 bits = bytes; bit 62 = the sender has gossip slots in use this tick
+constexpr unsigned long long XCNT_MASK = (1ull << 48) - 1, XFLAG_GOSSIP = 1ull << 62;
 
 // counters (swim_counters order after .tick)
 enum Ctr { C_R = 0, C_W, C_M, C_G, C_E, C_LOST, C_GCREATED, C_SYNCMERGE, C_NCTR = 16 };
@@ -108,11 +109,10 @@ struct Dev {
   uint32_t* nmsg;  // [2]
   uint64_t* arena[2];
   uint32_t* arena_used;  // [2]
-  uint32_t* m_idx;  // previous tick's messages sorted by m_key
-  uint32_t* m_head; // [N] first sorted message for each destination, NEVER if none (reset by the consumer)
+  uint32_t* m_next; // [MSGCAP] next message to the same destination (list built by k_sync_diff)
+  uint32_t* m_head; // [N] first message of each destination's list, NEVER if none (reset by the consumer)
   uint32_t* pending_inc; // [N] swim_update_incarnation requests for the next tick's P0
   uint32_t* next_evt; // [N] earliest tick at which a pending path / subscription / fetch needs the member
-  uint64_t* m_key;  // dst << 44 | src << 24 | (syncSeq & 0xFFFFFF)
   uint32_t* chunk_meta;                      // [MSGCAP][NCHUNK][2] (pool offset, count)
   uint64_t* pool;                            // candidate (subject << 34 | key)
   uint32_t* pool_used;
@@ -123,6 +123,7 @@ struct Dev {
   unsigned long long* ctr;  // [C_NCTR]
   uint32_t* err;            // [8] bits, info...
   const Dev* self;          // device-resident copy of this struct (kernels index it through a pointer)
+  uint32_t* hflag;          // host-mapped: [0] gossip slots in use after this tick's member control (W == 1)
 
   // ---- row sharding (W > 1) ----
   // This shard owns observers [lo, hi): their rows, lists, subscriptions, paths, fetches and groups are stored
@@ -168,12 +169,17 @@ struct TickEvents {
 
 // host-side kernel launchers (one HIP stream)
 void launch_init(const Dev& d, void* stream);
-void launch_tick(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr);
+// single GPU, per tick k: launch_diff(k) (k > 0), launch_member(k) (+ host flag), then launch_gossip(k) if the flag
+// says a gossip slot is in use; launch_diff(k+1) may be queued before launch_gossip(k)
+void launch_diff(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr);
+void launch_member(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr);
+void launch_gossip(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr);
 // sharded tick (W > 1): A = SYNC diff + member control + pack exchange A; B = unpack A, gossip sends, pack
-// exchange B; C = unpack B, apply receipts, routing, slot recycling. The host runs the exchanges in between.
+// exchange B; C = unpack B, apply receipts, routing, slot recycling. The host runs the exchanges in between and
+// skips the gossip half (and exchange B) when no shard has a gossip slot in use.
 void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr);
-void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr);
-void launch_tick_c(const Dev& d, uint32_t k, void* stream);
+void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool gossip);
+void launch_tick_c(const Dev& d, uint32_t k, void* stream, bool gossip);
 void launch_kill(const Dev& d, uint32_t member, void* stream);
 void launch_hash(const Dev& d, uint64_t* out, uint32_t now, void* stream);
 

@@ -104,55 +104,7 @@ __global__ void k_init_base(Dev d) {
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// routing: counting sort by destination member, then per-destination sort by a 64-bit key
-// the previous tick's SYNC / SYNC_ACK messages sorted by (dst, src, syncSeq): one block, bitonic in LDS
-__global__ void __launch_bounds__(1024) k_sort_msgs(const SyncMsg* msgs, const uint32_t* nmsg, uint32_t cap,
-                                                    uint64_t* key_out, uint32_t* idx_out, uint32_t* err) {
-  __shared__ uint64_t K[MSG_SORT_MAX];
-  __shared__ uint32_t V[MSG_SORT_MAX];
-  uint32_t n = *nmsg < cap ? *nmsg : cap;
-  if (n == 0) return;
-  if (n > MSG_SORT_MAX) {
-    if (threadIdx.x == 0) atomicOr(err, E_SORTCAP);
-    n = MSG_SORT_MAX;
-  }
-  uint32_t p2 = 1;
-  while (p2 < n) p2 <<= 1;
-  for (uint32_t i = threadIdx.x; i < p2; i += blockDim.x) {
-    if (i < n) {
-      const SyncMsg& m = msgs[i];
-      K[i] = ((uint64_t)m.dst << 44) | ((uint64_t)m.src << 24) | (m.seq & 0xFFFFFFu);
-      V[i] = i;
-    } else {
-      K[i] = ~0ull;
-      V[i] = 0;
-    }
-  }
-  __syncthreads();
-  for (uint32_t size = 2; size <= p2; size <<= 1)
-    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-      for (uint32_t i = threadIdx.x; i < p2; i += blockDim.x) {
-        uint32_t j = i ^ stride;
-        if (j > i) {
-          bool up = (i & size) == 0;
-          if ((K[i] > K[j]) == up) {
-            uint64_t tk = K[i];
-            K[i] = K[j];
-            K[j] = tk;
-            uint32_t tv = V[i];
-            V[i] = V[j];
-            V[j] = tv;
-          }
-        }
-      }
-      __syncthreads();
-    }
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-    key_out[i] = K[i];
-    idx_out[i] = V[i];
-  }
-}
-
+// receipt routing: counting sort of first receipts by member, then per-member sort by gossip id
 __global__ void k_count_rc(const uint64_t* raw, const uint32_t* n_, uint32_t cap, uint32_t* cnt) {
   uint32_t n = *n_ < cap ? *n_ : cap;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
@@ -166,16 +118,6 @@ __global__ void k_scatter_rc(const Dev d, const uint64_t* raw, const uint32_t* n
     uint32_t p = off[t] + atomicAdd(&fill[t], 1u);
     idx[p] = g;
     key[p] = d.slot_gid[g];
-  }
-}
-
-// first sorted message of every destination present this tick
-__global__ void k_msg_heads(const uint64_t* key, const uint32_t* nmsg, uint32_t cap, uint32_t* head) {
-  uint32_t n = *nmsg < cap ? *nmsg : cap;
-  n = n < MSG_SORT_MAX ? n : MSG_SORT_MAX;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    uint32_t dst = (uint32_t)(key[i] >> 44);
-    if (i == 0 || (uint32_t)(key[i - 1] >> 44) != dst) head[dst] = i;
   }
 }
 
@@ -281,9 +223,10 @@ __global__ void __launch_bounds__(256) k_seg_sort(uint64_t* key, uint32_t* val, 
 
 // ------------------------------------------------------------------------------------------------------------
 // k_sync_diff: for every SYNC / SYNC_ACK sent in tick k-1, stream the payload row (the sender's live row, or its
-// copy-on-write snapshot) against the receiver's row and extract, per 1024-subject chunk and in subject order,
+// copy-on-write snapshot) against the receiver's row and extract, per 2048-subject chunk and in subject order,
 // the records that differ (the eager `!r1.equals(table.get(id))` filter of syncMembership, :456-467).
-// This is the HBM-bound hot loop: 2 x 8 B read per subject per merge.
+// This is the HBM-bound hot loop: 2 x 8 B read per subject per merge. It also links every message into its
+// receiver's inbound list (m_head / m_next), which k_member_tick walks in (src, syncSeq) order.
 __global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b) {
   __shared__ uint32_t scan[256];
   __shared__ uint32_t base;
@@ -292,6 +235,7 @@ __global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b) {
   for (uint32_t w = blockIdx.x; w < total; w += gridDim.x) {
     uint32_t mi = w / d.NCHUNK, c = w % d.NCHUNK;
     const SyncMsg& mm = d.msgs[b][mi];
+    if (c == 0 && threadIdx.x == 0) d.m_next[mi] = atomicExch(&d.m_head[mm.dst], mi);
     const uint32_t s0 = c * CH + threadIdx.x * 8;
     // this lane's 8 payload records: the sender's live row or its copy-on-write snapshot; for a payload
     // received from another shard, the shipped chunk if it differs from the baseline, else the baseline
@@ -716,6 +660,42 @@ __global__ void __launch_bounds__(256) k_hash(Dev d, uint64_t* out, uint32_t now
   }
 }
 
+// after k_member_tick (W == 1): reset the per-tick counters the gossip plane of this tick and the SYNC diff and
+// member control of the next tick append to, and tell the host whether any gossip slot is in use (if none, the
+// gossip data plane of this tick has nothing to send, deliver, route or recycle and is not launched)
+__global__ void k_tick_flag(Dev d, uint32_t k) {
+  if (threadIdx.x != 0) return;
+  uint32_t nb = (k + 1) & 1;
+  d.nmsg[nb] = 0;
+  d.arena_used[nb] = 0;
+  *d.pool_used = 0;
+  *d.nactive = 0;
+  *d.deliv_n = 0;
+  *d.rc_n = 0;
+  d.hflag[0] = (uint32_t)((int32_t)d.SPR - *d.free_top);
+  __threadfence_system();
+}
+
+// end of a sharded tick (W > 1): the same resets, plus the exchange counters
+__global__ void k_tick_end(Dev d, uint32_t k) {
+  uint32_t t = threadIdx.x;
+  if (t < 8) d.xn[t] = 0;
+  if (t < d.W) {
+    d.rq_n[t] = 0;
+    d.xa_scnt[t] = 0;
+    d.xb_scnt[t] = 0;
+  }
+  if (t == 0) {
+    uint32_t nb = (k + 1) & 1;
+    d.nmsg[nb] = 0;
+    d.arena_used[nb] = 0;
+    *d.pool_used = 0;
+    *d.nactive = 0;
+    *d.deliv_n = 0;
+    *d.rc_n = 0;
+  }
+}
+
 // ------------------------------------------------------------------------------------------------------------
 // host launchers
 static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
@@ -729,47 +709,35 @@ void launch_init(const Dev& d, void* stream) {
   if (d.W > 1) hipLaunchKernelGGL(k_init_base, dim3(cdiv(d.NS, 256)), dim3(256), 0, st, d);
 }
 
-void launch_tick(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
+// single GPU: the tick is cut in three so that the host can hold back the gossip data plane when no slot is in
+// use; the SYNC diff of tick k+1 does not depend on the gossip plane of tick k and is queued in between
+void launch_diff(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
   hipStream_t st = (hipStream_t)stream;
-  uint32_t b = k & 1, pb = (k - 1) & 1;
-  // fresh per-tick output buffers for this tick's sends
-  hipMemsetAsync(d.nmsg + b, 0, sizeof(uint32_t), st);
-  hipMemsetAsync(d.arena_used + b, 0, sizeof(uint32_t), st);
-  hipMemsetAsync(d.pool_used, 0, sizeof(uint32_t), st);
-  if (k > 0) {
-    // the previous tick's SYNC / SYNC_ACK messages, sorted by (dst, src, syncSeq)
-    hipLaunchKernelGGL(k_sort_msgs, dim3(1), dim3(1024), 0, st, d.msgs[pb], d.nmsg + pb, d.MSGCAP, d.m_key, d.m_idx, d.err);
-    hipLaunchKernelGGL(k_msg_heads, dim3(32), dim3(256), 0, st, d.m_key, d.nmsg + pb, d.MSGCAP, d.m_head);
-    if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
-    hipLaunchKernelGGL(k_sync_diff, dim3(2048), dim3(256), 0, st, d, pb);
-    if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
-  }
+  if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
+  if (k > 0) hipLaunchKernelGGL(k_sync_diff, dim3(2048), dim3(256), 0, st, d, (k - 1) & 1);
+  if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
+}
+
+void launch_member(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
+  hipStream_t st = (hipStream_t)stream;
   if (prof) hipEventRecord((hipEvent_t)prof->ev[2], st);
   hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[3], st);
-  // gossip data plane for the rounds that ran in this tick
-  uint32_t* active = d.active;
-  uint32_t* nactive = d.nactive;
-  hipMemsetAsync(nactive, 0, sizeof(uint32_t), st);
-  hipMemsetAsync(d.deliv_n, 0, sizeof(uint32_t), st);
-  hipMemsetAsync(d.rc_n, 0, sizeof(uint32_t), st);
-  hipLaunchKernelGGL(k_gossip_active, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, st, d, active, nactive);
+  hipLaunchKernelGGL(k_tick_flag, dim3(1), dim3(64), 0, st, d, k);
+}
+
+static void launch_receipt_routing(const Dev& d, hipStream_t st);
+
+void launch_gossip(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_gossip_active, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, st, d, d.active, d.nactive);
   hipLaunchKernelGGL(k_gossip_contacts, dim3(cdiv((uint64_t)d.NL * d.F, 256)), dim3(256), 0, st, d, k);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[4], st);
-  hipLaunchKernelGGL(k_gossip_send, dim3(1024), dim3(256), 0, st, d.self, k, active, nactive);
+  hipLaunchKernelGGL(k_gossip_send, dim3(1024), dim3(256), 0, st, d.self, k, d.active, d.nactive);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[5], st);
   hipLaunchKernelGGL(k_gossip_apply, dim3(1024), dim3(256), 0, st, d, k);
-  // route this tick's first receipts by member (rc_cnt / rc_fill were zeroed by the consumers in k_member_tick)
-  hipLaunchKernelGGL(k_count_rc, dim3(256), dim3(256), 0, st, d.rc_raw, d.rc_n, d.RCAP, d.rc_cnt);
-  uint32_t nb = cdiv(d.N, 1024);
-  hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(256), 0, st, d.rc_cnt, d.rc_off, d.scan_part, d.N);
-  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, st, d.scan_part, nb);
-  hipLaunchKernelGGL(k_scan_add, dim3(cdiv(d.N, 256)), dim3(256), 0, st, d.rc_off, d.scan_part, d.N);
-  hipLaunchKernelGGL(k_scatter_rc, dim3(256), dim3(256), 0, st, d, d.rc_raw, d.rc_n, d.RCAP, d.rc_off, d.rc_fill,
-                     d.rc_slot, d.rc_key);
-  hipLaunchKernelGGL(k_seg_sort, dim3(1024), dim3(256), 0, st, d.rc_key, d.rc_slot, d.rc_off, d.rc_cnt, d.N, d.err,
-                     d.rc_n);
-  hipLaunchKernelGGL(k_gossip_free, dim3(1024), dim3(256), 0, st, d, active, nactive);
+  launch_receipt_routing(d, st);
+  hipLaunchKernelGGL(k_gossip_free, dim3(1024), dim3(256), 0, st, d, d.active, d.nactive);
 }
 
 // ---- sharded tick (W > 1): the same kernel sequence as launch_tick, cut at the two exchange points ----
@@ -788,19 +756,9 @@ static void launch_receipt_routing(const Dev& d, hipStream_t st) {
 void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
   hipStream_t st = (hipStream_t)stream;
   uint32_t b = k & 1, pb = (k - 1) & 1;
-  hipMemsetAsync(d.nmsg + b, 0, sizeof(uint32_t), st);
-  hipMemsetAsync(d.arena_used + b, 0, sizeof(uint32_t), st);
-  hipMemsetAsync(d.pool_used, 0, sizeof(uint32_t), st);
-  hipMemsetAsync(d.xn, 0, 8 * sizeof(uint32_t), st);
-  hipMemsetAsync(d.rq_n, 0, d.W * sizeof(uint32_t), st);
-  hipMemsetAsync(d.xa_scnt, 0, d.W * sizeof(unsigned long long), st);
-  if (k > 0) {
-    hipLaunchKernelGGL(k_sort_msgs, dim3(1), dim3(1024), 0, st, d.msgs[pb], d.nmsg + pb, d.MSGCAP, d.m_key, d.m_idx, d.err);
-    hipLaunchKernelGGL(k_msg_heads, dim3(32), dim3(256), 0, st, d.m_key, d.nmsg + pb, d.MSGCAP, d.m_head);
-    if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
-    hipLaunchKernelGGL(k_sync_diff, dim3(2048), dim3(256), 0, st, d, pb);
-    if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
-  }
+  if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
+  if (k > 0) hipLaunchKernelGGL(k_sync_diff, dim3(2048), dim3(256), 0, st, d, pb);
+  if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[2], st);
   hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[3], st);
@@ -810,15 +768,16 @@ void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   hipLaunchKernelGGL(k_pack_a_chunks, dim3(512, d.W), dim3(256), 0, st, d, b);
 }
 
-void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
+void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool gossip) {
   hipStream_t st = (hipStream_t)stream;
   uint32_t b = k & 1;
   hipLaunchKernelGGL(k_unpack_a, dim3(64, d.W), dim3(256), 0, st, d, k);
   hipLaunchKernelGGL(k_msgs_commit, dim3(64), dim3(256), 0, st, d, b);
-  hipMemsetAsync(d.nactive, 0, sizeof(uint32_t), st);
-  hipMemsetAsync(d.deliv_n, 0, sizeof(uint32_t), st);
-  hipMemsetAsync(d.rc_n, 0, sizeof(uint32_t), st);
-  hipMemsetAsync(d.xb_scnt, 0, d.W * sizeof(unsigned long long), st);
+  if (!gossip) {  // no gossip slot in use on any shard: nothing to send, deliver or recycle; no exchange B
+    if (prof) hipEventRecord((hipEvent_t)prof->ev[4], st);
+    if (prof) hipEventRecord((hipEvent_t)prof->ev[5], st);
+    return;
+  }
   hipLaunchKernelGGL(k_gossip_active, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, st, d, d.active, d.nactive);
   hipLaunchKernelGGL(k_gossip_contacts, dim3(cdiv((uint64_t)d.NL * d.F, 256)), dim3(256), 0, st, d, k);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[4], st);
@@ -827,14 +786,19 @@ void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   hipLaunchKernelGGL(k_pack_b, dim3(64, d.W), dim3(256), 0, st, d);
 }
 
-void launch_tick_c(const Dev& d, uint32_t k, void* stream) {
+void launch_tick_c(const Dev& d, uint32_t k, void* stream, bool gossip) {
   hipStream_t st = (hipStream_t)stream;
+  if (!gossip) {
+    hipLaunchKernelGGL(k_tick_end, dim3(1), dim3(64), 0, st, d, k);
+    return;
+  }
   hipLaunchKernelGGL(k_unpack_b_sweeps, dim3(64, d.W), dim3(256), 0, st, d);
   hipLaunchKernelGGL(k_unpack_b_deliv, dim3(64, d.W), dim3(256), 0, st, d);
   hipLaunchKernelGGL(k_gossip_apply, dim3(1024), dim3(256), 0, st, d, k);
   launch_receipt_routing(d, st);
   hipLaunchKernelGGL(k_gossip_free, dim3(1024), dim3(256), 0, st, d, d.active, d.nactive);
   hipLaunchKernelGGL(k_round_reset, dim3(16, d.W), dim3(256), 0, st, d);
+  hipLaunchKernelGGL(k_tick_end, dim3(1), dim3(64), 0, st, d, k);
 }
 
 void launch_kill(const Dev& d, uint32_t member, void* stream) {

@@ -27,8 +27,7 @@ struct ML {
   uint64_t* row;
   uint32_t *fdl, *gl, *subs, *paths, *fetch, *groups;
   unsigned long long c[8];
-  uint32_t pend[8];
-  uint32_t npend;
+  uint32_t pend;  // this tick's SYNC messages that carry the live row: a chain through SyncMsg.pad (NEVER = none)
   uint32_t tround;
 };
 
@@ -54,18 +53,18 @@ __device__ __forceinline__ void cow(ML& L) {
   uint32_t r = atomicAdd(&d.arena_used[b], 1u);
   if (r >= d.ARENA_ROWS) {
     set_err(d, E_ARENA);
-    L.npend = 0;
+    L.pend = NEVER;
     return;
   }
   uint64_t* dst = d.arena[b] + (size_t)r * d.NS;
-  for (uint32_t s = 0; s < L.N; ++s) dst[s] = L.row[s];
-  for (uint32_t i = 0; i < L.npend; ++i) d.msgs[b][L.pend[i]].payload = r;
-  L.npend = 0;
+  for (uint32_t s = 0; s < d.NS; ++s) dst[s] = L.row[s];  // with the zero padding k_sync_diff reads up to NS
+  for (uint32_t i = L.pend; i != NEVER; i = d.msgs[b][i].pad) d.msgs[b][i].payload = r;
+  L.pend = NEVER;
 }
 
 __device__ __forceinline__ void row_put(ML& L, uint32_t s, uint64_t v) {
   uint64_t old = L.row[s];
-  if (L.npend && ((old ^ v) & KEY_MASK)) cow(L);
+  if (L.pend != NEVER && ((old ^ v) & KEY_MASK)) cow(L);
   L.row[s] = v;
 }
 
@@ -94,10 +93,9 @@ __device__ __forceinline__ bool send_sync(ML& L, uint32_t kind, uint32_t dst, ui
   mm.payload = NEVER;
   mm.psize = L.tsize;
   mm.ncand = 0;
-  mm.pad = 0;
+  mm.pad = L.pend;  // chained so that a later row write can redirect the payload to a snapshot (cow)
   d.msgs[b][i] = mm;
-  if (L.npend == 8) cow(L);
-  L.pend[L.npend++] = i;
+  L.pend = i;
   return true;
 }
 
@@ -606,7 +604,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   L.fetch = d.fetch + li * d.FCAP * FREC;
   L.groups = d.groups + li * d.GRCAP * GREC;
   for (int i = 0; i < 8; ++i) L.c[i] = 0;
-  L.npend = 0;
+  L.pend = NEVER;
   L.tround = 0;
 
   // ---- P0 host requests: updateIncarnation (MembershipProtocolImpl.java:178-190) ----
@@ -645,16 +643,52 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   }
 
   // ---- P1 SYNC / SYNC_ACK (onMessage :320-331, onSync :346-367, onSyncAck :337-343) ----
+  // k_sync_diff linked this member's inbound messages into a list; they are handled in (src, syncSeq) order
   if (!dead && k > 0 && d.m_head[m] != NEVER) {
-    // this member's segment of the (dst, src, syncSeq)-sorted message list
-    uint32_t nm = d.nmsg[(k - 1) & 1];
-    nm = nm < d.MSGCAP ? nm : d.MSGCAP;
-    nm = nm < MSG_SORT_MAX ? nm : MSG_SORT_MAX;
-    uint32_t lo = d.m_head[m];
+    const uint32_t pb = (k - 1) & 1;
+    const uint32_t head = d.m_head[m];
     d.m_head[m] = NEVER;
-    for (uint32_t q = lo; q < nm && (uint32_t)(d.m_key[q] >> 44) == m; ++q) {
-      uint32_t mi = d.m_idx[q];
-      SyncMsg mm = d.msgs[(k - 1) & 1][mi];
+    constexpr uint32_t MQ = 16;
+    uint64_t key[MQ];
+    uint32_t idx[MQ], n = 0;
+    bool more = false;
+    for (uint32_t q = head; q != NEVER; q = d.m_next[q]) {
+      if (n == MQ) {
+        more = true;
+        break;
+      }
+      const SyncMsg& mq = d.msgs[pb][q];
+      uint64_t kq = ((uint64_t)mq.src << 32) | mq.seq;
+      uint32_t j = n++;
+      while (j > 0 && key[j - 1] > kq) {
+        key[j] = key[j - 1];
+        idx[j] = idx[j - 1];
+        --j;
+      }
+      key[j] = kq;
+      idx[j] = q;
+    }
+    uint64_t last = 0;
+    for (uint32_t r = 0;; ++r) {
+      uint32_t mi;
+      if (!more) {
+        if (r == n) break;
+        mi = idx[r];
+      } else {  // rare: more than MQ messages in one tick (a seed during a cold join): select the next key
+        uint64_t best = ~0ull;
+        mi = NEVER;
+        for (uint32_t q = head; q != NEVER; q = d.m_next[q]) {
+          const SyncMsg& mq = d.msgs[pb][q];
+          uint64_t kq = ((uint64_t)mq.src << 32) | mq.seq;
+          if ((r == 0 || kq > last) && kq < best) {
+            best = kq;
+            mi = q;
+          }
+        }
+        if (mi == NEVER) break;
+        last = best;
+      }
+      SyncMsg mm = d.msgs[pb][mi];
       if (mm.kind == K_SYNC) {
         int g = alloc_group(L, 0, mm.src, mm.cid_iss, mm.cid_cnt);
         merge_payload(L, mi, R_SYNC, g);

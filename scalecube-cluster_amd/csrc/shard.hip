@@ -106,7 +106,8 @@ __global__ void __launch_bounds__(256) k_pack_a(Dev d, uint32_t b) {
     H[3] = nchunk;
     H[4] = (uint32_t)data_off;
     H[5] = H[6] = H[7] = 0;
-    d.xa_scnt[q] = total;
+    // the flag rides on the byte count: every shard learns whether any shard has a gossip slot in use
+    d.xa_scnt[q] = total | ((int32_t)d.SPR - *d.free_top > 0 ? XFLAG_GOSSIP : 0ull);
     sh[0] = nslot;
     sh[1] = nround;
     sh[2] = nsync;
@@ -158,7 +159,7 @@ __global__ void __launch_bounds__(256) k_pack_a_chunks(Dev d, uint32_t b) {
 // replay peer p's gossip creations and rounds into the replicated gossip plane; queue its SYNC messages
 __global__ void __launch_bounds__(256) k_unpack_a(Dev d, uint32_t k) {
   const uint32_t p = blockIdx.y;
-  if (p == d.rank || d.xa_rcnt[p] < 32) return;
+  if (p == d.rank || (d.xa_rcnt[p] & XCNT_MASK) < 32) return;
   const uint8_t* R = d.xa_recv + (size_t)p * d.XA_PEER;
   const uint32_t* H = (const uint32_t*)R;
   const uint32_t nslot = H[0], nround = H[1], nsync = H[2], data_off = H[4];
@@ -247,7 +248,7 @@ __global__ void __launch_bounds__(256) k_pack_b(Dev d) {
 // peers' sweeps first (sweepGossips :283-308), so that a delivery to a member that swept g this tick re-creates it
 __global__ void k_unpack_b_sweeps(Dev d) {
   const uint32_t p = blockIdx.y;
-  if (p == d.rank || d.xb_rcnt[p] < 16) return;
+  if (p == d.rank || (d.xb_rcnt[p] & XCNT_MASK) < 16) return;
   const uint8_t* R = d.xb_recv + (size_t)p * d.XB_PEER;
   const uint32_t nd = ((const uint32_t*)R)[0], ns = ((const uint32_t*)R)[1];
   const uint64_t* V = (const uint64_t*)(R + 16) + nd;
@@ -262,7 +263,7 @@ __global__ void k_unpack_b_sweeps(Dev d) {
 // peers' first receipts join this shard's delivery list, deduplicated by the PENDING bit like local ones
 __global__ void k_unpack_b_deliv(Dev d) {
   const uint32_t p = blockIdx.y;
-  if (p == d.rank || d.xb_rcnt[p] < 16) return;
+  if (p == d.rank || (d.xb_rcnt[p] & XCNT_MASK) < 16) return;
   const uint8_t* R = d.xb_recv + (size_t)p * d.XB_PEER;
   const uint32_t nd = ((const uint32_t*)R)[0];
   const uint64_t* V = (const uint64_t*)(R + 16);
@@ -281,7 +282,7 @@ __global__ void k_unpack_b_deliv(Dev d) {
 // the peers' members are out of their gossip round again
 __global__ void k_round_reset(Dev d) {
   const uint32_t p = blockIdx.y;
-  if (p == d.rank || d.xa_rcnt[p] < 32) return;
+  if (p == d.rank || (d.xa_rcnt[p] & XCNT_MASK) < 32) return;
   const uint8_t* R = d.xa_recv + (size_t)p * d.XA_PEER;
   const uint32_t* H = (const uint32_t*)R;
   const uint32_t* RR = (const uint32_t*)(R + 32) + (size_t)H[0] * NSW;

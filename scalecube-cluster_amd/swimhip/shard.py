@@ -19,6 +19,9 @@ from .cluster import SimulatedCluster, SwimError
 from .config import SimConfig
 
 
+COUNT_MASK = (1 << 48) - 1  # exchange count words: bytes below bit 48, opaque flags above (swimhip_shard.h)
+
+
 def shard_range(n, world, rank):
     """[lo, hi) observers of a rank: contiguous ranges floor(r N / W) (engine.h shard_lo)."""
     return rank * n // world, (rank + 1) * n // world
@@ -69,11 +72,13 @@ class GlooExchange(_HostExchange):
     def _run(self, send, sb, recv, cap, rb):
         import torch
         W = self.world
-        scounts = [int(sb[q]) for q in range(W)]
-        sc = torch.tensor(scounts, dtype=torch.int64)
+        words = [int(sb[q]) for q in range(W)]  # bytes in the low 48 bits, flags above (delivered unchanged)
+        scounts = [w & COUNT_MASK for w in words]
+        sc = torch.tensor(words, dtype=torch.int64)
         rc = torch.empty(W, dtype=torch.int64)
         self.dist.all_to_all_single(rc, sc, group=self.group)
-        rcounts = [int(x) for x in rc.tolist()]
+        rwords = [int(x) for x in rc.tolist()]
+        rcounts = [w & COUNT_MASK for w in rwords]
         total_s, total_r = sum(scounts), sum(rcounts)
         if total_r > cap:
             raise RuntimeError(f"receive {total_r} bytes > capacity {cap}")
@@ -83,7 +88,7 @@ class GlooExchange(_HostExchange):
         if total_r:
             C.memmove(recv, out.numpy().ctypes.data, total_r)
         for p in range(W):
-            rb[p] = rcounts[p]
+            rb[p] = rwords[p]
 
 
 class ThreadExchange:
@@ -101,16 +106,17 @@ class ThreadExchange:
         class _End(_HostExchange):
             def _run(self, send, sb, recv, cap, rb):
                 W = ex.world
-                counts = [int(sb[q]) for q in range(W)]
+                words = [int(sb[q]) for q in range(W)]
+                counts = [w & COUNT_MASK for w in words]
                 data = C.string_at(send, sum(counts)) if sum(counts) else b""
-                ex.blocks[rank] = (counts, data)
+                ex.blocks[rank] = (counts, words, data)
                 ex.barrier.wait(timeout=300)
                 parts = []
                 for p in range(W):
-                    cnts, dat = ex.blocks[p]
+                    cnts, wds, dat = ex.blocks[p]
                     off = sum(cnts[:rank])
                     parts.append(dat[off:off + cnts[rank]])
-                    rb[p] = cnts[rank]
+                    rb[p] = wds[rank]
                 buf = b"".join(parts)
                 if len(buf) > cap:
                     raise RuntimeError("receive capacity")

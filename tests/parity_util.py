@@ -28,7 +28,21 @@ def explain(o, e, member):
     go_, ge_ = o.gossips(member), e.gossips(member)
     so, se = set(go_), set(ge_)
     gd = f"gossips oracle-only {sorted(so - se)[:6]} engine-only {sorted(se - so)[:6]} ({len(so)}/{len(se)}); "
-    return (gd + f"row diffs (subject, oracle, engine): {diffs}; fd len {len(fo)}/{len(fe)} eq={np.array_equal(fo, fe)} "
+    sc = ""
+    try:
+        import ctypes as C
+        names = ["cidCnt", "syncSeq", "gCounter", "nextSync", "fdPeriod", "gPeriod"]
+        vals = []
+        for c in (o, e):
+            fn = c.lib.swimdbg_scalars
+            fn.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64)]
+            out = (C.c_uint64 * 6)()
+            fn(c._h, member, out)
+            vals.append(list(out))
+        sc = "scalars oracle/engine " + ", ".join(f"{n} {a}/{b}" for n, a, b in zip(names, *vals)) + "; "
+    except Exception:  # noqa: BLE001 - debugging detail only
+        pass
+    return (sc + gd + f"row diffs (subject, oracle, engine): {diffs}; fd len {len(fo)}/{len(fe)} eq={np.array_equal(fo, fe)} "
             f"cursor {co}/{ce}; gossip len {len(go)}/{len(ge)} eq={np.array_equal(go, ge)}")
 
 
