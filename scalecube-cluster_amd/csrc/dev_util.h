@@ -8,6 +8,10 @@ namespace swim {
 
 __device__ __forceinline__ void set_err(const Dev& d, uint32_t bit) { atomicOr(d.err, bit); }
 
+// 16-B row loads
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u64x2 ld_c(const uint64_t* p) { return *(const u64x2*)p; }
+
 // settings epoch in force at tick k (the latest epoch that started at or before k)
 __device__ __forceinline__ int epoch_at(const Dev& d, uint32_t k) {
   int best = -1;

@@ -109,8 +109,8 @@ struct Dev {
   uint32_t* nmsg;  // [2]
   uint64_t* arena[2];
   uint32_t* arena_used;  // [2]
-  uint32_t* m_next; // [MSGCAP] next message to the same destination (list built by k_sync_diff)
-  uint32_t* m_head; // [N] first message of each destination's list, NEVER if none (reset by the consumer)
+  uint32_t* m_next; // [2][MSGCAP] next message of msgs[b] to the same destination
+  uint32_t* m_head; // [2][N] first message of msgs[b] to each destination, NEVER if none (reset by the consumer)
   uint32_t* pending_inc; // [N] swim_update_incarnation requests for the next tick's P0
   uint32_t* next_evt; // [N] earliest tick at which a pending path / subscription / fetch needs the member
   uint32_t* chunk_meta;                      // [MSGCAP][NCHUNK][2] (pool offset, count)

@@ -52,7 +52,7 @@ __global__ void k_init_members(Dev d) {
   d.rc_cnt[m] = 0;
   d.rc_off[m] = 0;
   d.rc_fill[m] = 0;
-  d.m_head[m] = NEVER;
+  d.m_head[m] = d.m_head[d.N + m] = NEVER;
   d.next_evt[m] = NEVER;
   d.pending_inc[m] = 0;
   if (m >= d.lo && m < d.hi)
@@ -225,8 +225,9 @@ __global__ void __launch_bounds__(256) k_seg_sort(uint64_t* key, uint32_t* val, 
 // k_sync_diff: for every SYNC / SYNC_ACK sent in tick k-1, stream the payload row (the sender's live row, or its
 // copy-on-write snapshot) against the receiver's row and extract, per 2048-subject chunk and in subject order,
 // the records that differ (the eager `!r1.equals(table.get(id))` filter of syncMembership, :456-467).
-// This is the HBM-bound hot loop: 2 x 8 B read per subject per merge. It also links every message into its
-// receiver's inbound list (m_head / m_next), which k_member_tick walks in (src, syncSeq) order.
+// This is the HBM-bound hot loop: 2 x 8 B read per subject per merge. SHARDED adds payloads received from other
+// shards (baseline row + shipped chunks); the single-GPU instance has only local rows and snapshots.
+template <bool SHARDED>
 __global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b) {
   __shared__ uint32_t scan[256];
   __shared__ uint32_t base;
@@ -235,14 +236,13 @@ __global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b) {
   for (uint32_t w = blockIdx.x; w < total; w += gridDim.x) {
     uint32_t mi = w / d.NCHUNK, c = w % d.NCHUNK;
     const SyncMsg& mm = d.msgs[b][mi];
-    if (c == 0 && threadIdx.x == 0) d.m_next[mi] = atomicExch(&d.m_head[mm.dst], mi);
     const uint32_t s0 = c * CH + threadIdx.x * 8;
     // this lane's 8 payload records: the sender's live row or its copy-on-write snapshot; for a payload
     // received from another shard, the shipped chunk if it differs from the baseline, else the baseline
     const uint64_t* p8;
     if (mm.payload == NEVER) {
       p8 = d.row + lidx(d, mm.src) * d.NS + s0;
-    } else if (mm.payload & PAY_RX) {
+    } else if (SHARDED && (mm.payload & PAY_RX)) {
       const uint32_t ri = mm.payload & ~PAY_RX;
       const uint64_t* mk = d.rx_mask + (size_t)ri * d.MW;
       if ((mk[c >> 6] >> (c & 63)) & 1ull) {
@@ -258,15 +258,19 @@ __global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b) {
     const uint64_t* rcv = d.row + lidx(d, mm.dst) * d.NS;
     uint64_t p[8], r[8];
     if (s0 < d.NS) {  // NS is a multiple of 8: the 64-B group is in bounds, padding entries are 0 (absent)
-      const ulonglong2* pv = (const ulonglong2*)p8;
-      const ulonglong2* rv = (const ulonglong2*)(rcv + s0);
+      // (non-temporal loads measured 1.5x slower here on gfx950)
+      u64x2 a[4], q[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        ulonglong2 a = pv[j], q = rv[j];
-        p[2 * j] = a.x;
-        p[2 * j + 1] = a.y;
-        r[2 * j] = q.x;
-        r[2 * j + 1] = q.y;
+        a[j] = ld_c(p8 + 2 * j);
+        q[j] = ld_c(rcv + s0 + 2 * j);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        p[2 * j] = a[j].x;
+        p[2 * j + 1] = a[j].y;
+        r[2 * j] = q[j].x;
+        r[2 * j + 1] = q[j].y;
       }
     } else {
 #pragma unroll
@@ -709,12 +713,19 @@ void launch_init(const Dev& d, void* stream) {
   if (d.W > 1) hipLaunchKernelGGL(k_init_base, dim3(cdiv(d.NS, 256)), dim3(256), 0, st, d);
 }
 
+static void launch_sync_diff(const Dev& d, uint32_t b, hipStream_t st) {
+  if (d.W > 1)
+    hipLaunchKernelGGL(k_sync_diff<true>, dim3(2048), dim3(256), 0, st, d, b);
+  else
+    hipLaunchKernelGGL(k_sync_diff<false>, dim3(2048), dim3(256), 0, st, d, b);
+}
+
 // single GPU: the tick is cut in three so that the host can hold back the gossip data plane when no slot is in
 // use; the SYNC diff of tick k+1 does not depend on the gossip plane of tick k and is queued in between
 void launch_diff(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
   hipStream_t st = (hipStream_t)stream;
   if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
-  if (k > 0) hipLaunchKernelGGL(k_sync_diff, dim3(2048), dim3(256), 0, st, d, (k - 1) & 1);
+  if (k > 0) launch_sync_diff(d, (k - 1) & 1, st);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
 }
 
@@ -757,7 +768,7 @@ void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   hipStream_t st = (hipStream_t)stream;
   uint32_t b = k & 1, pb = (k - 1) & 1;
   if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
-  if (k > 0) hipLaunchKernelGGL(k_sync_diff, dim3(2048), dim3(256), 0, st, d, pb);
+  if (k > 0) launch_sync_diff(d, pb, st);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[2], st);
   hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k);

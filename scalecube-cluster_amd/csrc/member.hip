@@ -96,6 +96,8 @@ __device__ __forceinline__ bool send_sync(ML& L, uint32_t kind, uint32_t dst, ui
   mm.pad = L.pend;  // chained so that a later row write can redirect the payload to a snapshot (cow)
   d.msgs[b][i] = mm;
   L.pend = i;
+  // the receiver's inbound list for the next tick (sharded handles build it when the exchange commits the list)
+  if (d.W == 1) d.m_next[(size_t)b * d.MSGCAP + i] = atomicExch(&d.m_head[(size_t)b * d.N + dst], i);
   return true;
 }
 
@@ -541,10 +543,10 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   if (dead) {
     d.rc_cnt[m] = 0;
     d.rc_fill[m] = 0;
-    if (k > 0) d.m_head[m] = NEVER;
+    if (k > 0) d.m_head[(size_t)((k - 1) & 1) * d.N + m] = NEVER;
   } else {
     // idle fast path: most members have nothing due in most ticks (a ping every 10 ticks, a SYNC every 300)
-    uint32_t mh = k > 0 ? d.m_head[m] : NEVER;
+    uint32_t mh = k > 0 ? d.m_head[(size_t)((k - 1) & 1) * d.N + m] : NEVER;
     bool busy = mh != NEVER || d.rc_cnt[m] != 0 || d.pending_inc[m] || d.next_evt[m] <= k || d.timerMin[m] <= k || k == d.nextPing[m] ||
                 k == d.nextSync[m] || (d.initFlags[m] & INIT_ACTIVE) || (k == 0 && d.init_mode == 0);
     if (!busy) {
@@ -643,16 +645,17 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   }
 
   // ---- P1 SYNC / SYNC_ACK (onMessage :320-331, onSync :346-367, onSyncAck :337-343) ----
-  // k_sync_diff linked this member's inbound messages into a list; they are handled in (src, syncSeq) order
-  if (!dead && k > 0 && d.m_head[m] != NEVER) {
+  // the senders linked this member's inbound messages into a list; they are handled in (src, syncSeq) order
+  const uint32_t* mnext = d.m_next + (size_t)((k - 1) & 1) * d.MSGCAP;
+  if (!dead && k > 0 && d.m_head[(size_t)((k - 1) & 1) * d.N + m] != NEVER) {
     const uint32_t pb = (k - 1) & 1;
-    const uint32_t head = d.m_head[m];
-    d.m_head[m] = NEVER;
+    const uint32_t head = d.m_head[(size_t)pb * d.N + m];
+    d.m_head[(size_t)pb * d.N + m] = NEVER;
     constexpr uint32_t MQ = 16;
     uint64_t key[MQ];
     uint32_t idx[MQ], n = 0;
     bool more = false;
-    for (uint32_t q = head; q != NEVER; q = d.m_next[q]) {
+    for (uint32_t q = head; q != NEVER; q = mnext[q]) {
       if (n == MQ) {
         more = true;
         break;
@@ -677,7 +680,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
       } else {  // rare: more than MQ messages in one tick (a seed during a cold join): select the next key
         uint64_t best = ~0ull;
         mi = NEVER;
-        for (uint32_t q = head; q != NEVER; q = d.m_next[q]) {
+        for (uint32_t q = head; q != NEVER; q = mnext[q]) {
           const SyncMsg& mq = d.msgs[pb][q];
           uint64_t kq = ((uint64_t)mq.src << 32) | mq.seq;
           if ((r == 0 || kq > last) && kq < best) {

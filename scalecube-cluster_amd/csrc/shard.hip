@@ -220,7 +220,10 @@ __global__ void __launch_bounds__(256) k_unpack_a(Dev d, uint32_t k) {
 // the assembled inbound list becomes msgs[b], which the next tick sorts and merges
 __global__ void k_msgs_commit(Dev d, uint32_t b) {
   uint32_t n = min(d.xn[4], d.MSGCAP);
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) d.msgs[b][i] = d.mtmp[i];
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    d.msgs[b][i] = d.mtmp[i];
+    d.m_next[(size_t)b * d.MSGCAP + i] = atomicExch(&d.m_head[(size_t)b * d.N + d.mtmp[i].dst], i);
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) d.nmsg[b] = n;
 }
 
