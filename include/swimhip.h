@@ -56,7 +56,8 @@ extern "C" {
 
 /* flags */
 #define SWIM_FLAG_RECORD_EVENTS 1u /* keep full event records for swim_drain_events (hashes are always kept) */
-#define SWIM_FLAG_PROFILE 2u       /* time the main kernels with HIP events on the engine stream (swim_counters *_ns) */
+#define SWIM_FLAG_PROFILE 2u       /* time k_sync_diff with HIP events on the engine stream (swim_counters diff_ns) */
+#define SWIM_FLAG_PROFILE_ALL 4u   /* also time k_member_tick and k_gossip_send (member_ns, gossip_ns); ~10 % slower */
 
 typedef struct swim_config {
   uint32_t n_members;

@@ -466,10 +466,11 @@ int swim_step(swim_handle* h, uint32_t n) {
   if (!h) return SWIM_EINVAL;
   hipSetDevice((int)h->cfg.device);
   if (h->tick + n >= (1ull << 28)) return SWIM_ECAPACITY;  // deadlines are stored in 29 bits
-  const bool profile = (h->cfg.flags & SWIM_FLAG_PROFILE) != 0;
+  const bool profile = (h->cfg.flags & (SWIM_FLAG_PROFILE | SWIM_FLAG_PROFILE_ALL)) != 0;
   if (profile)
     while (h->prof.size() < n) {
       TickEvents te;
+      te.all = (h->cfg.flags & SWIM_FLAG_PROFILE_ALL) ? 1 : 0;
       for (auto& e : te.ev) HIPCK(hipEventCreate((hipEvent_t*)&e));
       h->prof.push_back(te);
     }
@@ -488,7 +489,7 @@ int swim_step(swim_handle* h, uint32_t n) {
       HIPCK(hipEventSynchronize(h->ev_member));
       if (h->hflag[0] != 0 || h->no_skip) {
         launch_gossip(d, k, h->stream, te);
-      } else if (te) {
+      } else if (te && te->all) {
         HIPCK(hipEventRecord((hipEvent_t)te->ev[4], h->stream));
         HIPCK(hipEventRecord((hipEvent_t)te->ev[5], h->stream));
       }
@@ -512,6 +513,7 @@ int swim_step(swim_handle* h, uint32_t n) {
         h->prof_ms[0] += ms;
         h->prof_diff_launches++;
       }
+      if (!h->prof[i].all) continue;
       HIPCK(hipEventElapsedTime(&ms, (hipEvent_t)h->prof[i].ev[2], (hipEvent_t)h->prof[i].ev[3]));
       h->prof_ms[1] += ms;
       HIPCK(hipEventElapsedTime(&ms, (hipEvent_t)h->prof[i].ev[4], (hipEvent_t)h->prof[i].ev[5]));

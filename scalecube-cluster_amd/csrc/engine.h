@@ -165,6 +165,7 @@ __host__ __device__ __forceinline__ uint32_t shard_of(uint32_t N, uint32_t W, ui
 // optional per-tick timing of the three main kernels (HIP events on the engine's stream)
 struct TickEvents {
   void* ev[6];  // hipEvent_t: diff start/stop, member start/stop, gossip-send start/stop
+  int all;      // 0: only the diff pair is recorded (each timed event costs ~5 us of stream time)
 };
 
 // host-side kernel launchers (one HIP stream)

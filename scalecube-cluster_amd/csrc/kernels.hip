@@ -731,9 +731,9 @@ void launch_diff(const Dev& d, uint32_t k, void* stream, const TickEvents* prof)
 
 void launch_member(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
   hipStream_t st = (hipStream_t)stream;
-  if (prof) hipEventRecord((hipEvent_t)prof->ev[2], st);
+  if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[2], st);
   hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k);
-  if (prof) hipEventRecord((hipEvent_t)prof->ev[3], st);
+  if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[3], st);
   hipLaunchKernelGGL(k_tick_flag, dim3(1), dim3(64), 0, st, d, k);
 }
 
@@ -743,9 +743,9 @@ void launch_gossip(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(k_gossip_active, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, st, d, d.active, d.nactive);
   hipLaunchKernelGGL(k_gossip_contacts, dim3(cdiv((uint64_t)d.NL * d.F, 256)), dim3(256), 0, st, d, k);
-  if (prof) hipEventRecord((hipEvent_t)prof->ev[4], st);
+  if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[4], st);
   hipLaunchKernelGGL(k_gossip_send, dim3(1024), dim3(256), 0, st, d.self, k, d.active, d.nactive);
-  if (prof) hipEventRecord((hipEvent_t)prof->ev[5], st);
+  if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[5], st);
   hipLaunchKernelGGL(k_gossip_apply, dim3(1024), dim3(256), 0, st, d, k);
   launch_receipt_routing(d, st);
   hipLaunchKernelGGL(k_gossip_free, dim3(1024), dim3(256), 0, st, d, d.active, d.nactive);
@@ -770,9 +770,9 @@ void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
   if (k > 0) launch_sync_diff(d, pb, st);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
-  if (prof) hipEventRecord((hipEvent_t)prof->ev[2], st);
+  if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[2], st);
   hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k);
-  if (prof) hipEventRecord((hipEvent_t)prof->ev[3], st);
+  if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[3], st);
   hipLaunchKernelGGL(k_sync_route, dim3(cdiv(d.MSGCAP, 256)), dim3(256), 0, st, d, b);
   hipLaunchKernelGGL(k_sync_dirty, dim3(512, d.W), dim3(256), 0, st, d, b);
   hipLaunchKernelGGL(k_pack_a, dim3(d.W), dim3(256), 0, st, d, b);
@@ -785,15 +785,15 @@ void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   hipLaunchKernelGGL(k_unpack_a, dim3(64, d.W), dim3(256), 0, st, d, k);
   hipLaunchKernelGGL(k_msgs_commit, dim3(64), dim3(256), 0, st, d, b);
   if (!gossip) {  // no gossip slot in use on any shard: nothing to send, deliver or recycle; no exchange B
-    if (prof) hipEventRecord((hipEvent_t)prof->ev[4], st);
-    if (prof) hipEventRecord((hipEvent_t)prof->ev[5], st);
+    if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[4], st);
+    if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[5], st);
     return;
   }
   hipLaunchKernelGGL(k_gossip_active, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, st, d, d.active, d.nactive);
   hipLaunchKernelGGL(k_gossip_contacts, dim3(cdiv((uint64_t)d.NL * d.F, 256)), dim3(256), 0, st, d, k);
-  if (prof) hipEventRecord((hipEvent_t)prof->ev[4], st);
+  if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[4], st);
   hipLaunchKernelGGL(k_gossip_send, dim3(1024), dim3(256), 0, st, d.self, k, d.active, d.nactive);
-  if (prof) hipEventRecord((hipEvent_t)prof->ev[5], st);
+  if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[5], st);
   hipLaunchKernelGGL(k_pack_b, dim3(64, d.W), dim3(256), 0, st, d);
 }
 

@@ -17,6 +17,7 @@ INIT_PRECONVERGED = 1
 MODE_FULL = 0
 FLAG_RECORD_EVENTS = 1
 FLAG_PROFILE = 2
+FLAG_PROFILE_ALL = 4
 
 EV_ADDED, EV_REMOVED, EV_UPDATED = 0, 1, 2
 META_NONE = 0xFFFFFFFF
