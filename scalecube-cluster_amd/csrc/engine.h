@@ -113,6 +113,7 @@ struct Dev {
   uint32_t* m_head; // [2][N] first message of msgs[b] to each destination, NEVER if none (reset by the consumer)
   uint32_t* pending_inc; // [N] swim_update_incarnation requests for the next tick's P0
   uint32_t* next_evt; // [N] earliest tick at which a pending path / subscription / fetch needs the member
+  uint32_t *busy, *nbusy; // members that need the full control path this tick, per block of 256 (k_member_triage)
   uint32_t* chunk_meta;                      // [MSGCAP][NCHUNK][2] (pool offset, count)
   uint64_t* pool;                            // candidate (subject << 34 | key)
   uint32_t* pool_used;

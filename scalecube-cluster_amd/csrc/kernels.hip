@@ -6,6 +6,7 @@
 namespace swim {
 
 __global__ void k_member_tick(const Dev* __restrict__ dp, uint32_t k);  // member.hip
+__global__ void k_member_triage(const Dev* __restrict__ dp, uint32_t k);
 // shard.hip
 __global__ void k_sync_route(Dev d, uint32_t b);
 __global__ void k_sync_dirty(Dev d, uint32_t b);
@@ -732,6 +733,7 @@ void launch_diff(const Dev& d, uint32_t k, void* stream, const TickEvents* prof)
 void launch_member(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
   hipStream_t st = (hipStream_t)stream;
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[2], st);
+  hipLaunchKernelGGL(k_member_triage, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k);
   hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[3], st);
   hipLaunchKernelGGL(k_tick_flag, dim3(1), dim3(64), 0, st, d, k);
@@ -771,6 +773,7 @@ void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   if (k > 0) launch_sync_diff(d, pb, st);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[2], st);
+  hipLaunchKernelGGL(k_member_triage, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k);
   hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[3], st);
   hipLaunchKernelGGL(k_sync_route, dim3(cdiv(d.MSGCAP, 256)), dim3(256), 0, st, d, b);

@@ -536,37 +536,46 @@ __device__ __forceinline__ void merge_payload(ML& L, uint32_t mi, uint32_t reaso
   }
 }
 
-__device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint32_t k, unsigned long long (&cnt)[8]) {
+// Triage (k_member_triage): the idle fast path. Most members have nothing due in most ticks (a ping every 10 ticks,
+// a SYNC every 300); they only advance an empty gossip round here. Returns whether the member needs the full
+// control path of k_member_tick this tick.
+__device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t k) {
   // A dead member does nothing itself, but the remote hops of its in-flight requests still run at the live
   // responders (their sends fail against the dead issuer), so those hops are still evaluated for the counters.
-  const bool dead = dead_at(d, m, k);
+  // every word is loaded up front (no short-circuit chain of dependent loads); the SoA loads coalesce per wave
+  const uint32_t mh = d.m_head[(size_t)((k - 1) & 1) * d.N + m], rc = d.rc_cnt[m], pi = d.pending_inc[m],
+                 ne = d.next_evt[m], tm = d.timerMin[m], np = d.nextPing[m], ns = d.nextSync[m], inf = d.initFlags[m],
+                 ng = d.nextGossip[m], held = d.held[m], dt = d.dead_tick[m];
+  const bool dead = k >= dt;
   if (dead) {
     d.rc_cnt[m] = 0;
     d.rc_fill[m] = 0;
     if (k > 0) d.m_head[(size_t)((k - 1) & 1) * d.N + m] = NEVER;
   } else {
-    // idle fast path: most members have nothing due in most ticks (a ping every 10 ticks, a SYNC every 300)
-    uint32_t mh = k > 0 ? d.m_head[(size_t)((k - 1) & 1) * d.N + m] : NEVER;
-    bool busy = mh != NEVER || d.rc_cnt[m] != 0 || d.pending_inc[m] || d.next_evt[m] <= k || d.timerMin[m] <= k || k == d.nextPing[m] ||
-                k == d.nextSync[m] || (d.initFlags[m] & INIT_ACTIVE) || (k == 0 && d.init_mode == 0);
+    const bool busy = (k > 0 && mh != NEVER) | (rc != 0) | (pi != 0) | (ne <= k) | (tm <= k) | (k == np) | (k == ns) |
+                      ((inf & INIT_ACTIVE) != 0) | (k == 0 && d.init_mode == 0);
     if (!busy) {
-      uint32_t ng = d.nextGossip[m];
       if (k != ng) {
         d.tround[m] = 0;
-        return;
+        return false;
       }
-      if (d.held[m] == 0) {  // doSpreadGossip with no gossips: period++ only (GossipProtocolImpl.java:141-146)
+      if (held == 0) {  // doSpreadGossip with no gossips: period++ only (GossipProtocolImpl.java:141-146)
         d.gPeriod[m]++;
         d.nextGossip[m] = ng + d.gossip_t;
         d.tround[m] = 0;
-        return;
+        return false;
       }
     }
   }
   if (dead && d.npath[m] == 0 && d.nfetch[m] == 0) {
     d.tround[m] = 0;
-    return;
+    return false;
   }
+  return true;
+}
+
+__device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint32_t k, unsigned long long (&cnt)[8]) {
+  const bool dead = dead_at(d, m, k);
   ML L;
   L.d = &d;
   L.m = m;
@@ -1003,12 +1012,31 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   for (int i = 0; i < 8; ++i) cnt[i] += L.c[i];
 }
 
+// One thread per owned member: the idle fast path, and per block of 256 members a compact list of those that need
+// the full path (block-local ballot prefix, no atomics: one counter shared by 1.5k waves serialised at L2), so the
+// heavy kernel runs only ~1/3 of the waves and none of them mostly idle.
+__global__ void __launch_bounds__(256) k_member_triage(const Dev* __restrict__ dp, uint32_t k) {
+  const Dev& d = *dp;
+  __shared__ uint32_t wc[4];
+  const uint32_t m = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
+  const bool busy = m < d.hi && member_triage(d, m, k);
+  const uint64_t bal = __ballot(busy);
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) wc[w] = (uint32_t)__popcll(bal);
+  __syncthreads();
+  uint32_t base = 0;
+  for (uint32_t j = 0; j < w; ++j) base += wc[j];
+  if (busy) d.busy[(size_t)blockIdx.x * 256 + base + __popcll(bal & ((1ull << lane) - 1ull))] = m;
+  if (threadIdx.x == 0) d.nbusy[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
+}
+
 // Counters are summed across the wave first: 10^4 pingers per tick adding to one word would serialise on that address.
 __global__ void __launch_bounds__(256) k_member_tick(const Dev* __restrict__ dp, uint32_t k) {
   const Dev& d = *dp;  // global, not kernarg: taking its address must not copy ~1 KB into per-lane scratch
-  uint32_t m = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t nb = d.nbusy[blockIdx.x];
+  if ((threadIdx.x & ~63u) >= nb) return;  // whole wave past this block's busy list
   unsigned long long cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (m < d.hi) member_tick_body(d, m, k, cnt);
+  if (threadIdx.x < nb) member_tick_body(d, d.busy[(size_t)blockIdx.x * 256 + threadIdx.x], k, cnt);
   const uint32_t lane = threadIdx.x & 63;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
