@@ -18,6 +18,7 @@
 // them "spec-pinned", not reference-pinned.
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -171,6 +172,7 @@ struct Member {
 };
 
 struct Sim {
+  FILE* send_log = nullptr;  // debugging aid: SWIMREF_SEND_LOG=<path> lists every counted gossip send
   swim_config cfg;
   uint32_t N = 0;
   uint32_t ping_t = 0, pingTimeout_t = 0, gossip_t = 0, sync_t = 0, syncTimeout_t = 0, md_t = 0, lat = 1;
@@ -540,7 +542,9 @@ void Member::do_spread_gossip(uint64_t k) {
       if (g.infPeriod + sp < period) continue;
       if (g.infected.count(t)) continue;
       s.ctr.gossip_messages++;
-      if (s.lost_gossip(id, t, k, slot, kv.first)) continue;  // gossip losses are not counted (SEMANTICS.md §8)
+      const bool lost = s.lost_gossip(id, t, k, slot, kv.first);
+      if (s.send_log) fprintf(s.send_log, "S %llu %u %llu %u %d\n", (unsigned long long)k, id, (unsigned long long)kv.first, t, lost ? 1 : 0);
+      if (lost) continue;  // gossip losses are not counted (SEMANTICS.md §8)
       Msg m;
       m.kind = K_GOSSIP;
       m.src = id;
@@ -554,10 +558,12 @@ void Member::do_spread_gossip(uint64_t k) {
   }
   uint64_t sw = s.sweep_of(cluster);
   for (auto it = gossips.begin(); it != gossips.end();) {
-    if (period > it->second.infPeriod + sw)
+    if (period > it->second.infPeriod + sw) {
+      if (s.send_log) fprintf(s.send_log, "W %llu %u %llu\n", (unsigned long long)k, id, (unsigned long long)it->first);
       it = gossips.erase(it);
-    else
+    } else {
       ++it;
+    }
   }
 }
 
@@ -737,6 +743,7 @@ void Member::process(uint64_t k, std::vector<Msg>& inbox) {
   // ---- P4 gossip (onGossipReq :171-183) ----
   std::sort(gm.begin(), gm.end(), [](Msg* a, Msg* b) { return a->gid != b->gid ? a->gid < b->gid : a->src < b->src; });
   for (Msg* m : gm) {
+    if (s.send_log) fprintf(s.send_log, "R %llu %u %u %llu %d\n", (unsigned long long)k, id, m->src, (unsigned long long)m->gid, gossips.count(m->gid) ? 0 : 1);
     if (!gossips.count(m->gid)) {
       GState g;
       g.subj = m->g_subj;
@@ -870,6 +877,7 @@ __attribute__((visibility("default"))) int swim_create(const swim_config* cfg, s
   if (c.ping_timeout_ms >= c.ping_interval_ms) return SWIM_EINVAL;  // ClusterConfig.java:413-415
   if (c.gossip_fanout == 0 || c.gossip_fanout > 8 || c.n_seeds > 16) return SWIM_EINVAL;
   auto* h = new swim_handle();
+  if (const char* lp = getenv("SWIMREF_SEND_LOG")) h->sim.send_log = fopen(lp, "w");
   Sim& s = h->sim;
   s.cfg = c;
   s.N = c.n_members;
@@ -935,6 +943,7 @@ __attribute__((visibility("default"))) int swim_create(const swim_config* cfg, s
 }
 
 __attribute__((visibility("default"))) int swim_destroy(swim_handle* h) {
+  if (h && h->sim.send_log) fclose(h->sim.send_log);
   delete h;
   return SWIM_OK;
 }

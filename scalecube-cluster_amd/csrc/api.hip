@@ -199,6 +199,11 @@ int build(swim_handle* h) {
   A(d.m_next, 2ull * d.MSGCAP) A(d.m_head, 2 * N) A(d.next_evt, N) A(d.busy, (NL + 255) / 256 * 256) A(d.nbusy, (NL + 255) / 256) A(d.pending_inc, N) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
   A(d.pool, d.POOLCAP) A(d.pool_used, 1)
   A(d.ev, (uint64_t)d.EVCAP * 8) A(d.ev_n, 1) A(d.ctr, C_NCTR) A(d.err, 8)
+  if (getenv("SWIM_SEND_LOG")) {  // debugging aid: every counted gossip send
+    d.dbg_send_cap = (uint32_t)atoi(getenv("SWIM_SEND_LOG"));
+    A(d.dbg_send, 5ull * d.dbg_send_cap) A(d.dbg_send_n, 1)
+    HIPCK(hipMemsetAsync(d.dbg_send_n, 0, 4, h->stream));
+  }
   if (d.W > 1) {
     d.MW = (d.NCHUNK + 63) / 64;
     d.NSCAP = 1u << 16;
@@ -701,6 +706,19 @@ int swim_counters_get(swim_handle* h, swim_counters* out) {
 }
 
 const char* swim_last_error(swim_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+// debugging aid (not part of the ABI header): the gossip send log of SWIM_SEND_LOG (tick, sender, gid lo/hi, target)
+int swimdbg_send_log(swim_handle* h, uint32_t* out, size_t cap, size_t* n) {
+  if (!h || !h->d.dbg_send) return SWIM_EINVAL;
+  HIPCK(hipStreamSynchronize(h->stream));
+  uint32_t cnt = 0;
+  HIPCK(hipMemcpy(&cnt, h->d.dbg_send_n, 4, hipMemcpyDeviceToHost));
+  cnt = std::min<uint32_t>(cnt, h->d.dbg_send_cap);
+  cnt = (uint32_t)std::min<size_t>(cnt, cap);
+  HIPCK(hipMemcpy(out, h->d.dbg_send, 20ull * cnt, hipMemcpyDeviceToHost));
+  *n = cnt;
+  return SWIM_OK;
+}
 
 // debugging aid (not part of the ABI header): the scalar fields folded into the "misc" state-hash word
 int swimdbg_scalars(swim_handle* h, uint32_t m, uint64_t* out) {

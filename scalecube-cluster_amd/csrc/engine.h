@@ -125,6 +125,9 @@ struct Dev {
   uint32_t* err;            // [8] bits, info...
   const Dev* self;          // device-resident copy of this struct (kernels index it through a pointer)
   uint32_t* hflag;          // host-mapped: [0] gossip slots in use after this tick's member control (W == 1)
+  uint32_t* dbg_send;       // debugging aid (SWIM_SEND_LOG=cap): [cap][5] tick, sender, gid lo, gid hi, target
+  uint32_t* dbg_send_n;
+  uint32_t dbg_send_cap;
 
   // ---- row sharding (W > 1) ----
   // This shard owns observers [lo, hi): their rows, lists, subscriptions, paths, fetches and groups are stored

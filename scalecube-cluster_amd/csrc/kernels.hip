@@ -389,6 +389,21 @@ __device__ uint32_t inc_at(const Dev& d, uint32_t member, uint32_t g, uint64_t g
   return NEVER;
 }
 
+// Was x's incarnation of a gossip created at tick cs swept (sweepGossips :283-308) in one of x's rounds at ticks
+// [cs, t)? The window check alone is not enough: the spread is recomputed from the gossip list every round, so a
+// list that shrinks (members removed during a partition) and grows back reopens the window of a gossip already swept.
+// The ring holds every round in that range: the window at t bounds t - cs to ~spread rounds, LOGW >= 4 (spread + 2).
+__device__ bool swept_before(const Dev& d, uint32_t x, uint32_t cs, uint32_t t) {
+  const uint32_t infP = rounds_before(d, x, cs);
+  for (uint32_t e = 0; e < d.LOGW; ++e) {
+    const size_t li = (size_t)x * d.LOGW + e;
+    const uint32_t tr = d.log_tick[li];
+    if (tr == NEVER || tr < cs || tr >= t) continue;
+    if (rounds_before(d, x, tr) > infP + 2u * (d.log_spread[li] + 1u)) return true;
+  }
+  return false;
+}
+
 __device__ __noinline__ bool blocked_pair(const Dev& d, uint32_t x, uint32_t y, uint32_t g, uint64_t gid,
                                           uint32_t tau, uint32_t cx) {
   const uint32_t lat = d.lat;
@@ -439,6 +454,7 @@ __device__ __noinline__ bool blocked_pair(const Dev& d, uint32_t x, uint32_t y, 
       uint32_t cs = cinc[i];
       uint32_t snd = c.dir == 0 ? y : x;
       if (cs == NEVER || rounds_before(d, snd, cs) + c.spread < rounds_before(d, snd, c.tick)) continue;
+      if (swept_before(d, snd, cs, c.tick)) continue;
       uint32_t sin = 1 - rin;
       if (lo_in[sin] == NEVER || cs < lo_in[sin]) {
         lo_in[sin] = cs;
@@ -466,6 +482,7 @@ __device__ __noinline__ bool blocked_pair(const Dev& d, uint32_t x, uint32_t y, 
     uint32_t cs = inc_at(d, snd, g, gid, c.tick);
     if (cs == NEVER) continue;
     if (rounds_before(d, snd, cs) + c.spread < rounds_before(d, snd, c.tick)) continue;
+    if (swept_before(d, snd, cs, c.tick)) continue;  // x no longer held it
     // the receiver delivered g to the sender during that incarnation: infectedFrom (isInfected :247)
     uint32_t od = 1 - c.dir;  // opposite direction
     bool blocked = false;
@@ -528,6 +545,17 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
         uint32_t t = d.T[(size_t)m * d.F + s];
         if (d.tcontact[(size_t)m * d.F + s] && blocked_pair(d, m, t, g, gid, k, c)) continue;  // isInfected (:247)
         sends++;
+        if (d.dbg_send) {
+          uint32_t di = atomicAdd(d.dbg_send_n, 1u);
+          if (di < d.dbg_send_cap) {
+            uint32_t* r = d.dbg_send + (size_t)di * 5;
+            r[0] = k;
+            r[1] = m;
+            r[2] = (uint32_t)gid;
+            r[3] = (uint32_t)(gid >> 32);
+            r[4] = t;
+          }
+        }
         uint32_t et = Sg[t];
         bool potential = !s_held(et);
         if (!potential && d.tround[t]) {  // t sweeps g in its own round this tick -> a delivery re-creates it

@@ -1,0 +1,77 @@
+"""Golden scenarios: the configs the fixtures in this directory were recorded on.
+
+Each scenario is a list of actions on a SimulatedCluster-like object. The recorder (make_golden.py) runs them on the
+CPU oracle and stores, after every period: a digest of the per-member state hashes, the deterministic op counters,
+and a digest of that period's MembershipEvents; for C1 the full event list too. tests/test_golden.py replays them on
+the oracle (CPU) and on libswimhip (GPU) and requires identical records.
+"""
+import hashlib
+
+import numpy as np
+
+from swimhip import ClusterConfig, SimConfig, _abi
+
+COUNTERS = ["record_compares", "row_writes", "messages", "gossip_messages", "events", "messages_lost",
+            "gossips_created", "sync_merges"]
+
+
+def _c1():
+    cfg = SimConfig(n_members=64, cluster=ClusterConfig(seedMembers=[0]), init_mode=_abi.INIT_COLD_JOIN,
+                    record_events=True)
+    return cfg, [("periods", 10), ("kill", 63), ("periods", 60)]
+
+
+def _c2_small():  # C2-shaped: preconverged, 5 % loss on every link, reduced N
+    return SimConfig(n_members=300, record_events=True), [("loss", 5), ("periods", 12)]
+
+
+def _c4_small():  # C4-shaped: two groups blocked both ways, healed later; seed 0 is in group A
+    n = 48
+    g = [0] * (n // 2) + [1] * (n // 2)
+    return SimConfig(n_members=n, cluster=ClusterConfig(seedMembers=[0]), record_events=True), [
+        ("partition", g), ("periods", 34), ("unblock", None), ("periods", 40)]
+
+
+def _c3_small():  # C3-shaped: steady state SYNC / SYNC_ACK anti-entropy, no loss
+    return SimConfig(n_members=1000), [("periods", 35)]
+
+
+SCENARIOS = {"c1": _c1, "c2_small": _c2_small, "c4_small": _c4_small, "c3_small": _c3_small}
+FULL_EVENTS = {"c1"}
+
+
+def digest(a):
+    return hashlib.blake2b(np.ascontiguousarray(a).tobytes(), digest_size=16).hexdigest()
+
+
+def event_rows(evs):
+    return [[e.tick, e.observer, e.seq, {"ADDED": 0, "REMOVED": 1, "UPDATED": 2}[e.type], e.member,
+             -1 if e.oldMetadata is None else e.oldMetadata, -1 if e.newMetadata is None else e.newMetadata] for e in evs]
+
+
+def record(c, name):
+    """Run scenario `name` on cluster c (already created from the scenario's SimConfig); return the record."""
+    cfg, actions = SCENARIOS[name]()
+    out = {"periods": [], "events": [] if name in FULL_EVENTS else None}
+    period = 0
+    for what, arg in actions:
+        if what == "periods":
+            for _ in range(arg):
+                c.run_periods(1)
+                period += 1
+                ctr = c.counters()
+                rows = event_rows(c.events()) if cfg.record_events else []
+                if out["events"] is not None:
+                    out["events"].extend(rows)
+                out["periods"].append({"period": period, "state": digest(c.state_hash()),
+                                       "counters": [int(ctr[k]) for k in COUNTERS],
+                                       "events": digest(np.array(rows, dtype=np.int64).reshape(-1, 7))})
+        elif what == "kill":
+            c.kill(arg)
+        elif what == "loss":
+            c.set_default_loss(arg)
+        elif what == "partition":
+            c.partition(np.array(arg, dtype=np.uint32))
+        elif what == "unblock":
+            c.unblock_all()
+    return out
