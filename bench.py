@@ -45,7 +45,7 @@ def parse():
     p.add_argument("--loss", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-members", type=int, default=10_000)
-    p.add_argument("--cpu-periods", type=int, default=10)
+    p.add_argument("--cpu-periods", type=int, default=60)
     p.add_argument("--transport", choices=["rccl", "host"], default="rccl", help="N>1 shard exchange")
     p.add_argument("--no-events", action="store_true", help="no per-kernel HIP events (roofline unavailable)")
     p.add_argument("--rehearse-one-gpu", action="store_true",

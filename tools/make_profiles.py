@@ -1,0 +1,55 @@
+"""Copy a round's GPU profile outputs into profiles/ and summarise the k_sync_diff PMC passes.
+
+FETCH_SIZE / WRITE_SIZE are in KB per dispatch; on gfx950 FETCH_SIZE counts wide coalesced streaming reads at half
+(MI355X_MICROARCH.md, HBM / rocprofv3 section), so it is doubled. Launches of the first two ticks (empty message
+lists) are dropped; the median of the rest is the steady-state traffic per launch."""
+import csv
+import json
+import shutil
+import statistics
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+src = ROOT / "gpurun_out" / "round"
+tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+prof = ROOT / "profiles"
+
+
+def values(path):
+    rows = list(csv.DictReader(open(path)))
+    v = [float(r["Counter_Value"]) for r in rows if "k_sync_diff" in r["Kernel_Name"]]
+    return [x for x in v if x > 1000.0]  # steady-state launches (the first ticks carry no SYNC payloads)
+
+
+fetch = values(next((src / "pmc_fetch").rglob("*counter_collection.csv")))
+write = values(next((src / "pmc_write").rglob("*counter_collection.csv")))
+stats = next((src / "trace").rglob("*kernel_stats.csv"))
+avg_us = None
+for r in csv.DictReader(open(stats)):
+    if "k_sync_diff" in r["Name"]:
+        avg_us = float(r["AverageNs"]) / 1e3
+bench = json.loads((src / "bench.json").read_text())
+n = bench["config"]["members"]
+fm, wm = statistics.median(fetch), statistics.median(write)
+out = {
+    "round": int(tag[1:]),
+    "members": n,
+    "kernel": "k_sync_diff",
+    "workload": "C3 steady state, bench.py --steps 3 --warmup 1",
+    "fetch_size_kb_median": fm,
+    "write_size_kb_median": wm,
+    "gfx950_fetch_correction": "FETCH_SIZE x2 (MI355X_MICROARCH.md HBM section: wide coalesced reads are tallied at half)",
+    "bytes_per_launch": 2 * fm * 1024 + wm * 1024,
+    "algorithmic_bytes_per_launch": bench["roofline"]["algorithmic_bytes_per_launch"],
+    "rocprof_avg_duration_us": avg_us,
+    "bench_hip_event_avg_us": bench["roofline"]["avg_launch_us"],
+    "source_files": [f"{tag}_pmc_fetch_size_sync_diff.csv", f"{tag}_pmc_write_size_sync_diff.csv",
+                     f"{tag}_kernel_stats_c3_100k.csv"],
+}
+(prof / "pmc_sync_diff.json").write_text(json.dumps(out, indent=1))
+shutil.copy(next((src / "pmc_fetch").rglob("*counter_collection.csv")), prof / f"{tag}_pmc_fetch_size_sync_diff.csv")
+shutil.copy(next((src / "pmc_write").rglob("*counter_collection.csv")), prof / f"{tag}_pmc_write_size_sync_diff.csv")
+shutil.copy(stats, prof / f"{tag}_kernel_stats_c3_100k.csv")
+(prof / f"{tag}_bench_c3_100k.json").write_text((src / "bench.json").read_text())
+print(json.dumps(out, indent=1))
