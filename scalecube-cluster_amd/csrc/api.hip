@@ -43,6 +43,7 @@ struct swim_handle {
   double xchg_ms = 0;                 // host time spent in the exchanges
   bool xflag = false;                 // last exchange: some shard has a gossip slot in use
   volatile uint32_t* hflag = nullptr; // host-mapped flag word written by k_tick_flag (W == 1)
+  unsigned long long* xi_host_h = nullptr;  // host side of Dev::xi_host
   hipEvent_t ev_member = nullptr;
   bool no_skip = getenv("SWIM_NO_GOSSIP_SKIP") != nullptr;  // debugging aid: always run the gossip data plane
   bool no_pipe = getenv("SWIM_NO_PIPELINE") != nullptr;    // debugging aid: no early SYNC diff of the next tick
@@ -225,6 +226,9 @@ int build(swim_handle* h) {
     HIPCK(hipMemsetAsync(d.xa_rcnt, 0, 8ull * d.W, h->stream));
     HIPCK(hipMemsetAsync(d.xb_rcnt, 0, 8ull * d.W, h->stream));
     HIPCK(hipHostMalloc((void**)&h->hcnt, 16ull * d.W, hipHostMallocDefault));
+    A(d.xi_send, (uint64_t)d.W * XINL) A(d.xi_recv, (uint64_t)d.W * XINL)
+    HIPCK(hipHostMalloc((void**)&h->xi_host_h, 16ull * d.W, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCK(hipHostGetDevicePointer((void**)&d.xi_host, (void*)h->xi_host_h, 0));
     if (h->spec.transport == SWIM_TRANSPORT_HOST) {
       h->hsend.resize(d.W * std::max(d.XA_PEER, d.XB_PEER));
       h->hrecv.resize(d.W * std::max(d.XA_PEER, d.XB_PEER));
@@ -284,31 +288,43 @@ int exchange(swim_handle* h, uint8_t* send, uint8_t* recv, uint64_t cap, unsigne
   unsigned long long* hc = h->hcnt;
   auto t0 = std::chrono::steady_clock::now();
   if (h->spec.transport == SWIM_TRANSPORT_RCCL) {
-    if (ncclAllToAll(scnt, rcnt, 1, ncclUint64, h->comm, st) != ncclSuccess) {
-      h->err = "ncclAllToAll (exchange byte counts) failed";
+    // one fixed-size all-to-all (count word + the first XINL - 8 bytes of each region), one host read of the
+    // count words through mapped memory, and a send/recv group only for regions that did not fit
+    launch_inline_out(h->d, send, cap, scnt, st);
+    if (ncclAllToAll(h->d.xi_send, h->d.xi_recv, XINL, ncclUint8, h->comm, st) != ncclSuccess) {
+      h->err = "ncclAllToAll (inline exchange) failed";
       return SWIM_EDEVICE;
     }
-    HIPCK(hipMemcpyAsync(hc, scnt, 8ull * W, hipMemcpyDeviceToHost, st));
-    HIPCK(hipMemcpyAsync(hc + W, rcnt, 8ull * W, hipMemcpyDeviceToHost, st));
-    HIPCK(hipStreamSynchronize(st));
+    launch_inline_in(h->d, recv, cap, scnt, rcnt, st);
+    HIPCK(hipEventRecord(h->ev_member, st));
+    HIPCK(hipEventSynchronize(h->ev_member));
+    volatile unsigned long long* xh = h->d.xi_host;
+    for (uint32_t q = 0; q < 2 * W; ++q) hc[q] = xh[q];
     h->xflag = false;
-    for (uint32_t q = 0; q < 2 * W; ++q) h->xflag |= (hc[q] & XFLAG_GOSSIP) != 0;
-    for (uint32_t q = 0; q < W; ++q)
-      if ((hc[q] & XCNT_MASK) > cap || (hc[W + q] & XCNT_MASK) > cap) {
+    bool rest = false;
+    for (uint32_t q = 0; q < 2 * W; ++q) {
+      h->xflag |= (hc[q] & XFLAG_GOSSIP) != 0;
+      rest |= (hc[q] & XCNT_MASK) > XINL - 8;
+      if ((hc[q] & XCNT_MASK) > cap) {
         h->err = "exchange block larger than its region";
         return SWIM_ECAPACITY;
       }
-    bool ok = ncclGroupStart() == ncclSuccess;
-    for (uint32_t q = 0; q < W && ok; ++q) {
-      if (q == me) continue;
-      const uint64_t sb = hc[q] & XCNT_MASK, rb = hc[W + q] & XCNT_MASK;
-      if (sb) ok &= ncclSend(send + (size_t)q * cap, sb, ncclUint8, (int)q, h->comm, st) == ncclSuccess;
-      if (rb) ok &= ncclRecv(recv + (size_t)q * cap, rb, ncclUint8, (int)q, h->comm, st) == ncclSuccess;
     }
-    ok &= ncclGroupEnd() == ncclSuccess;
-    if (!ok) {
-      h->err = "RCCL send/recv group failed";
-      return SWIM_EDEVICE;
+    if (rest) {
+      bool ok = ncclGroupStart() == ncclSuccess;
+      for (uint32_t q = 0; q < W && ok; ++q) {
+        if (q == me) continue;
+        const uint64_t sb = hc[q] & XCNT_MASK, rb = hc[W + q] & XCNT_MASK;
+        if (sb > XINL - 8)
+          ok &= ncclSend(send + (size_t)q * cap + XINL - 8, sb - (XINL - 8), ncclUint8, (int)q, h->comm, st) == ncclSuccess;
+        if (rb > XINL - 8)
+          ok &= ncclRecv(recv + (size_t)q * cap + XINL - 8, rb - (XINL - 8), ncclUint8, (int)q, h->comm, st) == ncclSuccess;
+      }
+      ok &= ncclGroupEnd() == ncclSuccess;
+      if (!ok) {
+        h->err = "RCCL send/recv group failed";
+        return SWIM_EDEVICE;
+      }
     }
   } else {
     HIPCK(hipMemcpyAsync(hc, scnt, 8ull * W, hipMemcpyDeviceToHost, st));
@@ -461,6 +477,7 @@ int swim_destroy(swim_handle* h) {
   if (h->comm) ncclCommDestroy(h->comm);
   if (h->hcnt) hipHostFree(h->hcnt);
   if (h->hflag) hipHostFree((void*)h->hflag);
+  if (h->xi_host_h) hipHostFree(h->xi_host_h);
   if (h->ev_member) hipEventDestroy(h->ev_member);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;

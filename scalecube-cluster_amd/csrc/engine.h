@@ -36,6 +36,7 @@ constexpr uint32_t RRW = 12;              // words per gossip-round record: m, c
 constexpr uint32_t NSW = 8;               // words per new-gossip-slot record
 // exchange byte-count words: low 48 bits = bytes; bit 62 = the sender has gossip slots in use this tick
 constexpr unsigned long long XCNT_MASK = (1ull << 48) - 1, XFLAG_GOSSIP = 1ull << 62;
+constexpr uint32_t XINL = 16384;  // RCCL: bytes per peer moved by the fixed-size all-to-all (count word + region head)
 
 // counters (swim_counters order after .tick)
 enum Ctr { C_R = 0, C_W, C_M, C_G, C_E, C_LOST, C_GCREATED, C_SYNCMERGE, C_NCTR = 16 };
@@ -151,6 +152,8 @@ struct Dev {
   uint64_t* rx_off;    // [RXCAP] byte offset (in xa_recv) of the first shipped chunk of a received payload
   uint8_t *xa_send, *xa_recv, *xb_send, *xb_recv;  // [W][X*_PEER]
   unsigned long long *xa_scnt, *xa_rcnt, *xb_scnt, *xb_rcnt;  // [W] bytes per peer region
+  uint8_t *xi_send, *xi_recv;    // [W][XINL] inline all-to-all blocks
+  unsigned long long* xi_host;   // host-mapped [2W]: send and receive count words of the last exchange
 };
 
 // local index of an observer owned by this shard
@@ -185,6 +188,9 @@ void launch_gossip(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
 void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr);
 void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool gossip);
 void launch_tick_c(const Dev& d, uint32_t k, void* stream, bool gossip);
+void launch_inline_out(const Dev& d, const uint8_t* send, uint64_t cap, const unsigned long long* scnt, void* stream);
+void launch_inline_in(const Dev& d, uint8_t* recv, uint64_t cap, const unsigned long long* scnt, unsigned long long* rcnt,
+                      void* stream);
 void launch_kill(const Dev& d, uint32_t member, void* stream);
 void launch_hash(const Dev& d, uint64_t* out, uint32_t now, void* stream);
 

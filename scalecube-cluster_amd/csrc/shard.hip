@@ -292,4 +292,44 @@ __global__ void k_round_reset(Dev d) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < H[1]; i += gridDim.x * blockDim.x) d.tround[RR[(size_t)i * RRW]] = 0;
 }
 
+// RCCL exchange, fixed-size part: block q = the count word of region q followed by its first XINL - 8 bytes. The
+// all-to-all of these blocks needs no sizes on the host, and in the steady state carries the whole exchange.
+__global__ void __launch_bounds__(256) k_inline_out(const uint8_t* send, uint64_t cap, const unsigned long long* scnt,
+                                                    uint8_t* isend) {
+  const uint32_t q = blockIdx.x;
+  const unsigned long long w = scnt[q];
+  uint64_t* dst = (uint64_t*)(isend + (size_t)q * XINL);
+  if (threadIdx.x == 0) dst[0] = w;
+  const uint64_t n = min((uint64_t)(w & XCNT_MASK), (uint64_t)XINL - 8) / 8;  // regions are multiples of 8 B
+  const uint64_t* src = (const uint64_t*)(send + (size_t)q * cap);
+  for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) dst[1 + i] = src[i];
+}
+
+__global__ void __launch_bounds__(256) k_inline_in(const uint8_t* irecv, uint8_t* recv, uint64_t cap,
+                                                   const unsigned long long* scnt, unsigned long long* rcnt,
+                                                   unsigned long long* host, uint32_t W) {
+  const uint32_t p = blockIdx.x;
+  const uint64_t* src = (const uint64_t*)(irecv + (size_t)p * XINL);
+  const unsigned long long w = src[0];
+  const uint64_t n = min((uint64_t)(w & XCNT_MASK), (uint64_t)XINL - 8) / 8;
+  uint64_t* dst = (uint64_t*)(recv + (size_t)p * cap);
+  for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[1 + i];
+  if (threadIdx.x == 0) {
+    rcnt[p] = w;
+    host[p] = scnt[p];
+    host[W + p] = w;
+    __threadfence_system();
+  }
+}
+
+void launch_inline_out(const Dev& d, const uint8_t* send, uint64_t cap, const unsigned long long* scnt, void* stream) {
+  hipLaunchKernelGGL(k_inline_out, dim3(d.W), dim3(256), 0, (hipStream_t)stream, send, cap, scnt, d.xi_send);
+}
+
+void launch_inline_in(const Dev& d, uint8_t* recv, uint64_t cap, const unsigned long long* scnt, unsigned long long* rcnt,
+                      void* stream) {
+  hipLaunchKernelGGL(k_inline_in, dim3(d.W), dim3(256), 0, (hipStream_t)stream, d.xi_recv, recv, cap, scnt, rcnt,
+                     d.xi_host, d.W);
+}
+
 }  // namespace swim
