@@ -86,7 +86,8 @@ typedef struct swim_config {
   uint32_t event_cap;         /* buffered event records */
   uint32_t n_gpus;            /* 1 for now */
   uint32_t device;            /* first HIP device */
-  uint32_t reserved[7];
+  uint32_t list_slack;        /* FD / gossip list entries beyond N (duplicates after reordered ADDED / REMOVED) */
+  uint32_t reserved[6];
 } swim_config;
 
 typedef struct swim_event {
@@ -139,7 +140,13 @@ int swim_sync(swim_handle* h);                            /* wait for queued dev
 int swim_kill(swim_handle* h, uint32_t member);
 int swim_set_default_loss(swim_handle* h, uint32_t loss_percent);
 int swim_set_partition(swim_handle* h, const uint32_t* group_of_member); /* n_members entries */
-int swim_unblock_all(swim_handle* h);
+int swim_unblock_all(swim_handle* h); /* also clears every per-link setting (NetworkEmulator.unblockAll :186-192) */
+/* NetworkEmulator.setLinkSettings(destination, loss, 0) / block(destination) on member src's emulator (:97-150):
+ * a custom loss for messages src -> dst (100 = blocked) that replaces the default and partition settings for that link;
+ * swim_set_partition overwrites it on cross-group links, as block() does */
+int swim_set_link_loss(swim_handle* h, uint32_t src, uint32_t dst, uint32_t loss_percent);
+/* NetworkEmulator.unblock(destination) on member src's emulator (:158-175): back to the default settings */
+int swim_unblock_link(swim_handle* h, uint32_t src, uint32_t dst);
 /* MembershipProtocolImpl.updateIncarnation (:178-190): the member bumps its own incarnation and spreads it, at the
  * start (P0) of the next tick; what ClusterImpl.updateMetadata does after storing new metadata */
 int swim_update_incarnation(swim_handle* h, uint32_t member);

@@ -181,6 +181,7 @@ struct Sim {
   uint32_t loss = 0;
   bool partitioned = false;
   std::vector<uint32_t> group;
+  std::map<uint64_t, uint32_t> custom;  // NetworkEmulator.customLinkSettings: (src << 32 | dst) -> loss %
   std::vector<Member> members;
   std::vector<uint32_t> md_version;  // each member's own metadata version (GET_METADATA_RESP payload)
   std::vector<std::vector<Msg>> inflight;  // ring indexed by delivery tick % (lat+1)
@@ -195,20 +196,26 @@ struct Sim {
   uint32_t sweep_of(uint32_t cluster) const { return 2u * (spread_of(cluster) + 1u); }            // :99-102
 
   // NetworkEmulator.tryFail (transport/.../NetworkEmulator.java:231-248) + NetworkLinkSettings.evaluateLoss (:54-57)
-  bool blocked(uint32_t src, uint32_t dst) const {
-    if (!members[dst].alive) return true;
-    if (partitioned && group[src] != group[dst]) return true;
-    return false;
+  // getLinkSettings (:57-59): the custom setting of src's emulator for dst, else the default; a partition is the
+  // DEAD custom setting on every cross-group link. Returns the loss percent (100 for a dead destination).
+  uint32_t link_loss(uint32_t src, uint32_t dst) const {
+    if (!members[dst].alive) return 100;
+    if (!custom.empty()) {
+      auto it = custom.find(((uint64_t)src << 32) | dst);
+      if (it != custom.end()) return it->second;
+    }
+    if (partitioned && group[src] != group[dst]) return 100;
+    return loss;
   }
   bool lost(uint8_t kind, uint32_t src, uint32_t dst, uint64_t k, uint32_t aux, uint32_t id) const {
-    if (blocked(src, dst)) return true;
+    const uint32_t loss = link_loss(src, dst);
     if (loss == 0) return false;
     if (loss >= 100) return true;
     P4 r = philox4x32_10(src, dst, (uint32_t)k, id, seed_lo ^ (SALT_LOSS_BASE + kind), seed_hi ^ (aux * 0x9E3779B9u));
     return next_int(r.v[0], 100) < loss;
   }
   bool lost_gossip(uint32_t src, uint32_t dst, uint64_t k, uint32_t slot, uint64_t gid) const {
-    if (blocked(src, dst)) return true;
+    const uint32_t loss = link_loss(src, dst);
     if (loss == 0) return false;
     if (loss >= 100) return true;
     P4 r = philox4x32_10(src, (uint32_t)k ^ ((slot >> 2) << 31), (uint32_t)(gid >> 32), (uint32_t)gid,
@@ -983,11 +990,24 @@ __attribute__((visibility("default"))) int swim_set_partition(swim_handle* h, co
   }
   h->sim.group.assign(g, g + h->sim.N);
   h->sim.partitioned = true;
+  for (auto it = h->sim.custom.begin(); it != h->sim.custom.end();)  // block() overwrites cross-group custom settings
+    it = g[it->first >> 32] != g[(uint32_t)it->first] ? h->sim.custom.erase(it) : std::next(it);
   return SWIM_OK;
 }
 __attribute__((visibility("default"))) int swim_unblock_all(swim_handle* h) {
   if (!h) return SWIM_EINVAL;
   h->sim.partitioned = false;
+  h->sim.custom.clear();  // NetworkEmulator.unblockAll (:186-192)
+  return SWIM_OK;
+}
+__attribute__((visibility("default"))) int swim_set_link_loss(swim_handle* h, uint32_t src, uint32_t dst, uint32_t pct) {
+  if (!h || src >= h->sim.N || dst >= h->sim.N || pct > 100) return SWIM_EINVAL;
+  h->sim.custom[((uint64_t)src << 32) | dst] = pct;  // setLinkSettings / block (:97-150)
+  return SWIM_OK;
+}
+__attribute__((visibility("default"))) int swim_unblock_link(swim_handle* h, uint32_t src, uint32_t dst) {
+  if (!h || src >= h->sim.N || dst >= h->sim.N) return SWIM_EINVAL;
+  h->sim.custom.erase(((uint64_t)src << 32) | dst);  // unblock (:158-175)
   return SWIM_OK;
 }
 __attribute__((visibility("default"))) int swim_current_tick(swim_handle* h, uint64_t* t) {

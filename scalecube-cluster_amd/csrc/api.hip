@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -31,6 +32,9 @@ struct swim_handle {
   uint32_t loss = 0;
   bool partitioned = false;
   std::vector<uint32_t> group;
+  // per-link NetworkEmulator settings: current custom settings and each link's change history (mirrored to HBM)
+  std::map<uint64_t, uint32_t> link_cur;
+  std::map<uint64_t, std::vector<std::pair<uint32_t, uint32_t>>> link_hist;
   size_t bytes = 0;
   std::vector<TickEvents> prof;  // SWIM_FLAG_PROFILE: one event set per tick of the current swim_step
   double prof_ms[3] = {0, 0, 0};  // accumulated k_sync_diff, k_member_tick, k_gossip_send
@@ -118,6 +122,58 @@ int push_epoch(swim_handle* h) {
   return SWIM_OK;
 }
 
+// rebuild the device link table from the host history (fault calls are rare; the table is at most ~300 KB)
+int upload_links(swim_handle* h) {
+  const uint32_t now = (uint32_t)h->tick, look = h->d.LOOKBACK + 2 * h->d.ping_t + 16;
+  for (auto it = h->link_hist.begin(); it != h->link_hist.end();) {  // links back at default for long: forget them
+    const auto& v = it->second;
+    if (!h->link_cur.count(it->first) && v.back().second == LK_NONE && v.back().first + look < now)
+      it = h->link_hist.erase(it);
+    else
+      ++it;
+  }
+  if (h->link_hist.size() > LKCAP / 2) {
+    h->err = "more than 2048 links with custom NetworkEmulator settings";
+    return SWIM_ECAPACITY;
+  }
+  std::vector<uint64_t> keys(LKCAP, 0);
+  std::vector<uint32_t> hist((size_t)LKCAP * LKH * 2, LK_NONE);
+  for (const auto& kv : h->link_hist) {
+    uint32_t p = (uint32_t)mix64(kv.first) & (LKCAP - 1);
+    while (keys[p]) p = (p + 1) & (LKCAP - 1);
+    keys[p] = kv.first;
+    const auto& v = kv.second;
+    const size_t first = v.size() > LKH ? v.size() - LKH : 0;
+    for (size_t i = first; i < v.size(); ++i) {
+      hist[((size_t)p * LKH + (i - first)) * 2] = v[i].first;
+      hist[((size_t)p * LKH + (i - first)) * 2 + 1] = v[i].second;
+    }
+    if (first) hist[(size_t)p * LKH * 2] |= LK_TRUNC;
+  }
+  uint32_t n = (uint32_t)h->link_hist.size();
+  HIPCK(hipStreamSynchronize(h->stream));
+  HIPCK(hipMemcpy(h->d.link_key, keys.data(), 8ull * LKCAP, hipMemcpyHostToDevice));
+  HIPCK(hipMemcpy(h->d.link_hist, hist.data(), 4ull * hist.size(), hipMemcpyHostToDevice));
+  HIPCK(hipMemcpy(h->d.link_n, &n, 4, hipMemcpyHostToDevice));
+  return SWIM_OK;
+}
+
+// a change of link src -> dst effective from the next tick to run (NONE = back to the default settings)
+void link_change(swim_handle* h, uint64_t key, uint32_t v) {
+  auto& hv = h->link_hist[key];
+  const uint32_t now = (uint32_t)h->tick;
+  if (!hv.empty() && hv.back().first == now)
+    hv.back().second = v;
+  else
+    hv.emplace_back(now, v);
+  if (v == LK_NONE)
+    h->link_cur.erase(key);
+  else
+    h->link_cur[key] = v;
+}
+
+uint64_t link_key_of(uint32_t src, uint32_t dst) { return (((uint64_t)src << 32) | dst) + 1ull; }
+
 int build(swim_handle* h) {
   const swim_config& c = h->cfg;
   Dev& d = h->d;
@@ -154,7 +210,9 @@ int build(swim_handle* h) {
     if (!dup) d.seeds[d.n_seeds++] = s;
   }
   const uint64_t N = d.N;
-  d.LCAP = d.N + 64;
+  // FD / gossip lists: a member can be listed twice when its REMOVED overtakes the metadata fetch of its ADDED
+  // (emitMembershipEvent :543-588 is asynchronous), so the lists get slack beyond N - 1 entries
+  d.LCAP = d.N + (c.list_slack ? c.list_slack : 64);
   d.FCAP = c.pending_fetch_cap ? c.pending_fetch_cap : 256;
   d.GRCAP = c.init_mode == SWIM_INIT_COLD_JOIN ? std::min<uint32_t>(d.N + 16, 1024) : 32;
   uint32_t maxSpread = d.repeatMult * (32u - (uint32_t)__builtin_clz(d.LCAP + 1));
@@ -179,6 +237,7 @@ int build(swim_handle* h) {
   int rc;
 #define A(p, n)                                   \
   if ((rc = dalloc(h, &(p), (size_t)(n))) != 0) return rc;
+  A(d.link_n, 1) A(d.link_key, LKCAP) A(d.link_hist, (uint64_t)LKCAP * LKH * 2)
   A(d.dead_tick, N) A(d.ep_from, MAX_EPOCHS) A(d.ep_loss, MAX_EPOCHS) A(d.ep_part, MAX_EPOCHS)
   A(d.ep_group, MAX_EPOCHS * N) A(d.md_version, N)
   A(d.tsize, N) A(d.fdLen, N) A(d.gLen, N) A(d.fdPeriod, N) A(d.gPeriod, N) A(d.gCounter, N) A(d.nextPing, N)
@@ -244,6 +303,8 @@ int build(swim_handle* h) {
   HIPCK(hipMemsetAsync(d.arena_used, 0, 8, h->stream));
   HIPCK(hipMemsetAsync(d.tcnt, 0, N * 4, h->stream));
   HIPCK(hipMemsetAsync(d.pool_used, 0, 4, h->stream));
+  HIPCK(hipMemsetAsync(d.link_n, 0, 4, h->stream));
+  HIPCK(hipMemsetAsync(d.link_key, 0, 8ull * LKCAP, h->stream));
   HIPCK(hipMemsetAsync(d.nactive, 0, 4, h->stream));
   HIPCK(hipMemsetAsync(d.deliv_n, 0, 4, h->stream));
   HIPCK(hipMemsetAsync(d.rc_n, 0, 4, h->stream));
@@ -582,16 +643,47 @@ int swim_set_partition(swim_handle* h, const uint32_t* g) {
   if (g) {
     h->group.assign(g, g + h->d.N);
     h->partitioned = true;
+    // block() writes DEAD_LINK_SETTINGS over a custom setting of every cross-group link (NetworkEmulator.java:141-150)
+    std::vector<uint64_t> drop;
+    for (const auto& kv : h->link_cur) {
+      uint32_t src = (uint32_t)((kv.first - 1) >> 32), dst = (uint32_t)(kv.first - 1);
+      if (g[src] != g[dst]) drop.push_back(kv.first);
+    }
+    for (uint64_t key : drop) link_change(h, key, LK_NONE);
+    if (!drop.empty()) {
+      int rc = upload_links(h);
+      if (rc) return rc;
+    }
   } else {
     h->partitioned = false;
   }
   return push_epoch(h);
 }
 
-int swim_unblock_all(swim_handle* h) {
+int swim_unblock_all(swim_handle* h) {  // NetworkEmulator.unblockAll: customLinkSettings.clear() (:186-192)
   if (!h) return SWIM_EINVAL;
   h->partitioned = false;
+  if (!h->link_cur.empty()) {
+    std::vector<uint64_t> keys;
+    for (const auto& kv : h->link_cur) keys.push_back(kv.first);
+    for (uint64_t key : keys) link_change(h, key, LK_NONE);
+    int rc = upload_links(h);
+    if (rc) return rc;
+  }
   return push_epoch(h);
+}
+
+int swim_set_link_loss(swim_handle* h, uint32_t src, uint32_t dst, uint32_t pct) {
+  if (!h || src >= h->d.N || dst >= h->d.N || pct > 100) return SWIM_EINVAL;
+  link_change(h, link_key_of(src, dst), pct);
+  return upload_links(h);
+}
+
+int swim_unblock_link(swim_handle* h, uint32_t src, uint32_t dst) {
+  if (!h || src >= h->d.N || dst >= h->d.N) return SWIM_EINVAL;
+  if (!h->link_cur.count(link_key_of(src, dst))) return SWIM_OK;
+  link_change(h, link_key_of(src, dst), LK_NONE);
+  return upload_links(h);
 }
 
 int swim_current_tick(swim_handle* h, uint64_t* t) {

@@ -28,12 +28,40 @@ __device__ __forceinline__ int epoch_at(const Dev& d, uint32_t k) {
 
 __device__ __forceinline__ bool dead_at(const Dev& d, uint32_t x, uint32_t k) { return k >= d.dead_tick[x]; }
 
-// NetworkEmulator.tryFail (transport/.../NetworkEmulator.java:231-248) at the sender, evaluated for tick k:
-// a dead destination or a partition block fails the send; otherwise a loss draw unless loss is 0 or >= 100.
-__device__ __forceinline__ bool blocked_at(const Dev& d, int ep, uint32_t src, uint32_t dst, uint32_t k) {
-  if (dead_at(d, dst, k)) return true;
-  if (d.ep_part[ep] && d.ep_group[(size_t)ep * d.N + src] != d.ep_group[(size_t)ep * d.N + dst]) return true;
-  return false;
+// NetworkEmulator.getLinkSettings (:57-59): the custom setting of link src -> dst in force at tick k, or -1
+__device__ __noinline__ int link_loss_at(const Dev& d, uint32_t src, uint32_t dst, uint32_t k) {
+  const uint64_t key = (((uint64_t)src << 32) | dst) + 1ull;
+  for (uint32_t p = 0, h = (uint32_t)mix64(key) & (LKCAP - 1); p < LKCAP; ++p, h = (h + 1) & (LKCAP - 1)) {
+    const uint64_t kk = d.link_key[h];
+    if (kk == 0) return -1;
+    if (kk != key) continue;
+    const uint32_t* e = d.link_hist + (size_t)h * LKH * 2;
+    int best = -2;
+    for (uint32_t i = 0; i < LKH; ++i) {
+      const uint32_t from = (i == 0 ? e[0] & ~LK_TRUNC : e[2 * i]), v = e[2 * i + 1];
+      if (from == LK_NONE || from > k) break;
+      best = v == LK_NONE ? -1 : (int)v;
+    }
+    if (best == -2) {
+      if (e[0] & LK_TRUNC) set_err(d, E_LINKHIST);
+      return -1;
+    }
+    return best;
+  }
+  return -1;
+}
+
+// NetworkEmulator.tryFail (transport/.../NetworkEmulator.java:231-248) at the sender, evaluated for tick k: a dead
+// destination fails the send; then the link's custom setting if it has one (block = 100 %), else the partition
+// block and the default loss. Returns the loss percent to draw against, or 100 for a certain failure.
+__device__ __forceinline__ uint32_t link_loss(const Dev& d, int ep, uint32_t src, uint32_t dst, uint32_t k) {
+  if (dead_at(d, dst, k)) return 100;
+  if (*d.link_n) {
+    const int lp = link_loss_at(d, src, dst, k);
+    if (lp >= 0) return (uint32_t)lp;
+  }
+  if (d.ep_part[ep] && d.ep_group[(size_t)ep * d.N + src] != d.ep_group[(size_t)ep * d.N + dst]) return 100;
+  return d.ep_loss[ep];
 }
 
 __device__ __forceinline__ bool lost_msg(const Dev& d, uint32_t kind, uint32_t src, uint32_t dst, uint32_t k,
@@ -43,8 +71,7 @@ __device__ __forceinline__ bool lost_msg(const Dev& d, uint32_t kind, uint32_t s
     set_err(d, E_EPOCH);
     return true;
   }
-  if (blocked_at(d, ep, src, dst, k)) return true;
-  uint32_t loss = d.ep_loss[ep];
+  uint32_t loss = link_loss(d, ep, src, dst, k);
   if (loss == 0) return false;
   if (loss >= 100) return true;
   u32x4 r = philox(src, dst, k, id, d.seed_lo ^ (SALT_LOSS_BASE + kind), d.seed_hi ^ (aux * 0x9E3779B9u));
@@ -58,8 +85,7 @@ __device__ __forceinline__ bool lost_gossip(const Dev& d, uint32_t src, uint32_t
     set_err(d, E_EPOCH);
     return true;
   }
-  if (blocked_at(d, ep, src, dst, k)) return true;
-  uint32_t loss = d.ep_loss[ep];
+  uint32_t loss = link_loss(d, ep, src, dst, k);
   if (loss == 0) return false;
   if (loss >= 100) return true;
   u32x4 r = philox(src, k ^ ((slot >> 2) << 31), (uint32_t)(gid >> 32), (uint32_t)gid, d.seed_lo ^ SALT_LOSS_GOSSIP,

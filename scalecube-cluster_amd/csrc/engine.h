@@ -28,7 +28,10 @@ constexpr uint32_t S_TICK_MASK = (1u << 29) - 1u;
 constexpr uint32_t E_SLOTS = 1, E_FETCH = 2, E_SUBS = 4, E_PATHS = 8, E_GROUPS = 16, E_MSGS = 32, E_ARENA = 64,
                    E_POOL = 128, E_LIST = 256, E_DELIV = 512, E_RECEIPTS = 1024, E_CONTACTS = 2048,
                    E_REBORN = 4096, E_LOGWIN = 8192, E_EPOCH = 16384, E_EVENTS = 32768, E_SORTCAP = 65536,
-                   E_XCAP = 1u << 17;
+                   E_XCAP = 1u << 17, E_LINKHIST = 1u << 18;
+// per-link NetworkEmulator settings (setLinkSettings / block / unblock): hash of (src, dst) -> change history
+constexpr uint32_t LKCAP = 4096, LKH = 8;  // keys, history entries per key
+constexpr uint32_t LK_NONE = 0xFFFFFFFFu, LK_TRUNC = 0x80000000u;
 
 // row sharding: SyncMsg.payload values
 constexpr uint32_t PAY_RX = 0x40000000u;  // received from another shard: PAY_RX | rx index (dirty chunks + baseline)
@@ -63,6 +66,9 @@ struct Dev {
   uint32_t* ep_part;    // [MAX_EPOCHS] partition active
   uint32_t* ep_group;   // [MAX_EPOCHS][N]
   uint32_t* md_version; // [N]
+  uint32_t* link_n;     // [1] keys in the link table (0: no per-link setting was ever made)
+  uint64_t* link_key;   // [LKCAP] (src << 32 | dst) + 1, 0 = empty slot
+  uint32_t* link_hist;  // [LKCAP][LKH][2] (from tick, loss % or LK_NONE), oldest first; [0][0] | LK_TRUNC if older ones dropped
 
   // ---- per member scalars ----
   uint32_t *tsize, *fdLen, *gLen, *fdPeriod, *gPeriod, *gCounter, *nextPing, *nextGossip, *nextSync, *cidCnt, *syncSeq,

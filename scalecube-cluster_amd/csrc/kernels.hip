@@ -407,7 +407,8 @@ __device__ bool swept_before(const Dev& d, uint32_t x, uint32_t cs, uint32_t t) 
 __device__ __noinline__ bool blocked_pair(const Dev& d, uint32_t x, uint32_t y, uint32_t g, uint64_t gid,
                                           uint32_t tau, uint32_t cx) {
   const uint32_t lat = d.lat;
-  Contact ev[64];
+  constexpr uint32_t CMAX = 256;  // contact events between one pair inside the log window (small clusters: many)
+  Contact ev[CMAX];
   uint32_t n = 0;
   const uint32_t born = d.slot_ctick[g];  // no member could send g before it was created
   uint32_t oldest[2] = {0, 0};  // oldest tick still in each log, 0 if the ring never wrapped
@@ -424,7 +425,7 @@ __device__ __noinline__ bool blocked_pair(const Dev& d, uint32_t x, uint32_t y, 
       uint32_t cnt = d.log_cnt[li];
       for (uint32_t s2 = 0; s2 < cnt; ++s2)
         if (d.log_tg[li * d.F + s2] == to) {
-          if (n == 64) {
+          if (n == CMAX) {
             atomicOr(d.err, E_CONTACTS);
             return false;
           }
@@ -442,7 +443,7 @@ __device__ __noinline__ bool blocked_pair(const Dev& d, uint32_t x, uint32_t y, 
   // into x from cx on (the answer), and into a sender from its incarnation start for every relevant event
   // (its isInfected check). The fixpoint runs over at most 64 events. The ring must cover those ranges.
   uint32_t lo_in[2] = {cx, NEVER};  // [0]: deliveries into x, [1]: deliveries into y
-  uint32_t cinc[64];
+  uint32_t cinc[CMAX];
   for (uint32_t i = 0; i < n; ++i) cinc[i] = NEVER - 1;  // not computed yet
   for (int pass = 0; pass < 8; ++pass) {
     bool changed = false;
@@ -473,7 +474,7 @@ __device__ __noinline__ bool blocked_pair(const Dev& d, uint32_t x, uint32_t y, 
       d.err[5] = oldest[1];
     }
   }
-  uint32_t del[2][64];
+  uint32_t del[2][CMAX];
   uint32_t nd[2] = {0, 0};
   for (uint32_t i = 0; i < n; ++i) {
     const Contact& c = ev[i];

@@ -51,7 +51,8 @@ class SwimConfig(C.Structure):
         ("event_cap", C.c_uint32),
         ("n_gpus", C.c_uint32),
         ("device", C.c_uint32),
-        ("reserved", C.c_uint32 * 7),
+        ("list_slack", C.c_uint32),
+        ("reserved", C.c_uint32 * 6),
     ]
 
 
@@ -107,6 +108,8 @@ SIGNATURES = {
     "swim_set_default_loss": (C.c_int, [_H, C.c_uint32]),
     "swim_set_partition": (C.c_int, [_H, _U32P]),
     "swim_unblock_all": (C.c_int, [_H]),
+    "swim_set_link_loss": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.c_uint32]),
+    "swim_unblock_link": (C.c_int, [_H, C.c_uint32, C.c_uint32]),
     "swim_update_incarnation": (C.c_int, [_H, C.c_uint32]),
     "swim_current_tick": (C.c_int, [_H, C.POINTER(C.c_uint64)]),
     "swim_read_row": (C.c_int, [_H, C.c_uint32, C.POINTER(C.c_uint64), C.c_size_t]),

@@ -128,6 +128,20 @@ class SimulatedCluster:
     def unblock_all(self):
         self._ck(self.lib.swim_unblock_all(self._h), "swim_unblock_all")
 
+    def set_link_loss(self, src, dst, pct):
+        """NetworkEmulator.setLinkSettings on src's emulator for destination dst; 100 = block(dst)."""
+        self._ck(self.lib.swim_set_link_loss(self._h, src, dst, pct), "swim_set_link_loss")
+
+    def block(self, src, *dsts):
+        """NetworkEmulator.block(destinations) on src's emulator (NetworkEmulator.java:141-150)."""
+        for dst in dsts:
+            self.set_link_loss(src, dst, 100)
+
+    def unblock(self, src, *dsts):
+        """NetworkEmulator.unblock(destinations) on src's emulator (NetworkEmulator.java:158-175)."""
+        for dst in dsts:
+            self._ck(self.lib.swim_unblock_link(self._h, src, dst), "swim_unblock_link")
+
     # -- readback -------------------------------------------------------------------------------------------
     def row(self, observer) -> np.ndarray:
         out = np.zeros(self.n, dtype=np.uint64)

@@ -66,6 +66,7 @@ class SimConfig:
     gossip_slot_cap: int = 0
     pending_fetch_cap: int = 0
     event_cap: int = 0
+    list_slack: int = 0
     device: int = 0
 
     def to_abi(self):
@@ -99,4 +100,5 @@ class SimConfig:
         a.event_cap = self.event_cap
         a.n_gpus = 1
         a.device = self.device
+        a.list_slack = self.list_slack
         return a

@@ -239,6 +239,18 @@ class ThreadShardGroup:
         for s in self.shards:
             s.unblock_all()
 
+    def set_link_loss(self, src, dst, pct):
+        for s in self.shards:
+            s.set_link_loss(src, dst, pct)
+
+    def block(self, src, *dsts):
+        for s in self.shards:
+            s.block(src, *dsts)
+
+    def unblock(self, src, *dsts):
+        for s in self.shards:
+            s.unblock(src, *dsts)
+
     def update_incarnation(self, m):
         for s in self.shards:
             s.update_incarnation(m)

@@ -23,10 +23,10 @@ def schedule(seed):
           ClusterConfig.defaultLocalConfig().with_(seedMembers=[0, n // 2])][preset]
     cold = bool(rng.integers(2))
     cfg = SimConfig(n_members=n, cluster=cc, init_mode=_abi.INIT_COLD_JOIN if cold else _abi.INIT_PRECONVERGED,
-                    record_events=True, seed=int(rng.integers(1 << 31)))
+                    record_events=True, seed=int(rng.integers(1 << 31)), list_slack=4096, pending_fetch_cap=4096)
     acts = [("run", int(rng.integers(20, 60)))]
     for _ in range(int(rng.integers(4, 8))):
-        kind = rng.choice(["loss", "part2", "part3", "heal", "kill", "inc"])
+        kind = rng.choice(["loss", "part2", "part3", "heal", "kill", "inc", "link", "block", "unblock"])
         if kind == "loss":
             acts.append(("loss", int(rng.choice([0, 5, 20, 50]))))
         elif kind in ("part2", "part3"):
@@ -35,8 +35,15 @@ def schedule(seed):
             acts.append(("heal", None))
         elif kind == "kill":
             acts.append(("kill", int(rng.integers(1, n))))
-        else:
+        elif kind == "inc":
             acts.append(("inc", int(rng.integers(n))))
+        elif kind == "link":  # a handful of per-link loss settings (NetworkEmulator.setLinkSettings)
+            acts.append(("link", [(int(rng.integers(n)), int(rng.integers(n)), int(rng.choice([0, 30, 100])))
+                                  for _ in range(int(rng.integers(1, 6)))]))
+        elif kind == "block":  # one member's outbound links to a few others (NetworkEmulator.block)
+            acts.append(("block", (int(rng.integers(n)), [int(x) for x in rng.integers(n, size=3)])))
+        else:
+            acts.append(("unblock", (int(rng.integers(n)), [int(x) for x in rng.integers(n, size=3)])))
         acts.append(("run", int(rng.integers(20, 200))))
     return cfg, acts
 
@@ -60,11 +67,18 @@ def play(o, e, acts, where):
                 c.kill(arg)
             elif what == "inc":
                 c.update_incarnation(arg)
+            elif what == "link":
+                for src, dst, pct in arg:
+                    c.set_link_loss(src, dst, pct)
+            elif what == "block":
+                c.block(arg[0], *arg[1])
+            elif what == "unblock":
+                c.unblock(arg[0], *arg[1])
         if what == "kill":
             dead.add(arg)
 
 
-@pytest.mark.parametrize("seed", range(20))
+@pytest.mark.parametrize("seed", range(24))
 def test_fuzz_single_gpu(oracle, engine, seed):
     cfg, acts = schedule(seed)
     o, e = SimulatedCluster(oracle, cfg), SimulatedCluster(engine, cfg)

@@ -107,3 +107,30 @@ def test_kill_many_with_loss(oracle, engine):
         o.kill(victim)
         e.kill(victim)
     run_lockstep(o, e, 500, 50, "after kills")
+
+
+def test_asymmetric_blocks_and_link_loss(oracle, engine):
+    """FailureDetectorTest block matrices (:118-341) inside the full stack: one-directional blocks, per-link loss
+    over a default loss, a partition that overwrites custom settings, unblock of single links, unblockAll."""
+    n = 40
+    cfg = SimConfig(n_members=n, cluster=ClusterConfig(seedMembers=[0, 39]), record_events=True)
+    o, e = pair(oracle, engine, cfg)
+    for c in (o, e):
+        c.set_default_loss(5)
+        c.block(0, 1, 2, 3)
+        c.block(7, 30)
+        c.set_link_loss(5, 6, 60)
+        c.set_link_loss(9, 10, 0)
+    run_lockstep(o, e, 120, 20, "asymmetric")
+    g = np.array([0] * 20 + [1] * 20, dtype=np.uint32)
+    for c in (o, e):
+        c.partition(g)
+        c.set_link_loss(3, 25, 0)  # a custom setting made after the partition punches through it
+    run_lockstep(o, e, 200, 40, "partition + custom")
+    for c in (o, e):
+        c.unblock(0, 1, 2)
+        c.unblock(3, 25)
+    run_lockstep(o, e, 100, 25, "single unblocks")
+    for c in (o, e):
+        c.unblock_all()
+    run_lockstep(o, e, 200, 50, "unblockAll")

@@ -101,6 +101,63 @@ def test_fd_all_suspected(oracle):  # FailureDetectorTest.testSuspected: every l
         assert suspected(c, o) == sorted(set(range(3)) - {o})
 
 
+def test_fd_trusted_despite_bad_network(oracle):  # FailureDetectorTest.testTrustedDespiteBadNetwork (:118-146)
+    c = SimulatedCluster(oracle, fd_config(3))
+    c.block(0, 1)  # a.networkEmulator().block(b.address()): only a -> b is cut; ping-req through c covers it
+    c.step(ticks_for_seconds(2))
+    for o in range(3):
+        assert trusted(c, o) == [0, 1, 2]
+        assert suspected(c, o) == []
+
+
+def test_fd_suspected_member_with_normal_network(oracle):
+    # FailureDetectorTest.testSuspectedMemberWithNormalNetworkGetsPartitioned (:240-299): a, b, c block d (outbound
+    # only). d's pings reach them but every ack towards d is dropped, so d suspects all three and they suspect d.
+    c = SimulatedCluster(oracle, fd_config(4))
+    for src in (0, 1, 2):
+        c.block(src, 3)
+    c.step(ticks_for_seconds(1))
+    for o in (0, 1, 2):
+        assert 3 in suspected(c, o)
+    assert suspected(c, 3) == [0, 1, 2]
+    c.unblock_all()  # unblock d everywhere: the network recovers (:282-296)
+    c.step(ticks_for_seconds(3))
+    for o in range(4):
+        assert sorted(c.members(o)) == [0, 1, 2, 3] and suspected(c, o) == []
+
+
+def test_fd_member_status_change_after_network_recovery(oracle):
+    # FailureDetectorTest.testMemberStatusChangeAfterNetworkRecovery (:303-341): a and b block each other
+    c = SimulatedCluster(oracle, fd_config(2))
+    c.block(0, 1)
+    c.block(1, 0)
+    c.step(ticks_for_seconds(1))
+    assert suspected(c, 0) == [1] and suspected(c, 1) == [0]
+    c.unblock(0, 1)
+    c.unblock(1, 0)
+    c.step(ticks_for_seconds(2))
+    assert trusted(c, 0) == [0, 1] and trusted(c, 1) == [0, 1]
+
+
+def test_link_loss_overrides_default_and_partition(oracle):
+    """NetworkEmulator precedence: a link's custom setting replaces the default (:57-59); block() of a partition
+    overwrites custom settings on cross-group links (:141-150); unblockAll clears every custom setting (:186-192)."""
+    n = 6
+    c = SimulatedCluster(oracle, SimConfig(n_members=n))
+    c.set_default_loss(100)       # every default link is dead ...
+    c.set_link_loss(0, 1, 0)      # ... except the custom 0 -> 1 and 1 -> 0
+    c.set_link_loss(1, 0, 0)
+    c.run_periods(3)
+    ctr = c.counters()
+    assert ctr["messages_lost"] < ctr["messages"]
+    c.partition(np.array([0, 1, 0, 0, 0, 0], dtype=np.uint32))  # 0 and 1 now in different groups: custom dropped
+    c.set_default_loss(0)
+    before = c.counters()["messages_lost"]
+    c.run_periods(2)
+    assert c.counters()["messages_lost"] > before  # 1 is cut off from everyone
+    c.unblock_all()
+
+
 def test_kill_yields_removed_everywhere(oracle):  # ClusterTest.testShutdownCluster... (:306-373)
     n = 16
     c = SimulatedCluster(oracle, SimConfig(n_members=n, record_events=True))
