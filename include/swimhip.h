@@ -150,6 +150,10 @@ int swim_unblock_link(swim_handle* h, uint32_t src, uint32_t dst);
 /* MembershipProtocolImpl.updateIncarnation (:178-190): the member bumps its own incarnation and spreads it, at the
  * start (P0) of the next tick; what ClusterImpl.updateMetadata does after storing new metadata */
 int swim_update_incarnation(swim_handle* h, uint32_t member);
+/* ClusterImpl.shutdown -> MembershipProtocolImpl.leaveCluster (ClusterImpl.java:297-313, MembershipProtocolImpl.java:197-206):
+ * at the start (P0) of the next tick the member's own record becomes DEAD inc+1 and is spread as gossip; when that
+ * gossip is swept at the member (the leave Mono completes), the member stops as if killed, from the next tick */
+int swim_leave(swim_handle* h, uint32_t member);
 
 /* readback */
 int swim_current_tick(swim_handle* h, uint64_t* tick);

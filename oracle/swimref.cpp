@@ -143,6 +143,7 @@ struct Member {
 
   uint64_t nextPing = NEVER, nextGossip = NEVER, nextSync = NEVER;
   bool pendingInc = false;  // swim_update_incarnation, applied in P0 of the next tick
+  bool pendingLeave = false;  // swim_leave (leaveCluster), applied in P0 of the next tick after pendingInc
   uint32_t cidCnt = 0, syncSeq = 0, evSeq = 0;
   uint32_t sel[8] = {0};
   uint64_t evHash = 0;
@@ -182,6 +183,7 @@ struct Sim {
   bool partitioned = false;
   std::vector<uint32_t> group;
   std::map<uint64_t, uint32_t> custom;  // NetworkEmulator.customLinkSettings: (src << 32 | dst) -> loss %
+  std::vector<uint32_t> leaving_done;   // members whose leave completed this tick: stopped from the next tick
   std::vector<Member> members;
   std::vector<uint32_t> md_version;  // each member's own metadata version (GET_METADATA_RESP payload)
   std::vector<std::vector<Msg>> inflight;  // ring indexed by delivery tick % (lat+1)
@@ -566,6 +568,10 @@ void Member::do_spread_gossip(uint64_t k) {
   uint64_t sw = s.sweep_of(cluster);
   for (auto it = gossips.begin(); it != gossips.end();) {
     if (period > it->second.infPeriod + sw) {
+      // the leave notification swept at its origin: leaveCluster's Mono completes and ClusterImpl.doShutdown
+      // disposes the member and stops its transport (ClusterImpl.java:305-313, GossipProtocolImpl.java:296-306)
+      if ((uint32_t)(it->first >> 32) == id && it->second.subj == id && it->second.rec.st == DEAD)
+        s.leaving_done.push_back(id);
       if (s.send_log) fprintf(s.send_log, "W %llu %u %llu\n", (unsigned long long)k, id, (unsigned long long)it->first);
       it = gossips.erase(it);
     } else {
@@ -624,6 +630,13 @@ void Member::process(uint64_t k, std::vector<Msg>& inbox) {
   if (pendingInc) {  // updateIncarnation (MembershipProtocolImpl.java:178-190)
     pendingInc = false;
     Rec r{ALIVE, table[id].inc + 1};
+    table[id] = r;
+    s.ctr.row_writes++;
+    spread(id, r);
+  }
+  if (pendingLeave) {  // leaveCluster (MembershipProtocolImpl.java:197-206): own record DEAD inc+1, spread
+    pendingLeave = false;
+    Rec r{DEAD, table[id].inc + 1};
     table[id] = r;
     s.ctr.row_writes++;
     spread(id, r);
@@ -832,6 +845,11 @@ void Sim::run_tick() {
     for (auto& m : members) m.start(0);
   for (uint32_t i = 0; i < N; ++i)
     if (members[i].alive) members[i].process(k, inbox[i]);
+  for (uint32_t m : leaving_done) {  // as swim_kill between this tick and the next
+    members[m].alive = false;
+    members[m].gossips.clear();
+  }
+  leaving_done.clear();
   tick++;
   ctr.tick = tick;
 }
@@ -975,6 +993,11 @@ __attribute__((visibility("default"))) int swim_kill(swim_handle* h, uint32_t m)
 __attribute__((visibility("default"))) int swim_update_incarnation(swim_handle* h, uint32_t m) {
   if (!h || m >= h->sim.N || !h->sim.members[m].alive) return SWIM_EINVAL;
   h->sim.members[m].pendingInc = true;
+  return SWIM_OK;
+}
+__attribute__((visibility("default"))) int swim_leave(swim_handle* h, uint32_t m) {
+  if (!h || m >= h->sim.N || !h->sim.members[m].alive) return SWIM_EINVAL;
+  h->sim.members[m].pendingLeave = true;
   return SWIM_OK;
 }
 __attribute__((visibility("default"))) int swim_set_default_loss(swim_handle* h, uint32_t pct) {

@@ -253,10 +253,10 @@ int build(swim_handle* h) {
   A(d.slot_gid, d.SLOTS) A(d.slot_subj, d.SLOTS) A(d.slot_ctick, d.SLOTS) A(d.slot_key, d.SLOTS) A(d.slot_holders, d.SLOTS)
   A(d.slot_used, d.SLOTS) A(d.S, (uint64_t)d.SLOTS * N) A(d.free_list, d.SLOTS) A(d.free_top, 1)
   A(d.deliv, d.DCAP) A(d.deliv_n, 1) A(d.rc_raw, d.RCAP) A(d.rc_n, 1) A(d.rc_cnt, N) A(d.rc_off, N) A(d.rc_fill, N) A(d.scan_part, 1024)
-  A(d.rc_slot, d.RCAP) A(d.rc_key, d.RCAP) A(d.active, d.SLOTS) A(d.nactive, 1) A(d.hist, (uint64_t)d.HCAP * 6)
+  A(d.rc_slot, d.RCAP) A(d.rc_key, d.RCAP) A(d.active, d.SLOTS) A(d.nactive, 1) A(d.hist, (uint64_t)d.HCAP * HREC)
   A(d.msgs[0], d.MSGCAP) A(d.msgs[1], d.MSGCAP) A(d.nmsg, 2) A(d.arena[0], (uint64_t)d.ARENA_ROWS * d.NS)
   A(d.arena[1], (uint64_t)d.ARENA_ROWS * d.NS) A(d.arena_used, 2)
-  A(d.m_next, 2ull * d.MSGCAP) A(d.m_head, 2 * N) A(d.next_evt, N) A(d.busy, (NL + 255) / 256 * 256) A(d.nbusy, (NL + 255) / 256) A(d.pending_inc, N) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
+  A(d.m_next, 2ull * d.MSGCAP) A(d.m_head, 2 * N) A(d.deaths, 2ull * DEATHCAP) A(d.deaths_n, 2) A(d.next_evt, N) A(d.busy, (NL + 255) / 256 * 256) A(d.nbusy, (NL + 255) / 256) A(d.pending_inc, N) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
   A(d.pool, d.POOLCAP) A(d.pool_used, 1)
   A(d.ev, (uint64_t)d.EVCAP * 8) A(d.ev_n, 1) A(d.ctr, C_NCTR) A(d.err, 8)
   if (getenv("SWIM_SEND_LOG")) {  // debugging aid: every counted gossip send
@@ -296,13 +296,14 @@ int build(swim_handle* h) {
 #undef A
   HIPCK(hipMemsetAsync(d.S, 0, (size_t)d.SLOTS * N * 4, h->stream));
   HIPCK(hipMemsetAsync(d.ctr, 0, C_NCTR * 8, h->stream));
-  HIPCK(hipMemsetAsync(d.hist, 0, (size_t)d.HCAP * 48, h->stream));
+  HIPCK(hipMemsetAsync(d.hist, 0, (size_t)d.HCAP * HREC * 8, h->stream));
   HIPCK(hipMemsetAsync(d.err, 0, 32, h->stream));
   HIPCK(hipMemsetAsync(d.ev_n, 0, 4, h->stream));
   HIPCK(hipMemsetAsync(d.nmsg, 0, 8, h->stream));
   HIPCK(hipMemsetAsync(d.arena_used, 0, 8, h->stream));
   HIPCK(hipMemsetAsync(d.tcnt, 0, N * 4, h->stream));
   HIPCK(hipMemsetAsync(d.pool_used, 0, 4, h->stream));
+  HIPCK(hipMemsetAsync(d.deaths_n, 0, 8, h->stream));
   HIPCK(hipMemsetAsync(d.link_n, 0, 4, h->stream));
   HIPCK(hipMemsetAsync(d.link_key, 0, 8ull * LKCAP, h->stream));
   HIPCK(hipMemsetAsync(d.nactive, 0, 4, h->stream));
@@ -624,11 +625,28 @@ int swim_kill(swim_handle* h, uint32_t m) {
 int swim_update_incarnation(swim_handle* h, uint32_t m) {
   if (!h || m >= h->d.N) return SWIM_EINVAL;
   if (!owns(h, m)) return SWIM_OK;  // the owning shard bumps it; the others learn it from its gossip
-  uint32_t one = 1, dt = 0;
+  uint32_t req = 0, dt = 0;
   HIPCK(hipStreamSynchronize(h->stream));
   HIPCK(hipMemcpy(&dt, h->d.dead_tick + m, 4, hipMemcpyDeviceToHost));
   if (dt != NEVER) return SWIM_EINVAL;
-  HIPCK(hipMemcpy(h->d.pending_inc + m, &one, 4, hipMemcpyHostToDevice));
+  HIPCK(hipMemcpy(&req, h->d.pending_inc + m, 4, hipMemcpyDeviceToHost));
+  req |= 1u;
+  HIPCK(hipMemcpy(h->d.pending_inc + m, &req, 4, hipMemcpyHostToDevice));
+  return SWIM_OK;
+}
+
+// MembershipProtocolImpl.leaveCluster (:197-206) via ClusterImpl.shutdown -> doShutdown (:297-313): in P0 of the next
+// tick the member's own record becomes DEAD inc+1 and is spread; when that gossip is swept at the member, it stops
+int swim_leave(swim_handle* h, uint32_t m) {
+  if (!h || m >= h->d.N) return SWIM_EINVAL;
+  HIPCK(hipStreamSynchronize(h->stream));
+  uint32_t dt = 0, req = 0;
+  HIPCK(hipMemcpy(&dt, h->d.dead_tick + m, 4, hipMemcpyDeviceToHost));
+  if (dt != NEVER) return SWIM_EINVAL;
+  if (!owns(h, m)) return SWIM_OK;
+  HIPCK(hipMemcpy(&req, h->d.pending_inc + m, 4, hipMemcpyDeviceToHost));
+  req |= 2u;
+  HIPCK(hipMemcpy(h->d.pending_inc + m, &req, 4, hipMemcpyHostToDevice));
   return SWIM_OK;
 }
 

@@ -102,6 +102,20 @@ __device__ __forceinline__ uint32_t rounds_before(const Dev& d, uint32_t x, uint
 
 __device__ __forceinline__ uint32_t spread_of(const Dev& d, uint32_t cluster) { return d.repeatMult * bitlen(cluster); }
 
+// member m swept gossip slot g at tick k: if g is m's own leave notification, leaveCluster completes and
+// ClusterImpl.doShutdown stops the member (ClusterImpl.java:305-313, GossipProtocolImpl.java:296-306); it is dead
+// from tick k + 1 and its held gossips stop counting as held at the start of that tick's gossip plane
+__device__ __forceinline__ void on_sweep(const Dev& d, uint32_t g, uint32_t m, uint32_t k) {
+  if ((uint32_t)(d.slot_gid[g] >> 32) != m || d.slot_subj[g] != m || rec_status(d.slot_key[g]) != ST_DEAD) return;
+  d.dead_tick[m] = k + 1u;
+  const uint32_t b = k & 1u;
+  const uint32_t i = atomicAdd(&d.deaths_n[b], 1u);
+  if (i < DEATHCAP)
+    d.deaths[(size_t)b * DEATHCAP + i] = m;
+  else
+    atomicOr(d.err, E_DEATHS);
+}
+
 __device__ __forceinline__ uint32_t s_ctick(uint32_t e) { return (e & S_TICK_MASK) - 1u; }
 __device__ __forceinline__ bool s_ever(uint32_t e) { return (e & S_TICK_MASK) != 0; }
 __device__ __forceinline__ bool s_held(uint32_t e) { return (e & S_TICK_MASK) != 0 && !(e & S_SWEPT); }

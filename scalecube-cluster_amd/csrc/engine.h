@@ -28,9 +28,13 @@ constexpr uint32_t S_TICK_MASK = (1u << 29) - 1u;
 constexpr uint32_t E_SLOTS = 1, E_FETCH = 2, E_SUBS = 4, E_PATHS = 8, E_GROUPS = 16, E_MSGS = 32, E_ARENA = 64,
                    E_POOL = 128, E_LIST = 256, E_DELIV = 512, E_RECEIPTS = 1024, E_CONTACTS = 2048,
                    E_REBORN = 4096, E_LOGWIN = 8192, E_EPOCH = 16384, E_EVENTS = 32768, E_SORTCAP = 65536,
-                   E_XCAP = 1u << 17, E_LINKHIST = 1u << 18;
+                   E_XCAP = 1u << 17, E_LINKHIST = 1u << 18, E_DEATHS = 1u << 19;
 // per-link NetworkEmulator settings (setLinkSettings / block / unblock): hash of (src, dst) -> change history
 constexpr uint32_t LKCAP = 4096, LKH = 8;  // keys, history entries per key
+constexpr uint32_t DEATHCAP = 4096;        // completed leaves per tick
+// gossip incarnation history entry: 3 header words + HKEEP creation ticks of swept incarnations (small clusters
+// under loss re-infect a member with the same gossip many times: each late sender restarts the chain)
+constexpr uint32_t HREC = 11, HKEEP = 16;
 constexpr uint32_t LK_NONE = 0xFFFFFFFFu, LK_TRUNC = 0x80000000u;
 
 // row sharding: SyncMsg.payload values
@@ -109,7 +113,7 @@ struct Dev {
   uint32_t* rc_slot;  // [RCAP] sorted by member then gossip id
   uint64_t* rc_key;   // [RCAP] gossip id sort key
   uint32_t *active, *nactive;  // slots in use at the start of the gossip phase
-  uint64_t* hist;  // [HCAP][6] incarnation history: tag, gid, member | n << 32, 6 x u32 creation ticks
+  uint64_t* hist;  // [HCAP][HREC] incarnation history: tag, gid, member | n << 32, HKEEP x u32 creation ticks
 
   // ---- SYNC messages (double-buffered by tick parity) ----
   SyncMsg* msgs[2];
@@ -118,7 +122,8 @@ struct Dev {
   uint32_t* arena_used;  // [2]
   uint32_t* m_next; // [2][MSGCAP] next message of msgs[b] to the same destination
   uint32_t* m_head; // [2][N] first message of msgs[b] to each destination, NEVER if none (reset by the consumer)
-  uint32_t* pending_inc; // [N] swim_update_incarnation requests for the next tick's P0
+  uint32_t* pending_inc; // [N] host requests for the next tick's P0: 1 updateIncarnation, 2 leaveCluster
+  uint32_t *deaths, *deaths_n;  // [2][DEATHCAP], [2]: members whose leave completed at tick k (parity k & 1)
   uint32_t* next_evt; // [N] earliest tick at which a pending path / subscription / fetch needs the member
   uint32_t *busy, *nbusy; // members that need the full control path this tick, per block of 256 (k_member_triage)
   uint32_t* chunk_meta;                      // [MSGCAP][NCHUNK][2] (pool offset, count)

@@ -15,7 +15,7 @@ __global__ void k_pack_a_chunks(Dev d, uint32_t b);
 __global__ void k_unpack_a(Dev d, uint32_t k);
 __global__ void k_msgs_commit(Dev d, uint32_t b);
 __global__ void k_pack_b(Dev d);
-__global__ void k_unpack_b_sweeps(Dev d);
+__global__ void k_unpack_b_sweeps(Dev d, uint32_t k);
 __global__ void k_unpack_b_deliv(Dev d);
 __global__ void k_round_reset(Dev d);
 
@@ -347,7 +347,7 @@ __device__ void hist_push(const Dev& d, uint64_t gid, uint32_t member, uint32_t 
   uint64_t tag = hist_tag(gid, member);
   uint32_t mask = d.HCAP - 1;
   for (uint32_t p = 0; p < d.HCAP; ++p) {
-    unsigned long long* e = (unsigned long long*)(d.hist + (size_t)((tag + p) & mask) * 6);
+    unsigned long long* e = (unsigned long long*)(d.hist + (size_t)((tag + p) & mask) * HREC);
     unsigned long long old = atomicCAS(e, 0ull, (unsigned long long)tag);
     if (old != 0ull && old != tag) continue;
     if (old == 0ull) {
@@ -356,7 +356,7 @@ __device__ void hist_push(const Dev& d, uint64_t gid, uint32_t member, uint32_t 
     }
     uint32_t n = (uint32_t)(e[2] >> 32);  // total rebirths so far; the ring keeps the latest 6
     uint32_t* c = (uint32_t*)(e + 3);
-    c[n % 6] = cprev;
+    c[n % HKEEP] = cprev;
     e[2] = (uint64_t)member | ((uint64_t)(n + 1) << 32);
     return;
   }
@@ -373,17 +373,17 @@ __device__ uint32_t inc_at(const Dev& d, uint32_t member, uint32_t g, uint64_t g
   uint64_t tag = hist_tag(gid, member);
   uint32_t mask = d.HCAP - 1;
   for (uint32_t p = 0; p < d.HCAP; ++p) {
-    const uint64_t* h = d.hist + (size_t)((tag + p) & mask) * 6;
+    const uint64_t* h = d.hist + (size_t)((tag + p) & mask) * HREC;
     if (h[0] == 0) break;
     if (h[0] != tag || h[1] != gid || (uint32_t)h[2] != member) continue;
     uint32_t n = (uint32_t)(h[2] >> 32), best = NEVER, oldest = NEVER;
     const uint32_t* cc = (const uint32_t*)(h + 3);
-    uint32_t kept = n < 6 ? n : 6;
+    uint32_t kept = n < HKEEP ? n : HKEEP;
     for (uint32_t i = 0; i < kept; ++i) {
       if (cc[i] < oldest) oldest = cc[i];
       if (cc[i] <= tau && (best == NEVER || cc[i] > best)) best = cc[i];
     }
-    if (best == NEVER && n > 6 && tau < oldest) atomicOr(d.err, E_REBORN);  // an incarnation the ring dropped
+    if (best == NEVER && n > HKEEP && tau < oldest) atomicOr(d.err, E_REBORN);  // an incarnation the ring dropped
     return best;
   }
   return NEVER;
@@ -497,9 +497,14 @@ __device__ __noinline__ bool blocked_pair(const Dev& d, uint32_t x, uint32_t y, 
   return false;
 }
 
-__global__ void k_gossip_active(Dev d, uint32_t* active, uint32_t* nactive) {
+__global__ void k_gossip_active(Dev d, uint32_t k, uint32_t* active, uint32_t* nactive) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g < d.SLOTS && d.slot_used[g]) active[atomicAdd(nactive, 1u)] = g;
+  if (g >= d.SLOTS || !d.slot_used[g]) return;
+  // members stopped after their leave completed at tick k - 1 hold nothing any more (as k_kill)
+  const uint32_t pb = (k - 1) & 1u, nd = k > 0 ? min(d.deaths_n[pb], DEATHCAP) : 0u;
+  for (uint32_t i = 0; i < nd; ++i)
+    if (s_held(d.S[(size_t)g * d.N + d.deaths[(size_t)pb * DEATHCAP + i]])) atomicSub(&d.slot_holders[g], 1);
+  active[atomicAdd(nactive, 1u)] = g;
 }
 
 // contact flags: did target t = T[m][s] choose m in a logged round inside the look-back window?
@@ -579,6 +584,7 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
       atomicOr(&Sg[m], S_SWEPT);
       atomicSub(&d.held[m], 1u);
       atomicSub(&d.slot_holders[g], 1);
+      on_sweep(d, g, m, k);
       if (d.W > 1) {  // applied on the other shards from exchange B
         uint32_t i = atomicAdd(&d.xn[2], 1u);
         if (i < d.SWCAP)
@@ -706,6 +712,7 @@ __global__ void k_tick_flag(Dev d, uint32_t k) {
   *d.nactive = 0;
   *d.deliv_n = 0;
   *d.rc_n = 0;
+  d.deaths_n[(k + 1) & 1] = 0;
   d.hflag[0] = (uint32_t)((int32_t)d.SPR - *d.free_top);
   __threadfence_system();
 }
@@ -727,6 +734,7 @@ __global__ void k_tick_end(Dev d, uint32_t k) {
     *d.nactive = 0;
     *d.deliv_n = 0;
     *d.rc_n = 0;
+    d.deaths_n[(k + 1) & 1] = 0;
   }
 }
 
@@ -772,7 +780,7 @@ static void launch_receipt_routing(const Dev& d, hipStream_t st);
 
 void launch_gossip(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_gossip_active, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, st, d, d.active, d.nactive);
+  hipLaunchKernelGGL(k_gossip_active, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, st, d, k, d.active, d.nactive);
   hipLaunchKernelGGL(k_gossip_contacts, dim3(cdiv((uint64_t)d.NL * d.F, 256)), dim3(256), 0, st, d, k);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[4], st);
   hipLaunchKernelGGL(k_gossip_send, dim3(1024), dim3(256), 0, st, d.self, k, d.active, d.nactive);
@@ -821,7 +829,7 @@ void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
     if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[5], st);
     return;
   }
-  hipLaunchKernelGGL(k_gossip_active, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, st, d, d.active, d.nactive);
+  hipLaunchKernelGGL(k_gossip_active, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, st, d, k, d.active, d.nactive);
   hipLaunchKernelGGL(k_gossip_contacts, dim3(cdiv((uint64_t)d.NL * d.F, 256)), dim3(256), 0, st, d, k);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[4], st);
   hipLaunchKernelGGL(k_gossip_send, dim3(1024), dim3(256), 0, st, d.self, k, d.active, d.nactive);
@@ -835,7 +843,7 @@ void launch_tick_c(const Dev& d, uint32_t k, void* stream, bool gossip) {
     hipLaunchKernelGGL(k_tick_end, dim3(1), dim3(64), 0, st, d, k);
     return;
   }
-  hipLaunchKernelGGL(k_unpack_b_sweeps, dim3(64, d.W), dim3(256), 0, st, d);
+  hipLaunchKernelGGL(k_unpack_b_sweeps, dim3(64, d.W), dim3(256), 0, st, d, k);
   hipLaunchKernelGGL(k_unpack_b_deliv, dim3(64, d.W), dim3(256), 0, st, d);
   hipLaunchKernelGGL(k_gossip_apply, dim3(1024), dim3(256), 0, st, d, k);
   launch_receipt_routing(d, st);

@@ -618,14 +618,24 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   L.pend = NEVER;
   L.tround = 0;
 
-  // ---- P0 host requests: updateIncarnation (MembershipProtocolImpl.java:178-190) ----
-  if (!dead && d.pending_inc[m]) {
+  // ---- P0 host requests: updateIncarnation (MembershipProtocolImpl.java:178-190), then leaveCluster (:197-206) ----
+  const uint32_t preq = dead ? 0u : d.pending_inc[m];
+  if (preq) {
     d.pending_inc[m] = 0;
-    uint64_t v0 = L.row[m];
-    uint32_t ni = rec_inc(v0) + 1u;
-    row_put(L, m, (v0 & ~KEY_MASK) | rec_key(ST_ALIVE, ni));
-    L.c[C_W]++;
-    spread(L, m, ST_ALIVE, ni);
+    if (preq & 1u) {
+      uint64_t v0 = L.row[m];
+      uint32_t ni = rec_inc(v0) + 1u;
+      row_put(L, m, (v0 & ~KEY_MASK) | rec_key(ST_ALIVE, ni));
+      L.c[C_W]++;
+      spread(L, m, ST_ALIVE, ni);
+    }
+    if (preq & 2u) {  // the own record becomes DEAD inc+1 (the only DEAD record a table keeps) and is spread
+      uint64_t v0 = L.row[m];
+      uint32_t ni = rec_inc(v0) + 1u;
+      row_put(L, m, (v0 & ~KEY_MASK) | rec_key(ST_DEAD, ni));
+      L.c[C_W]++;
+      spread(L, m, ST_DEAD, ni);
+    }
   }
 
   // ---- P0 start: ClusterImpl.join0 -> MembershipProtocolImpl.start0 (:216-251), COLD_JOIN at tick 0 ----

@@ -249,7 +249,7 @@ __global__ void __launch_bounds__(256) k_pack_b(Dev d) {
 }
 
 // peers' sweeps first (sweepGossips :283-308), so that a delivery to a member that swept g this tick re-creates it
-__global__ void k_unpack_b_sweeps(Dev d) {
+__global__ void k_unpack_b_sweeps(Dev d, uint32_t k) {
   const uint32_t p = blockIdx.y;
   if (p == d.rank || (d.xb_rcnt[p] & XCNT_MASK) < 16) return;
   const uint8_t* R = d.xb_recv + (size_t)p * d.XB_PEER;
@@ -260,6 +260,7 @@ __global__ void k_unpack_b_sweeps(Dev d) {
     atomicOr(&d.S[(size_t)g * d.N + m], S_SWEPT);
     atomicSub(&d.held[m], 1u);
     atomicSub(&d.slot_holders[g], 1);
+    on_sweep(d, g, m, k);
   }
 }
 

@@ -111,6 +111,7 @@ SIGNATURES = {
     "swim_set_link_loss": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.c_uint32]),
     "swim_unblock_link": (C.c_int, [_H, C.c_uint32, C.c_uint32]),
     "swim_update_incarnation": (C.c_int, [_H, C.c_uint32]),
+    "swim_leave": (C.c_int, [_H, C.c_uint32]),
     "swim_current_tick": (C.c_int, [_H, C.POINTER(C.c_uint64)]),
     "swim_read_row": (C.c_int, [_H, C.c_uint32, C.POINTER(C.c_uint64), C.c_size_t]),
     "swim_state_hash": (C.c_int, [_H, C.POINTER(C.c_uint64), C.c_size_t]),

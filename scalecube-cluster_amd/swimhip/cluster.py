@@ -53,7 +53,7 @@ class MembershipRecord:
 
 
 _TYPES = {_abi.EV_ADDED: "ADDED", _abi.EV_REMOVED: "REMOVED", _abi.EV_UPDATED: "UPDATED"}
-_STATUS = {_abi.ST_ALIVE: "ALIVE", _abi.ST_SUSPECT: "SUSPECT"}
+_STATUS = {_abi.ST_ALIVE: "ALIVE", _abi.ST_SUSPECT: "SUSPECT", _abi.ST_DEAD: "DEAD"}  # DEAD: a leaving member's own
 
 
 def _meta(v):
@@ -127,6 +127,10 @@ class SimulatedCluster:
 
     def unblock_all(self):
         self._ck(self.lib.swim_unblock_all(self._h), "swim_unblock_all")
+
+    def leave(self, member):
+        """Cluster.shutdown(): graceful leave (MembershipProtocolImpl.leaveCluster, ClusterImpl.doShutdown)."""
+        self._ck(self.lib.swim_leave(self._h, member), "swim_leave")
 
     def set_link_loss(self, src, dst, pct):
         """NetworkEmulator.setLinkSettings on src's emulator for destination dst; 100 = block(dst)."""

@@ -239,6 +239,10 @@ class ThreadShardGroup:
         for s in self.shards:
             s.unblock_all()
 
+    def leave(self, m):
+        for s in self.shards:
+            s.leave(m)
+
     def set_link_loss(self, src, dst, pct):
         for s in self.shards:
             s.set_link_loss(src, dst, pct)

@@ -26,7 +26,7 @@ def schedule(seed):
                     record_events=True, seed=int(rng.integers(1 << 31)), list_slack=4096, pending_fetch_cap=4096)
     acts = [("run", int(rng.integers(20, 60)))]
     for _ in range(int(rng.integers(4, 8))):
-        kind = rng.choice(["loss", "part2", "part3", "heal", "kill", "inc", "link", "block", "unblock"])
+        kind = rng.choice(["loss", "part2", "part3", "heal", "kill", "inc", "link", "block", "unblock", "leave"])
         if kind == "loss":
             acts.append(("loss", int(rng.choice([0, 5, 20, 50]))))
         elif kind in ("part2", "part3"):
@@ -37,6 +37,8 @@ def schedule(seed):
             acts.append(("kill", int(rng.integers(1, n))))
         elif kind == "inc":
             acts.append(("inc", int(rng.integers(n))))
+        elif kind == "leave":
+            acts.append(("leave", int(rng.integers(1, n))))
         elif kind == "link":  # a handful of per-link loss settings (NetworkEmulator.setLinkSettings)
             acts.append(("link", [(int(rng.integers(n)), int(rng.integers(n)), int(rng.choice([0, 30, 100])))
                                   for _ in range(int(rng.integers(1, 6)))]))
@@ -54,7 +56,7 @@ def play(o, e, acts, where):
         if what == "run":
             run_lockstep(o, e, arg, max(10, arg // 3), where)
             continue
-        if what == "inc" and arg in dead:
+        if what in ("inc", "leave") and arg in dead:
             continue
         for c in (o, e):
             if what == "loss":
@@ -67,6 +69,8 @@ def play(o, e, acts, where):
                 c.kill(arg)
             elif what == "inc":
                 c.update_incarnation(arg)
+            elif what == "leave":
+                c.leave(arg)
             elif what == "link":
                 for src, dst, pct in arg:
                     c.set_link_loss(src, dst, pct)
@@ -74,7 +78,7 @@ def play(o, e, acts, where):
                 c.block(arg[0], *arg[1])
             elif what == "unblock":
                 c.unblock(arg[0], *arg[1])
-        if what == "kill":
+        if what in ("kill", "leave"):
             dead.add(arg)
 
 

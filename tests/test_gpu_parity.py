@@ -134,3 +134,23 @@ def test_asymmetric_blocks_and_link_loss(oracle, engine):
     for c in (o, e):
         c.unblock_all()
     run_lockstep(o, e, 200, 50, "unblockAll")
+
+
+def test_graceful_leaves(oracle, engine):
+    """Cluster.shutdown() -> leaveCluster: own DEAD record spread as gossip, REMOVED everywhere, the leaver stops when
+    its gossip is swept (ClusterImpl.java:297-313, MembershipProtocolImpl.java:197-206); under loss, one at a time
+    and two at once, plus an incarnation bump and a leave requested in the same tick."""
+    cfg = SimConfig(n_members=120, record_events=True)
+    o, e = pair(oracle, engine, cfg)
+    run_lockstep(o, e, 30, 10, "warm")
+    for c in (o, e):
+        c.leave(7)
+    run_lockstep(o, e, 60, 20, "leave 7")
+    for c in (o, e):
+        c.set_default_loss(10)
+        c.leave(8)
+        c.leave(90)
+        c.update_incarnation(91)
+        c.leave(91)
+    ev = run_lockstep(o, e, 400, 50, "leave 8, 90, 91 under loss")
+    assert {x.member for x in ev if x.isRemoved()} >= {8, 90, 91}

@@ -158,6 +158,22 @@ def test_link_loss_overrides_default_and_partition(oracle):
     c.unblock_all()
 
 
+def test_graceful_leave_yields_removed_everywhere(oracle):
+    """Cluster.shutdown() (ClusterImpl.java:297-313): leaveCluster spreads the member's own DEAD record; every other
+    member emits REMOVED long before a suspicion timeout could, and the leaver stops once its gossip is swept
+    (ClusterTest.testMembersAccessFromScheduler / testShutdownCluster shape, ClusterTest.java:306-373)."""
+    n = 16
+    c = SimulatedCluster(oracle, SimConfig(n_members=n, record_events=True))
+    c.run_periods(3)
+    c.leave(5)
+    c.run_periods(3)  # far below the 25-period suspicion timeout
+    ev = [e for e in c.events() if e.member == 5]
+    assert sorted(e.observer for e in ev if e.isRemoved()) == [o for o in range(n) if o != 5]
+    assert [r.status for r in c.records(5) if r.member == 5] == ["DEAD"]  # its own table keeps the DEAD record
+    c.run_periods(12)  # spread 3 * bitlen(16) = 15 rounds, swept after 32 rounds (6.4 s)
+    assert c.gossips(5) == []  # stopped: a stopped member holds nothing
+
+
 def test_kill_yields_removed_everywhere(oracle):  # ClusterTest.testShutdownCluster... (:306-373)
     n = 16
     c = SimulatedCluster(oracle, SimConfig(n_members=n, record_events=True))
