@@ -220,9 +220,11 @@ int build(swim_handle* h) {
   while (d.LOGW < 4 * (maxSpread + 2)) d.LOGW <<= 1;  // rounds kept for the infectedFrom replay
   d.LOOKBACK = d.LOGW * d.gossip_t;
   d.HCAP = 1u << 20;
-  uint64_t slots = c.gossip_slot_cap ? c.gossip_slot_cap : std::min<uint64_t>(65535, std::max<uint64_t>(1024, (1ull << 30) / (4 * N)));
+  // default: 64 slots per member, at most 32 GB of holder table (C2's SYNC re-spread storm keeps ~10^5 gossips alive)
+  uint64_t slots = c.gossip_slot_cap ? c.gossip_slot_cap
+                                     : std::min<uint64_t>(1ull << 22, std::max<uint64_t>(1024, std::min<uint64_t>(64 * N, (32ull << 30) / (4 * N))));
   // every shard allocates new gossips from its own slot range; the slot table itself is replicated
-  d.SPR = (uint32_t)std::min<uint64_t>(slots, 65535 / d.W);
+  d.SPR = (uint32_t)std::min<uint64_t>(slots, (1ull << 22) / d.W);
   d.SLOTS = d.SPR * d.W;
   uint64_t mc = N / d.sync_t * 4 + N / d.ping_t + 1024;
   if (c.init_mode == SWIM_INIT_COLD_JOIN) mc = std::max<uint64_t>(mc, N + 1024);
@@ -230,7 +232,7 @@ int build(swim_handle* h) {
   d.NCHUNK = (uint32_t)((d.NS + CH - 1) / CH);
   d.POOLCAP = (uint32_t)std::min<uint64_t>(1ull << 26, std::max<uint64_t>(1ull << 20, N * 64));
   d.EVCAP = c.event_cap ? c.event_cap : (1u << 20);
-  d.DCAP = (uint32_t)std::min<uint64_t>(1ull << 26, std::max<uint64_t>(1ull << 16, N * 512));
+  d.DCAP = (uint32_t)std::min<uint64_t>(1ull << 27, std::max<uint64_t>(1ull << 16, N * 16384));
   d.RCAP = d.DCAP;
   d.ARENA_ROWS = 64;
 
@@ -247,13 +249,13 @@ int build(swim_handle* h) {
   const uint64_t NL = d.NL;  // per-observer arrays: this shard's rows only
   A(d.row, NL * d.NS) A(d.fdl, NL * d.LCAP) A(d.gl, NL * d.LCAP)
   A(d.subs, NL * SUBCAP * 4) A(d.paths, NL * PATHCAP * 5) A(d.fetch, NL * d.FCAP * FREC) A(d.groups, NL * d.GRCAP * GREC)
-  A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F)
+  A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.cev, N * d.F * CEVW)
   A(d.log_tick, N * d.LOGW) A(d.log_spread, N * d.LOGW) A(d.log_cnt, N * d.LOGW) A(d.log_tg, N * d.LOGW * d.F)
   A(d.log_pos, N)
   A(d.slot_gid, d.SLOTS) A(d.slot_subj, d.SLOTS) A(d.slot_ctick, d.SLOTS) A(d.slot_key, d.SLOTS) A(d.slot_holders, d.SLOTS)
   A(d.slot_used, d.SLOTS) A(d.S, (uint64_t)d.SLOTS * N) A(d.free_list, d.SLOTS) A(d.free_top, 1)
   A(d.deliv, d.DCAP) A(d.deliv_n, 1) A(d.rc_raw, d.RCAP) A(d.rc_n, 1) A(d.rc_cnt, N) A(d.rc_off, N) A(d.rc_fill, N) A(d.scan_part, 1024)
-  A(d.rc_slot, d.RCAP) A(d.rc_key, d.RCAP) A(d.active, d.SLOTS) A(d.nactive, 1) A(d.hist, (uint64_t)d.HCAP * HREC)
+  A(d.rc_slot, d.RCAP) A(d.rc_key, d.RCAP) A(d.rc_slot2, d.RCAP) A(d.rc_key2, d.RCAP) A(d.active, d.SLOTS) A(d.nactive, 1) A(d.hist, (uint64_t)d.HCAP * HREC)
   A(d.msgs[0], d.MSGCAP) A(d.msgs[1], d.MSGCAP) A(d.nmsg, 2) A(d.arena[0], (uint64_t)d.ARENA_ROWS * d.NS)
   A(d.arena[1], (uint64_t)d.ARENA_ROWS * d.NS) A(d.arena_used, 2)
   A(d.m_next, 2ull * d.MSGCAP) A(d.m_head, 2 * N) A(d.deaths, 2ull * DEATHCAP) A(d.deaths_n, 2) A(d.next_evt, N) A(d.busy, (NL + 255) / 256 * 256) A(d.nbusy, (NL + 255) / 256) A(d.pending_inc, N) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)

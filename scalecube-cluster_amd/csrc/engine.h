@@ -32,6 +32,7 @@ constexpr uint32_t E_SLOTS = 1, E_FETCH = 2, E_SUBS = 4, E_PATHS = 8, E_GROUPS =
 // per-link NetworkEmulator settings (setLinkSettings / block / unblock): hash of (src, dst) -> change history
 constexpr uint32_t LKCAP = 4096, LKH = 8;  // keys, history entries per key
 constexpr uint32_t DEATHCAP = 4096;        // completed leaves per tick
+constexpr uint32_t CEV = 6, CEVW = 4 + 2 * CEV;  // cached contact events per (sender, target): n, oldest[2], events
 // gossip incarnation history entry: 3 header words + HKEEP creation ticks of swept incarnations (small clusters
 // under loss re-infect a member with the same gossip many times: each late sender restarts the chain)
 constexpr uint32_t HREC = 11, HKEEP = 16;
@@ -91,6 +92,7 @@ struct Dev {
 
   // ---- gossip round of the current tick ----
   uint32_t *tround, *tcnt, *tspread, *tperiod, *T, *tcontact;  // T, tcontact: [N][F]
+  uint32_t* cev;  // [N][F][CEVW] contact events of (m, T[m][s]) cached by k_gossip_contacts when tcontact is set
   uint32_t *log_tick, *log_spread, *log_cnt, *log_tg, *log_pos;  // [N][LOGW], tg [N][LOGW][F], pos [N]
 
   // ---- gossip slots ----
@@ -112,6 +114,8 @@ struct Dev {
   uint32_t* scan_part;                  // block partial sums of the exclusive scan
   uint32_t* rc_slot;  // [RCAP] sorted by member then gossip id
   uint64_t* rc_key;   // [RCAP] gossip id sort key
+  uint32_t* rc_slot2;  // [RCAP] merge scratch of k_seg_sort (segments above SORT_MAX)
+  uint64_t* rc_key2;
   uint32_t *active, *nactive;  // slots in use at the start of the gossip phase
   uint64_t* hist;  // [HCAP][HREC] incarnation history: tag, gid, member | n << 32, HKEEP x u32 creation ticks
 

@@ -174,51 +174,103 @@ __global__ void k_scan_add(uint32_t* out, const uint32_t* part, uint32_t n) {
   if (i < n) out[i] += part[i / 1024];
 }
 
-// per-segment sort of (key, val) by key: one block per segment, bitonic in LDS (<= 4096 entries)
+// per-segment sort of (key, val) by key (keys are unique within a segment): one block per segment. Segments of
+// up to SORT_MAX entries are sorted bitonically in LDS; larger ones (a member receiving thousands of new gossips in
+// one tick, C2-style storms) sort SORT_MAX runs in LDS and then merge run pairs through the scratch arrays, each
+// element finding its output position by a binary search in the partner run (merge path, no atomics).
 constexpr uint32_t SORT_MAX = 4096;
-__global__ void __launch_bounds__(256) k_seg_sort(uint64_t* key, uint32_t* val, const uint32_t* off, const uint32_t* cnt,
-                                                  uint32_t nseg, uint32_t* err, const uint32_t* nitems) {
+__device__ void lds_bitonic(uint64_t* K, uint32_t* V, const uint64_t* key, const uint32_t* val, uint32_t n,
+                            uint64_t* okey, uint32_t* oval) {
+  uint32_t p2 = 1;
+  while (p2 < n) p2 <<= 1;
+  for (uint32_t i = threadIdx.x; i < p2; i += blockDim.x) {
+    K[i] = i < n ? key[i] : ~0ull;
+    V[i] = i < n ? val[i] : 0;
+  }
+  __syncthreads();
+  for (uint32_t size = 2; size <= p2; size <<= 1)
+    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+      for (uint32_t i = threadIdx.x; i < p2; i += blockDim.x) {
+        uint32_t j = i ^ stride;
+        if (j > i) {
+          bool up = (i & size) == 0;
+          if ((K[i] > K[j]) == up) {
+            uint64_t tk = K[i];
+            K[i] = K[j];
+            K[j] = tk;
+            uint32_t tv = V[i];
+            V[i] = V[j];
+            V[j] = tv;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    okey[i] = K[i];
+    oval[i] = V[i];
+  }
+  __syncthreads();
+}
+
+// number of entries of the sorted run r[0..n) that are < x
+__device__ __forceinline__ uint32_t lower_rank(const uint64_t* r, uint32_t n, uint64_t x) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (r[mid] < x)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+__global__ void __launch_bounds__(256) k_seg_sort(uint64_t* key, uint32_t* val, uint64_t* tkey, uint32_t* tval,
+                                                  const uint32_t* off, const uint32_t* cnt, uint32_t nseg,
+                                                  const uint32_t* nitems) {
   __shared__ uint64_t K[SORT_MAX];
   __shared__ uint32_t V[SORT_MAX];
   if (*nitems == 0) return;  // nothing was routed this tick
   for (uint32_t sgi = blockIdx.x; sgi < nseg; sgi += gridDim.x) {
-    uint32_t n = cnt[sgi];
+    const uint32_t n = cnt[sgi];
     if (n <= 1) continue;
-    if (n > SORT_MAX) {
-      if (threadIdx.x == 0) atomicOr(err, E_SORTCAP);
+    const uint32_t o = off[sgi];
+    if (n <= SORT_MAX) {
+      lds_bitonic(K, V, key + o, val + o, n, key + o, val + o);
       continue;
     }
-    uint32_t o = off[sgi];
-    uint32_t p2 = 1;
-    while (p2 < n) p2 <<= 1;
-    for (uint32_t i = threadIdx.x; i < p2; i += blockDim.x) {
-      K[i] = i < n ? key[o + i] : ~0ull;
-      V[i] = i < n ? val[o + i] : 0;
-    }
-    __syncthreads();
-    for (uint32_t size = 2; size <= p2; size <<= 1)
-      for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-        for (uint32_t i = threadIdx.x; i < p2; i += blockDim.x) {
-          uint32_t j = i ^ stride;
-          if (j > i) {
-            bool up = (i & size) == 0;
-            if ((K[i] > K[j]) == up) {
-              uint64_t tk = K[i];
-              K[i] = K[j];
-              K[j] = tk;
-              uint32_t tv = V[i];
-              V[i] = V[j];
-              V[j] = tv;
-            }
-          }
-        }
-        __syncthreads();
+    for (uint32_t c = 0; c < n; c += SORT_MAX)
+      lds_bitonic(K, V, key + o + c, val + o + c, min(SORT_MAX, n - c), key + o + c, val + o + c);
+    uint64_t *sk = key + o, *dk = tkey + o;
+    uint32_t *sv = val + o, *dv = tval + o;
+    for (uint32_t w = SORT_MAX; w < n; w <<= 1) {
+      for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint32_t base = i / (2 * w) * (2 * w), mid = min(base + w, n), end = min(base + 2 * w, n);
+        const uint64_t x = sk[i];
+        uint32_t pos;
+        if (i < mid)  // run A element: its index in A plus the B entries below it
+          pos = i + lower_rank(sk + mid, end - mid, x);
+        else  // run B element: its index in B plus the A entries below it
+          pos = base + (i - mid) + lower_rank(sk + base, mid - base, x);
+        dk[pos] = x;
+        dv[pos] = sv[i];
       }
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-      key[o + i] = K[i];
-      val[o + i] = V[i];
+      __syncthreads();
+      uint64_t* tk = sk;
+      sk = dk;
+      dk = tk;
+      uint32_t* tv = sv;
+      sv = dv;
+      dv = tv;
     }
-    __syncthreads();
+    if (sk != key + o) {
+      for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        key[o + i] = sk[i];
+        val[o + i] = sv[i];
+      }
+      __syncthreads();
+    }
   }
 }
 
@@ -393,57 +445,32 @@ __device__ uint32_t inc_at(const Dev& d, uint32_t member, uint32_t g, uint64_t g
 // [cs, t)? The window check alone is not enough: the spread is recomputed from the gossip list every round, so a
 // list that shrinks (members removed during a partition) and grows back reopens the window of a gossip already swept.
 // The ring holds every round in that range: the window at t bounds t - cs to ~spread rounds, LOGW >= 4 (spread + 2).
+// The ring is walked from the newest round back to cs (ring order is tick order), so the cost is the rounds since cs.
 __device__ bool swept_before(const Dev& d, uint32_t x, uint32_t cs, uint32_t t) {
   const uint32_t infP = rounds_before(d, x, cs);
-  for (uint32_t e = 0; e < d.LOGW; ++e) {
-    const size_t li = (size_t)x * d.LOGW + e;
+  const uint32_t pos = d.log_pos[x], n = min(pos, d.LOGW);
+  for (uint32_t e = 1; e <= n; ++e) {
+    const size_t li = (size_t)x * d.LOGW + (pos - e) % d.LOGW;
     const uint32_t tr = d.log_tick[li];
-    if (tr == NEVER || tr < cs || tr >= t) continue;
+    if (tr == NEVER || tr >= t) continue;
+    if (tr < cs) break;
     if (rounds_before(d, x, tr) > infP + 2u * (d.log_spread[li] + 1u)) return true;
   }
   return false;
 }
 
-__device__ __noinline__ bool blocked_pair(const Dev& d, uint32_t x, uint32_t y, uint32_t g, uint64_t gid,
-                                          uint32_t tau, uint32_t cx) {
+// The replay over the sorted contact events of the pair (x, y) for gossip g (see the comment above Contact).
+// oldest[0]: oldest tick in y's log, oldest[1]: in x's log (0 if that ring never wrapped).
+template <uint32_t CM>
+__device__ __forceinline__ bool replay_pair(const Dev& d, uint32_t x, uint32_t y, uint32_t g, uint64_t gid,
+                                            uint32_t tau, uint32_t cx, const Contact* ev, uint32_t n,
+                                            const uint32_t* oldest) {
   const uint32_t lat = d.lat;
-  constexpr uint32_t CMAX = 256;  // contact events between one pair inside the log window (small clusters: many)
-  Contact ev[CMAX];
-  uint32_t n = 0;
-  const uint32_t born = d.slot_ctick[g];  // no member could send g before it was created
-  uint32_t oldest[2] = {0, 0};  // oldest tick still in each log, 0 if the ring never wrapped
-  for (int side = 0; side < 2; ++side) {
-    uint32_t from = side == 0 ? y : x, to = side == 0 ? x : y;
-    bool wrapped = d.log_pos[from] > d.LOGW;
-    uint32_t old = NEVER;
-    for (uint32_t e = 0; e < d.LOGW; ++e) {
-      size_t li = (size_t)from * d.LOGW + e;
-      uint32_t t2 = d.log_tick[li];
-      if (t2 == NEVER) continue;
-      if (t2 < old) old = t2;
-      if (t2 + lat > tau || t2 < born) continue;
-      uint32_t cnt = d.log_cnt[li];
-      for (uint32_t s2 = 0; s2 < cnt; ++s2)
-        if (d.log_tg[li * d.F + s2] == to) {
-          if (n == CMAX) {
-            atomicOr(d.err, E_CONTACTS);
-            return false;
-          }
-          uint32_t j = n++;
-          while (j > 0 && ev[j - 1].tick > t2) {
-            ev[j] = ev[j - 1];
-            --j;
-          }
-          ev[j] = Contact{t2, s2, d.log_spread[li], (uint32_t)side};
-        }
-    }
-    oldest[side] = wrapped ? old : 0;
-  }
-  // oldest[0] is y's log (y -> x events), oldest[1] is x's log (x -> y events). Find which deliveries can matter:
-  // into x from cx on (the answer), and into a sender from its incarnation start for every relevant event
-  // (its isInfected check). The fixpoint runs over at most 64 events. The ring must cover those ranges.
+  // Find which deliveries can matter: into x from cx on (the answer), and into a sender from its incarnation start
+  // for every relevant event (its isInfected check). The fixpoint runs over at most CM events. The ring must cover
+  // those ranges.
   uint32_t lo_in[2] = {cx, NEVER};  // [0]: deliveries into x, [1]: deliveries into y
-  uint32_t cinc[CMAX];
+  uint32_t cinc[CM];
   for (uint32_t i = 0; i < n; ++i) cinc[i] = NEVER - 1;  // not computed yet
   for (int pass = 0; pass < 8; ++pass) {
     bool changed = false;
@@ -474,13 +501,13 @@ __device__ __noinline__ bool blocked_pair(const Dev& d, uint32_t x, uint32_t y, 
       d.err[5] = oldest[1];
     }
   }
-  uint32_t del[2][CMAX];
+  uint32_t del[2][CM];
   uint32_t nd[2] = {0, 0};
   for (uint32_t i = 0; i < n; ++i) {
     const Contact& c = ev[i];
     uint32_t snd = c.dir == 0 ? y : x;
     // the sender held g at that round (its incarnation then), inside its spread window (selectGossipsToSend :246)
-    uint32_t cs = inc_at(d, snd, g, gid, c.tick);
+    uint32_t cs = cinc[i] != NEVER - 1 ? cinc[i] : inc_at(d, snd, g, gid, c.tick);
     if (cs == NEVER) continue;
     if (rounds_before(d, snd, cs) + c.spread < rounds_before(d, snd, c.tick)) continue;
     if (swept_before(d, snd, cs, c.tick)) continue;  // x no longer held it
@@ -497,6 +524,70 @@ __device__ __noinline__ bool blocked_pair(const Dev& d, uint32_t x, uint32_t y, 
   return false;
 }
 
+// contact events of the pair (x, y) in both logs up to tick tau - lat, in tick order; n = CM + 1 on overflow
+template <uint32_t CM>
+__device__ __forceinline__ uint32_t collect_contacts(const Dev& d, uint32_t x, uint32_t y, uint32_t tau, uint32_t born,
+                                                     Contact* ev, uint32_t* oldest) {
+  uint32_t n = 0;
+  for (int side = 0; side < 2; ++side) {
+    uint32_t from = side == 0 ? y : x, to = side == 0 ? x : y;
+    bool wrapped = d.log_pos[from] > d.LOGW;
+    uint32_t old = NEVER;
+    for (uint32_t e = 0; e < d.LOGW; ++e) {
+      size_t li = (size_t)from * d.LOGW + e;
+      uint32_t t2 = d.log_tick[li];
+      if (t2 == NEVER) continue;
+      if (t2 < old) old = t2;
+      if (t2 + d.lat > tau || t2 < born) continue;
+      uint32_t cnt = d.log_cnt[li];
+      for (uint32_t s2 = 0; s2 < cnt; ++s2)
+        if (d.log_tg[li * d.F + s2] == to) {
+          if (n == CM) return CM + 1;
+          uint32_t j = n++;
+          while (j > 0 && ev[j - 1].tick > t2) {
+            ev[j] = ev[j - 1];
+            --j;
+          }
+          ev[j] = Contact{t2, s2, d.log_spread[li], (uint32_t)side};
+        }
+    }
+    oldest[side] = wrapped ? old : 0;
+  }
+  return n;
+}
+
+// isInfected replay from a full scan of both logs (used when the cached contact list of the pair overflowed)
+__device__ __noinline__ bool blocked_pair(const Dev& d, uint32_t x, uint32_t y, uint32_t g, uint64_t gid,
+                                          uint32_t tau, uint32_t cx) {
+  constexpr uint32_t CMAX = 256;  // contact events between one pair inside the log window (small clusters: many)
+  Contact ev[CMAX];
+  uint32_t oldest[2];
+  const uint32_t n = collect_contacts<CMAX>(d, x, y, tau, d.slot_ctick[g], ev, oldest);
+  if (n > CMAX) {
+    atomicOr(d.err, E_CONTACTS);
+    return false;
+  }
+  return replay_pair<CMAX>(d, x, y, g, gid, tau, cx, ev, n, oldest);
+}
+
+// isInfected replay from the pair's contact list cached by k_gossip_contacts (gossip-independent; the creation
+// tick of g filters it: nobody could send g before it existed)
+__device__ __forceinline__ bool blocked_pair_cached(const Dev& d, uint32_t x, uint32_t y, uint32_t g, uint64_t gid,
+                                                    uint32_t tau, uint32_t cx, const uint32_t* rec) {
+  const uint32_t nall = rec[0];
+  if (nall > CEV) return blocked_pair(d, x, y, g, gid, tau, cx);
+  const uint32_t born = d.slot_ctick[g];
+  Contact ev[CEV];
+  uint32_t n = 0;
+  for (uint32_t i = 0; i < nall; ++i) {
+    const uint32_t t2 = rec[4 + 2 * i], w = rec[5 + 2 * i];
+    if (t2 < born) continue;
+    ev[n++] = Contact{t2, w & 0xFFu, w >> 16, (w >> 8) & 1u};
+  }
+  const uint32_t oldest[2] = {rec[1], rec[2]};
+  return replay_pair<CEV>(d, x, y, g, gid, tau, cx, ev, n, oldest);
+}
+
 __global__ void k_gossip_active(Dev d, uint32_t k, uint32_t* active, uint32_t* nactive) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= d.SLOTS || !d.slot_used[g]) return;
@@ -507,7 +598,8 @@ __global__ void k_gossip_active(Dev d, uint32_t k, uint32_t* active, uint32_t* n
   active[atomicAdd(nactive, 1u)] = g;
 }
 
-// contact flags: did target t = T[m][s] choose m in a logged round inside the look-back window?
+// contact lists: did target t = T[m][s] choose m in a logged round inside the look-back window? If so, cache the
+// pair's contact events in both directions (independent of the gossip) for blocked_pair_cached
 __global__ void k_gossip_contacts(Dev d, uint32_t k) {
   uint32_t i = d.lo * d.F + blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= d.hi * d.F) return;
@@ -522,6 +614,20 @@ __global__ void k_gossip_contacts(Dev d, uint32_t k) {
       uint32_t n = d.log_cnt[lo];
       for (uint32_t s2 = 0; s2 < n; ++s2)
         if (d.log_tg[lo * d.F + s2] == m) flag = 1;
+    }
+    if (flag) {
+      Contact ev[CEV];
+      uint32_t oldest[2];
+      uint32_t* rec = d.cev + (size_t)i * CEVW;
+      const uint32_t n = collect_contacts<CEV>(d, m, t, k, 0, ev, oldest);
+      rec[0] = n;
+      rec[1] = oldest[0];
+      rec[2] = oldest[1];
+      if (n <= CEV)
+        for (uint32_t j = 0; j < n; ++j) {
+          rec[4 + 2 * j] = ev[j].tick;
+          rec[5 + 2 * j] = ev[j].slot | (ev[j].dir << 8) | (ev[j].spread << 16);
+        }
     }
   }
   d.tcontact[i] = flag;
@@ -549,7 +655,9 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
       uint32_t n = d.tcnt[m];
       for (uint32_t s = 0; s < n; ++s) {
         uint32_t t = d.T[(size_t)m * d.F + s];
-        if (d.tcontact[(size_t)m * d.F + s] && blocked_pair(d, m, t, g, gid, k, c)) continue;  // isInfected (:247)
+        if (d.tcontact[(size_t)m * d.F + s] &&
+            blocked_pair_cached(d, m, t, g, gid, k, c, d.cev + ((size_t)m * d.F + s) * CEVW))
+          continue;  // isInfected (:247)
         sends++;
         if (d.dbg_send) {
           uint32_t di = atomicAdd(d.dbg_send_n, 1u);
@@ -799,8 +907,8 @@ static void launch_receipt_routing(const Dev& d, hipStream_t st) {
   hipLaunchKernelGGL(k_scan_add, dim3(cdiv(d.N, 256)), dim3(256), 0, st, d.rc_off, d.scan_part, d.N);
   hipLaunchKernelGGL(k_scatter_rc, dim3(256), dim3(256), 0, st, d, d.rc_raw, d.rc_n, d.RCAP, d.rc_off, d.rc_fill,
                      d.rc_slot, d.rc_key);
-  hipLaunchKernelGGL(k_seg_sort, dim3(1024), dim3(256), 0, st, d.rc_key, d.rc_slot, d.rc_off, d.rc_cnt, d.N, d.err,
-                     d.rc_n);
+  hipLaunchKernelGGL(k_seg_sort, dim3(1024), dim3(256), 0, st, d.rc_key, d.rc_slot, d.rc_key2, d.rc_slot2, d.rc_off,
+                     d.rc_cnt, d.N, d.rc_n);
 }
 
 void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {

@@ -1,12 +1,28 @@
+"""C2: N members (default 10k), PRECONVERGED, 5 % loss on every link, one GPU.
+Prints the per-period gossip load (created, sends G, events E) and the throughput after warm-up."""
 import sys, time
 sys.path.insert(0, "scalecube-cluster_amd")
 import swimhip
 from swimhip import SimConfig
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
+P = int(sys.argv[2]) if len(sys.argv) > 2 else 30
 c = swimhip.cluster(SimConfig(n_members=N, profile=True))
 c.set_default_loss(5)
-t = time.perf_counter(); c.run_periods(10); print("warm 10 periods", time.perf_counter() - t, c.counters(), flush=True)
-for r in range(3):
-    b = c.counters(); t = time.perf_counter(); c.run_periods(10); dt = time.perf_counter() - t; e = c.counters()
-    d = {k: e[k] - b[k] for k in e}
-    print(f"10 periods: {dt:.3f}s -> {N*10/dt:.3e} member-periods/s; member {d['member_ns']/1e6:.1f} ms diff {d['diff_ns']/1e6:.1f} ms gossip_send {d['gossip_ns']/1e6:.1f} ms; G={d['gossip_messages']:.3e} E={d['events']} created={d['gossips_created']}", flush=True)
+prev = c.counters()
+t0 = time.perf_counter()
+tw = None
+for p in range(P):
+    t = time.perf_counter()
+    c.run_periods(1)
+    c.sync()
+    dt = time.perf_counter() - t
+    e = c.counters()
+    d = {k: e[k] - prev[k] for k in e}
+    prev = e
+    print(f"period {p}: {dt*1e3:.1f} ms created {d['gossips_created']} G {d['gossip_messages']:.3e} E {d['events']} "
+          f"R {d['record_compares']:.3e} member {d['member_ns']/1e6:.1f} ms diff {d['diff_ns']/1e6:.1f} ms", flush=True)
+    if p == 9:
+        tw = time.perf_counter()
+if tw is not None and P > 10:
+    dt = time.perf_counter() - tw
+    print(f"C2 steady state (periods 10..{P-1}): {dt/(P-10)*1e3:.1f} ms/period -> {N*(P-10)/dt:.3e} member-periods/s", flush=True)
