@@ -201,6 +201,7 @@ int build(swim_handle* h) {
   d.seed_hi = (uint32_t)(c.seed >> 32);
   d.init_mode = c.init_mode;
   d.flags = c.flags;
+  d.exp = getenv("SWIM_EXP") ? (uint32_t)atoi(getenv("SWIM_EXP")) : 0u;  // timing experiments: wrong results
   // seeds: LinkedHashSet of valid ids (MembershipProtocolImpl.java:160-166); self is skipped per member
   for (uint32_t i = 0; i < c.n_seeds; ++i) {
     uint32_t s = c.seeds[i];
@@ -234,6 +235,7 @@ int build(swim_handle* h) {
   d.EVCAP = c.event_cap ? c.event_cap : (1u << 20);
   d.DCAP = (uint32_t)std::min<uint64_t>(1ull << 27, std::max<uint64_t>(1ull << 16, N * 16384));
   d.RCAP = d.DCAP;
+  d.SLOWCAP = d.DCAP;
   d.ARENA_ROWS = 64;
 
   int rc;
@@ -249,9 +251,9 @@ int build(swim_handle* h) {
   const uint64_t NL = d.NL;  // per-observer arrays: this shard's rows only
   A(d.row, NL * d.NS) A(d.fdl, NL * d.LCAP) A(d.gl, NL * d.LCAP)
   A(d.subs, NL * SUBCAP * 4) A(d.paths, NL * PATHCAP * 5) A(d.fetch, NL * d.FCAP * FREC) A(d.groups, NL * d.GRCAP * GREC)
-  A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.cev, N * d.F * CEVW)
+  A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.slow, d.SLOWCAP) A(d.slow_n, 1) A(d.rlist, N) A(d.rn, 1) A(d.cev, N * d.F * CEVW)
   A(d.log_tick, N * d.LOGW) A(d.log_spread, N * d.LOGW) A(d.log_cnt, N * d.LOGW) A(d.log_tg, N * d.LOGW * d.F)
-  A(d.log_pos, N)
+  A(d.log_pos, N) A(d.spchg, N)
   A(d.slot_gid, d.SLOTS) A(d.slot_subj, d.SLOTS) A(d.slot_ctick, d.SLOTS) A(d.slot_key, d.SLOTS) A(d.slot_holders, d.SLOTS)
   A(d.slot_used, d.SLOTS) A(d.S, (uint64_t)d.SLOTS * N) A(d.free_list, d.SLOTS) A(d.free_top, 1)
   A(d.deliv, d.DCAP) A(d.deliv_n, 1) A(d.rc_raw, d.RCAP) A(d.rc_n, 1) A(d.rc_cnt, N) A(d.rc_off, N) A(d.rc_fill, N) A(d.scan_part, 1024)

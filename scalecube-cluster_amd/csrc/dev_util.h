@@ -94,6 +94,19 @@ __device__ __forceinline__ bool lost_gossip(const Dev& d, uint32_t src, uint32_t
 }
 
 // gPeriod of member x before its gossip task at tick c = number of its gossip rounds at ticks < c
+// wave-aggregated append: the active lanes that call it together reserve consecutive indices with ONE atomic on
+// the shared counter (a hot single-address atomic per lane serialises at L2 under C2's receipt storms)
+__device__ __forceinline__ uint32_t wave_append(uint32_t* ctr) {
+  const uint64_t mask = __ballot(1);
+  const uint32_t lane = __lane_id();
+  const uint32_t leader = (uint32_t)__ffsll((unsigned long long)mask) - 1u;
+  const uint32_t rank = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(ctr, (uint32_t)__popcll(mask));
+  base = __shfl(base, (int)leader);
+  return base + rank;
+}
+
 __device__ __forceinline__ uint32_t rounds_before(const Dev& d, uint32_t x, uint32_t c) {
   uint32_t f = d.firstGossip[x];
   if (f == NEVER || c <= f) return 0;

@@ -92,6 +92,11 @@ struct Dev {
 
   // ---- gossip round of the current tick ----
   uint32_t *tround, *tcnt, *tspread, *tperiod, *T, *tcontact;  // T, tcontact: [N][F]
+  uint32_t* spchg;  // [N] tick of the member's latest gossip round whose spread differs from the round before
+  uint64_t* slow;  // [SLOWCAP] (slot << 32 | m * F + s) sends deferred to k_gossip_send_slow
+  uint32_t* slow_n;
+  uint32_t SLOWCAP;
+  uint32_t *rlist, *rn;  // [N] members with a gossip round this tick (built by k_gossip_contacts)
   uint32_t* cev;  // [N][F][CEVW] contact events of (m, T[m][s]) cached by k_gossip_contacts when tcontact is set
   uint32_t *log_tick, *log_spread, *log_cnt, *log_tg, *log_pos;  // [N][LOGW], tg [N][LOGW][F], pos [N]
 
@@ -144,6 +149,7 @@ struct Dev {
   uint32_t* dbg_send;       // debugging aid (SWIM_SEND_LOG=cap): [cap][5] tick, sender, gid lo, gid hi, target
   uint32_t* dbg_send_n;
   uint32_t dbg_send_cap;
+  uint32_t exp;  // timing experiments only (SWIM_EXP): 1 = no infectedFrom replay, 2 = no per-target work
 
   // ---- row sharding (W > 1) ----
   // This shard owns observers [lo, hi): their rows, lists, subscriptions, paths, fetches and groups are stored

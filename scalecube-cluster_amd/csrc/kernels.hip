@@ -48,6 +48,7 @@ __global__ void k_init_members(Dev d) {
   d.evHash[m] = 0;
   d.tround[m] = 0;
   d.log_pos[m] = 0;
+  d.spchg[m] = 0;
   d.dead_tick[m] = NEVER;
   d.md_version[m] = 0;
   d.rc_cnt[m] = 0;
@@ -446,15 +447,19 @@ __device__ uint32_t inc_at(const Dev& d, uint32_t member, uint32_t g, uint64_t g
 // list that shrinks (members removed during a partition) and grows back reopens the window of a gossip already swept.
 // The ring holds every round in that range: the window at t bounds t - cs to ~spread rounds, LOGW >= 4 (spread + 2).
 // The ring is walked from the newest round back to cs (ring order is tick order), so the cost is the rounds since cs.
+// While x's spread has not changed since cs (spchg: tick of x's latest round whose spread differs from the round
+// before), the sweep condition is monotone in the round, so only the latest round before t needs a check.
 __device__ bool swept_before(const Dev& d, uint32_t x, uint32_t cs, uint32_t t) {
   const uint32_t infP = rounds_before(d, x, cs);
   const uint32_t pos = d.log_pos[x], n = min(pos, d.LOGW);
+  const bool steady = d.spchg[x] <= cs;
   for (uint32_t e = 1; e <= n; ++e) {
     const size_t li = (size_t)x * d.LOGW + (pos - e) % d.LOGW;
     const uint32_t tr = d.log_tick[li];
     if (tr == NEVER || tr >= t) continue;
     if (tr < cs) break;
     if (rounds_before(d, x, tr) > infP + 2u * (d.log_spread[li] + 1u)) return true;
+    if (steady) break;
   }
   return false;
 }
@@ -577,6 +582,14 @@ __device__ __forceinline__ bool blocked_pair_cached(const Dev& d, uint32_t x, ui
   const uint32_t nall = rec[0];
   if (nall > CEV) return blocked_pair(d, x, y, g, gid, tau, cx);
   const uint32_t born = d.slot_ctick[g];
+  // only a delivery y -> x at or after x's incarnation start cx can put y in infectedFrom_x (most cached contacts
+  // are older than the gossip)
+  bool relevant = false;
+  for (uint32_t i = 0; i < nall; ++i) {
+    const uint32_t t2 = rec[4 + 2 * i];
+    relevant |= ((rec[5 + 2 * i] >> 8) & 1u) == 0 && t2 >= born && t2 + d.lat >= cx;
+  }
+  if (!relevant) return false;
   Contact ev[CEV];
   uint32_t n = 0;
   for (uint32_t i = 0; i < nall; ++i) {
@@ -590,6 +603,7 @@ __device__ __forceinline__ bool blocked_pair_cached(const Dev& d, uint32_t x, ui
 
 __global__ void k_gossip_active(Dev d, uint32_t k, uint32_t* active, uint32_t* nactive) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g == 0) *d.slow_n = *d.rn = 0;  // deferred sends and round members of this tick
   if (g >= d.SLOTS || !d.slot_used[g]) return;
   // members stopped after their leave completed at tick k - 1 hold nothing any more (as k_kill)
   const uint32_t pb = (k - 1) & 1u, nd = k > 0 ? min(d.deaths_n[pb], DEATHCAP) : 0u;
@@ -631,74 +645,109 @@ __global__ void k_gossip_contacts(Dev d, uint32_t k) {
     }
   }
   d.tcontact[i] = flag;
+  if (s == 0 && d.tround[m]) {  // compact list of this tick's round members (k_gossip_send iterates over it)
+    uint32_t r = wave_append(d.rn);
+    d.rlist[r] = m;
+  }
 }
 
-// one thread per (active slot, member): the member's round sends of this gossip, then its sweep
+// one counted send of gossip g from m to its round target t = T[m][s] (isInfected already checked): the receipt is
+// potential unless t holds g past this tick; a loss draw, then the first sender of (g, t) queues the delivery
+__device__ __forceinline__ void send_tail(const Dev& d, uint32_t g, uint32_t m, uint32_t s, uint32_t t, uint32_t k,
+                                          uint64_t gid, uint32_t* Sg) {
+  if (d.dbg_send) {
+    uint32_t di = atomicAdd(d.dbg_send_n, 1u);
+    if (di < d.dbg_send_cap) {
+      uint32_t* r = d.dbg_send + (size_t)di * 5;
+      r[0] = k;
+      r[1] = m;
+      r[2] = (uint32_t)gid;
+      r[3] = (uint32_t)(gid >> 32);
+      r[4] = t;
+    }
+  }
+  uint32_t et = Sg[t];
+  bool potential = !s_held(et);
+  if (!potential && d.tround[t]) {  // t sweeps g in its own round this tick -> a delivery re-creates it
+    uint32_t it = rounds_before(d, t, s_ctick(et));
+    potential = d.tperiod[t] > it + 2u * (d.tspread[t] + 1u);
+  }
+  if (!potential) return;
+  if (lost_gossip(d, m, t, k, s, gid)) return;
+  uint32_t old = atomicOr(&Sg[t], S_PENDING);
+  if (!(old & S_PENDING)) {
+    uint32_t di = wave_append(d.deliv_n);
+    if (di < d.DCAP)
+      d.deliv[di] = ((uint64_t)g << 32) | t;
+    else
+      atomicOr(d.err, E_DELIV);
+  }
+}
+
+// Work item = (256 round members of this tick, GB active slots). Each thread loads its member's round once and
+// the member's GB holder entries as independent loads (memory-level parallelism), then per held slot: the round
+// sends (selectGossipsToSend :239-250 + isInfected) and the sweep (:283-308). Consecutive blocks share the slot
+// group, so its holder rows stay in L2 for the random target reads. A pair whose cached contact list overflowed is
+// deferred to k_gossip_send_slow (the full replay needs a large stack).
+constexpr uint32_t GB = 16;
 __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp, uint32_t k, const uint32_t* active,
                                                      const uint32_t* nactive) {
   const Dev& d = *dp;
   __shared__ unsigned long long red[256];
-  uint32_t na = *nactive;
-  uint32_t mchunks = (d.NL + 255) / 256;  // this shard's senders
+  const uint32_t na = *nactive, nr = *d.rn;
+  const uint32_t rchunks = (nr + 255) / 256, gchunks = (na + GB - 1) / GB;
   unsigned long long sends = 0;
-  for (uint32_t w = blockIdx.x; w < na * mchunks; w += gridDim.x) {
-    uint32_t g = active[w / mchunks];
-    uint32_t m = d.lo + (w % mchunks) * 256 + threadIdx.x;
-    if (m >= d.hi || !d.tround[m]) continue;
-    uint32_t* Sg = d.S + (size_t)g * d.N;
-    uint32_t e = Sg[m];
-    if (!s_held(e)) continue;
-    uint32_t c = s_ctick(e);
-    uint32_t infP = rounds_before(d, m, c), per = d.tperiod[m], sp = d.tspread[m];
-    uint64_t gid = d.slot_gid[g];
-    if (infP + sp >= per) {  // selectGossipsToSend window (:246)
-      uint32_t n = d.tcnt[m];
-      for (uint32_t s = 0; s < n; ++s) {
-        uint32_t t = d.T[(size_t)m * d.F + s];
-        if (d.tcontact[(size_t)m * d.F + s] &&
-            blocked_pair_cached(d, m, t, g, gid, k, c, d.cev + ((size_t)m * d.F + s) * CEVW))
-          continue;  // isInfected (:247)
-        sends++;
-        if (d.dbg_send) {
-          uint32_t di = atomicAdd(d.dbg_send_n, 1u);
-          if (di < d.dbg_send_cap) {
-            uint32_t* r = d.dbg_send + (size_t)di * 5;
-            r[0] = k;
-            r[1] = m;
-            r[2] = (uint32_t)gid;
-            r[3] = (uint32_t)(gid >> 32);
-            r[4] = t;
+  for (uint32_t w = blockIdx.x; w < rchunks * gchunks; w += gridDim.x) {
+    const uint32_t gc = w / rchunks, ri = (w % rchunks) * 256 + threadIdx.x;
+    if (ri >= nr) continue;
+    const uint32_t m = d.rlist[ri];
+    const uint32_t per = d.tperiod[m], sp = d.tspread[m], fg = d.firstGossip[m];
+    const uint32_t n = d.exp == 2 ? 0u : d.tcnt[m];
+    const uint32_t g0 = gc * GB, gn = min(GB, na - g0);
+    uint32_t e[GB];
+#pragma unroll
+    for (uint32_t j = 0; j < GB; ++j) e[j] = j < gn ? d.S[(size_t)active[g0 + j] * d.N + m] : 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < GB; ++j) {
+      if (!s_held(e[j])) continue;
+      const uint32_t g = active[g0 + j];
+      uint32_t* Sg = d.S + (size_t)g * d.N;
+      const uint32_t c = s_ctick(e[j]);
+      const uint32_t infP = (fg == NEVER || c <= fg) ? 0u : (c - fg + d.gossip_t - 1) / d.gossip_t;  // rounds_before
+      if (infP + sp >= per) {  // selectGossipsToSend window (:246)
+        const uint64_t gid = d.slot_gid[g];
+        if (d.exp == 2) sends += d.tcnt[m];
+        for (uint32_t s = 0; s < n; ++s) {
+          const size_t ms = (size_t)m * d.F + s;
+          const uint32_t t = d.T[ms];
+          if (d.exp != 1 && d.tcontact[ms]) {
+            const uint32_t* rec = d.cev + ms * CEVW;
+            if (rec[0] > CEV) {  // overflowed contact list: the full replay runs in k_gossip_send_slow
+              uint32_t i = wave_append(d.slow_n);
+              if (i < d.SLOWCAP)
+                d.slow[i] = ((uint64_t)g << 32) | (uint32_t)ms;
+              else
+                atomicOr(d.err, E_CONTACTS);
+              continue;
+            }
+            if (blocked_pair_cached(d, m, t, g, gid, k, c, rec)) continue;  // isInfected (:247)
           }
-        }
-        uint32_t et = Sg[t];
-        bool potential = !s_held(et);
-        if (!potential && d.tround[t]) {  // t sweeps g in its own round this tick -> a delivery re-creates it
-          uint32_t it = rounds_before(d, t, s_ctick(et));
-          potential = d.tperiod[t] > it + 2u * (d.tspread[t] + 1u);
-        }
-        if (!potential) continue;
-        if (lost_gossip(d, m, t, k, s, gid)) continue;
-        uint32_t old = atomicOr(&Sg[t], S_PENDING);
-        if (!(old & S_PENDING)) {
-          uint32_t di = atomicAdd(d.deliv_n, 1u);
-          if (di < d.DCAP)
-            d.deliv[di] = ((uint64_t)g << 32) | t;
-          else
-            atomicOr(d.err, E_DELIV);
+          sends++;
+          send_tail(d, g, m, s, t, k, gid, Sg);
         }
       }
-    }
-    if (per > infP + 2u * (sp + 1u)) {  // sweepGossips (:283-308)
-      atomicOr(&Sg[m], S_SWEPT);
-      atomicSub(&d.held[m], 1u);
-      atomicSub(&d.slot_holders[g], 1);
-      on_sweep(d, g, m, k);
-      if (d.W > 1) {  // applied on the other shards from exchange B
-        uint32_t i = atomicAdd(&d.xn[2], 1u);
-        if (i < d.SWCAP)
-          d.sw_rec[i] = ((uint64_t)g << 32) | m;
-        else
-          atomicOr(d.err, E_XCAP);
+      if (per > infP + 2u * (sp + 1u)) {  // sweepGossips (:283-308)
+        atomicOr(&Sg[m], S_SWEPT);
+        atomicSub(&d.held[m], 1u);
+        atomicSub(&d.slot_holders[g], 1);
+        on_sweep(d, g, m, k);
+        if (d.W > 1) {  // applied on the other shards from exchange B
+          uint32_t i = atomicAdd(&d.xn[2], 1u);
+          if (i < d.SWCAP)
+            d.sw_rec[i] = ((uint64_t)g << 32) | m;
+          else
+            atomicOr(d.err, E_XCAP);
+        }
       }
     }
   }
@@ -709,6 +758,24 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
     __syncthreads();
   }
   if (threadIdx.x == 0 && red[0]) atomicAdd(&d.ctr[C_G], red[0]);
+}
+
+// deferred sends whose pair had more contact events than the cache holds (small clusters): full log scan + replay
+__global__ void __launch_bounds__(256) k_gossip_send_slow(const Dev* __restrict__ dp, uint32_t k) {
+  const Dev& d = *dp;
+  const uint32_t n = min(*d.slow_n, d.SLOWCAP);
+  unsigned long long sends = 0;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint64_t v = d.slow[i];
+    const uint32_t g = (uint32_t)(v >> 32), ms = (uint32_t)v, m = ms / d.F, s = ms % d.F;
+    uint32_t* Sg = d.S + (size_t)g * d.N;
+    const uint32_t t = d.T[ms], c = s_ctick(Sg[m]);
+    const uint64_t gid = d.slot_gid[g];
+    if (blocked_pair(d, m, t, g, gid, k, c)) continue;  // isInfected (:247)
+    sends++;
+    send_tail(d, g, m, s, t, k, gid, Sg);
+  }
+  if (sends) atomicAdd(&d.ctr[C_G], sends);
 }
 
 // first receipts (onGossipReq :176-180): create the holder state at tick k + lat and queue the record for P4
@@ -729,7 +796,7 @@ __global__ void k_gossip_apply(Dev d, uint32_t k) {
     atomicAdd(&d.held[t], 1u);
     atomicAdd(&d.slot_holders[g], 1);
     if (t < d.lo || t >= d.hi) continue;  // P4 of another shard's member
-    uint32_t ri = atomicAdd(d.rc_n, 1u);
+    uint32_t ri = wave_append(d.rc_n);
     if (ri < d.RCAP)
       d.rc_raw[ri] = ((uint64_t)t << 32) | g;
     else
@@ -886,12 +953,15 @@ void launch_member(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
 
 static void launch_receipt_routing(const Dev& d, hipStream_t st);
 
+constexpr uint32_t SEND_GRID = 2048;  // 8 blocks per CU: the send loop is latency-bound
+
 void launch_gossip(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(k_gossip_active, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, st, d, k, d.active, d.nactive);
   hipLaunchKernelGGL(k_gossip_contacts, dim3(cdiv((uint64_t)d.NL * d.F, 256)), dim3(256), 0, st, d, k);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[4], st);
-  hipLaunchKernelGGL(k_gossip_send, dim3(1024), dim3(256), 0, st, d.self, k, d.active, d.nactive);
+  hipLaunchKernelGGL(k_gossip_send, dim3(SEND_GRID), dim3(256), 0, st, d.self, k, d.active, d.nactive);
+  hipLaunchKernelGGL(k_gossip_send_slow, dim3(256), dim3(256), 0, st, d.self, k);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[5], st);
   hipLaunchKernelGGL(k_gossip_apply, dim3(1024), dim3(256), 0, st, d, k);
   launch_receipt_routing(d, st);
@@ -940,7 +1010,8 @@ void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   hipLaunchKernelGGL(k_gossip_active, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, st, d, k, d.active, d.nactive);
   hipLaunchKernelGGL(k_gossip_contacts, dim3(cdiv((uint64_t)d.NL * d.F, 256)), dim3(256), 0, st, d, k);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[4], st);
-  hipLaunchKernelGGL(k_gossip_send, dim3(1024), dim3(256), 0, st, d.self, k, d.active, d.nactive);
+  hipLaunchKernelGGL(k_gossip_send, dim3(SEND_GRID), dim3(256), 0, st, d.self, k, d.active, d.nactive);
+  hipLaunchKernelGGL(k_gossip_send_slow, dim3(256), dim3(256), 0, st, d.self, k);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[5], st);
   hipLaunchKernelGGL(k_pack_b, dim3(64, d.W), dim3(256), 0, st, d);
 }

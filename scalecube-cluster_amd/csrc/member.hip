@@ -460,6 +460,7 @@ __device__ __forceinline__ void do_spread_gossip(ML& L) {
   d.tperiod[L.m] = period;
   uint32_t pos = d.log_pos[L.m] % d.LOGW;
   size_t lo = (size_t)L.m * d.LOGW + pos;
+  if (d.log_pos[L.m] > 0 && d.log_spread[(size_t)L.m * d.LOGW + (d.log_pos[L.m] - 1) % d.LOGW] != sp) d.spchg[L.m] = L.k;
   d.log_tick[lo] = L.k;
   d.log_spread[lo] = sp;
   d.log_cnt[lo] = cnt;

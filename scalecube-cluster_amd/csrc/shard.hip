@@ -189,6 +189,7 @@ __global__ void __launch_bounds__(256) k_unpack_a(Dev d, uint32_t k) {
     d.tperiod[m] = r[3];
     uint32_t pos = d.log_pos[m] % d.LOGW;
     size_t lo = (size_t)m * d.LOGW + pos;
+    if (d.log_pos[m] > 0 && d.log_spread[(size_t)m * d.LOGW + (d.log_pos[m] - 1) % d.LOGW] != r[2]) d.spchg[m] = k;
     d.log_tick[lo] = k;
     d.log_spread[lo] = r[2];
     d.log_cnt[lo] = cnt;
