@@ -47,6 +47,7 @@ extern "C" {
 #define SWIM_EV_ADDED 0u
 #define SWIM_EV_REMOVED 1u
 #define SWIM_EV_UPDATED 2u
+#define SWIM_EV_GOSSIP 3u /* Cluster.listenGossips(): first receipt of a user gossip; subject = origin, old/new_meta = payload lo/hi */
 #define SWIM_META_NONE 0xFFFFFFFFu
 
 /* status codes used by swim_read_row: MemberStatus (membership/MemberStatus.java:6-15); 0 = no row */
@@ -154,6 +155,11 @@ int swim_update_incarnation(swim_handle* h, uint32_t member);
  * at the start (P0) of the next tick the member's own record becomes DEAD inc+1 and is spread as gossip; when that
  * gossip is swept at the member (the leave Mono completes), the member stops as if killed, from the next tick */
 int swim_leave(swim_handle* h, uint32_t member);
+/* Cluster.spreadGossip(message) -> GossipProtocolImpl.spread (ClusterImpl.java:208-211, GossipProtocolImpl.java:124-128):
+ * at the start (P0) of the next tick the member creates a user gossip carrying the 64-bit payload, before any
+ * incarnation bump or leave queued for the same tick, in call order. Every other member that receives it first emits a
+ * SWIM_EV_GOSSIP event (listenGossips, ClusterImpl.java:213-216); membership ignores it (MembershipProtocolImpl :401-408) */
+int swim_spread_gossip(swim_handle* h, uint32_t member, uint64_t payload);
 
 /* readback */
 int swim_current_tick(swim_handle* h, uint64_t* tick);

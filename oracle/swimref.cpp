@@ -35,6 +35,7 @@ namespace {
 
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint64_t NEVER = ~0ull;
+constexpr uint32_t USER_SUBJ = 0xFFFFFFFFu;  // gossip subject of a user gossip (no membership record)
 
 enum St : uint8_t { ABSENT = 0, ALIVE = 1, SUSPECT = 2, DEAD = 3 };  // MemberStatus.java:6-15 (+absent)
 enum Kind : uint8_t { K_SYNC = 1, K_SYNC_ACK, K_PING, K_PING_REQ, K_PING_ACK, K_GMD_REQ, K_GMD_RESP, K_GOSSIP };
@@ -73,6 +74,7 @@ struct Msg {
   uint32_t slot = 0;                                      // target slot of a GOSSIP_REQ
   uint32_t g_subj = 0;
   Rec g_rec;                                              // gossip payload: MembershipRecord
+  uint64_t g_payload = 0;                                 // user gossip payload (g_subj == USER_SUBJ)
 };
 
 struct Sim;
@@ -108,8 +110,9 @@ struct Member {
   uint64_t gPeriod = 0;
   uint32_t gCounter = 0;
   struct GState {
-    uint32_t subj;
+    uint32_t subj;  // USER_SUBJ: a user gossip (Cluster.spreadGossip) carrying payload
     Rec rec;
+    uint64_t payload = 0;
     uint64_t infPeriod;
     std::set<uint32_t> infected;
   };
@@ -144,6 +147,7 @@ struct Member {
   uint64_t nextPing = NEVER, nextGossip = NEVER, nextSync = NEVER;
   bool pendingInc = false;  // swim_update_incarnation, applied in P0 of the next tick
   bool pendingLeave = false;  // swim_leave (leaveCluster), applied in P0 of the next tick after pendingInc
+  std::vector<uint64_t> pendingUser;  // swim_spread_gossip payloads, spread in P0 of the next tick before pendingInc
   uint32_t cidCnt = 0, syncSeq = 0, evSeq = 0;
   uint32_t sel[8] = {0};
   uint64_t evHash = 0;
@@ -157,7 +161,7 @@ struct Member {
   bool send_sync(uint8_t kind, uint32_t dst, uint32_t cid_iss, uint32_t cid_cnt, uint64_t k);
   void emit_event(uint32_t type, uint32_t subj, uint32_t oldm, uint32_t newm, uint64_t k);
   void on_member_event(uint32_t type, uint32_t subj);
-  void spread(uint32_t subj, Rec rec);
+  void spread(uint32_t subj, Rec rec, uint64_t payload = 0);
   void update_membership(uint32_t subj, Rec r1, int reason, int group, uint64_t k);
   void finish(int group, bool error, uint64_t k);
   void do_finally(uint32_t subj, Rec r1, int reason);
@@ -310,11 +314,12 @@ void Member::on_member_event(uint32_t type, uint32_t subj) {
 }
 
 // GossipProtocolImpl.spread -> createAndPutGossip (:124-128,163-169)
-void Member::spread(uint32_t subj, Rec rec) {
+void Member::spread(uint32_t subj, Rec rec, uint64_t payload) {
   uint64_t gid = ((uint64_t)id << 32) | gCounter++;
   GState g;
   g.subj = subj;
   g.rec = rec;
+  g.payload = payload;
   g.infPeriod = gPeriod;
   gossips.emplace(gid, std::move(g));
   sim->ctr.gossips_created++;
@@ -562,6 +567,7 @@ void Member::do_spread_gossip(uint64_t k) {
       m.slot = slot;
       m.g_subj = g.subj;
       m.g_rec = g.rec;
+      m.g_payload = g.payload;
       send(std::move(m), k, true);
     }
   }
@@ -627,6 +633,8 @@ static bool fd_less(const Msg& a, const Msg& b) {
 
 void Member::process(uint64_t k, std::vector<Msg>& inbox) {
   Sim& s = *sim;
+  for (uint64_t p : pendingUser) spread(USER_SUBJ, Rec{}, p);  // Cluster.spreadGossip (ClusterImpl.java:208-211)
+  pendingUser.clear();
   if (pendingInc) {  // updateIncarnation (MembershipProtocolImpl.java:178-190)
     pendingInc = false;
     Rec r{ALIVE, table[id].inc + 1};
@@ -768,10 +776,15 @@ void Member::process(uint64_t k, std::vector<Msg>& inbox) {
       GState g;
       g.subj = m->g_subj;
       g.rec = m->g_rec;
+      g.payload = m->g_payload;
       g.infPeriod = gPeriod;
       gossips.emplace(m->gid, std::move(g));
-      s.ctr.record_compares++;
-      update_membership(m->g_subj, m->g_rec, R_GOSSIP, -1, k);  // onMembershipGossip (:401-408)
+      if (m->g_subj == USER_SUBJ) {  // sink.next -> ClusterImpl.listenGossips (:213-216); membership filters it out
+        emit_event(SWIM_EV_GOSSIP, (uint32_t)(m->gid >> 32), (uint32_t)m->g_payload, (uint32_t)(m->g_payload >> 32), k);
+      } else {
+        s.ctr.record_compares++;
+        update_membership(m->g_subj, m->g_rec, R_GOSSIP, -1, k);  // onMembershipGossip (:401-408)
+      }
     }
     gossips[m->gid].infected.insert(m->src);
   }
@@ -998,6 +1011,11 @@ __attribute__((visibility("default"))) int swim_update_incarnation(swim_handle* 
 __attribute__((visibility("default"))) int swim_leave(swim_handle* h, uint32_t m) {
   if (!h || m >= h->sim.N || !h->sim.members[m].alive) return SWIM_EINVAL;
   h->sim.members[m].pendingLeave = true;
+  return SWIM_OK;
+}
+__attribute__((visibility("default"))) int swim_spread_gossip(swim_handle* h, uint32_t m, uint64_t payload) {
+  if (!h || m >= h->sim.N || !h->sim.members[m].alive) return SWIM_EINVAL;
+  h->sim.members[m].pendingUser.push_back(payload);
   return SWIM_OK;
 }
 __attribute__((visibility("default"))) int swim_set_default_loss(swim_handle* h, uint32_t pct) {

@@ -46,6 +46,9 @@ struct swim_handle {
   std::vector<uint8_t> hsend, hrecv;  // SWIM_TRANSPORT_HOST staging
   double xchg_ms = 0;                 // host time spent in the exchanges
   bool xflag = false;                 // last exchange: some shard has a gossip slot in use
+  std::vector<uint64_t> ugq;  // swim_spread_gossip queue: (member, payload) pairs for P0 of the next tick
+  uint64_t* ug_dev = nullptr;  // device copy of ugq
+  size_t ug_cap = 0;
   volatile uint32_t* hflag = nullptr; // host-mapped flag word written by k_tick_flag (W == 1)
   unsigned long long* xi_host_h = nullptr;  // host side of Dev::xi_host
   hipEvent_t ev_member = nullptr;
@@ -564,6 +567,18 @@ int swim_step(swim_handle* h, uint32_t n) {
     }
   uint64_t first = h->tick;
   const Dev& d = h->d;
+  if (n > 0 && !h->ugq.empty()) {  // user gossips queued since the last step: P0 of this step's first tick
+    const size_t pairs = h->ugq.size() / 2;
+    if (pairs > h->ug_cap) {
+      int rc;
+      h->ug_cap = std::max<size_t>(pairs, 1024);
+      if ((rc = dalloc(h, &h->ug_dev, 2 * h->ug_cap)) != SWIM_OK) return rc;
+    }
+    HIPCK(hipMemcpyAsync(h->ug_dev, h->ugq.data(), h->ugq.size() * 8, hipMemcpyHostToDevice, h->stream));
+    launch_user_gossips(d, (uint32_t)h->tick, h->ug_dev, (uint32_t)pairs, h->stream);
+    HIPCK(hipStreamSynchronize(h->stream));  // the host queue is reused after this
+    h->ugq.clear();
+  }
   for (uint32_t i = 0; i < n; ++i) {
     const TickEvents* te = profile ? &h->prof[i] : nullptr;
     const uint32_t k = (uint32_t)h->tick;
@@ -593,6 +608,12 @@ int swim_step(swim_handle* h, uint32_t n) {
     h->tick++;
   }
   int rc = check_err(h);
+  if (rc == SWIM_OK && (d.exp & 4)) {  // timing experiments: gossip-send work counters since the last step
+    unsigned long long c[5];
+    HIPCK(hipMemcpy(c, d.ctr + 8, sizeof(c), hipMemcpyDeviceToHost));
+    HIPCK(hipMemset(d.ctr + 8, 0, sizeof(c)));
+    fprintf(stderr, "exp: held %llu window %llu replays %llu slots(sum) %llu rounds(sum) %llu\n", c[0], c[1], c[2], c[3], c[4]);
+  }
   if (rc == SWIM_OK && profile) {
     for (uint32_t i = 0; i < n; ++i) {
       float ms = 0;
@@ -624,6 +645,18 @@ int swim_kill(swim_handle* h, uint32_t m) {
   HIPCK(hipMemcpyAsync(h->d.dead_tick + m, &t, 4, hipMemcpyHostToDevice, h->stream));
   launch_kill(h->d, m, h->stream);
   return check_err(h);
+}
+
+int swim_spread_gossip(swim_handle* h, uint32_t m, uint64_t payload) {
+  if (!h || m >= h->d.N) return SWIM_EINVAL;
+  if (!owns(h, m)) return SWIM_OK;  // the owning shard creates it; the others receive its slot in exchange A
+  uint32_t dt = 0;
+  HIPCK(hipStreamSynchronize(h->stream));
+  HIPCK(hipMemcpy(&dt, h->d.dead_tick + m, 4, hipMemcpyDeviceToHost));
+  if (dt != NEVER) return SWIM_EINVAL;
+  h->ugq.push_back(m);
+  h->ugq.push_back(payload);
+  return SWIM_OK;
 }
 
 int swim_update_incarnation(swim_handle* h, uint32_t m) {

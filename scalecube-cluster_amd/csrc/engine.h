@@ -213,6 +213,7 @@ void launch_inline_out(const Dev& d, const uint8_t* send, uint64_t cap, const un
 void launch_inline_in(const Dev& d, uint8_t* recv, uint64_t cap, const unsigned long long* scnt, unsigned long long* rcnt,
                       void* stream);
 void launch_kill(const Dev& d, uint32_t member, void* stream);
+void launch_user_gossips(const Dev& d, uint32_t k, const uint64_t* q, uint32_t n, void* stream);
 void launch_hash(const Dev& d, uint64_t* out, uint32_t now, void* stream);
 
 }  // namespace swim

@@ -579,8 +579,7 @@ __device__ __noinline__ bool blocked_pair(const Dev& d, uint32_t x, uint32_t y, 
 // tick of g filters it: nobody could send g before it existed)
 __device__ __forceinline__ bool blocked_pair_cached(const Dev& d, uint32_t x, uint32_t y, uint32_t g, uint64_t gid,
                                                     uint32_t tau, uint32_t cx, const uint32_t* rec) {
-  const uint32_t nall = rec[0];
-  if (nall > CEV) return blocked_pair(d, x, y, g, gid, tau, cx);
+  const uint32_t nall = rec[0];  // <= CEV: overflowed pairs go to k_gossip_send_slow
   const uint32_t born = d.slot_ctick[g];
   // only a delivery y -> x at or after x's incarnation start cx can put y in infectedFrom_x (most cached contacts
   // are older than the gossip)
@@ -637,11 +636,14 @@ __global__ void k_gossip_contacts(Dev d, uint32_t k) {
       rec[0] = n;
       rec[1] = oldest[0];
       rec[2] = oldest[1];
+      uint32_t last_in = NEVER;  // latest y -> x contact (NEVER: none); overflow is flagged by n alone
       if (n <= CEV)
         for (uint32_t j = 0; j < n; ++j) {
           rec[4 + 2 * j] = ev[j].tick;
           rec[5 + 2 * j] = ev[j].slot | (ev[j].dir << 8) | (ev[j].spread << 16);
+          if (ev[j].dir == 0) last_in = ev[j].tick;  // events are in tick order
         }
+      rec[3] = last_in;
     }
   }
   d.tcontact[i] = flag;
@@ -689,7 +691,7 @@ __device__ __forceinline__ void send_tail(const Dev& d, uint32_t g, uint32_t m, 
 // sends (selectGossipsToSend :239-250 + isInfected) and the sweep (:283-308). Consecutive blocks share the slot
 // group, so its holder rows stay in L2 for the random target reads. A pair whose cached contact list overflowed is
 // deferred to k_gossip_send_slow (the full replay needs a large stack).
-constexpr uint32_t GB = 16;
+constexpr uint32_t GB = 8, FMAX = 8;  // slots per work item; gossip fanout limit (swim_create)
 __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp, uint32_t k, const uint32_t* active,
                                                      const uint32_t* nactive) {
   const Dev& d = *dp;
@@ -697,6 +699,11 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
   const uint32_t na = *nactive, nr = *d.rn;
   const uint32_t rchunks = (nr + 255) / 256, gchunks = (na + GB - 1) / GB;
   unsigned long long sends = 0;
+  uint32_t st[3] = {0, 0, 0};  // SWIM_EXP & 4: held entries, in-window entries, replays
+  if ((d.exp & 4) && blockIdx.x == 0 && threadIdx.x == 0) {
+    atomicAdd(&d.ctr[11], (unsigned long long)na);
+    atomicAdd(&d.ctr[12], (unsigned long long)nr);
+  }
   for (uint32_t w = blockIdx.x; w < rchunks * gchunks; w += gridDim.x) {
     const uint32_t gc = w / rchunks, ri = (w % rchunks) * 256 + threadIdx.x;
     if (ri >= nr) continue;
@@ -704,33 +711,51 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
     const uint32_t per = d.tperiod[m], sp = d.tspread[m], fg = d.firstGossip[m];
     const uint32_t n = d.exp == 2 ? 0u : d.tcnt[m];
     const uint32_t g0 = gc * GB, gn = min(GB, na - g0);
+    // the round's targets and, per target, whether a cached contact can matter: cin = latest y -> x contact tick
+    // (NEVER: none; CIN_SLOW: the contact list overflowed)
+    constexpr uint32_t CIN_SLOW = NEVER - 1u;
+    uint32_t tt[FMAX], cin[FMAX];
+#pragma unroll
+    for (uint32_t s = 0; s < FMAX; ++s) {
+      tt[s] = s < n ? d.T[(size_t)m * d.F + s] : 0u;
+      cin[s] = NEVER;
+      if (s < n && d.exp != 1 && d.tcontact[(size_t)m * d.F + s]) {
+        const uint32_t* rec = d.cev + ((size_t)m * d.F + s) * CEVW;
+        cin[s] = rec[0] > CEV ? CIN_SLOW : rec[3];
+      }
+    }
     uint32_t e[GB];
 #pragma unroll
     for (uint32_t j = 0; j < GB; ++j) e[j] = j < gn ? d.S[(size_t)active[g0 + j] * d.N + m] : 0u;
-#pragma unroll
     for (uint32_t j = 0; j < GB; ++j) {
       if (!s_held(e[j])) continue;
+      if (d.exp & 4) st[0]++;
       const uint32_t g = active[g0 + j];
       uint32_t* Sg = d.S + (size_t)g * d.N;
       const uint32_t c = s_ctick(e[j]);
       const uint32_t infP = (fg == NEVER || c <= fg) ? 0u : (c - fg + d.gossip_t - 1) / d.gossip_t;  // rounds_before
       if (infP + sp >= per) {  // selectGossipsToSend window (:246)
         const uint64_t gid = d.slot_gid[g];
+        const uint32_t born = d.slot_ctick[g];
+        if (d.exp & 4) st[1]++;
         if (d.exp == 2) sends += d.tcnt[m];
-        for (uint32_t s = 0; s < n; ++s) {
+#pragma unroll
+        for (uint32_t s = 0; s < FMAX; ++s) {
+          if (s >= n) break;
           const size_t ms = (size_t)m * d.F + s;
-          const uint32_t t = d.T[ms];
-          if (d.exp != 1 && d.tcontact[ms]) {
-            const uint32_t* rec = d.cev + ms * CEVW;
-            if (rec[0] > CEV) {  // overflowed contact list: the full replay runs in k_gossip_send_slow
-              uint32_t i = wave_append(d.slow_n);
-              if (i < d.SLOWCAP)
-                d.slow[i] = ((uint64_t)g << 32) | (uint32_t)ms;
-              else
-                atomicOr(d.err, E_CONTACTS);
-              continue;
-            }
-            if (blocked_pair_cached(d, m, t, g, gid, k, c, rec)) continue;  // isInfected (:247)
+          const uint32_t t = tt[s];
+          if (cin[s] == CIN_SLOW) {  // overflowed contact list: the full replay runs in k_gossip_send_slow
+            uint32_t i = wave_append(d.slow_n);
+            if (i < d.SLOWCAP)
+              d.slow[i] = ((uint64_t)g << 32) | (uint32_t)ms;
+            else
+              atomicOr(d.err, E_CONTACTS);
+            continue;
+          }
+          // only a delivery y -> x at or after x's incarnation start c (and after g existed) can block the send
+          if (cin[s] != NEVER && cin[s] >= born && cin[s] + d.lat >= c) {
+            if (d.exp & 4) st[2]++;
+            if (blocked_pair_cached(d, m, t, g, gid, k, c, d.cev + ms * CEVW)) continue;  // isInfected (:247)
           }
           sends++;
           send_tail(d, g, m, s, t, k, gid, Sg);
@@ -751,6 +776,9 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
       }
     }
   }
+  if (d.exp & 4)
+    for (int q = 0; q < 3; ++q)
+      if (st[q]) atomicAdd(&d.ctr[8 + q], (unsigned long long)st[q]);
   red[threadIdx.x] = sends;
   __syncthreads();
   for (uint32_t o = 128; o > 0; o >>= 1) {

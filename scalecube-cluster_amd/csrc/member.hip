@@ -154,42 +154,67 @@ __device__ __forceinline__ void emit_event(ML& L, uint32_t type, uint32_t subj, 
   on_member_event(L, type, subj);
 }
 
-// GossipProtocolImpl.spread -> createAndPutGossip (:124-128,163-169): a new global gossip slot held by this member
-__device__ __forceinline__ void spread(ML& L, uint32_t subj, uint32_t st, uint32_t inc) {
-  const Dev& d = *L.d;
-  uint64_t gid = ((uint64_t)L.m << 32) | L.gCounter++;
+// createAndPutGossip (GossipProtocolImpl.java:163-169): a new global gossip slot held by member m since tick k
+__device__ __forceinline__ bool new_slot(const Dev& d, uint32_t m, uint32_t k, uint64_t gid, uint32_t subj, uint64_t key) {
   int pos = atomicSub(d.free_top, 1) - 1;
   if (pos < 0) {
     set_err(d, E_SLOTS);
-    return;
+    return false;
   }
   uint32_t g = d.free_list[pos];
   d.slot_gid[g] = gid;
   d.slot_subj[g] = subj;
-  d.slot_ctick[g] = L.k;
-  d.slot_key[g] = rec_key(st, inc);
+  d.slot_ctick[g] = k;
+  d.slot_key[g] = key;
   d.slot_holders[g] = 1;
   d.slot_used[g] = 1;
-  d.S[(size_t)g * L.N + L.m] = (L.k + 1u) & S_TICK_MASK;
-  L.held++;
-  L.c[C_GCREATED]++;
+  d.S[(size_t)g * d.N + m] = (k + 1u) & S_TICK_MASK;
   if (d.W > 1) {  // replicated on the other shards from exchange A
     uint32_t i = atomicAdd(&d.xn[0], 1u);
     if (i >= d.NSCAP) {
       set_err(d, E_XCAP);
-      return;
+      return true;
     }
     uint32_t* r = d.ns_rec + (size_t)i * NSW;
-    uint64_t key = d.slot_key[g];
     r[0] = g;
     r[1] = (uint32_t)gid;
     r[2] = (uint32_t)(gid >> 32);
     r[3] = subj;
-    r[4] = L.k;
+    r[4] = k;
     r[5] = (uint32_t)key;
     r[6] = (uint32_t)(key >> 32);
-    r[7] = L.m;
+    r[7] = m;
   }
+  return true;
+}
+
+// GossipProtocolImpl.spread -> createAndPutGossip (:124-128,163-169): a membership gossip held by this member
+__device__ __forceinline__ void spread(ML& L, uint32_t subj, uint32_t st, uint32_t inc) {
+  uint64_t gid = ((uint64_t)L.m << 32) | L.gCounter++;
+  if (!new_slot(*L.d, L.m, L.k, gid, subj, rec_key(st, inc))) return;
+  L.held++;
+  L.c[C_GCREATED]++;
+}
+
+// Cluster.spreadGossip (ClusterImpl.java:208-211) queued by swim_spread_gossip: user gossips of this shard's live
+// members, in call order, at P0 of tick k (before the member kernel loads gCounter / held). One thread: the order
+// of the gossip counters of one member must follow the calls.
+__global__ void k_user_gossips(Dev d, uint32_t k, const uint64_t* q, uint32_t n) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  unsigned long long created = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t m = (uint32_t)q[2 * i];
+    if (m < d.lo || m >= d.hi || dead_at(d, m, k)) continue;
+    const uint64_t gid = ((uint64_t)m << 32) | d.gCounter[m]++;
+    if (!new_slot(d, m, k, gid, USER_SUBJ, q[2 * i + 1])) continue;
+    d.held[m]++;
+    created++;
+  }
+  if (created) atomicAdd(&d.ctr[C_GCREATED], created);
+}
+
+void launch_user_gossips(const Dev& d, uint32_t k, const uint64_t* q, uint32_t n, void* stream) {
+  hipLaunchKernelGGL(k_user_gossips, dim3(1), dim3(64), 0, (hipStream_t)stream, d, k, q, n);
 }
 
 __device__ __forceinline__ uint32_t* grp(ML& L, int g) { return L.groups + (size_t)g * GREC; }
@@ -892,6 +917,10 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
     for (uint32_t q = 0; q < n; ++q) {
       uint32_t g = d.rc_slot[off + q];
       uint64_t key = d.slot_key[g];
+      if (d.slot_subj[g] == USER_SUBJ) {  // sink.next -> ClusterImpl.listenGossips (:213-216), not membership
+        emit_event(L, 3, (uint32_t)(d.slot_gid[g] >> 32), (uint32_t)key, (uint32_t)(key >> 32));
+        continue;
+      }
       L.c[C_R]++;
       update_membership(L, d.slot_subj[g], rec_status(key), rec_inc(key), R_GOSSIP, -1);
     }

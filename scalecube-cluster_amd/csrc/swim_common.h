@@ -18,6 +18,7 @@
 namespace swim {
 
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
+constexpr uint32_t USER_SUBJ = 0xFFFFFFFFu;  // slot subject of a user gossip (Cluster.spreadGossip): payload in the key
 constexpr uint32_t ST_ABSENT = 0, ST_ALIVE = 1, ST_SUSPECT = 2, ST_DEAD = 3;
 
 constexpr uint64_t KEY_MASK = (1ull << 34) - 1;  // inc | status

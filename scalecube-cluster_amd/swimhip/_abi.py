@@ -19,7 +19,7 @@ FLAG_RECORD_EVENTS = 1
 FLAG_PROFILE = 2
 FLAG_PROFILE_ALL = 4
 
-EV_ADDED, EV_REMOVED, EV_UPDATED = 0, 1, 2
+EV_ADDED, EV_REMOVED, EV_UPDATED, EV_GOSSIP = 0, 1, 2, 3
 META_NONE = 0xFFFFFFFF
 ST_ABSENT, ST_ALIVE, ST_SUSPECT, ST_DEAD = 0, 1, 2, 3
 HASH_WORDS = 6  # row, fd list, gossip list, events, gossips held, misc
@@ -112,6 +112,7 @@ SIGNATURES = {
     "swim_unblock_link": (C.c_int, [_H, C.c_uint32, C.c_uint32]),
     "swim_update_incarnation": (C.c_int, [_H, C.c_uint32]),
     "swim_leave": (C.c_int, [_H, C.c_uint32]),
+    "swim_spread_gossip": (C.c_int, [_H, C.c_uint32, C.c_uint64]),
     "swim_current_tick": (C.c_int, [_H, C.POINTER(C.c_uint64)]),
     "swim_read_row": (C.c_int, [_H, C.c_uint32, C.POINTER(C.c_uint64), C.c_size_t]),
     "swim_state_hash": (C.c_int, [_H, C.POINTER(C.c_uint64), C.c_size_t]),

@@ -28,7 +28,7 @@ class MembershipEvent:
     tick: int
     observer: int
     seq: int
-    type: str  # "ADDED" | "REMOVED" | "UPDATED"
+    type: str  # "ADDED" | "REMOVED" | "UPDATED" | "GOSSIP" (listenGossips: member = origin, metadata = payload lo / hi)
     member: int
     oldMetadata: Optional[int]
     newMetadata: Optional[int]
@@ -42,6 +42,13 @@ class MembershipEvent:
     def isUpdated(self):
         return self.type == "UPDATED"
 
+    def isGossip(self):
+        return self.type == "GOSSIP"
+
+    def payload(self):
+        """64-bit payload of a GOSSIP event (Cluster.spreadGossip message)."""
+        return (self.newMetadata << 32) | self.oldMetadata
+
 
 @dataclass(frozen=True)
 class MembershipRecord:
@@ -52,7 +59,7 @@ class MembershipRecord:
     suspicion_deadline: Optional[int]
 
 
-_TYPES = {_abi.EV_ADDED: "ADDED", _abi.EV_REMOVED: "REMOVED", _abi.EV_UPDATED: "UPDATED"}
+_TYPES = {_abi.EV_ADDED: "ADDED", _abi.EV_REMOVED: "REMOVED", _abi.EV_UPDATED: "UPDATED", _abi.EV_GOSSIP: "GOSSIP"}
 _STATUS = {_abi.ST_ALIVE: "ALIVE", _abi.ST_SUSPECT: "SUSPECT", _abi.ST_DEAD: "DEAD"}  # DEAD: a leaving member's own
 
 
@@ -127,6 +134,10 @@ class SimulatedCluster:
 
     def unblock_all(self):
         self._ck(self.lib.swim_unblock_all(self._h), "swim_unblock_all")
+
+    def spread_gossip(self, member, payload):
+        """Cluster.spreadGossip(message): a user gossip from member carrying a 64-bit payload (ClusterImpl.java:208)."""
+        self._ck(self.lib.swim_spread_gossip(self._h, member, int(payload) & (2**64 - 1)), "swim_spread_gossip")
 
     def leave(self, member):
         """Cluster.shutdown(): graceful leave (MembershipProtocolImpl.leaveCluster, ClusterImpl.doShutdown)."""
@@ -211,7 +222,11 @@ class SimulatedCluster:
             self._ck(self.lib.swim_drain_events(self._h, buf, cap, C.byref(n)), "swim_drain_events")
             for i in range(n.value):
                 e = buf[i]
-                out.append(MembershipEvent(e.tick, e.observer, e.seq, _TYPES[e.type], e.subject, _meta(e.old_meta),
-                                           _meta(e.new_meta)))
+                if e.type == _abi.EV_GOSSIP:  # payload words, not metadata versions
+                    out.append(MembershipEvent(e.tick, e.observer, e.seq, "GOSSIP", e.subject, int(e.old_meta),
+                                               int(e.new_meta)))
+                else:
+                    out.append(MembershipEvent(e.tick, e.observer, e.seq, _TYPES[e.type], e.subject,
+                                               _meta(e.old_meta), _meta(e.new_meta)))
             if n.value < cap:
                 return out

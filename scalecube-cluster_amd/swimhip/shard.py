@@ -243,6 +243,10 @@ class ThreadShardGroup:
         for s in self.shards:
             s.leave(m)
 
+    def spread_gossip(self, m, payload):
+        for s in self.shards:
+            s.spread_gossip(m, payload)
+
     def set_link_loss(self, src, dst, pct):
         for s in self.shards:
             s.set_link_loss(src, dst, pct)

@@ -47,6 +47,11 @@ def schedule(seed):
         else:
             acts.append(("unblock", (int(rng.integers(n)), [int(x) for x in rng.integers(n, size=3)])))
         acts.append(("run", int(rng.integers(20, 200))))
+    # user gossips (Cluster.spreadGossip) from a separate stream, so the fault schedules above stay as they were
+    rg = np.random.default_rng(seed + 10_000)
+    for _ in range(int(rg.integers(1, 4))):
+        pos = 1 + 2 * int(rg.integers(len(acts) // 2))
+        acts.insert(pos, ("gossip", [(int(rg.integers(n)), int(rg.integers(1 << 63))) for _ in range(int(rg.integers(1, 4)))]))
     return cfg, acts
 
 
@@ -58,6 +63,8 @@ def play(o, e, acts, where):
             continue
         if what in ("inc", "leave") and arg in dead:
             continue
+        if what == "gossip":
+            arg = [(m, p) for m, p in arg if m not in dead]
         for c in (o, e):
             if what == "loss":
                 c.set_default_loss(arg)
@@ -78,6 +85,9 @@ def play(o, e, acts, where):
                 c.block(arg[0], *arg[1])
             elif what == "unblock":
                 c.unblock(arg[0], *arg[1])
+            elif what == "gossip":
+                for m, p in arg:
+                    c.spread_gossip(m, p)
         if what in ("kill", "leave"):
             dead.add(arg)
 

@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 from swimhip import ClusterConfig, SimConfig, _abi
+from swimhip.cluster import SimulatedCluster
 
 from parity_util import assert_same, pair, run_lockstep
 
@@ -154,3 +155,40 @@ def test_graceful_leaves(oracle, engine):
         c.leave(91)
     ev = run_lockstep(o, e, 400, 50, "leave 8, 90, 91 under loss")
     assert {x.member for x in ev if x.isRemoved()} >= {8, 90, 91}
+
+
+def test_user_gossips(oracle, engine):
+    """Cluster.spreadGossip / listenGossips (ClusterImpl.java:208-216): user gossips beside the membership gossips,
+    two from one member in one tick, under loss, from a member that leaves meanwhile; GOSSIP events must match."""
+    cfg = SimConfig(n_members=90, record_events=True)
+    o, e = pair(oracle, engine, cfg)
+    run_lockstep(o, e, 12, 4, "warm")
+    for c in (o, e):
+        c.set_default_loss(10)
+        c.spread_gossip(3, 0xDEADBEEF00000001)
+        c.spread_gossip(3, 2)
+        c.spread_gossip(70, 3)
+        c.update_incarnation(3)
+    ev = run_lockstep(o, e, 80, 10, "three user gossips under loss")
+    for c in (o, e):
+        c.spread_gossip(9, 4)
+        c.leave(9)
+    ev += run_lockstep(o, e, 150, 25, "gossip then leave")
+    got = {}
+    for x in ev:
+        if x.isGossip():
+            got.setdefault(x.payload(), set()).add(x.observer)
+    assert got[0xDEADBEEF00000001] == set(range(90)) - {3}
+
+
+def test_user_gossips_sharded(oracle, engine):
+    from swimhip.shard import ThreadShardGroup
+    cfg = SimConfig(n_members=75, record_events=True)
+    o, e = SimulatedCluster(oracle, cfg), ThreadShardGroup(engine, cfg, 3)
+    run_lockstep(o, e, 8, 4, "warm W=3")
+    for c in (o, e):
+        c.set_default_loss(5)
+        for m in (1, 30, 31, 60):  # origins on every shard
+            c.spread_gossip(m, 1000 + m)
+    run_lockstep(o, e, 100, 20, "user gossips W=3")
+    e.close()

@@ -209,3 +209,43 @@ def test_gossip_dissemination(oracle, n, loss):  # GossipProtocolTest.testGossip
     for e in ev:
         per_observer[e.observer] = per_observer.get(e.observer, 0) + 1
     assert all(v == 1 for v in per_observer.values()), "double delivery"
+
+
+# GossipProtocolTest.experiments (:50-64) with mean delay 2 ms (delay is not modelled: one tick of latency); a user
+# gossip (Cluster.spreadGossip -> GossipProtocolImpl.spread) from member 0. Assertions of testGossipProtocol
+# (:150-175): all N-1 members receive it (listenGossips), within gossipTimeoutToSweep, and none twice.
+@pytest.mark.parametrize("n,loss", [(2, 0), (3, 0), (5, 0), (10, 0), (10, 10), (10, 25), (10, 50), (50, 0), (50, 10)])
+def test_user_gossip_experiments(oracle, n, loss):
+    c = SimulatedCluster(oracle, SimConfig(n_members=n, record_events=True))
+    c.set_default_loss(loss)
+    c.step(3)
+    c.spread_gossip(0, 0xC0FFEE00000000 | n)
+    t0 = c.tick
+    sweep_ticks = 2 * (3 * int(n).bit_length() + 1) * 2  # gossipTimeoutToSweep(3, n, 200 ms) in 100 ms ticks
+    c.step(sweep_ticks + 3 * 2)  # awaitFullCompletion: lifetime plus three gossip intervals
+    ev = [e for e in c.events() if e.isGossip()]
+    assert all(e.member == 0 and e.payload() == 0xC0FFEE00000000 | n for e in ev)
+    receivers = [e.observer for e in ev]
+    assert sorted(set(receivers)) == list(range(1, n)), "not all members received the gossip"
+    assert len(receivers) == len(set(receivers)), "delivered gossip twice to the same member"
+    assert max(e.tick for e in ev) - t0 < sweep_ticks, "dissemination slower than the gossip timeout"
+
+
+def test_user_gossips_order_and_dead_origin(oracle):
+    """Two gossips of one member in one tick keep call order in their ids; a killed member's queued gossip never
+    starts; swim_spread_gossip on a dead member is rejected."""
+    c = SimulatedCluster(oracle, SimConfig(n_members=20, record_events=True))
+    c.step(2)
+    c.spread_gossip(3, 1)
+    c.spread_gossip(3, 2)
+    c.spread_gossip(4, 3)
+    c.kill(4)
+    c.step(60)
+    got = {}
+    for e in c.events():
+        if e.isGossip():
+            got.setdefault(e.payload(), set()).add(e.observer)
+    assert got[1] == got[2] == set(range(20)) - {3, 4}
+    assert 3 not in got
+    with pytest.raises(Exception):
+        c.spread_gossip(4, 9)
