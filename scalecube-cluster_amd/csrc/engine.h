@@ -32,6 +32,7 @@ constexpr uint32_t E_SLOTS = 1, E_FETCH = 2, E_SUBS = 4, E_PATHS = 8, E_GROUPS =
 // per-link NetworkEmulator settings (setLinkSettings / block / unblock): hash of (src, dst) -> change history
 constexpr uint32_t LKCAP = 4096, LKH = 8;  // keys, history entries per key
 constexpr uint32_t DEATHCAP = 4096;        // completed leaves per tick
+constexpr uint32_t CIN_SLOW = 0xFFFFFFFEu;
 constexpr uint32_t CEV = 6, CEVW = 4 + 2 * CEV;  // cached contact events per (sender, target): n, oldest[2], events
 // gossip incarnation history entry: 3 header words + HKEEP creation ticks of swept incarnations (small clusters
 // under loss re-infect a member with the same gossip many times: each late sender restarts the chain)
@@ -97,6 +98,8 @@ struct Dev {
   uint32_t* slow_n;
   uint32_t SLOWCAP;
   uint32_t *rlist, *rn;  // [N] members with a gossip round this tick (built by k_gossip_contacts)
+  uint32_t* cin;    // [N][F] latest cached contact t -> m of (m, T[m][s]); NEVER: none, CIN_SLOW: list overflowed
+  uint32_t* swthr;  // [N] round sweep bound of this tick (k_round_info)
   uint32_t* cev;  // [N][F][CEVW] contact events of (m, T[m][s]) cached by k_gossip_contacts when tcontact is set
   uint32_t *log_tick, *log_spread, *log_cnt, *log_tg, *log_pos;  // [N][LOGW], tg [N][LOGW][F], pos [N]
 

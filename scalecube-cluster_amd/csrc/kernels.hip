@@ -611,6 +611,20 @@ __global__ void k_gossip_active(Dev d, uint32_t k, uint32_t* active, uint32_t* n
   active[atomicAdd(nactive, 1u)] = g;
 }
 
+// per member (all N, every shard): swthr = creation-tick bound of the gossips it sweeps in its round this tick
+// (sweepGossips :283-308): sweeps g iff rounds_before(c) < P = period - 2 (spread + 1) iff c < swthr; 0 = sweeps none
+__global__ void k_round_info(Dev d) {
+  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= d.N) return;
+  uint32_t thr = 0;
+  if (d.tround[m]) {
+    const int64_t P = (int64_t)d.tperiod[m] - 2 * ((int64_t)d.tspread[m] + 1);
+    const uint32_t f = d.firstGossip[m];
+    if (P >= 1) thr = f == NEVER ? NEVER : (uint32_t)min<int64_t>((int64_t)NEVER, (int64_t)f + (P - 1) * d.gossip_t + 1);
+  }
+  d.swthr[m] = thr;
+}
+
 // contact lists: did target t = T[m][s] choose m in a logged round inside the look-back window? If so, cache the
 // pair's contact events in both directions (independent of the gossip) for blocked_pair_cached
 __global__ void k_gossip_contacts(Dev d, uint32_t k) {
@@ -644,9 +658,11 @@ __global__ void k_gossip_contacts(Dev d, uint32_t k) {
           if (ev[j].dir == 0) last_in = ev[j].tick;  // events are in tick order
         }
       rec[3] = last_in;
+      d.cin[i] = n > CEV ? CIN_SLOW : last_in;
     }
   }
   d.tcontact[i] = flag;
+  if (!flag) d.cin[i] = NEVER;
   if (s == 0 && d.tround[m]) {  // compact list of this tick's round members (k_gossip_send iterates over it)
     uint32_t r = wave_append(d.rn);
     d.rlist[r] = m;
@@ -669,12 +685,8 @@ __device__ __forceinline__ void send_tail(const Dev& d, uint32_t g, uint32_t m, 
     }
   }
   uint32_t et = Sg[t];
-  bool potential = !s_held(et);
-  if (!potential && d.tround[t]) {  // t sweeps g in its own round this tick -> a delivery re-creates it
-    uint32_t it = rounds_before(d, t, s_ctick(et));
-    potential = d.tperiod[t] > it + 2u * (d.tspread[t] + 1u);
-  }
-  if (!potential) return;
+  // potential unless t holds g and does not sweep it in its own round this tick (a delivery would re-create it)
+  if (s_held(et) && !(s_ctick(et) < d.swthr[t])) return;
   if (lost_gossip(d, m, t, k, s, gid)) return;
   uint32_t old = atomicOr(&Sg[t], S_PENDING);
   if (!(old & S_PENDING)) {
@@ -686,106 +698,121 @@ __device__ __forceinline__ void send_tail(const Dev& d, uint32_t g, uint32_t m, 
   }
 }
 
-// Work item = (256 round members of this tick, GB active slots). Each thread loads its member's round once and
-// the member's GB holder entries as independent loads (memory-level parallelism), then per held slot: the round
-// sends (selectGossipsToSend :239-250 + isInfected) and the sweep (:283-308). Consecutive blocks share the slot
-// group, so its holder rows stay in L2 for the random target reads. A pair whose cached contact list overflowed is
+// One block per group of gs active slots (grid-stride). The block first turns each slot's holder row into an LDS
+// bitmap of the members that hold it past this tick (held and not sweeping it in their own round: swthr), streaming
+// the rows once, coalesced. Then each round member of this tick loads its round (targets, cached contact bounds)
+// once and, for every slot of the group it holds in its window, sends it (selectGossipsToSend :239-250) to each
+// target not in infectedFrom (cached contact replay); only targets outside the bitmap can be first receipts, so
+// the per-send work is an LDS lookup. Then the member's sweep (:283-308). A pair whose contact list overflowed is
 // deferred to k_gossip_send_slow (the full replay needs a large stack).
-constexpr uint32_t GB = 8, FMAX = 8;  // slots per work item; gossip fanout limit (swim_create)
+constexpr uint32_t GSMAX = 8, FMAX = 8;  // slots per block group; gossip fanout limit (swim_create)
 __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp, uint32_t k, const uint32_t* active,
-                                                     const uint32_t* nactive) {
+                                                     const uint32_t* nactive, uint32_t gs) {
   const Dev& d = *dp;
-  __shared__ unsigned long long red[256];
-  const uint32_t na = *nactive, nr = *d.rn;
-  const uint32_t rchunks = (nr + 255) / 256, gchunks = (na + GB - 1) / GB;
+  extern __shared__ unsigned long long hb[];  // [gs][ceil(N / 64)] holder bitmaps of the group's slots
+  __shared__ unsigned long long red[4];
+  __shared__ uint32_t sg[GSMAX], sborn[GSMAX];
+  __shared__ uint64_t sgid[GSMAX];
+  const uint32_t na = *nactive, nr = *d.rn, nw = (d.N + 63) / 64, ngroups = (na + gs - 1) / gs;
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   unsigned long long sends = 0;
-  uint32_t st[3] = {0, 0, 0};  // SWIM_EXP & 4: held entries, in-window entries, replays
-  if ((d.exp & 4) && blockIdx.x == 0 && threadIdx.x == 0) {
-    atomicAdd(&d.ctr[11], (unsigned long long)na);
-    atomicAdd(&d.ctr[12], (unsigned long long)nr);
-  }
-  for (uint32_t w = blockIdx.x; w < rchunks * gchunks; w += gridDim.x) {
-    const uint32_t gc = w / rchunks, ri = (w % rchunks) * 256 + threadIdx.x;
-    if (ri >= nr) continue;
-    const uint32_t m = d.rlist[ri];
-    const uint32_t per = d.tperiod[m], sp = d.tspread[m], fg = d.firstGossip[m];
-    const uint32_t n = d.exp == 2 ? 0u : d.tcnt[m];
-    const uint32_t g0 = gc * GB, gn = min(GB, na - g0);
-    // the round's targets and, per target, whether a cached contact can matter: cin = latest y -> x contact tick
-    // (NEVER: none; CIN_SLOW: the contact list overflowed)
-    constexpr uint32_t CIN_SLOW = NEVER - 1u;
-    uint32_t tt[FMAX], cin[FMAX];
-#pragma unroll
-    for (uint32_t s = 0; s < FMAX; ++s) {
-      tt[s] = s < n ? d.T[(size_t)m * d.F + s] : 0u;
-      cin[s] = NEVER;
-      if (s < n && d.exp != 1 && d.tcontact[(size_t)m * d.F + s]) {
-        const uint32_t* rec = d.cev + ((size_t)m * d.F + s) * CEVW;
-        cin[s] = rec[0] > CEV ? CIN_SLOW : rec[3];
+  for (uint32_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    const uint32_t a0 = grp * gs, gn = min(gs, na - a0);
+    if (threadIdx.x < gn) {
+      const uint32_t g = active[a0 + threadIdx.x];
+      sg[threadIdx.x] = g;
+      sgid[threadIdx.x] = d.slot_gid[g];
+      sborn[threadIdx.x] = d.slot_ctick[g];
+    }
+    for (uint32_t base = 0; base < d.N; base += 256) {
+      const uint32_t t = base + threadIdx.x;
+      const uint32_t thr = t < d.N ? d.swthr[t] : 0u;
+      for (uint32_t j = 0; j < gn; ++j) {
+        bool keep = false;
+        if (t < d.N) {
+          const uint32_t e = d.S[(size_t)active[a0 + j] * d.N + t];
+          keep = s_held(e) && !(s_ctick(e) < thr);
+        }
+        const unsigned long long w = __ballot(keep);
+        if (lane == 0 && base / 64 + wave < nw) hb[j * nw + base / 64 + wave] = w;
       }
     }
-    uint32_t e[GB];
-#pragma unroll
-    for (uint32_t j = 0; j < GB; ++j) e[j] = j < gn ? d.S[(size_t)active[g0 + j] * d.N + m] : 0u;
-    for (uint32_t j = 0; j < GB; ++j) {
-      if (!s_held(e[j])) continue;
-      if (d.exp & 4) st[0]++;
-      const uint32_t g = active[g0 + j];
-      uint32_t* Sg = d.S + (size_t)g * d.N;
-      const uint32_t c = s_ctick(e[j]);
-      const uint32_t infP = (fg == NEVER || c <= fg) ? 0u : (c - fg + d.gossip_t - 1) / d.gossip_t;  // rounds_before
-      if (infP + sp >= per) {  // selectGossipsToSend window (:246)
-        const uint64_t gid = d.slot_gid[g];
-        const uint32_t born = d.slot_ctick[g];
-        if (d.exp & 4) st[1]++;
-        if (d.exp == 2) sends += d.tcnt[m];
-#pragma unroll
-        for (uint32_t s = 0; s < FMAX; ++s) {
-          if (s >= n) break;
-          const size_t ms = (size_t)m * d.F + s;
-          const uint32_t t = tt[s];
-          if (cin[s] == CIN_SLOW) {  // overflowed contact list: the full replay runs in k_gossip_send_slow
-            uint32_t i = wave_append(d.slow_n);
-            if (i < d.SLOWCAP)
-              d.slow[i] = ((uint64_t)g << 32) | (uint32_t)ms;
-            else
-              atomicOr(d.err, E_CONTACTS);
-            continue;
-          }
-          // only a delivery y -> x at or after x's incarnation start c (and after g existed) can block the send
-          if (cin[s] != NEVER && cin[s] >= born && cin[s] + d.lat >= c) {
-            if (d.exp & 4) st[2]++;
-            if (blocked_pair_cached(d, m, t, g, gid, k, c, d.cev + ms * CEVW)) continue;  // isInfected (:247)
-          }
-          sends++;
-          send_tail(d, g, m, s, t, k, gid, Sg);
-        }
-      }
-      if (per > infP + 2u * (sp + 1u)) {  // sweepGossips (:283-308)
-        atomicOr(&Sg[m], S_SWEPT);
-        atomicSub(&d.held[m], 1u);
-        atomicSub(&d.slot_holders[g], 1);
-        on_sweep(d, g, m, k);
-        if (d.W > 1) {  // applied on the other shards from exchange B
-          uint32_t i = atomicAdd(&d.xn[2], 1u);
-          if (i < d.SWCAP)
-            d.sw_rec[i] = ((uint64_t)g << 32) | m;
-          else
-            atomicOr(d.err, E_XCAP);
-        }
-      }
-    }
-  }
-  if (d.exp & 4)
-    for (int q = 0; q < 3; ++q)
-      if (st[q]) atomicAdd(&d.ctr[8 + q], (unsigned long long)st[q]);
-  red[threadIdx.x] = sends;
-  __syncthreads();
-  for (uint32_t o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
     __syncthreads();
+    for (uint32_t ri = threadIdx.x; ri < nr; ri += 256) {
+      const uint32_t m = d.rlist[ri];
+      uint32_t e[GSMAX];
+#pragma unroll
+      for (uint32_t j = 0; j < GSMAX; ++j) e[j] = j < gn ? d.S[(size_t)sg[j] * d.N + m] : 0u;
+      const uint32_t per = d.tperiod[m], sp = d.tspread[m], fg = d.firstGossip[m], n = d.tcnt[m];
+      uint32_t tt[FMAX], ci[FMAX];
+#pragma unroll
+      for (uint32_t s = 0; s < FMAX; ++s) {
+        tt[s] = s < n ? d.T[(size_t)m * d.F + s] : 0u;
+        ci[s] = s < n ? d.cin[(size_t)m * d.F + s] : NEVER;
+      }
+      for (uint32_t j = 0; j < gn; ++j) {
+        if (!s_held(e[j])) continue;
+        const uint32_t g = sg[j];
+        uint32_t* Sg = d.S + (size_t)g * d.N;
+        const uint32_t c = s_ctick(e[j]);
+        const uint32_t infP = (fg == NEVER || c <= fg) ? 0u : (c - fg + d.gossip_t - 1) / d.gossip_t;  // rounds_before
+        if (infP + sp >= per) {  // selectGossipsToSend window (:246)
+          const uint64_t gid = sgid[j];
+          const uint32_t born = sborn[j];
+          const unsigned long long* hbj = hb + j * nw;
+#pragma unroll
+          for (uint32_t s = 0; s < FMAX; ++s) {
+            if (s >= n) break;
+            const size_t ms = (size_t)m * d.F + s;
+            const uint32_t t = tt[s];
+            if (ci[s] == CIN_SLOW) {  // overflowed contact list: the full replay runs in k_gossip_send_slow
+              uint32_t i = wave_append(d.slow_n);
+              if (i < d.SLOWCAP)
+                d.slow[i] = ((uint64_t)g << 32) | (uint32_t)ms;
+              else
+                atomicOr(d.err, E_CONTACTS);
+              continue;
+            }
+            // only a delivery t -> m at or after m's incarnation start c (and after g existed) can block the send
+            if (ci[s] != NEVER && ci[s] >= born && ci[s] + d.lat >= c &&
+                blocked_pair_cached(d, m, t, g, gid, k, c, d.cev + ms * CEVW))
+              continue;  // isInfected (:247)
+            sends++;
+            if (d.dbg_send || !((hbj[t >> 6] >> (t & 63u)) & 1ull)) send_tail(d, g, m, s, t, k, gid, Sg);
+          }
+        }
+        if (per > infP + 2u * (sp + 1u)) {  // sweepGossips (:283-308)
+          atomicOr(&Sg[m], S_SWEPT);
+          atomicSub(&d.held[m], 1u);
+          atomicSub(&d.slot_holders[g], 1);
+          on_sweep(d, g, m, k);
+          if (d.W > 1) {  // applied on the other shards from exchange B
+            uint32_t i = atomicAdd(&d.xn[2], 1u);
+            if (i < d.SWCAP)
+              d.sw_rec[i] = ((uint64_t)g << 32) | m;
+            else
+              atomicOr(d.err, E_XCAP);
+          }
+        }
+      }
+    }
+    __syncthreads();  // the bitmaps and slot ids are rebuilt for the next group
   }
-  if (threadIdx.x == 0 && red[0]) atomicAdd(&d.ctr[C_G], red[0]);
+  for (uint32_t o = 32; o > 0; o >>= 1) sends += __shfl_xor(sends, o);
+  if (lane == 0) red[wave] = sends;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long tot = red[0] + red[1] + red[2] + red[3];
+    if (tot) atomicAdd(&d.ctr[C_G], tot);
+  }
+}
+
+// slots per k_gossip_send block: as many holder bitmaps as fit in 64 KB of LDS, at most GSMAX
+static uint32_t send_group(const Dev& d) {
+  static const char* ev = getenv("SWIM_SEND_GROUP");  // tuning knob
+  const uint64_t bytes = (uint64_t)(d.N + 63) / 64 * 8;
+  const uint64_t want = ev ? (uint64_t)atoi(ev) : 1;
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(std::min<uint64_t>(GSMAX, want), (64ull << 10) / bytes));
 }
 
 // deferred sends whose pair had more contact events than the cache holds (small clusters): full log scan + replay
@@ -986,9 +1013,11 @@ constexpr uint32_t SEND_GRID = 2048;  // 8 blocks per CU: the send loop is laten
 void launch_gossip(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(k_gossip_active, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, st, d, k, d.active, d.nactive);
+  hipLaunchKernelGGL(k_round_info, dim3(cdiv(d.N, 256)), dim3(256), 0, st, d);
   hipLaunchKernelGGL(k_gossip_contacts, dim3(cdiv((uint64_t)d.NL * d.F, 256)), dim3(256), 0, st, d, k);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[4], st);
-  hipLaunchKernelGGL(k_gossip_send, dim3(SEND_GRID), dim3(256), 0, st, d.self, k, d.active, d.nactive);
+  hipLaunchKernelGGL(k_gossip_send, dim3(SEND_GRID), dim3(256), (size_t)(d.N + 63) / 64 * 8 * send_group(d), st, d.self, k,
+                     d.active, d.nactive, send_group(d));
   hipLaunchKernelGGL(k_gossip_send_slow, dim3(256), dim3(256), 0, st, d.self, k);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[5], st);
   hipLaunchKernelGGL(k_gossip_apply, dim3(1024), dim3(256), 0, st, d, k);
@@ -1036,9 +1065,11 @@ void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
     return;
   }
   hipLaunchKernelGGL(k_gossip_active, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, st, d, k, d.active, d.nactive);
+  hipLaunchKernelGGL(k_round_info, dim3(cdiv(d.N, 256)), dim3(256), 0, st, d);
   hipLaunchKernelGGL(k_gossip_contacts, dim3(cdiv((uint64_t)d.NL * d.F, 256)), dim3(256), 0, st, d, k);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[4], st);
-  hipLaunchKernelGGL(k_gossip_send, dim3(SEND_GRID), dim3(256), 0, st, d.self, k, d.active, d.nactive);
+  hipLaunchKernelGGL(k_gossip_send, dim3(SEND_GRID), dim3(256), (size_t)(d.N + 63) / 64 * 8 * send_group(d), st, d.self, k,
+                     d.active, d.nactive, send_group(d));
   hipLaunchKernelGGL(k_gossip_send_slow, dim3(256), dim3(256), 0, st, d.self, k);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[5], st);
   hipLaunchKernelGGL(k_pack_b, dim3(64, d.W), dim3(256), 0, st, d);
