@@ -41,8 +41,11 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=30, help="timed FD periods")
     p.add_argument("--warmup", type=int, default=3, help="untimed FD periods")
-    p.add_argument("--members", type=int, default=100_000)
-    p.add_argument("--loss", type=int, default=0)
+    p.add_argument("--workload", choices=["c3", "c2", "c5"], default="c3",
+                   help="c3 (default, the headline): 100k full views; c2: 10k full views with 5%% loss; "
+                        "c5: rumor-only (SWIM_MODE_RUMOR) with 1%% churn per period")
+    p.add_argument("--members", type=int, default=None, help="default: 100k (c3, c5), 10k (c2)")
+    p.add_argument("--loss", type=int, default=None, help="default: 5 (c2), 0 otherwise")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-members", type=int, default=10_000)
     p.add_argument("--cpu-periods", type=int, default=60)
@@ -68,7 +71,13 @@ def traffic_from_profiles(n_members):
     return None
 
 
-def cpu_baseline(members, periods):
+def workload_config(a, SimConfig, _abi, members, **kw):
+    if a.workload == "c5":
+        return SimConfig(n_members=members, mode=_abi.MODE_RUMOR, churn_per_period=max(1, members // 100), **kw)
+    return SimConfig(n_members=members, **kw)
+
+
+def cpu_baseline(a, members, periods):
     """Bounded CPU sample: the oracle on the same workload shape at `members` members, one thread."""
     from swimhip import SimConfig, SimulatedCluster, _abi
     lib_path = ROOT / "oracle" / "liboracle_swimref.so"
@@ -76,16 +85,29 @@ def cpu_baseline(members, periods):
         import subprocess
         subprocess.check_call(["make", "-s", "-C", str(ROOT / "oracle")])
     lib = _abi.load(lib_path)
-    c = SimulatedCluster(lib, SimConfig(n_members=members))
+    c = SimulatedCluster(lib, workload_config(a, SimConfig, _abi, members))
+    if a.loss:
+        c.set_default_loss(a.loss)
     c.run_periods(1)
     t0 = time.perf_counter()
     c.run_periods(periods)
     dt = time.perf_counter() - t0
     c.close()
+    note = {"c3": "per-member work grows ~linearly with N (SYNC payloads), so at 100k it is ~10x slower per "
+                  "member·period",
+            "c2": "per-member gossip load grows ~N (SYNC re-spread storm), so at 10k it is far slower per member·period",
+            "c5": "per-member rumor load grows ~N at 1 % churn, so at full N it is slower per member·period"}[a.workload]
     return {"value": members * periods / dt, "unit": "member·periods/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/swimref.cpp, {members} members (same C3 shape, 1/10 of N), {periods} periods "
-                      f"after 1 warm-up period, {dt:.1f} s; per-member work grows ~linearly with N (SYNC payloads), "
-                      f"so at 100k it is ~10x slower per member·period"}
+            "sample": f"oracle/swimref.cpp, {members} members (same {a.workload.upper()} shape, reduced N), {periods} "
+                      f"periods after 1 warm-up period, {dt:.1f} s; {note}"}
+
+
+def workload_name(a, n):
+    if a.workload == "c3":
+        return BASELINE_WORKLOAD if (n == 100_000 and not a.loss) else f"{n} members, full views, loss {a.loss}%"
+    if a.workload == "c2":
+        return f"C2: {n} members, full views, preconverged, loss {a.loss}%"
+    return f"C5 (reduced N): {n} members, rumor-only, {max(1, n // 100)} churn rumors per period, loss {a.loss}%"
 
 
 def main():
@@ -104,7 +126,11 @@ def main():
     import swimhip
     from swimhip import SimConfig, _abi
 
-    cfg = SimConfig(n_members=a.members, device=local, profile=not a.no_events)
+    if a.members is None:
+        a.members = 10_000 if a.workload == "c2" else 100_000
+    if a.loss is None:
+        a.loss = 5 if a.workload == "c2" else 0
+    cfg = workload_config(a, SimConfig, _abi, a.members, device=local, profile=not a.no_events)
     if world > 1:
         import torch.distributed as dist
         from swimhip.shard import GlooExchange, ShardedCluster, rccl_unique_id
@@ -164,7 +190,7 @@ def main():
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic (PRECONVERGED full views, seeded Philox selector)",
-            "config": {"workload": BASELINE_WORKLOAD if (n == 100_000 and not a.loss) else f"{n} members, loss {a.loss}%",
+            "config": {"workload": workload_name(a, n),
                        "members": n, "periods_per_step": 1, "ticks_per_period": 10,
                        "parallelism": f"row-sharded x{world} ({a.transport})" if world > 1 else "single-gpu"},
             "roofline": {"bound": "hbm", "kernel": "k_sync_diff", "achieved": achieved, "peak": HBM_PEAK_GBPS,
@@ -179,8 +205,15 @@ def main():
             "device_bytes": ctr["device_bytes"],
             "exchange_ms_per_step": d["exchange_ns"] * 1e-6 / a.steps,
         }
+        if a.workload != "c3":  # the gossip plane dominates: whole-step algorithmic bytes against HBM
+            line["metric"] = f"member·periods/sec, {a.workload.upper()} workload (not the headline)"
+            line["roofline"] = {"bound": "hbm", "kernel": "whole step (k_gossip_send dominates)",
+                                "achieved": B / dt / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                                "frac": B / dt / 1e9 / HBM_PEAK_GBPS, "traffic": None}
+            line["kernel_time_share"] = {}
         if not a.no_cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline(a.cpu_members, a.cpu_periods)
+            cm, cp = {"c3": (a.cpu_members, a.cpu_periods), "c2": (500, 6), "c5": (2000, 10)}[a.workload]
+            line["cpu_baseline"] = cpu_baseline(a, cm, cp)
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)

@@ -42,6 +42,7 @@ extern "C" {
 
 /* mode */
 #define SWIM_MODE_FULL 0u
+#define SWIM_MODE_RUMOR 1u /* gossip layer only (SEMANTICS.md §9): no FD, SYNC or metadata; churn_per_period rumors per period */
 
 /* event types: MembershipEvent.Type (membership/MembershipEvent.java:13-17) */
 #define SWIM_EV_ADDED 0u
@@ -88,7 +89,8 @@ typedef struct swim_config {
   uint32_t n_gpus;            /* 1 for now */
   uint32_t device;            /* first HIP device */
   uint32_t list_slack;        /* FD / gossip list entries beyond N (duplicates after reordered ADDED / REMOVED) */
-  uint32_t reserved[6];
+  uint32_t churn_per_period;  /* SWIM_MODE_RUMOR: churn events (one rumor each) drawn at the start of every FD period */
+  uint32_t reserved[5];
 } swim_config;
 
 typedef struct swim_event {

@@ -856,6 +856,21 @@ void Sim::run_tick() {
   for (auto& m : arrived) inbox[m.dst].push_back(std::move(m));
   if (k == 0 && cfg.init_mode == SWIM_INIT_COLD_JOIN)
     for (auto& m : members) m.start(0);
+  if (cfg.mode == SWIM_MODE_RUMOR && cfg.churn_per_period && k % ping_t == 0) {
+    // churn of period p (SEMANTICS.md §9): event i picks a churned member v and a live origin o != v, which spreads
+    // the rumor (p << 32 | v) at P0, before the user gossips queued by the host, in event order
+    const uint32_t p = (uint32_t)(k / ping_t);
+    std::vector<std::vector<uint64_t>> add(N);
+    for (uint32_t i = 0; i < cfg.churn_per_period; ++i) {
+      P4 r = philox4x32_10(p, i, 0, 0, seed_lo ^ SALT_CHURN, seed_hi);
+      const uint32_t v = next_int(r.v[0], N);
+      uint32_t o = next_int(r.v[1], N - 1);
+      o += o >= v ? 1u : 0u;
+      if (members[o].alive) add[o].push_back(((uint64_t)p << 32) | v);
+    }
+    for (uint32_t o = 0; o < N; ++o)
+      if (!add[o].empty()) members[o].pendingUser.insert(members[o].pendingUser.begin(), add[o].begin(), add[o].end());
+  }
   for (uint32_t i = 0; i < N; ++i)
     if (members[i].alive) members[i].process(k, inbox[i]);
   for (uint32_t m : leaving_done) {  // as swim_kill between this tick and the next
@@ -914,6 +929,7 @@ __attribute__((visibility("default"))) int swim_create(const swim_config* cfg, s
   if (c.n_members < 1 || c.tick_ms == 0 || c.latency_ticks == 0) return SWIM_EINVAL;
   if (c.ping_timeout_ms >= c.ping_interval_ms) return SWIM_EINVAL;  // ClusterConfig.java:413-415
   if (c.gossip_fanout == 0 || c.gossip_fanout > 8 || c.n_seeds > 16) return SWIM_EINVAL;
+  if (c.mode > SWIM_MODE_RUMOR || (c.mode == SWIM_MODE_RUMOR && c.init_mode != SWIM_INIT_PRECONVERGED)) return SWIM_EINVAL;
   auto* h = new swim_handle();
   if (const char* lp = getenv("SWIMREF_SEND_LOG")) h->sim.send_log = fopen(lp, "w");
   Sim& s = h->sim;
@@ -974,6 +990,7 @@ __attribute__((visibility("default"))) int swim_create(const swim_config* cfg, s
       mb.nextPing = 1 + s.init_draw(m, 1, 0) % s.ping_t;
       mb.nextGossip = 1 + s.init_draw(m, 2, 0) % s.gossip_t;
       mb.nextSync = 1 + s.init_draw(m, 3, 0) % s.sync_t;
+      if (c.mode == SWIM_MODE_RUMOR) mb.nextPing = mb.nextSync = NEVER;  // gossip layer only (SEMANTICS.md §9)
     }
   }
   *out = h;

@@ -203,6 +203,8 @@ int build(swim_handle* h) {
   d.seed_lo = (uint32_t)c.seed;
   d.seed_hi = (uint32_t)(c.seed >> 32);
   d.init_mode = c.init_mode;
+  d.mode = c.mode;
+  d.churn = c.mode == SWIM_MODE_RUMOR ? c.churn_per_period : 0u;
   d.flags = c.flags;
   d.exp = getenv("SWIM_EXP") ? (uint32_t)atoi(getenv("SWIM_EXP")) : 0u;  // timing experiments: wrong results
   // seeds: LinkedHashSet of valid ids (MembershipProtocolImpl.java:160-166); self is skipped per member
@@ -254,7 +256,7 @@ int build(swim_handle* h) {
   const uint64_t NL = d.NL;  // per-observer arrays: this shard's rows only
   A(d.row, NL * d.NS) A(d.fdl, NL * d.LCAP) A(d.gl, NL * d.LCAP)
   A(d.subs, NL * SUBCAP * 4) A(d.paths, NL * PATHCAP * 5) A(d.fetch, NL * d.FCAP * FREC) A(d.groups, NL * d.GRCAP * GREC)
-  A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.slow, d.SLOWCAP) A(d.slow_n, 1) A(d.rlist, N) A(d.rn, 1) A(d.cin, N * d.F) A(d.swthr, N) A(d.cev, N * d.F * CEVW)
+  A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.slow, d.SLOWCAP) A(d.slow_n, 1) A(d.rlist, N) A(d.rn, 1) A(d.churn_q, 2ull * d.churn) A(d.cin, N * d.F) A(d.swthr, N) A(d.cev, N * d.F * CEVW)
   A(d.log_tick, N * d.LOGW) A(d.log_spread, N * d.LOGW) A(d.log_cnt, N * d.LOGW) A(d.log_tg, N * d.LOGW * d.F)
   A(d.log_pos, N) A(d.spchg, N)
   A(d.slot_gid, d.SLOTS) A(d.slot_subj, d.SLOTS) A(d.slot_ctick, d.SLOTS) A(d.slot_key, d.SLOTS) A(d.slot_holders, d.SLOTS)
@@ -440,7 +442,8 @@ int create(const swim_config* cfg, const swim_shard_spec* spec, swim_handle** ou
   *out = nullptr;
   const swim_config& c = *cfg;
   if (c.n_members < 2 || c.n_members > (1u << 20) || c.ping_timeout_ms >= c.ping_interval_ms || c.gossip_fanout == 0 || c.gossip_fanout > 8 ||
-      c.ping_req_members > 8 || c.n_seeds > 16 || c.mode != SWIM_MODE_FULL)
+      c.ping_req_members > 8 || c.n_seeds > 16 || c.mode > SWIM_MODE_RUMOR ||
+      (c.mode == SWIM_MODE_RUMOR && c.init_mode != SWIM_INIT_PRECONVERGED))
     return SWIM_EINVAL;
   if (c.latency_ticks != 1) return SWIM_EUNSUPPORTED;  // gossip data plane assumes one-tick hops
   if (spec) {
@@ -567,21 +570,23 @@ int swim_step(swim_handle* h, uint32_t n) {
     }
   uint64_t first = h->tick;
   const Dev& d = h->d;
-  if (n > 0 && !h->ugq.empty()) {  // user gossips queued since the last step: P0 of this step's first tick
-    const size_t pairs = h->ugq.size() / 2;
-    if (pairs > h->ug_cap) {
-      int rc;
-      h->ug_cap = std::max<size_t>(pairs, 1024);
-      if ((rc = dalloc(h, &h->ug_dev, 2 * h->ug_cap)) != SWIM_OK) return rc;
-    }
-    HIPCK(hipMemcpyAsync(h->ug_dev, h->ugq.data(), h->ugq.size() * 8, hipMemcpyHostToDevice, h->stream));
-    launch_user_gossips(d, (uint32_t)h->tick, h->ug_dev, (uint32_t)pairs, h->stream);
-    HIPCK(hipStreamSynchronize(h->stream));  // the host queue is reused after this
-    h->ugq.clear();
-  }
   for (uint32_t i = 0; i < n; ++i) {
     const TickEvents* te = profile ? &h->prof[i] : nullptr;
     const uint32_t k = (uint32_t)h->tick;
+    // P0 gossip creations before the member kernel: RUMOR-mode churn rumors, then the user gossips queued by the host
+    if (d.churn && k % d.ping_t == 0) launch_churn(d, k, h->stream);
+    if (i == 0 && !h->ugq.empty()) {
+      const size_t pairs = h->ugq.size() / 2;
+      if (pairs > h->ug_cap) {
+        int rc;
+        h->ug_cap = std::max<size_t>(pairs, 1024);
+        if ((rc = dalloc(h, &h->ug_dev, 2 * h->ug_cap)) != SWIM_OK) return rc;
+      }
+      HIPCK(hipMemcpyAsync(h->ug_dev, h->ugq.data(), h->ugq.size() * 8, hipMemcpyHostToDevice, h->stream));
+      launch_user_gossips(d, k, h->ug_dev, (uint32_t)pairs, h->stream);
+      HIPCK(hipStreamSynchronize(h->stream));  // the host queue is reused after this
+      h->ugq.clear();
+    }
     if (d.W == 1) {
       // SYNC diff(k) was queued in the previous iteration, except for the first tick of this call
       if (i == 0 || h->no_pipe) launch_diff(d, k, h->stream, te);

@@ -62,6 +62,8 @@ struct Dev {
   // ---- configuration ----
   uint32_t N, NS, F, kreq, ping_t, pingTimeout_t, gossip_t, sync_t, syncTimeout_t, md_t, lat, suspMult, repeatMult;
   uint32_t seed_lo, seed_hi, init_mode, flags, n_seeds;
+  uint32_t mode, churn;  // SWIM_MODE_RUMOR: gossip layer only, churn rumors per FD period (SEMANTICS.md §9)
+  uint64_t* churn_q;     // [churn][2] (origin, payload) of this period's rumors
   uint32_t seeds[16];
   uint32_t LCAP, FCAP, GRCAP, LOGW, SLOTS, MSGCAP, NCHUNK, POOLCAP, EVCAP, DCAP, RCAP, ARENA_ROWS, LOOKBACK, HCAP;
 
@@ -217,6 +219,7 @@ void launch_inline_in(const Dev& d, uint8_t* recv, uint64_t cap, const unsigned 
                       void* stream);
 void launch_kill(const Dev& d, uint32_t member, void* stream);
 void launch_user_gossips(const Dev& d, uint32_t k, const uint64_t* q, uint32_t n, void* stream);
+void launch_churn(const Dev& d, uint32_t k, void* stream);  // RUMOR mode, at ticks k % ping_t == 0
 void launch_hash(const Dev& d, uint64_t* out, uint32_t now, void* stream);
 
 }  // namespace swim

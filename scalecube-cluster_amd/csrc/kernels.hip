@@ -38,6 +38,7 @@ __global__ void k_init_members(Dev d) {
   d.nextGossip[m] = ng;
   d.firstGossip[m] = ng;
   d.nextSync[m] = pre ? 1 + init_draw(d, m, 3, 0) % d.sync_t : NEVER;
+  if (d.mode == 1u) d.nextPing[m] = d.nextSync[m] = NEVER;  // RUMOR: gossip layer only (SEMANTICS.md §9)
   d.cidCnt[m] = d.syncSeq[m] = d.evSeq[m] = d.held[m] = 0;
   d.timerMin[m] = NEVER;
   d.initFlags[m] = d.initDeadline[m] = d.initCidBase[m] = d.initN[m] = 0;
@@ -497,7 +498,9 @@ __device__ __forceinline__ bool replay_pair(const Dev& d, uint32_t x, uint32_t y
     if (!changed) break;
   }
   // deliveries into x come from y's log (oldest[0]); into y from x's log (oldest[1])
-  if ((lo_in[0] != NEVER && lo_in[0] < oldest[0] + lat) || (lo_in[1] != NEVER && lo_in[1] < oldest[1] + lat)) {
+  // (oldest 0: that ring never wrapped, so it holds every round since tick 0)
+  if ((lo_in[0] != NEVER && oldest[0] && lo_in[0] < oldest[0] + lat) ||
+      (lo_in[1] != NEVER && oldest[1] && lo_in[1] < oldest[1] + lat)) {
     if (atomicOr(d.err, E_LOGWIN) == 0) {
       d.err[1] = tau;
       d.err[2] = lo_in[0];

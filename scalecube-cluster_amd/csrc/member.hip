@@ -213,6 +213,25 @@ __global__ void k_user_gossips(Dev d, uint32_t k, const uint64_t* q, uint32_t n)
   if (created) atomicAdd(&d.ctr[C_GCREATED], created);
 }
 
+// RUMOR-mode churn of period p = k / ping_t (SEMANTICS.md §9): event i picks the churned member v and an origin
+// o != v; the rumor (p << 32 | v) is then spread by o through k_user_gossips, in event order
+__global__ void k_churn(Dev d, uint32_t k) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= d.churn) return;
+  const uint32_t p = k / d.ping_t;
+  const u32x4 r = philox(p, i, 0, 0, d.seed_lo ^ SALT_CHURN, d.seed_hi);
+  const uint32_t v = next_int(r.x, d.N);
+  uint32_t o = next_int(r.y, d.N - 1);
+  o += o >= v ? 1u : 0u;
+  d.churn_q[2 * i] = o;
+  d.churn_q[2 * i + 1] = ((uint64_t)p << 32) | v;
+}
+
+void launch_churn(const Dev& d, uint32_t k, void* stream) {
+  hipLaunchKernelGGL(k_churn, dim3((d.churn + 255) / 256), dim3(256), 0, (hipStream_t)stream, d, k);
+  hipLaunchKernelGGL(k_user_gossips, dim3(1), dim3(64), 0, (hipStream_t)stream, d, k, d.churn_q, d.churn);
+}
+
 void launch_user_gossips(const Dev& d, uint32_t k, const uint64_t* q, uint32_t n, void* stream) {
   hipLaunchKernelGGL(k_user_gossips, dim3(1), dim3(64), 0, (hipStream_t)stream, d, k, q, n);
 }

@@ -85,7 +85,7 @@ SW_HD u32x4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t 
 SW_HD uint32_t pick(const u32x4& r, uint32_t i) { return i == 0 ? r.x : i == 1 ? r.y : i == 2 ? r.z : r.w; }
 
 constexpr uint32_t SALT_SEL = 0x53454C31u, SALT_INIT = 0x494E4954u, SALT_LOSS_BASE = 0x4C4F5300u,
-                   SALT_LOSS_GOSSIP = 0x474F5353u;
+                   SALT_LOSS_GOSSIP = 0x474F5353u, SALT_CHURN = 0x43485552u;
 // message kinds (loss-key salts; SEMANTICS.md §2)
 constexpr uint32_t K_SYNC = 1, K_SYNC_ACK = 2, K_PING = 3, K_PING_REQ = 4, K_PING_ACK = 5, K_GMD_REQ = 6,
                    K_GMD_RESP = 7;

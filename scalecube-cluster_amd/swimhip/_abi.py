@@ -14,7 +14,7 @@ SWIM_EUNSUPPORTED = -5
 
 INIT_COLD_JOIN = 0
 INIT_PRECONVERGED = 1
-MODE_FULL = 0
+MODE_FULL, MODE_RUMOR = 0, 1
 FLAG_RECORD_EVENTS = 1
 FLAG_PROFILE = 2
 FLAG_PROFILE_ALL = 4
@@ -52,7 +52,8 @@ class SwimConfig(C.Structure):
         ("n_gpus", C.c_uint32),
         ("device", C.c_uint32),
         ("list_slack", C.c_uint32),
-        ("reserved", C.c_uint32 * 6),
+        ("churn_per_period", C.c_uint32),
+        ("reserved", C.c_uint32 * 5),
     ]
 
 

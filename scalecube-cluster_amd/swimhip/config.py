@@ -67,6 +67,8 @@ class SimConfig:
     pending_fetch_cap: int = 0
     event_cap: int = 0
     list_slack: int = 0
+    mode: int = _abi.MODE_FULL  # MODE_RUMOR: gossip layer only, churn_per_period rumors per period (SEMANTICS.md §9)
+    churn_per_period: int = 0
     device: int = 0
 
     def to_abi(self):
@@ -87,7 +89,8 @@ class SimConfig:
         a.gossip_fanout = c.gossipFanout
         a.gossip_repeat_mult = c.gossipRepeatMult
         a.metadata_timeout_ms = c.metadataTimeout
-        a.mode = _abi.MODE_FULL
+        a.mode = self.mode
+        a.churn_per_period = self.churn_per_period
         a.flags = (_abi.FLAG_RECORD_EVENTS if self.record_events else 0) | (_abi.FLAG_PROFILE if self.profile else 0)
         seeds = list(dict.fromkeys(c.seedMembers))
         if len(seeds) > 16:

@@ -2,8 +2,8 @@
 
 The reference (Java 8 + Reactor) cannot run in this image: there is no JDK. The oracle is its
 restatement, pinned by the reference's own known-answer tests (tests/test_oracle_known_answers.py). These fixtures
-freeze the oracle's behaviour on the C1 / C2 / C3 / C4 shapes so that any later change to either backend that moves a
-single bit of state, a counter or an event shows up. Run from the repo root:  python tests/golden/make_golden.py
+freeze the oracle's behaviour on the C1 / C2 / C3 / C4 / C5 shapes so that any later change to either backend that moves a
+single bit of state, a counter or an event shows up. Run from the repo root:  python tests/golden/make_golden.py [scenario ...]
 """
 import json
 import sys
@@ -23,7 +23,10 @@ from scenarios import SCENARIOS, record  # noqa: E402
 
 def main():
     lib = _abi.load(ROOT / "oracle" / "liboracle_swimref.so")
+    only = set(sys.argv[1:])  # optional: scenario names to (re)record
     for name, make in SCENARIOS.items():
+        if only and name not in only:
+            continue
         cfg, _ = make()
         t0 = time.time()
         c = SimulatedCluster(lib, cfg)

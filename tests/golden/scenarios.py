@@ -36,7 +36,11 @@ def _c3_small():  # C3-shaped: steady state SYNC / SYNC_ACK anti-entropy, no los
     return SimConfig(n_members=1000), [("periods", 35)]
 
 
-SCENARIOS = {"c1": _c1, "c2_small": _c2_small, "c4_small": _c4_small, "c3_small": _c3_small}
+def _c5_small():  # C5-shaped: rumor-only dissemination with 1 % churn per period (SEMANTICS.md §9), reduced N
+    return SimConfig(n_members=400, mode=_abi.MODE_RUMOR, churn_per_period=4, record_events=True), [("periods", 30)]
+
+
+SCENARIOS = {"c1": _c1, "c2_small": _c2_small, "c4_small": _c4_small, "c3_small": _c3_small, "c5_small": _c5_small}
 FULL_EVENTS = {"c1"}
 
 
@@ -45,7 +49,7 @@ def digest(a):
 
 
 def event_rows(evs):
-    return [[e.tick, e.observer, e.seq, {"ADDED": 0, "REMOVED": 1, "UPDATED": 2}[e.type], e.member,
+    return [[e.tick, e.observer, e.seq, {"ADDED": 0, "REMOVED": 1, "UPDATED": 2, "GOSSIP": 3}[e.type], e.member,
              -1 if e.oldMetadata is None else e.oldMetadata, -1 if e.newMetadata is None else e.newMetadata] for e in evs]
 
 

@@ -192,3 +192,25 @@ def test_user_gossips_sharded(oracle, engine):
             c.spread_gossip(m, 1000 + m)
     run_lockstep(o, e, 100, 20, "user gossips W=3")
     e.close()
+
+
+@pytest.mark.parametrize("loss", [0, 10])
+def test_rumor_mode(oracle, engine, loss):
+    """RUMOR mode (C5 shape, SEMANTICS.md §9): churn rumors every period, plus a user gossip and a crash."""
+    cfg = SimConfig(n_members=300, mode=_abi.MODE_RUMOR, churn_per_period=3, record_events=True)
+    o, e = pair(oracle, engine, cfg)
+    for c in (o, e):
+        c.set_default_loss(loss)
+    run_lockstep(o, e, 120, 20, f"rumor loss {loss}")
+    for c in (o, e):
+        c.spread_gossip(17, 99)
+        c.kill(40)
+    run_lockstep(o, e, 150, 30, f"rumor + user gossip + kill, loss {loss}")
+
+
+def test_rumor_mode_sharded(oracle, engine):
+    from swimhip.shard import ThreadShardGroup
+    cfg = SimConfig(n_members=240, mode=_abi.MODE_RUMOR, churn_per_period=4, record_events=True)
+    o, e = SimulatedCluster(oracle, cfg), ThreadShardGroup(engine, cfg, 2)
+    run_lockstep(o, e, 200, 40, "rumor W=2")
+    e.close()

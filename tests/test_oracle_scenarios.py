@@ -249,3 +249,29 @@ def test_user_gossips_order_and_dead_origin(oracle):
     assert 3 not in got
     with pytest.raises(Exception):
         c.spread_gossip(4, 9)
+
+
+def test_rumor_mode_churn(oracle):
+    """RUMOR mode (SEMANTICS.md §9, C5 shape): no FD / SYNC / metadata traffic; every period `churn` rumors about
+    Philox-chosen members, each delivered to all N - 1 other members exactly once (GossipProtocolTest :150-175)."""
+    n, churn, periods = 200, 3, 25
+    c = SimulatedCluster(oracle, SimConfig(n_members=n, mode=_abi.MODE_RUMOR, churn_per_period=churn, record_events=True))
+    c.run_periods(periods)
+    ctr = c.counters()
+    assert ctr["messages"] == 0 and ctr["sync_merges"] == 0 and ctr["record_compares"] == 0
+    assert ctr["gossips_created"] == churn * periods
+    got = {}
+    for e in c.events():
+        assert e.isGossip()
+        got.setdefault((e.member, e.payload()), []).append(e.observer)
+    done = [(o, p) for (o, p) in got if (p >> 32) < periods - 4]  # rumors old enough to have finished
+    assert len(done) == churn * (periods - 4)
+    for key in done:
+        obs = got[key]
+        assert sorted(obs) == sorted(set(range(n)) - {key[0]}), key
+    assert all((p & 0xFFFFFFFF) != o for (o, p) in got)  # the origin is never the churned member
+
+
+def test_rumor_mode_requires_preconverged(oracle):
+    with pytest.raises(Exception):
+        SimulatedCluster(oracle, SimConfig(n_members=10, mode=_abi.MODE_RUMOR, init_mode=_abi.INIT_COLD_JOIN))
