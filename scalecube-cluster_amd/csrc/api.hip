@@ -256,7 +256,7 @@ int build(swim_handle* h) {
   const uint64_t NL = d.NL;  // per-observer arrays: this shard's rows only
   A(d.row, NL * d.NS) A(d.fdl, NL * d.LCAP) A(d.gl, NL * d.LCAP)
   A(d.subs, NL * SUBCAP * 4) A(d.paths, NL * PATHCAP * 5) A(d.fetch, NL * d.FCAP * FREC) A(d.groups, NL * d.GRCAP * GREC)
-  A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.slow, d.SLOWCAP) A(d.slow_n, 1) A(d.rlist, N) A(d.rn, 1) A(d.churn_q, 2ull * d.churn) A(d.cin, N * d.F) A(d.swthr, N) A(d.cev, N * d.F * CEVW)
+  A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.slow, d.SLOWCAP) A(d.slow_n, 1) A(d.rlist, N) A(d.rn, 1) A(d.churn_q, 2ull * d.churn) A(d.cin, N * d.F) A(d.swthr, N) A(d.HB, (uint64_t)(d.SLOTS / 64 + 1) * N) A(d.WB, (uint64_t)(d.SLOTS / 64 + 1) * N) A(d.cev, N * d.F * CEVW)
   A(d.log_tick, N * d.LOGW) A(d.log_spread, N * d.LOGW) A(d.log_cnt, N * d.LOGW) A(d.log_tg, N * d.LOGW * d.F)
   A(d.log_pos, N) A(d.spchg, N)
   A(d.slot_gid, d.SLOTS) A(d.slot_subj, d.SLOTS) A(d.slot_ctick, d.SLOTS) A(d.slot_key, d.SLOTS) A(d.slot_holders, d.SLOTS)
@@ -617,7 +617,7 @@ int swim_step(swim_handle* h, uint32_t n) {
     unsigned long long c[5];
     HIPCK(hipMemcpy(c, d.ctr + 8, sizeof(c), hipMemcpyDeviceToHost));
     HIPCK(hipMemset(d.ctr + 8, 0, sizeof(c)));
-    fprintf(stderr, "exp: held %llu window %llu replays %llu slots(sum) %llu rounds(sum) %llu\n", c[0], c[1], c[2], c[3], c[4]);
+    fprintf(stderr, "exp: items %llu contact-bits %llu replays %llu candidates %llu\n", c[0], c[1], c[2], c[3]);
   }
   if (rc == SWIM_OK && profile) {
     for (uint32_t i = 0; i < n; ++i) {

@@ -102,6 +102,7 @@ struct Dev {
   uint32_t *rlist, *rn;  // [N] members with a gossip round this tick (built by k_gossip_contacts)
   uint32_t* cin;    // [N][F] latest cached contact t -> m of (m, T[m][s]); NEVER: none, CIN_SLOW: list overflowed
   uint32_t* swthr;  // [N] round sweep bound of this tick (k_round_info)
+  unsigned long long *HB, *WB;  // [SLOTS / 64 + 1][N] per 64-slot group: held past this tick / in a round window
   uint32_t* cev;  // [N][F][CEVW] contact events of (m, T[m][s]) cached by k_gossip_contacts when tcontact is set
   uint32_t *log_tick, *log_spread, *log_cnt, *log_tg, *log_pos;  // [N][LOGW], tg [N][LOGW][F], pos [N]
 

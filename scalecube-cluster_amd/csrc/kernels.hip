@@ -661,7 +661,13 @@ __global__ void k_gossip_contacts(Dev d, uint32_t k) {
           if (ev[j].dir == 0) last_in = ev[j].tick;  // events are in tick order
         }
       rec[3] = last_in;
-      d.cin[i] = n > CEV ? CIN_SLOW : last_in;
+      // a gossip inside m's window this round was created after tick k - (spread + 1) * gossip_t, so a contact
+      // t -> m at or before that tick - lat can never put t in infectedFrom_m of any gossip m sends now
+      const int64_t horizon = (int64_t)k - (int64_t)(d.tspread[m] + 1u) * d.gossip_t;
+      if (n > CEV)
+        d.cin[i] = CIN_SLOW;
+      else
+        d.cin[i] = last_in == NEVER || (int64_t)last_in + d.lat <= horizon ? NEVER : last_in;
     }
   }
   d.tcontact[i] = flag;
@@ -701,106 +707,116 @@ __device__ __forceinline__ void send_tail(const Dev& d, uint32_t g, uint32_t m, 
   }
 }
 
-// One block per group of gs active slots (grid-stride). The block first turns each slot's holder row into an LDS
-// bitmap of the members that hold it past this tick (held and not sweeping it in their own round: swthr), streaming
-// the rows once, coalesced. Then each round member of this tick loads its round (targets, cached contact bounds)
-// once and, for every slot of the group it holds in its window, sends it (selectGossipsToSend :239-250) to each
-// target not in infectedFrom (cached contact replay); only targets outside the bitmap can be first receipts, so
-// the per-send work is an LDS lookup. Then the member's sweep (:283-308). A pair whose contact list overflowed is
-// deferred to k_gossip_send_slow (the full replay needs a large stack).
-constexpr uint32_t GSMAX = 8, FMAX = 8;  // slots per block group; gossip fanout limit (swim_create)
-__global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp, uint32_t k, const uint32_t* active,
-                                                     const uint32_t* nactive, uint32_t gs) {
+// The gossip round is bit-parallel over groups of 64 active slots (active[64 q .. 64 q + 63] = group q):
+//   k_gossip_scan  streams the holder table once per tick, coalesced (lane = member), and writes per (group, member)
+//                  two 64-bit masks: HB = slots the member holds past this tick (held and not sweeping them in its
+//                  round: swthr), WB = slots a round member holds inside its spread window (selectGossipsToSend
+//                  :239-250). It also performs the round members' sweeps (sweepGossips :283-308).
+//   k_gossip_send  per (round member, group): each target t gets WB minus the slots t is in infectedFrom of
+//                  (isInfected, cached contact replay, only where a contact can matter); the count is a popcount,
+//                  and the first-receipt candidates are WB & ~HB[t].
+// A pair whose contact list overflowed is deferred to k_gossip_send_slow (the full replay needs a large stack).
+__global__ void __launch_bounds__(256) k_gossip_scan(const Dev* __restrict__ dp, uint32_t k, const uint32_t* active,
+                                                     const uint32_t* nactive) {
   const Dev& d = *dp;
-  extern __shared__ unsigned long long hb[];  // [gs][ceil(N / 64)] holder bitmaps of the group's slots
+  const uint32_t na = *nactive, ngroups = (na + 63) / 64;
+  const uint32_t mchunks = (d.N + 255) / 256;
+  for (uint32_t w = blockIdx.x; w < ngroups * mchunks; w += gridDim.x) {
+    const uint32_t q = w / mchunks, m = (w % mchunks) * 256 + threadIdx.x;
+    if (m >= d.N) continue;
+    const uint32_t gn = min(64u, na - q * 64);
+    const uint32_t thr = d.swthr[m];
+    const bool rnd = d.tround[m] && m >= d.lo && m < d.hi;  // this shard's round members send and sweep
+    uint32_t per = 0, sp = 0, fg = NEVER;
+    if (rnd) {
+      per = d.tperiod[m];
+      sp = d.tspread[m];
+      fg = d.firstGossip[m];
+    }
+    unsigned long long hb = 0, wb = 0;
+    for (uint32_t j = 0; j < gn; ++j) {
+      const uint32_t g = active[q * 64 + j];
+      const uint32_t e = d.S[(size_t)g * d.N + m];
+      if (!s_held(e)) continue;
+      const uint32_t c = s_ctick(e);
+      if (!(c < thr)) hb |= 1ull << j;
+      if (!rnd) continue;
+      const uint32_t infP = (fg == NEVER || c <= fg) ? 0u : (c - fg + d.gossip_t - 1) / d.gossip_t;  // rounds_before
+      if (infP + sp >= per) wb |= 1ull << j;  // selectGossipsToSend window (:246)
+      if (per > infP + 2u * (sp + 1u)) {      // sweepGossips (:283-308)
+        atomicOr(&d.S[(size_t)g * d.N + m], S_SWEPT);
+        atomicSub(&d.held[m], 1u);
+        atomicSub(&d.slot_holders[g], 1);
+        on_sweep(d, g, m, k);
+        if (d.W > 1) {  // applied on the other shards from exchange B
+          uint32_t i = atomicAdd(&d.xn[2], 1u);
+          if (i < d.SWCAP)
+            d.sw_rec[i] = ((uint64_t)g << 32) | m;
+          else
+            atomicOr(d.err, E_XCAP);
+        }
+      }
+    }
+    d.HB[(size_t)q * d.N + m] = hb;
+    d.WB[(size_t)q * d.N + m] = wb;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp, uint32_t k, const uint32_t* active,
+                                                     const uint32_t* nactive) {
+  const Dev& d = *dp;
   __shared__ unsigned long long red[4];
-  __shared__ uint32_t sg[GSMAX], sborn[GSMAX];
-  __shared__ uint64_t sgid[GSMAX];
-  const uint32_t na = *nactive, nr = *d.rn, nw = (d.N + 63) / 64, ngroups = (na + gs - 1) / gs;
+  const uint32_t na = *nactive, nr = *d.rn, ngroups = (na + 63) / 64, rchunks = (nr + 255) / 256;
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   unsigned long long sends = 0;
-  for (uint32_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
-    const uint32_t a0 = grp * gs, gn = min(gs, na - a0);
-    if (threadIdx.x < gn) {
-      const uint32_t g = active[a0 + threadIdx.x];
-      sg[threadIdx.x] = g;
-      sgid[threadIdx.x] = d.slot_gid[g];
-      sborn[threadIdx.x] = d.slot_ctick[g];
-    }
-    for (uint32_t base = 0; base < d.N; base += 256) {
-      const uint32_t t = base + threadIdx.x;
-      const uint32_t thr = t < d.N ? d.swthr[t] : 0u;
-      for (uint32_t j = 0; j < gn; ++j) {
-        bool keep = false;
-        if (t < d.N) {
-          const uint32_t e = d.S[(size_t)active[a0 + j] * d.N + t];
-          keep = s_held(e) && !(s_ctick(e) < thr);
+  uint32_t st[4] = {0, 0, 0, 0};  // SWIM_EXP & 4: items with window bits, contact-loop bits, replays, first-receipt candidates
+  for (uint32_t w = blockIdx.x; w < ngroups * rchunks; w += gridDim.x) {
+    const uint32_t q = w / rchunks, ri = (w % rchunks) * 256 + threadIdx.x;
+    if (ri >= nr) continue;
+    const uint32_t m = d.rlist[ri];
+    const unsigned long long wb = d.WB[(size_t)q * d.N + m];
+    if (!wb) continue;
+    if (d.exp & 4) st[0]++;
+    const uint32_t n = d.tcnt[m];
+    const uint32_t* ga = active + q * 64;
+    for (uint32_t s = 0; s < n; ++s) {
+      const size_t ms = (size_t)m * d.F + s;
+      const uint32_t t = d.T[ms], ci = d.cin[ms];
+      unsigned long long ok = wb;
+      if (ci == CIN_SLOW) {  // overflowed contact list: the full replay runs in k_gossip_send_slow
+        for (unsigned long long b = wb; b; b &= b - 1) {
+          const uint32_t g = ga[__ffsll(b) - 1];
+          uint32_t i = wave_append(d.slow_n);
+          if (i < d.SLOWCAP)
+            d.slow[i] = ((uint64_t)g << 32) | (uint32_t)ms;
+          else
+            atomicOr(d.err, E_CONTACTS);
         }
-        const unsigned long long w = __ballot(keep);
-        if (lane == 0 && base / 64 + wave < nw) hb[j * nw + base / 64 + wave] = w;
+        continue;
       }
-    }
-    __syncthreads();
-    for (uint32_t ri = threadIdx.x; ri < nr; ri += 256) {
-      const uint32_t m = d.rlist[ri];
-      uint32_t e[GSMAX];
-#pragma unroll
-      for (uint32_t j = 0; j < GSMAX; ++j) e[j] = j < gn ? d.S[(size_t)sg[j] * d.N + m] : 0u;
-      const uint32_t per = d.tperiod[m], sp = d.tspread[m], fg = d.firstGossip[m], n = d.tcnt[m];
-      uint32_t tt[FMAX], ci[FMAX];
-#pragma unroll
-      for (uint32_t s = 0; s < FMAX; ++s) {
-        tt[s] = s < n ? d.T[(size_t)m * d.F + s] : 0u;
-        ci[s] = s < n ? d.cin[(size_t)m * d.F + s] : NEVER;
-      }
-      for (uint32_t j = 0; j < gn; ++j) {
-        if (!s_held(e[j])) continue;
-        const uint32_t g = sg[j];
-        uint32_t* Sg = d.S + (size_t)g * d.N;
-        const uint32_t c = s_ctick(e[j]);
-        const uint32_t infP = (fg == NEVER || c <= fg) ? 0u : (c - fg + d.gossip_t - 1) / d.gossip_t;  // rounds_before
-        if (infP + sp >= per) {  // selectGossipsToSend window (:246)
-          const uint64_t gid = sgid[j];
-          const uint32_t born = sborn[j];
-          const unsigned long long* hbj = hb + j * nw;
-#pragma unroll
-          for (uint32_t s = 0; s < FMAX; ++s) {
-            if (s >= n) break;
-            const size_t ms = (size_t)m * d.F + s;
-            const uint32_t t = tt[s];
-            if (ci[s] == CIN_SLOW) {  // overflowed contact list: the full replay runs in k_gossip_send_slow
-              uint32_t i = wave_append(d.slow_n);
-              if (i < d.SLOWCAP)
-                d.slow[i] = ((uint64_t)g << 32) | (uint32_t)ms;
-              else
-                atomicOr(d.err, E_CONTACTS);
-              continue;
-            }
-            // only a delivery t -> m at or after m's incarnation start c (and after g existed) can block the send
-            if (ci[s] != NEVER && ci[s] >= born && ci[s] + d.lat >= c &&
-                blocked_pair_cached(d, m, t, g, gid, k, c, d.cev + ms * CEVW))
-              continue;  // isInfected (:247)
-            sends++;
-            if (d.dbg_send || !((hbj[t >> 6] >> (t & 63u)) & 1ull)) send_tail(d, g, m, s, t, k, gid, Sg);
-          }
-        }
-        if (per > infP + 2u * (sp + 1u)) {  // sweepGossips (:283-308)
-          atomicOr(&Sg[m], S_SWEPT);
-          atomicSub(&d.held[m], 1u);
-          atomicSub(&d.slot_holders[g], 1);
-          on_sweep(d, g, m, k);
-          if (d.W > 1) {  // applied on the other shards from exchange B
-            uint32_t i = atomicAdd(&d.xn[2], 1u);
-            if (i < d.SWCAP)
-              d.sw_rec[i] = ((uint64_t)g << 32) | m;
-            else
-              atomicOr(d.err, E_XCAP);
+      if (ci != NEVER) {  // a cached contact t -> m: replay per slot where it can matter (isInfected :247)
+        for (unsigned long long b = wb; b; b &= b - 1) {
+          const uint32_t j = __ffsll(b) - 1, g = ga[j];
+          const uint32_t c = s_ctick(d.S[(size_t)g * d.N + m]);
+          if (d.exp & 4) st[1]++;
+          if (ci >= d.slot_ctick[g] && ci + d.lat >= c) {
+            if (d.exp & 4) st[2]++;
+            if (blocked_pair_cached(d, m, t, g, d.slot_gid[g], k, c, d.cev + ms * CEVW)) ok &= ~(1ull << j);
           }
         }
       }
+      sends += __popcll(ok);
+      unsigned long long cand = d.dbg_send ? ok : ok & ~d.HB[(size_t)q * d.N + t];
+      for (; cand; cand &= cand - 1) {
+        const uint32_t g = ga[__ffsll(cand) - 1];
+        if (d.exp & 4) st[3]++;
+        send_tail(d, g, m, s, t, k, d.slot_gid[g], d.S + (size_t)g * d.N);
+      }
     }
-    __syncthreads();  // the bitmaps and slot ids are rebuilt for the next group
   }
+  if (d.exp & 4)
+    for (int q2 = 0; q2 < 4; ++q2)
+      if (st[q2]) atomicAdd(&d.ctr[8 + q2], (unsigned long long)st[q2]);
   for (uint32_t o = 32; o > 0; o >>= 1) sends += __shfl_xor(sends, o);
   if (lane == 0) red[wave] = sends;
   __syncthreads();
@@ -808,14 +824,6 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
     const unsigned long long tot = red[0] + red[1] + red[2] + red[3];
     if (tot) atomicAdd(&d.ctr[C_G], tot);
   }
-}
-
-// slots per k_gossip_send block: as many holder bitmaps as fit in 64 KB of LDS, at most GSMAX
-static uint32_t send_group(const Dev& d) {
-  static const char* ev = getenv("SWIM_SEND_GROUP");  // tuning knob
-  const uint64_t bytes = (uint64_t)(d.N + 63) / 64 * 8;
-  const uint64_t want = ev ? (uint64_t)atoi(ev) : 1;
-  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(std::min<uint64_t>(GSMAX, want), (64ull << 10) / bytes));
 }
 
 // deferred sends whose pair had more contact events than the cache holds (small clusters): full log scan + replay
@@ -1011,7 +1019,7 @@ void launch_member(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
 
 static void launch_receipt_routing(const Dev& d, hipStream_t st);
 
-constexpr uint32_t SEND_GRID = 2048;  // 8 blocks per CU: the send loop is latency-bound
+constexpr uint32_t SEND_GRID = 4096;  // 16 blocks per CU, grid-stride
 
 void launch_gossip(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
   hipStream_t st = (hipStream_t)stream;
@@ -1019,8 +1027,8 @@ void launch_gossip(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   hipLaunchKernelGGL(k_round_info, dim3(cdiv(d.N, 256)), dim3(256), 0, st, d);
   hipLaunchKernelGGL(k_gossip_contacts, dim3(cdiv((uint64_t)d.NL * d.F, 256)), dim3(256), 0, st, d, k);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[4], st);
-  hipLaunchKernelGGL(k_gossip_send, dim3(SEND_GRID), dim3(256), (size_t)(d.N + 63) / 64 * 8 * send_group(d), st, d.self, k,
-                     d.active, d.nactive, send_group(d));
+  hipLaunchKernelGGL(k_gossip_scan, dim3(SEND_GRID), dim3(256), 0, st, d.self, k, d.active, d.nactive);
+  hipLaunchKernelGGL(k_gossip_send, dim3(SEND_GRID), dim3(256), 0, st, d.self, k, d.active, d.nactive);
   hipLaunchKernelGGL(k_gossip_send_slow, dim3(256), dim3(256), 0, st, d.self, k);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[5], st);
   hipLaunchKernelGGL(k_gossip_apply, dim3(1024), dim3(256), 0, st, d, k);
@@ -1071,8 +1079,8 @@ void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   hipLaunchKernelGGL(k_round_info, dim3(cdiv(d.N, 256)), dim3(256), 0, st, d);
   hipLaunchKernelGGL(k_gossip_contacts, dim3(cdiv((uint64_t)d.NL * d.F, 256)), dim3(256), 0, st, d, k);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[4], st);
-  hipLaunchKernelGGL(k_gossip_send, dim3(SEND_GRID), dim3(256), (size_t)(d.N + 63) / 64 * 8 * send_group(d), st, d.self, k,
-                     d.active, d.nactive, send_group(d));
+  hipLaunchKernelGGL(k_gossip_scan, dim3(SEND_GRID), dim3(256), 0, st, d.self, k, d.active, d.nactive);
+  hipLaunchKernelGGL(k_gossip_send, dim3(SEND_GRID), dim3(256), 0, st, d.self, k, d.active, d.nactive);
   hipLaunchKernelGGL(k_gossip_send_slow, dim3(256), dim3(256), 0, st, d.self, k);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[5], st);
   hipLaunchKernelGGL(k_pack_b, dim3(64, d.W), dim3(256), 0, st, d);

@@ -8,3 +8,5 @@ timeout -k 10 700 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fu
 tail -2 $O/parity.log
 timeout -k 10 400 python -u bench.py --workload c5 --members ${C5N:-100000} --warmup 25 --steps 10 --no-cpu-baseline > $O/c5.log 2>&1 || { tail -20 $O/c5.log; exit 1; }
 tail -1 $O/c5.log | cut -c1-400
+timeout -k 10 400 python -u bench.py --workload c2 --warmup 12 --steps 8 --no-cpu-baseline > $O/c2.log 2>&1 || { tail -20 $O/c2.log; exit 1; }
+tail -1 $O/c2.log | cut -c1-300
