@@ -90,7 +90,8 @@ typedef struct swim_config {
   uint32_t device;            /* first HIP device */
   uint32_t list_slack;        /* FD / gossip list entries beyond N (duplicates after reordered ADDED / REMOVED) */
   uint32_t churn_per_period;  /* SWIM_MODE_RUMOR: churn events (one rumor each) drawn at the start of every FD period */
-  uint32_t reserved[5];
+  uint32_t n_dormant;         /* COLD_JOIN: the last n_dormant members are not started; each starts on swim_join */
+  uint32_t reserved[4];
 } swim_config;
 
 typedef struct swim_event {
@@ -162,6 +163,12 @@ int swim_leave(swim_handle* h, uint32_t member);
  * incarnation bump or leave queued for the same tick, in call order. Every other member that receives it first emits a
  * SWIM_EV_GOSSIP event (listenGossips, ClusterImpl.java:213-216); membership ignores it (MembershipProtocolImpl :401-408) */
 int swim_spread_gossip(swim_handle* h, uint32_t member, uint64_t payload);
+/* Cluster.join(config) of a new process (ClusterImpl.join0 -> MembershipProtocolImpl.start0, ClusterImpl.java:85-152,
+ * MembershipProtocolImpl.java:216-251) for a dormant member (swim_config.n_dormant): at the next tick it starts with
+ * its own seed list (seedMembers, deduplicated, self skipped; at most 16), its schedules starting at that tick. A
+ * restart of a crashed member is swim_kill of the old id plus swim_join of a dormant id (a restarted member has a new
+ * id in the reference, FailureDetectorTest.java:345-401). A member joins at most once. */
+int swim_join(swim_handle* h, uint32_t member, const uint32_t* seeds, uint32_t n_seeds);
 
 /* readback */
 int swim_current_tick(swim_handle* h, uint64_t* tick);

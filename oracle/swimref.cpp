@@ -147,6 +147,8 @@ struct Member {
   uint64_t nextPing = NEVER, nextGossip = NEVER, nextSync = NEVER;
   bool pendingInc = false;  // swim_update_incarnation, applied in P0 of the next tick
   bool pendingLeave = false;  // swim_leave (leaveCluster), applied in P0 of the next tick after pendingInc
+  uint64_t startTick = NEVER;  // COLD_JOIN: 0 for the initial members, the join tick for a dormant one (swim_join)
+  bool dormant = false;
   std::vector<uint64_t> pendingUser;  // swim_spread_gossip payloads, spread in P0 of the next tick before pendingInc
   uint32_t cidCnt = 0, syncSeq = 0, evSeq = 0;
   uint32_t sel[8] = {0};
@@ -854,8 +856,8 @@ void Sim::run_tick() {
   arrived.swap(inflight[k % (lat + 1)]);
   std::vector<std::vector<Msg>> inbox(N);
   for (auto& m : arrived) inbox[m.dst].push_back(std::move(m));
-  if (k == 0 && cfg.init_mode == SWIM_INIT_COLD_JOIN)
-    for (auto& m : members) m.start(0);
+  for (auto& m : members)  // ClusterImpl.join0 -> start0: the initial members at tick 0, joined ones at their tick
+    if (m.alive && m.startTick == k) m.start(k);
   if (cfg.mode == SWIM_MODE_RUMOR && cfg.churn_per_period && k % ping_t == 0) {
     // churn of period p (SEMANTICS.md §9): event i picks a churned member v and a live origin o != v, which spreads
     // the rumor (p << 32 | v) at P0, before the user gossips queued by the host, in event order
@@ -930,6 +932,7 @@ __attribute__((visibility("default"))) int swim_create(const swim_config* cfg, s
   if (c.ping_timeout_ms >= c.ping_interval_ms) return SWIM_EINVAL;  // ClusterConfig.java:413-415
   if (c.gossip_fanout == 0 || c.gossip_fanout > 8 || c.n_seeds > 16) return SWIM_EINVAL;
   if (c.mode > SWIM_MODE_RUMOR || (c.mode == SWIM_MODE_RUMOR && c.init_mode != SWIM_INIT_PRECONVERGED)) return SWIM_EINVAL;
+  if (c.n_dormant > c.n_members || (c.n_dormant && c.init_mode != SWIM_INIT_COLD_JOIN)) return SWIM_EINVAL;
   auto* h = new swim_handle();
   if (const char* lp = getenv("SWIMREF_SEND_LOG")) h->sim.send_log = fopen(lp, "w");
   Sim& s = h->sim;
@@ -963,6 +966,11 @@ __attribute__((visibility("default"))) int swim_create(const swim_config* cfg, s
       uint32_t sd = c.seeds[i];
       if (sd >= s.N || sd == m) continue;
       if (std::find(mb.seeds.begin(), mb.seeds.end(), sd) == mb.seeds.end()) mb.seeds.push_back(sd);
+    }
+    if (c.init_mode == SWIM_INIT_COLD_JOIN) {
+      mb.dormant = m >= s.N - c.n_dormant;
+      mb.alive = !mb.dormant;  // a process not started yet refuses connections, like a dead one
+      mb.startTick = mb.dormant ? NEVER : 0;
     }
     mb.table[m] = Rec{ALIVE, 0};  // :133
     mb.tsize = 1;
@@ -1033,6 +1041,19 @@ __attribute__((visibility("default"))) int swim_leave(swim_handle* h, uint32_t m
 __attribute__((visibility("default"))) int swim_spread_gossip(swim_handle* h, uint32_t m, uint64_t payload) {
   if (!h || m >= h->sim.N || !h->sim.members[m].alive) return SWIM_EINVAL;
   h->sim.members[m].pendingUser.push_back(payload);
+  return SWIM_OK;
+}
+__attribute__((visibility("default"))) int swim_join(swim_handle* h, uint32_t m, const uint32_t* seeds, uint32_t n) {
+  if (!h || m >= h->sim.N || n > 16 || (n && !seeds)) return SWIM_EINVAL;
+  Member& mb = h->sim.members[m];
+  if (!mb.dormant) return SWIM_EINVAL;
+  mb.dormant = false;
+  mb.alive = true;
+  mb.startTick = h->sim.tick;
+  mb.seeds.clear();  // LinkedHashSet of valid ids minus self (MembershipProtocolImpl.java:160-166)
+  for (uint32_t i = 0; i < n; ++i)
+    if (seeds[i] < h->sim.N && seeds[i] != m && std::find(mb.seeds.begin(), mb.seeds.end(), seeds[i]) == mb.seeds.end())
+      mb.seeds.push_back(seeds[i]);
   return SWIM_OK;
 }
 __attribute__((visibility("default"))) int swim_set_default_loss(swim_handle* h, uint32_t pct) {

@@ -46,6 +46,7 @@ struct swim_handle {
   std::vector<uint8_t> hsend, hrecv;  // SWIM_TRANSPORT_HOST staging
   double xchg_ms = 0;                 // host time spent in the exchanges
   bool xflag = false;                 // last exchange: some shard has a gossip slot in use
+  std::vector<uint8_t> joined;  // swim_join: dormant members that were started
   std::vector<uint64_t> ugq;  // swim_spread_gossip queue: (member, payload) pairs for P0 of the next tick
   uint64_t* ug_dev = nullptr;  // device copy of ugq
   size_t ug_cap = 0;
@@ -204,6 +205,7 @@ int build(swim_handle* h) {
   d.seed_hi = (uint32_t)(c.seed >> 32);
   d.init_mode = c.init_mode;
   d.mode = c.mode;
+  d.n_dormant = c.n_dormant;
   d.churn = c.mode == SWIM_MODE_RUMOR ? c.churn_per_period : 0u;
   d.flags = c.flags;
   d.exp = getenv("SWIM_EXP") ? (uint32_t)atoi(getenv("SWIM_EXP")) : 0u;  // timing experiments: wrong results
@@ -256,7 +258,7 @@ int build(swim_handle* h) {
   const uint64_t NL = d.NL;  // per-observer arrays: this shard's rows only
   A(d.row, NL * d.NS) A(d.fdl, NL * d.LCAP) A(d.gl, NL * d.LCAP)
   A(d.subs, NL * SUBCAP * 4) A(d.paths, NL * PATHCAP * 5) A(d.fetch, NL * d.FCAP * FREC) A(d.groups, NL * d.GRCAP * GREC)
-  A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.slow, d.SLOWCAP) A(d.slow_n, 1) A(d.rlist, N) A(d.rn, 1) A(d.churn_q, 2ull * d.churn) A(d.cin, N * d.F) A(d.swthr, N) A(d.HB, (uint64_t)(d.SLOTS / 64 + 1) * N) A(d.WB, (uint64_t)(d.SLOTS / 64 + 1) * N) A(d.cev, N * d.F * CEVW)
+  A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.slow, d.SLOWCAP) A(d.slow_n, 1) A(d.rlist, N) A(d.rn, 1) A(d.start_tick, N) A(d.jseed_n, N) A(d.jseeds, 16 * N) A(d.churn_q, 2ull * d.churn) A(d.cin, N * d.F) A(d.swthr, N) A(d.HB, (uint64_t)(d.SLOTS / 64 + 1) * N) A(d.WB, (uint64_t)(d.SLOTS / 64 + 1) * N) A(d.cev, N * d.F * CEVW)
   A(d.log_tick, N * d.LOGW) A(d.log_spread, N * d.LOGW) A(d.log_cnt, N * d.LOGW) A(d.log_tg, N * d.LOGW * d.F)
   A(d.log_pos, N) A(d.spchg, N)
   A(d.slot_gid, d.SLOTS) A(d.slot_subj, d.SLOTS) A(d.slot_ctick, d.SLOTS) A(d.slot_key, d.SLOTS) A(d.slot_holders, d.SLOTS)
@@ -443,7 +445,8 @@ int create(const swim_config* cfg, const swim_shard_spec* spec, swim_handle** ou
   const swim_config& c = *cfg;
   if (c.n_members < 2 || c.n_members > (1u << 20) || c.ping_timeout_ms >= c.ping_interval_ms || c.gossip_fanout == 0 || c.gossip_fanout > 8 ||
       c.ping_req_members > 8 || c.n_seeds > 16 || c.mode > SWIM_MODE_RUMOR ||
-      (c.mode == SWIM_MODE_RUMOR && c.init_mode != SWIM_INIT_PRECONVERGED))
+      (c.mode == SWIM_MODE_RUMOR && c.init_mode != SWIM_INIT_PRECONVERGED) || c.n_dormant > c.n_members ||
+      (c.n_dormant && c.init_mode != SWIM_INIT_COLD_JOIN))
     return SWIM_EINVAL;
   if (c.latency_ticks != 1) return SWIM_EUNSUPPORTED;  // gossip data plane assumes one-tick hops
   if (spec) {
@@ -649,6 +652,22 @@ int swim_kill(swim_handle* h, uint32_t m) {
   uint32_t t = (uint32_t)h->tick;
   HIPCK(hipMemcpyAsync(h->d.dead_tick + m, &t, 4, hipMemcpyHostToDevice, h->stream));
   launch_kill(h->d, m, h->stream);
+  return check_err(h);
+}
+
+int swim_join(swim_handle* h, uint32_t m, const uint32_t* seeds, uint32_t n) {
+  if (!h || m >= h->d.N || n > 16 || (n && !seeds)) return SWIM_EINVAL;
+  if (m < h->d.N - h->d.n_dormant) return SWIM_EINVAL;  // only a dormant member starts later
+  if (h->joined.empty()) h->joined.assign(h->d.N, 0);
+  if (h->joined[m]) return SWIM_EINVAL;
+  h->joined[m] = 1;
+  uint32_t sd[16], ns = 0;  // LinkedHashSet of valid ids minus self (MembershipProtocolImpl.java:160-166)
+  for (uint32_t i = 0; i < n; ++i) {
+    bool dup = seeds[i] >= h->d.N || seeds[i] == m;
+    for (uint32_t j = 0; j < ns; ++j) dup |= sd[j] == seeds[i];
+    if (!dup) sd[ns++] = seeds[i];
+  }
+  launch_join(h->d, m, (uint32_t)h->tick, sd, ns, h->stream);  // every shard: the arrays are replicated
   return check_err(h);
 }
 

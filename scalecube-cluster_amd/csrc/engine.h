@@ -62,6 +62,10 @@ struct Dev {
   // ---- configuration ----
   uint32_t N, NS, F, kreq, ping_t, pingTimeout_t, gossip_t, sync_t, syncTimeout_t, md_t, lat, suspMult, repeatMult;
   uint32_t seed_lo, seed_hi, init_mode, flags, n_seeds;
+  uint32_t n_dormant;    // COLD_JOIN: members [N - n_dormant, N) start only on swim_join
+  uint32_t* start_tick;  // [N] tick of start0 (0: initial COLD_JOIN members; NEVER: PRECONVERGED or not joined yet)
+  uint32_t* jseed_n;     // [N] seeds of a joined member (NONE32: the config's seeds)
+  uint32_t* jseeds;      // [N][16]
   uint32_t mode, churn;  // SWIM_MODE_RUMOR: gossip layer only, churn rumors per FD period (SEMANTICS.md §9)
   uint64_t* churn_q;     // [churn][2] (origin, payload) of this period's rumors
   uint32_t seeds[16];
@@ -220,7 +224,8 @@ void launch_inline_in(const Dev& d, uint8_t* recv, uint64_t cap, const unsigned 
                       void* stream);
 void launch_kill(const Dev& d, uint32_t member, void* stream);
 void launch_user_gossips(const Dev& d, uint32_t k, const uint64_t* q, uint32_t n, void* stream);
-void launch_churn(const Dev& d, uint32_t k, void* stream);  // RUMOR mode, at ticks k % ping_t == 0
+void launch_churn(const Dev& d, uint32_t k, void* stream);
+void launch_join(const Dev& d, uint32_t m, uint32_t k, const uint32_t* seeds, uint32_t n, void* stream);  // RUMOR mode, at ticks k % ping_t == 0
 void launch_hash(const Dev& d, uint64_t* out, uint32_t now, void* stream);
 
 }  // namespace swim

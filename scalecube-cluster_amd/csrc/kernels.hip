@@ -39,6 +39,9 @@ __global__ void k_init_members(Dev d) {
   d.firstGossip[m] = ng;
   d.nextSync[m] = pre ? 1 + init_draw(d, m, 3, 0) % d.sync_t : NEVER;
   if (d.mode == 1u) d.nextPing[m] = d.nextSync[m] = NEVER;  // RUMOR: gossip layer only (SEMANTICS.md §9)
+  const bool dormant = m >= d.N - d.n_dormant;  // not started until swim_join (k_join)
+  d.start_tick[m] = (pre || dormant) ? NEVER : 0u;
+  d.jseed_n[m] = NONE32;
   d.cidCnt[m] = d.syncSeq[m] = d.evSeq[m] = d.held[m] = 0;
   d.timerMin[m] = NEVER;
   d.initFlags[m] = d.initDeadline[m] = d.initCidBase[m] = d.initN[m] = 0;
@@ -50,7 +53,7 @@ __global__ void k_init_members(Dev d) {
   d.tround[m] = 0;
   d.log_pos[m] = 0;
   d.spchg[m] = 0;
-  d.dead_tick[m] = NEVER;
+  d.dead_tick[m] = dormant ? 0u : NEVER;  // a process not started yet refuses connections, like a dead one
   d.md_version[m] = 0;
   d.rc_cnt[m] = 0;
   d.rc_off[m] = 0;
@@ -567,7 +570,7 @@ __device__ __forceinline__ uint32_t collect_contacts(const Dev& d, uint32_t x, u
 // isInfected replay from a full scan of both logs (used when the cached contact list of the pair overflowed)
 __device__ __noinline__ bool blocked_pair(const Dev& d, uint32_t x, uint32_t y, uint32_t g, uint64_t gid,
                                           uint32_t tau, uint32_t cx) {
-  constexpr uint32_t CMAX = 256;  // contact events between one pair inside the log window (small clusters: many)
+  constexpr uint32_t CMAX = 512;  // contact events between one pair inside the log window (small clusters: many)
   Contact ev[CMAX];
   uint32_t oldest[2];
   const uint32_t n = collect_contacts<CMAX>(d, x, y, tau, d.slot_ctick[g], ev, oldest);
@@ -827,7 +830,7 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
 }
 
 // deferred sends whose pair had more contact events than the cache holds (small clusters): full log scan + replay
-__global__ void __launch_bounds__(256) k_gossip_send_slow(const Dev* __restrict__ dp, uint32_t k) {
+__global__ void __launch_bounds__(64) k_gossip_send_slow(const Dev* __restrict__ dp, uint32_t k) {
   const Dev& d = *dp;
   const uint32_t n = min(*d.slow_n, d.SLOWCAP);
   unsigned long long sends = 0;
@@ -1029,7 +1032,7 @@ void launch_gossip(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[4], st);
   hipLaunchKernelGGL(k_gossip_scan, dim3(SEND_GRID), dim3(256), 0, st, d.self, k, d.active, d.nactive);
   hipLaunchKernelGGL(k_gossip_send, dim3(SEND_GRID), dim3(256), 0, st, d.self, k, d.active, d.nactive);
-  hipLaunchKernelGGL(k_gossip_send_slow, dim3(256), dim3(256), 0, st, d.self, k);
+  hipLaunchKernelGGL(k_gossip_send_slow, dim3(64), dim3(64), 0, st, d.self, k);  // rare; ~14 KB of stack per lane
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[5], st);
   hipLaunchKernelGGL(k_gossip_apply, dim3(1024), dim3(256), 0, st, d, k);
   launch_receipt_routing(d, st);
@@ -1081,7 +1084,7 @@ void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[4], st);
   hipLaunchKernelGGL(k_gossip_scan, dim3(SEND_GRID), dim3(256), 0, st, d.self, k, d.active, d.nactive);
   hipLaunchKernelGGL(k_gossip_send, dim3(SEND_GRID), dim3(256), 0, st, d.self, k, d.active, d.nactive);
-  hipLaunchKernelGGL(k_gossip_send_slow, dim3(256), dim3(256), 0, st, d.self, k);
+  hipLaunchKernelGGL(k_gossip_send_slow, dim3(64), dim3(64), 0, st, d.self, k);  // rare; ~14 KB of stack per lane
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[5], st);
   hipLaunchKernelGGL(k_pack_b, dim3(64, d.W), dim3(256), 0, st, d);
 }
@@ -1099,6 +1102,26 @@ void launch_tick_c(const Dev& d, uint32_t k, void* stream, bool gossip) {
   hipLaunchKernelGGL(k_gossip_free, dim3(1024), dim3(256), 0, st, d, d.active, d.nactive);
   hipLaunchKernelGGL(k_round_reset, dim3(16, d.W), dim3(256), 0, st, d);
   hipLaunchKernelGGL(k_tick_end, dim3(1), dim3(64), 0, st, d, k);
+}
+
+// swim_join: a dormant member starts at tick k as a fresh process (ClusterImpl.join0, schedules from k) with its seeds
+struct JoinSeeds {
+  uint32_t s[16];
+};
+__global__ void k_join(Dev d, uint32_t m, uint32_t k, JoinSeeds js, uint32_t n) {
+  if (threadIdx.x != 0) return;
+  d.dead_tick[m] = NEVER;
+  d.start_tick[m] = k;
+  d.nextPing[m] = k + d.ping_t;
+  d.nextGossip[m] = d.firstGossip[m] = k + d.gossip_t;
+  d.jseed_n[m] = n;
+  for (uint32_t i = 0; i < n; ++i) d.jseeds[(size_t)m * 16 + i] = js.s[i];
+}
+
+void launch_join(const Dev& d, uint32_t m, uint32_t k, const uint32_t* seeds, uint32_t n, void* stream) {
+  JoinSeeds js{};
+  for (uint32_t i = 0; i < n && i < 16; ++i) js.s[i] = seeds[i];
+  hipLaunchKernelGGL(k_join, dim3(1), dim3(64), 0, (hipStream_t)stream, d, m, k, js, n);
 }
 
 void launch_kill(const Dev& d, uint32_t member, void* stream) {

@@ -525,19 +525,34 @@ __device__ __forceinline__ void do_spread_gossip(ML& L) {
   }
 }
 
+// the member's seedMembers: its own list if it joined through swim_join, else the config's (deduplicated; self is
+// skipped by the callers, MembershipProtocolImpl.java:160-166)
+__device__ __forceinline__ const uint32_t* member_seeds(const Dev& d, uint32_t m, uint32_t* n) {
+  const uint32_t jn = d.jseed_n[m];
+  if (jn != NONE32) {
+    *n = jn;
+    return d.jseeds + (size_t)m * 16;
+  }
+  *n = d.n_seeds;
+  return d.seeds;
+}
+
 __device__ __forceinline__ bool is_seed(const Dev& d, uint32_t m, uint32_t s) {
   if (s == m) return false;
-  for (uint32_t i = 0; i < d.n_seeds; ++i)
-    if (d.seeds[i] == s) return true;
+  uint32_t n;
+  const uint32_t* sd = member_seeds(d, m, &n);
+  for (uint32_t i = 0; i < n; ++i)
+    if (sd[i] == s) return true;
   return false;
 }
 
 // doSync (MembershipProtocolImpl.java:298-314) + selectSyncAddress (:410-421)
 __device__ __forceinline__ void do_sync(ML& L) {
   const Dev& d = *L.d;
-  uint32_t extra = 0;
-  for (uint32_t i = 0; i < d.n_seeds; ++i) {
-    uint32_t s = d.seeds[i];
+  uint32_t extra = 0, nsd;
+  const uint32_t* sd = member_seeds(d, L.m, &nsd);
+  for (uint32_t i = 0; i < nsd; ++i) {
+    uint32_t s = sd[i];
     if (s != L.m && rec_status(L.row[s]) == ST_ABSENT) extra++;
   }
   uint32_t count = (L.tsize - 1u) + extra;
@@ -590,7 +605,7 @@ __device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t
   // every word is loaded up front (no short-circuit chain of dependent loads); the SoA loads coalesce per wave
   const uint32_t mh = d.m_head[(size_t)((k - 1) & 1) * d.N + m], rc = d.rc_cnt[m], pi = d.pending_inc[m],
                  ne = d.next_evt[m], tm = d.timerMin[m], np = d.nextPing[m], ns = d.nextSync[m], inf = d.initFlags[m],
-                 ng = d.nextGossip[m], held = d.held[m], dt = d.dead_tick[m];
+                 ng = d.nextGossip[m], held = d.held[m], dt = d.dead_tick[m], st = d.start_tick[m];
   const bool dead = k >= dt;
   if (dead) {
     d.rc_cnt[m] = 0;
@@ -598,7 +613,7 @@ __device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t
     if (k > 0) d.m_head[(size_t)((k - 1) & 1) * d.N + m] = NEVER;
   } else {
     const bool busy = (k > 0 && mh != NEVER) | (rc != 0) | (pi != 0) | (ne <= k) | (tm <= k) | (k == np) | (k == ns) |
-                      ((inf & INIT_ACTIVE) != 0) | (k == 0 && d.init_mode == 0);
+                      ((inf & INIT_ACTIVE) != 0) | (k == st);
     if (!busy) {
       if (k != ng) {
         d.tround[m] = 0;
@@ -683,11 +698,14 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
     }
   }
 
-  // ---- P0 start: ClusterImpl.join0 -> MembershipProtocolImpl.start0 (:216-251), COLD_JOIN at tick 0 ----
-  if (!dead && k == 0 && d.init_mode == 0) {
+  // ---- P0 start: ClusterImpl.join0 -> MembershipProtocolImpl.start0 (:216-251): COLD_JOIN members at tick 0, joined
+  // (swim_join) members at their join tick, with their own seeds ----
+  if (!dead && k == d.start_tick[m]) {
+    uint32_t nsd;
+    const uint32_t* sd = member_seeds(d, m, &nsd);
     uint32_t ns = 0;
-    for (uint32_t i = 0; i < d.n_seeds; ++i)
-      if (d.seeds[i] != m) ns++;
+    for (uint32_t i = 0; i < nsd; ++i)
+      if (sd[i] != m) ns++;
     if (ns == 0) {
       L.nextSync = k + d.sync_t;
     } else {
@@ -696,10 +714,10 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
       L.initCidBase = L.cidCnt;
       L.initN = ns;
       uint32_t failed = 0;
-      for (uint32_t i = 0; i < d.n_seeds; ++i) {
-        if (d.seeds[i] == m) continue;
+      for (uint32_t i = 0; i < nsd; ++i) {
+        if (sd[i] == m) continue;
         uint32_t cnt = L.cidCnt++;
-        if (!send_sync(L, K_SYNC, d.seeds[i], m, cnt)) failed++;
+        if (!send_sync(L, K_SYNC, sd[i], m, cnt)) failed++;
       }
       if (failed == ns) {
         L.initFlags = 0;

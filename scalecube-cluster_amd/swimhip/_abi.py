@@ -53,7 +53,8 @@ class SwimConfig(C.Structure):
         ("device", C.c_uint32),
         ("list_slack", C.c_uint32),
         ("churn_per_period", C.c_uint32),
-        ("reserved", C.c_uint32 * 5),
+        ("n_dormant", C.c_uint32),
+        ("reserved", C.c_uint32 * 4),
     ]
 
 
@@ -114,6 +115,7 @@ SIGNATURES = {
     "swim_update_incarnation": (C.c_int, [_H, C.c_uint32]),
     "swim_leave": (C.c_int, [_H, C.c_uint32]),
     "swim_spread_gossip": (C.c_int, [_H, C.c_uint32, C.c_uint64]),
+    "swim_join": (C.c_int, [_H, C.c_uint32, C.POINTER(C.c_uint32), C.c_uint32]),
     "swim_current_tick": (C.c_int, [_H, C.POINTER(C.c_uint64)]),
     "swim_read_row": (C.c_int, [_H, C.c_uint32, C.POINTER(C.c_uint64), C.c_size_t]),
     "swim_state_hash": (C.c_int, [_H, C.POINTER(C.c_uint64), C.c_size_t]),

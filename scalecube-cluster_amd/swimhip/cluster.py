@@ -135,6 +135,11 @@ class SimulatedCluster:
     def unblock_all(self):
         self._ck(self.lib.swim_unblock_all(self._h), "swim_unblock_all")
 
+    def join(self, member, seeds=()):
+        """Cluster.join of a new process for a dormant member (SimConfig.n_dormant) with its own seedMembers."""
+        arr = (C.c_uint32 * max(1, len(seeds)))(*[int(x) for x in seeds])
+        self._ck(self.lib.swim_join(self._h, member, arr, len(seeds)), "swim_join")
+
     def spread_gossip(self, member, payload):
         """Cluster.spreadGossip(message): a user gossip from member carrying a 64-bit payload (ClusterImpl.java:208)."""
         self._ck(self.lib.swim_spread_gossip(self._h, member, int(payload) & (2**64 - 1)), "swim_spread_gossip")

@@ -69,6 +69,7 @@ class SimConfig:
     list_slack: int = 0
     mode: int = _abi.MODE_FULL  # MODE_RUMOR: gossip layer only, churn_per_period rumors per period (SEMANTICS.md §9)
     churn_per_period: int = 0
+    n_dormant: int = 0  # COLD_JOIN: the last n_dormant members start only on join()
     device: int = 0
 
     def to_abi(self):
@@ -91,6 +92,7 @@ class SimConfig:
         a.metadata_timeout_ms = c.metadataTimeout
         a.mode = self.mode
         a.churn_per_period = self.churn_per_period
+        a.n_dormant = self.n_dormant
         a.flags = (_abi.FLAG_RECORD_EVENTS if self.record_events else 0) | (_abi.FLAG_PROFILE if self.profile else 0)
         seeds = list(dict.fromkeys(c.seedMembers))
         if len(seeds) > 16:

@@ -247,6 +247,10 @@ class ThreadShardGroup:
         for s in self.shards:
             s.spread_gossip(m, payload)
 
+    def join(self, m, seeds=()):
+        for s in self.shards:
+            s.join(m, seeds)
+
     def set_link_loss(self, src, dst, pct):
         for s in self.shards:
             s.set_link_loss(src, dst, pct)

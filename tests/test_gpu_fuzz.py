@@ -49,14 +49,22 @@ def schedule(seed):
         acts.append(("run", int(rng.integers(20, 200))))
     # user gossips (Cluster.spreadGossip) from a separate stream, so the fault schedules above stay as they were
     rg = np.random.default_rng(seed + 10_000)
+    if cold and rg.integers(2):  # late joins: the last two members are dormant and start with their own seeds
+        import dataclasses
+        cfg = dataclasses.replace(cfg, n_dormant=2)
+        for m in (n - 2, n - 1):
+            pos = 1 + 2 * int(rg.integers(len(acts) // 2))
+            acts.insert(pos, ("join", (m, [int(x) for x in rg.integers(n - 2, size=int(rg.integers(0, 3)))])))
     for _ in range(int(rg.integers(1, 4))):
         pos = 1 + 2 * int(rg.integers(len(acts) // 2))
         acts.insert(pos, ("gossip", [(int(rg.integers(n)), int(rg.integers(1 << 63))) for _ in range(int(rg.integers(1, 4)))]))
     return cfg, acts
 
 
-def play(o, e, acts, where):
+def play(o, e, acts, where, n_dormant=0):
     dead = set()
+    n = o.n
+    dormant = set(range(n - n_dormant, n))
     for what, arg in acts:
         if what == "run":
             run_lockstep(o, e, arg, max(10, arg // 3), where)
@@ -65,6 +73,10 @@ def play(o, e, acts, where):
             continue
         if what == "gossip":
             arg = [(m, p) for m, p in arg if m not in dead]
+        if what in ("inc", "leave", "kill") and arg in dormant:
+            continue
+        if what == "gossip":
+            arg = [(m, p) for m, p in arg if m not in dormant]
         for c in (o, e):
             if what == "loss":
                 c.set_default_loss(arg)
@@ -88,15 +100,19 @@ def play(o, e, acts, where):
             elif what == "gossip":
                 for m, p in arg:
                     c.spread_gossip(m, p)
+            elif what == "join":
+                c.join(arg[0], arg[1])
         if what in ("kill", "leave"):
             dead.add(arg)
+        if what == "join":
+            dormant.discard(arg[0])
 
 
 @pytest.mark.parametrize("seed", range(24))
 def test_fuzz_single_gpu(oracle, engine, seed):
     cfg, acts = schedule(seed)
     o, e = SimulatedCluster(oracle, cfg), SimulatedCluster(engine, cfg)
-    play(o, e, acts, f"fuzz seed {seed} N={cfg.n_members}")
+    play(o, e, acts, f"fuzz seed {seed} N={cfg.n_members}", cfg.n_dormant)
     e.close()
 
 
@@ -105,5 +121,5 @@ def test_fuzz_sharded(oracle, engine, seed):
     from swimhip.shard import ThreadShardGroup
     cfg, acts = schedule(seed)
     o, e = SimulatedCluster(oracle, cfg), ThreadShardGroup(engine, cfg, 2)
-    play(o, e, acts, f"fuzz seed {seed} N={cfg.n_members} W=2")
+    play(o, e, acts, f"fuzz seed {seed} N={cfg.n_members} W=2", cfg.n_dormant)
     e.close()

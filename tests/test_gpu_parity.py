@@ -214,3 +214,40 @@ def test_rumor_mode_sharded(oracle, engine):
     o, e = SimulatedCluster(oracle, cfg), ThreadShardGroup(engine, cfg, 2)
     run_lockstep(o, e, 200, 40, "rumor W=2")
     e.close()
+
+
+def test_joins_and_restarts(oracle, engine):
+    """ClusterImpl.join0 of late processes (MembershipProtocolTest.testLimitedSeedMembers / testRestartFailedMembers
+    shapes): dormant members join with their own seeds, crashed members are replaced by new ids, under 10 % loss."""
+    cfg = SimConfig(n_members=60, cluster=ClusterConfig(seedMembers=[0]), init_mode=_abi.INIT_COLD_JOIN,
+                    record_events=True, n_dormant=12)
+    o, e = pair(oracle, engine, cfg)
+    run_lockstep(o, e, 40, 10, "initial 48")
+    for c in (o, e):
+        c.join(48, [0])
+        c.join(49, [5, 6])
+        c.join(50, [])
+    run_lockstep(o, e, 60, 15, "three joins")
+    for c in (o, e):
+        c.set_default_loss(10)
+        c.kill(3)
+        c.kill(4)
+        c.join(51, [0, 1])
+    run_lockstep(o, e, 250, 50, "kills + restart under loss")
+    for c in (o, e):
+        for m in range(52, 60):
+            c.join(m, [m - 52, 48])
+    run_lockstep(o, e, 200, 50, "eight joins at once")
+
+
+def test_joins_sharded(oracle, engine):
+    from swimhip.shard import ThreadShardGroup
+    cfg = SimConfig(n_members=45, cluster=ClusterConfig(seedMembers=[0]), init_mode=_abi.INIT_COLD_JOIN,
+                    record_events=True, n_dormant=6)
+    o, e = SimulatedCluster(oracle, cfg), ThreadShardGroup(engine, cfg, 3)
+    run_lockstep(o, e, 30, 10, "initial W=3")
+    for c in (o, e):
+        for m in range(39, 45):
+            c.join(m, [m % 7])
+    run_lockstep(o, e, 120, 30, "joins W=3")
+    e.close()

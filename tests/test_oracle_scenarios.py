@@ -275,3 +275,51 @@ def test_rumor_mode_churn(oracle):
 def test_rumor_mode_requires_preconverged(oracle):
     with pytest.raises(Exception):
         SimulatedCluster(oracle, SimConfig(n_members=10, mode=_abi.MODE_RUMOR, init_mode=_abi.INIT_COLD_JOIN))
+
+
+def test_limited_seed_members(oracle):  # MembershipProtocolTest.testLimitedSeedMembers (:433-462)
+    """a has no seeds, b and c seed on a, d and e seed on b; after 3 s everyone trusts everyone."""
+    cfg = mp_config(5, n_dormant=5)
+    c = SimulatedCluster(oracle, cfg)
+    for m, seeds in [(0, []), (1, [0]), (2, [0]), (3, [1]), (4, [1])]:
+        c.join(m, seeds)
+    c.step(ticks_for_seconds(3))
+    for o in range(5):
+        assert trusted(c, o) == [0, 1, 2, 3, 4] and suspected(c, o) == []
+
+
+def test_restart_failed_members(oracle):  # MembershipProtocolTest.testRestartFailedMembers (:369-430)
+    """c and d stop; after the suspicion timeout a and b trust only each other; c and d restart (new ids 4 and 5, as
+    the reference's restarted members get new ids) seeded on a and b, and all four trust each other."""
+    c = SimulatedCluster(oracle, mp_config(6, n_dormant=2))  # members 4, 5: the restarted c, d
+    c.step(ticks_for_seconds(1))
+    for o in range(4):
+        assert trusted(c, o) == [0, 1, 2, 3]
+    c.kill(2)
+    c.kill(3)
+    c.step(ticks_for_seconds(1))
+    for o in (0, 1):
+        assert trusted(c, o) == [0, 1] and suspected(c, o) == [2, 3]
+    susp_sec = 5 * 3 * 200 // 1000  # ClusterMath.suspicionTimeout(5, 4, 200) / 1000
+    c.step(ticks_for_seconds(susp_sec + 1))
+    for o in (0, 1):
+        assert trusted(c, o) == [0, 1] and suspected(c, o) == []
+    c.join(4, [0, 1])
+    c.join(5, [0, 1])
+    c.step(ticks_for_seconds(1))
+    for o in (0, 1, 4, 5):
+        assert trusted(c, o) == [0, 1, 4, 5] and suspected(c, o) == [], o
+
+
+def test_join_rules(oracle):
+    c = SimulatedCluster(oracle, mp_config(4, n_dormant=1))
+    with pytest.raises(Exception):
+        c.join(1, [0])  # not dormant
+    c.step(5)
+    c.join(3, [0, 0, 3, 99])  # duplicates, self and unknown ids are dropped
+    with pytest.raises(Exception):
+        c.join(3, [0])  # joins once
+    c.step(ticks_for_seconds(1))
+    assert trusted(c, 3) == [0, 1, 2, 3]
+    with pytest.raises(Exception):
+        SimulatedCluster(oracle, SimConfig(n_members=4, n_dormant=1))  # PRECONVERGED has no dormant members
