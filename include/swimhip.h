@@ -154,6 +154,10 @@ int swim_unblock_link(swim_handle* h, uint32_t src, uint32_t dst);
 /* MembershipProtocolImpl.updateIncarnation (:178-190): the member bumps its own incarnation and spreads it, at the
  * start (P0) of the next tick; what ClusterImpl.updateMetadata does after storing new metadata */
 int swim_update_incarnation(swim_handle* h, uint32_t member);
+/* ClusterImpl.updateMetadata (:254-258): metadataStore.updateMetadata, then membership.updateIncarnation. The member's
+ * metadata version (what GET_METADATA_RESP carries, MetadataStoreImpl.java:202-241) is bumped at once, between ticks;
+ * the incarnation bump and its gossip follow at P0 of the next tick, as swim_update_incarnation */
+int swim_update_metadata(swim_handle* h, uint32_t member);
 /* ClusterImpl.shutdown -> MembershipProtocolImpl.leaveCluster (ClusterImpl.java:297-313, MembershipProtocolImpl.java:197-206):
  * at the start (P0) of the next tick the member's own record becomes DEAD inc+1 and is spread as gossip; when that
  * gossip is swept at the member (the leave Mono completes), the member stops as if killed, from the next tick */

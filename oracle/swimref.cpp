@@ -145,7 +145,7 @@ struct Member {
   uint64_t initDeadline = NEVER;
 
   uint64_t nextPing = NEVER, nextGossip = NEVER, nextSync = NEVER;
-  bool pendingInc = false;  // swim_update_incarnation, applied in P0 of the next tick
+  uint32_t pendingInc = 0;  // swim_update_incarnation calls, applied in P0 of the next tick (one bump each)
   bool pendingLeave = false;  // swim_leave (leaveCluster), applied in P0 of the next tick after pendingInc
   uint64_t startTick = NEVER;  // COLD_JOIN: 0 for the initial members, the join tick for a dormant one (swim_join)
   bool dormant = false;
@@ -637,8 +637,7 @@ void Member::process(uint64_t k, std::vector<Msg>& inbox) {
   Sim& s = *sim;
   for (uint64_t p : pendingUser) spread(USER_SUBJ, Rec{}, p);  // Cluster.spreadGossip (ClusterImpl.java:208-211)
   pendingUser.clear();
-  if (pendingInc) {  // updateIncarnation (MembershipProtocolImpl.java:178-190)
-    pendingInc = false;
+  for (; pendingInc > 0; --pendingInc) {  // updateIncarnation (MembershipProtocolImpl.java:178-190), once per call
     Rec r{ALIVE, table[id].inc + 1};
     table[id] = r;
     s.ctr.row_writes++;
@@ -1030,7 +1029,13 @@ __attribute__((visibility("default"))) int swim_kill(swim_handle* h, uint32_t m)
 }
 __attribute__((visibility("default"))) int swim_update_incarnation(swim_handle* h, uint32_t m) {
   if (!h || m >= h->sim.N || !h->sim.members[m].alive) return SWIM_EINVAL;
-  h->sim.members[m].pendingInc = true;
+  h->sim.members[m].pendingInc++;
+  return SWIM_OK;
+}
+__attribute__((visibility("default"))) int swim_update_metadata(swim_handle* h, uint32_t m) {
+  if (!h || m >= h->sim.N || !h->sim.members[m].alive) return SWIM_EINVAL;
+  h->sim.md_version[m]++;  // MetadataStoreImpl.updateMetadata (:111-132), effective for the next response
+  h->sim.members[m].pendingInc++;
   return SWIM_OK;
 }
 __attribute__((visibility("default"))) int swim_leave(swim_handle* h, uint32_t m) {

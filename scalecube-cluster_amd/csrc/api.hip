@@ -47,6 +47,7 @@ struct swim_handle {
   double xchg_ms = 0;                 // host time spent in the exchanges
   bool xflag = false;                 // last exchange: some shard has a gossip slot in use
   std::vector<uint8_t> joined;  // swim_join: dormant members that were started
+  std::vector<uint32_t> md_cols;  // swim_update_metadata: members that own a metadata-version column
   std::vector<uint64_t> ugq;  // swim_spread_gossip queue: (member, payload) pairs for P0 of the next tick
   uint64_t* ug_dev = nullptr;  // device copy of ugq
   size_t ug_cap = 0;
@@ -258,7 +259,7 @@ int build(swim_handle* h) {
   const uint64_t NL = d.NL;  // per-observer arrays: this shard's rows only
   A(d.row, NL * d.NS) A(d.fdl, NL * d.LCAP) A(d.gl, NL * d.LCAP)
   A(d.subs, NL * SUBCAP * 4) A(d.paths, NL * PATHCAP * 5) A(d.fetch, NL * d.FCAP * FREC) A(d.groups, NL * d.GRCAP * GREC)
-  A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.slow, d.SLOWCAP) A(d.slow_n, 1) A(d.rlist, N) A(d.rn, 1) A(d.start_tick, N) A(d.jseed_n, N) A(d.jseeds, 16 * N) A(d.churn_q, 2ull * d.churn) A(d.cin, N * d.F) A(d.swthr, N) A(d.HB, (uint64_t)(d.SLOTS / 64 + 1) * N) A(d.WB, (uint64_t)(d.SLOTS / 64 + 1) * N) A(d.cev, N * d.F * CEVW)
+  A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.slow, d.SLOWCAP) A(d.slow_n, 1) A(d.rlist, N) A(d.rn, 1) A(d.start_tick, N) A(d.jseed_n, N) A(d.jseeds, 16 * N) A(d.md_uidx, N) A(d.md_ver, NL * MDU) A(d.churn_q, 2ull * d.churn) A(d.cin, N * d.F) A(d.swthr, N) A(d.HB, (uint64_t)(d.SLOTS / 64 + 1) * N) A(d.WB, (uint64_t)(d.SLOTS / 64 + 1) * N) A(d.cev, N * d.F * CEVW)
   A(d.log_tick, N * d.LOGW) A(d.log_spread, N * d.LOGW) A(d.log_cnt, N * d.LOGW) A(d.log_tg, N * d.LOGW * d.F)
   A(d.log_pos, N) A(d.spchg, N)
   A(d.slot_gid, d.SLOTS) A(d.slot_subj, d.SLOTS) A(d.slot_ctick, d.SLOTS) A(d.slot_key, d.SLOTS) A(d.slot_holders, d.SLOTS)
@@ -683,6 +684,28 @@ int swim_spread_gossip(swim_handle* h, uint32_t m, uint64_t payload) {
   return SWIM_OK;
 }
 
+int swim_update_metadata(swim_handle* h, uint32_t m) {
+  if (!h || m >= h->d.N) return SWIM_EINVAL;
+  uint32_t dt = 0, ver = 0;
+  HIPCK(hipStreamSynchronize(h->stream));
+  HIPCK(hipMemcpy(&dt, h->d.dead_tick + m, 4, hipMemcpyDeviceToHost));
+  if (dt != NEVER) return SWIM_EINVAL;
+  if (std::find(h->md_cols.begin(), h->md_cols.end(), m) == h->md_cols.end()) {
+    if (h->md_cols.size() >= MDU) {
+      h->err = "swim_update_metadata: more than " + std::to_string(MDU) + " members with updated metadata";
+      return SWIM_ECAPACITY;
+    }
+    launch_md_column(h->d, m, (uint32_t)h->md_cols.size(), h->stream);
+    h->md_cols.push_back(m);
+    HIPCK(hipStreamSynchronize(h->stream));
+  }
+  // every shard keeps the versions of all members (responses are evaluated at the issuer's shard)
+  HIPCK(hipMemcpy(&ver, h->d.md_version + m, 4, hipMemcpyDeviceToHost));
+  ++ver;
+  HIPCK(hipMemcpy(h->d.md_version + m, &ver, 4, hipMemcpyHostToDevice));
+  return swim_update_incarnation(h, m);
+}
+
 int swim_update_incarnation(swim_handle* h, uint32_t m) {
   if (!h || m >= h->d.N) return SWIM_EINVAL;
   if (!owns(h, m)) return SWIM_OK;  // the owning shard bumps it; the others learn it from its gossip
@@ -691,7 +714,7 @@ int swim_update_incarnation(swim_handle* h, uint32_t m) {
   HIPCK(hipMemcpy(&dt, h->d.dead_tick + m, 4, hipMemcpyDeviceToHost));
   if (dt != NEVER) return SWIM_EINVAL;
   HIPCK(hipMemcpy(&req, h->d.pending_inc + m, 4, hipMemcpyDeviceToHost));
-  req |= 1u;
+  req += 4u;  // bits 2..: incarnation bumps requested (one per call), bit 1: leave
   HIPCK(hipMemcpy(h->d.pending_inc + m, &req, 4, hipMemcpyHostToDevice));
   return SWIM_OK;
 }

@@ -33,6 +33,7 @@ constexpr uint32_t E_SLOTS = 1, E_FETCH = 2, E_SUBS = 4, E_PATHS = 8, E_GROUPS =
 constexpr uint32_t LKCAP = 4096, LKH = 8;  // keys, history entries per key
 constexpr uint32_t DEATHCAP = 4096;        // completed leaves per tick
 constexpr uint32_t CIN_SLOW = 0xFFFFFFFEu;
+constexpr uint32_t MDU = 64;  // members with updated metadata per handle
 constexpr uint32_t CEV = 6, CEVW = 4 + 2 * CEV;  // cached contact events per (sender, target): n, oldest[2], events
 // gossip incarnation history entry: 3 header words + HKEEP creation ticks of swept incarnations (small clusters
 // under loss re-infect a member with the same gossip many times: each late sender restarts the chain)
@@ -66,6 +67,8 @@ struct Dev {
   uint32_t* start_tick;  // [N] tick of start0 (0: initial COLD_JOIN members; NEVER: PRECONVERGED or not joined yet)
   uint32_t* jseed_n;     // [N] seeds of a joined member (NONE32: the config's seeds)
   uint32_t* jseeds;      // [N][16]
+  uint32_t* md_uidx;  // [N] column of a member whose metadata was updated (swim_update_metadata), NONE32 if never
+  uint32_t* md_ver;   // [NL][MDU] metadata version each observer stores for those members (the others: 0 if known)
   uint32_t mode, churn;  // SWIM_MODE_RUMOR: gossip layer only, churn rumors per FD period (SEMANTICS.md §9)
   uint64_t* churn_q;     // [churn][2] (origin, payload) of this period's rumors
   uint32_t seeds[16];
@@ -141,7 +144,7 @@ struct Dev {
   uint32_t* arena_used;  // [2]
   uint32_t* m_next; // [2][MSGCAP] next message of msgs[b] to the same destination
   uint32_t* m_head; // [2][N] first message of msgs[b] to each destination, NEVER if none (reset by the consumer)
-  uint32_t* pending_inc; // [N] host requests for the next tick's P0: 1 updateIncarnation, 2 leaveCluster
+  uint32_t* pending_inc; // [N] host requests for the next tick's P0: bits 2.. updateIncarnation calls, bit 1 leaveCluster
   uint32_t *deaths, *deaths_n;  // [2][DEATHCAP], [2]: members whose leave completed at tick k (parity k & 1)
   uint32_t* next_evt; // [N] earliest tick at which a pending path / subscription / fetch needs the member
   uint32_t *busy, *nbusy; // members that need the full control path this tick, per block of 256 (k_member_triage)
@@ -225,6 +228,7 @@ void launch_inline_in(const Dev& d, uint8_t* recv, uint64_t cap, const unsigned 
 void launch_kill(const Dev& d, uint32_t member, void* stream);
 void launch_user_gossips(const Dev& d, uint32_t k, const uint64_t* q, uint32_t n, void* stream);
 void launch_churn(const Dev& d, uint32_t k, void* stream);
+void launch_md_column(const Dev& d, uint32_t m, uint32_t u, void* stream);
 void launch_join(const Dev& d, uint32_t m, uint32_t k, const uint32_t* seeds, uint32_t n, void* stream);  // RUMOR mode, at ticks k % ping_t == 0
 void launch_hash(const Dev& d, uint64_t* out, uint32_t now, void* stream);
 

@@ -42,6 +42,7 @@ __global__ void k_init_members(Dev d) {
   const bool dormant = m >= d.N - d.n_dormant;  // not started until swim_join (k_join)
   d.start_tick[m] = (pre || dormant) ? NEVER : 0u;
   d.jseed_n[m] = NONE32;
+  d.md_uidx[m] = NONE32;
   d.cidCnt[m] = d.syncSeq[m] = d.evSeq[m] = d.held[m] = 0;
   d.timerMin[m] = NEVER;
   d.initFlags[m] = d.initDeadline[m] = d.initCidBase[m] = d.initN[m] = 0;
@@ -1102,6 +1103,18 @@ void launch_tick_c(const Dev& d, uint32_t k, void* stream, bool gossip) {
   hipLaunchKernelGGL(k_gossip_free, dim3(1024), dim3(256), 0, st, d, d.active, d.nactive);
   hipLaunchKernelGGL(k_round_reset, dim3(16, d.W), dim3(256), 0, st, d);
   hipLaunchKernelGGL(k_tick_end, dim3(1), dim3(64), 0, st, d, k);
+}
+
+// swim_update_metadata of a member with no column yet: column u; every local observer stores version 0 (the only
+// version it could have fetched so far)
+__global__ void k_md_column(Dev d, uint32_t m, uint32_t u) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) d.md_uidx[m] = u;
+  if (i < d.NL) d.md_ver[(size_t)i * MDU + u] = 0;
+}
+
+void launch_md_column(const Dev& d, uint32_t m, uint32_t u, void* stream) {
+  hipLaunchKernelGGL(k_md_column, dim3((d.NL + 255) / 256), dim3(256), 0, (hipStream_t)stream, d, m, u);
 }
 
 // swim_join: a dormant member starts at tick k as a fresh process (ClusterImpl.join0, schedules from k) with its seeds

@@ -236,6 +236,14 @@ void launch_user_gossips(const Dev& d, uint32_t k, const uint64_t* q, uint32_t n
   hipLaunchKernelGGL(k_user_gossips, dim3(1), dim3(64), 0, (hipStream_t)stream, d, k, q, n);
 }
 
+// the metadata version this observer stores for subj (MetadataStoreImpl.membersMetadata), NONE32 if unknown
+__device__ __forceinline__ uint32_t known_meta(const ML& L, uint32_t subj, uint64_t v) {
+  if (!(v & META_BIT)) return NONE32;
+  const Dev& d = *L.d;
+  const uint32_t u = d.md_uidx[subj];
+  return u == NONE32 ? 0u : d.md_ver[lidx(d, L.m) * MDU + u];
+}
+
 __device__ __forceinline__ uint32_t* grp(ML& L, int g) { return L.groups + (size_t)g * GREC; }
 
 __device__ __forceinline__ void complete_group(ML& L, int g) {
@@ -341,7 +349,7 @@ __device__ __forceinline__ void update_membership(ML& L, uint32_t subj, uint32_t
   }
   L.c[C_W]++;
   if (s1 == ST_DEAD) {
-    uint32_t oldm = (v0 & META_BIT) ? 0u : NONE32;  // metadataStore.removeMetadata
+    uint32_t oldm = known_meta(L, subj, v0);  // metadataStore.removeMetadata
     emit_event(L, 1, subj, oldm, NONE32);
     finish(L, g, false);
     do_finally(L, subj, s1, i1, reason);
@@ -682,7 +690,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   const uint32_t preq = dead ? 0u : d.pending_inc[m];
   if (preq) {
     d.pending_inc[m] = 0;
-    if (preq & 1u) {
+    for (uint32_t b = preq >> 2; b > 0; --b) {  // one bump and one gossip per swim_update_incarnation call
       uint64_t v0 = L.row[m];
       uint32_t ni = rec_inc(v0) + 1u;
       row_put(L, m, (v0 & ~KEY_MASK) | rec_key(ST_ALIVE, ni));
@@ -921,8 +929,10 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
         uint32_t st = w3 & 0xFF, reason = (w3 >> 8) & 0xFF, added = (w3 >> 16) & 0xFF;
         // doOnSuccess (:563-567, :576-581): updateMetadata then sink.next
         uint64_t v = L.row[subj];
-        uint32_t oldm = (v & META_BIT) ? 0u : NONE32;
+        uint32_t oldm = known_meta(L, subj, v);
         L.row[subj] = v | META_BIT;
+        const uint32_t u = d.md_uidx[subj];
+        if (u != NONE32) d.md_ver[lidx(d, m) * MDU + u] = meta;
         if (added)
           emit_event(L, 0, subj, NONE32, meta);
         else

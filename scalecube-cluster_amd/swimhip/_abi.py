@@ -113,6 +113,7 @@ SIGNATURES = {
     "swim_set_link_loss": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.c_uint32]),
     "swim_unblock_link": (C.c_int, [_H, C.c_uint32, C.c_uint32]),
     "swim_update_incarnation": (C.c_int, [_H, C.c_uint32]),
+    "swim_update_metadata": (C.c_int, [_H, C.c_uint32]),
     "swim_leave": (C.c_int, [_H, C.c_uint32]),
     "swim_spread_gossip": (C.c_int, [_H, C.c_uint32, C.c_uint64]),
     "swim_join": (C.c_int, [_H, C.c_uint32, C.POINTER(C.c_uint32), C.c_uint32]),

@@ -132,6 +132,10 @@ class SimulatedCluster:
     def update_incarnation(self, member):
         self._ck(self.lib.swim_update_incarnation(self._h, member), "swim_update_incarnation")
 
+    def update_metadata(self, member):
+        """Cluster.updateMetadata: a new metadata version for member, then updateIncarnation (ClusterImpl.java:254)."""
+        self._ck(self.lib.swim_update_metadata(self._h, member), "swim_update_metadata")
+
     def unblock_all(self):
         self._ck(self.lib.swim_unblock_all(self._h), "swim_unblock_all")
 

@@ -267,6 +267,10 @@ class ThreadShardGroup:
         for s in self.shards:
             s.update_incarnation(m)
 
+    def update_metadata(self, m):
+        for s in self.shards:
+            s.update_metadata(m)
+
     def state_hash(self):
         h = self.shards[0].state_hash().copy()
         for s in self.shards[1:]:

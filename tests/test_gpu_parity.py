@@ -251,3 +251,21 @@ def test_joins_sharded(oracle, engine):
             c.join(m, [m % 7])
     run_lockstep(o, e, 120, 30, "joins W=3")
     e.close()
+
+
+def test_update_metadata(oracle, engine):
+    """ClusterImpl.updateMetadata: new metadata version + incarnation bump; UPDATED events carry the new version;
+    two updates of one member in one step, and one under loss."""
+    cfg = SimConfig(n_members=70, record_events=True)
+    o, e = pair(oracle, engine, cfg)
+    run_lockstep(o, e, 15, 5, "warm")
+    for c in (o, e):
+        c.update_metadata(4)
+        c.update_metadata(4)
+        c.update_metadata(33)
+    ev = run_lockstep(o, e, 60, 15, "metadata updates")
+    assert {x.newMetadata for x in ev if x.isUpdated() and x.member == 4} == {2}
+    for c in (o, e):
+        c.set_default_loss(15)
+        c.update_metadata(33)
+    run_lockstep(o, e, 120, 30, "metadata update under loss")

@@ -323,3 +323,22 @@ def test_join_rules(oracle):
     assert trusted(c, 3) == [0, 1, 2, 3]
     with pytest.raises(Exception):
         SimulatedCluster(oracle, SimConfig(n_members=4, n_dormant=1))  # PRECONVERGED has no dormant members
+
+
+def test_update_metadata(oracle):  # ClusterTest.testUpdateMetadata (:108-169)
+    """A seed, a metadata member and ten others join; after 3 s all know the metadata member with its metadata
+    (version 0); after updateMetadata every other member emits UPDATED carrying the new version and stores it."""
+    n = 12
+    cfg = SimConfig(n_members=n, cluster=ClusterConfig(seedMembers=[0]), init_mode=_abi.INIT_COLD_JOIN,
+                    record_events=True)
+    c = SimulatedCluster(oracle, cfg)
+    c.step(ticks_for_seconds(3, 100))
+    for o in range(n):
+        recs = {r.member: r for r in c.records(o)}
+        assert 1 in recs and recs[1].has_metadata
+    c.events()
+    c.update_metadata(1)
+    c.step(ticks_for_seconds(3, 100))
+    ups = [e for e in c.events() if e.isUpdated() and e.member == 1]
+    assert sorted(e.observer for e in ups) == [o for o in range(n) if o != 1]
+    assert all(e.oldMetadata == 0 and e.newMetadata == 1 for e in ups)
