@@ -269,3 +269,39 @@ def test_update_metadata(oracle, engine):
         c.set_default_loss(15)
         c.update_metadata(33)
     run_lockstep(o, e, 120, 30, "metadata update under loss")
+
+
+def test_fast_config_blocks_restart_lockstep(oracle, engine):
+    """MembershipProtocolTest's double partition, disabled network and restart scenarios (fast config) in lockstep:
+    per-member blocks, unblockAll, a crash, a restart under a new id, a join whose only seed never started."""
+    n = 7
+    cc = ClusterConfig(seedMembers=[0, 1, 2, 3], syncInterval=500, syncTimeout=100, pingInterval=200,
+                       pingTimeout=100, metadataTimeout=100)
+    cfg = SimConfig(n_members=n, cluster=cc, init_mode=_abi.INIT_COLD_JOIN, tick_ms=10, record_events=True,
+                    n_dormant=3)
+    o, e = pair(oracle, engine, cfg)
+    run_lockstep(o, e, 100, 20, "joined")
+    for c in (o, e):
+        c.block(1, 0, 2, 3)
+        c.block(0, 1)
+        c.block(2, 1)
+    run_lockstep(o, e, 100, 20, "b lost")
+    for c in (o, e):
+        c.block(0, 2)
+        c.block(2, 0)
+    run_lockstep(o, e, 100, 20, "a, c lost")
+    for c in (o, e):
+        c.unblock_all()
+    run_lockstep(o, e, 100, 20, "recovered")
+    for c in (o, e):
+        for m in range(4):
+            c.block(m, 0, 1, 2, 3)
+    run_lockstep(o, e, 100, 20, "network disabled")
+    for c in (o, e):
+        c.unblock_all()
+        c.kill(3)
+    run_lockstep(o, e, 150, 30, "recovered, 3 crashed")
+    for c in (o, e):
+        c.join(4, [0])
+        c.join(5, [6])  # 6 never starts
+    run_lockstep(o, e, 600, 50, "restart as 4, lonely 5")

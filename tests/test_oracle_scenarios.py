@@ -342,3 +342,68 @@ def test_update_metadata(oracle):  # ClusterTest.testUpdateMetadata (:108-169)
     ups = [e for e in c.events() if e.isUpdated() and e.member == 1]
     assert sorted(e.observer for e in ups) == [o for o in range(n) if o != 1]
     assert all(e.oldMetadata == 0 and e.newMetadata == 1 for e in ups)
+
+
+def _check_views(c, views):
+    for o, (tr, su) in views.items():
+        assert trusted(c, o) == tr and suspected(c, o) == su, (o, trusted(c, o), suspected(c, o))
+
+
+def test_double_partition_then_recover(oracle):  # MembershipProtocolTest.testDoublePartitionThenRecover (:188-256)
+    c = SimulatedCluster(oracle, mp_config(3))
+    c.step(ticks_for_seconds(1))
+    _check_views(c, {o: ([0, 1, 2], []) for o in range(3)})
+    c.block(1, 0, 2)  # b lost the network
+    c.block(0, 1)
+    c.block(2, 1)
+    c.step(ticks_for_seconds(1))
+    _check_views(c, {0: ([0, 2], [1]), 1: ([1], [0, 2]), 2: ([0, 2], [1])})
+    c.block(0, 2)  # a and c lost the network
+    c.block(2, 0)
+    c.step(ticks_for_seconds(1))
+    _check_views(c, {0: ([0], [1, 2]), 1: ([1], [0, 2]), 2: ([2], [0, 1])})
+    c.unblock_all()
+    c.step(ticks_for_seconds(1))
+    _check_views(c, {o: ([0, 1, 2], []) for o in range(3)})
+
+
+def test_network_disabled_then_recovered(oracle):  # MembershipProtocolTest.testNetworkDisabledThenRecovered (:258-311)
+    c = SimulatedCluster(oracle, mp_config(3))
+    c.step(ticks_for_seconds(1))
+    _check_views(c, {o: ([0, 1, 2], []) for o in range(3)})
+    for m in range(3):
+        c.block(m, 0, 1, 2)  # block(members): every link, including to itself
+    c.step(ticks_for_seconds(1))
+    _check_views(c, {0: ([0], [1, 2]), 1: ([1], [0, 2]), 2: ([2], [0, 1])})
+    c.unblock_all()
+    c.step(ticks_for_seconds(1))
+    _check_views(c, {o: ([0, 1, 2], []) for o in range(3)})
+
+
+def test_fd_status_change_after_member_restart(oracle):  # FailureDetectorTest.testStatusChangeAfterMemberRestart
+    """(:345-401) a, b, x; x stops, then a new process x' (new id) starts seeded on a: a and b see x suspected, then
+    x' trusted. (Later, the cold-join ALIVE gossips about x that are still circulating re-add x after its removal, with
+    no ADDED event because its metadata cannot be fetched: the reference's own zombie behaviour, not asserted there.)"""
+    c = SimulatedCluster(oracle, mp_config(4, n_dormant=1))  # member 3 = x'
+    c.step(ticks_for_seconds(1))
+    c.kill(2)
+    c.step(ticks_for_seconds(1))
+    for o in (0, 1):
+        assert 2 in suspected(c, o)
+    c.join(3, [0])
+    c.step(ticks_for_seconds(1))
+    for o in (0, 1, 3):
+        assert 3 in trusted(c, o) and 3 not in suspected(c, o)
+
+
+def test_join_seed_cluster_with_no_existing_seed_member(oracle):  # ClusterTest (:376-392)
+    """A member whose only seed does not exist (a dead id) starts alone: the initial sync fails and it keeps running
+    with itself as the only member."""
+    cc = ClusterConfig(seedMembers=[0], syncInterval=500, syncTimeout=100, pingInterval=200, pingTimeout=100,
+                       metadataTimeout=100)
+    c = SimulatedCluster(oracle, SimConfig(n_members=3, cluster=cc, init_mode=_abi.INIT_COLD_JOIN, tick_ms=10,
+                                           n_dormant=2, record_events=True))
+    c.join(2, [1])  # member 1 never starts: a seed address with no member behind it
+    c.step(ticks_for_seconds(2))
+    assert trusted(c, 2) == [2] and suspected(c, 2) == []
+    assert trusted(c, 0) == [0]
