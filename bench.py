@@ -212,7 +212,7 @@ def main():
                                 "frac": B / dt / 1e9 / HBM_PEAK_GBPS, "traffic": None}
             line["kernel_time_share"] = {}
         if not a.no_cpu_baseline and world == 1:
-            cm, cp = {"c3": (a.cpu_members, a.cpu_periods), "c2": (500, 6), "c5": (2000, 10)}[a.workload]
+            cm, cp = {"c3": (a.cpu_members, a.cpu_periods), "c2": (600, 25), "c5": (2000, 12)}[a.workload]
             line["cpu_baseline"] = cpu_baseline(a, cm, cp)
         else:
             line["cpu_baseline"] = None
