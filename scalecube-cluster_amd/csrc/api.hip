@@ -244,6 +244,7 @@ int build(swim_handle* h) {
   d.DCAP = (uint32_t)std::min<uint64_t>(1ull << 27, std::max<uint64_t>(1ull << 16, N * 16384));
   d.RCAP = d.DCAP;
   d.SLOWCAP = d.DCAP;
+  d.RPCAP = d.DCAP;
   d.ARENA_ROWS = 64;
 
   int rc;
@@ -259,7 +260,7 @@ int build(swim_handle* h) {
   const uint64_t NL = d.NL;  // per-observer arrays: this shard's rows only
   A(d.row, NL * d.NS) A(d.fdl, NL * d.LCAP) A(d.gl, NL * d.LCAP)
   A(d.subs, NL * SUBCAP * 4) A(d.paths, NL * PATHCAP * 5) A(d.fetch, NL * d.FCAP * FREC) A(d.groups, NL * d.GRCAP * GREC)
-  A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.slow, d.SLOWCAP) A(d.slow_n, 1) A(d.rlist, N) A(d.rn, 1) A(d.start_tick, N) A(d.jseed_n, N) A(d.jseeds, 16 * N) A(d.md_uidx, N) A(d.md_ver, NL * MDU) A(d.churn_q, 2ull * d.churn) A(d.cin, N * d.F) A(d.swthr, N) A(d.HB, (uint64_t)(d.SLOTS / 64 + 1) * N) A(d.WB, (uint64_t)(d.SLOTS / 64 + 1) * N) A(d.cev, N * d.F * CEVW)
+  A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.slow, d.SLOWCAP) A(d.slow_n, 1) A(d.rp, d.RPCAP) A(d.rp_n, 1) A(d.rlist, N) A(d.rn, 1) A(d.start_tick, N) A(d.jseed_n, N) A(d.jseeds, 16 * N) A(d.md_uidx, N) A(d.md_ver, NL * MDU) A(d.churn_q, 2ull * d.churn) A(d.cin, N * d.F) A(d.swthr, N) A(d.HB, (uint64_t)(d.SLOTS / 64 + 1) * N) A(d.WB, (uint64_t)(d.SLOTS / 64 + 1) * N) A(d.cev, N * d.F * CEVW)
   A(d.log_tick, N * d.LOGW) A(d.log_spread, N * d.LOGW) A(d.log_cnt, N * d.LOGW) A(d.log_tg, N * d.LOGW * d.F)
   A(d.log_pos, N) A(d.spchg, N)
   A(d.slot_gid, d.SLOTS) A(d.slot_subj, d.SLOTS) A(d.slot_ctick, d.SLOTS) A(d.slot_key, d.SLOTS) A(d.slot_holders, d.SLOTS)

@@ -110,6 +110,9 @@ struct Dev {
   uint32_t* cin;    // [N][F] latest cached contact t -> m of (m, T[m][s]); NEVER: none, CIN_SLOW: list overflowed
   uint32_t* swthr;  // [N] round sweep bound of this tick (k_round_info)
   unsigned long long *HB, *WB;  // [SLOTS / 64 + 1][N] per 64-slot group: held past this tick / in a round window
+  uint64_t* rp;  // [RPCAP] (slot << 32 | m * F + s): sends of pairs with a cached contact, for k_gossip_replay
+  uint32_t* rp_n;
+  uint32_t RPCAP;
   uint32_t* cev;  // [N][F][CEVW] contact events of (m, T[m][s]) cached by k_gossip_contacts when tcontact is set
   uint32_t *log_tick, *log_spread, *log_cnt, *log_tg, *log_pos;  // [N][LOGW], tg [N][LOGW][F], pos [N]
 

@@ -609,7 +609,7 @@ __device__ __forceinline__ bool blocked_pair_cached(const Dev& d, uint32_t x, ui
 
 __global__ void k_gossip_active(Dev d, uint32_t k, uint32_t* active, uint32_t* nactive) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g == 0) *d.slow_n = *d.rn = 0;  // deferred sends and round members of this tick
+  if (g == 0) *d.slow_n = *d.rn = *d.rp_n = 0;  // deferred sends, round members and replays of this tick
   if (g >= d.SLOTS || !d.slot_used[g]) return;
   // members stopped after their leave completed at tick k - 1 hold nothing any more (as k_kill)
   const uint32_t pb = (k - 1) & 1u, nd = k > 0 ? min(d.deaths_n[pb], DEATHCAP) : 0u;
@@ -798,16 +798,17 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
         }
         continue;
       }
-      if (ci != NEVER) {  // a cached contact t -> m: replay per slot where it can matter (isInfected :247)
-        for (unsigned long long b = wb; b; b &= b - 1) {
-          const uint32_t j = __ffsll(b) - 1, g = ga[j];
-          const uint32_t c = s_ctick(d.S[(size_t)g * d.N + m]);
-          if (d.exp & 4) st[1]++;
-          if (ci >= d.slot_ctick[g] && ci + d.lat >= c) {
-            if (d.exp & 4) st[2]++;
-            if (blocked_pair_cached(d, m, t, g, d.slot_gid[g], k, c, d.cev + ms * CEVW)) ok &= ~(1ull << j);
-          }
+      if (ci != NEVER) {  // a cached contact t -> m: every slot of the pair goes to k_gossip_replay (isInfected :247)
+        const uint32_t nb = __popcll(wb);
+        if (d.exp & 4) st[1] += nb;
+        uint32_t i = atomicAdd(d.rp_n, nb);
+        for (unsigned long long b = wb; b; b &= b - 1, ++i) {
+          if (i < d.RPCAP)
+            d.rp[i] = ((uint64_t)ga[__ffsll(b) - 1] << 32) | (uint32_t)ms;
+          else
+            atomicOr(d.err, E_CONTACTS);
         }
+        continue;
       }
       sends += __popcll(ok);
       unsigned long long cand = d.dbg_send ? ok : ok & ~d.HB[(size_t)q * d.N + t];
@@ -821,6 +822,34 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
   if (d.exp & 4)
     for (int q2 = 0; q2 < 4; ++q2)
       if (st[q2]) atomicAdd(&d.ctr[8 + q2], (unsigned long long)st[q2]);
+  for (uint32_t o = 32; o > 0; o >>= 1) sends += __shfl_xor(sends, o);
+  if (lane == 0) red[wave] = sends;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long tot = red[0] + red[1] + red[2] + red[3];
+    if (tot) atomicAdd(&d.ctr[C_G], tot);
+  }
+}
+
+// sends of pairs with a cached contact, one thread per (slot, sender, target): the isInfected replay runs only where
+// the contact can matter (t -> m at or after m's incarnation start and after the gossip existed), then the send
+__global__ void __launch_bounds__(256) k_gossip_replay(const Dev* __restrict__ dp, uint32_t k) {
+  const Dev& d = *dp;
+  __shared__ unsigned long long red[4];
+  const uint32_t n = min(*d.rp_n, d.RPCAP);
+  unsigned long long sends = 0;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint64_t v = d.rp[i];
+    const uint32_t g = (uint32_t)(v >> 32), ms = (uint32_t)v, m = ms / d.F, s = ms % d.F;
+    uint32_t* Sg = d.S + (size_t)g * d.N;
+    const uint32_t t = d.T[ms], c = s_ctick(Sg[m]), ci = d.cin[ms];
+    const uint64_t gid = d.slot_gid[g];
+    if (ci >= d.slot_ctick[g] && ci + d.lat >= c && blocked_pair_cached(d, m, t, g, gid, k, c, d.cev + (size_t)ms * CEVW))
+      continue;
+    sends++;
+    send_tail(d, g, m, s, t, k, gid, Sg);
+  }
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   for (uint32_t o = 32; o > 0; o >>= 1) sends += __shfl_xor(sends, o);
   if (lane == 0) red[wave] = sends;
   __syncthreads();
@@ -1034,6 +1063,7 @@ void launch_gossip(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   hipLaunchKernelGGL(k_gossip_scan, dim3(SEND_GRID), dim3(256), 0, st, d.self, k, d.active, d.nactive);
   hipLaunchKernelGGL(k_gossip_send, dim3(SEND_GRID), dim3(256), 0, st, d.self, k, d.active, d.nactive);
   hipLaunchKernelGGL(k_gossip_send_slow, dim3(64), dim3(64), 0, st, d.self, k);  // rare; ~14 KB of stack per lane
+  hipLaunchKernelGGL(k_gossip_replay, dim3(2048), dim3(256), 0, st, d.self, k);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[5], st);
   hipLaunchKernelGGL(k_gossip_apply, dim3(1024), dim3(256), 0, st, d, k);
   launch_receipt_routing(d, st);
@@ -1086,6 +1116,7 @@ void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   hipLaunchKernelGGL(k_gossip_scan, dim3(SEND_GRID), dim3(256), 0, st, d.self, k, d.active, d.nactive);
   hipLaunchKernelGGL(k_gossip_send, dim3(SEND_GRID), dim3(256), 0, st, d.self, k, d.active, d.nactive);
   hipLaunchKernelGGL(k_gossip_send_slow, dim3(64), dim3(64), 0, st, d.self, k);  // rare; ~14 KB of stack per lane
+  hipLaunchKernelGGL(k_gossip_replay, dim3(2048), dim3(256), 0, st, d.self, k);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[5], st);
   hipLaunchKernelGGL(k_pack_b, dim3(64, d.W), dim3(256), 0, st, d);
 }
