@@ -20,7 +20,7 @@ The JSON line also carries:
   roofline      k_sync_diff algorithmic bytes (16 B x N per merged payload) / its HIP-event time, against 8 TB/s;
                 traffic = measured HBM bytes per launch from rocprofv3 PMC when available (profiles/), else null.
   cpu_baseline  the CPU oracle (oracle/swimref.cpp, a port) on a bounded sample: same workload shape at 10k members,
-                one core, timed here on the host.
+                timed here on the host on all its cores (worker threads over observer ranges, at most 16) and on one.
 """
 import argparse
 import json
@@ -48,7 +48,7 @@ def parse():
     p.add_argument("--loss", type=int, default=None, help="default: 5 (c2), 0 otherwise")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-members", type=int, default=10_000)
-    p.add_argument("--cpu-periods", type=int, default=60)
+    p.add_argument("--cpu-periods", type=int, default=120)
     p.add_argument("--transport", choices=["rccl", "host"], default="rccl", help="N>1 shard exchange")
     p.add_argument("--no-events", action="store_true", help="no per-kernel HIP events (roofline unavailable)")
     p.add_argument("--rehearse-one-gpu", action="store_true",
@@ -77,14 +77,9 @@ def workload_config(a, SimConfig, _abi, members, **kw):
     return SimConfig(n_members=members, **kw)
 
 
-def cpu_baseline(a, members, periods):
-    """Bounded CPU sample: the oracle on the same workload shape at `members` members, one thread."""
+def _oracle_rate(a, lib, members, periods, threads):
     from swimhip import SimConfig, SimulatedCluster, _abi
-    lib_path = ROOT / "oracle" / "liboracle_swimref.so"
-    if not lib_path.exists():
-        import subprocess
-        subprocess.check_call(["make", "-s", "-C", str(ROOT / "oracle")])
-    lib = _abi.load(lib_path)
+    os.environ["SWIMREF_THREADS"] = str(threads)  # read when the oracle handle is created
     c = SimulatedCluster(lib, workload_config(a, SimConfig, _abi, members))
     if a.loss:
         c.set_default_loss(a.loss)
@@ -93,13 +88,31 @@ def cpu_baseline(a, members, periods):
     c.run_periods(periods)
     dt = time.perf_counter() - t0
     c.close()
+    return members * periods / dt, dt
+
+
+def cpu_baseline(a, members, periods):
+    """Bounded CPU sample: the oracle on the same workload shape at `members` members, on all host cores (observer
+    ranges per worker thread, SWIMREF_THREADS) and, for reference, on one core."""
+    from swimhip import _abi
+    lib_path = ROOT / "oracle" / "liboracle_swimref.so"
+    if not lib_path.exists():
+        import subprocess
+        subprocess.check_call(["make", "-s", "-C", str(ROOT / "oracle")])
+    lib = _abi.load(lib_path)
+    cores = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count() or 1))
+    one, dt1 = _oracle_rate(a, lib, members, max(1, periods // 4), 1)
+    allc, dtn = _oracle_rate(a, lib, members, periods, cores)
+    os.environ.pop("SWIMREF_THREADS", None)
     note = {"c3": "per-member work grows ~linearly with N (SYNC payloads), so at 100k it is ~10x slower per "
                   "member·period",
             "c2": "per-member gossip load grows ~N (SYNC re-spread storm), so at 10k it is far slower per member·period",
             "c5": "per-member rumor load grows ~N at 1 % churn, so at full N it is slower per member·period"}[a.workload]
-    return {"value": members * periods / dt, "unit": "member·periods/s", "cores": 1, "kind": "port",
+    return {"value": allc, "unit": "member·periods/s", "cores": cores, "kind": "port",
+            "single_core_value": one,
             "sample": f"oracle/swimref.cpp, {members} members (same {a.workload.upper()} shape, reduced N), {periods} "
-                      f"periods after 1 warm-up period, {dt:.1f} s; {note}"}
+                      f"periods after 1 warm-up period on {cores} worker threads ({dtn:.1f} s), and {max(1, periods // 4)} "
+                      f"periods on one ({dt1:.1f} s); {note}"}
 
 
 def workload_name(a, n):
@@ -212,7 +225,7 @@ def main():
                                 "frac": B / dt / 1e9 / HBM_PEAK_GBPS, "traffic": None}
             line["kernel_time_share"] = {}
         if not a.no_cpu_baseline and world == 1:
-            cm, cp = {"c3": (a.cpu_members, a.cpu_periods), "c2": (600, 25), "c5": (2000, 12)}[a.workload]
+            cm, cp = {"c3": (a.cpu_members, a.cpu_periods), "c2": (600, 40), "c5": (2000, 24)}[a.workload]
             line["cpu_baseline"] = cpu_baseline(a, cm, cp)
         else:
             line["cpu_baseline"] = None

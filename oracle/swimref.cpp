@@ -17,6 +17,10 @@
 // is pinned by its closed forms. Event ordering and timing are pinned only by SEMANTICS.md, which makes parity for
 // them "spec-pinned", not reference-pinned.
 #include <algorithm>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -78,6 +82,66 @@ struct Msg {
 };
 
 struct Sim;
+
+// What one worker produces while it processes its range of members in a tick (SWIMREF_THREADS > 1 splits the members
+// into contiguous ranges; the lanes are merged in member order after the tick, so results do not depend on the split)
+struct Lane {
+  swim_counters ctr;
+  std::vector<Msg> out;
+  std::vector<swim_event> events;
+  std::vector<uint32_t> leaving;
+};
+thread_local Lane* tl_lane = nullptr;
+
+// a fixed pool of worker threads; the calling thread runs part 0
+struct Pool {
+  std::vector<std::thread> th;
+  std::mutex mu;
+  std::condition_variable cv, done;
+  std::function<void(int)> job;
+  uint64_t gen = 0;
+  int pending = 0;
+  bool stop = false;
+  void start(int n) {
+    for (int i = 1; i < n; ++i)
+      th.emplace_back([this, i] {
+        uint64_t seen = 0;
+        for (;;) {
+          std::function<void(int)> f;
+          {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return stop || gen != seen; });
+            if (stop) return;
+            seen = gen;
+            f = job;
+          }
+          f(i);
+          std::lock_guard<std::mutex> lk(mu);
+          if (--pending == 0) done.notify_one();
+        }
+      });
+  }
+  void run(const std::function<void(int)>& f) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      job = f;
+      pending = (int)th.size();
+      gen++;
+    }
+    cv.notify_all();
+    f(0);
+    std::unique_lock<std::mutex> lk(mu);
+    done.wait(lk, [&] { return pending == 0; });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto& t : th) t.join();
+  }
+};
 
 struct Member {
   Sim* sim = nullptr;
@@ -196,6 +260,9 @@ struct Sim {
   std::vector<swim_event> events;
   swim_counters ctr;
   std::string err;
+  int threads = 1;  // SWIMREF_THREADS
+  std::vector<Lane> lanes;
+  std::unique_ptr<Pool> pool;
 
   uint32_t suspicion_ticks(uint32_t size) const {  // ClusterMath.suspicionTimeout (ClusterMath.java:123-125)
     return cfg.suspicion_mult * bitlen(size) * ping_t;
@@ -254,16 +321,18 @@ void Member::shuffle(std::vector<uint32_t>& v, int stream) {
 void Member::send(Msg&& m, uint64_t k, bool gossip) {
   (void)gossip;
   Sim& s = *sim;
-  s.inflight[(k + s.lat) % (s.lat + 1)].push_back(std::move(m));
+  (void)s;
+  (void)k;
+  tl_lane->out.push_back(std::move(m));  // merged into inflight[(k + lat) % (lat + 1)] after the tick
 }
 
 // prepareSyncDataMsg (:446-454) + transport.send; returns false when the send failed
 bool Member::send_sync(uint8_t kind, uint32_t dst, uint32_t cid_iss, uint32_t cid_cnt, uint64_t k) {
   Sim& s = *sim;
   uint32_t seq = syncSeq++;
-  s.ctr.messages++;
+  tl_lane->ctr.messages++;
   if (s.lost(kind, id, dst, k, id, seq)) {
-    s.ctr.messages_lost++;
+    tl_lane->ctr.messages_lost++;
     return false;
   }
   Msg m;
@@ -288,10 +357,10 @@ void Member::emit_event(uint32_t type, uint32_t subj, uint32_t oldm, uint32_t ne
   uint32_t seq = evSeq++;
   evHash = hpair(evHash, ((uint64_t)k << 32) | ((uint64_t)type << 30) | subj);
   evHash = hpair(evHash, ((uint64_t)oldm << 32) | newm);
-  s.ctr.events++;
+  tl_lane->ctr.events++;
   if (s.cfg.flags & SWIM_FLAG_RECORD_EVENTS) {
     swim_event e{(uint32_t)k, id, seq, type, subj, oldm, newm, 0};
-    s.events.push_back(e);
+    tl_lane->events.push_back(e);
   }
   on_member_event(type, subj);
 }
@@ -324,7 +393,7 @@ void Member::spread(uint32_t subj, Rec rec, uint64_t payload) {
   g.payload = payload;
   g.infPeriod = gPeriod;
   gossips.emplace(gid, std::move(g));
-  sim->ctr.gossips_created++;
+  tl_lane->ctr.gossips_created++;
 }
 
 // MembershipProtocolImpl.updateMembership (:475-541)
@@ -335,7 +404,7 @@ void Member::update_membership(uint32_t subj, Rec r1, int reason, int group, uin
   if (subj == id) {                   // :488-509 local member: refute with a higher incarnation
     Rec r2{r0.st, std::max(r0.inc, r1.inc) + 1};
     table[id] = r2;
-    s.ctr.row_writes++;
+    tl_lane->ctr.row_writes++;
     spread(id, r2);
     return;
   }
@@ -346,7 +415,7 @@ void Member::update_membership(uint32_t subj, Rec r1, int reason, int group, uin
     if (r0.st == ABSENT) tsize++;
     table[subj] = r1;
   }
-  s.ctr.row_writes++;
+  tl_lane->ctr.row_writes++;
   if (r1.st == SUSPECT) {  // :519-523, scheduleSuspicionTimeoutTask (:597-606) computeIfAbsent
     if (!timers.count(subj)) timers[subj] = k + s.suspicion_ticks(tsize);
   } else {
@@ -405,9 +474,9 @@ void Member::complete_group(int g, uint64_t k) {
 void Member::fetch(uint32_t subj, Rec r1, int reason, bool added, int group, uint64_t k) {
   Sim& s = *sim;
   uint32_t cnt = cidCnt++;
-  s.ctr.messages++;
+  tl_lane->ctr.messages++;
   if (s.lost(K_GMD_REQ, id, subj, k, id, cnt)) {  // requestResponse send error -> sink.error
-    s.ctr.messages_lost++;
+    tl_lane->ctr.messages_lost++;
     if (group >= 0) groups[group].error = true;  // error propagates to whenDelayError
     do_finally(subj, r1, reason);
     return;
@@ -426,9 +495,8 @@ void Member::fetch(uint32_t subj, Rec r1, int reason, bool added, int group, uin
 
 // syncMembership (:456-467): eager filter of differing records, then sequential updateMembership
 void Member::sync_membership(const Payload& p, int reason, int group, uint64_t k) {
-  Sim& s = *sim;
-  s.ctr.record_compares += p.size();
-  s.ctr.sync_merges++;
+  tl_lane->ctr.record_compares += p.size();
+  tl_lane->ctr.sync_merges++;
   std::vector<std::pair<uint32_t, Rec>> diff;
   for (auto& e : p)
     if (e.second != table[e.first]) diff.push_back(e);
@@ -443,7 +511,7 @@ void Member::on_fd_event(uint32_t target, uint8_t status, uint64_t k) {
   if (status == ALIVE) {
     send_sync(K_SYNC, target, NONE, 0, k);
   } else {
-    sim->ctr.record_compares++;
+    tl_lane->ctr.record_compares++;
     update_membership(target, Rec{SUSPECT, r0.inc}, R_FD, -1, k);
   }
 }
@@ -473,9 +541,9 @@ void Member::ping_req_step(uint32_t target, uint32_t cnt, uint64_t k) {
     return;
   }
   for (uint32_t h : helpers) {
-    s.ctr.messages++;
+    tl_lane->ctr.messages++;
     if (s.lost(K_PING_REQ, id, h, k, id, cnt)) {
-      s.ctr.messages_lost++;
+      tl_lane->ctr.messages_lost++;
       on_fd_event(target, SUSPECT, k);
       continue;
     }
@@ -514,9 +582,9 @@ void Member::do_ping(uint64_t k) {
   }
   uint32_t target = ping[(size_t)pingIdx++];
   uint32_t cnt = cidCnt++;
-  s.ctr.messages++;
+  tl_lane->ctr.messages++;
   if (s.lost(K_PING, id, target, k, id, cnt)) {
-    s.ctr.messages_lost++;
+    tl_lane->ctr.messages_lost++;
     ping_req_step(target, cnt, k);
     return;
   }
@@ -557,7 +625,7 @@ void Member::do_spread_gossip(uint64_t k) {
       GState& g = kv.second;
       if (g.infPeriod + sp < period) continue;
       if (g.infected.count(t)) continue;
-      s.ctr.gossip_messages++;
+      tl_lane->ctr.gossip_messages++;
       const bool lost = s.lost_gossip(id, t, k, slot, kv.first);
       if (s.send_log) fprintf(s.send_log, "S %llu %u %llu %u %d\n", (unsigned long long)k, id, (unsigned long long)kv.first, t, lost ? 1 : 0);
       if (lost) continue;  // gossip losses are not counted (SEMANTICS.md §8)
@@ -579,7 +647,7 @@ void Member::do_spread_gossip(uint64_t k) {
       // the leave notification swept at its origin: leaveCluster's Mono completes and ClusterImpl.doShutdown
       // disposes the member and stops its transport (ClusterImpl.java:305-313, GossipProtocolImpl.java:296-306)
       if ((uint32_t)(it->first >> 32) == id && it->second.subj == id && it->second.rec.st == DEAD)
-        s.leaving_done.push_back(id);
+        tl_lane->leaving.push_back(id);
       if (s.send_log) fprintf(s.send_log, "W %llu %u %llu\n", (unsigned long long)k, id, (unsigned long long)it->first);
       it = gossips.erase(it);
     } else {
@@ -640,14 +708,14 @@ void Member::process(uint64_t k, std::vector<Msg>& inbox) {
   for (; pendingInc > 0; --pendingInc) {  // updateIncarnation (MembershipProtocolImpl.java:178-190), once per call
     Rec r{ALIVE, table[id].inc + 1};
     table[id] = r;
-    s.ctr.row_writes++;
+    tl_lane->ctr.row_writes++;
     spread(id, r);
   }
   if (pendingLeave) {  // leaveCluster (MembershipProtocolImpl.java:197-206): own record DEAD inc+1, spread
     pendingLeave = false;
     Rec r{DEAD, table[id].inc + 1};
     table[id] = r;
-    s.ctr.row_writes++;
+    tl_lane->ctr.row_writes++;
     spread(id, r);
   }
   std::vector<Msg*> syncm, fdm, mdm, gm;
@@ -688,9 +756,9 @@ void Member::process(uint64_t k, std::vector<Msg>& inbox) {
   for (Msg* m : fdm) {
     if (m->kind == K_PING) {  // onPing (:230-255)
       if (m->pd_to != id) continue;
-      s.ctr.messages++;
+      tl_lane->ctr.messages++;
       if (s.lost(K_PING_ACK, id, m->pd_from, k, m->cid_iss, m->cid_cnt)) {
-        s.ctr.messages_lost++;
+        tl_lane->ctr.messages_lost++;
         continue;
       }
       Msg a = *m;
@@ -699,9 +767,9 @@ void Member::process(uint64_t k, std::vector<Msg>& inbox) {
       a.dst = m->pd_from;
       send(std::move(a), k);
     } else if (m->kind == K_PING_REQ) {  // onPingReq (:258-284): transit ping
-      s.ctr.messages++;
+      tl_lane->ctr.messages++;
       if (s.lost(K_PING, id, m->pd_to, k, m->cid_iss, m->cid_cnt)) {
-        s.ctr.messages_lost++;
+        tl_lane->ctr.messages_lost++;
         continue;
       }
       Msg p;
@@ -715,9 +783,9 @@ void Member::process(uint64_t k, std::vector<Msg>& inbox) {
       p.pd_orig = m->pd_from;
       send(std::move(p), k);
     } else if (m->pd_orig != NONE) {  // onTransitPingAck (:290-315)
-      s.ctr.messages++;
+      tl_lane->ctr.messages++;
       if (s.lost(K_PING_ACK, id, m->pd_orig, k, m->cid_iss, m->cid_cnt)) {
-        s.ctr.messages_lost++;
+        tl_lane->ctr.messages_lost++;
         continue;
       }
       Msg a;
@@ -738,9 +806,9 @@ void Member::process(uint64_t k, std::vector<Msg>& inbox) {
   for (Msg* m : mdm) {
     if (m->kind == K_GMD_REQ) {
       if (m->md_subject != id) continue;
-      s.ctr.messages++;
+      tl_lane->ctr.messages++;
       if (s.lost(K_GMD_RESP, id, m->src, k, m->cid_iss, m->cid_cnt)) {
-        s.ctr.messages_lost++;
+        tl_lane->ctr.messages_lost++;
         continue;
       }
       Msg r;
@@ -783,7 +851,7 @@ void Member::process(uint64_t k, std::vector<Msg>& inbox) {
       if (m->g_subj == USER_SUBJ) {  // sink.next -> ClusterImpl.listenGossips (:213-216); membership filters it out
         emit_event(SWIM_EV_GOSSIP, (uint32_t)(m->gid >> 32), (uint32_t)m->g_payload, (uint32_t)(m->g_payload >> 32), k);
       } else {
-        s.ctr.record_compares++;
+        tl_lane->ctr.record_compares++;
         update_membership(m->g_subj, m->g_rec, R_GOSSIP, -1, k);  // onMembershipGossip (:401-408)
       }
     }
@@ -829,7 +897,7 @@ void Member::process(uint64_t k, std::vector<Msg>& inbox) {
       timers.erase(it);
       Rec r = table[subj];
       if (r.st != ABSENT) {
-        s.ctr.record_compares++;
+        tl_lane->ctr.record_compares++;
         update_membership(subj, Rec{DEAD, r.inc}, R_TIMEOUT, -1, k);
       }
     }
@@ -855,6 +923,15 @@ void Sim::run_tick() {
   arrived.swap(inflight[k % (lat + 1)]);
   std::vector<std::vector<Msg>> inbox(N);
   for (auto& m : arrived) inbox[m.dst].push_back(std::move(m));
+  const int T = threads;
+  if ((int)lanes.size() != T) lanes.assign(T, Lane{});
+  for (auto& l : lanes) {
+    std::memset(&l.ctr, 0, sizeof(l.ctr));
+    l.out.clear();
+    l.events.clear();
+    l.leaving.clear();
+  }
+  tl_lane = &lanes[0];
   for (auto& m : members)  // ClusterImpl.join0 -> start0: the initial members at tick 0, joined ones at their tick
     if (m.alive && m.startTick == k) m.start(k);
   if (cfg.mode == SWIM_MODE_RUMOR && cfg.churn_per_period && k % ping_t == 0) {
@@ -872,8 +949,30 @@ void Sim::run_tick() {
     for (uint32_t o = 0; o < N; ++o)
       if (!add[o].empty()) members[o].pendingUser.insert(members[o].pendingUser.begin(), add[o].begin(), add[o].end());
   }
-  for (uint32_t i = 0; i < N; ++i)
-    if (members[i].alive) members[i].process(k, inbox[i]);
+  auto work = [&](int part) {
+    tl_lane = &lanes[part];
+    const uint32_t lo = (uint32_t)((uint64_t)N * part / T), hi = (uint32_t)((uint64_t)N * (part + 1) / T);
+    for (uint32_t i = lo; i < hi; ++i)
+      if (members[i].alive) members[i].process(k, inbox[i]);
+  };
+  if (T > 1)
+    pool->run(work);
+  else
+    work(0);
+  auto& slot = inflight[(k + lat) % (lat + 1)];
+  for (auto& l : lanes) {  // member order: the lanes hold contiguous member ranges
+    for (auto& m : l.out) slot.push_back(std::move(m));
+    events.insert(events.end(), l.events.begin(), l.events.end());
+    leaving_done.insert(leaving_done.end(), l.leaving.begin(), l.leaving.end());
+    ctr.record_compares += l.ctr.record_compares;
+    ctr.row_writes += l.ctr.row_writes;
+    ctr.messages += l.ctr.messages;
+    ctr.gossip_messages += l.ctr.gossip_messages;
+    ctr.events += l.ctr.events;
+    ctr.messages_lost += l.ctr.messages_lost;
+    ctr.gossips_created += l.ctr.gossips_created;
+    ctr.sync_merges += l.ctr.sync_merges;
+  }
   for (uint32_t m : leaving_done) {  // as swim_kill between this tick and the next
     members[m].alive = false;
     members[m].gossips.clear();
@@ -933,7 +1032,13 @@ __attribute__((visibility("default"))) int swim_create(const swim_config* cfg, s
   if (c.mode > SWIM_MODE_RUMOR || (c.mode == SWIM_MODE_RUMOR && c.init_mode != SWIM_INIT_PRECONVERGED)) return SWIM_EINVAL;
   if (c.n_dormant > c.n_members || (c.n_dormant && c.init_mode != SWIM_INIT_COLD_JOIN)) return SWIM_EINVAL;
   auto* h = new swim_handle();
-  if (const char* lp = getenv("SWIMREF_SEND_LOG")) h->sim.send_log = fopen(lp, "w");
+  if (const char* th = getenv("SWIMREF_THREADS")) h->sim.threads = std::max(1, std::min(256, atoi(th)));
+  if (h->sim.threads > 1) {
+    h->sim.pool.reset(new Pool());
+    h->sim.pool->start(h->sim.threads);
+  } else if (const char* lp = getenv("SWIMREF_SEND_LOG")) {  // single-threaded only
+    h->sim.send_log = fopen(lp, "w");
+  }
   Sim& s = h->sim;
   s.cfg = c;
   s.N = c.n_members;

@@ -55,3 +55,16 @@ def test_sharded_engine_matches_golden(engine, name, world):
     g = ThreadShardGroup(engine, cfg, world)
     check(record(g, name), load(name), f"gfx950 x{world} shards")
     g.close()
+
+
+@pytest.mark.parametrize("name", ["c2_small", "c4_small", "c5_small"])
+def test_threaded_oracle_matches_golden(oracle, name, monkeypatch):
+    """The oracle with SWIMREF_THREADS=3 (member ranges per worker, lanes merged in member order) reproduces the
+    fixtures exactly; bench.py times the CPU baseline this way on all host cores."""
+    monkeypatch.setenv("SWIMREF_THREADS", "3")
+    cfg, _ = SCENARIOS[name]()
+    c = SimulatedCluster(oracle, cfg)
+    rec = record(c, name)
+    c.close()
+    gold = json.loads((GOLDEN / f"{name}.json").read_text())
+    assert rec["periods"] == gold["periods"]
