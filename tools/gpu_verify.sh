@@ -1,0 +1,10 @@
+# fresh-box check of the committed tree: smoke, the whole -m gpu suite, one short default bench line
+set -e
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/verify
+mkdir -p $O
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > $O/gpu_tests.log 2>&1
+timeout -k 10 400 python -u bench.py --steps 20 --warmup 2 --no-cpu-baseline > $O/bench.log 2>&1
+tail -3 $O/gpu_tests.log; grep metric $O/bench.log
