@@ -7,17 +7,18 @@ ClusterConfig (ping 1 s / 500 ms, ping-req 3, gossip 200 ms x fanout 3 x repeat 
 "step" = one FD period (pingInterval = 10 ticks of 100 ms) for every member. In this steady state every member pings
 one peer per period, and periodic SYNC / SYNC_ACK anti-entropy streams whole 100k-record payloads against whole
 receiver rows (N/30 syncs per period in each direction), so the dominant kernel is k_sync_diff. It is HBM-bound
-(16 B of algorithmic traffic per record compare) with no dense math, so no MFMA.
+(8 B of algorithmic traffic per record compare: the 4-B record keys of payload and receiver; SURVEY.md
+§8d priced it at 16 B for 8-B keys) with no dense math, so no MFMA.
 
-With N=1, all 100k members run on one MI355X (about 165 GB of HBM). With --gpus N under torch.distributed.run, the
-SAME 100k-member cluster is row-sharded: rank r owns observers [r N/W, (r+1) N/W) and its rows (about 165/W GB), the
+With N=1, all 100k members run on one MI355X (about 206 GB of HBM). With --gpus N under torch.distributed.run, the
+SAME 100k-member cluster is row-sharded: rank r owns observers [r N/W, (r+1) N/W) and its rows (about 206/W GB), the
 gossip plane is replicated, and every tick the shards exchange gossip records and SYNC payloads with RCCL send/recv
 groups over xGMI inside libswimhip (include/swimhip_shard.h). Total work is fixed as N grows, so
 scaling is "strong" and `value` is the whole cluster's member·periods/s. torch.distributed (gloo) only bootstraps:
 it broadcasts the RCCL unique id, runs the barriers and takes the max time over ranks.
 
 The JSON line also carries:
-  roofline      k_sync_diff algorithmic bytes (16 B x N per merged payload) / its HIP-event time, against 8 TB/s;
+  roofline      k_sync_diff algorithmic bytes (8 B x N per merged payload) / its HIP-event time, against 8 TB/s;
                 traffic = measured HBM bytes per launch from rocprofv3 PMC when available (profiles/), else null.
   cpu_baseline  the CPU oracle (oracle/swimref.cpp, a port) on a bounded sample: same workload shape at 10k members,
                 timed here on the host on all its cores (worker threads over observer ranges, at most 16) and on one.
@@ -59,7 +60,7 @@ def parse():
 
 def traffic_from_profiles(n_members):
     """HBM bytes per k_sync_diff launch from a committed rocprofv3 PMC summary for this member count, if present."""
-    f = ROOT / "profiles" / "pmc_sync_diff.json"
+    f = ROOT / "profiles" / "pmc_sync_diff_k32.json"  # measured with the 4-B key plane
     if not f.exists():
         return None
     try:
@@ -186,10 +187,10 @@ def main():
         merges = d["sync_merges"]
         diff_s = d["diff_ns"] * 1e-9
         launches = max(1, d["diff_launches"])
-        bytes_per_launch = 16.0 * n * merges / launches  # payload row + receiver row, 8 B each per subject
-        achieved = (16.0 * n * merges) / diff_s / 1e9 if diff_s > 0 else 0.0
-        # whole-step algorithmic bytes, SURVEY.md §8d: B = 16R + 8W + 32M + 0.375G + 24E
-        B = 16 * d["record_compares"] + 8 * d["row_writes"] + 32 * d["messages"] + 0.375 * d["gossip_messages"] + 24 * d["events"]
+        bytes_per_launch = 8.0 * n * merges / launches  # payload keys + receiver keys, 4 B each per subject
+        achieved = (8.0 * n * merges) / diff_s / 1e9 if diff_s > 0 else 0.0
+        # whole-step algorithmic bytes, SURVEY.md §8d with 4-B record keys: B = 8R + 8W + 32M + 0.375G + 24E
+        B = 8 * d["record_compares"] + 8 * d["row_writes"] + 32 * d["messages"] + 0.375 * d["gossip_messages"] + 24 * d["events"]
         line = {
             "metric": "member·periods/sec at 100k members (whole node); achieved HBM GB/s",
             "value": n * a.steps / dt,

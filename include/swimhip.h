@@ -33,7 +33,8 @@ extern "C" {
 #define SWIM_EINVAL -1    /* bad argument / config (e.g. pingTimeout >= pingInterval, ClusterConfig.java:413-415) */
 #define SWIM_ENOMEM -2    /* device or host allocation failed */
 #define SWIM_EDEVICE -3   /* HIP / RCCL failure, or no GPU present */
-#define SWIM_ECAPACITY -4 /* a fixed-capacity structure overflowed (gossip slots, pending fetches, arenas) */
+#define SWIM_ECAPACITY -4 /* a fixed-capacity structure overflowed (gossip slots, pending fetches, arenas), or an
+                           stored incarnation reached 2^30 (the device key plane holds inc << 2 | status) */
 #define SWIM_EUNSUPPORTED -5
 
 /* init_mode */
@@ -176,7 +177,8 @@ int swim_join(swim_handle* h, uint32_t member, const uint32_t* seeds, uint32_t n
 
 /* readback */
 int swim_current_tick(swim_handle* h, uint64_t* tick);
-/* row of one observer: keys[s] = inc | status<<32 | meta_present<<34 | timer_deadline<<35 (SEMANTICS.md §8) */
+/* row of one observer: keys[s] = inc | status<<32 | meta_present<<34 | timer_deadline<<35 (SEMANTICS.md §8); the
+ * device stores it as two u32 planes (key32 = inc << 2 | status, and the bits from 34 up), joined here */
 int swim_read_row(swim_handle* h, uint32_t observer, uint64_t* keys_out, size_t cap);
 /* per-observer hashes: out[6*m + {0:row, 1:fd list, 2:gossip list, 3:events, 4:gossips held, 5:counters}] */
 int swim_state_hash(swim_handle* h, uint64_t* out, size_t cap);

@@ -258,7 +258,7 @@ int build(swim_handle* h) {
   A(d.initFlags, N) A(d.initDeadline, N) A(d.initCidBase, N) A(d.initN, N) A(d.firstGossip, N) A(d.nsub, N)
   A(d.npath, N) A(d.nfetch, N) A(d.pingIdx, N) A(d.remoteIdx, N) A(d.sel, N * 8) A(d.evHash, N)
   const uint64_t NL = d.NL;  // per-observer arrays: this shard's rows only
-  A(d.row, NL * d.NS) A(d.fdl, NL * d.LCAP) A(d.gl, NL * d.LCAP)
+  A(d.rowk, NL * d.NS) A(d.rowa, NL * d.NS) A(d.fdl, NL * d.LCAP) A(d.gl, NL * d.LCAP)
   A(d.subs, NL * SUBCAP * 4) A(d.paths, NL * PATHCAP * 5) A(d.fetch, NL * d.FCAP * FREC) A(d.groups, NL * d.GRCAP * GREC)
   A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.slow, d.SLOWCAP) A(d.slow_n, 1) A(d.rp, d.RPCAP) A(d.rp_n, 1) A(d.rlist, N) A(d.rn, 1) A(d.start_tick, N) A(d.jseed_n, N) A(d.jseeds, 16 * N) A(d.md_uidx, N) A(d.md_ver, NL * MDU) A(d.churn_q, 2ull * d.churn) A(d.cin, N * d.F) A(d.swthr, N) A(d.HB, (uint64_t)(d.SLOTS / 64 + 1) * N) A(d.WB, (uint64_t)(d.SLOTS / 64 + 1) * N) A(d.cev, N * d.F * CEVW)
   A(d.log_tick, N * d.LOGW) A(d.log_spread, N * d.LOGW) A(d.log_cnt, N * d.LOGW) A(d.log_tg, N * d.LOGW * d.F)
@@ -287,7 +287,7 @@ int build(swim_handle* h) {
     d.CHCAP = h->spec.chunk_cap ? h->spec.chunk_cap : (uint32_t)std::min<uint64_t>(4096, (uint64_t)d.MSGCAP * d.NCHUNK);
     uint64_t se = sizeof(SyncMsg) + 8 + 8ull * d.MW;
     d.XA_PEER = ((32 + 4ull * NSW * d.NSCAP + 4ull * RRW * d.RRCAP + se * d.RQCAP + 511) & ~255ull) +
-                (uint64_t)d.CHCAP * CH * 8;
+                (uint64_t)d.CHCAP * CH * 4;
     d.XB_PEER = 16 + 8ull * std::min<uint64_t>((uint64_t)d.DCAP + d.SWCAP, 1ull << 25);
     A(d.base_row, d.NS) A(d.xn, 8) A(d.ns_rec, (uint64_t)d.NSCAP * NSW) A(d.rr_rec, (uint64_t)d.RRCAP * RRW)
     A(d.sw_rec, d.SWCAP) A(d.rq_n, d.W) A(d.rq_list, (uint64_t)d.W * d.RQCAP)
@@ -299,6 +299,9 @@ int build(swim_handle* h) {
     HIPCK(hipMemsetAsync(d.xb_rcnt, 0, 8ull * d.W, h->stream));
     HIPCK(hipHostMalloc((void**)&h->hcnt, 16ull * d.W, hipHostMallocDefault));
     A(d.xi_send, (uint64_t)d.W * XINL) A(d.xi_recv, (uint64_t)d.W * XINL)
+    A(d.xdone, d.W)
+    HIPCK(hipMemsetAsync(d.xdone, 0, 4ull * d.W, h->stream));
+    d.inl = h->spec.transport == SWIM_TRANSPORT_RCCL ? 1u : 0u;
     HIPCK(hipHostMalloc((void**)&h->xi_host_h, 16ull * d.W, hipHostMallocMapped | hipHostMallocCoherent));
     HIPCK(hipHostGetDevicePointer((void**)&d.xi_host, (void*)h->xi_host_h, 0));
     if (h->spec.transport == SWIM_TRANSPORT_HOST) {
@@ -354,10 +357,19 @@ int build(swim_handle* h) {
   return check_err(h);
 }
 
+// The host waits for the end of every tick's exchange A. A blocking event wait falls back to an interrupt after a
+// short active phase, and that wake-up would stall the GPU, which has nothing queued behind the exchange: spin.
+hipError_t spin_wait(hipEvent_t ev) {
+  hipError_t e;
+  while ((e = hipEventQuery(ev)) == hipErrorNotReady) {
+  }
+  return e;
+}
+
 // one all-to-all of per-peer byte blocks (fixed-capacity regions of `cap` bytes in send / recv, rank order).
 // The byte counts are device-resident (written by the pack kernels); the transport needs them on the host.
 int exchange(swim_handle* h, uint8_t* send, uint8_t* recv, uint64_t cap, unsigned long long* scnt,
-             unsigned long long* rcnt) {
+             unsigned long long* rcnt, bool inline_packed) {
   const uint32_t W = h->d.W, me = h->d.rank;
   hipStream_t st = h->stream;
   unsigned long long* hc = h->hcnt;
@@ -365,14 +377,14 @@ int exchange(swim_handle* h, uint8_t* send, uint8_t* recv, uint64_t cap, unsigne
   if (h->spec.transport == SWIM_TRANSPORT_RCCL) {
     // one fixed-size all-to-all (count word + the first XINL - 8 bytes of each region), one host read of the
     // count words through mapped memory, and a send/recv group only for regions that did not fit
-    launch_inline_out(h->d, send, cap, scnt, st);
+    if (!inline_packed) launch_inline_out(h->d, send, cap, scnt, st);  // exchange A: k_pack_a_chunks wrote them
     if (ncclAllToAll(h->d.xi_send, h->d.xi_recv, XINL, ncclUint8, h->comm, st) != ncclSuccess) {
       h->err = "ncclAllToAll (inline exchange) failed";
       return SWIM_EDEVICE;
     }
     launch_inline_in(h->d, recv, cap, scnt, rcnt, st);
     HIPCK(hipEventRecord(h->ev_member, st));
-    HIPCK(hipEventSynchronize(h->ev_member));
+    HIPCK(spin_wait(h->ev_member));
     volatile unsigned long long* xh = h->d.xi_host;
     for (uint32_t q = 0; q < 2 * W; ++q) hc[q] = xh[q];
     h->xflag = false;
@@ -609,10 +621,10 @@ int swim_step(swim_handle* h, uint32_t n) {
     } else {
       int xr;
       launch_tick_a(d, k, h->stream, te);
-      if ((xr = exchange(h, d.xa_send, d.xa_recv, d.XA_PEER, d.xa_scnt, d.xa_rcnt)) != SWIM_OK) return xr;
+      if ((xr = exchange(h, d.xa_send, d.xa_recv, d.XA_PEER, d.xa_scnt, d.xa_rcnt, true)) != SWIM_OK) return xr;
       const bool gossip = h->xflag;
       launch_tick_b(d, k, h->stream, te, gossip);
-      if (gossip && (xr = exchange(h, d.xb_send, d.xb_recv, d.XB_PEER, d.xb_scnt, d.xb_rcnt)) != SWIM_OK) return xr;
+      if (gossip && (xr = exchange(h, d.xb_send, d.xb_recv, d.XB_PEER, d.xb_scnt, d.xb_rcnt, false)) != SWIM_OK) return xr;
       launch_tick_c(d, k, h->stream, gossip);
     }
     h->tick++;
@@ -798,9 +810,10 @@ int swim_current_tick(swim_handle* h, uint64_t* t) {
 int swim_read_row(swim_handle* h, uint32_t obs, uint64_t* out, size_t cap) {
   if (!h || obs >= h->d.N || cap < h->d.N || !owns(h, obs)) return SWIM_EINVAL;
   HIPCK(hipStreamSynchronize(h->stream));
-  HIPCK(hipMemcpy(out, h->d.row + lidx(h->d, obs) * h->d.NS, 8ull * h->d.N, hipMemcpyDeviceToHost));
-  for (uint32_t s = 0; s < h->d.N; ++s)
-    if (rec_status(out[s]) == ST_ABSENT) out[s] = 0;
+  std::vector<uint32_t> k(h->d.N), a(h->d.N);  // the two planes, joined into logical records (swim_common.h)
+  HIPCK(hipMemcpy(k.data(), h->d.rowk + lidx(h->d, obs) * h->d.NS, 4ull * h->d.N, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(a.data(), h->d.rowa + lidx(h->d, obs) * h->d.NS, 4ull * h->d.N, hipMemcpyDeviceToHost));
+  for (uint32_t s = 0; s < h->d.N; ++s) out[s] = (k[s] & 3u) == ST_ABSENT ? 0 : rec_join(k[s], a[s]);
   return SWIM_OK;
 }
 

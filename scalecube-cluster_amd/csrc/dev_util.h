@@ -10,7 +10,7 @@ __device__ __forceinline__ void set_err(const Dev& d, uint32_t bit) { atomicOr(d
 
 // 16-B row loads
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ u64x2 ld_c(const uint64_t* p) { return *(const u64x2*)p; }
+__device__ __forceinline__ uint4 ld_c4(const uint32_t* p) { return *(const uint4*)p; }
 
 // settings epoch in force at tick k (the latest epoch that started at or before k)
 __device__ __forceinline__ int epoch_at(const Dev& d, uint32_t k) {
@@ -132,5 +132,27 @@ __device__ __forceinline__ void on_sweep(const Dev& d, uint32_t g, uint32_t m, u
 __device__ __forceinline__ uint32_t s_ctick(uint32_t e) { return (e & S_TICK_MASK) - 1u; }
 __device__ __forceinline__ bool s_ever(uint32_t e) { return (e & S_TICK_MASK) != 0; }
 __device__ __forceinline__ bool s_held(uint32_t e) { return (e & S_TICK_MASK) != 0 && !(e & S_SWEPT); }
+
+// end of a sharded tick (W > 1): the same resets, plus the exchange counters (one block)
+__device__ __forceinline__ void tick_end(const Dev& d, uint32_t k) {
+  uint32_t t = threadIdx.x;
+  if (t < 8) d.xn[t] = 0;
+  if (t < d.W) {
+    d.rq_n[t] = 0;
+    d.xa_scnt[t] = 0;
+    d.xb_scnt[t] = 0;
+    d.xdone[t] = 0;
+  }
+  if (t == 0) {
+    uint32_t nb = (k + 1) & 1;
+    d.nmsg[nb] = 0;
+    d.arena_used[nb] = 0;
+    *d.pool_used = 0;
+    *d.nactive = 0;
+    *d.deliv_n = 0;
+    *d.rc_n = 0;
+    d.deaths_n[(k + 1) & 1] = 0;
+  }
+}
 
 }  // namespace swim

@@ -1,7 +1,8 @@
 // engine.h — device-resident state of libswimhip and the per-tick kernel pipeline.
 //
 // Layout in HBM, one GPU, N members (all arrays are SoA; "per member" = indexed by observer id):
-//   row        u64[N][N]          membership table + metadata bit + suspicion deadline (swim_common.h)
+//   rowk, rowa u32[N][NS] x 2      membership table: key plane (inc << 2 | status) and aux plane (metadata bit,
+//                                  suspicion deadline), swim_common.h
 //   fdl, gl    u32[N][LCAP]       FailureDetectorImpl.pingMembers / GossipProtocolImpl.remoteMembers
 //   S          u32[SLOTS][N]      gossip slot x holder: creation tick | PENDING | SWEPT | REBORN
 //   logs       per member ring of the last LOGW gossip rounds: (tick, spread, targets[F])
@@ -28,7 +29,8 @@ constexpr uint32_t S_TICK_MASK = (1u << 29) - 1u;
 constexpr uint32_t E_SLOTS = 1, E_FETCH = 2, E_SUBS = 4, E_PATHS = 8, E_GROUPS = 16, E_MSGS = 32, E_ARENA = 64,
                    E_POOL = 128, E_LIST = 256, E_DELIV = 512, E_RECEIPTS = 1024, E_CONTACTS = 2048,
                    E_REBORN = 4096, E_LOGWIN = 8192, E_EPOCH = 16384, E_EVENTS = 32768, E_SORTCAP = 65536,
-                   E_XCAP = 1u << 17, E_LINKHIST = 1u << 18, E_DEATHS = 1u << 19;
+                   E_XCAP = 1u << 17, E_LINKHIST = 1u << 18, E_DEATHS = 1u << 19,
+                   E_INC = 1u << 20;  // an incarnation >= 2^30 would not fit the key plane (swim_common.h)
 // per-link NetworkEmulator settings (setLinkSettings / block / unblock): hash of (src, dst) -> change history
 constexpr uint32_t LKCAP = 4096, LKH = 8;  // keys, history entries per key
 constexpr uint32_t DEATHCAP = 4096;        // completed leaves per tick
@@ -92,7 +94,8 @@ struct Dev {
   uint32_t* sel;  // [N][8]
   uint64_t* evHash;
 
-  uint64_t* row;  // [N][NS]: row stride NS = N rounded up to 8 (64-B aligned rows for 16-B loads)
+  uint32_t* rowk;  // [N][NS] key plane: row stride NS = N rounded up to 8 (32-B aligned rows for 16-B loads)
+  uint32_t* rowa;  // [N][NS] aux plane
   uint32_t *fdl, *gl;  // [N][LCAP]
 
   uint32_t* subs;    // [N][SUBCAP][4]  cnt, kind, target, deadline
@@ -143,7 +146,7 @@ struct Dev {
   // ---- SYNC messages (double-buffered by tick parity) ----
   SyncMsg* msgs[2];
   uint32_t* nmsg;  // [2]
-  uint64_t* arena[2];
+  uint32_t* arena[2];  // [ARENA_ROWS][NS] key-plane snapshots (a payload carries keys only)
   uint32_t* arena_used;  // [2]
   uint32_t* m_next; // [2][MSGCAP] next message of msgs[b] to the same destination
   uint32_t* m_head; // [2][N] first message of msgs[b] to each destination, NEVER if none (reset by the consumer)
@@ -174,7 +177,7 @@ struct Dev {
   uint32_t W, rank, lo, hi, NL, SPR, MW;  // SPR: gossip slots owned per shard; MW: u64 words per chunk mask
   uint32_t NSCAP, RRCAP, SWCAP, RQCAP, RXCAP, CHCAP;
   uint64_t XA_PEER, XB_PEER;  // bytes per peer region of the two exchange buffers
-  uint64_t* base_row;  // [NS] baseline record keys: a remote SYNC payload ships only its chunks that differ
+  uint32_t* base_row;  // [NS] baseline key plane: a remote SYNC payload ships only its chunks that differ
   uint32_t* xn;        // [8] 0 new slots, 1 round records, 2 sweeps, 4 inbound msgs (mtmp), 5 rx payloads
   uint32_t* ns_rec;    // [NSCAP][NSW] gossips created on this shard this tick
   uint32_t* rr_rec;    // [RRCAP][RRW] gossip rounds of this shard's members this tick
@@ -191,6 +194,8 @@ struct Dev {
   unsigned long long *xa_scnt, *xa_rcnt, *xb_scnt, *xb_rcnt;  // [W] bytes per peer region
   uint8_t *xi_send, *xi_recv;    // [W][XINL] inline all-to-all blocks
   unsigned long long* xi_host;   // host-mapped [2W]: send and receive count words of the last exchange
+  uint32_t* xdone;  // [W] finished k_pack_a_chunks blocks per peer column (the last one writes the inline block)
+  uint32_t inl;     // RCCL transport: exchange A's inline blocks are written by k_pack_a_chunks
 };
 
 // local index of an observer owned by this shard

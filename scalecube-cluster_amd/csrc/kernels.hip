@@ -12,8 +12,7 @@ __global__ void k_sync_route(Dev d, uint32_t b);
 __global__ void k_sync_dirty(Dev d, uint32_t b);
 __global__ void k_pack_a(Dev d, uint32_t b);
 __global__ void k_pack_a_chunks(Dev d, uint32_t b);
-__global__ void k_unpack_a(Dev d, uint32_t k);
-__global__ void k_msgs_commit(Dev d, uint32_t b);
+__global__ void k_unpack_a(Dev d, uint32_t k, uint32_t end);
 __global__ void k_pack_b(Dev d);
 __global__ void k_unpack_b_sweeps(Dev d, uint32_t k);
 __global__ void k_unpack_b_deliv(Dev d);
@@ -67,14 +66,18 @@ __global__ void k_init_members(Dev d) {
   for (uint32_t e = 0; e < d.LOGW; ++e) d.log_tick[(size_t)m * d.LOGW + e] = NEVER;
 }
 
-// one block per observer row (grid-strided): rows are written with coalesced 8-B stores
+// one block per observer row (grid-strided): both planes are written with coalesced 4-B stores
 __global__ void k_init_rows(Dev d) {
-  uint64_t full = rec_key(ST_ALIVE, 0) | META_BIT;
+  const uint64_t full = rec_key(ST_ALIVE, 0) | META_BIT;
   for (uint32_t li = blockIdx.x; li < d.NL; li += gridDim.x) {
     uint32_t m = d.lo + li;
-    uint64_t* row = d.row + (size_t)li * d.NS;
-    for (uint32_t s = threadIdx.x; s < d.NS; s += blockDim.x)
-      row[s] = s >= d.N ? 0ull : (d.init_mode == 1 || m == s) ? full : 0ull;
+    uint32_t* rk = d.rowk + (size_t)li * d.NS;
+    uint32_t* ra = d.rowa + (size_t)li * d.NS;
+    for (uint32_t s = threadIdx.x; s < d.NS; s += blockDim.x) {
+      const uint64_t v = s >= d.N ? 0ull : (d.init_mode == 1 || m == s) ? full : 0ull;
+      rk[s] = key32(v);
+      ra[s] = aux32(v);
+    }
   }
 }
 
@@ -107,7 +110,7 @@ __global__ void k_init_slots(Dev d) {
 // the SYNC baseline row (record keys): what a PRECONVERGED row starts as, an empty row for a cold join
 __global__ void k_init_base(Dev d) {
   uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s < d.NS) d.base_row[s] = (s < d.N && d.init_mode == 1) ? rec_key(ST_ALIVE, 0) : 0ull;
+  if (s < d.NS) d.base_row[s] = (s < d.N && d.init_mode == 1) ? key32(rec_key(ST_ALIVE, 0)) : 0u;
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -281,11 +284,12 @@ __global__ void __launch_bounds__(256) k_seg_sort(uint64_t* key, uint32_t* val, 
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// k_sync_diff: for every SYNC / SYNC_ACK sent in tick k-1, stream the payload row (the sender's live row, or its
-// copy-on-write snapshot) against the receiver's row and extract, per 2048-subject chunk and in subject order,
-// the records that differ (the eager `!r1.equals(table.get(id))` filter of syncMembership, :456-467).
-// This is the HBM-bound hot loop: 2 x 8 B read per subject per merge. SHARDED adds payloads received from other
-// shards (baseline row + shipped chunks); the single-GPU instance has only local rows and snapshots.
+// k_sync_diff: for every SYNC / SYNC_ACK sent in tick k-1, stream the payload's key plane (the sender's live row,
+// or its copy-on-write snapshot) against the receiver's key plane and extract, per 2048-subject chunk and in
+// subject order, the records that differ (the eager `!r1.equals(table.get(id))` filter of syncMembership,
+// :456-467). This is the HBM-bound hot loop: 2 x 4 B read per subject per merge (key32, swim_common.h). SHARDED adds
+// payloads received from other shards (baseline row + shipped chunks); the single-GPU instance has only local rows
+// and snapshots.
 template <bool SHARDED>
 __global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b) {
   __shared__ uint32_t scan[256];
@@ -296,51 +300,39 @@ __global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b) {
     uint32_t mi = w / d.NCHUNK, c = w % d.NCHUNK;
     const SyncMsg& mm = d.msgs[b][mi];
     const uint32_t s0 = c * CH + threadIdx.x * 8;
-    // this lane's 8 payload records: the sender's live row or its copy-on-write snapshot; for a payload
-    // received from another shard, the shipped chunk if it differs from the baseline, else the baseline
-    const uint64_t* p8;
+    // this lane's 8 payload keys: the sender's live row or its copy-on-write snapshot; for a payload received
+    // from another shard, the shipped chunk if it differs from the baseline, else the baseline
+    const uint32_t* p8;
     if (mm.payload == NEVER) {
-      p8 = d.row + lidx(d, mm.src) * d.NS + s0;
+      p8 = d.rowk + lidx(d, mm.src) * d.NS + s0;
     } else if (SHARDED && (mm.payload & PAY_RX)) {
       const uint32_t ri = mm.payload & ~PAY_RX;
       const uint64_t* mk = d.rx_mask + (size_t)ri * d.MW;
       if ((mk[c >> 6] >> (c & 63)) & 1ull) {
         uint32_t rank = __popcll(mk[c >> 6] & ((1ull << (c & 63)) - 1ull));
         for (uint32_t q = 0; q < (c >> 6); ++q) rank += __popcll(mk[q]);
-        p8 = (const uint64_t*)(d.xa_recv + d.rx_off[ri]) + (size_t)rank * CH + threadIdx.x * 8;
+        p8 = (const uint32_t*)(d.xa_recv + d.rx_off[ri]) + (size_t)rank * CH + threadIdx.x * 8;
       } else {
         p8 = d.base_row + s0;
       }
     } else {
       p8 = d.arena[b] + (size_t)mm.payload * d.NS + s0;
     }
-    const uint64_t* rcv = d.row + lidx(d, mm.dst) * d.NS;
-    uint64_t p[8], r[8];
-    if (s0 < d.NS) {  // NS is a multiple of 8: the 64-B group is in bounds, padding entries are 0 (absent)
+    const uint32_t* rcv = d.rowk + lidx(d, mm.dst) * d.NS;
+    uint32_t p[8], r[8];
+    if (s0 < d.NS) {  // NS is a multiple of 8: the 32-B group is in bounds, padding entries are 0 (absent)
       // (non-temporal loads measured 1.5x slower here on gfx950)
-      u64x2 a[4], q[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        a[j] = ld_c(p8 + 2 * j);
-        q[j] = ld_c(rcv + s0 + 2 * j);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        p[2 * j] = a[j].x;
-        p[2 * j + 1] = a[j].y;
-        r[2 * j] = q[j].x;
-        r[2 * j + 1] = q[j].y;
-      }
+      const uint4 a0 = ld_c4(p8), a1 = ld_c4(p8 + 4), q0 = ld_c4(rcv + s0), q1 = ld_c4(rcv + s0 + 4);
+      p[0] = a0.x, p[1] = a0.y, p[2] = a0.z, p[3] = a0.w, p[4] = a1.x, p[5] = a1.y, p[6] = a1.z, p[7] = a1.w;
+      r[0] = q0.x, r[1] = q0.y, r[2] = q0.z, r[3] = q0.w, r[4] = q1.x, r[5] = q1.y, r[6] = q1.z, r[7] = q1.w;
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) p[j] = r[j] = 0;
     }
     uint32_t mask = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      uint64_t r1 = p[j] & KEY_MASK;
-      if (rec_status(r1) != ST_ABSENT && r1 != (r[j] & KEY_MASK)) mask |= 1u << j;
-    }
+    for (int j = 0; j < 8; ++j)
+      if ((p[j] & 3u) != ST_ABSENT && p[j] != r[j]) mask |= 1u << j;
     uint32_t nc = __popc(mask);
     if (!__syncthreads_or(nc)) {  // steady state: the whole 2048-subject item matches
       if (threadIdx.x == 0) {
@@ -378,7 +370,7 @@ __global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b) {
     if (o + nc <= d.POOLCAP)
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        if (mask & (1u << j)) d.pool[o++] = ((uint64_t)(s0 + j) << 34) | (p[j] & KEY_MASK);
+        if (mask & (1u << j)) d.pool[o++] = ((uint64_t)(s0 + j) << 34) | key34(p[j]);
     __syncthreads();
   }
 }
@@ -936,10 +928,11 @@ __global__ void __launch_bounds__(256) k_hash(Dev d, uint64_t* out, uint32_t now
   uint32_t m = d.lo + blockIdx.x;
   if (m >= d.hi) return;
   unsigned long long hr = 0, hf = 0, hg = 0, hgs = 0;
-  const uint64_t* row = d.row + lidx(d, m) * d.NS;
+  const uint32_t* rk = d.rowk + lidx(d, m) * d.NS;
+  const uint32_t* ra = d.rowa + lidx(d, m) * d.NS;
   for (uint32_t s = threadIdx.x; s < d.N; s += blockDim.x) {
-    uint64_t v = row[s];
-    if (rec_status(v) != ST_ABSENT) hr += hpair(s, v);
+    const uint32_t k = rk[s];
+    if ((k & 3u) != ST_ABSENT) hr += hpair(s, rec_join(k, ra[s]));
   }
   uint32_t fl = d.fdLen[m], gl = d.gLen[m];
   for (uint32_t p = threadIdx.x; p < fl; p += blockDim.x) hf += hpair((uint64_t)p | (1ull << 40), d.fdl[lidx(d, m) * d.LCAP + p]);
@@ -991,26 +984,7 @@ __global__ void k_tick_flag(Dev d, uint32_t k) {
   __threadfence_system();
 }
 
-// end of a sharded tick (W > 1): the same resets, plus the exchange counters
-__global__ void k_tick_end(Dev d, uint32_t k) {
-  uint32_t t = threadIdx.x;
-  if (t < 8) d.xn[t] = 0;
-  if (t < d.W) {
-    d.rq_n[t] = 0;
-    d.xa_scnt[t] = 0;
-    d.xb_scnt[t] = 0;
-  }
-  if (t == 0) {
-    uint32_t nb = (k + 1) & 1;
-    d.nmsg[nb] = 0;
-    d.arena_used[nb] = 0;
-    *d.pool_used = 0;
-    *d.nactive = 0;
-    *d.deliv_n = 0;
-    *d.rc_n = 0;
-    d.deaths_n[(k + 1) & 1] = 0;
-  }
-}
+__global__ void k_tick_end(Dev d, uint32_t k) { tick_end(d, k); }
 
 // ------------------------------------------------------------------------------------------------------------
 // host launchers
@@ -1096,14 +1070,12 @@ void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   hipLaunchKernelGGL(k_sync_route, dim3(cdiv(d.MSGCAP, 256)), dim3(256), 0, st, d, b);
   hipLaunchKernelGGL(k_sync_dirty, dim3(512, d.W), dim3(256), 0, st, d, b);
   hipLaunchKernelGGL(k_pack_a, dim3(d.W), dim3(256), 0, st, d, b);
-  hipLaunchKernelGGL(k_pack_a_chunks, dim3(512, d.W), dim3(256), 0, st, d, b);
+  hipLaunchKernelGGL(k_pack_a_chunks, dim3(64, d.W), dim3(256), 0, st, d, b);
 }
 
 void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool gossip) {
   hipStream_t st = (hipStream_t)stream;
-  uint32_t b = k & 1;
-  hipLaunchKernelGGL(k_unpack_a, dim3(64, d.W), dim3(256), 0, st, d, k);
-  hipLaunchKernelGGL(k_msgs_commit, dim3(64), dim3(256), 0, st, d, b);
+  hipLaunchKernelGGL(k_unpack_a, dim3(32, d.W), dim3(256), 0, st, d, k, gossip ? 0u : 1u);
   if (!gossip) {  // no gossip slot in use on any shard: nothing to send, deliver or recycle; no exchange B
     if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[4], st);
     if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[5], st);
@@ -1123,10 +1095,7 @@ void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
 
 void launch_tick_c(const Dev& d, uint32_t k, void* stream, bool gossip) {
   hipStream_t st = (hipStream_t)stream;
-  if (!gossip) {
-    hipLaunchKernelGGL(k_tick_end, dim3(1), dim3(64), 0, st, d, k);
-    return;
-  }
+  if (!gossip) return;  // k_unpack_a closed the tick
   hipLaunchKernelGGL(k_unpack_b_sweeps, dim3(64, d.W), dim3(256), 0, st, d, k);
   hipLaunchKernelGGL(k_unpack_b_deliv, dim3(64, d.W), dim3(256), 0, st, d);
   hipLaunchKernelGGL(k_gossip_apply, dim3(1024), dim3(256), 0, st, d, k);

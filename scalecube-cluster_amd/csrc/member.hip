@@ -24,7 +24,7 @@ struct ML {
   int32_t pingIdx, remoteIdx;
   uint32_t sel[8];
   uint64_t evHash;
-  uint64_t* row;
+  uint32_t *rk, *ra;  // this observer's row: key plane and aux plane (swim_common.h)
   uint32_t *fdl, *gl, *subs, *paths, *fetch, *groups;
   unsigned long long c[8];
   uint32_t pend;  // this tick's SYNC messages that carry the live row: a chain through SyncMsg.pad (NEVER = none)
@@ -56,16 +56,21 @@ __device__ __forceinline__ void cow(ML& L) {
     L.pend = NEVER;
     return;
   }
-  uint64_t* dst = d.arena[b] + (size_t)r * d.NS;
-  for (uint32_t s = 0; s < d.NS; ++s) dst[s] = L.row[s];  // with the zero padding k_sync_diff reads up to NS
+  uint32_t* dst = d.arena[b] + (size_t)r * d.NS;
+  for (uint32_t s = 0; s < d.NS; ++s) dst[s] = L.rk[s];  // keys only, with the zero padding k_sync_diff reads up to NS
   for (uint32_t i = L.pend; i != NEVER; i = d.msgs[b][i].pad) d.msgs[b][i].payload = r;
   L.pend = NEVER;
 }
 
+__device__ __forceinline__ uint64_t row_ld(const ML& L, uint32_t s) { return rec_join(L.rk[s], L.ra[s]); }
+__device__ __forceinline__ uint32_t row_status(const ML& L, uint32_t s) { return L.rk[s] & 3u; }
+
 __device__ __forceinline__ void row_put(ML& L, uint32_t s, uint64_t v) {
-  uint64_t old = L.row[s];
-  if (L.pend != NEVER && ((old ^ v) & KEY_MASK)) cow(L);
-  L.row[s] = v;
+  const uint32_t k = key32(v);
+  if (rec_inc(v) >= INC_LIMIT) set_err(*L.d, E_INC);
+  if (L.pend != NEVER && L.rk[s] != k) cow(L);
+  L.rk[s] = k;
+  L.ra[s] = aux32(v);
 }
 
 // prepareSyncDataMsg (MembershipProtocolImpl.java:446-454) + transport.send; false if the send failed
@@ -320,7 +325,7 @@ __device__ __forceinline__ void fetch_md(ML& L, uint32_t subj, uint32_t st, uint
 // MembershipProtocolImpl.updateMembership (:475-541) + emitMembershipEvent (:543-588)
 __device__ __forceinline__ void update_membership(ML& L, uint32_t subj, uint32_t s1, uint32_t i1, uint32_t reason, int g) {
   const Dev& d = *L.d;
-  uint64_t v0 = L.row[subj];
+  uint64_t v0 = row_ld(L, subj);
   uint32_t s0 = rec_status(v0), i0 = rec_inc(v0);
   if (!overrides(s1, i1, s0, i0)) return;
   if (subj == L.m) {  // :488-509 refute with max(inc)+1, keep r0's status, spread, no event
@@ -369,7 +374,7 @@ __device__ __forceinline__ void update_membership(ML& L, uint32_t subj, uint32_t
 
 // onFailureDetectorEvent (:370-398)
 __device__ __forceinline__ void on_fd_event(ML& L, uint32_t target, uint32_t status) {
-  uint64_t v0 = L.row[target];
+  uint64_t v0 = row_ld(L, target);
   uint32_t s0 = rec_status(v0);
   if (s0 == ST_ABSENT || s0 == status) return;
   if (status == ST_ALIVE) {
@@ -561,7 +566,7 @@ __device__ __forceinline__ void do_sync(ML& L) {
   const uint32_t* sd = member_seeds(d, L.m, &nsd);
   for (uint32_t i = 0; i < nsd; ++i) {
     uint32_t s = sd[i];
-    if (s != L.m && rec_status(L.row[s]) == ST_ABSENT) extra++;
+    if (s != L.m && row_status(L, s) == ST_ABSENT) extra++;
   }
   uint32_t count = (L.tsize - 1u) + extra;
   if (count == 0) return;
@@ -572,7 +577,7 @@ __device__ __forceinline__ void do_sync(ML& L) {
   } else {
     target = NONE32;
     for (uint32_t s = 0; s < L.N; ++s) {
-      bool in = (s != L.m && rec_status(L.row[s]) != ST_ABSENT) || is_seed(d, L.m, s);
+      bool in = (s != L.m && row_status(L, s) != ST_ABSENT) || is_seed(d, L.m, s);
       if (!in) continue;
       if (i == 0) {
         target = s;
@@ -598,7 +603,7 @@ __device__ __forceinline__ void merge_payload(ML& L, uint32_t mi, uint32_t reaso
       uint64_t rec = d.pool[(size_t)off + e];
       uint32_t subj = (uint32_t)(rec >> 34);
       uint64_t key = rec & KEY_MASK;
-      if (key == (L.row[subj] & KEY_MASK)) continue;  // !r1.equals(table.get(id)) at processing time
+      if (key == key34(L.rk[subj])) continue;  // !r1.equals(table.get(id)) at processing time
       update_membership(L, subj, rec_status(key), rec_inc(key), reason, g);
     }
   }
@@ -675,7 +680,8 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   for (int i = 0; i < 8; ++i) L.sel[i] = d.sel[(size_t)m * 8 + i];
   L.evHash = d.evHash[m];
   const size_t li = lidx(d, m);  // per-observer arrays hold only this shard's rows
-  L.row = d.row + li * d.NS;
+  L.rk = d.rowk + li * d.NS;
+  L.ra = d.rowa + li * d.NS;
   L.fdl = d.fdl + li * d.LCAP;
   L.gl = d.gl + li * d.LCAP;
   L.subs = d.subs + li * SUBCAP * 4;
@@ -691,14 +697,14 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   if (preq) {
     d.pending_inc[m] = 0;
     for (uint32_t b = preq >> 2; b > 0; --b) {  // one bump and one gossip per swim_update_incarnation call
-      uint64_t v0 = L.row[m];
+      uint64_t v0 = row_ld(L, m);
       uint32_t ni = rec_inc(v0) + 1u;
       row_put(L, m, (v0 & ~KEY_MASK) | rec_key(ST_ALIVE, ni));
       L.c[C_W]++;
       spread(L, m, ST_ALIVE, ni);
     }
     if (preq & 2u) {  // the own record becomes DEAD inc+1 (the only DEAD record a table keeps) and is spread
-      uint64_t v0 = L.row[m];
+      uint64_t v0 = row_ld(L, m);
       uint32_t ni = rec_inc(v0) + 1u;
       row_put(L, m, (v0 & ~KEY_MASK) | rec_key(ST_DEAD, ni));
       L.c[C_W]++;
@@ -928,9 +934,9 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
         L.nfetch--;
         uint32_t st = w3 & 0xFF, reason = (w3 >> 8) & 0xFF, added = (w3 >> 16) & 0xFF;
         // doOnSuccess (:563-567, :576-581): updateMetadata then sink.next
-        uint64_t v = L.row[subj];
+        uint64_t v = row_ld(L, subj);
         uint32_t oldm = known_meta(L, subj, v);
-        L.row[subj] = v | META_BIT;
+        L.ra[subj] = aux32(v | META_BIT);
         const uint32_t u = d.md_uidx[subj];
         if (u != NONE32) d.md_ver[lidx(d, m) * MDU + u] = meta;
         if (added)
@@ -1031,11 +1037,12 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   if (L.timerMin <= k) {  // suspicion timeouts (:608-618), ascending subject; lazy minimum
     uint32_t nmin = NEVER;
     for (uint32_t s = 0; s < L.N; ++s) {
-      uint64_t v = L.row[s];
-      uint32_t dl = rec_timer(v);
+      const uint32_t a = L.ra[s];  // the aux plane alone holds the deadline
+      uint32_t dl = rec_timer((uint64_t)a << 34);
       if (dl == 0) continue;
+      const uint64_t v = rec_join(L.rk[s], a);
       if (dl == k) {
-        L.row[s] = rec_with_timer(v, 0);
+        L.ra[s] = aux32(rec_with_timer(v, 0));
         if (rec_status(v) != ST_ABSENT) {
           L.c[C_R]++;
           update_membership(L, s, ST_DEAD, rec_inc(v), R_TIMEOUT, -1);

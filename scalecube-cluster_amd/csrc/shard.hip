@@ -19,10 +19,24 @@
 
 namespace swim {
 
+// the block that finishes last (all earlier blocks' stores are visible to it after the fence)
+__device__ __forceinline__ bool last_block(uint32_t* ctr, uint32_t nblocks) {
+  __shared__ bool last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(ctr, 1u) == nblocks - 1u;
+  }
+  __syncthreads();
+  if (last) __threadfence();
+  return last;
+}
+
 __device__ __forceinline__ uint64_t sync_entry_bytes(const Dev& d) { return sizeof(SyncMsg) + 8 + 8ull * d.MW; }
 
-__device__ __forceinline__ const uint64_t* payload_row(const Dev& d, const SyncMsg& mm, uint32_t b) {
-  return mm.payload == NEVER ? d.row + lidx(d, mm.src) * d.NS : d.arena[b] + (size_t)mm.payload * d.NS;
+// a payload's key plane: the sender's live row or its copy-on-write snapshot
+__device__ __forceinline__ const uint32_t* payload_row(const Dev& d, const SyncMsg& mm, uint32_t b) {
+  return mm.payload == NEVER ? d.rowk + lidx(d, mm.src) * d.NS : d.arena[b] + (size_t)mm.payload * d.NS;
 }
 
 // this tick's sends: local destinations go straight to the next tick's inbound list, the rest are queued per shard
@@ -48,7 +62,7 @@ __global__ void k_sync_route(Dev d, uint32_t b) {
   }
 }
 
-// chunk masks: which 2048-record chunks of each outbound payload differ (in record key) from the baseline row
+// chunk masks: which 2048-record chunks of each outbound payload differ (in key32) from the baseline row
 __global__ void __launch_bounds__(256) k_sync_dirty(Dev d, uint32_t b) {
   const uint32_t q = blockIdx.y;
   if (q == d.rank) return;
@@ -60,12 +74,12 @@ __global__ void __launch_bounds__(256) k_sync_dirty(Dev d, uint32_t b) {
     const uint32_t s0 = c * CH + threadIdx.x * 8;
     bool diff = false;
     if (s0 < d.NS) {
-      const ulonglong2* pv = (const ulonglong2*)(payload_row(d, mm, b) + s0);
-      const ulonglong2* bv = (const ulonglong2*)(d.base_row + s0);
+      const uint4* pv = (const uint4*)(payload_row(d, mm, b) + s0);
+      const uint4* bv = (const uint4*)(d.base_row + s0);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        ulonglong2 a = pv[k], z = bv[k];
-        diff |= ((a.x ^ z.x) & KEY_MASK) != 0 || ((a.y ^ z.y) & KEY_MASK) != 0;
+      for (int k = 0; k < 2; ++k) {
+        const uint4 a = pv[k], z = bv[k];
+        diff |= ((a.x ^ z.x) | (a.y ^ z.y) | (a.z ^ z.z) | (a.w ^ z.w)) != 0;
       }
     }
     if (__syncthreads_or(diff) && threadIdx.x == 0) {
@@ -92,7 +106,7 @@ __global__ void __launch_bounds__(256) k_pack_a(Dev d, uint32_t b) {
     }
     uint64_t off_sync = 32 + 4ull * NSW * nslot + 4ull * RRW * nround;
     uint64_t data_off = (off_sync + SE * nsync + 255) & ~255ull;
-    uint64_t total = data_off + (uint64_t)nchunk * CH * 8;
+    uint64_t total = data_off + (uint64_t)nchunk * CH * 4;
     if (total > d.XA_PEER || nchunk > d.CHCAP) {
       atomicOr(d.err, E_XCAP);
       nslot = nround = nsync = nchunk = 0;
@@ -130,102 +144,124 @@ __global__ void __launch_bounds__(256) k_pack_a(Dev d, uint32_t b) {
   }
 }
 
-// copy the differing payload chunks into peer q's region (16-B loads and stores, 8 records per lane)
+// copy the differing payload chunks (key plane) into peer q's region (16-B loads and stores, 8 keys per lane). With
+// RCCL, the last block of peer q's column then writes q's inline all-to-all block (count word + region head), so
+// exchange A needs no separate copy kernel.
 __global__ void __launch_bounds__(256) k_pack_a_chunks(Dev d, uint32_t b) {
   const uint32_t q = blockIdx.y;
-  if (q == d.rank) return;
+  if (q == d.rank) {  // the block to itself carries an empty region
+    if (d.inl && blockIdx.x == 0 && threadIdx.x == 0) *(uint64_t*)(d.xi_send + (size_t)q * XINL) = 0ull;
+    return;
+  }
   uint8_t* R = d.xa_send + (size_t)q * d.XA_PEER;
   const uint32_t* H = (const uint32_t*)R;
   const uint32_t nsync = H[2], data_off = H[4];
-  if (H[3] == 0) return;
-  uint64_t* dst0 = (uint64_t*)(R + data_off);
-  for (uint32_t w = blockIdx.x; w < nsync * d.NCHUNK; w += gridDim.x) {
-    const uint32_t j = w / d.NCHUNK, c = w % d.NCHUNK;
-    const size_t e = (size_t)q * d.RQCAP + j;
-    const uint64_t* mk = d.rq_mask + e * d.MW;
-    if (!((mk[c >> 6] >> (c & 63)) & 1ull)) continue;
-    uint32_t rank = __popcll(mk[c >> 6] & ((1ull << (c & 63)) - 1ull));
-    for (uint32_t x = 0; x < (c >> 6); ++x) rank += __popcll(mk[x]);
-    const uint32_t s0 = c * CH + threadIdx.x * 8;
-    if (s0 >= d.NS) continue;
-    const SyncMsg& mm = d.msgs[b][d.rq_list[e]];
-    const ulonglong2* src = (const ulonglong2*)(payload_row(d, mm, b) + s0);
-    ulonglong2* dst = (ulonglong2*)(dst0 + (size_t)(d.rq_base[e] + rank) * CH + threadIdx.x * 8);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) dst[k] = src[k];
+  if (H[3] != 0) {
+    uint32_t* dst0 = (uint32_t*)(R + data_off);
+    for (uint32_t w = blockIdx.x; w < nsync * d.NCHUNK; w += gridDim.x) {
+      const uint32_t j = w / d.NCHUNK, c = w % d.NCHUNK;
+      const size_t e = (size_t)q * d.RQCAP + j;
+      const uint64_t* mk = d.rq_mask + e * d.MW;
+      if (!((mk[c >> 6] >> (c & 63)) & 1ull)) continue;
+      uint32_t rank = __popcll(mk[c >> 6] & ((1ull << (c & 63)) - 1ull));
+      for (uint32_t x = 0; x < (c >> 6); ++x) rank += __popcll(mk[x]);
+      const uint32_t s0 = c * CH + threadIdx.x * 8;
+      if (s0 >= d.NS) continue;
+      const SyncMsg& mm = d.msgs[b][d.rq_list[e]];
+      const uint4* src = (const uint4*)(payload_row(d, mm, b) + s0);
+      uint4* dst = (uint4*)(dst0 + (size_t)(d.rq_base[e] + rank) * CH + threadIdx.x * 8);
+      dst[0] = src[0];
+      dst[1] = src[1];
+    }
   }
+  if (!d.inl || !last_block(&d.xdone[q], gridDim.x)) return;
+  const unsigned long long w = d.xa_scnt[q];
+  uint64_t* idst = (uint64_t*)(d.xi_send + (size_t)q * XINL);
+  if (threadIdx.x == 0) idst[0] = w;
+  const uint64_t n = min((uint64_t)(w & XCNT_MASK), (uint64_t)XINL - 8) / 8;  // regions are multiples of 8 B
+  const uint64_t* isrc = (const uint64_t*)R;
+  for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) idst[1 + i] = isrc[i];
 }
 
-// replay peer p's gossip creations and rounds into the replicated gossip plane; queue its SYNC messages
-__global__ void __launch_bounds__(256) k_unpack_a(Dev d, uint32_t k) {
-  const uint32_t p = blockIdx.y;
-  if (p == d.rank || (d.xa_rcnt[p] & XCNT_MASK) < 32) return;
-  const uint8_t* R = d.xa_recv + (size_t)p * d.XA_PEER;
-  const uint32_t* H = (const uint32_t*)R;
-  const uint32_t nslot = H[0], nround = H[1], nsync = H[2], data_off = H[4];
-  const uint32_t* S = (const uint32_t*)(R + 32);
-  const uint32_t* RR = S + (size_t)nslot * NSW;
-  const uint8_t* E = (const uint8_t*)(RR + (size_t)nround * RRW);
-  const uint64_t SE = sync_entry_bytes(d);
-  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
-  for (uint32_t i = tid; i < nslot; i += nth) {  // spread -> createAndPutGossip at the origin (member.hip)
-    const uint32_t* r = S + (size_t)i * NSW;
-    uint32_t g = r[0], origin = r[7];
-    d.slot_gid[g] = (uint64_t)r[1] | ((uint64_t)r[2] << 32);
-    d.slot_subj[g] = r[3];
-    d.slot_ctick[g] = r[4];
-    d.slot_key[g] = (uint64_t)r[5] | ((uint64_t)r[6] << 32);
-    d.slot_holders[g] = 1;
-    d.slot_used[g] = 1;
-    d.S[(size_t)g * d.N + origin] = (r[4] + 1u) & S_TICK_MASK;
-    atomicAdd(&d.held[origin], 1u);
-  }
-  for (uint32_t i = tid; i < nround; i += nth) {  // do_spread_gossip at the sender (member.hip)
-    const uint32_t* r = RR + (size_t)i * RRW;
-    uint32_t m = r[0], cnt = r[1];
-    d.tround[m] = 1;
-    d.tcnt[m] = cnt;
-    d.tspread[m] = r[2];
-    d.tperiod[m] = r[3];
-    uint32_t pos = d.log_pos[m] % d.LOGW;
-    size_t lo = (size_t)m * d.LOGW + pos;
-    if (d.log_pos[m] > 0 && d.log_spread[(size_t)m * d.LOGW + (d.log_pos[m] - 1) % d.LOGW] != r[2]) d.spchg[m] = k;
-    d.log_tick[lo] = k;
-    d.log_spread[lo] = r[2];
-    d.log_cnt[lo] = cnt;
-    for (uint32_t j = 0; j < cnt; ++j) {
-      d.T[(size_t)m * d.F + j] = r[4 + j];
-      d.log_tg[lo * d.F + j] = r[4 + j];
-    }
-    d.log_pos[m]++;
-  }
-  for (uint32_t i = tid; i < nsync; i += nth) {
-    const uint8_t* e = E + SE * i;
-    SyncMsg mm = *(const SyncMsg*)e;
-    uint32_t base = ((const uint32_t*)(e + sizeof(SyncMsg)))[0];
-    const uint64_t* mk = (const uint64_t*)(e + sizeof(SyncMsg) + 8);
-    uint32_t ri = atomicAdd(&d.xn[5], 1u);
-    uint32_t j = atomicAdd(&d.xn[4], 1u);
-    if (ri >= d.RXCAP || j >= d.MSGCAP) {
-      atomicOr(d.err, E_XCAP);
-      continue;
-    }
-    for (uint32_t w = 0; w < d.MW; ++w) d.rx_mask[(size_t)ri * d.MW + w] = mk[w];
-    d.rx_off[ri] = (uint64_t)p * d.XA_PEER + data_off + (uint64_t)base * CH * 8;
-    mm.payload = PAY_RX | ri;
-    mm.ncand = 0;
-    d.mtmp[j] = mm;
-  }
-}
-
-// the assembled inbound list becomes msgs[b], which the next tick sorts and merges
-__global__ void k_msgs_commit(Dev d, uint32_t b) {
+// the assembled inbound list becomes msgs[b], which the next tick sorts and merges (one block)
+__device__ void msgs_commit(const Dev& d, uint32_t b) {
   uint32_t n = min(d.xn[4], d.MSGCAP);
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
     d.msgs[b][i] = d.mtmp[i];
     d.m_next[(size_t)b * d.MSGCAP + i] = atomicExch(&d.m_head[(size_t)b * d.N + d.mtmp[i].dst], i);
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) d.nmsg[b] = n;
+  if (threadIdx.x == 0) d.nmsg[b] = n;
+}
+
+// replay peer p's gossip creations and rounds into the replicated gossip plane; queue its SYNC messages. The block
+// that finishes last commits the inbound list, and, when no shard has a gossip slot in use (`end`), closes the tick
+// (k_tick_end): the steady-state tick after exchange A is this one launch.
+__global__ void __launch_bounds__(256) k_unpack_a(Dev d, uint32_t k, uint32_t end) {
+  const uint32_t p = blockIdx.y;
+  if (p != d.rank && (d.xa_rcnt[p] & XCNT_MASK) >= 32) {
+    const uint8_t* R = d.xa_recv + (size_t)p * d.XA_PEER;
+    const uint32_t* H = (const uint32_t*)R;
+    const uint32_t nslot = H[0], nround = H[1], nsync = H[2], data_off = H[4];
+    const uint32_t* S = (const uint32_t*)(R + 32);
+    const uint32_t* RR = S + (size_t)nslot * NSW;
+    const uint8_t* E = (const uint8_t*)(RR + (size_t)nround * RRW);
+    const uint64_t SE = sync_entry_bytes(d);
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+    for (uint32_t i = tid; i < nslot; i += nth) {  // spread -> createAndPutGossip at the origin (member.hip)
+      const uint32_t* r = S + (size_t)i * NSW;
+      uint32_t g = r[0], origin = r[7];
+      d.slot_gid[g] = (uint64_t)r[1] | ((uint64_t)r[2] << 32);
+      d.slot_subj[g] = r[3];
+      d.slot_ctick[g] = r[4];
+      d.slot_key[g] = (uint64_t)r[5] | ((uint64_t)r[6] << 32);
+      d.slot_holders[g] = 1;
+      d.slot_used[g] = 1;
+      d.S[(size_t)g * d.N + origin] = (r[4] + 1u) & S_TICK_MASK;
+      atomicAdd(&d.held[origin], 1u);
+    }
+    for (uint32_t i = tid; i < nround; i += nth) {  // do_spread_gossip at the sender (member.hip)
+      const uint32_t* r = RR + (size_t)i * RRW;
+      uint32_t m = r[0], cnt = r[1];
+      d.tround[m] = 1;
+      d.tcnt[m] = cnt;
+      d.tspread[m] = r[2];
+      d.tperiod[m] = r[3];
+      uint32_t pos = d.log_pos[m] % d.LOGW;
+      size_t lo = (size_t)m * d.LOGW + pos;
+      if (d.log_pos[m] > 0 && d.log_spread[(size_t)m * d.LOGW + (d.log_pos[m] - 1) % d.LOGW] != r[2]) d.spchg[m] = k;
+      d.log_tick[lo] = k;
+      d.log_spread[lo] = r[2];
+      d.log_cnt[lo] = cnt;
+      for (uint32_t j = 0; j < cnt; ++j) {
+        d.T[(size_t)m * d.F + j] = r[4 + j];
+        d.log_tg[lo * d.F + j] = r[4 + j];
+      }
+      d.log_pos[m]++;
+    }
+    for (uint32_t i = tid; i < nsync; i += nth) {
+      const uint8_t* e = E + SE * i;
+      SyncMsg mm = *(const SyncMsg*)e;
+      uint32_t base = ((const uint32_t*)(e + sizeof(SyncMsg)))[0];
+      const uint64_t* mk = (const uint64_t*)(e + sizeof(SyncMsg) + 8);
+      uint32_t ri = atomicAdd(&d.xn[5], 1u);
+      uint32_t j = atomicAdd(&d.xn[4], 1u);
+      if (ri >= d.RXCAP || j >= d.MSGCAP) {
+        atomicOr(d.err, E_XCAP);
+        continue;
+      }
+      for (uint32_t w = 0; w < d.MW; ++w) d.rx_mask[(size_t)ri * d.MW + w] = mk[w];
+      d.rx_off[ri] = (uint64_t)p * d.XA_PEER + data_off + (uint64_t)base * CH * 4;
+      mm.payload = PAY_RX | ri;
+      mm.ncand = 0;
+      d.mtmp[j] = mm;
+    }
+  }
+  if (!last_block(&d.xn[6], gridDim.x * gridDim.y)) return;
+  msgs_commit(d, k & 1);
+  if (end) {
+    __syncthreads();
+    tick_end(d, k);
+  }
 }
 
 __global__ void __launch_bounds__(256) k_pack_b(Dev d) {

@@ -6,6 +6,11 @@
 //   bit  34      metadata known         MetadataStoreImpl.membersMetadata contains the subject
 //   bits 35..63  suspicion deadline     scheduleSuspicionTimeoutTask deadline tick, 0 = no timer (:597-606)
 // The record key (inc | status<<32) is what SYNC payloads carry and what isOverrides compares.
+//
+// Physical layout: a row is two u32 planes. The key plane holds key32 = inc << 2 | status, the only
+// part of a record that SYNC payloads carry and k_sync_diff compares (4 B per record instead of 8); the aux plane
+// holds bits 34..63 of the logical record (metadata known, suspicion deadline). Incarnations therefore must stay
+// below 2^30 in a stored row; a larger one raises E_INC instead of being truncated.
 #pragma once
 #include <stdint.h>
 
@@ -29,6 +34,11 @@ constexpr uint64_t TIMER_MASK29 = (1ull << 29) - 1;
 SW_HD uint32_t rec_status(uint64_t v) { return (uint32_t)(v >> 32) & 3u; }
 SW_HD uint32_t rec_inc(uint64_t v) { return (uint32_t)v; }
 SW_HD uint64_t rec_key(uint32_t st, uint32_t inc) { return (uint64_t)inc | ((uint64_t)st << 32); }
+constexpr uint32_t INC_LIMIT = 1u << 30;
+SW_HD uint32_t key32(uint64_t v) { return ((uint32_t)v << 2) | rec_status(v); }
+SW_HD uint64_t key34(uint32_t k) { return (uint64_t)(k >> 2) | ((uint64_t)(k & 3u) << 32); }
+SW_HD uint32_t aux32(uint64_t v) { return (uint32_t)(v >> 34); }
+SW_HD uint64_t rec_join(uint32_t k, uint32_t a) { return key34(k) | ((uint64_t)a << 34); }
 SW_HD uint32_t rec_timer(uint64_t v) { return (uint32_t)(v >> TIMER_SHIFT); }
 SW_HD uint64_t rec_with_timer(uint64_t v, uint32_t dl) {
   return (v & ((1ull << TIMER_SHIFT) - 1)) | ((uint64_t)(dl & TIMER_MASK29) << TIMER_SHIFT);
