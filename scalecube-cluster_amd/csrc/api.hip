@@ -611,7 +611,7 @@ int swim_step(swim_handle* h, uint32_t n) {
       HIPCK(hipEventRecord(h->ev_member, h->stream));
       const bool pipe = i + 1 < n && !h->no_pipe;
       if (pipe) launch_diff(d, k + 1, h->stream, profile ? &h->prof[i + 1] : nullptr);  // overlaps the wait
-      HIPCK(hipEventSynchronize(h->ev_member));
+      HIPCK(hipEventSynchronize(h->ev_member));  // (a spin wait measured the same here: diff(k+1) hides the wake-up)
       if (h->hflag[0] != 0 || h->no_skip) {
         launch_gossip(d, k, h->stream, te);
       } else if (te && te->all) {
