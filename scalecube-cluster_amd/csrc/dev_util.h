@@ -155,4 +155,20 @@ __device__ __forceinline__ void tick_end(const Dev& d, uint32_t k) {
   }
 }
 
+// end of k_member_tick (W == 1, the last block, one thread): reset the per-tick counters the gossip plane of this tick and the SYNC diff and
+// member control of the next tick append to, and tell the host whether any gossip slot is in use (if none, the
+// gossip data plane of this tick has nothing to send, deliver, route or recycle and is not launched)
+__device__ __forceinline__ void tick_flag(const Dev& d, uint32_t k) {
+  uint32_t nb = (k + 1) & 1;
+  d.nmsg[nb] = 0;
+  d.arena_used[nb] = 0;
+  *d.pool_used = 0;
+  *d.nactive = 0;
+  *d.deliv_n = 0;
+  *d.rc_n = 0;
+  d.deaths_n[(k + 1) & 1] = 0;
+  d.hflag[0] = (uint32_t)((int32_t)d.SPR - *d.free_top);
+  __threadfence_system();
+}
+
 }  // namespace swim

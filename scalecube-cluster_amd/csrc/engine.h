@@ -153,7 +153,7 @@ struct Dev {
   uint32_t* pending_inc; // [N] host requests for the next tick's P0: bits 2.. updateIncarnation calls, bit 1 leaveCluster
   uint32_t *deaths, *deaths_n;  // [2][DEATHCAP], [2]: members whose leave completed at tick k (parity k & 1)
   uint32_t* next_evt; // [N] earliest tick at which a pending path / subscription / fetch needs the member
-  uint32_t *busy, *nbusy; // members that need the full control path this tick, per block of 256 (k_member_triage)
+  uint32_t* mdone;  // finished k_member_tick blocks this tick (the last one runs the end-of-tick resets)
   uint32_t* chunk_meta;                      // [MSGCAP][NCHUNK][2] (pool offset, count)
   uint64_t* pool;                            // candidate (subject << 34 | key)
   uint32_t* pool_used;

@@ -5,8 +5,7 @@
 
 namespace swim {
 
-__global__ void k_member_tick(const Dev* __restrict__ dp, uint32_t k);  // member.hip
-__global__ void k_member_triage(const Dev* __restrict__ dp, uint32_t k);
+__global__ void k_member_tick(const Dev* __restrict__ dp, uint32_t k, uint32_t flag);  // member.hip
 // shard.hip
 __global__ void k_sync_route(Dev d, uint32_t b);
 __global__ void k_sync_dirty(Dev d, uint32_t b);
@@ -967,22 +966,6 @@ __global__ void __launch_bounds__(256) k_hash(Dev d, uint64_t* out, uint32_t now
   }
 }
 
-// after k_member_tick (W == 1): reset the per-tick counters the gossip plane of this tick and the SYNC diff and
-// member control of the next tick append to, and tell the host whether any gossip slot is in use (if none, the
-// gossip data plane of this tick has nothing to send, deliver, route or recycle and is not launched)
-__global__ void k_tick_flag(Dev d, uint32_t k) {
-  if (threadIdx.x != 0) return;
-  uint32_t nb = (k + 1) & 1;
-  d.nmsg[nb] = 0;
-  d.arena_used[nb] = 0;
-  *d.pool_used = 0;
-  *d.nactive = 0;
-  *d.deliv_n = 0;
-  *d.rc_n = 0;
-  d.deaths_n[(k + 1) & 1] = 0;
-  d.hflag[0] = (uint32_t)((int32_t)d.SPR - *d.free_top);
-  __threadfence_system();
-}
 
 __global__ void k_tick_end(Dev d, uint32_t k) { tick_end(d, k); }
 
@@ -1018,10 +1001,8 @@ void launch_diff(const Dev& d, uint32_t k, void* stream, const TickEvents* prof)
 void launch_member(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
   hipStream_t st = (hipStream_t)stream;
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[2], st);
-  hipLaunchKernelGGL(k_member_triage, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k);
-  hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k);
+  hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k, 1u);  // + k_tick_flag's work
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[3], st);
-  hipLaunchKernelGGL(k_tick_flag, dim3(1), dim3(64), 0, st, d, k);
 }
 
 static void launch_receipt_routing(const Dev& d, hipStream_t st);
@@ -1064,8 +1045,7 @@ void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   if (k > 0) launch_sync_diff(d, pb, st);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[2], st);
-  hipLaunchKernelGGL(k_member_triage, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k);
-  hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k);
+  hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k, 0u);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[3], st);
   hipLaunchKernelGGL(k_sync_route, dim3(cdiv(d.MSGCAP, 256)), dim3(256), 0, st, d, b);
   hipLaunchKernelGGL(k_sync_dirty, dim3(512, d.W), dim3(256), 0, st, d, b);

@@ -1106,12 +1106,16 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   for (int i = 0; i < 8; ++i) cnt[i] += L.c[i];
 }
 
-// One thread per owned member: the idle fast path, and per block of 256 members a compact list of those that need
-// the full path (block-local ballot prefix, no atomics: one counter shared by 1.5k waves serialised at L2), so the
-// heavy kernel runs only ~1/3 of the waves and none of them mostly idle.
-__global__ void __launch_bounds__(256) k_member_triage(const Dev* __restrict__ dp, uint32_t k) {
-  const Dev& d = *dp;
+// One launch per tick for member control. Each block triages its 256 members (the idle fast path, one thread per
+// member, unconditional coalesced loads) and compacts the busy ones into an LDS list with a block-local ballot
+// prefix (no atomics); its first waves then run the full control path for them, so no wave runs mostly idle lanes.
+// Counters are summed across the wave first: 10^4 pingers per tick adding to one word would serialise on that
+// address. With `flag` (W == 1) the block that finishes last runs the end-of-tick resets and raises the host flag.
+__global__ void __launch_bounds__(256) k_member_tick(const Dev* __restrict__ dp, uint32_t k, uint32_t flag) {
+  const Dev& d = *dp;  // global, not kernarg: taking its address must not copy ~1 KB into per-lane scratch
   __shared__ uint32_t wc[4];
+  __shared__ uint32_t list[256];
+  __shared__ bool last;
   const uint32_t m = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
   const bool busy = m < d.hi && member_triage(d, m, k);
   const uint64_t bal = __ballot(busy);
@@ -1120,28 +1124,34 @@ __global__ void __launch_bounds__(256) k_member_triage(const Dev* __restrict__ d
   __syncthreads();
   uint32_t base = 0;
   for (uint32_t j = 0; j < w; ++j) base += wc[j];
-  if (busy) d.busy[(size_t)blockIdx.x * 256 + base + __popcll(bal & ((1ull << lane) - 1ull))] = m;
-  if (threadIdx.x == 0) d.nbusy[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
-}
-
-// Counters are summed across the wave first: 10^4 pingers per tick adding to one word would serialise on that address.
-__global__ void __launch_bounds__(256) k_member_tick(const Dev* __restrict__ dp, uint32_t k) {
-  const Dev& d = *dp;  // global, not kernarg: taking its address must not copy ~1 KB into per-lane scratch
-  const uint32_t nb = d.nbusy[blockIdx.x];
-  if ((threadIdx.x & ~63u) >= nb) return;  // whole wave past this block's busy list
-  unsigned long long cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (threadIdx.x < nb) member_tick_body(d, d.busy[(size_t)blockIdx.x * 256 + threadIdx.x], k, cnt);
-  const uint32_t lane = threadIdx.x & 63;
+  if (busy) list[base + __popcll(bal & ((1ull << lane) - 1ull))] = m;
+  __syncthreads();
+  const uint32_t nb = wc[0] + wc[1] + wc[2] + wc[3];
+  if ((threadIdx.x & ~63u) < nb) {  // waves wholly past the busy list skip to the end
+    unsigned long long cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (threadIdx.x < nb) member_tick_body(d, list[threadIdx.x], k, cnt);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    unsigned long long v = cnt[i];
+    for (int i = 0; i < 8; ++i) {
+      unsigned long long v = cnt[i];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      uint32_t lo = __shfl_xor((uint32_t)v, o), hi = __shfl_xor((uint32_t)(v >> 32), o);
-      v += ((unsigned long long)hi << 32) | lo;
+      for (int o = 32; o > 0; o >>= 1) {
+        uint32_t lo = __shfl_xor((uint32_t)v, o), hi = __shfl_xor((uint32_t)(v >> 32), o);
+        v += ((unsigned long long)hi << 32) | lo;
+      }
+      if (lane == 0 && v) atomicAdd(&d.ctr[i], v);
     }
-    if (lane == 0 && v) atomicAdd(&d.ctr[i], v);
   }
+  if (!flag) return;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(d.mdone, 1u) == gridDim.x - 1u;
+  }
+  __syncthreads();
+  if (!last || threadIdx.x != 0) return;
+  __threadfence();
+  *d.mdone = 0;
+  tick_flag(d, k);
 }
 
 }  // namespace swim
