@@ -232,8 +232,11 @@ int build(swim_handle* h) {
   // default: 64 slots per member, at most 32 GB of holder table (C2's SYNC re-spread storm keeps ~10^5 gossips alive)
   uint64_t slots = c.gossip_slot_cap ? c.gossip_slot_cap
                                      : std::min<uint64_t>(1ull << 22, std::max<uint64_t>(1024, std::min<uint64_t>(64 * N, (32ull << 30) / (4 * N))));
-  // every shard allocates new gossips from its own slot range; the slot table itself is replicated
-  d.SPR = (uint32_t)std::min<uint64_t>(slots, (1ull << 22) / d.W);
+  // every shard allocates new gossips from its own slot range; the slot table itself is replicated, so the ranges
+  // split the budget (twice over, for shards that create more than their share) instead of multiplying it by W: at
+  // 100k members and W = 8 a full range per shard would be a 275 GB holder table on every GPU
+  const uint64_t share = d.W == 1 ? slots : std::max<uint64_t>(1024, (2 * slots + d.W - 1) / d.W);
+  d.SPR = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(slots, share), (1ull << 22) / d.W);
   d.SLOTS = d.SPR * d.W;
   uint64_t mc = N / d.sync_t * 4 + N / d.ping_t + 1024;
   if (c.init_mode == SWIM_INIT_COLD_JOIN) mc = std::max<uint64_t>(mc, N + 1024);
@@ -289,6 +292,8 @@ int build(swim_handle* h) {
     d.XA_PEER = ((32 + 4ull * NSW * d.NSCAP + 4ull * RRW * d.RRCAP + se * d.RQCAP + 511) & ~255ull) +
                 (uint64_t)d.CHCAP * CH * 4;
     d.XB_PEER = 16 + 8ull * std::min<uint64_t>((uint64_t)d.DCAP + d.SWCAP, 1ull << 25);
+    A(d.rdirty, (uint64_t)NL * d.MW) A(d.arena_dirty[0], (uint64_t)d.ARENA_ROWS * d.MW)
+    A(d.arena_dirty[1], (uint64_t)d.ARENA_ROWS * d.MW)
     A(d.base_row, d.NS) A(d.xn, 8) A(d.ns_rec, (uint64_t)d.NSCAP * NSW) A(d.rr_rec, (uint64_t)d.RRCAP * RRW)
     A(d.sw_rec, d.SWCAP) A(d.rq_n, d.W) A(d.rq_list, (uint64_t)d.W * d.RQCAP)
     A(d.rq_mask, (uint64_t)d.W * d.RQCAP * d.MW) A(d.rq_cnt, (uint64_t)d.W * d.RQCAP) A(d.rq_base, (uint64_t)d.W * d.RQCAP)

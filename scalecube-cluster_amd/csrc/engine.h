@@ -177,6 +177,9 @@ struct Dev {
   uint32_t W, rank, lo, hi, NL, SPR, MW;  // SPR: gossip slots owned per shard; MW: u64 words per chunk mask
   uint32_t NSCAP, RRCAP, SWCAP, RQCAP, RXCAP, CHCAP;
   uint64_t XA_PEER, XB_PEER;  // bytes per peer region of the two exchange buffers
+  uint64_t* rdirty;    // [NL][MW] per own observer: the 2048-record chunks of its key plane ever written with a key
+                       // that differs from base_row (conservative: never cleared); a payload ships exactly these
+  uint64_t* arena_dirty[2];  // [ARENA_ROWS][MW] the sender's rdirty at copy-on-write time
   uint32_t* base_row;  // [NS] baseline key plane: a remote SYNC payload ships only its chunks that differ
   uint32_t* xn;        // [8] 0 new slots, 1 round records, 2 sweeps, 4 inbound msgs (mtmp), 5 rx payloads
   uint32_t* ns_rec;    // [NSCAP][NSW] gossips created on this shard this tick

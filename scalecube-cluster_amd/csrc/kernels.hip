@@ -8,7 +8,6 @@ namespace swim {
 __global__ void k_member_tick(const Dev* __restrict__ dp, uint32_t k, uint32_t flag);  // member.hip
 // shard.hip
 __global__ void k_sync_route(Dev d, uint32_t b);
-__global__ void k_sync_dirty(Dev d, uint32_t b);
 __global__ void k_pack_a(Dev d, uint32_t b);
 __global__ void k_pack_a_chunks(Dev d, uint32_t b);
 __global__ void k_unpack_a(Dev d, uint32_t k, uint32_t end);
@@ -77,6 +76,9 @@ __global__ void k_init_rows(Dev d) {
       rk[s] = key32(v);
       ra[s] = aux32(v);
     }
+    if (d.W > 1)  // dirty chunks against base_row: none for a PRECONVERGED row, the own chunk for a cold join
+      for (uint32_t w = threadIdx.x; w < d.MW; w += blockDim.x)
+        d.rdirty[(size_t)li * d.MW + w] = (d.init_mode != 1 && (m / CH) >> 6 == w) ? 1ull << ((m / CH) & 63) : 0ull;
   }
 }
 
@@ -1048,7 +1050,6 @@ void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k, 0u);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[3], st);
   hipLaunchKernelGGL(k_sync_route, dim3(cdiv(d.MSGCAP, 256)), dim3(256), 0, st, d, b);
-  hipLaunchKernelGGL(k_sync_dirty, dim3(512, d.W), dim3(256), 0, st, d, b);
   hipLaunchKernelGGL(k_pack_a, dim3(d.W), dim3(256), 0, st, d, b);
   hipLaunchKernelGGL(k_pack_a_chunks, dim3(64, d.W), dim3(256), 0, st, d, b);
 }

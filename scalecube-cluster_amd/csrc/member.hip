@@ -25,6 +25,7 @@ struct ML {
   uint32_t sel[8];
   uint64_t evHash;
   uint32_t *rk, *ra;  // this observer's row: key plane and aux plane (swim_common.h)
+  uint64_t* rd;       // W > 1: its dirty-chunk mask against base_row (Dev::rdirty), else null
   uint32_t *fdl, *gl, *subs, *paths, *fetch, *groups;
   unsigned long long c[8];
   uint32_t pend;  // this tick's SYNC messages that carry the live row: a chain through SyncMsg.pad (NEVER = none)
@@ -58,6 +59,8 @@ __device__ __forceinline__ void cow(ML& L) {
   }
   uint32_t* dst = d.arena[b] + (size_t)r * d.NS;
   for (uint32_t s = 0; s < d.NS; ++s) dst[s] = L.rk[s];  // keys only, with the zero padding k_sync_diff reads up to NS
+  if (L.rd)
+    for (uint32_t w = 0; w < d.MW; ++w) d.arena_dirty[b][(size_t)r * d.MW + w] = L.rd[w];
   for (uint32_t i = L.pend; i != NEVER; i = d.msgs[b][i].pad) d.msgs[b][i].payload = r;
   L.pend = NEVER;
 }
@@ -70,6 +73,7 @@ __device__ __forceinline__ void row_put(ML& L, uint32_t s, uint64_t v) {
   if (rec_inc(v) >= INC_LIMIT) set_err(*L.d, E_INC);
   if (L.pend != NEVER && L.rk[s] != k) cow(L);
   L.rk[s] = k;
+  if (L.rd && k != L.d->base_row[s]) L.rd[(s / CH) >> 6] |= 1ull << ((s / CH) & 63);
   L.ra[s] = aux32(v);
 }
 
@@ -682,6 +686,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   const size_t li = lidx(d, m);  // per-observer arrays hold only this shard's rows
   L.rk = d.rowk + li * d.NS;
   L.ra = d.rowa + li * d.NS;
+  L.rd = d.W > 1 ? d.rdirty + li * d.MW : nullptr;
   L.fdl = d.fdl + li * d.LCAP;
   L.gl = d.gl + li * d.LCAP;
   L.subs = d.subs + li * SUBCAP * 4;

@@ -40,6 +40,7 @@ __device__ __forceinline__ const uint32_t* payload_row(const Dev& d, const SyncM
 }
 
 // this tick's sends: local destinations go straight to the next tick's inbound list, the rest are queued per shard
+// with their payload's dirty-chunk mask (maintained at every key write, member.hip row_put; no scan of the payload)
 __global__ void k_sync_route(Dev d, uint32_t b) {
   uint32_t n = d.nmsg[b] < d.MSGCAP ? d.nmsg[b] : d.MSGCAP;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -55,37 +56,17 @@ __global__ void k_sync_route(Dev d, uint32_t b) {
       atomicOr(d.err, E_XCAP);
       continue;
     }
+    // the payload's chunk mask against base_row: the sender's dirty chunks, as of its copy-on-write if it made one
+    const uint64_t* dm = mm.payload == NEVER ? d.rdirty + lidx(d, mm.src) * d.MW : d.arena_dirty[b] + (size_t)mm.payload * d.MW;
     size_t e = (size_t)q * d.RQCAP + j;
     d.rq_list[e] = i;
-    d.rq_cnt[e] = 0;
-    for (uint32_t w = 0; w < d.MW; ++w) d.rq_mask[e * d.MW + w] = 0;
-  }
-}
-
-// chunk masks: which 2048-record chunks of each outbound payload differ (in key32) from the baseline row
-__global__ void __launch_bounds__(256) k_sync_dirty(Dev d, uint32_t b) {
-  const uint32_t q = blockIdx.y;
-  if (q == d.rank) return;
-  const uint32_t nq = min(d.rq_n[q], d.RQCAP);
-  for (uint32_t w = blockIdx.x; w < nq * d.NCHUNK; w += gridDim.x) {
-    const uint32_t j = w / d.NCHUNK, c = w % d.NCHUNK;
-    const size_t e = (size_t)q * d.RQCAP + j;
-    const SyncMsg& mm = d.msgs[b][d.rq_list[e]];
-    const uint32_t s0 = c * CH + threadIdx.x * 8;
-    bool diff = false;
-    if (s0 < d.NS) {
-      const uint4* pv = (const uint4*)(payload_row(d, mm, b) + s0);
-      const uint4* bv = (const uint4*)(d.base_row + s0);
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const uint4 a = pv[k], z = bv[k];
-        diff |= ((a.x ^ z.x) | (a.y ^ z.y) | (a.z ^ z.z) | (a.w ^ z.w)) != 0;
-      }
+    uint32_t nc = 0;
+    for (uint32_t w = 0; w < d.MW; ++w) {
+      const uint64_t x = dm[w];
+      d.rq_mask[e * d.MW + w] = x;
+      nc += __popcll(x);
     }
-    if (__syncthreads_or(diff) && threadIdx.x == 0) {
-      atomicOr((unsigned long long*)&d.rq_mask[e * d.MW + (c >> 6)], 1ull << (c & 63));
-      atomicAdd(&d.rq_cnt[e], 1u);
-    }
+    d.rq_cnt[e] = nc;
   }
 }
 

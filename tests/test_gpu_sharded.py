@@ -100,3 +100,20 @@ def test_sharded_kill_many_with_loss(oracle, engine):
         e.kill(victim)
     run_lockstep(o, e, 500, 100, "after kills W=2")
     e.close()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_sharded_c3_memory_fits(engine, world):
+    """C3 at the driver's N = 2/4/8: rank 0's share of a 100k-member cluster fits one MI355X (288 GB) with room to
+    spare. The gossip slot table is replicated, so the per-shard slot ranges split one budget; a full range per shard
+    would grow it W-fold (a 275 GB holder table on every GPU at W = 8)."""
+    from swimhip.shard import ShardedCluster, ThreadExchange
+    c = ShardedCluster(engine, SimConfig(n_members=100_000), 0, world, _abi.TRANSPORT_HOST,
+                       exchange=ThreadExchange(world).endpoint(0))
+    try:
+        nbytes = c.counters()["device_bytes"]
+    finally:
+        c.close()
+    assert nbytes < 216e9, (world, nbytes)
+    if world == 8:
+        assert nbytes < 120e9, nbytes
