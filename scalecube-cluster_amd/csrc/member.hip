@@ -615,8 +615,10 @@ __device__ __forceinline__ void merge_payload(ML& L, uint32_t mi, uint32_t reaso
 
 // Triage (k_member_triage): the idle fast path. Most members have nothing due in most ticks (a ping every 10 ticks,
 // a SYNC every 300); they only advance an empty gossip round here. Returns whether the member needs the full
-// control path of k_member_tick this tick.
-__device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t k) {
+// control path of k_member_tick this tick, and its work class: 1 = a ping is due and nothing else, 2 = only
+// request-state events (ping hops, ack arrivals, timeouts), 3 = both, 0 = anything else (SYNC receipt, gossip
+// receipts or round, timers, host requests, start).
+__device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t k, uint32_t& cls) {
   // A dead member does nothing itself, but the remote hops of its in-flight requests still run at the live
   // responders (their sends fail against the dead issuer), so those hops are still evaluated for the counters.
   // every word is loaded up front (no short-circuit chain of dependent loads); the SoA loads coalesce per wave
@@ -624,6 +626,7 @@ __device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t
                  ne = d.next_evt[m], tm = d.timerMin[m], np = d.nextPing[m], ns = d.nextSync[m], inf = d.initFlags[m],
                  ng = d.nextGossip[m], held = d.held[m], dt = d.dead_tick[m], st = d.start_tick[m];
   const bool dead = k >= dt;
+  cls = 0;
   if (dead) {
     d.rc_cnt[m] = 0;
     d.rc_fill[m] = 0;
@@ -631,6 +634,9 @@ __device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t
   } else {
     const bool busy = (k > 0 && mh != NEVER) | (rc != 0) | (pi != 0) | (ne <= k) | (tm <= k) | (k == np) | (k == ns) |
                       ((inf & INIT_ACTIVE) != 0) | (k == st);
+    const bool other = (k > 0 && mh != NEVER) | (rc != 0) | (pi != 0) | (tm <= k) | (k == ns) |
+                       ((inf & INIT_ACTIVE) != 0) | (k == st) | (k == ng && held != 0);
+    cls = other ? 0u : (k == np ? 1u : 0u) | (ne <= k ? 2u : 0u);
     if (!busy) {
       if (k != ng) {
         d.tround[m] = 0;
@@ -1112,29 +1118,46 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
 }
 
 // One launch per tick for member control. Each block triages its 256 members (the idle fast path, one thread per
-// member, unconditional coalesced loads) and compacts the busy ones into an LDS list with a block-local ballot
-// prefix (no atomics); its first waves then run the full control path for them, so no wave runs mostly idle lanes.
-// Counters are summed across the wave first: 10^4 pingers per tick adding to one word would serialise on that
-// address. With `flag` (W == 1) the block that finishes last runs the end-of-tick resets and raises the host flag.
+// member, unconditional coalesced loads) and places the busy ones in an LDS list grouped by work class, each class
+// starting on a wave boundary when they fit (block-local ballot prefixes, no atomics). Its waves then run the full
+// control path for them: a wave holds one kind of work, so it does not serialise the latency chains of a ping, a
+// ping hop and an ack arrival, and no wave runs mostly idle lanes. Counters are summed across the wave first: 10^4
+// pingers per tick adding to one word would serialise on that address. With `flag` (W == 1) the block that finishes
+// last runs the end-of-tick resets and raises the host flag.
 __global__ void __launch_bounds__(256) k_member_tick(const Dev* __restrict__ dp, uint32_t k, uint32_t flag) {
   const Dev& d = *dp;  // global, not kernarg: taking its address must not copy ~1 KB into per-lane scratch
-  __shared__ uint32_t wc[4];
+  __shared__ uint32_t wc[4][4];  // [wave][class] busy members
   __shared__ uint32_t list[256];
   __shared__ bool last;
   const uint32_t m = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
-  const bool busy = m < d.hi && member_triage(d, m, k);
-  const uint64_t bal = __ballot(busy);
+  uint32_t cls = 0;
+  const bool busy = m < d.hi && member_triage(d, m, k, cls);
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (lane == 0) wc[w] = (uint32_t)__popcll(bal);
+  const uint64_t b0 = __ballot(busy && cls == 0), b1 = __ballot(busy && cls == 1), b2 = __ballot(busy && cls == 2),
+                 b3 = __ballot(busy && cls == 3);
+  if (lane == 0) {
+    wc[w][0] = (uint32_t)__popcll(b0);
+    wc[w][1] = (uint32_t)__popcll(b1);
+    wc[w][2] = (uint32_t)__popcll(b2);
+    wc[w][3] = (uint32_t)__popcll(b3);
+  }
+  list[threadIdx.x] = NEVER;
   __syncthreads();
-  uint32_t base = 0;
-  for (uint32_t j = 0; j < w; ++j) base += wc[j];
-  if (busy) list[base + __popcll(bal & ((1ull << lane) - 1ull))] = m;
+  uint32_t aligned = 0, dense = 0, all = 0, before = 0;
+  for (uint32_t c = 0; c < 4; ++c) {
+    const uint32_t t = wc[0][c] + wc[1][c] + wc[2][c] + wc[3][c];
+    all += (t + 63u) & ~63u;
+    if (c < cls) aligned += (t + 63u) & ~63u, dense += t;
+  }
+  const uint32_t start = all <= 256 ? aligned : dense;  // classes on wave boundaries when they fit, else packed
+  for (uint32_t j = 0; j < w; ++j) before += wc[j][cls];
+  const uint64_t bal = cls == 0 ? b0 : cls == 1 ? b1 : cls == 2 ? b2 : b3;
+  if (busy) list[start + before + __popcll(bal & ((1ull << lane) - 1ull))] = m;
   __syncthreads();
-  const uint32_t nb = wc[0] + wc[1] + wc[2] + wc[3];
-  if ((threadIdx.x & ~63u) < nb) {  // waves wholly past the busy list skip to the end
+  const uint32_t me = list[threadIdx.x];
+  if (__ballot(me != NEVER)) {  // waves with no busy member skip to the end
     unsigned long long cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (threadIdx.x < nb) member_tick_body(d, list[threadIdx.x], k, cnt);
+    if (me != NEVER) member_tick_body(d, me, k, cnt);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       unsigned long long v = cnt[i];
