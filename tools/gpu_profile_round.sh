@@ -5,9 +5,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/round
 mkdir -p $O
-timeout -k 10 300 python -u bench.py --steps 20 --warmup 2 --no-cpu-baseline > $O/bench_spin.log 2>&1
-SWIM_BLOCKING_WAIT=1 timeout -k 10 300 python -u bench.py --steps 20 --warmup 2 --no-cpu-baseline > $O/bench_block.log 2>&1
-echo "spin: $(grep -o '"ms_per_step": [0-9.]*' $O/bench_spin.log) block: $(grep -o '"ms_per_step": [0-9.]*' $O/bench_block.log)"
+
 timeout -k 10 600 python -u bench.py > $O/bench.log 2>&1
 grep metric $O/bench.log > $O/bench.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 bench.py --steps 30 --warmup 3 --no-cpu-baseline > $O/trace_bench.log 2>&1
