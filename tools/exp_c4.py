@@ -1,0 +1,32 @@
+"""C4-shaped: N members PRECONVERGED, two halves blocked both ways from period 0, unblockAll at period
+`heal`, run to period `end`; prints wall time per 20-period chunk and the counters (gossip created, events)."""
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "scalecube-cluster_amd"))
+import swimhip  # noqa: E402
+from swimhip import ClusterConfig, SimConfig  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
+heal = int(sys.argv[2]) if len(sys.argv) > 2 else 200
+end = int(sys.argv[3]) if len(sys.argv) > 3 else 320
+slots = int(sys.argv[4]) if len(sys.argv) > 4 else 1 << 20  # the DEAD-gossip storm needs far more than 64 per member
+c = swimhip.cluster(SimConfig(n_members=n, cluster=ClusterConfig(seedMembers=[0]), gossip_slot_cap=slots))
+c.partition([0] * (n // 2) + [1] * (n - n // 2))
+p, t_all = 0, time.perf_counter()
+while p < end:
+    if p == heal:
+        c.unblock_all()
+    step = min(20, (heal if p < heal else end) - p)
+    t0 = time.perf_counter()
+    c.run_periods(step)
+    c.sync()
+    dt = time.perf_counter() - t0
+    p += step
+    ctr = c.counters()
+    print(f"N={n} periods {p - step}-{p}: {dt / step * 1e3:.1f} ms/period, created {ctr['gossips_created']}, "
+          f"events {ctr['events']}, G {ctr['gossip_messages']}", flush=True)
+print(f"N={n} total {time.perf_counter() - t_all:.1f} s for {end} periods", flush=True)
+c.close()
