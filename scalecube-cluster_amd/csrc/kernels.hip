@@ -291,45 +291,64 @@ __global__ void __launch_bounds__(256) k_seg_sort(uint64_t* key, uint32_t* val, 
 // :456-467). This is the HBM-bound hot loop: 2 x 4 B read per subject per merge (key32, swim_common.h). SHARDED adds
 // payloads received from other shards (baseline row + shipped chunks); the single-GPU instance has only local rows
 // and snapshots.
+// this lane's 8 payload keys and 8 receiver keys of work item w (message w / NCHUNK, chunk w % NCHUNK): the payload
+// is the sender's live row or its copy-on-write snapshot; for a payload received from another shard, the shipped
+// chunk if it differs from the baseline, else the baseline
+template <bool SHARDED>
+__device__ __forceinline__ void diff_fetch(const Dev& d, uint32_t b, uint32_t w, uint4 (&x)[4]) {
+  const uint32_t mi = w / d.NCHUNK, c = w % d.NCHUNK;
+  const SyncMsg& mm = d.msgs[b][mi];
+  const uint32_t s0 = c * CH + threadIdx.x * 8;
+  if (s0 >= d.NS) {  // NS is a multiple of 8: a 32-B group is wholly in or out; padding entries are 0 (absent)
+    x[0] = x[1] = x[2] = x[3] = make_uint4(0, 0, 0, 0);
+    return;
+  }
+  const uint32_t* p8;
+  if (mm.payload == NEVER) {
+    p8 = d.rowk + lidx(d, mm.src) * d.NS + s0;
+  } else if (SHARDED && (mm.payload & PAY_RX)) {
+    const uint32_t ri = mm.payload & ~PAY_RX;
+    const uint64_t* mk = d.rx_mask + (size_t)ri * d.MW;
+    if ((mk[c >> 6] >> (c & 63)) & 1ull) {
+      uint32_t rank = __popcll(mk[c >> 6] & ((1ull << (c & 63)) - 1ull));
+      for (uint32_t q = 0; q < (c >> 6); ++q) rank += __popcll(mk[q]);
+      p8 = (const uint32_t*)(d.xa_recv + d.rx_off[ri]) + (size_t)rank * CH + threadIdx.x * 8;
+    } else {
+      p8 = d.base_row + s0;
+    }
+  } else {
+    p8 = d.arena[b] + (size_t)mm.payload * d.NS + s0;
+  }
+  const uint32_t* r8 = d.rowk + lidx(d, mm.dst) * d.NS + s0;
+  // (non-temporal loads measured 1.5x slower here on gfx950)
+  x[0] = ld_c4(p8);
+  x[1] = ld_c4(p8 + 4);
+  x[2] = ld_c4(r8);
+  x[3] = ld_c4(r8 + 4);
+}
+
+// k_sync_diff: for every SYNC / SYNC_ACK sent in tick k-1, stream the payload's key plane (the sender's live row,
+// or its copy-on-write snapshot) against the receiver's key plane and extract, per 2048-subject chunk and in
+// subject order, the records that differ (the eager `!r1.equals(table.get(id))` filter of syncMembership,
+// :456-467). This is the HBM-bound hot loop: 2 x 4 B read per subject per merge (key32, swim_common.h). Each block
+// walks its work items grid-strided with the next item's loads in flight while it tests the current one. SHARDED
+// adds payloads received from other shards (baseline row + shipped chunks); the single-GPU instance has only local
+// rows and snapshots.
 template <bool SHARDED>
 __global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b) {
   __shared__ uint32_t scan[256];
   __shared__ uint32_t base;
   uint32_t nmsg = d.nmsg[b] < d.MSGCAP ? d.nmsg[b] : d.MSGCAP;
   uint32_t total = nmsg * d.NCHUNK;
+  uint4 cur[4];
+  if (blockIdx.x < total) diff_fetch<SHARDED>(d, b, blockIdx.x, cur);
   for (uint32_t w = blockIdx.x; w < total; w += gridDim.x) {
-    uint32_t mi = w / d.NCHUNK, c = w % d.NCHUNK;
-    const SyncMsg& mm = d.msgs[b][mi];
+    uint4 nxt[4];
+    if (w + gridDim.x < total) diff_fetch<SHARDED>(d, b, w + gridDim.x, nxt);
+    const uint32_t mi = w / d.NCHUNK, c = w % d.NCHUNK;
     const uint32_t s0 = c * CH + threadIdx.x * 8;
-    // this lane's 8 payload keys: the sender's live row or its copy-on-write snapshot; for a payload received
-    // from another shard, the shipped chunk if it differs from the baseline, else the baseline
-    const uint32_t* p8;
-    if (mm.payload == NEVER) {
-      p8 = d.rowk + lidx(d, mm.src) * d.NS + s0;
-    } else if (SHARDED && (mm.payload & PAY_RX)) {
-      const uint32_t ri = mm.payload & ~PAY_RX;
-      const uint64_t* mk = d.rx_mask + (size_t)ri * d.MW;
-      if ((mk[c >> 6] >> (c & 63)) & 1ull) {
-        uint32_t rank = __popcll(mk[c >> 6] & ((1ull << (c & 63)) - 1ull));
-        for (uint32_t q = 0; q < (c >> 6); ++q) rank += __popcll(mk[q]);
-        p8 = (const uint32_t*)(d.xa_recv + d.rx_off[ri]) + (size_t)rank * CH + threadIdx.x * 8;
-      } else {
-        p8 = d.base_row + s0;
-      }
-    } else {
-      p8 = d.arena[b] + (size_t)mm.payload * d.NS + s0;
-    }
-    const uint32_t* rcv = d.rowk + lidx(d, mm.dst) * d.NS;
-    uint32_t p[8], r[8];
-    if (s0 < d.NS) {  // NS is a multiple of 8: the 32-B group is in bounds, padding entries are 0 (absent)
-      // (non-temporal loads measured 1.5x slower here on gfx950)
-      const uint4 a0 = ld_c4(p8), a1 = ld_c4(p8 + 4), q0 = ld_c4(rcv + s0), q1 = ld_c4(rcv + s0 + 4);
-      p[0] = a0.x, p[1] = a0.y, p[2] = a0.z, p[3] = a0.w, p[4] = a1.x, p[5] = a1.y, p[6] = a1.z, p[7] = a1.w;
-      r[0] = q0.x, r[1] = q0.y, r[2] = q0.z, r[3] = q0.w, r[4] = q1.x, r[5] = q1.y, r[6] = q1.z, r[7] = q1.w;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) p[j] = r[j] = 0;
-    }
+    const uint32_t p[8] = {cur[0].x, cur[0].y, cur[0].z, cur[0].w, cur[1].x, cur[1].y, cur[1].z, cur[1].w};
+    const uint32_t r[8] = {cur[2].x, cur[2].y, cur[2].z, cur[2].w, cur[3].x, cur[3].y, cur[3].z, cur[3].w};
     uint32_t mask = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j)
@@ -341,38 +360,40 @@ __global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b) {
         cm[0] = 0;
         cm[1] = 0;
       }
-      continue;
-    }
-    scan[threadIdx.x] = nc;
-    __syncthreads();
-    for (uint32_t o = 1; o < 256; o <<= 1) {
-      uint32_t v = threadIdx.x >= o ? scan[threadIdx.x - o] : 0;
+    } else {
+      scan[threadIdx.x] = nc;
       __syncthreads();
-      scan[threadIdx.x] += v;
-      __syncthreads();
-    }
-    uint32_t incl = scan[threadIdx.x];
-    uint32_t totc = scan[255];
-    if (threadIdx.x == 0) {
-      uint32_t bo = atomicAdd(d.pool_used, totc);
-      if (bo + totc > d.POOLCAP) {
-        atomicOr(d.err, E_POOL);
-        totc = 0;
-        bo = 0;
+      for (uint32_t o = 1; o < 256; o <<= 1) {
+        uint32_t v = threadIdx.x >= o ? scan[threadIdx.x - o] : 0;
+        __syncthreads();
+        scan[threadIdx.x] += v;
+        __syncthreads();
       }
-      base = bo;
-      uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NCHUNK + c) * 2;
-      cm[0] = bo;
-      cm[1] = totc;
-      if (totc) atomicAdd(&d.msgs[b][mi].ncand, totc);
-    }
-    __syncthreads();
-    uint32_t o = base + incl - nc;
-    if (o + nc <= d.POOLCAP)
+      uint32_t incl = scan[threadIdx.x];
+      uint32_t totc = scan[255];
+      if (threadIdx.x == 0) {
+        uint32_t bo = atomicAdd(d.pool_used, totc);
+        if (bo + totc > d.POOLCAP) {
+          atomicOr(d.err, E_POOL);
+          totc = 0;
+          bo = 0;
+        }
+        base = bo;
+        uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NCHUNK + c) * 2;
+        cm[0] = bo;
+        cm[1] = totc;
+        if (totc) atomicAdd(&d.msgs[b][mi].ncand, totc);
+      }
+      __syncthreads();
+      uint32_t o = base + incl - nc;
+      if (o + nc <= d.POOLCAP)
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (mask & (1u << j)) d.pool[o++] = ((uint64_t)(s0 + j) << 34) | key34(p[j]);
-    __syncthreads();
+        for (int j = 0; j < 8; ++j)
+          if (mask & (1u << j)) d.pool[o++] = ((uint64_t)(s0 + j) << 34) | key34(p[j]);
+      __syncthreads();
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
   }
 }
 
