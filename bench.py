@@ -187,8 +187,10 @@ def main():
         merges = d["sync_merges"]
         diff_s = d["diff_ns"] * 1e-9
         launches = max(1, d["diff_launches"])
-        bytes_per_launch = 8.0 * n * merges / launches  # payload keys + receiver keys, 4 B each per subject
-        achieved = (8.0 * n * merges) / diff_s / 1e9 if diff_s > 0 else 0.0
+        # one GPU: the engine times every 5th tick's k_sync_diff and counts the payloads those launches streamed
+        timed_msgs = d["diff_msgs"] if world == 1 else merges
+        bytes_per_launch = 8.0 * n * timed_msgs / launches  # payload keys + receiver keys, 4 B each per subject
+        achieved = (8.0 * n * timed_msgs) / diff_s / 1e9 if diff_s > 0 else 0.0
         # whole-step algorithmic bytes, SURVEY.md §8d with 4-B record keys: B = 8R + 8W + 32M + 0.375G + 24E
         B = 8 * d["record_compares"] + 8 * d["row_writes"] + 32 * d["messages"] + 0.375 * d["gossip_messages"] + 24 * d["events"]
         line = {
@@ -212,7 +214,7 @@ def main():
                          "algorithmic_bytes_per_launch": bytes_per_launch,
                          "avg_launch_us": diff_s * 1e6 / launches,
                          "traffic": traffic_from_profiles(n) if world == 1 else None},
-            "kernel_time_share": {"k_sync_diff": diff_s / dt},  # the other kernels: profiles/*kernel_stats*
+            "kernel_time_share": {"k_sync_diff": diff_s / launches * 10 * a.steps / dt},  # the other kernels: profiles/*kernel_stats*
             "whole_step_algorithmic_GBps": B / dt / 1e9,
             "counters": {k: d[k] for k in ("record_compares", "row_writes", "messages", "gossip_messages", "events",
                                            "sync_merges")},

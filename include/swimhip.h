@@ -124,7 +124,7 @@ typedef struct swim_counters {
   uint64_t gossip_ns;     /* k_gossip_send: gossip data plane */
   uint64_t diff_launches;
   uint64_t exchange_ns; /* sharded handles: host time spent in the per-tick shard exchanges */
-  uint64_t reserved[1];
+  uint64_t diff_msgs;   /* SYNC / SYNC_ACK payloads streamed by the timed k_sync_diff launches (diff_launches) */
 } swim_counters;
 
 typedef struct swim_handle swim_handle;

@@ -579,6 +579,8 @@ int swim_destroy(swim_handle* h) {
   return SWIM_OK;
 }
 
+constexpr uint64_t DIFF_SAMPLE = 5;
+
 int swim_step(swim_handle* h, uint32_t n) {
   if (!h) return SWIM_EINVAL;
   hipSetDevice((int)h->cfg.device);
@@ -593,8 +595,13 @@ int swim_step(swim_handle* h, uint32_t n) {
     }
   uint64_t first = h->tick;
   const Dev& d = h->d;
+  // W == 1 with SWIM_FLAG_PROFILE: only every DIFF_SAMPLE-th tick's k_sync_diff is bracketed by events (each event
+  // pair costs ~6.7 us of GPU time per tick); the timed launches count their own messages (diff_msgs)
+  auto timed = [&](uint64_t kk) {
+    return profile && ((h->cfg.flags & SWIM_FLAG_PROFILE_ALL) || d.W > 1 || kk % DIFF_SAMPLE == 0);
+  };
   for (uint32_t i = 0; i < n; ++i) {
-    const TickEvents* te = profile ? &h->prof[i] : nullptr;
+    const TickEvents* te = timed(h->tick) ? &h->prof[i] : nullptr;
     const uint32_t k = (uint32_t)h->tick;
     // P0 gossip creations before the member kernel: RUMOR-mode churn rumors, then the user gossips queued by the host
     if (d.churn && k % d.ping_t == 0) launch_churn(d, k, h->stream);
@@ -616,7 +623,7 @@ int swim_step(swim_handle* h, uint32_t n) {
       launch_member(d, k, h->stream, te);
       HIPCK(hipEventRecord(h->ev_member, h->stream));
       const bool pipe = i + 1 < n && !h->no_pipe;
-      if (pipe) launch_diff(d, k + 1, h->stream, profile ? &h->prof[i + 1] : nullptr);  // overlaps the wait
+      if (pipe) launch_diff(d, k + 1, h->stream, timed(k + 1ull) ? &h->prof[i + 1] : nullptr);  // overlaps the wait
       HIPCK(hipEventSynchronize(h->ev_member));  // (a spin wait measured the same here: diff(k+1) hides the wake-up)
       if (h->hflag[0] != 0 || h->no_skip) {
         launch_gossip(d, k, h->stream, te);
@@ -645,6 +652,7 @@ int swim_step(swim_handle* h, uint32_t n) {
   if (rc == SWIM_OK && profile) {
     for (uint32_t i = 0; i < n; ++i) {
       float ms = 0;
+      if (!timed(first + i)) continue;
       if (first + i > 0) {
         HIPCK(hipEventElapsedTime(&ms, (hipEvent_t)h->prof[i].ev[0], (hipEvent_t)h->prof[i].ev[1]));
         h->prof_ms[0] += ms;
@@ -932,6 +940,7 @@ int swim_counters_get(swim_handle* h, swim_counters* out) {
   out->member_ns = (uint64_t)(h->prof_ms[1] * 1e6);
   out->gossip_ns = (uint64_t)(h->prof_ms[2] * 1e6);
   out->diff_launches = h->prof_diff_launches;
+  out->diff_msgs = c[C_DIFFMSG];
   out->exchange_ns = (uint64_t)(h->xchg_ms * 1e6);
   return SWIM_OK;
 }

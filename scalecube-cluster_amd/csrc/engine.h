@@ -51,7 +51,7 @@ constexpr unsigned long long XCNT_MASK = (1ull << 48) - 1, XFLAG_GOSSIP = 1ull <
 constexpr uint32_t XINL = 16384;  // RCCL: bytes per peer moved by the fixed-size all-to-all (count word + region head)
 
 // counters (swim_counters order after .tick)
-enum Ctr { C_R = 0, C_W, C_M, C_G, C_E, C_LOST, C_GCREATED, C_SYNCMERGE, C_NCTR = 16 };
+enum Ctr { C_R = 0, C_W, C_M, C_G, C_E, C_LOST, C_GCREATED, C_SYNCMERGE, C_DIFFMSG = 13, C_NCTR = 16 };  // 8..12: SWIM_EXP & 4
 
 struct SyncMsg {
   uint32_t src, dst, kind, seq, cid_iss, cid_cnt;

@@ -335,10 +335,11 @@ __device__ __forceinline__ void diff_fetch(const Dev& d, uint32_t b, uint32_t w,
 // adds payloads received from other shards (baseline row + shipped chunks); the single-GPU instance has only local
 // rows and snapshots.
 template <bool SHARDED>
-__global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b) {
+__global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b, uint32_t timed) {
   __shared__ uint32_t scan[256];
   __shared__ uint32_t base;
   uint32_t nmsg = d.nmsg[b] < d.MSGCAP ? d.nmsg[b] : d.MSGCAP;
+  if (timed && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&d.ctr[C_DIFFMSG], (unsigned long long)nmsg);
   uint32_t total = nmsg * d.NCHUNK;
   uint4 cur[4];
   if (blockIdx.x < total) diff_fetch<SHARDED>(d, b, blockIdx.x, cur);
@@ -1005,11 +1006,12 @@ void launch_init(const Dev& d, void* stream) {
   if (d.W > 1) hipLaunchKernelGGL(k_init_base, dim3(cdiv(d.NS, 256)), dim3(256), 0, st, d);
 }
 
-static void launch_sync_diff(const Dev& d, uint32_t b, hipStream_t st) {
+// timed: this launch is bracketed by profiling events; it adds its message count to ctr[C_DIFFMSG]
+static void launch_sync_diff(const Dev& d, uint32_t b, hipStream_t st, uint32_t timed) {
   if (d.W > 1)
-    hipLaunchKernelGGL(k_sync_diff<true>, dim3(2048), dim3(256), 0, st, d, b);
+    hipLaunchKernelGGL(k_sync_diff<true>, dim3(2048), dim3(256), 0, st, d, b, timed);
   else
-    hipLaunchKernelGGL(k_sync_diff<false>, dim3(2048), dim3(256), 0, st, d, b);
+    hipLaunchKernelGGL(k_sync_diff<false>, dim3(2048), dim3(256), 0, st, d, b, timed);
 }
 
 // single GPU: the tick is cut in three so that the host can hold back the gossip data plane when no slot is in
@@ -1017,7 +1019,7 @@ static void launch_sync_diff(const Dev& d, uint32_t b, hipStream_t st) {
 void launch_diff(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
   hipStream_t st = (hipStream_t)stream;
   if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
-  if (k > 0) launch_sync_diff(d, (k - 1) & 1, st);
+  if (k > 0) launch_sync_diff(d, (k - 1) & 1, st, prof ? 1u : 0u);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
 }
 
@@ -1065,7 +1067,7 @@ void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   hipStream_t st = (hipStream_t)stream;
   uint32_t b = k & 1, pb = (k - 1) & 1;
   if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
-  if (k > 0) launch_sync_diff(d, pb, st);
+  if (k > 0) launch_sync_diff(d, pb, st, prof ? 1u : 0u);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[2], st);
   hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k, 0u);

@@ -88,7 +88,7 @@ class SwimCounters(C.Structure):
         ("gossip_ns", C.c_uint64),
         ("diff_launches", C.c_uint64),
         ("exchange_ns", C.c_uint64),
-        ("reserved", C.c_uint64 * 1),
+        ("diff_msgs", C.c_uint64),
     ]
 
     def as_dict(self):
