@@ -47,7 +47,7 @@ out = {
     "source_files": [f"{tag}_pmc_fetch_size_sync_diff.csv", f"{tag}_pmc_write_size_sync_diff.csv",
                      f"{tag}_kernel_stats_c3_100k.csv"],
 }
-(prof / "pmc_sync_diff.json").write_text(json.dumps(out, indent=1))
+(prof / "pmc_sync_diff_k32.json").write_text(json.dumps(out, indent=1))
 shutil.copy(next((src / "pmc_fetch").rglob("*counter_collection.csv")), prof / f"{tag}_pmc_fetch_size_sync_diff.csv")
 shutil.copy(next((src / "pmc_write").rglob("*counter_collection.csv")), prof / f"{tag}_pmc_write_size_sync_diff.csv")
 shutil.copy(stats, prof / f"{tag}_kernel_stats_c3_100k.csv")
