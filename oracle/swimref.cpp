@@ -17,6 +17,7 @@
 // is pinned by its closed forms. Event ordering and timing are pinned only by SEMANTICS.md, which makes parity for
 // them "spec-pinned", not reference-pinned.
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -31,6 +32,7 @@
 #include <vector>
 
 #include "../include/swimhip.h"
+#include "../include/swimhip_selftest.h"
 #include "rng.h"
 
 using namespace swimref;
@@ -233,6 +235,7 @@ struct Member {
   void do_finally(uint32_t subj, Rec r1, int reason);
   void fetch(uint32_t subj, Rec r1, int reason, bool added, int group, uint64_t k);
   void sync_membership(const Payload& p, int reason, int group, uint64_t k);
+  const std::vector<Rec>* tickStart = nullptr;  // SWIMREF_DEBUG: the table at the start of P1 (several payloads)
   void complete_group(int g, uint64_t k);
   void on_fd_event(uint32_t target, uint8_t status, uint64_t k);
   void ping_req_step(uint32_t target, uint32_t cnt, uint64_t k);
@@ -261,6 +264,10 @@ struct Sim {
   swim_counters ctr;
   std::string err;
   int threads = 1;  // SWIMREF_THREADS
+  // debugging aid (SWIMREF_DEBUG=1): payload records that equal the receiver's start-of-tick row but differ from its
+  // live row when a later SYNC / SYNC_ACK of the same tick is merged ([0]), and those of them that override it ([1])
+  bool debug = false;
+  std::atomic<uint64_t> dbg[4] = {};
   std::vector<Lane> lanes;
   std::unique_ptr<Pool> pool;
 
@@ -500,6 +507,12 @@ void Member::sync_membership(const Payload& p, int reason, int group, uint64_t k
   std::vector<std::pair<uint32_t, Rec>> diff;
   for (auto& e : p)
     if (e.second != table[e.first]) diff.push_back(e);
+  if (tickStart)
+    for (auto& e : diff)
+      if (e.second == (*tickStart)[e.first]) {
+        sim->dbg[0]++;
+        if (is_overrides(e.second, table[e.first])) sim->dbg[1]++;
+      }
   for (auto& e : diff) update_membership(e.first, e.second, reason, group, k);
 }
 
@@ -733,6 +746,11 @@ void Member::process(uint64_t k, std::vector<Msg>& inbox) {
   }
   // ---- P1 SYNC / SYNC_ACK (onMessage :320-331, onSync :346-367, onSyncAck :337-343) ----
   std::sort(syncm.begin(), syncm.end(), [](Msg* a, Msg* b) { return a->src != b->src ? a->src < b->src : a->seq < b->seq; });
+  std::vector<Rec> startTable;
+  if (s.debug && syncm.size() > 1) {
+    startTable = table;
+    tickStart = &startTable;
+  }
   for (Msg* m : syncm) {
     if (m->kind == K_SYNC) {
       int g = nextGroup++;
@@ -751,6 +769,7 @@ void Member::process(uint64_t k, std::vector<Msg>& inbox) {
       finish(g, false, k);
     }
   }
+  tickStart = nullptr;
   // ---- P2 FD (onMessage :219-227) ----
   std::sort(fdm.begin(), fdm.end(), [](Msg* a, Msg* b) { return fd_less(*a, *b); });
   for (Msg* m : fdm) {
@@ -1032,6 +1051,7 @@ __attribute__((visibility("default"))) int swim_create(const swim_config* cfg, s
   if (c.mode > SWIM_MODE_RUMOR || (c.mode == SWIM_MODE_RUMOR && c.init_mode != SWIM_INIT_PRECONVERGED)) return SWIM_EINVAL;
   if (c.n_dormant > c.n_members || (c.n_dormant && c.init_mode != SWIM_INIT_COLD_JOIN)) return SWIM_EINVAL;
   auto* h = new swim_handle();
+  h->sim.debug = getenv("SWIMREF_DEBUG") != nullptr;
   if (const char* th = getenv("SWIMREF_THREADS")) h->sim.threads = std::max(1, std::min(256, atoi(th)));
   if (h->sim.threads > 1) {
     h->sim.pool.reset(new Pool());
@@ -1247,6 +1267,39 @@ __attribute__((visibility("default"))) int swim_state_hash(swim_handle* h, uint6
     out[6 * m + 5] = misc;
   }
   return SWIM_OK;
+}
+
+// include/swimhip_selftest.h: the oracle's own functions on caller inputs (the engine runs its device code)
+__attribute__((visibility("default"))) int swim_selftest_eval(uint32_t op, const uint32_t* in, uint32_t* out, size_t n,
+                                                              uint32_t device) {
+  (void)device;
+  if (op > SWIM_SELFTEST_CLUSTER_MATH || (n && (!in || !out))) return SWIM_EINVAL;
+  for (size_t i = 0; i < n; ++i) {
+    if (op == SWIM_SELFTEST_OVERRIDES) {
+      const uint32_t* a = in + 4 * i;
+      out[i] = is_overrides(Rec{(uint8_t)a[0], a[1]}, Rec{(uint8_t)a[2], a[3]}) ? 1u : 0u;
+    } else if (op == SWIM_SELFTEST_PHILOX) {
+      const uint32_t* a = in + 6 * i;
+      const P4 r = philox4x32_10(a[0], a[1], a[2], a[3], a[4], a[5]);
+      for (int j = 0; j < 4; ++j) out[4 * i + j] = r.v[j];
+    } else {
+      const uint32_t* a = in + 4 * i;
+      Sim s;  // the ClusterMath restatements the simulation uses (Sim::spread_of / sweep_of / suspicion_ticks)
+      s.cfg.gossip_repeat_mult = a[1];
+      s.cfg.suspicion_mult = a[2];
+      s.ping_t = a[3];
+      out[4 * i] = bitlen(a[0]);
+      out[4 * i + 1] = s.spread_of(a[0]);
+      out[4 * i + 2] = s.sweep_of(a[0]);
+      out[4 * i + 3] = s.suspicion_ticks(a[0]);
+    }
+  }
+  return SWIM_OK;
+}
+
+// debugging aid (not in the ABI header): SWIMREF_DEBUG counters (Sim::dbg)
+__attribute__((visibility("default"))) uint64_t swimdbg_counter(swim_handle* h, uint32_t i) {
+  return h && i < 4 ? h->sim.dbg[i].load() : 0;
 }
 
 // debugging aid (not in the ABI header): the scalar fields folded into the "misc" state-hash word

@@ -107,13 +107,52 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* ctr) {
   return base + rank;
 }
 
+// A receiver with several SYNC / SYNC_ACK payloads in one tick reads the later ones' records for the subjects an
+// earlier one changed (member.hip, merge_payload), after their senders may have written their live rows again:
+// such a live-row payload gets an arena row that k_sync_diff fills with its keys. A lost CAS race wastes a row.
+__device__ __forceinline__ void pin_msg(const Dev& d, uint32_t b, uint32_t j) {
+  uint32_t* p = &d.msgs[b][j].pin;
+  if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != NEVER) return;
+  const uint32_t r = atomicAdd(&d.arena_used[b], 1u);
+  if (r >= d.ARENA_ROWS) {
+    set_err(d, E_ARENA);
+    return;
+  }
+  atomicCAS(p, NEVER, r);
+}
+
+// key32 of subject s in payload mm (messages of buffer b): its copy-on-write snapshot, its pinned copy, or a
+// payload received from another shard (shipped chunk or baseline row). Only for payloads that are immutable now.
+__device__ __forceinline__ uint32_t payload_key_at(const Dev& d, const SyncMsg& mm, uint32_t b, uint32_t s) {
+  if (mm.payload == NEVER) {
+    if (mm.pin == NEVER) {
+      set_err(d, E_PIN);
+      return 0;
+    }
+    return d.arena[b][(size_t)mm.pin * d.NS + s];
+  }
+  if (mm.payload & PAY_RX) {
+    const uint32_t ri = mm.payload & ~PAY_RX, c = s / CH;
+    const uint64_t* mk = d.rx_mask + (size_t)ri * d.MW;
+    if (!((mk[c >> 6] >> (c & 63)) & 1ull)) return d.base_row[s];
+    uint32_t rank = __popcll(mk[c >> 6] & ((1ull << (c & 63)) - 1ull));
+    for (uint32_t q = 0; q < (c >> 6); ++q) rank += __popcll(mk[q]);
+    return ((const uint32_t*)(d.xa_recv + d.rx_off[ri]))[(size_t)rank * CH + s % CH];
+  }
+  return d.arena[b][(size_t)mm.payload * d.NS + s];
+}
+
 __device__ __forceinline__ uint32_t rounds_before(const Dev& d, uint32_t x, uint32_t c) {
   uint32_t f = d.firstGossip[x];
   if (f == NEVER || c <= f) return 0;
   return (c - f + d.gossip_t - 1) / d.gossip_t;
 }
 
+// ClusterMath (ClusterMath.java:99-125): gossipPeriodsToSpread, gossipPeriodsToSweep (from the spread), and
+// suspicionTimeout in ticks; swim_selftest_eval exposes these exact functions for the known-answer tests
 __device__ __forceinline__ uint32_t spread_of(const Dev& d, uint32_t cluster) { return d.repeatMult * bitlen(cluster); }
+__device__ __forceinline__ uint32_t sweep_after(uint32_t spread) { return 2u * (spread + 1u); }
+__device__ __forceinline__ uint32_t suspicion_ticks(const Dev& d, uint32_t size) { return d.suspMult * bitlen(size) * d.ping_t; }
 
 // member m swept gossip slot g at tick k: if g is m's own leave notification, leaveCluster completes and
 // ClusterImpl.doShutdown stops the member (ClusterImpl.java:305-313, GossipProtocolImpl.java:296-306); it is dead

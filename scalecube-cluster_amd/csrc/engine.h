@@ -20,6 +20,7 @@ constexpr uint32_t NEVER = 0xFFFFFFFFu;
 constexpr uint32_t MAX_EPOCHS = 8;
 constexpr uint32_t SUBCAP = 8, PATHCAP = 8, FREC = 8, GREC = 8;
 constexpr uint32_t CH = 2048;  // subjects per SYNC-diff work item (256 threads x 8)
+constexpr uint32_t TRK = 16;   // subjects written in one tick's P1 that are re-checked against later payloads
 
 // S entry flags (gossip slot x member)
 constexpr uint32_t S_PENDING = 1u << 29, S_SWEPT = 1u << 30, S_REBORN = 1u << 31;
@@ -30,7 +31,8 @@ constexpr uint32_t E_SLOTS = 1, E_FETCH = 2, E_SUBS = 4, E_PATHS = 8, E_GROUPS =
                    E_POOL = 128, E_LIST = 256, E_DELIV = 512, E_RECEIPTS = 1024, E_CONTACTS = 2048,
                    E_REBORN = 4096, E_LOGWIN = 8192, E_EPOCH = 16384, E_EVENTS = 32768, E_SORTCAP = 65536,
                    E_XCAP = 1u << 17, E_LINKHIST = 1u << 18, E_DEATHS = 1u << 19,
-                   E_INC = 1u << 20;  // an incarnation >= 2^30 would not fit the key plane (swim_common.h)
+                   E_INC = 1u << 20,  // an incarnation >= 2^30 would not fit the key plane (swim_common.h)
+                   E_PIN = 1u << 21;  // a later SYNC payload of a receiver's tick had no readable copy (pin)
 // per-link NetworkEmulator settings (setLinkSettings / block / unblock): hash of (src, dst) -> change history
 constexpr uint32_t LKCAP = 4096, LKH = 8;  // keys, history entries per key
 constexpr uint32_t DEATHCAP = 4096;        // completed leaves per tick
@@ -59,6 +61,10 @@ struct SyncMsg {
   uint32_t psize;    // records in the payload = the sender's table size when it sent
   uint32_t ncand;    // filled by k_sync_diff: payload records that differ from the receiver's row
   uint32_t pad;
+  // arena row that k_sync_diff fills with a copy of a live-row payload (NEVER: none). Set when the receiver has
+  // several SYNC / SYNC_ACK payloads in one tick: the member kernel then reads later payloads' records directly (the
+  // sender may write its live row meanwhile), for the subjects an earlier payload of that tick changed
+  uint32_t pin;
 };
 
 struct Dev {
@@ -154,6 +160,7 @@ struct Dev {
   uint32_t *deaths, *deaths_n;  // [2][DEATHCAP], [2]: members whose leave completed at tick k (parity k & 1)
   uint32_t* next_evt; // [N] earliest tick at which a pending path / subscription / fetch needs the member
   uint32_t* mdone;  // finished k_member_tick blocks this tick (the last one runs the end-of-tick resets)
+  uint32_t* trk;    // [NL][TRK] per receiver: subjects its row changed earlier in this tick's P1 (member.hip)
   uint32_t* chunk_meta;                      // [MSGCAP][NCHUNK][2] (pool offset, count)
   uint64_t* pool;                            // candidate (subject << 34 | key)
   uint32_t* pool_used;

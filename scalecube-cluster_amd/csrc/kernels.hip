@@ -348,6 +348,12 @@ __global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b, uint32_t t
     if (w + gridDim.x < total) diff_fetch<SHARDED>(d, b, w + gridDim.x, nxt);
     const uint32_t mi = w / d.NCHUNK, c = w % d.NCHUNK;
     const uint32_t s0 = c * CH + threadIdx.x * 8;
+    const uint32_t pin = d.msgs[b][mi].pin;
+    if (pin != NEVER && d.msgs[b][mi].payload == NEVER && s0 < d.NS) {  // a live-row payload read again later (pin_msg)
+      uint4* dst = (uint4*)(d.arena[b] + (size_t)pin * d.NS + s0);
+      dst[0] = cur[0];
+      dst[1] = cur[1];
+    }
     const uint32_t p[8] = {cur[0].x, cur[0].y, cur[0].z, cur[0].w, cur[1].x, cur[1].y, cur[1].z, cur[1].w};
     const uint32_t r[8] = {cur[2].x, cur[2].y, cur[2].z, cur[2].w, cur[3].x, cur[3].y, cur[3].z, cur[3].w};
     uint32_t mask = 0;
@@ -478,7 +484,7 @@ __device__ bool swept_before(const Dev& d, uint32_t x, uint32_t cs, uint32_t t) 
     const uint32_t tr = d.log_tick[li];
     if (tr == NEVER || tr >= t) continue;
     if (tr < cs) break;
-    if (rounds_before(d, x, tr) > infP + 2u * (d.log_spread[li] + 1u)) return true;
+    if (rounds_before(d, x, tr) > infP + sweep_after(d.log_spread[li])) return true;
     if (steady) break;
   }
   return false;
@@ -640,7 +646,7 @@ __global__ void k_round_info(Dev d) {
   if (m >= d.N) return;
   uint32_t thr = 0;
   if (d.tround[m]) {
-    const int64_t P = (int64_t)d.tperiod[m] - 2 * ((int64_t)d.tspread[m] + 1);
+    const int64_t P = (int64_t)d.tperiod[m] - (int64_t)sweep_after(d.tspread[m]);
     const uint32_t f = d.firstGossip[m];
     if (P >= 1) thr = f == NEVER ? NEVER : (uint32_t)min<int64_t>((int64_t)NEVER, (int64_t)f + (P - 1) * d.gossip_t + 1);
   }
@@ -762,7 +768,7 @@ __global__ void __launch_bounds__(256) k_gossip_scan(const Dev* __restrict__ dp,
       if (!rnd) continue;
       const uint32_t infP = (fg == NEVER || c <= fg) ? 0u : (c - fg + d.gossip_t - 1) / d.gossip_t;  // rounds_before
       if (infP + sp >= per) wb |= 1ull << j;  // selectGossipsToSend window (:246)
-      if (per > infP + 2u * (sp + 1u)) {      // sweepGossips (:283-308)
+      if (per > infP + sweep_after(sp)) {  // sweepGossips (:283-308)
         atomicOr(&d.S[(size_t)g * d.N + m], S_SWEPT);
         atomicSub(&d.held[m], 1u);
         atomicSub(&d.slot_holders[g], 1);

@@ -30,6 +30,9 @@ struct ML {
   unsigned long long c[8];
   uint32_t pend;  // this tick's SYNC messages that carry the live row: a chain through SyncMsg.pad (NEVER = none)
   uint32_t tround;
+  uint32_t* trk;  // subjects whose key changed in this tick's P1 (several payloads only); ntrk > TRK: overflowed
+  uint32_t ntrk;
+  bool trk_on;
 };
 
 __device__ __forceinline__ uint32_t draw(ML& L, uint32_t stream) {
@@ -72,6 +75,14 @@ __device__ __forceinline__ void row_put(ML& L, uint32_t s, uint64_t v) {
   const uint32_t k = key32(v);
   if (rec_inc(v) >= INC_LIMIT) set_err(*L.d, E_INC);
   if (L.pend != NEVER && L.rk[s] != k) cow(L);
+  if (L.trk_on && L.rk[s] != k && L.ntrk <= TRK) {  // merge_payload re-checks it against the later payloads
+    bool seen = false;
+    for (uint32_t i = 0; i < L.ntrk; ++i) seen |= L.trk[i] == s;
+    if (!seen) {
+      if (L.ntrk < TRK) L.trk[L.ntrk] = s;
+      L.ntrk++;
+    }
+  }
   L.rk[s] = k;
   if (L.rd && k != L.d->base_row[s]) L.rd[(s / CH) >> 6] |= 1ull << ((s / CH) & 63);
   L.ra[s] = aux32(v);
@@ -103,10 +114,20 @@ __device__ __forceinline__ bool send_sync(ML& L, uint32_t kind, uint32_t dst, ui
   mm.psize = L.tsize;
   mm.ncand = 0;
   mm.pad = L.pend;  // chained so that a later row write can redirect the payload to a snapshot (cow)
+  mm.pin = NEVER;
   d.msgs[b][i] = mm;
   L.pend = i;
-  // the receiver's inbound list for the next tick (sharded handles build it when the exchange commits the list)
-  if (d.W == 1) d.m_next[(size_t)b * d.MSGCAP + i] = atomicExch(&d.m_head[(size_t)b * d.N + dst], i);
+  // the receiver's inbound list for the next tick (sharded handles build it when the exchange commits the list);
+  // a receiver with several payloads gets them pinned (pin_msg). The fence publishes the record before its index.
+  if (d.W == 1) {
+    __threadfence();
+    const uint32_t old = atomicExch(&d.m_head[(size_t)b * d.N + dst], i);
+    d.m_next[(size_t)b * d.MSGCAP + i] = old;
+    if (old != NEVER) {
+      pin_msg(d, b, i);
+      pin_msg(d, b, old);
+    }
+  }
   return true;
 }
 
@@ -347,7 +368,7 @@ __device__ __forceinline__ void update_membership(ML& L, uint32_t subj, uint32_t
     uint64_t v = (v0 & ~KEY_MASK) | rec_key(s1, i1);
     if (s1 == ST_SUSPECT) {  // scheduleSuspicionTimeoutTask (:597-606): computeIfAbsent
       if (rec_timer(v) == 0) {
-        uint32_t dl = L.k + d.suspMult * bitlen(L.tsize) * d.ping_t;
+        uint32_t dl = L.k + suspicion_ticks(d, L.tsize);
         v = rec_with_timer(v, dl);
         if (dl < L.timerMin) L.timerMin = dl;
       }
@@ -593,24 +614,52 @@ __device__ __forceinline__ void do_sync(ML& L) {
   send_sync(L, K_SYNC, target, NONE32, 0);
 }
 
-// syncMembership (:456-467) over the candidates k_sync_diff extracted from one payload
+// payload record r1 (key32 k1) of subject s against the live row: `.filter(r1 -> !r1.equals(table.get(id)))`, then
+// updateMembership (:462-464)
+__device__ __forceinline__ void merge_record(ML& L, uint32_t s, uint32_t k1, uint32_t reason, int g) {
+  if ((k1 & 3u) == ST_ABSENT || k1 == L.rk[s]) return;
+  const uint64_t key = key34(k1);
+  update_membership(L, s, rec_status(key), rec_inc(key), reason, g);
+}
+
+// syncMembership (:456-467) of one payload. The reference filters every payload record against the live table when
+// that payload is processed. k_sync_diff extracted the records that differ from the receiver's row as it stood at
+// the start of the tick, in subject order; that is exact for the first payload of the tick. A later payload can
+// also hold, for a subject an earlier payload changed, a record equal to the start row but not to the live one (a
+// leaver's own DEAD record removes it, then another member's ALIVE record of the old incarnation re-adds it,
+// MembershipRecord.java:67-69). Those subjects (L.trk) are read from the payload itself and merged into the
+// candidate walk in subject order; past TRK of them, the whole payload is compared against the live row.
 __device__ __forceinline__ void merge_payload(ML& L, uint32_t mi, uint32_t reason, int g) {
   const Dev& d = *L.d;
-  const SyncMsg& mm = d.msgs[(L.k - 1) & 1][mi];
+  const uint32_t b = (L.k - 1) & 1;
+  const SyncMsg& mm = d.msgs[b][mi];
   L.c[C_R] += mm.psize;
   L.c[C_SYNCMERGE]++;
-  if (mm.ncand == 0) return;  // steady state: nothing differs, skip the chunk walk
-  for (uint32_t c = 0; c < d.NCHUNK; ++c) {
+  const uint32_t nt = L.ntrk;
+  if (nt > TRK) {  // rare: many subjects changed earlier in this tick; exact full walk
+    for (uint32_t s = 0; s < L.N; ++s) merge_record(L, s, payload_key_at(d, mm, b, s), reason, g);
+    return;
+  }
+  if (mm.ncand == 0 && nt == 0) return;  // steady state: nothing differs, skip the chunk walk
+  for (uint32_t i = 1; i < nt; ++i)  // the tracked subjects in ascending order (insertion sort, at most TRK)
+    for (uint32_t j = i; j > 0 && L.trk[j - 1] > L.trk[j]; --j) {
+      const uint32_t t = L.trk[j];
+      L.trk[j] = L.trk[j - 1];
+      L.trk[j - 1] = t;
+    }
+  uint32_t ti = 0;
+  for (uint32_t c = 0; c < d.NCHUNK && mm.ncand; ++c) {
     const uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NCHUNK + c) * 2;
     uint32_t off = cm[0], n = cm[1];
     for (uint32_t e = 0; e < n; ++e) {
       uint64_t rec = d.pool[(size_t)off + e];
       uint32_t subj = (uint32_t)(rec >> 34);
-      uint64_t key = rec & KEY_MASK;
-      if (key == key34(L.rk[subj])) continue;  // !r1.equals(table.get(id)) at processing time
-      update_membership(L, subj, rec_status(key), rec_inc(key), reason, g);
+      for (; ti < nt && L.trk[ti] < subj; ++ti) merge_record(L, L.trk[ti], payload_key_at(d, mm, b, L.trk[ti]), reason, g);
+      if (ti < nt && L.trk[ti] == subj) ++ti;  // a candidate: its record is the pool's
+      merge_record(L, subj, key32(rec & KEY_MASK), reason, g);
     }
   }
+  for (; ti < nt; ++ti) merge_record(L, L.trk[ti], payload_key_at(d, mm, b, L.trk[ti]), reason, g);
 }
 
 // Triage (k_member_triage): the idle fast path. Most members have nothing due in most ticks (a ping every 10 ticks,
@@ -702,6 +751,9 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   for (int i = 0; i < 8; ++i) L.c[i] = 0;
   L.pend = NEVER;
   L.tround = 0;
+  L.trk = d.trk + li * TRK;
+  L.ntrk = 0;
+  L.trk_on = false;
 
   // ---- P0 host requests: updateIncarnation (MembershipProtocolImpl.java:178-190), then leaveCluster (:197-206) ----
   const uint32_t preq = dead ? 0u : d.pending_inc[m];
@@ -779,6 +831,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
       idx[j] = q;
     }
     uint64_t last = 0;
+    L.trk_on = n > 1 || more;  // several payloads: later ones re-check the subjects earlier ones changed
     for (uint32_t r = 0;; ++r) {
       uint32_t mi;
       if (!more) {
@@ -819,6 +872,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
         }
       }
     }
+    L.trk_on = false;
   }
 
   // ---- P2 FD: remote hops of pending pings, then PING_ACK arrivals in cid order ----

@@ -165,11 +165,21 @@ __global__ void __launch_bounds__(256) k_pack_a_chunks(Dev d, uint32_t b) {
 }
 
 // the assembled inbound list becomes msgs[b], which the next tick sorts and merges (one block)
+// (one block). A receiver with several payloads gets its live-row payloads pinned (pin_msg, dev_util.h).
 __device__ void msgs_commit(const Dev& d, uint32_t b) {
   uint32_t n = min(d.xn[4], d.MSGCAP);
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
     d.msgs[b][i] = d.mtmp[i];
-    d.m_next[(size_t)b * d.MSGCAP + i] = atomicExch(&d.m_head[(size_t)b * d.N + d.mtmp[i].dst], i);
+    d.msgs[b][i].pin = NEVER;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint32_t old = atomicExch(&d.m_head[(size_t)b * d.N + d.mtmp[i].dst], i);
+    d.m_next[(size_t)b * d.MSGCAP + i] = old;
+    if (old != NEVER) {
+      if (d.msgs[b][i].payload == NEVER) pin_msg(d, b, i);
+      if (d.msgs[b][old].payload == NEVER) pin_msg(d, b, old);
+    }
   }
   if (threadIdx.x == 0) d.nmsg[b] = n;
 }

@@ -157,6 +157,28 @@ SHARD_SIGNATURES = {
 }
 
 
+# include/swimhip_selftest.h (known-answer surface; exported by libswimhip and by the oracle)
+SELFTEST_OVERRIDES, SELFTEST_PHILOX, SELFTEST_CLUSTER_MATH = 0, 1, 2
+SELFTEST_SIGNATURES = {
+    "swim_selftest_eval": (C.c_int, [C.c_uint32, _U32P, _U32P, C.c_size_t, C.c_uint32]),
+}
+
+
+def selftest_eval(lib, op, rows, device=0):
+    """Evaluate `op` on a list of input tuples through swim_selftest_eval; returns a list of output tuples."""
+    fn = lib.swim_selftest_eval
+    fn.restype, fn.argtypes = SELFTEST_SIGNATURES["swim_selftest_eval"]
+    win, wout = {SELFTEST_OVERRIDES: (4, 1), SELFTEST_PHILOX: (6, 4), SELFTEST_CLUSTER_MATH: (4, 4)}[op]
+    flat = [int(x) & 0xFFFFFFFF for r in rows for x in r]
+    assert len(flat) == win * len(rows)
+    cin = (C.c_uint32 * max(1, len(flat)))(*flat)
+    cout = (C.c_uint32 * max(1, wout * len(rows)))()
+    rc = fn(op, cin, cout, len(rows), device)
+    if rc != 0:
+        raise RuntimeError(f"swim_selftest_eval(op={op}) rc={rc}")
+    return [tuple(cout[i * wout:(i + 1) * wout]) for i in range(len(rows))]
+
+
 def bind_shard(lib):
     """Attach the sharding entry points (engine library only)."""
     for name, (res, args) in SHARD_SIGNATURES.items():

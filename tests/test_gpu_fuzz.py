@@ -15,12 +15,14 @@ from parity_util import run_lockstep
 pytestmark = pytest.mark.gpu
 
 
-def schedule(seed):
+def schedule(seed, fast_sync=False):
     rng = np.random.default_rng(seed)
     n = int(rng.choice([12, 24, 40, 64]))
     preset = rng.integers(3)
     cc = [ClusterConfig(seedMembers=[0]), ClusterConfig(seedMembers=[0, n - 1], syncInterval=5000),
           ClusterConfig.defaultLocalConfig().with_(seedMembers=[0, n // 2])][preset]
+    if fast_sync:  # SYNC every 2-5 ticks: several payloads per receiver and tick (MembershipProtocolImpl.java:456-467)
+        cc = cc.with_(syncInterval=int(rng.choice([200, 300, 500])), syncTimeout=100)
     cold = bool(rng.integers(2))
     cfg = SimConfig(n_members=n, cluster=cc, init_mode=_abi.INIT_COLD_JOIN if cold else _abi.INIT_PRECONVERGED,
                     record_events=True, seed=int(rng.integers(1 << 31)), list_slack=4096, pending_fetch_cap=4096)
@@ -113,6 +115,16 @@ def test_fuzz_single_gpu(oracle, engine, seed):
     cfg, acts = schedule(seed)
     o, e = SimulatedCluster(oracle, cfg), SimulatedCluster(engine, cfg)
     play(o, e, acts, f"fuzz seed {seed} N={cfg.n_members}", cfg.n_dormant)
+    e.close()
+
+
+@pytest.mark.parametrize("seed", range(200, 210))
+def test_fuzz_fast_sync(oracle, engine, seed):
+    """Fast SYNC presets, where a receiver often merges several payloads in one tick and an earlier one changes a
+    row a later one holds at its start-of-tick value (leaves, suspicion removals, partitions)."""
+    cfg, acts = schedule(seed, fast_sync=True)
+    o, e = SimulatedCluster(oracle, cfg), SimulatedCluster(engine, cfg)
+    play(o, e, acts, f"fast-sync fuzz seed {seed} N={cfg.n_members}", cfg.n_dormant)
     e.close()
 
 

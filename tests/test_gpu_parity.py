@@ -56,6 +56,43 @@ def test_partition_and_heal(oracle, engine):
     run_lockstep(o, e, 650, 25, "healed")
 
 
+def _sametick_counter(lib, cluster, i):
+    import ctypes as C
+    fn = lib.swimdbg_counter
+    fn.restype, fn.argtypes = C.c_uint64, [C.c_void_p, C.c_uint32]
+    return fn(cluster._h, i)
+
+
+@pytest.mark.parametrize("shards", [1, 2])
+def test_sync_same_tick_resurrection(oracle, engine, monkeypatch, shards):
+    """Several SYNC / SYNC_ACK payloads reach one receiver in the same tick, and an earlier one changes a row that a
+    later one holds as it stood at the start of the tick. syncMembership filters each payload against the LIVE table
+    (MembershipProtocolImpl.java:456-467): leaver 0's own `DEAD inc+1` (kept in its table, :197-206) removes it at R,
+    then a SYNC from M > 0 still holding `0 ALIVE inc` (equal to R's start-of-tick row) re-adds it, because an absent
+    row accepts any ALIVE record (MembershipRecord.java:67-69), with an ADDED after the metadata fetch. Fast SYNC
+    (every 2 ticks) on 8 members makes such ticks frequent; the oracle counts them (SWIMREF_DEBUG)."""
+    monkeypatch.setenv("SWIMREF_DEBUG", "1")
+    cc = ClusterConfig(seedMembers=[0], syncInterval=200, syncTimeout=100)
+    cfg = SimConfig(n_members=8, cluster=cc, record_events=True)
+    o = SimulatedCluster(oracle, cfg)
+    if shards == 1:
+        e = SimulatedCluster(engine, cfg)
+    else:
+        from swimhip.shard import ThreadShardGroup
+        e = ThreadShardGroup(engine, cfg, shards)
+    run_lockstep(o, e, 7, 7, "warm")
+    for c in (o, e):
+        c.leave(0)
+    run_lockstep(o, e, 60, 1, "leave 0, fast SYNC")
+    assert _sametick_counter(oracle, o, 1) > 0, "the scenario did not occur"
+    for c in (o, e):
+        c.set_default_loss(20)
+        c.leave(5)
+        c.kill(3)
+    run_lockstep(o, e, 200, 5, "leave 5, kill 3, loss 20")
+    e.close()
+
+
 def test_preconverged_sync_large(oracle, engine):
     """C3-shaped at reduced N: no loss, steady state; exercises periodic SYNC / SYNC_ACK merges."""
     cfg = SimConfig(n_members=1500)
