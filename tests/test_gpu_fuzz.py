@@ -21,11 +21,14 @@ def schedule(seed, fast_sync=False):
     preset = rng.integers(3)
     cc = [ClusterConfig(seedMembers=[0]), ClusterConfig(seedMembers=[0, n - 1], syncInterval=5000),
           ClusterConfig.defaultLocalConfig().with_(seedMembers=[0, n // 2])][preset]
+    slots = 0
     if fast_sync:  # SYNC every 2-5 ticks: several payloads per receiver and tick (MembershipProtocolImpl.java:456-467)
         cc = cc.with_(syncInterval=int(rng.choice([200, 300, 500])), syncTimeout=100)
+        slots = 1 << 16  # every SYNC re-spreads the records the receiver lacked: many more live gossips
     cold = bool(rng.integers(2))
     cfg = SimConfig(n_members=n, cluster=cc, init_mode=_abi.INIT_COLD_JOIN if cold else _abi.INIT_PRECONVERGED,
-                    record_events=True, seed=int(rng.integers(1 << 31)), list_slack=4096, pending_fetch_cap=4096)
+                    record_events=True, seed=int(rng.integers(1 << 31)), list_slack=4096, pending_fetch_cap=4096,
+                    gossip_slot_cap=slots)
     acts = [("run", int(rng.integers(20, 60)))]
     for _ in range(int(rng.integers(4, 8))):
         kind = rng.choice(["loss", "part2", "part3", "heal", "kill", "inc", "link", "block", "unblock", "leave"])
