@@ -95,6 +95,21 @@ typedef struct swim_config {
   uint32_t reserved[4];
 } swim_config;
 
+/* One member's own configuration where it differs from the handle's config. The reference builds every member from its own
+ * ClusterConfig (ClusterImpl.java:85-152); FailureDetectorTest.testTrustedDespiteDifferentPingTimings runs members with
+ * different ping timings (FailureDetectorTest.java:150-178). The FailureDetectorConfig fields drive the member's
+ * doPing schedule, ping / ping-req timeouts and helper count, and its suspicion timeout
+ * (ClusterMath.suspicionTimeout(mult, size, pingInterval), MembershipProtocolImpl.java:597-606). sync_group is
+ * MembershipConfig.syncGroup as an id: a member ignores SYNC / SYNC_ACK data of another group (checkSyncGroup,
+ * MembershipProtocolImpl.java:320-331,431-437); members configured by swim_config alone are in group 0. */
+typedef struct swim_member_config {
+  uint32_t ping_interval_ms;
+  uint32_t ping_timeout_ms; /* < ping_interval_ms (ClusterConfig.java:413-415) */
+  uint32_t ping_req_members;
+  uint32_t sync_group;
+  uint32_t reserved[4];
+} swim_member_config;
+
 typedef struct swim_event {
   uint32_t tick;
   uint32_t observer;
@@ -174,6 +189,9 @@ int swim_spread_gossip(swim_handle* h, uint32_t member, uint64_t payload);
  * restart of a crashed member is swim_kill of the old id plus swim_join of a dormant id (a restarted member has a new
  * id in the reference, FailureDetectorTest.java:345-401). A member joins at most once. */
 int swim_join(swim_handle* h, uint32_t member, const uint32_t* seeds, uint32_t n_seeds);
+/* the member's own FailureDetectorConfig / syncGroup (swim_member_config). Allowed before the first swim_step, or for a
+ * dormant member before its swim_join (a running member's config is fixed, as a Cluster's is) */
+int swim_set_member_config(swim_handle* h, uint32_t member, const swim_member_config* mc);
 
 /* readback */
 int swim_current_tick(swim_handle* h, uint64_t* tick);

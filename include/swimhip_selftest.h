@@ -9,6 +9,8 @@
  *                                known-answer vectors
  *   SWIM_SELFTEST_CLUSTER_MATH   ClusterMath.ceilLog2 / gossipPeriodsToSpread / gossipPeriodsToSweep / suspicionTimeout
  *                                (ClusterMath.java:99-135) as the engine evaluates them
+ *   SWIM_SELFTEST_LOSS_ROLL      the per-message loss draw of the NetworkEmulator (TransportTest.testNetworkSettings,
+ *                                transport/src/test/.../TransportTest.java:130-153, checks its statistics)
  * Not part of the simulation API; the oracle evaluates the same functions on the CPU.
  */
 #ifndef SWIMHIP_SELFTEST_H
@@ -26,6 +28,9 @@ extern "C" {
 #define SWIM_SELFTEST_PHILOX 1u       /* in[6i..6i+5] = ctr0..ctr3, key0, key1 -> out[4i..4i+3] */
 #define SWIM_SELFTEST_CLUSTER_MATH 2u /* in[4i..4i+3] = cluster size, repeatMult, suspicionMult, pingInterval ticks
                                          -> out[4i..4i+3] = ceilLog2, periods to spread, periods to sweep, suspicion ticks */
+#define SWIM_SELFTEST_LOSS_ROLL 3u    /* in[8i..8i+7] = message kind, src, dst, tick, issuer, id, seed lo, seed hi
+                                         -> out[i] = the roll in [0,100) a send is lost below (NetworkLinkSettings
+                                         .evaluateLoss, transport/.../NetworkLinkSettings.java:54-57) */
 
 /* evaluates n cases of `op` on HIP device `device` (libswimhip) or on the host (oracle); 0 or a negative SWIM_E* code */
 int swim_selftest_eval(uint32_t op, const uint32_t* in, uint32_t* out, size_t n, uint32_t device);

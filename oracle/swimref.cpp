@@ -211,6 +211,8 @@ struct Member {
   uint64_t initDeadline = NEVER;
 
   uint64_t nextPing = NEVER, nextGossip = NEVER, nextSync = NEVER;
+  // this member's own FailureDetectorConfig and syncGroup (swim_set_member_config; else the swim_config values)
+  uint32_t ping_t = 0, pingTimeout_t = 0, kreq = 0, syncGroup = 0;
   uint32_t pendingInc = 0;  // swim_update_incarnation calls, applied in P0 of the next tick (one bump each)
   bool pendingLeave = false;  // swim_leave (leaveCluster), applied in P0 of the next tick after pendingInc
   uint64_t startTick = NEVER;  // COLD_JOIN: 0 for the initial members, the join tick for a dormant one (swim_join)
@@ -271,8 +273,9 @@ struct Sim {
   std::vector<Lane> lanes;
   std::unique_ptr<Pool> pool;
 
-  uint32_t suspicion_ticks(uint32_t size) const {  // ClusterMath.suspicionTimeout (ClusterMath.java:123-125)
-    return cfg.suspicion_mult * bitlen(size) * ping_t;
+  // ClusterMath.suspicionTimeout (ClusterMath.java:123-125) with the member's own pingInterval
+  uint32_t suspicion_ticks(uint32_t size, uint32_t member_ping_t) const {
+    return cfg.suspicion_mult * bitlen(size) * member_ping_t;
   }
   uint32_t spread_of(uint32_t cluster) const { return cfg.gossip_repeat_mult * bitlen(cluster); }  // :111-113
   uint32_t sweep_of(uint32_t cluster) const { return 2u * (spread_of(cluster) + 1u); }            // :99-102
@@ -293,8 +296,12 @@ struct Sim {
     const uint32_t loss = link_loss(src, dst);
     if (loss == 0) return false;
     if (loss >= 100) return true;
+    return loss_roll(kind, src, dst, k, aux, id) < loss;
+  }
+  // NetworkLinkSettings.evaluateLoss (:54-57): nextInt(100) on the message's LOSS_<kind> draw (SEMANTICS.md §2)
+  uint32_t loss_roll(uint8_t kind, uint32_t src, uint32_t dst, uint64_t k, uint32_t aux, uint32_t id) const {
     P4 r = philox4x32_10(src, dst, (uint32_t)k, id, seed_lo ^ (SALT_LOSS_BASE + kind), seed_hi ^ (aux * 0x9E3779B9u));
-    return next_int(r.v[0], 100) < loss;
+    return next_int(r.v[0], 100);
   }
   bool lost_gossip(uint32_t src, uint32_t dst, uint64_t k, uint32_t slot, uint64_t gid) const {
     const uint32_t loss = link_loss(src, dst);
@@ -424,7 +431,7 @@ void Member::update_membership(uint32_t subj, Rec r1, int reason, int group, uin
   }
   tl_lane->ctr.row_writes++;
   if (r1.st == SUSPECT) {  // :519-523, scheduleSuspicionTimeoutTask (:597-606) computeIfAbsent
-    if (!timers.count(subj)) timers[subj] = k + s.suspicion_ticks(tsize);
+    if (!timers.count(subj)) timers[subj] = k + s.suspicion_ticks(tsize, ping_t);
   } else {
     timers.erase(subj);  // cancelSuspicionTimeoutTask (:590-595)
   }
@@ -533,7 +540,7 @@ void Member::on_fd_event(uint32_t target, uint8_t status, uint64_t k) {
 void Member::ping_req_step(uint32_t target, uint32_t cnt, uint64_t k) {
   Sim& s = *sim;
   std::vector<uint32_t> helpers;
-  uint32_t kreq = s.cfg.ping_req_members;
+  (void)s;
   if (kreq > 0) {
     std::vector<uint32_t> cand(ping);
     auto it = std::find(cand.begin(), cand.end(), target);
@@ -548,7 +555,7 @@ void Member::ping_req_step(uint32_t target, uint32_t cnt, uint64_t k) {
       helpers.assign(cand.begin(), cand.begin() + kk);
     }
   }
-  int timeLeft = (int)s.ping_t - (int)s.pingTimeout_t;
+  int timeLeft = (int)ping_t - (int)pingTimeout_t;
   if (timeLeft <= 0 || helpers.empty()) {
     on_fd_event(target, SUSPECT, k);
     return;
@@ -610,7 +617,7 @@ void Member::do_ping(uint64_t k) {
   m.pd_from = id;
   m.pd_to = target;
   send(std::move(m), k);
-  subs.push_back(Sub{cnt, 0, NONE, target, k + s.pingTimeout_t, subOrder++});
+  subs.push_back(Sub{cnt, 0, NONE, target, k + pingTimeout_t, subOrder++});
 }
 
 // doSpreadGossip (:139-157), selectGossipMembers (:252-273), selectGossipsToSend (:239-250), sweepGossips (:283-308)
@@ -687,7 +694,7 @@ void Member::do_sync(uint64_t k) {
 // ClusterImpl.join0 (:85-152) -> MembershipProtocolImpl.start0 (:216-251), COLD_JOIN only
 void Member::start(uint64_t k) {
   Sim& s = *sim;
-  nextPing = k + s.ping_t;
+  nextPing = k + ping_t;
   nextGossip = k + s.gossip_t;
   if (seeds.empty()) {
     nextSync = k + s.sync_t;
@@ -752,6 +759,7 @@ void Member::process(uint64_t k, std::vector<Msg>& inbox) {
     tickStart = &startTable;
   }
   for (Msg* m : syncm) {
+    if (s.members[m->src].syncGroup != syncGroup) continue;  // checkSyncGroup (:320-321,431-437): SyncData of another group
     if (m->kind == K_SYNC) {
       int g = nextGroup++;
       groups[g] = Group{0, m->src, m->cid_iss, m->cid_cnt, 0, false, false};
@@ -923,7 +931,7 @@ void Member::process(uint64_t k, std::vector<Msg>& inbox) {
   }
   // ---- P6 periodic tasks ----
   if (k == nextPing) {
-    nextPing += s.ping_t;
+    nextPing += ping_t;
     do_ping(k);
   }
   if (k == nextGossip) {
@@ -1083,6 +1091,9 @@ __attribute__((visibility("default"))) int swim_create(const swim_config* cfg, s
     Member& mb = s.members[m];
     mb.sim = &s;
     mb.id = m;
+    mb.ping_t = s.ping_t;
+    mb.pingTimeout_t = s.pingTimeout_t;
+    mb.kreq = c.ping_req_members;
     mb.table.assign(s.N, Rec{});
     mb.meta.assign(s.N, NONE);
     // seeds: LinkedHashSet, minus self (MembershipProtocolImpl.java:160-166)
@@ -1119,7 +1130,7 @@ __attribute__((visibility("default"))) int swim_create(const swim_config* cfg, s
       }
       mb.pingIdx = 0;
       mb.remoteIdx = 0;
-      mb.nextPing = 1 + s.init_draw(m, 1, 0) % s.ping_t;
+      mb.nextPing = 1 + s.init_draw(m, 1, 0) % mb.ping_t;
       mb.nextGossip = 1 + s.init_draw(m, 2, 0) % s.gossip_t;
       mb.nextSync = 1 + s.init_draw(m, 3, 0) % s.sync_t;
       if (c.mode == SWIM_MODE_RUMOR) mb.nextPing = mb.nextSync = NEVER;  // gossip layer only (SEMANTICS.md §9)
@@ -1184,6 +1195,23 @@ __attribute__((visibility("default"))) int swim_join(swim_handle* h, uint32_t m,
   for (uint32_t i = 0; i < n; ++i)
     if (seeds[i] < h->sim.N && seeds[i] != m && std::find(mb.seeds.begin(), mb.seeds.end(), seeds[i]) == mb.seeds.end())
       mb.seeds.push_back(seeds[i]);
+  return SWIM_OK;
+}
+__attribute__((visibility("default"))) int swim_set_member_config(swim_handle* h, uint32_t m, const swim_member_config* mc) {
+  if (!h || !mc || m >= h->sim.N) return SWIM_EINVAL;
+  Sim& s = h->sim;
+  Member& mb = s.members[m];
+  if (s.tick > 0 && !mb.dormant) return SWIM_EINVAL;  // a running member's ClusterConfig is fixed
+  uint32_t pt, tt;
+  if (mc->ping_timeout_ms >= mc->ping_interval_ms || mc->ping_req_members > 8 ||
+      !ms_to_ticks(mc->ping_interval_ms, s.cfg.tick_ms, &pt) || !ms_to_ticks(mc->ping_timeout_ms, s.cfg.tick_ms, &tt) || pt == 0)
+    return SWIM_EINVAL;
+  mb.ping_t = pt;
+  mb.pingTimeout_t = tt;
+  mb.kreq = mc->ping_req_members;
+  mb.syncGroup = mc->sync_group;
+  if (s.cfg.init_mode == SWIM_INIT_PRECONVERGED && s.cfg.mode != SWIM_MODE_RUMOR)
+    mb.nextPing = 1 + s.init_draw(m, 1, 0) % mb.ping_t;  // the schedule phase under the member's own interval
   return SWIM_OK;
 }
 __attribute__((visibility("default"))) int swim_set_default_loss(swim_handle* h, uint32_t pct) {
@@ -1273,11 +1301,17 @@ __attribute__((visibility("default"))) int swim_state_hash(swim_handle* h, uint6
 __attribute__((visibility("default"))) int swim_selftest_eval(uint32_t op, const uint32_t* in, uint32_t* out, size_t n,
                                                               uint32_t device) {
   (void)device;
-  if (op > SWIM_SELFTEST_CLUSTER_MATH || (n && (!in || !out))) return SWIM_EINVAL;
+  if (op > SWIM_SELFTEST_LOSS_ROLL || (n && (!in || !out))) return SWIM_EINVAL;
   for (size_t i = 0; i < n; ++i) {
     if (op == SWIM_SELFTEST_OVERRIDES) {
       const uint32_t* a = in + 4 * i;
       out[i] = is_overrides(Rec{(uint8_t)a[0], a[1]}, Rec{(uint8_t)a[2], a[3]}) ? 1u : 0u;
+    } else if (op == SWIM_SELFTEST_LOSS_ROLL) {
+      const uint32_t* a = in + 8 * i;
+      Sim s;
+      s.seed_lo = a[6];
+      s.seed_hi = a[7];
+      out[i] = s.loss_roll((uint8_t)a[0], a[1], a[2], a[3], a[4], a[5]);
     } else if (op == SWIM_SELFTEST_PHILOX) {
       const uint32_t* a = in + 6 * i;
       const P4 r = philox4x32_10(a[0], a[1], a[2], a[3], a[4], a[5]);
@@ -1291,7 +1325,7 @@ __attribute__((visibility("default"))) int swim_selftest_eval(uint32_t op, const
       out[4 * i] = bitlen(a[0]);
       out[4 * i + 1] = s.spread_of(a[0]);
       out[4 * i + 2] = s.sweep_of(a[0]);
-      out[4 * i + 3] = s.suspicion_ticks(a[0]);
+      out[4 * i + 3] = s.suspicion_ticks(a[0], a[3]);
     }
   }
   return SWIM_OK;

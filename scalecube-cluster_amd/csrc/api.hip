@@ -264,7 +264,7 @@ int build(swim_handle* h) {
   const uint64_t NL = d.NL;  // per-observer arrays: this shard's rows only
   A(d.rowk, NL * d.NS) A(d.rowa, NL * d.NS) A(d.fdl, NL * d.LCAP) A(d.gl, NL * d.LCAP)
   A(d.subs, NL * SUBCAP * 4) A(d.paths, NL * PATHCAP * 5) A(d.fetch, NL * d.FCAP * FREC) A(d.groups, NL * d.GRCAP * GREC)
-  A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.slow, d.SLOWCAP) A(d.slow_n, 1) A(d.rp, d.RPCAP) A(d.rp_n, 1) A(d.rlist, N) A(d.rn, 1) A(d.start_tick, N) A(d.jseed_n, N) A(d.jseeds, 16 * N) A(d.md_uidx, N) A(d.md_ver, NL * MDU) A(d.churn_q, 2ull * d.churn) A(d.cin, N * d.F) A(d.swthr, N) A(d.HB, (uint64_t)(d.SLOTS / 64 + 1) * N) A(d.WB, (uint64_t)(d.SLOTS / 64 + 1) * N) A(d.cev, N * d.F * CEVW)
+  A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.slow, d.SLOWCAP) A(d.slow_n, 1) A(d.rp, d.RPCAP) A(d.rp_n, 1) A(d.rlist, N) A(d.rn, 1) A(d.start_tick, N) A(d.jseed_n, N) A(d.jseeds, 16 * N) A(d.md_uidx, N) A(d.mcfg, 4 * N) A(d.md_ver, NL * MDU) A(d.churn_q, 2ull * d.churn) A(d.cin, N * d.F) A(d.swthr, N) A(d.HB, (uint64_t)(d.SLOTS / 64 + 1) * N) A(d.WB, (uint64_t)(d.SLOTS / 64 + 1) * N) A(d.cev, N * d.F * CEVW)
   A(d.log_tick, N * d.LOGW) A(d.log_spread, N * d.LOGW) A(d.log_cnt, N * d.LOGW) A(d.log_tg, N * d.LOGW * d.F)
   A(d.log_pos, N) A(d.spchg, N)
   A(d.slot_gid, d.SLOTS) A(d.slot_subj, d.SLOTS) A(d.slot_ctick, d.SLOTS) A(d.slot_key, d.SLOTS) A(d.slot_holders, d.SLOTS)
@@ -346,6 +346,17 @@ int build(swim_handle* h) {
   HIPCK(hipMemsetAsync(d.subs, 0, NL * SUBCAP * 16, h->stream));
   int32_t top = (int32_t)d.SPR;
   HIPCK(hipMemcpyAsync(d.free_top, &top, 4, hipMemcpyHostToDevice, h->stream));
+  {  // every member starts with the swim_config FailureDetectorConfig and sync group 0 (swim_set_member_config)
+    std::vector<uint32_t> mc(4ull * N);
+    for (uint64_t m = 0; m < N; ++m) {
+      mc[4 * m] = d.ping_t;
+      mc[4 * m + 1] = d.pingTimeout_t;
+      mc[4 * m + 2] = d.kreq;
+      mc[4 * m + 3] = 0;
+    }
+    HIPCK(hipMemcpyAsync(d.mcfg, mc.data(), 16ull * N, hipMemcpyHostToDevice, h->stream));
+    HIPCK(hipStreamSynchronize(h->stream));
+  }
   std::vector<uint32_t> never(MAX_EPOCHS, NEVER);
   HIPCK(hipMemcpyAsync(d.ep_from, never.data(), 4 * MAX_EPOCHS, hipMemcpyHostToDevice, h->stream));
   HIPCK(hipStreamSynchronize(h->stream));  // `top` and `never` live on this stack frame
@@ -759,6 +770,30 @@ int swim_leave(swim_handle* h, uint32_t m) {
   HIPCK(hipMemcpy(&req, h->d.pending_inc + m, 4, hipMemcpyDeviceToHost));
   req |= 2u;
   HIPCK(hipMemcpy(h->d.pending_inc + m, &req, 4, hipMemcpyHostToDevice));
+  return SWIM_OK;
+}
+
+int swim_set_member_config(swim_handle* h, uint32_t m, const swim_member_config* mc) {
+  if (!h || !mc || m >= h->d.N) return SWIM_EINVAL;
+  Dev& d = h->d;
+  const bool dormant = m >= d.N - d.n_dormant && (h->joined.empty() || !h->joined[m]);
+  if (h->tick > 0 && !dormant) return SWIM_EINVAL;  // a running member's ClusterConfig is fixed
+  uint32_t pt = 0, tt = 0;
+  if (mc->ping_timeout_ms >= mc->ping_interval_ms || mc->ping_req_members > 8 ||
+      !to_ticks(mc->ping_interval_ms, h->cfg.tick_ms, &pt) || !to_ticks(mc->ping_timeout_ms, h->cfg.tick_ms, &tt) || pt == 0)
+    return SWIM_EINVAL;
+  const uint32_t v[4] = {pt, tt, mc->ping_req_members, mc->sync_group};
+  HIPCK(hipStreamSynchronize(h->stream));
+  HIPCK(hipMemcpy(d.mcfg + 4ull * m, v, sizeof(v), hipMemcpyHostToDevice));
+  if (h->cfg.init_mode == SWIM_INIT_PRECONVERGED && d.mode != SWIM_MODE_RUMOR) {
+    // the PRECONVERGED schedule phase under the member's own interval (k_init_members, SEMANTICS.md §3)
+    const uint32_t np = 1u + philox(m, 1, 0, 0, d.seed_lo ^ SALT_INIT, d.seed_hi).x % pt;
+    HIPCK(hipMemcpy(d.nextPing + m, &np, 4, hipMemcpyHostToDevice));
+  }
+  if (!d.permember) {  // the kernels read mcfg from now on (Dev is passed by value and through d.self)
+    d.permember = 1;
+    HIPCK(hipMemcpy((void*)d.self, &d, sizeof(Dev), hipMemcpyHostToDevice));
+  }
   return SWIM_OK;
 }
 

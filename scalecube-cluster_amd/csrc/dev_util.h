@@ -28,6 +28,14 @@ __device__ __forceinline__ int epoch_at(const Dev& d, uint32_t k) {
 
 __device__ __forceinline__ bool dead_at(const Dev& d, uint32_t x, uint32_t k) { return k >= d.dead_tick[x]; }
 
+// member m's own FailureDetectorConfig and syncGroup (swim_set_member_config), else the handle's
+__device__ __forceinline__ uint32_t mc_ping_t(const Dev& d, uint32_t m) { return d.permember ? d.mcfg[4 * m] : d.ping_t; }
+__device__ __forceinline__ uint32_t mc_timeout_t(const Dev& d, uint32_t m) {
+  return d.permember ? d.mcfg[4 * m + 1] : d.pingTimeout_t;
+}
+__device__ __forceinline__ uint32_t mc_kreq(const Dev& d, uint32_t m) { return d.permember ? d.mcfg[4 * m + 2] : d.kreq; }
+__device__ __forceinline__ uint32_t mc_group(const Dev& d, uint32_t m) { return d.permember ? d.mcfg[4 * m + 3] : 0u; }
+
 // NetworkEmulator.getLinkSettings (:57-59): the custom setting of link src -> dst in force at tick k, or -1
 __device__ __noinline__ int link_loss_at(const Dev& d, uint32_t src, uint32_t dst, uint32_t k) {
   const uint64_t key = (((uint64_t)src << 32) | dst) + 1ull;
@@ -74,8 +82,7 @@ __device__ __forceinline__ bool lost_msg(const Dev& d, uint32_t kind, uint32_t s
   uint32_t loss = link_loss(d, ep, src, dst, k);
   if (loss == 0) return false;
   if (loss >= 100) return true;
-  u32x4 r = philox(src, dst, k, id, d.seed_lo ^ (SALT_LOSS_BASE + kind), d.seed_hi ^ (aux * 0x9E3779B9u));
-  return next_int(r.x, 100) < loss;
+  return loss_roll(d.seed_lo, d.seed_hi, kind, src, dst, k, aux, id) < loss;
 }
 
 __device__ __forceinline__ bool lost_gossip(const Dev& d, uint32_t src, uint32_t dst, uint32_t k, uint32_t slot,
@@ -152,7 +159,9 @@ __device__ __forceinline__ uint32_t rounds_before(const Dev& d, uint32_t x, uint
 // suspicionTimeout in ticks; swim_selftest_eval exposes these exact functions for the known-answer tests
 __device__ __forceinline__ uint32_t spread_of(const Dev& d, uint32_t cluster) { return d.repeatMult * bitlen(cluster); }
 __device__ __forceinline__ uint32_t sweep_after(uint32_t spread) { return 2u * (spread + 1u); }
-__device__ __forceinline__ uint32_t suspicion_ticks(const Dev& d, uint32_t size) { return d.suspMult * bitlen(size) * d.ping_t; }
+__device__ __forceinline__ uint32_t suspicion_ticks(const Dev& d, uint32_t size, uint32_t ping_t) {
+  return d.suspMult * bitlen(size) * ping_t;  // the member's own pingInterval (mc_ping_t)
+}
 
 // member m swept gossip slot g at tick k: if g is m's own leave notification, leaveCluster completes and
 // ClusterImpl.doShutdown stops the member (ClusterImpl.java:305-313, GossipProtocolImpl.java:296-306); it is dead

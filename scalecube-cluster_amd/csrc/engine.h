@@ -75,6 +75,10 @@ struct Dev {
   uint32_t* start_tick;  // [N] tick of start0 (0: initial COLD_JOIN members; NEVER: PRECONVERGED or not joined yet)
   uint32_t* jseed_n;     // [N] seeds of a joined member (NONE32: the config's seeds)
   uint32_t* jseeds;      // [N][16]
+  // per-member FailureDetectorConfig + syncGroup (swim_set_member_config): [N][4] = ping_t, pingTimeout_t,
+  // pingReqMembers, sync group; read only when permember (else the swim_config values above)
+  uint32_t permember;
+  uint32_t* mcfg;
   uint32_t* md_uidx;  // [N] column of a member whose metadata was updated (swim_update_metadata), NONE32 if never
   uint32_t* md_ver;   // [NL][MDU] metadata version each observer stores for those members (the others: 0 if known)
   uint32_t mode, churn;  // SWIM_MODE_RUMOR: gossip layer only, churn rumors per FD period (SEMANTICS.md §9)

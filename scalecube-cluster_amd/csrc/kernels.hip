@@ -1135,7 +1135,7 @@ __global__ void k_join(Dev d, uint32_t m, uint32_t k, JoinSeeds js, uint32_t n) 
   if (threadIdx.x != 0) return;
   d.dead_tick[m] = NEVER;
   d.start_tick[m] = k;
-  d.nextPing[m] = k + d.ping_t;
+  d.nextPing[m] = k + mc_ping_t(d, m);
   d.nextGossip[m] = d.firstGossip[m] = k + d.gossip_t;
   d.jseed_n[m] = n;
   for (uint32_t i = 0; i < n; ++i) d.jseeds[(size_t)m * 16 + i] = js.s[i];

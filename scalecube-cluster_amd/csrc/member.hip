@@ -368,7 +368,7 @@ __device__ __forceinline__ void update_membership(ML& L, uint32_t subj, uint32_t
     uint64_t v = (v0 & ~KEY_MASK) | rec_key(s1, i1);
     if (s1 == ST_SUSPECT) {  // scheduleSuspicionTimeoutTask (:597-606): computeIfAbsent
       if (rec_timer(v) == 0) {
-        uint32_t dl = L.k + suspicion_ticks(d, L.tsize);
+        uint32_t dl = L.k + suspicion_ticks(d, L.tsize, mc_ping_t(d, L.m));
         v = rec_with_timer(v, dl);
         if (dl < L.timerMin) L.timerMin = dl;
       }
@@ -439,7 +439,8 @@ __device__ __forceinline__ void ping_req_step(ML& L, uint32_t target, uint32_t c
   const Dev& d = *L.d;
   uint32_t helpers[8];
   uint32_t nh = 0;
-  if (d.kreq > 0) {
+  const uint32_t kreq = mc_kreq(d, L.m);
+  if (kreq > 0) {
     uint32_t pos = L.fdLen;
     for (uint32_t i = 0; i < L.fdLen; ++i)
       if (L.fdl[i] == target) {
@@ -448,7 +449,7 @@ __device__ __forceinline__ void ping_req_step(ML& L, uint32_t target, uint32_t c
       }
     uint32_t n = L.fdLen - (pos < L.fdLen ? 1u : 0u);
     if (n > 0) {
-      uint32_t kk = d.kreq < n ? d.kreq : n;
+      uint32_t kk = kreq < n ? kreq : n;
       uint32_t ovp[16], ovv[16], nov = 0;  // positions touched by the partial Fisher-Yates
       auto get = [&](uint32_t i) -> uint32_t {
         for (uint32_t q = 0; q < nov; ++q)
@@ -475,7 +476,7 @@ __device__ __forceinline__ void ping_req_step(ML& L, uint32_t target, uint32_t c
       nh = kk;
     }
   }
-  int timeLeft = (int)d.ping_t - (int)d.pingTimeout_t;
+  int timeLeft = (int)mc_ping_t(d, L.m) - (int)mc_timeout_t(d, L.m);
   if (timeLeft <= 0 || nh == 0) {
     on_fd_event(L, target, ST_SUSPECT);
     return;
@@ -510,7 +511,7 @@ __device__ __forceinline__ void do_ping(ML& L) {
     ping_req_step(L, target, cnt);
     return;
   }
-  add_sub(L, cnt, 0, target, L.k + d.pingTimeout_t);
+  add_sub(L, cnt, 0, target, L.k + mc_timeout_t(d, L.m));
   add_path(L, cnt, P_DIRECT | 1, L.k + d.lat, target, 0);
 }
 
@@ -852,6 +853,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
         last = best;
       }
       SyncMsg mm = d.msgs[pb][mi];
+      if (mc_group(d, mm.src) != mc_group(d, m)) continue;  // checkSyncGroup (:320-321,431-437): another group's data
       if (mm.kind == K_SYNC) {
         int g = alloc_group(L, 0, mm.src, mm.cid_iss, mm.cid_cnt);
         merge_payload(L, mi, R_SYNC, g);
@@ -1121,7 +1123,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
 
   // ---- P6 periodic tasks (schedulePeriodically) ----
   if (k == L.nextPing) {
-    L.nextPing += d.ping_t;
+    L.nextPing += mc_ping_t(d, m);
     do_ping(L);
   }
   if (k == L.nextGossip) {

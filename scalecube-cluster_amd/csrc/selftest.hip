@@ -23,6 +23,9 @@ __global__ void k_selftest(uint32_t op, const uint32_t* in, uint32_t* out, uint3
     out[4ull * i + 1] = r.y;
     out[4ull * i + 2] = r.z;
     out[4ull * i + 3] = r.w;
+  } else if (op == SWIM_SELFTEST_LOSS_ROLL) {
+    const uint32_t* a = in + 8ull * i;  // the roll lost_msg compares with the link's loss percent (dev_util.h)
+    out[i] = loss_roll(a[6], a[7], a[0], a[1], a[2], a[3], a[4], a[5]);
   } else {
     const uint32_t* a = in + 4ull * i;
     Dev d;  // only the fields the ClusterMath helpers read (dev_util.h)
@@ -33,16 +36,17 @@ __global__ void k_selftest(uint32_t op, const uint32_t* in, uint32_t* out, uint3
     out[4ull * i] = bitlen(a[0]);
     out[4ull * i + 1] = sp;
     out[4ull * i + 2] = sweep_after(sp);
-    out[4ull * i + 3] = suspicion_ticks(d, a[0]);
+    out[4ull * i + 3] = suspicion_ticks(d, a[0], a[3]);
   }
 }
 
 }  // namespace swim
 
 extern "C" int swim_selftest_eval(uint32_t op, const uint32_t* in, uint32_t* out, size_t n, uint32_t device) {
-  if (op > SWIM_SELFTEST_CLUSTER_MATH || (n && (!in || !out)) || n > (1u << 24)) return SWIM_EINVAL;
+  if (op > SWIM_SELFTEST_LOSS_ROLL || (n && (!in || !out)) || n > (1u << 24)) return SWIM_EINVAL;
   if (n == 0) return SWIM_OK;
-  const size_t win = op == SWIM_SELFTEST_PHILOX ? 6 : 4, wout = op == SWIM_SELFTEST_OVERRIDES ? 1 : 4;
+  const size_t win = op == SWIM_SELFTEST_PHILOX ? 6 : op == SWIM_SELFTEST_LOSS_ROLL ? 8 : 4;
+  const size_t wout = (op == SWIM_SELFTEST_OVERRIDES || op == SWIM_SELFTEST_LOSS_ROLL) ? 1 : 4;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= (int)device || hipSetDevice((int)device) != hipSuccess)
     return SWIM_EDEVICE;

@@ -104,6 +104,14 @@ constexpr uint32_t S_FD_SHUFFLE = 1, S_FD_INSERT = 2, S_PINGREQ = 3, S_GOSSIP_SH
 
 SW_HD uint32_t next_int(uint32_t x, uint32_t bound) { return (uint32_t)(((uint64_t)x * bound) >> 32); }
 
+// NetworkLinkSettings.evaluateLoss (:54-57): `nextInt(100) < loss` on the LOSS_<kind> draw of one message
+// (SEMANTICS.md §2); the roll in [0, 100) of message `id` sent by src to dst at tick k, aux = the id's issuer
+SW_HD uint32_t loss_roll(uint32_t seed_lo, uint32_t seed_hi, uint32_t kind, uint32_t src, uint32_t dst, uint32_t k,
+                         uint32_t aux, uint32_t id) {
+  const u32x4 r = philox(src, dst, k, id, seed_lo ^ (SALT_LOSS_BASE + kind), seed_hi ^ (aux * 0x9E3779B9u));
+  return next_int(r.x, 100);
+}
+
 SW_HD uint64_t mix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;

@@ -58,6 +58,16 @@ class SwimConfig(C.Structure):
     ]
 
 
+class SwimMemberConfig(C.Structure):
+    _fields_ = [
+        ("ping_interval_ms", C.c_uint32),
+        ("ping_timeout_ms", C.c_uint32),
+        ("ping_req_members", C.c_uint32),
+        ("sync_group", C.c_uint32),
+        ("reserved", C.c_uint32 * 4),
+    ]
+
+
 class SwimEvent(C.Structure):
     _fields_ = [
         ("tick", C.c_uint32),
@@ -117,6 +127,7 @@ SIGNATURES = {
     "swim_leave": (C.c_int, [_H, C.c_uint32]),
     "swim_spread_gossip": (C.c_int, [_H, C.c_uint32, C.c_uint64]),
     "swim_join": (C.c_int, [_H, C.c_uint32, C.POINTER(C.c_uint32), C.c_uint32]),
+    "swim_set_member_config": (C.c_int, [_H, C.c_uint32, C.POINTER(SwimMemberConfig)]),
     "swim_current_tick": (C.c_int, [_H, C.POINTER(C.c_uint64)]),
     "swim_read_row": (C.c_int, [_H, C.c_uint32, C.POINTER(C.c_uint64), C.c_size_t]),
     "swim_state_hash": (C.c_int, [_H, C.POINTER(C.c_uint64), C.c_size_t]),
@@ -158,7 +169,7 @@ SHARD_SIGNATURES = {
 
 
 # include/swimhip_selftest.h (known-answer surface; exported by libswimhip and by the oracle)
-SELFTEST_OVERRIDES, SELFTEST_PHILOX, SELFTEST_CLUSTER_MATH = 0, 1, 2
+SELFTEST_OVERRIDES, SELFTEST_PHILOX, SELFTEST_CLUSTER_MATH, SELFTEST_LOSS_ROLL = 0, 1, 2, 3
 SELFTEST_SIGNATURES = {
     "swim_selftest_eval": (C.c_int, [C.c_uint32, _U32P, _U32P, C.c_size_t, C.c_uint32]),
 }
@@ -168,7 +179,8 @@ def selftest_eval(lib, op, rows, device=0):
     """Evaluate `op` on a list of input tuples through swim_selftest_eval; returns a list of output tuples."""
     fn = lib.swim_selftest_eval
     fn.restype, fn.argtypes = SELFTEST_SIGNATURES["swim_selftest_eval"]
-    win, wout = {SELFTEST_OVERRIDES: (4, 1), SELFTEST_PHILOX: (6, 4), SELFTEST_CLUSTER_MATH: (4, 4)}[op]
+    win, wout = {SELFTEST_OVERRIDES: (4, 1), SELFTEST_PHILOX: (6, 4), SELFTEST_CLUSTER_MATH: (4, 4),
+                 SELFTEST_LOSS_ROLL: (8, 1)}[op]
     flat = [int(x) & 0xFFFFFFFF for r in rows for x in r]
     assert len(flat) == win * len(rows)
     cin = (C.c_uint32 * max(1, len(flat)))(*flat)

@@ -77,6 +77,7 @@ class SimulatedCluster:
         rc = lib.swim_create(C.byref(a), C.byref(self._h))
         if rc != 0:
             raise SwimError(f"swim_create failed rc={rc}")
+        self._groups = {cfg.cluster.syncGroup: 0}  # MembershipConfig.syncGroup names -> ABI ids
 
     # -- lifecycle ------------------------------------------------------------------------------------------
     def close(self):
@@ -143,6 +144,18 @@ class SimulatedCluster:
         """Cluster.join of a new process for a dormant member (SimConfig.n_dormant) with its own seedMembers."""
         arr = (C.c_uint32 * max(1, len(seeds)))(*[int(x) for x in seeds])
         self._ck(self.lib.swim_join(self._h, member, arr, len(seeds)), "swim_join")
+
+    def set_member_config(self, member, cc):
+        """Member `member` runs with its own ClusterConfig `cc` (ClusterImpl.join0 builds every member from its own
+        config): its FailureDetectorConfig (ping interval / timeout / ping-req members) and its syncGroup. Before the
+        first step, or for a dormant member before join()."""
+        cc.validate()
+        mc = _abi.SwimMemberConfig()
+        mc.ping_interval_ms = cc.pingInterval
+        mc.ping_timeout_ms = cc.pingTimeout
+        mc.ping_req_members = cc.pingReqMembers
+        mc.sync_group = self._groups.setdefault(cc.syncGroup, len(self._groups))
+        self._ck(self.lib.swim_set_member_config(self._h, member, C.byref(mc)), "swim_set_member_config")
 
     def spread_gossip(self, member, payload):
         """Cluster.spreadGossip(message): a user gossip from member carrying a 64-bit payload (ClusterImpl.java:208)."""

@@ -157,6 +157,7 @@ class ShardedCluster(SimulatedCluster):
         rc = lib.swim_create_sharded(C.byref(a), C.byref(spec), C.byref(self._h))
         if rc != 0:
             raise SwimError(f"swim_create_sharded failed rc={rc} (rank {rank} of {world})")
+        self._groups = {cfg.cluster.syncGroup: 0}
         lo, hi = C.c_uint32(), C.c_uint32()
         self._ck(lib.swim_shard_range(self._h, C.byref(lo), C.byref(hi)), "swim_shard_range")
         self.lo, self.hi = lo.value, hi.value
@@ -266,6 +267,10 @@ class ThreadShardGroup:
     def update_incarnation(self, m):
         for s in self.shards:
             s.update_incarnation(m)
+
+    def set_member_config(self, m, cc):
+        for s in self.shards:  # replicated on every shard, like the network settings
+            s.set_member_config(m, cc)
 
     def update_metadata(self, m):
         for s in self.shards:

@@ -93,6 +93,51 @@ def test_sync_same_tick_resurrection(oracle, engine, monkeypatch, shards):
     e.close()
 
 
+@pytest.mark.parametrize("shards", [1, 2])
+def test_member_configs(oracle, engine, shards):
+    """Members with their own ClusterConfig (swim_set_member_config): FD timings and ping-req counts per member
+    (FailureDetectorTest.testTrustedDespiteDifferentPingTimings, :150-178; the member's suspicion timeout follows its
+    own pingInterval, MembershipProtocolImpl.java:597-606) and two syncGroups whose SYNC data the other side ignores
+    (checkSyncGroup, :431-437), under loss and with a crash; bit-exact with the oracle."""
+    n = 60
+    cfg = SimConfig(n_members=n, cluster=ClusterConfig(seedMembers=[0, 55], syncInterval=3000), record_events=True)
+    o = SimulatedCluster(oracle, cfg)
+    if shards == 1:
+        e = SimulatedCluster(engine, cfg)
+    else:
+        from swimhip.shard import ThreadShardGroup
+        e = ThreadShardGroup(engine, cfg, shards)
+    for c in (o, e):
+        for m in range(0, 10):
+            c.set_member_config(m, ClusterConfig(pingInterval=500, pingTimeout=200, pingReqMembers=1))
+        for m in range(10, 20):
+            c.set_member_config(m, ClusterConfig(pingInterval=2000, pingTimeout=1000, pingReqMembers=4))
+        for m in range(50, 60):
+            c.set_member_config(m, ClusterConfig(syncGroup="b"))
+        c.set_default_loss(10)
+    run_lockstep(o, e, 150, 25, "mixed configs, loss 10")
+    for c in (o, e):
+        c.kill(12)
+        c.kill(52)
+    run_lockstep(o, e, 450, 50, "kills")
+    e.close()
+
+
+def test_fd_bad_network_per_member_unblock(oracle, engine):
+    """FailureDetectorTest.testSuspectedMemberWithBadNetworkGetsPartitioned (:181-237) in lockstep: member 0 blocks
+    every outbound link, then unblocks its own links only (a.networkEmulator().unblockAll(), per-link here)."""
+    cc = ClusterConfig(pingInterval=200, pingTimeout=100, pingReqMembers=2, metadataTimeout=100)
+    cfg = SimConfig(n_members=4, cluster=cc, tick_ms=10, record_events=True)
+    o, e = pair(oracle, engine, cfg)
+    for c in (o, e):
+        c.block(0, 0, 1, 2, 3)
+    run_lockstep(o, e, 100, 10, "0 blocked")
+    for c in (o, e):
+        c.unblock(0, 0, 1, 2, 3)
+    run_lockstep(o, e, 400, 25, "0 unblocked")
+    assert sorted(e.trusted(0)) == [0, 1, 2, 3]
+
+
 def test_preconverged_sync_large(oracle, engine):
     """C3-shaped at reduced N: no loss, steady state; exercises periodic SYNC / SYNC_ACK merges."""
     cfg = SimConfig(n_members=1500)

@@ -66,6 +66,24 @@ def check_cluster_math(lib):
     assert got == [(0, 0, 2, 0), (1, 3, 8, 300), (2, 4, 10, 600)]
 
 
+def check_network_settings(lib):
+    """TransportTest.testNetworkSettings (transport/src/test/.../TransportTest.java:130-153): 1000 messages from
+    client to server with a 50 % loss link setting; the server receives fewer than total / 100 * (50 + 5). The rolls
+    are the library's own loss draw (K_PING = 3, one correlation id per message), for three seeds."""
+    total, lost_pct = 1000, 50
+    for seed in (0x5EED5EED, 1, 0xDEADBEEF12345678):
+        rows = [(3, 0, 1, 7, 0, i, seed & 0xFFFFFFFF, seed >> 32) for i in range(total)]
+        received = sum(1 for (r,) in _abi.selftest_eval(lib, _abi.SELFTEST_LOSS_ROLL, rows) if not r < lost_pct)
+        assert received < total // 100 * lost_pct + total // 100 * 5, received
+        assert received > total // 100 * lost_pct - total // 100 * 5, received  # and not a degenerate draw
+    rolls = _abi.selftest_eval(lib, _abi.SELFTEST_LOSS_ROLL, [(3, 0, 1, t, 0, 0, 7, 0) for t in range(4000)])
+    assert sorted(set(r for (r,) in rolls)) == list(range(100))  # every roll in [0, 100) occurs
+
+
+def test_network_settings_loss_statistics(oracle):
+    check_network_settings(oracle)
+
+
 def test_is_overrides_truth_table(oracle):
     check_truth_table(oracle)
     for r1, r0, want in CASES:  # the exported scalar helper too
@@ -89,6 +107,8 @@ def test_engine_device_known_answers(engine):
     check_truth_table(engine)
     check_philox(engine)
     check_cluster_math(engine)
+    check_network_settings(engine)
+    # the same rolls on both libraries (the device draw is the oracle's)
 
 
 def test_default_config_matches_cluster_config(oracle):

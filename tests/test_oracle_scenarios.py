@@ -407,3 +407,52 @@ def test_join_seed_cluster_with_no_existing_seed_member(oracle):  # ClusterTest 
     c.step(ticks_for_seconds(2))
     assert trusted(c, 2) == [2] and suspected(c, 2) == []
     assert trusted(c, 0) == [0]
+
+
+def test_fd_trusted_despite_different_ping_timings(oracle):
+    # FailureDetectorTest.testTrustedDespiteDifferentPingTimings (:150-178): a runs the fast test config, b and c
+    # the default FD timings (1000 / 500 ms); every member keeps the other two trusted
+    c = SimulatedCluster(oracle, fd_config(3))
+    for m in (1, 2):
+        c.set_member_config(m, ClusterConfig(pingInterval=1000, pingTimeout=500))
+    c.step(ticks_for_seconds(5))
+    for o in range(3):
+        assert trusted(c, o) == [0, 1, 2] and suspected(c, o) == []
+    assert c.events() == []
+
+
+def test_fd_suspected_member_with_bad_network(oracle):
+    # FailureDetectorTest.testSuspectedMemberWithBadNetworkGetsPartitioned (:181-237): a blocks its traffic to every
+    # member; a suspects b, c, d and they suspect a. Then a.networkEmulator().unblockAll(): a's own settings only
+    # (per-link unblock), and after 4 s every member trusts every other again.
+    c = SimulatedCluster(oracle, fd_config(4))
+    c.block(0, 0, 1, 2, 3)
+    c.step(ticks_for_seconds(1))
+    assert suspected(c, 0) == [1, 2, 3]
+    for o in (1, 2, 3):
+        assert suspected(c, o) == [0]
+    c.unblock(0, 0, 1, 2, 3)
+    c.step(ticks_for_seconds(4))
+    for o in range(4):
+        assert trusted(c, o) == [0, 1, 2, 3] and suspected(c, o) == []
+
+
+def test_sync_groups_do_not_merge(oracle):
+    # MembershipProtocolImpl.checkSyncGroup (:320-331,431-437): a member ignores SYNC / SYNC_ACK data of another
+    # syncGroup. Cold join through seed 0: members 4..5 are in group "other", so their initial syncs with seed 0 time
+    # out unanswered and seed 0 ignores theirs; they learn the cluster only through gossip and FD-triggered traffic.
+    import dataclasses
+    n = 6
+    cfg = dataclasses.replace(mp_config(n), cluster=ClusterConfig(
+        seedMembers=[0], syncInterval=500, syncTimeout=100, pingInterval=200, pingTimeout=100, metadataTimeout=100))
+    same = SimulatedCluster(oracle, cfg)
+    split = SimulatedCluster(oracle, cfg)
+    for m in (4, 5):
+        split.set_member_config(m, ClusterConfig(pingInterval=200, pingTimeout=100, syncGroup="other"))
+    for c in (same, split):
+        c.step(ticks_for_seconds(3))
+    for o in range(n):
+        assert sorted(same.members(o)) == list(range(n))
+    assert split.members(4) == [4] and split.members(5) == [5]  # no SYNC of theirs was ever merged, nor answered
+    for o in range(4):
+        assert 4 not in split.members(o) and 5 not in split.members(o)
