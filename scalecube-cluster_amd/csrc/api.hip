@@ -14,6 +14,7 @@
 
 #include "../../include/swimhip.h"
 #include "../../include/swimhip_shard.h"
+#include "../../include/swimhip_wire.h"
 #include "engine.h"
 
 using namespace swim;
@@ -865,6 +866,17 @@ int swim_read_row(swim_handle* h, uint32_t obs, uint64_t* out, size_t cap) {
   HIPCK(hipMemcpy(a.data(), h->d.rowa + lidx(h->d, obs) * h->d.NS, 4ull * h->d.N, hipMemcpyDeviceToHost));
   for (uint32_t s = 0; s < h->d.N; ++s) out[s] = (k[s] & 3u) == ST_ABSENT ? 0 : rec_join(k[s], a[s]);
   return SWIM_OK;
+}
+
+int swim_export_sync_frame(swim_handle* h, uint32_t obs, uint32_t kind, uint8_t* buf, size_t cap, size_t* len) {
+  if (!h || !len) return SWIM_EINVAL;
+  std::vector<uint64_t> row(h->d.N);
+  int rc = swim_read_row(h, obs, row.data(), row.size());
+  if (rc != SWIM_OK) return rc;
+  std::vector<swim_wire_record> recs;  // prepareSyncDataMsg (MembershipProtocolImpl.java:446-454): the whole table
+  for (uint32_t s = 0; s < h->d.N; ++s)
+    if (rec_status(row[s]) != ST_ABSENT) recs.push_back(swim_wire_record{s, rec_status(row[s]), rec_inc(row[s])});
+  return swim_wire_sync_frame(kind, obs, nullptr, "default", recs.data(), recs.size(), buf, cap, len);
 }
 
 int swim_state_hash(swim_handle* h, uint64_t* out, size_t cap) {

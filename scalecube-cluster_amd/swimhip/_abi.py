@@ -191,6 +191,58 @@ def selftest_eval(lib, op, rows, device=0):
     return [tuple(cout[i * wout:(i + 1) * wout]) for i in range(len(rows))]
 
 
+# include/swimhip_wire.h (wire-format export; libswimhip only)
+class SwimWireRecord(C.Structure):
+    _fields_ = [("member", C.c_uint32), ("status", C.c_uint32), ("incarnation", C.c_uint32)]
+
+
+WIRE_SYNC, WIRE_SYNC_ACK = 1, 2
+_U8P = C.POINTER(C.c_uint8)
+WIRE_SIGNATURES = {
+    "swim_wire_sync_frame": (C.c_int, [C.c_uint32, C.c_uint32, C.c_char_p, C.c_char_p, C.POINTER(SwimWireRecord),
+                                       C.c_size_t, _U8P, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "swim_wire_gossip_frame": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(SwimWireRecord), _U8P,
+                                         C.c_size_t, C.POINTER(C.c_size_t)]),
+    "swim_export_sync_frame": (C.c_int, [_H, C.c_uint32, C.c_uint32, _U8P, C.c_size_t, C.POINTER(C.c_size_t)]),
+}
+
+
+def bind_wire(lib):
+    for name, (res, args) in WIRE_SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+def _frame_call(fn, *args):
+    """Call an encoder twice: once for the size, once into a buffer of that size; returns the frame bytes."""
+    n = C.c_size_t()
+    fn(*args, None, 0, C.byref(n))
+    buf = (C.c_uint8 * n.value)()
+    rc = fn(*args, buf, n.value, C.byref(n))
+    if rc != 0:
+        raise RuntimeError(f"{fn.__name__} rc={rc}")
+    return bytes(buf)
+
+
+def wire_sync_frame(lib, kind, sender, records, cid=None, sync_group="default"):
+    bind_wire(lib)
+    arr = (SwimWireRecord * max(1, len(records)))(*[SwimWireRecord(*r) for r in records])
+    return _frame_call(lib.swim_wire_sync_frame, kind, sender, cid.encode() if cid else None, sync_group.encode(),
+                       arr, len(records))
+
+
+def wire_gossip_frame(lib, sender, origin, counter, record):
+    bind_wire(lib)
+    return _frame_call(lib.swim_wire_gossip_frame, sender, origin, counter, C.byref(SwimWireRecord(*record)))
+
+
+def export_sync_frame(lib, handle, observer, kind=WIRE_SYNC):
+    bind_wire(lib)
+    return _frame_call(lib.swim_export_sync_frame, handle, observer, kind)
+
+
 def bind_shard(lib):
     """Attach the sharding entry points (engine library only)."""
     for name, (res, args) in SHARD_SIGNATURES.items():

@@ -13,6 +13,7 @@ from swimhip import _abi, LIB_PATH
 HEADER = Path(__file__).resolve().parent.parent / "include" / "swimhip.h"
 SHARD_HEADER = Path(__file__).resolve().parent.parent / "include" / "swimhip_shard.h"
 SELFTEST_HEADER = Path(__file__).resolve().parent.parent / "include" / "swimhip_selftest.h"
+WIRE_HEADER = Path(__file__).resolve().parent.parent / "include" / "swimhip_wire.h"
 
 
 def declared_symbols(header=HEADER):
@@ -28,6 +29,10 @@ def test_shard_header_and_ctypes_agree():
     assert set(declared_symbols(SHARD_HEADER)) == set(_abi.SHARD_SIGNATURES)
 
 
+def test_wire_header_and_ctypes_agree():
+    assert set(declared_symbols(WIRE_HEADER)) == set(_abi.WIRE_SIGNATURES)
+
+
 def test_selftest_header_and_ctypes_agree():
     assert set(declared_symbols(SELFTEST_HEADER)) == set(_abi.SELFTEST_SIGNATURES)
 
@@ -41,7 +46,8 @@ def test_engine_library_exports_every_symbol():
     if not LIB_PATH.exists():
         pytest.skip("libswimhip.so not built (run __graft_entry__.build())")
     lib = _abi.load(LIB_PATH)  # loading initialises no device
-    for name in declared_symbols() + declared_symbols(SHARD_HEADER) + declared_symbols(SELFTEST_HEADER):
+    for name in (declared_symbols() + declared_symbols(SHARD_HEADER) + declared_symbols(SELFTEST_HEADER)
+                 + declared_symbols(WIRE_HEADER)):
         assert hasattr(lib, name), name
     assert lib.swim_abi_version() == 1
     # pure helpers run on the host side of the library
