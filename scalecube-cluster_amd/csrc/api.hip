@@ -3,6 +3,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -18,6 +21,8 @@
 #include "engine.h"
 
 using namespace swim;
+
+struct Group;  // swim_config.n_gpus > 1: one handle over several row-sharded shard handles (below)
 
 struct swim_handle {
   swim_config cfg;
@@ -57,6 +62,7 @@ struct swim_handle {
   hipEvent_t ev_member = nullptr;
   bool no_skip = getenv("SWIM_NO_GOSSIP_SKIP") != nullptr;  // debugging aid: always run the gossip data plane
   bool no_pipe = getenv("SWIM_NO_PIPELINE") != nullptr;    // debugging aid: no early SYNC diff of the next tick
+  Group* grp = nullptr;  // n_gpus > 1: every call is forwarded to the shards (d holds shard 0's constants only)
 };
 
 namespace {
@@ -523,6 +529,179 @@ bool owns(const swim_handle* h, uint32_t m) { return m >= h->d.lo && m < h->d.hi
 
 }  // namespace
 
+// ---------------------------------------------------------------------------------------------------------------
+// One handle over several GPUs (swim_config.n_gpus = W > 1; SURVEY.md §8b: "RCCL communicators created in
+// swim_create", ClusterConfig unchanged for the caller). The handle owns W row-sharded shard handles
+// (swimhip_shard.h), one per device, and forwards every call: stepping runs the shards on W host threads in
+// lockstep; fault injection goes to every shard; readback goes to the owning shard (rows, lists, gossips) or is
+// summed / merged over them (hashes, counters, events), exactly as a multi-process deployment would combine them.
+// Transport: RCCL between W distinct devices (one communicator per shard, initialised together); on a node with
+// fewer devices (the single-GPU test box) the shards share the devices and exchange through host memory inside this
+// process (SWIM_GROUP_HOST=1 forces that).
+struct Group {
+  std::vector<swim_handle*> shards;
+  std::vector<uint32_t> lo, hi;
+  uint32_t transport = SWIM_TRANSPORT_HOST;
+  // in-process host exchange: each rank deposits its blocks, waits for all, copies its own, waits again
+  std::mutex mu;
+  std::condition_variable cv;
+  uint32_t arrived = 0;
+  uint64_t gen = 0;
+  bool abort = false;
+  struct Block {
+    const uint8_t* data = nullptr;
+    std::vector<uint64_t> words;
+  };
+  std::vector<Block> blocks;
+  struct End {
+    Group* g;
+    uint32_t rank;
+  };
+  std::vector<End> ends;
+  std::vector<swim_event> events;
+};
+
+namespace {
+
+bool group_barrier(Group* g) {
+  std::unique_lock<std::mutex> lk(g->mu);
+  if (g->abort) return false;
+  const uint64_t my = g->gen;
+  if (++g->arrived == g->shards.size()) {
+    g->arrived = 0;
+    g->gen++;
+    g->cv.notify_all();
+    return true;
+  }
+  const bool ok = g->cv.wait_for(lk, std::chrono::seconds(600), [&] { return g->gen != my || g->abort; });
+  return ok && !g->abort;
+}
+
+void group_abort(Group* g) {
+  std::lock_guard<std::mutex> lk(g->mu);
+  g->abort = true;
+  g->cv.notify_all();
+}
+
+// swim_exchange_fn of the in-process transport (the contract of swimhip_shard.h)
+int group_exchange(void* ctx, const void* send, const uint64_t* sb, void* recv, uint64_t cap, uint64_t* rb) {
+  const Group::End* e = (const Group::End*)ctx;
+  Group* g = e->g;
+  const uint32_t W = (uint32_t)g->shards.size(), r = e->rank;
+  g->blocks[r].data = (const uint8_t*)send;
+  g->blocks[r].words.assign(sb, sb + W);
+  if (!group_barrier(g)) return -1;
+  uint64_t out = 0;
+  for (uint32_t p = 0; p < W; ++p) {
+    const Group::Block& B = g->blocks[p];
+    uint64_t off = 0;
+    for (uint32_t q = 0; q < r; ++q) off += B.words[q] & SWIM_XCOUNT_MASK;
+    const uint64_t n = B.words[r] & SWIM_XCOUNT_MASK;
+    if (out + n > cap) {
+      group_abort(g);
+      return -1;
+    }
+    if (n) std::memcpy((uint8_t*)recv + out, B.data + off, n);
+    out += n;
+    rb[p] = B.words[r];
+  }
+  return group_barrier(g) ? 0 : -1;  // every peer has copied before the send buffers are reused
+}
+
+int fail(swim_handle* h, int rc, const std::string& what) {
+  h->err = what;
+  return rc;
+}
+
+int create_group(const swim_config* cfg, swim_handle** out) {
+  const uint32_t W = cfg->n_gpus;
+  if (W > 64 || W > cfg->n_members / 2) return SWIM_EINVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= (int)cfg->device) return SWIM_EDEVICE;
+  auto* h = new swim_handle();
+  h->cfg = *cfg;
+  Group* g = h->grp = new Group();
+  const bool rccl = (uint64_t)cfg->device + W <= (uint64_t)ndev && !getenv("SWIM_GROUP_HOST");
+  g->transport = rccl ? SWIM_TRANSPORT_RCCL : SWIM_TRANSPORT_HOST;
+  g->shards.assign(W, nullptr);
+  g->blocks.resize(W);
+  for (uint32_t r = 0; r < W; ++r) g->ends.push_back(Group::End{g, r});
+  std::vector<int> rc(W, SWIM_OK);
+  auto make = [&](uint32_t r, const uint8_t* id) {
+    swim_config c = *cfg;
+    c.n_gpus = 1;
+    c.device = rccl ? cfg->device + r : cfg->device + r % (uint32_t)(ndev - (int)cfg->device);
+    swim_shard_spec sp{};
+    sp.rank = r;
+    sp.world = W;
+    sp.transport = g->transport;
+    if (rccl) {
+      std::memcpy(sp.rccl_id, id, 128);
+    } else {
+      sp.exchange = group_exchange;
+      sp.ctx = &g->ends[r];
+    }
+    rc[r] = create(&c, &sp, &g->shards[r]);
+  };
+  if (rccl) {  // ncclCommInitRank is collective: every rank's call runs on its own thread
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) {
+      swim_destroy(h);
+      return SWIM_EDEVICE;
+    }
+    std::vector<std::thread> th;
+    for (uint32_t r = 0; r < W; ++r) th.emplace_back(make, r, (const uint8_t*)&id);
+    for (auto& t : th) t.join();
+  } else {
+    for (uint32_t r = 0; r < W; ++r) make(r, nullptr);
+  }
+  for (uint32_t r = 0; r < W; ++r)
+    if (rc[r] != SWIM_OK) {
+      swim_destroy(h);
+      return rc[r];
+    }
+  for (swim_handle* s : g->shards) {
+    g->lo.push_back(s->d.lo);
+    g->hi.push_back(s->d.hi);
+  }
+  h->d = g->shards[0]->d;  // constants only (N, ping_t, ...): the group handle itself launches nothing
+  *out = h;
+  return SWIM_OK;
+}
+
+// run f on every shard (on its device), in rank order; the first error is the group's
+template <class F>
+int group_all(swim_handle* h, F f) {
+  Group* g = h->grp;
+  for (size_t r = 0; r < g->shards.size(); ++r) {
+    hipSetDevice((int)g->shards[r]->cfg.device);
+    const int rc = f(g->shards[r]);
+    if (rc != SWIM_OK) return fail(h, rc, "shard " + std::to_string(r) + ": " + g->shards[r]->err);
+  }
+  return SWIM_OK;
+}
+
+// run f on the shard that owns observer m
+template <class F>
+int group_owner(swim_handle* h, uint32_t m, F f) {
+  Group* g = h->grp;
+  for (size_t r = 0; r < g->shards.size(); ++r)
+    if (m >= g->lo[r] && m < g->hi[r]) {
+      hipSetDevice((int)g->shards[r]->cfg.device);
+      const int rc = f(g->shards[r]);
+      if (rc != SWIM_OK) return fail(h, rc, "shard " + std::to_string(r) + ": " + g->shards[r]->err);
+      return rc;
+    }
+  return SWIM_EINVAL;
+}
+
+}  // namespace
+
+#define GROUP_ALL(call)                                            \
+  if (h && h->grp) return group_all(h, [&](swim_handle* s) { return call; })
+#define GROUP_OWNER(m, call)                                       \
+  if (h && h->grp) return group_owner(h, (m), [&](swim_handle* s) { return call; })
+
 extern "C" {
 
 uint32_t swim_abi_version(void) { return SWIM_ABI_VERSION; }
@@ -550,8 +729,11 @@ int swim_is_overrides(uint32_t s1, uint32_t i1, uint32_t s0, uint32_t i0) { retu
 uint32_t swim_ceil_log2(uint32_t n) { return bitlen(n); }
 
 int swim_create(const swim_config* cfg, swim_handle** out) {
-  // one handle for all N observers on one GPU; several GPUs shard the observers (swim_create_sharded)
-  if (cfg && cfg->n_gpus > 1) return SWIM_EUNSUPPORTED;
+  // one handle for all N observers: on one GPU, or row-sharded over n_gpus devices inside this process (Group)
+  if (cfg && out && cfg->n_gpus > 1) {
+    *out = nullptr;
+    return create_group(cfg, out);
+  }
   return create(cfg, nullptr, out);
 }
 
@@ -570,6 +752,11 @@ int swim_rccl_unique_id(uint8_t* out128) {
 
 int swim_shard_range(swim_handle* h, uint32_t* lo, uint32_t* hi) {
   if (!h || !lo || !hi) return SWIM_EINVAL;
+  if (h->grp) {  // the group reports on every observer
+    *lo = 0;
+    *hi = h->d.N;
+    return SWIM_OK;
+  }
   *lo = h->d.lo;
   *hi = h->d.hi;
   return SWIM_OK;
@@ -577,6 +764,13 @@ int swim_shard_range(swim_handle* h, uint32_t* lo, uint32_t* hi) {
 
 int swim_destroy(swim_handle* h) {
   if (!h) return SWIM_EINVAL;
+  if (h->grp) {
+    for (swim_handle* s : h->grp->shards)
+      if (s) swim_destroy(s);
+    delete h->grp;
+    delete h;
+    return SWIM_OK;
+  }
   hipSetDevice((int)h->cfg.device);
   if (h->stream) hipStreamSynchronize(h->stream);
   for (void* p : h->allocs) hipFree(p);
@@ -596,6 +790,24 @@ constexpr uint64_t DIFF_SAMPLE = 5;
 
 int swim_step(swim_handle* h, uint32_t n) {
   if (!h) return SWIM_EINVAL;
+  if (h->grp) {  // the shards in lockstep, one host thread each (their exchanges meet inside swim_step)
+    Group* g = h->grp;
+    std::vector<int> rc(g->shards.size(), SWIM_OK);
+    std::vector<std::thread> th;
+    for (size_t r = 0; r < g->shards.size(); ++r)
+      th.emplace_back([&, r] {
+        rc[r] = swim_step(g->shards[r], n);
+        if (rc[r] != SWIM_OK) group_abort(g);  // peers waiting in an exchange give up
+      });
+    for (auto& t : th) t.join();
+    h->tick = g->shards[0]->tick;
+    for (size_t r = 0; r < rc.size(); ++r)
+      if (rc[r] != SWIM_OK && g->shards[r]->err.size())
+        return fail(h, rc[r], "shard " + std::to_string(r) + ": " + g->shards[r]->err);
+    for (size_t r = 0; r < rc.size(); ++r)
+      if (rc[r] != SWIM_OK) return fail(h, rc[r], "shard " + std::to_string(r) + " failed in a peer's exchange");
+    return SWIM_OK;
+  }
   hipSetDevice((int)h->cfg.device);
   if (h->tick + n >= (1ull << 28)) return SWIM_ECAPACITY;  // deadlines are stored in 29 bits
   const bool profile = (h->cfg.flags & (SWIM_FLAG_PROFILE | SWIM_FLAG_PROFILE_ALL)) != 0;
@@ -686,9 +898,13 @@ int swim_run_periods(swim_handle* h, uint32_t n) {
   return swim_step(h, n * h->d.ping_t);
 }
 
-int swim_sync(swim_handle* h) { return h ? check_err(h) : SWIM_EINVAL; }
+int swim_sync(swim_handle* h) {
+  GROUP_ALL(swim_sync(s));
+  return h ? check_err(h) : SWIM_EINVAL;
+}
 
 int swim_kill(swim_handle* h, uint32_t m) {
+  GROUP_ALL(swim_kill(s, m));
   if (!h || m >= h->d.N) return SWIM_EINVAL;
   uint32_t t = (uint32_t)h->tick;
   HIPCK(hipMemcpyAsync(h->d.dead_tick + m, &t, 4, hipMemcpyHostToDevice, h->stream));
@@ -697,6 +913,7 @@ int swim_kill(swim_handle* h, uint32_t m) {
 }
 
 int swim_join(swim_handle* h, uint32_t m, const uint32_t* seeds, uint32_t n) {
+  GROUP_ALL(swim_join(s, m, seeds, n));
   if (!h || m >= h->d.N || n > 16 || (n && !seeds)) return SWIM_EINVAL;
   if (m < h->d.N - h->d.n_dormant) return SWIM_EINVAL;  // only a dormant member starts later
   if (h->joined.empty()) h->joined.assign(h->d.N, 0);
@@ -713,6 +930,7 @@ int swim_join(swim_handle* h, uint32_t m, const uint32_t* seeds, uint32_t n) {
 }
 
 int swim_spread_gossip(swim_handle* h, uint32_t m, uint64_t payload) {
+  GROUP_ALL(swim_spread_gossip(s, m, payload));
   if (!h || m >= h->d.N) return SWIM_EINVAL;
   if (!owns(h, m)) return SWIM_OK;  // the owning shard creates it; the others receive its slot in exchange A
   uint32_t dt = 0;
@@ -725,6 +943,7 @@ int swim_spread_gossip(swim_handle* h, uint32_t m, uint64_t payload) {
 }
 
 int swim_update_metadata(swim_handle* h, uint32_t m) {
+  GROUP_ALL(swim_update_metadata(s, m));
   if (!h || m >= h->d.N) return SWIM_EINVAL;
   uint32_t dt = 0, ver = 0;
   HIPCK(hipStreamSynchronize(h->stream));
@@ -747,6 +966,7 @@ int swim_update_metadata(swim_handle* h, uint32_t m) {
 }
 
 int swim_update_incarnation(swim_handle* h, uint32_t m) {
+  GROUP_ALL(swim_update_incarnation(s, m));
   if (!h || m >= h->d.N) return SWIM_EINVAL;
   if (!owns(h, m)) return SWIM_OK;  // the owning shard bumps it; the others learn it from its gossip
   uint32_t req = 0, dt = 0;
@@ -762,6 +982,7 @@ int swim_update_incarnation(swim_handle* h, uint32_t m) {
 // MembershipProtocolImpl.leaveCluster (:197-206) via ClusterImpl.shutdown -> doShutdown (:297-313): in P0 of the next
 // tick the member's own record becomes DEAD inc+1 and is spread; when that gossip is swept at the member, it stops
 int swim_leave(swim_handle* h, uint32_t m) {
+  GROUP_ALL(swim_leave(s, m));
   if (!h || m >= h->d.N) return SWIM_EINVAL;
   HIPCK(hipStreamSynchronize(h->stream));
   uint32_t dt = 0, req = 0;
@@ -775,6 +996,7 @@ int swim_leave(swim_handle* h, uint32_t m) {
 }
 
 int swim_set_member_config(swim_handle* h, uint32_t m, const swim_member_config* mc) {
+  GROUP_ALL(swim_set_member_config(s, m, mc));
   if (!h || !mc || m >= h->d.N) return SWIM_EINVAL;
   Dev& d = h->d;
   const bool dormant = m >= d.N - d.n_dormant && (h->joined.empty() || !h->joined[m]);
@@ -799,12 +1021,14 @@ int swim_set_member_config(swim_handle* h, uint32_t m, const swim_member_config*
 }
 
 int swim_set_default_loss(swim_handle* h, uint32_t pct) {
+  GROUP_ALL(swim_set_default_loss(s, pct));
   if (!h || pct > 100) return SWIM_EINVAL;
   h->loss = pct;
   return push_epoch(h);
 }
 
 int swim_set_partition(swim_handle* h, const uint32_t* g) {
+  GROUP_ALL(swim_set_partition(s, g));
   if (!h) return SWIM_EINVAL;
   if (g) {
     h->group.assign(g, g + h->d.N);
@@ -827,6 +1051,7 @@ int swim_set_partition(swim_handle* h, const uint32_t* g) {
 }
 
 int swim_unblock_all(swim_handle* h) {  // NetworkEmulator.unblockAll: customLinkSettings.clear() (:186-192)
+  GROUP_ALL(swim_unblock_all(s));
   if (!h) return SWIM_EINVAL;
   h->partitioned = false;
   if (!h->link_cur.empty()) {
@@ -840,12 +1065,14 @@ int swim_unblock_all(swim_handle* h) {  // NetworkEmulator.unblockAll: customLin
 }
 
 int swim_set_link_loss(swim_handle* h, uint32_t src, uint32_t dst, uint32_t pct) {
+  GROUP_ALL(swim_set_link_loss(s, src, dst, pct));
   if (!h || src >= h->d.N || dst >= h->d.N || pct > 100) return SWIM_EINVAL;
   link_change(h, link_key_of(src, dst), pct);
   return upload_links(h);
 }
 
 int swim_unblock_link(swim_handle* h, uint32_t src, uint32_t dst) {
+  GROUP_ALL(swim_unblock_link(s, src, dst));
   if (!h || src >= h->d.N || dst >= h->d.N) return SWIM_EINVAL;
   if (!h->link_cur.count(link_key_of(src, dst))) return SWIM_OK;
   link_change(h, link_key_of(src, dst), LK_NONE);
@@ -859,6 +1086,7 @@ int swim_current_tick(swim_handle* h, uint64_t* t) {
 }
 
 int swim_read_row(swim_handle* h, uint32_t obs, uint64_t* out, size_t cap) {
+  GROUP_OWNER(obs, swim_read_row(s, obs, out, cap));
   if (!h || obs >= h->d.N || cap < h->d.N || !owns(h, obs)) return SWIM_EINVAL;
   HIPCK(hipStreamSynchronize(h->stream));
   std::vector<uint32_t> k(h->d.N), a(h->d.N);  // the two planes, joined into logical records (swim_common.h)
@@ -881,6 +1109,15 @@ int swim_export_sync_frame(swim_handle* h, uint32_t obs, uint32_t kind, uint8_t*
 
 int swim_state_hash(swim_handle* h, uint64_t* out, size_t cap) {
   if (!h || cap < 6ull * h->d.N) return SWIM_EINVAL;
+  if (h->grp) {  // each shard fills its observers' words and leaves the others zero
+    std::vector<uint64_t> part(6ull * h->d.N);
+    std::fill(out, out + 6ull * h->d.N, 0ull);
+    return group_all(h, [&](swim_handle* s) {
+      const int rc = swim_state_hash(s, part.data(), part.size());
+      for (size_t i = 0; rc == SWIM_OK && i < part.size(); ++i) out[i] += part[i];
+      return rc;
+    });
+  }
   uint64_t* dout = nullptr;
   HIPCK(hipMalloc(&dout, 48ull * h->d.N));
   HIPCK(hipMemsetAsync(dout, 0, 48ull * h->d.N, h->stream));  // other shards' observers stay zero
@@ -893,6 +1130,7 @@ int swim_state_hash(swim_handle* h, uint64_t* out, size_t cap) {
 
 int swim_read_lists(swim_handle* h, uint32_t obs, uint32_t* fd, uint32_t* fd_len, uint32_t* gl, uint32_t* g_len,
                     size_t cap, int32_t* cursors) {
+  GROUP_OWNER(obs, swim_read_lists(s, obs, fd, fd_len, gl, g_len, cap, cursors));
   if (!h || obs >= h->d.N || !owns(h, obs)) return SWIM_EINVAL;
   HIPCK(hipStreamSynchronize(h->stream));
   uint32_t fl = 0, glen = 0;
@@ -909,6 +1147,7 @@ int swim_read_lists(swim_handle* h, uint32_t obs, uint32_t* fd, uint32_t* fd_len
 }
 
 int swim_read_gossips(swim_handle* h, uint32_t obs, uint64_t* ids, uint32_t* inf, size_t cap, size_t* n_out) {
+  GROUP_OWNER(obs, swim_read_gossips(s, obs, ids, inf, cap, n_out));
   if (!h || obs >= h->d.N || !n_out || !owns(h, obs)) return SWIM_EINVAL;
   HIPCK(hipStreamSynchronize(h->stream));
   const Dev& d = h->d;
@@ -945,6 +1184,30 @@ int swim_read_gossips(swim_handle* h, uint32_t obs, uint64_t* ids, uint32_t* inf
 
 int swim_drain_events(swim_handle* h, swim_event* out, size_t cap, size_t* n_out) {
   if (!h || !n_out) return SWIM_EINVAL;
+  if (h->grp) {  // every shard's events, merged in (tick, observer, seq) order
+    auto& ev = h->grp->events;
+    std::vector<swim_event> buf(65536);
+    const int rc = group_all(h, [&](swim_handle* s) {
+      size_t n = 0;
+      do {
+        const int r = swim_drain_events(s, buf.data(), buf.size(), &n);
+        if (r != SWIM_OK) return r;
+        ev.insert(ev.end(), buf.begin(), buf.begin() + (long)n);
+      } while (n == buf.size());
+      return SWIM_OK;
+    });
+    if (rc != SWIM_OK) return rc;
+    std::stable_sort(ev.begin(), ev.end(), [](const swim_event& a, const swim_event& b) {
+      if (a.tick != b.tick) return a.tick < b.tick;
+      if (a.observer != b.observer) return a.observer < b.observer;
+      return a.seq < b.seq;
+    });
+    const size_t k = std::min(cap, ev.size());
+    std::copy(ev.begin(), ev.begin() + (long)k, out);
+    ev.erase(ev.begin(), ev.begin() + (long)k);
+    *n_out = k;
+    return SWIM_OK;
+  }
   HIPCK(hipStreamSynchronize(h->stream));
   uint32_t n = 0;
   HIPCK(hipMemcpy(&n, h->d.ev_n, 4, hipMemcpyDeviceToHost));
@@ -970,6 +1233,19 @@ int swim_drain_events(swim_handle* h, swim_event* out, size_t cap, size_t* n_out
 
 int swim_counters_get(swim_handle* h, swim_counters* out) {
   if (!h || !out) return SWIM_EINVAL;
+  if (h->grp) {  // the shards' shares summed (the tick is common)
+    swim_counters sum{}, c{};
+    const int rc = group_all(h, [&](swim_handle* s) {
+      const int r = swim_counters_get(s, &c);
+      const uint64_t* a = (const uint64_t*)&c;
+      uint64_t* t = (uint64_t*)&sum;
+      for (size_t i = 1; r == SWIM_OK && i < sizeof(c) / 8; ++i) t[i] += a[i];
+      sum.tick = c.tick;
+      return r;
+    });
+    *out = sum;
+    return rc;
+  }
   HIPCK(hipStreamSynchronize(h->stream));
   unsigned long long c[C_NCTR];
   HIPCK(hipMemcpy(c, h->d.ctr, sizeof(c), hipMemcpyDeviceToHost));

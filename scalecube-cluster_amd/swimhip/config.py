@@ -71,6 +71,7 @@ class SimConfig:
     churn_per_period: int = 0
     n_dormant: int = 0  # COLD_JOIN: the last n_dormant members start only on join()
     device: int = 0
+    n_gpus: int = 1  # > 1: one handle row-sharded over n_gpus devices in this process (swim_create)
 
     def to_abi(self):
         c = self.cluster.validate()
@@ -103,7 +104,7 @@ class SimConfig:
         a.gossip_slot_cap = self.gossip_slot_cap
         a.pending_fetch_cap = self.pending_fetch_cap
         a.event_cap = self.event_cap
-        a.n_gpus = 1
+        a.n_gpus = self.n_gpus
         a.device = self.device
         a.list_slack = self.list_slack
         return a
