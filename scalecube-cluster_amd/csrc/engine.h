@@ -122,7 +122,10 @@ struct Dev {
   uint32_t *rlist, *rn;  // [N] members with a gossip round this tick (built by k_gossip_contacts)
   uint32_t* cin;    // [N][F] latest cached contact t -> m of (m, T[m][s]); NEVER: none, CIN_SLOW: list overflowed
   uint32_t* swthr;  // [N] round sweep bound of this tick (k_round_info)
-  unsigned long long *HB, *WB;  // [SLOTS / 64 + 1][N] per 64-slot group: held past this tick / in a round window
+  unsigned long long *HB, *WB;  // [N][QW] per member and 64-slot group (member-major): held past this tick / in a
+                                // round window
+  uint32_t QW;                  // words per member row of HB / WB = SLOTS / 64 + 1
+  unsigned long long *HBq, *WBq;  // [QW][N] the same masks group-major, as k_gossip_scan writes them
   uint64_t* rp;  // [RPCAP] (slot << 32 | m * F + s): sends of pairs with a cached contact, for k_gossip_replay
   uint32_t* rp_n;
   uint32_t RPCAP;
@@ -147,6 +150,8 @@ struct Dev {
   uint32_t *rc_cnt, *rc_off, *rc_fill;  // [N]
   uint32_t* scan_part;                  // block partial sums of the exclusive scan
   uint32_t* rc_slot;  // [RCAP] sorted by member then gossip id
+  uint32_t* rc_keep;   // [RCAP] per member segment: positions of the receipts k_receipt_filter kept, ascending
+  uint32_t *rc_nkeep, *rc_nuser;  // [N] kept receipts, user-gossip receipts of the segment
   uint64_t* rc_key;   // [RCAP] gossip id sort key
   uint32_t* rc_slot2;  // [RCAP] merge scratch of k_seg_sort (segments above SORT_MAX)
   uint64_t* rc_key2;

@@ -284,6 +284,56 @@ __global__ void __launch_bounds__(256) k_seg_sort(uint64_t* key, uint32_t* val, 
   }
 }
 
+// P4 pre-filter (onMembershipGossip -> updateMembership, MembershipProtocolImpl.java:401-408,475-485): a first receipt
+// whose record does not override the receiver's row as it stands at the start of the next tick cannot override it
+// later in that tick either, as long as the row keeps its presence (rows only move up the isOverrides order, except a
+// removal by DEAD, and an absent row accepts only ALIVE). k_member_tick walks the kept receipts and falls back to the
+// whole segment from the first presence change on (member.hip P4). One block per member segment; a block-wide
+// compaction keeps the gossip-id order. User gossips are always kept (each one emits a GOSSIP event).
+__global__ void __launch_bounds__(256) k_receipt_filter(Dev d) {
+  __shared__ uint32_t sc[256];
+  __shared__ uint32_t base_sh;
+  for (uint32_t t = d.lo + blockIdx.x; t < d.hi; t += gridDim.x) {
+    const uint32_t n = d.rc_cnt[t];
+    if (n == 0) continue;
+    const uint32_t off = d.rc_off[t];
+    const uint32_t* rk = d.rowk + lidx(d, t) * d.NS;
+    uint32_t kept = 0, users = 0;
+    for (uint32_t b0 = 0; b0 < n; b0 += 256) {
+      const uint32_t i = b0 + threadIdx.x;
+      uint32_t keep = 0, user = 0;
+      if (i < n) {
+        const uint32_t g = d.rc_slot[off + i], subj = d.slot_subj[g];
+        if (subj == USER_SUBJ) {
+          keep = user = 1;
+        } else {
+          const uint64_t key = d.slot_key[g];
+          const uint32_t r0 = rk[subj];
+          keep = overrides(rec_status(key), rec_inc(key), r0 & 3u, r0 >> 2) ? 1u : 0u;
+        }
+      }
+      sc[threadIdx.x] = keep | (user << 16);
+      __syncthreads();
+      for (uint32_t o = 1; o < 256; o <<= 1) {
+        const uint32_t v = threadIdx.x >= o ? sc[threadIdx.x - o] : 0u;
+        __syncthreads();
+        sc[threadIdx.x] += v;
+        __syncthreads();
+      }
+      const uint32_t incl = sc[threadIdx.x], tot = sc[255];
+      if (keep) d.rc_keep[off + kept + (incl & 0xFFFFu) - 1] = i;
+      kept += tot & 0xFFFFu;
+      users += tot >> 16;
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      d.rc_nkeep[t] = kept;
+      d.rc_nuser[t] = users;
+    }
+  }
+  (void)base_sh;
+}
+
 // ------------------------------------------------------------------------------------------------------------
 // k_sync_diff: for every SYNC / SYNC_ACK sent in tick k-1, stream the payload's key plane (the sender's live row,
 // or its copy-on-write snapshot) against the receiver's key plane and extract, per 2048-subject chunk and in
@@ -732,12 +782,16 @@ __device__ __forceinline__ void send_tail(const Dev& d, uint32_t g, uint32_t m, 
   }
 }
 
-// The gossip round is bit-parallel over groups of 64 active slots (active[64 q .. 64 q + 63] = group q):
-//   k_gossip_scan  streams the holder table once per tick, coalesced (lane = member), and writes per (group, member)
+// The gossip round is bit-parallel over groups of 64 active slots (active[64 q .. 64 q + 63] = group q). Both masks
+// are member-major, [member][QW] words, so a sender reads its window mask and its target's held mask as contiguous
+// rows:
+//   k_gossip_scan  streams the holder table once per tick, coalesced (lane = member), and writes per (member, group)
 //                  two 64-bit masks: HB = slots the member holds past this tick (held and not sweeping them in its
 //                  round: swthr), WB = slots a round member holds inside its spread window (selectGossipsToSend
-//                  :239-250). It also performs the round members' sweeps (sweepGossips :283-308).
-//   k_gossip_send  per (round member, group): each target t gets WB minus the slots t is in infectedFrom of
+//                  :239-250). It also performs the round members' sweeps (sweepGossips :283-308). A block covers 256
+//                  members x QT groups and transposes the masks through LDS, so every row segment is one 128-B store.
+//   k_gossip_send  one wave per (round member m, target slot s), lanes over the groups: each load of WB[m][q] and
+//                  HB[t][q] is a 512-B contiguous segment. t gets WB minus the slots t is in infectedFrom of
 //                  (isInfected, cached contact replay, only where a contact can matter); the count is a popcount,
 //                  and the first-receipt candidates are WB & ~HB[t].
 // A pair whose contact list overflowed is deferred to k_gossip_send_slow (the full replay needs a large stack).
@@ -768,7 +822,7 @@ __global__ void __launch_bounds__(256) k_gossip_scan(const Dev* __restrict__ dp,
       if (!rnd) continue;
       const uint32_t infP = (fg == NEVER || c <= fg) ? 0u : (c - fg + d.gossip_t - 1) / d.gossip_t;  // rounds_before
       if (infP + sp >= per) wb |= 1ull << j;  // selectGossipsToSend window (:246)
-      if (per > infP + sweep_after(sp)) {  // sweepGossips (:283-308)
+      if (per > infP + sweep_after(sp)) {     // sweepGossips (:283-308)
         atomicOr(&d.S[(size_t)g * d.N + m], S_SWEPT);
         atomicSub(&d.held[m], 1u);
         atomicSub(&d.slot_holders[g], 1);
@@ -782,47 +836,103 @@ __global__ void __launch_bounds__(256) k_gossip_scan(const Dev* __restrict__ dp,
         }
       }
     }
-    d.HB[(size_t)q * d.N + m] = hb;
-    d.WB[(size_t)q * d.N + m] = wb;
+    d.HBq[(size_t)q * d.N + m] = hb;  // group-major here (coalesced); k_mask_transpose makes the member-major rows
+    d.WBq[(size_t)q * d.N + m] = wb;
   }
+}
+
+// [q][N] -> [N][QW] for both masks, 64 x 64 word tiles through LDS (512-B contiguous reads and writes)
+__global__ void __launch_bounds__(256) k_mask_transpose(const Dev* __restrict__ dp, const uint32_t* nactive) {
+  const Dev& d = *dp;
+  __shared__ unsigned long long tile[2][64][65];
+  const uint32_t ngroups = (*nactive + 63) / 64, qt = (ngroups + 63) / 64, mt = (d.N + 63) / 64;
+  const uint32_t lane = threadIdx.x & 63, row0 = threadIdx.x >> 6;  // 4 rows per pass
+  for (uint32_t w = blockIdx.x; w < qt * mt; w += gridDim.x) {
+    const uint32_t q0 = (w / mt) * 64, m0 = (w % mt) * 64;
+    for (uint32_t r = row0; r < 64; r += 4) {  // rows q0 + r, columns m0 + lane
+      const uint32_t q = q0 + r, m = m0 + lane;
+      const bool in = q < ngroups && m < d.N;
+      tile[0][r][lane] = in ? d.HBq[(size_t)q * d.N + m] : 0ull;
+      tile[1][r][lane] = in ? d.WBq[(size_t)q * d.N + m] : 0ull;
+    }
+    __syncthreads();
+    for (uint32_t r = row0; r < 64; r += 4) {  // rows m0 + r, columns q0 + lane
+      const uint32_t m = m0 + r, q = q0 + lane;
+      if (m < d.N && q < ngroups) {
+        d.HB[(size_t)m * d.QW + q] = tile[0][lane][r];
+        d.WB[(size_t)m * d.QW + q] = tile[1][lane][r];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// the r-th (from 0) set bit of w
+__device__ __forceinline__ uint32_t nth_bit(unsigned long long w, uint32_t r) {
+  uint32_t pos = 0;
+#pragma unroll
+  for (uint32_t half = 32; half > 0; half >>= 1) {
+    const uint32_t c = (uint32_t)__popcll(w & ((1ull << half) - 1ull));
+    if (r >= c) {
+      r -= c;
+      w >>= half;
+      pos += half;
+    }
+  }
+  return pos;
+}
+
+// reserve n entries per lane on a wave-shared counter with one atomic (every lane of the wave must call it)
+__device__ __forceinline__ uint32_t wave_reserve(uint32_t* ctr, uint32_t n) {
+  const uint32_t lane = __lane_id();
+  uint32_t incl = n;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  const uint32_t total = __shfl(incl, 63);
+  uint32_t base = 0;
+  if (lane == 0 && total) base = atomicAdd(ctr, total);
+  return __shfl(base, 0) + incl - n;
 }
 
 __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp, uint32_t k, const uint32_t* active,
                                                      const uint32_t* nactive) {
   const Dev& d = *dp;
   __shared__ unsigned long long red[4];
-  const uint32_t na = *nactive, nr = *d.rn, ngroups = (na + 63) / 64, rchunks = (nr + 255) / 256;
+  const uint32_t na = *nactive, nr = *d.rn, ngroups = (na + 63) / 64;
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   unsigned long long sends = 0;
   uint32_t st[4] = {0, 0, 0, 0};  // SWIM_EXP & 4: items with window bits, contact-loop bits, replays, first-receipt candidates
-  for (uint32_t w = blockIdx.x; w < ngroups * rchunks; w += gridDim.x) {
-    const uint32_t q = w / rchunks, ri = (w % rchunks) * 256 + threadIdx.x;
-    if (ri >= nr) continue;
+  for (uint32_t w = blockIdx.x * 4 + wave; w < nr * d.F; w += gridDim.x * 4) {  // wave-uniform item
+    const uint32_t ri = w / d.F, s = w % d.F;
     const uint32_t m = d.rlist[ri];
-    const unsigned long long wb = d.WB[(size_t)q * d.N + m];
-    if (!wb) continue;
-    if (d.exp & 4) st[0]++;
-    const uint32_t n = d.tcnt[m];
-    const uint32_t* ga = active + q * 64;
-    for (uint32_t s = 0; s < n; ++s) {
-      const size_t ms = (size_t)m * d.F + s;
-      const uint32_t t = d.T[ms], ci = d.cin[ms];
-      unsigned long long ok = wb;
+    if (s >= d.tcnt[m]) continue;
+    const size_t ms = (size_t)m * d.F + s;
+    const uint32_t t = d.T[ms], ci = d.cin[ms];
+    const unsigned long long* wrow = d.WB + (size_t)m * d.QW;
+    const unsigned long long* hrow = d.HB + (size_t)t * d.QW;
+    for (uint32_t q0 = 0; q0 < ngroups; q0 += 64) {
+      const uint32_t q = q0 + lane;
+      const unsigned long long wb = q < ngroups ? wrow[q] : 0ull;
+      if (__ballot(wb != 0ull) == 0ull) continue;
+      if (d.exp & 4) st[0] += wb != 0ull;
+      const uint32_t* ga = active + (size_t)q * 64;
       if (ci == CIN_SLOW) {  // overflowed contact list: the full replay runs in k_gossip_send_slow
-        for (unsigned long long b = wb; b; b &= b - 1) {
-          const uint32_t g = ga[__ffsll(b) - 1];
-          uint32_t i = wave_append(d.slow_n);
+        uint32_t i = wave_reserve(d.slow_n, (uint32_t)__popcll(wb));
+        for (unsigned long long b = wb; b; b &= b - 1, ++i) {
           if (i < d.SLOWCAP)
-            d.slow[i] = ((uint64_t)g << 32) | (uint32_t)ms;
+            d.slow[i] = ((uint64_t)ga[__ffsll(b) - 1] << 32) | (uint32_t)ms;
           else
             atomicOr(d.err, E_CONTACTS);
         }
         continue;
       }
       if (ci != NEVER) {  // a cached contact t -> m: every slot of the pair goes to k_gossip_replay (isInfected :247)
-        const uint32_t nb = __popcll(wb);
+        const uint32_t nb = (uint32_t)__popcll(wb);
         if (d.exp & 4) st[1] += nb;
-        uint32_t i = atomicAdd(d.rp_n, nb);
+        uint32_t i = wave_reserve(d.rp_n, nb);
         for (unsigned long long b = wb; b; b &= b - 1, ++i) {
           if (i < d.RPCAP)
             d.rp[i] = ((uint64_t)ga[__ffsll(b) - 1] << 32) | (uint32_t)ms;
@@ -831,12 +941,31 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
         }
         continue;
       }
-      sends += __popcll(ok);
-      unsigned long long cand = d.dbg_send ? ok : ok & ~d.HB[(size_t)q * d.N + t];
-      for (; cand; cand &= cand - 1) {
-        const uint32_t g = ga[__ffsll(cand) - 1];
-        if (d.exp & 4) st[3]++;
-        send_tail(d, g, m, s, t, k, d.slot_gid[g], d.S + (size_t)g * d.N);
+      sends += __popcll(wb);
+      const unsigned long long cand = d.dbg_send ? wb : wb & ~(q < ngroups ? hrow[q] : 0ull);
+      // the wave's candidates are spread over its lanes (a few groups hold most of them: new gossips take recently
+      // freed slots): lane p takes candidates p, p + 64, ... of the wave's list in (group, slot) order
+      const uint32_t c = (uint32_t)__popcll(cand);
+      uint32_t incl = c;
+#pragma unroll
+      for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+      }
+      const uint32_t total = __shfl(incl, 63);
+      for (uint32_t b0 = 0; b0 < total; b0 += 64) {  // wave-uniform: every lane takes part in the shuffles
+        const uint32_t j = b0 + lane;
+        uint32_t own = 0;  // the lane whose word holds candidate j: the number of lanes with incl <= j
+#pragma unroll
+        for (uint32_t step = 32; step > 0; step >>= 1)
+          if (__shfl(incl, (int)(own + step - 1)) <= j) own += step;
+        const unsigned long long word = __shfl(cand, (int)own);
+        const uint32_t r = j - (__shfl(incl, (int)own) - (uint32_t)__popcll(word));
+        if (j < total) {
+          const uint32_t g = active[(size_t)(q0 + own) * 64 + nth_bit(word, r)];
+          if (d.exp & 4) st[3]++;
+          send_tail(d, g, m, s, t, k, d.slot_gid[g], d.S + (size_t)g * d.N);
+        }
       }
     }
   }
@@ -1047,6 +1176,7 @@ void launch_gossip(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   hipLaunchKernelGGL(k_gossip_contacts, dim3(cdiv((uint64_t)d.NL * d.F, 256)), dim3(256), 0, st, d, k);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[4], st);
   hipLaunchKernelGGL(k_gossip_scan, dim3(SEND_GRID), dim3(256), 0, st, d.self, k, d.active, d.nactive);
+  hipLaunchKernelGGL(k_mask_transpose, dim3(SEND_GRID), dim3(256), 0, st, d.self, d.nactive);
   hipLaunchKernelGGL(k_gossip_send, dim3(SEND_GRID), dim3(256), 0, st, d.self, k, d.active, d.nactive);
   hipLaunchKernelGGL(k_gossip_send_slow, dim3(64), dim3(64), 0, st, d.self, k);  // rare; ~14 KB of stack per lane
   hipLaunchKernelGGL(k_gossip_replay, dim3(2048), dim3(256), 0, st, d.self, k);
@@ -1067,6 +1197,7 @@ static void launch_receipt_routing(const Dev& d, hipStream_t st) {
                      d.rc_slot, d.rc_key);
   hipLaunchKernelGGL(k_seg_sort, dim3(1024), dim3(256), 0, st, d.rc_key, d.rc_slot, d.rc_key2, d.rc_slot2, d.rc_off,
                      d.rc_cnt, d.N, d.rc_n);
+  hipLaunchKernelGGL(k_receipt_filter, dim3(2048), dim3(256), 0, st, d);
 }
 
 void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
@@ -1096,6 +1227,7 @@ void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   hipLaunchKernelGGL(k_gossip_contacts, dim3(cdiv((uint64_t)d.NL * d.F, 256)), dim3(256), 0, st, d, k);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[4], st);
   hipLaunchKernelGGL(k_gossip_scan, dim3(SEND_GRID), dim3(256), 0, st, d.self, k, d.active, d.nactive);
+  hipLaunchKernelGGL(k_mask_transpose, dim3(SEND_GRID), dim3(256), 0, st, d.self, d.nactive);
   hipLaunchKernelGGL(k_gossip_send, dim3(SEND_GRID), dim3(256), 0, st, d.self, k, d.active, d.nactive);
   hipLaunchKernelGGL(k_gossip_send_slow, dim3(64), dim3(64), 0, st, d.self, k);  // rare; ~14 KB of stack per lane
   hipLaunchKernelGGL(k_gossip_replay, dim3(2048), dim3(256), 0, st, d.self, k);

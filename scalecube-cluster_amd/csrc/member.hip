@@ -33,6 +33,7 @@ struct ML {
   uint32_t* trk;  // subjects whose key changed in this tick's P1 (several payloads only); ntrk > TRK: overflowed
   uint32_t ntrk;
   bool trk_on;
+  bool pchg;  // a row changed presence (absent <-> present) in this tick: P4 then walks every receipt
 };
 
 __device__ __forceinline__ uint32_t draw(ML& L, uint32_t stream) {
@@ -75,6 +76,7 @@ __device__ __forceinline__ void row_put(ML& L, uint32_t s, uint64_t v) {
   const uint32_t k = key32(v);
   if (rec_inc(v) >= INC_LIMIT) set_err(*L.d, E_INC);
   if (L.pend != NEVER && L.rk[s] != k) cow(L);
+  if (((L.rk[s] & 3u) == ST_ABSENT) != ((k & 3u) == ST_ABSENT)) L.pchg = true;
   if (L.trk_on && L.rk[s] != k && L.ntrk <= TRK) {  // merge_payload re-checks it against the later payloads
     bool seen = false;
     for (uint32_t i = 0; i < L.ntrk; ++i) seen |= L.trk[i] == s;
@@ -755,6 +757,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   L.trk = d.trk + li * TRK;
   L.ntrk = 0;
   L.trk_on = false;
+  L.pchg = false;
 
   // ---- P0 host requests: updateIncarnation (MembershipProtocolImpl.java:178-190), then leaveCluster (:197-206) ----
   const uint32_t preq = dead ? 0u : d.pending_inc[m];
@@ -1028,21 +1031,37 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   }
 
   // ---- P4 gossip first receipts in gossip-id order -> onMembershipGossip (:401-408) ----
+  // k_receipt_filter kept the receipts that can override the row (and every user gossip); from the first presence
+  // change of any row in this tick on, every receipt of the segment is walked (see k_receipt_filter)
   {
-    uint32_t off = d.rc_off[m], n = d.rc_cnt[m];
+    const uint32_t off = d.rc_off[m], n = d.rc_cnt[m];
     if (n) {
       d.rc_cnt[m] = 0;  // the next receipt routing counts from zero
       d.rc_fill[m] = 0;
-    }
-    for (uint32_t q = 0; q < n; ++q) {
-      uint32_t g = d.rc_slot[off + q];
-      uint64_t key = d.slot_key[g];
-      if (d.slot_subj[g] == USER_SUBJ) {  // sink.next -> ClusterImpl.listenGossips (:213-216), not membership
-        emit_event(L, 3, (uint32_t)(d.slot_gid[g] >> 32), (uint32_t)key, (uint32_t)(key >> 32));
-        continue;
+      L.c[C_R] += n - d.rc_nuser[m];  // every membership receipt is a record compare
+      auto receipt = [&](uint32_t q) {
+        const uint32_t g = d.rc_slot[off + q];
+        const uint64_t key = d.slot_key[g];
+        if (d.slot_subj[g] == USER_SUBJ) {  // sink.next -> ClusterImpl.listenGossips (:213-216), not membership
+          emit_event(L, 3, (uint32_t)(d.slot_gid[g] >> 32), (uint32_t)key, (uint32_t)(key >> 32));
+          return;
+        }
+        update_membership(L, d.slot_subj[g], rec_status(key), rec_inc(key), R_GOSSIP, -1);
+      };
+      uint32_t from = 0;  // first position of the whole segment still to walk (n: none)
+      if (!L.pchg) {
+        const uint32_t nk = d.rc_nkeep[m];
+        from = n;
+        for (uint32_t j = 0; j < nk; ++j) {
+          const uint32_t q = d.rc_keep[off + j];
+          receipt(q);
+          if (L.pchg) {
+            from = q + 1;
+            break;
+          }
+        }
       }
-      L.c[C_R]++;
-      update_membership(L, d.slot_subj[g], rec_status(key), rec_inc(key), R_GOSSIP, -1);
+      for (uint32_t q = from; q < n; ++q) receipt(q);
     }
   }
 
