@@ -270,6 +270,7 @@ struct Sim {
   // live row when a later SYNC / SYNC_ACK of the same tick is merged ([0]), and those of them that override it ([1])
   bool debug = false;
   std::atomic<uint64_t> dbg[4] = {};
+  std::vector<uint8_t> leaveRequested;  // SWIMREF_DEBUG: swim_leave was called for the member
   std::vector<Lane> lanes;
   std::unique_ptr<Pool> pool;
 
@@ -723,6 +724,8 @@ static bool fd_less(const Msg& a, const Msg& b) {
 
 void Member::process(uint64_t k, std::vector<Msg>& inbox) {
   Sim& s = *sim;
+  std::vector<Rec> tickStartAll;  // SWIMREF_DEBUG: the table before P0 (what the engine's receipt filter reads)
+  if (s.debug) tickStartAll = table;
   for (uint64_t p : pendingUser) spread(USER_SUBJ, Rec{}, p);  // Cluster.spreadGossip (ClusterImpl.java:208-211)
   pendingUser.clear();
   for (; pendingInc > 0; --pendingInc) {  // updateIncarnation (MembershipProtocolImpl.java:178-190), once per call
@@ -866,7 +869,21 @@ void Member::process(uint64_t k, std::vector<Msg>& inbox) {
   }
   // ---- P4 gossip (onGossipReq :171-183) ----
   std::sort(gm.begin(), gm.end(), [](Msg* a, Msg* b) { return a->gid != b->gid ? a->gid < b->gid : a->src < b->src; });
+  bool deadStamp = false;  // SWIMREF_DEBUG: a DEAD membership record among this tick's first receipts
+  if (s.debug)
+    for (Msg* m : gm)
+      if (!gossips.count(m->gid) && m->g_subj != USER_SUBJ && m->g_rec.st == DEAD) deadStamp = true;
   for (Msg* m : gm) {
+    if (s.debug && !gossips.count(m->gid) && m->g_subj != USER_SUBJ) {  // the engine's receipt_matters rule
+      const Rec r0 = tickStartAll[m->g_subj], r1 = m->g_rec;
+      const bool keep = r0.st == ABSENT || is_overrides(r1, r0) || deadStamp || s.leaveRequested[m->g_subj];
+      if (!keep && is_overrides(r1, table[m->g_subj])) {
+        s.dbg[2]++;
+        fprintf(stderr, "receipt filter miss: tick %llu member %u subject %u r1 %u/%u start %u/%u live %u/%u\n",
+                (unsigned long long)k, id, m->g_subj, r1.st, r1.inc, r0.st, r0.inc, table[m->g_subj].st,
+                table[m->g_subj].inc);
+      }
+    }
     if (s.send_log) fprintf(s.send_log, "R %llu %u %u %llu %d\n", (unsigned long long)k, id, m->src, (unsigned long long)m->gid, gossips.count(m->gid) ? 0 : 1);
     if (!gossips.count(m->gid)) {
       GState g;
@@ -1060,6 +1077,7 @@ __attribute__((visibility("default"))) int swim_create(const swim_config* cfg, s
   if (c.n_dormant > c.n_members || (c.n_dormant && c.init_mode != SWIM_INIT_COLD_JOIN)) return SWIM_EINVAL;
   auto* h = new swim_handle();
   h->sim.debug = getenv("SWIMREF_DEBUG") != nullptr;
+  h->sim.leaveRequested.assign(c.n_members, 0);
   if (const char* th = getenv("SWIMREF_THREADS")) h->sim.threads = std::max(1, std::min(256, atoi(th)));
   if (h->sim.threads > 1) {
     h->sim.pool.reset(new Pool());
@@ -1177,6 +1195,8 @@ __attribute__((visibility("default"))) int swim_update_metadata(swim_handle* h, 
 __attribute__((visibility("default"))) int swim_leave(swim_handle* h, uint32_t m) {
   if (!h || m >= h->sim.N || !h->sim.members[m].alive) return SWIM_EINVAL;
   h->sim.members[m].pendingLeave = true;
+  if (h->sim.leaveRequested.size() != h->sim.N) h->sim.leaveRequested.assign(h->sim.N, 0);
+  h->sim.leaveRequested[m] = 1;
   return SWIM_OK;
 }
 __attribute__((visibility("default"))) int swim_spread_gossip(swim_handle* h, uint32_t m, uint64_t payload) {

@@ -119,6 +119,14 @@ int check_err(swim_handle* h) {
   return SWIM_OK;
 }
 
+// Host -> device update of engine state between ticks: ordered on the engine stream, so the next tick's kernels see
+// it (a plain hipMemcpy runs on the null stream, which a non-blocking stream does not wait for), and finished before
+// returning (the source is often a stack or vector buffer)
+hipError_t h2d(hipStream_t st, void* dst, const void* src, size_t bytes) {
+  hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
+  return e != hipSuccess ? e : hipStreamSynchronize(st);
+}
+
 // open a new NetworkEmulator-settings epoch that starts at the next tick to run
 int push_epoch(swim_handle* h) {
   int e = h->cur_ep;
@@ -127,10 +135,10 @@ int push_epoch(swim_handle* h) {
   h->ep_from[e] = (uint32_t)h->tick;
   h->ep_loss[e] = h->loss;
   h->ep_part[e] = h->partitioned ? 1u : 0u;
-  HIPCK(hipMemcpy(h->d.ep_from + e, &h->ep_from[e], 4, hipMemcpyHostToDevice));
-  HIPCK(hipMemcpy(h->d.ep_loss + e, &h->ep_loss[e], 4, hipMemcpyHostToDevice));
-  HIPCK(hipMemcpy(h->d.ep_part + e, &h->ep_part[e], 4, hipMemcpyHostToDevice));
-  HIPCK(hipMemcpy(h->d.ep_group + (size_t)e * h->d.N, h->group.data(), 4ull * h->d.N, hipMemcpyHostToDevice));
+  HIPCK(h2d(h->stream, h->d.ep_from + e, &h->ep_from[e], 4));
+  HIPCK(h2d(h->stream, h->d.ep_loss + e, &h->ep_loss[e], 4));
+  HIPCK(h2d(h->stream, h->d.ep_part + e, &h->ep_part[e], 4));
+  HIPCK(h2d(h->stream, h->d.ep_group + (size_t)e * h->d.N, h->group.data(), 4ull * h->d.N));
   return SWIM_OK;
 }
 
@@ -164,9 +172,9 @@ int upload_links(swim_handle* h) {
   }
   uint32_t n = (uint32_t)h->link_hist.size();
   HIPCK(hipStreamSynchronize(h->stream));
-  HIPCK(hipMemcpy(h->d.link_key, keys.data(), 8ull * LKCAP, hipMemcpyHostToDevice));
-  HIPCK(hipMemcpy(h->d.link_hist, hist.data(), 4ull * hist.size(), hipMemcpyHostToDevice));
-  HIPCK(hipMemcpy(h->d.link_n, &n, 4, hipMemcpyHostToDevice));
+  HIPCK(h2d(h->stream, h->d.link_key, keys.data(), 8ull * LKCAP));
+  HIPCK(h2d(h->stream, h->d.link_hist, hist.data(), 4ull * hist.size()));
+  HIPCK(h2d(h->stream, h->d.link_n, &n, 4));
   return SWIM_OK;
 }
 
@@ -278,7 +286,7 @@ int build(swim_handle* h) {
   A(d.slot_gid, d.SLOTS) A(d.slot_subj, d.SLOTS) A(d.slot_ctick, d.SLOTS) A(d.slot_key, d.SLOTS) A(d.slot_holders, d.SLOTS)
   A(d.slot_used, d.SLOTS) A(d.S, (uint64_t)d.SLOTS * N) A(d.free_list, d.SLOTS) A(d.free_top, 1)
   A(d.deliv, d.DCAP) A(d.deliv_n, 1) A(d.rc_raw, d.RCAP) A(d.rc_n, 1) A(d.rc_cnt, N) A(d.rc_off, N) A(d.rc_fill, N) A(d.scan_part, 1024)
-  A(d.rc_slot, d.RCAP) A(d.rc_keep, d.RCAP) A(d.rc_nkeep, N) A(d.rc_nuser, N) A(d.rc_key, d.RCAP) A(d.rc_slot2, d.RCAP) A(d.rc_key2, d.RCAP) A(d.active, d.SLOTS) A(d.nactive, 1) A(d.hist, (uint64_t)d.HCAP * HREC)
+  A(d.rc_slot, d.RCAP) A(d.rc_ndrop, N) A(d.dead_rx, N) A(d.leaving, N) A(d.rc_key, d.RCAP) A(d.rc_slot2, d.RCAP) A(d.rc_key2, d.RCAP) A(d.active, d.SLOTS) A(d.nactive, 1) A(d.hist, (uint64_t)d.HCAP * HREC)
   A(d.msgs[0], d.MSGCAP) A(d.msgs[1], d.MSGCAP) A(d.nmsg, 2) A(d.arena[0], (uint64_t)d.ARENA_ROWS * d.NS)
   A(d.arena[1], (uint64_t)d.ARENA_ROWS * d.NS) A(d.arena_used, 2)
   A(d.m_next, 2ull * d.MSGCAP) A(d.m_head, 2 * N) A(d.deaths, 2ull * DEATHCAP) A(d.deaths_n, 2) A(d.next_evt, N) A(d.mdone, 1) A(d.trk, NL * TRK) A(d.pending_inc, N) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
@@ -340,6 +348,9 @@ int build(swim_handle* h) {
   HIPCK(hipMemsetAsync(d.nactive, 0, 4, h->stream));
   HIPCK(hipMemsetAsync(d.deliv_n, 0, 4, h->stream));
   HIPCK(hipMemsetAsync(d.rc_n, 0, 4, h->stream));
+  HIPCK(hipMemsetAsync(d.rc_ndrop, 0, 4 * N, h->stream));
+  HIPCK(hipMemsetAsync(d.dead_rx, 0, 4 * N, h->stream));
+  HIPCK(hipMemsetAsync(d.leaving, 0, 4 * N, h->stream));
   HIPCK(hipMemsetAsync(d.m_head, 0xFF, 2 * N * 4, h->stream));
   if (d.W > 1) {
     HIPCK(hipMemsetAsync(d.xn, 0, 32, h->stream));
@@ -962,7 +973,7 @@ int swim_update_metadata(swim_handle* h, uint32_t m) {
   // every shard keeps the versions of all members (responses are evaluated at the issuer's shard)
   HIPCK(hipMemcpy(&ver, h->d.md_version + m, 4, hipMemcpyDeviceToHost));
   ++ver;
-  HIPCK(hipMemcpy(h->d.md_version + m, &ver, 4, hipMemcpyHostToDevice));
+  HIPCK(h2d(h->stream, h->d.md_version + m, &ver, 4));
   return swim_update_incarnation(h, m);
 }
 
@@ -976,7 +987,7 @@ int swim_update_incarnation(swim_handle* h, uint32_t m) {
   if (dt != NEVER) return SWIM_EINVAL;
   HIPCK(hipMemcpy(&req, h->d.pending_inc + m, 4, hipMemcpyDeviceToHost));
   req += 4u;  // bits 2..: incarnation bumps requested (one per call), bit 1: leave
-  HIPCK(hipMemcpy(h->d.pending_inc + m, &req, 4, hipMemcpyHostToDevice));
+  HIPCK(h2d(h->stream, h->d.pending_inc + m, &req, 4));
   return SWIM_OK;
 }
 
@@ -989,10 +1000,12 @@ int swim_leave(swim_handle* h, uint32_t m) {
   uint32_t dt = 0, req = 0;
   HIPCK(hipMemcpy(&dt, h->d.dead_tick + m, 4, hipMemcpyDeviceToHost));
   if (dt != NEVER) return SWIM_EINVAL;
+  const uint32_t one = 1;  // every shard: k_gossip_apply keeps ALIVE receipts about a leaver (its DEAD may arrive in P1)
+  HIPCK(h2d(h->stream, h->d.leaving + m, &one, 4));
   if (!owns(h, m)) return SWIM_OK;
   HIPCK(hipMemcpy(&req, h->d.pending_inc + m, 4, hipMemcpyDeviceToHost));
   req |= 2u;
-  HIPCK(hipMemcpy(h->d.pending_inc + m, &req, 4, hipMemcpyHostToDevice));
+  HIPCK(h2d(h->stream, h->d.pending_inc + m, &req, 4));
   return SWIM_OK;
 }
 
@@ -1008,15 +1021,15 @@ int swim_set_member_config(swim_handle* h, uint32_t m, const swim_member_config*
     return SWIM_EINVAL;
   const uint32_t v[4] = {pt, tt, mc->ping_req_members, mc->sync_group};
   HIPCK(hipStreamSynchronize(h->stream));
-  HIPCK(hipMemcpy(d.mcfg + 4ull * m, v, sizeof(v), hipMemcpyHostToDevice));
+  HIPCK(h2d(h->stream, d.mcfg + 4ull * m, v, sizeof(v)));
   if (h->cfg.init_mode == SWIM_INIT_PRECONVERGED && d.mode != SWIM_MODE_RUMOR) {
     // the PRECONVERGED schedule phase under the member's own interval (k_init_members, SEMANTICS.md §3)
     const uint32_t np = 1u + philox(m, 1, 0, 0, d.seed_lo ^ SALT_INIT, d.seed_hi).x % pt;
-    HIPCK(hipMemcpy(d.nextPing + m, &np, 4, hipMemcpyHostToDevice));
+    HIPCK(h2d(h->stream, d.nextPing + m, &np, 4));
   }
   if (!d.permember) {  // the kernels read mcfg from now on (Dev is passed by value and through d.self)
     d.permember = 1;
-    HIPCK(hipMemcpy((void*)d.self, &d, sizeof(Dev), hipMemcpyHostToDevice));
+    HIPCK(h2d(h->stream, (void*)d.self, &d, sizeof(Dev)));
   }
   return SWIM_OK;
 }

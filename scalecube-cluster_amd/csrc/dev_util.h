@@ -8,6 +8,29 @@ namespace swim {
 
 __device__ __forceinline__ void set_err(const Dev& d, uint32_t bit) { atomicOr(d.err, bit); }
 
+// The workgroup that finishes last on `ctr` (nblocks workgroups) sees every other workgroup's plain stores. The
+// hand-off of MI355X_MICROARCH.md / cdna_hip_programming.md §6 Guideline 16 (counter form): every wave drains its
+// stores, then one lane releases at agent scope (write-back of its XCD's L2) and draws a ticket; the last one acquires
+// (invalidates its CU's L1) before any wave of it loads. Without the per-wave drain and the explicit waits, a
+// producer on another XCD can still hold its stores in L2 when the last workgroup reads them (ROCm 7.2 may also drop
+// the fence's own wait).
+__device__ __forceinline__ bool last_block(uint32_t* ctr, uint32_t nblocks) {
+  __shared__ bool last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblocks - 1u;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  return last;
+}
+
 // 16-B row loads
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint4 ld_c4(const uint32_t* p) { return *(const uint4*)p; }

@@ -150,8 +150,9 @@ struct Dev {
   uint32_t *rc_cnt, *rc_off, *rc_fill;  // [N]
   uint32_t* scan_part;                  // block partial sums of the exclusive scan
   uint32_t* rc_slot;  // [RCAP] sorted by member then gossip id
-  uint32_t* rc_keep;   // [RCAP] per member segment: positions of the receipts k_receipt_filter kept, ascending
-  uint32_t *rc_nkeep, *rc_nuser;  // [N] kept receipts, user-gossip receipts of the segment
+  uint32_t* rc_ndrop;  // [N] receipts k_gossip_apply did not route (they cannot change the row): counted in P4
+  uint32_t* dead_rx;   // [N] tick whose P4 receives a DEAD membership record (set by the delivering sender)
+  uint32_t* leaving;   // [N] 1 once the member's leave was requested (its own DEAD record may travel in SYNC data)
   uint64_t* rc_key;   // [RCAP] gossip id sort key
   uint32_t* rc_slot2;  // [RCAP] merge scratch of k_seg_sort (segments above SORT_MAX)
   uint64_t* rc_key2;

@@ -13,7 +13,7 @@ __global__ void k_pack_a_chunks(Dev d, uint32_t b);
 __global__ void k_unpack_a(Dev d, uint32_t k, uint32_t end);
 __global__ void k_pack_b(Dev d);
 __global__ void k_unpack_b_sweeps(Dev d, uint32_t k);
-__global__ void k_unpack_b_deliv(Dev d);
+__global__ void k_unpack_b_deliv(Dev d, uint32_t k);
 __global__ void k_round_reset(Dev d);
 
 // ------------------------------------------------------------------------------------------------------------
@@ -282,56 +282,6 @@ __global__ void __launch_bounds__(256) k_seg_sort(uint64_t* key, uint32_t* val, 
       __syncthreads();
     }
   }
-}
-
-// P4 pre-filter (onMembershipGossip -> updateMembership, MembershipProtocolImpl.java:401-408,475-485): a first receipt
-// whose record does not override the receiver's row as it stands at the start of the next tick cannot override it
-// later in that tick either, as long as the row keeps its presence (rows only move up the isOverrides order, except a
-// removal by DEAD, and an absent row accepts only ALIVE). k_member_tick walks the kept receipts and falls back to the
-// whole segment from the first presence change on (member.hip P4). One block per member segment; a block-wide
-// compaction keeps the gossip-id order. User gossips are always kept (each one emits a GOSSIP event).
-__global__ void __launch_bounds__(256) k_receipt_filter(Dev d) {
-  __shared__ uint32_t sc[256];
-  __shared__ uint32_t base_sh;
-  for (uint32_t t = d.lo + blockIdx.x; t < d.hi; t += gridDim.x) {
-    const uint32_t n = d.rc_cnt[t];
-    if (n == 0) continue;
-    const uint32_t off = d.rc_off[t];
-    const uint32_t* rk = d.rowk + lidx(d, t) * d.NS;
-    uint32_t kept = 0, users = 0;
-    for (uint32_t b0 = 0; b0 < n; b0 += 256) {
-      const uint32_t i = b0 + threadIdx.x;
-      uint32_t keep = 0, user = 0;
-      if (i < n) {
-        const uint32_t g = d.rc_slot[off + i], subj = d.slot_subj[g];
-        if (subj == USER_SUBJ) {
-          keep = user = 1;
-        } else {
-          const uint64_t key = d.slot_key[g];
-          const uint32_t r0 = rk[subj];
-          keep = overrides(rec_status(key), rec_inc(key), r0 & 3u, r0 >> 2) ? 1u : 0u;
-        }
-      }
-      sc[threadIdx.x] = keep | (user << 16);
-      __syncthreads();
-      for (uint32_t o = 1; o < 256; o <<= 1) {
-        const uint32_t v = threadIdx.x >= o ? sc[threadIdx.x - o] : 0u;
-        __syncthreads();
-        sc[threadIdx.x] += v;
-        __syncthreads();
-      }
-      const uint32_t incl = sc[threadIdx.x], tot = sc[255];
-      if (keep) d.rc_keep[off + kept + (incl & 0xFFFFu) - 1] = i;
-      kept += tot & 0xFFFFu;
-      users += tot >> 16;
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-      d.rc_nkeep[t] = kept;
-      d.rc_nuser[t] = users;
-    }
-  }
-  (void)base_sh;
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -1027,6 +977,34 @@ __global__ void __launch_bounds__(64) k_gossip_send_slow(const Dev* __restrict__
   if (sends) atomicAdd(&d.ctr[C_G], sends);
 }
 
+// P4 pre-filter (onMembershipGossip -> updateMembership, MembershipProtocolImpl.java:401-408,475-485). A first
+// receipt is routed to P4 of tick k4 unless it provably cannot change t's row there: its record does not override
+// the row as it stands now (= at the start of tick k4), the row is present, and the row cannot be removed before the
+// receipt in that tick. Present rows only move up the isOverrides order except through a removal, so a record that
+// does not override the start row overrides no later one. A removal needs a DEAD record: in P4 another receipt
+// (k_stamp_dead set dead_rx[t] = k4), or in P1 a leaver's own record in SYNC data (leaving[subject]); after one the
+// row is absent or re-added at any incarnation (an absent row accepts any ALIVE, MembershipRecord.java:67-69), so
+// every receipt is kept then. An absent start row keeps every receipt (the row may become present earlier in the
+// tick). User gossips are always routed (each one emits a GOSSIP event).
+__device__ __forceinline__ bool receipt_matters(const Dev& d, uint32_t t, uint32_t g, uint32_t k4) {
+  const uint32_t subj = d.slot_subj[g];
+  if (subj == USER_SUBJ || (d.exp & 8)) return true;  // SWIM_EXP & 8: route every receipt (debugging aid)
+  const uint64_t key = d.slot_key[g];
+  const uint32_t r0 = d.rowk[lidx(d, t) * d.NS + subj], s1 = rec_status(key);
+  if ((r0 & 3u) == ST_ABSENT || overrides(s1, rec_inc(key), r0 & 3u, r0 >> 2)) return true;
+  return d.dead_rx[t] == k4 || d.leaving[subj];
+}
+
+// the deliveries of DEAD membership records: their targets receive one in P4 of tick k + lat (receipt_matters)
+__global__ void k_stamp_dead(Dev d, uint32_t k) {
+  const uint32_t n = *d.deliv_n < d.DCAP ? *d.deliv_n : d.DCAP;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint64_t v = d.deliv[i];
+    const uint32_t g = (uint32_t)(v >> 32), t = (uint32_t)v;
+    if (rec_status(d.slot_key[g]) == ST_DEAD && d.slot_subj[g] != USER_SUBJ) d.dead_rx[t] = k + d.lat;
+  }
+}
+
 // first receipts (onGossipReq :176-180): create the holder state at tick k + lat and queue the record for P4
 __global__ void k_gossip_apply(Dev d, uint32_t k) {
   uint32_t n = *d.deliv_n < d.DCAP ? *d.deliv_n : d.DCAP;
@@ -1045,6 +1023,10 @@ __global__ void k_gossip_apply(Dev d, uint32_t k) {
     atomicAdd(&d.held[t], 1u);
     atomicAdd(&d.slot_holders[g], 1);
     if (t < d.lo || t >= d.hi) continue;  // P4 of another shard's member
+    if (!receipt_matters(d, t, g, k + d.lat)) {  // counted as a record compare in P4, nothing else
+      atomicAdd(&d.rc_ndrop[t], 1u);
+      continue;
+    }
     uint32_t ri = wave_append(d.rc_n);
     if (ri < d.RCAP)
       d.rc_raw[ri] = ((uint64_t)t << 32) | g;
@@ -1181,6 +1163,7 @@ void launch_gossip(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   hipLaunchKernelGGL(k_gossip_send_slow, dim3(64), dim3(64), 0, st, d.self, k);  // rare; ~14 KB of stack per lane
   hipLaunchKernelGGL(k_gossip_replay, dim3(2048), dim3(256), 0, st, d.self, k);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[5], st);
+  hipLaunchKernelGGL(k_stamp_dead, dim3(1024), dim3(256), 0, st, d, k);
   hipLaunchKernelGGL(k_gossip_apply, dim3(1024), dim3(256), 0, st, d, k);
   launch_receipt_routing(d, st);
   hipLaunchKernelGGL(k_gossip_free, dim3(1024), dim3(256), 0, st, d, d.active, d.nactive);
@@ -1197,7 +1180,6 @@ static void launch_receipt_routing(const Dev& d, hipStream_t st) {
                      d.rc_slot, d.rc_key);
   hipLaunchKernelGGL(k_seg_sort, dim3(1024), dim3(256), 0, st, d.rc_key, d.rc_slot, d.rc_key2, d.rc_slot2, d.rc_off,
                      d.rc_cnt, d.N, d.rc_n);
-  hipLaunchKernelGGL(k_receipt_filter, dim3(2048), dim3(256), 0, st, d);
 }
 
 void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
@@ -1239,7 +1221,8 @@ void launch_tick_c(const Dev& d, uint32_t k, void* stream, bool gossip) {
   hipStream_t st = (hipStream_t)stream;
   if (!gossip) return;  // k_unpack_a closed the tick
   hipLaunchKernelGGL(k_unpack_b_sweeps, dim3(64, d.W), dim3(256), 0, st, d, k);
-  hipLaunchKernelGGL(k_unpack_b_deliv, dim3(64, d.W), dim3(256), 0, st, d);
+  hipLaunchKernelGGL(k_unpack_b_deliv, dim3(64, d.W), dim3(256), 0, st, d, k);
+  hipLaunchKernelGGL(k_stamp_dead, dim3(1024), dim3(256), 0, st, d, k);
   hipLaunchKernelGGL(k_gossip_apply, dim3(1024), dim3(256), 0, st, d, k);
   launch_receipt_routing(d, st);
   hipLaunchKernelGGL(k_gossip_free, dim3(1024), dim3(256), 0, st, d, d.active, d.nactive);

@@ -33,7 +33,7 @@ struct ML {
   uint32_t* trk;  // subjects whose key changed in this tick's P1 (several payloads only); ntrk > TRK: overflowed
   uint32_t ntrk;
   bool trk_on;
-  bool pchg;  // a row changed presence (absent <-> present) in this tick: P4 then walks every receipt
+
 };
 
 __device__ __forceinline__ uint32_t draw(ML& L, uint32_t stream) {
@@ -76,7 +76,6 @@ __device__ __forceinline__ void row_put(ML& L, uint32_t s, uint64_t v) {
   const uint32_t k = key32(v);
   if (rec_inc(v) >= INC_LIMIT) set_err(*L.d, E_INC);
   if (L.pend != NEVER && L.rk[s] != k) cow(L);
-  if (((L.rk[s] & 3u) == ST_ABSENT) != ((k & 3u) == ST_ABSENT)) L.pchg = true;
   if (L.trk_on && L.rk[s] != k && L.ntrk <= TRK) {  // merge_payload re-checks it against the later payloads
     bool seen = false;
     for (uint32_t i = 0; i < L.ntrk; ++i) seen |= L.trk[i] == s;
@@ -670,15 +669,21 @@ __device__ __forceinline__ void merge_payload(ML& L, uint32_t mi, uint32_t reaso
 // control path of k_member_tick this tick, and its work class: 1 = a ping is due and nothing else, 2 = only
 // request-state events (ping hops, ack arrivals, timeouts), 3 = both, 0 = anything else (SYNC receipt, gossip
 // receipts or round, timers, host requests, start).
-__device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t k, uint32_t& cls) {
+__device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t k, uint32_t& cls, uint32_t& drops) {
   // A dead member does nothing itself, but the remote hops of its in-flight requests still run at the live
   // responders (their sends fail against the dead issuer), so those hops are still evaluated for the counters.
   // every word is loaded up front (no short-circuit chain of dependent loads); the SoA loads coalesce per wave
   const uint32_t mh = d.m_head[(size_t)((k - 1) & 1) * d.N + m], rc = d.rc_cnt[m], pi = d.pending_inc[m],
                  ne = d.next_evt[m], tm = d.timerMin[m], np = d.nextPing[m], ns = d.nextSync[m], inf = d.initFlags[m],
-                 ng = d.nextGossip[m], held = d.held[m], dt = d.dead_tick[m], st = d.start_tick[m];
+                 ng = d.nextGossip[m], held = d.held[m], dt = d.dead_tick[m], st = d.start_tick[m],
+                 nd = d.rc_ndrop[m];
   const bool dead = k >= dt;
   cls = 0;
+  drops = 0;
+  if (nd) {  // receipts that could not change the row: P4's record compares (none for a dead member)
+    d.rc_ndrop[m] = 0;
+    if (!dead) drops = nd;
+  }
   if (dead) {
     d.rc_cnt[m] = 0;
     d.rc_fill[m] = 0;
@@ -757,7 +762,6 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   L.trk = d.trk + li * TRK;
   L.ntrk = 0;
   L.trk_on = false;
-  L.pchg = false;
 
   // ---- P0 host requests: updateIncarnation (MembershipProtocolImpl.java:178-190), then leaveCluster (:197-206) ----
   const uint32_t preq = dead ? 0u : d.pending_inc[m];
@@ -1031,37 +1035,23 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   }
 
   // ---- P4 gossip first receipts in gossip-id order -> onMembershipGossip (:401-408) ----
-  // k_receipt_filter kept the receipts that can override the row (and every user gossip); from the first presence
-  // change of any row in this tick on, every receipt of the segment is walked (see k_receipt_filter)
+  // only the receipts that can change the row were routed (receipt_matters, kernels.hip); the others were counted
+  // as record compares by the triage
   {
-    const uint32_t off = d.rc_off[m], n = d.rc_cnt[m];
+    uint32_t off = d.rc_off[m], n = d.rc_cnt[m];
     if (n) {
       d.rc_cnt[m] = 0;  // the next receipt routing counts from zero
       d.rc_fill[m] = 0;
-      L.c[C_R] += n - d.rc_nuser[m];  // every membership receipt is a record compare
-      auto receipt = [&](uint32_t q) {
-        const uint32_t g = d.rc_slot[off + q];
-        const uint64_t key = d.slot_key[g];
-        if (d.slot_subj[g] == USER_SUBJ) {  // sink.next -> ClusterImpl.listenGossips (:213-216), not membership
-          emit_event(L, 3, (uint32_t)(d.slot_gid[g] >> 32), (uint32_t)key, (uint32_t)(key >> 32));
-          return;
-        }
-        update_membership(L, d.slot_subj[g], rec_status(key), rec_inc(key), R_GOSSIP, -1);
-      };
-      uint32_t from = 0;  // first position of the whole segment still to walk (n: none)
-      if (!L.pchg) {
-        const uint32_t nk = d.rc_nkeep[m];
-        from = n;
-        for (uint32_t j = 0; j < nk; ++j) {
-          const uint32_t q = d.rc_keep[off + j];
-          receipt(q);
-          if (L.pchg) {
-            from = q + 1;
-            break;
-          }
-        }
+    }
+    for (uint32_t q = 0; q < n; ++q) {
+      uint32_t g = d.rc_slot[off + q];
+      uint64_t key = d.slot_key[g];
+      if (d.slot_subj[g] == USER_SUBJ) {  // sink.next -> ClusterImpl.listenGossips (:213-216), not membership
+        emit_event(L, 3, (uint32_t)(d.slot_gid[g] >> 32), (uint32_t)key, (uint32_t)(key >> 32));
+        continue;
       }
-      for (uint32_t q = from; q < n; ++q) receipt(q);
+      L.c[C_R]++;
+      update_membership(L, d.slot_subj[g], rec_status(key), rec_inc(key), R_GOSSIP, -1);
     }
   }
 
@@ -1203,10 +1193,15 @@ __global__ void __launch_bounds__(256) k_member_tick(const Dev* __restrict__ dp,
   const Dev& d = *dp;  // global, not kernarg: taking its address must not copy ~1 KB into per-lane scratch
   __shared__ uint32_t wc[4][4];  // [wave][class] busy members
   __shared__ uint32_t list[256];
-  __shared__ bool last;
   const uint32_t m = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t cls = 0;
-  const bool busy = m < d.hi && member_triage(d, m, k, cls);
+  uint32_t cls = 0, drops = 0;
+  const bool busy = m < d.hi && member_triage(d, m, k, cls, drops);
+  {  // the triage's record compares, one atomic per wave
+    uint32_t v = drops;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(&d.ctr[C_R], (unsigned long long)v);
+  }
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t b0 = __ballot(busy && cls == 0), b1 = __ballot(busy && cls == 1), b2 = __ballot(busy && cls == 2),
                  b3 = __ballot(busy && cls == 3);
@@ -1245,14 +1240,7 @@ __global__ void __launch_bounds__(256) k_member_tick(const Dev* __restrict__ dp,
     }
   }
   if (!flag) return;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    last = atomicAdd(d.mdone, 1u) == gridDim.x - 1u;
-  }
-  __syncthreads();
-  if (!last || threadIdx.x != 0) return;
-  __threadfence();
+  if (!last_block(d.mdone, gridDim.x) || threadIdx.x != 0) return;
   *d.mdone = 0;
   tick_flag(d, k);
 }

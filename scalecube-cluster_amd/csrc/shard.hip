@@ -19,18 +19,6 @@
 
 namespace swim {
 
-// the block that finishes last (all earlier blocks' stores are visible to it after the fence)
-__device__ __forceinline__ bool last_block(uint32_t* ctr, uint32_t nblocks) {
-  __shared__ bool last;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    last = atomicAdd(ctr, 1u) == nblocks - 1u;
-  }
-  __syncthreads();
-  if (last) __threadfence();
-  return last;
-}
 
 __device__ __forceinline__ uint64_t sync_entry_bytes(const Dev& d) { return sizeof(SyncMsg) + 8 + 8ull * d.MW; }
 
@@ -293,7 +281,7 @@ __global__ void k_unpack_b_sweeps(Dev d, uint32_t k) {
 }
 
 // peers' first receipts join this shard's delivery list, deduplicated by the PENDING bit like local ones
-__global__ void k_unpack_b_deliv(Dev d) {
+__global__ void k_unpack_b_deliv(Dev d, uint32_t k) {
   const uint32_t p = blockIdx.y;
   if (p == d.rank || (d.xb_rcnt[p] & XCNT_MASK) < 16) return;
   const uint8_t* R = d.xb_recv + (size_t)p * d.XB_PEER;
