@@ -105,8 +105,9 @@ def cpu_baseline(a, members, periods):
     one, dt1 = _oracle_rate(a, lib, members, max(1, periods // 4), 1)
     allc, dtn = _oracle_rate(a, lib, members, periods, cores)
     os.environ.pop("SWIMREF_THREADS", None)
-    note = {"c3": "per-member work grows ~linearly with N (SYNC payloads), so at 100k it is ~10x slower per "
-                  "member·period",
+    note = {"c3": "per-member work grows ~linearly with N (SYNC payloads); the full 100k size is not sampled here: "
+                  "the oracle holds ~20 B per member pair (~200 GB of host RAM at 100k) and its preconverged setup "
+                  "alone takes minutes (one-off measurement: profiles/r02_cpu_baseline_c3_100k.json)",
             "c2": "per-member gossip load grows ~N (SYNC re-spread storm), so at 10k it is far slower per member·period",
             "c5": "per-member rumor load grows ~N at 1 % churn, so at full N it is slower per member·period"}[a.workload]
     return {"value": allc, "unit": "member·periods/s", "cores": cores, "kind": "port",
@@ -184,6 +185,7 @@ def main():
 
     if rank == 0:
         n = a.members
+        ticks_per_period = cfg.cluster.pingInterval // cfg.tick_ms
         merges = d["sync_merges"]
         diff_s = d["diff_ns"] * 1e-9
         launches = max(1, d["diff_launches"])
@@ -204,21 +206,25 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "u64",
+            "dtype": "u32",  # record keys: inc << 2 | status (30-bit incarnation, SEMANTICS.md §8), u32 list entries
             "data": "synthetic (PRECONVERGED full views, seeded Philox selector)",
             "config": {"workload": workload_name(a, n),
-                       "members": n, "periods_per_step": 1, "ticks_per_period": 10,
+                       "members": n, "periods_per_step": 1, "ticks_per_period": ticks_per_period,
                        "parallelism": f"row-sharded x{world} ({a.transport})" if world > 1 else "single-gpu"},
             "roofline": {"bound": "hbm", "kernel": "k_sync_diff", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                          "algorithmic_bytes_per_launch": bytes_per_launch,
                          "avg_launch_us": diff_s * 1e6 / launches,
                          "traffic": traffic_from_profiles(n) if world == 1 else None},
-            "kernel_time_share": {"k_sync_diff": diff_s / launches * 10 * a.steps / dt},  # the other kernels: profiles/*kernel_stats*
+            # the engine times a sample of the launches (every 5th tick on one GPU): average x launches per period
+            "kernel_time_share": {"k_sync_diff": diff_s / launches * ticks_per_period * a.steps / dt},  # others: profiles/*kernel_stats*
             "whole_step_algorithmic_GBps": B / dt / 1e9,
             "counters": {k: d[k] for k in ("record_compares", "row_writes", "messages", "gossip_messages", "events",
                                            "sync_merges")},
             "device_bytes": ctr["device_bytes"],
+            # since the handle was created (warm-up included): a profiler pass over the whole process prices its
+            # k_sync_diff traffic against 8 B x N x these merges (tools/make_profiles.py)
+            "run_totals": {"sync_merges": ctr["sync_merges"], "ticks": ctr["tick"]},
             "exchange_ms_per_step": d["exchange_ns"] * 1e-6 / a.steps,
         }
         if a.workload != "c3":  # the gossip plane dominates: whole-step algorithmic bytes against HBM

@@ -59,7 +59,9 @@ extern "C" {
 
 /* flags */
 #define SWIM_FLAG_RECORD_EVENTS 1u /* keep full event records for swim_drain_events (hashes are always kept) */
-#define SWIM_FLAG_PROFILE 2u       /* time k_sync_diff with HIP events on the engine stream (swim_counters diff_ns) */
+#define SWIM_FLAG_PROFILE 2u       /* time a SAMPLE of the k_sync_diff launches with HIP events on the engine stream:
+                                      one GPU: the launches of ticks k % 5 == 0; sharded or with PROFILE_ALL: every
+                                      launch (swim_counters diff_ns / diff_launches / diff_msgs cover the same set) */
 #define SWIM_FLAG_PROFILE_ALL 4u   /* also time k_member_tick and k_gossip_send (member_ns, gossip_ns); ~10 % slower */
 
 typedef struct swim_config {
@@ -134,7 +136,8 @@ typedef struct swim_counters {
   uint64_t sync_merges;       /* SYNC + SYNC_ACK payloads merged */
   /* engine-side measurements (0 on the oracle); *_ns need SWIM_FLAG_PROFILE */
   uint64_t device_bytes;  /* HBM allocated for the simulation state */
-  uint64_t diff_ns;       /* k_sync_diff: SYNC payload x receiver-row stream */
+  uint64_t diff_ns;       /* k_sync_diff time of the TIMED launches only (see SWIM_FLAG_PROFILE): average per launch =
+                             diff_ns / diff_launches; a total needs x (all launches / timed launches) */
   uint64_t member_ns;     /* k_member_tick: per-member protocol control */
   uint64_t gossip_ns;     /* k_gossip_send: gossip data plane */
   uint64_t diff_launches;

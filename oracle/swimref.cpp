@@ -1105,7 +1105,8 @@ __attribute__((visibility("default"))) int swim_create(const swim_config* cfg, s
   s.group.assign(s.N, 0);
   s.md_version.assign(s.N, 0);
   s.members.resize(s.N);
-  for (uint32_t m = 0; m < s.N; ++m) {
+  // members are independent (every draw is keyed by the member id): worker threads take interleaved member ranges
+  auto init_member = [&](uint32_t m) {
     Member& mb = s.members[m];
     mb.sim = &s;
     mb.id = m;
@@ -1153,6 +1154,15 @@ __attribute__((visibility("default"))) int swim_create(const swim_config* cfg, s
       mb.nextSync = 1 + s.init_draw(m, 3, 0) % s.sync_t;
       if (c.mode == SWIM_MODE_RUMOR) mb.nextPing = mb.nextSync = NEVER;  // gossip layer only (SEMANTICS.md §9)
     }
+  };
+  if (s.pool) {
+    const uint32_t T = (uint32_t)s.threads;
+    s.pool->run([&](int w) {
+      for (uint32_t b = (uint32_t)w * 64; b < s.N; b += 64 * T)
+        for (uint32_t m = b; m < std::min(s.N, b + 64); ++m) init_member(m);
+    });
+  } else {
+    for (uint32_t m = 0; m < s.N; ++m) init_member(m);
   }
   *out = h;
   return SWIM_OK;

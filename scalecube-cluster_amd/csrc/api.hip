@@ -276,7 +276,7 @@ int build(swim_handle* h) {
   A(d.tsize, N) A(d.fdLen, N) A(d.gLen, N) A(d.fdPeriod, N) A(d.gPeriod, N) A(d.gCounter, N) A(d.nextPing, N)
   A(d.nextGossip, N) A(d.nextSync, N) A(d.cidCnt, N) A(d.syncSeq, N) A(d.evSeq, N) A(d.held, N) A(d.timerMin, N)
   A(d.initFlags, N) A(d.initDeadline, N) A(d.initCidBase, N) A(d.initN, N) A(d.firstGossip, N) A(d.nsub, N)
-  A(d.npath, N) A(d.nfetch, N) A(d.pingIdx, N) A(d.remoteIdx, N) A(d.sel, N * 8) A(d.evHash, N)
+  A(d.npath, N) A(d.nfetch, N) A(d.fnext, N) A(d.pingIdx, N) A(d.remoteIdx, N) A(d.sel, N * 8) A(d.evHash, N)
   const uint64_t NL = d.NL;  // per-observer arrays: this shard's rows only
   A(d.rowk, NL * d.NS) A(d.rowa, NL * d.NS) A(d.fdl, NL * d.LCAP) A(d.gl, NL * d.LCAP)
   A(d.subs, NL * SUBCAP * 4) A(d.paths, NL * PATHCAP * 5) A(d.fetch, NL * d.FCAP * FREC) A(d.groups, NL * d.GRCAP * GREC)
@@ -880,6 +880,12 @@ int swim_step(swim_handle* h, uint32_t n) {
     h->tick++;
   }
   int rc = check_err(h);
+  if (rc == SWIM_OK && (d.exp & 16)) {  // timing experiments: member-kernel shader cycles per phase since the last step
+    unsigned long long c[5];
+    HIPCK(hipMemcpy(c, d.ctr + 8, sizeof(c), hipMemcpyDeviceToHost));
+    HIPCK(hipMemset(d.ctr + 8, 0, sizeof(c)));
+    fprintf(stderr, "exp: member cycles P0+P1 %llu P2+P3 %llu P4 %llu P5 %llu P6 %llu\n", c[0], c[1], c[2], c[3], c[4]);
+  }
   if (rc == SWIM_OK && (d.exp & 4)) {  // timing experiments: gossip-send work counters since the last step
     unsigned long long c[5];
     HIPCK(hipMemcpy(c, d.ctr + 8, sizeof(c), hipMemcpyDeviceToHost));

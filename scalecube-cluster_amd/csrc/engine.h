@@ -99,7 +99,8 @@ struct Dev {
 
   // ---- per member scalars ----
   uint32_t *tsize, *fdLen, *gLen, *fdPeriod, *gPeriod, *gCounter, *nextPing, *nextGossip, *nextSync, *cidCnt, *syncSeq,
-      *evSeq, *held, *timerMin, *initFlags, *initDeadline, *initCidBase, *initN, *firstGossip, *nsub, *npath, *nfetch;
+      *evSeq, *held, *timerMin, *initFlags, *initDeadline, *initCidBase, *initN, *firstGossip, *nsub, *npath, *nfetch,
+      *fnext;  // [N] earliest tick at which a pending metadata fetch needs the member (NEVER: none)
   int32_t *pingIdx, *remoteIdx;
   uint32_t* sel;  // [N][8]
   uint64_t* evHash;

@@ -44,6 +44,7 @@ __global__ void k_init_members(Dev d) {
   d.timerMin[m] = NEVER;
   d.initFlags[m] = d.initDeadline[m] = d.initCidBase[m] = d.initN[m] = 0;
   d.nsub[m] = d.npath[m] = d.nfetch[m] = 0;
+  d.fnext[m] = NEVER;
   d.pingIdx[m] = 0;
   d.remoteIdx[m] = pre ? 0 : -1;
   for (int i = 0; i < 8; ++i) d.sel[(size_t)m * 8 + i] = 0;
@@ -380,10 +381,10 @@ __global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b, uint32_t t
       uint32_t totc = scan[255];
       if (threadIdx.x == 0) {
         uint32_t bo = atomicAdd(d.pool_used, totc);
-        if (bo + totc > d.POOLCAP) {
+        if (bo + totc > d.POOLCAP) {  // no room: nothing of this item is written (the error aborts the step)
           atomicOr(d.err, E_POOL);
           totc = 0;
-          bo = 0;
+          bo = NEVER;
         }
         base = bo;
         uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NCHUNK + c) * 2;
@@ -393,7 +394,7 @@ __global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b, uint32_t t
       }
       __syncthreads();
       uint32_t o = base + incl - nc;
-      if (o + nc <= d.POOLCAP)
+      if (base != NEVER)  // (an overflowed item must not overwrite other items' candidates)
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if (mask & (1u << j)) d.pool[o++] = ((uint64_t)(s0 + j) << 34) | key34(p[j]);

@@ -21,6 +21,7 @@ struct ML {
   uint32_t m, k, N;
   uint32_t tsize, fdLen, gLen, fdPeriod, gPeriod, gCounter, nextPing, nextGossip, nextSync, cidCnt, syncSeq, evSeq,
       held, timerMin, initFlags, initDeadline, initCidBase, initN, nsub, npath, nfetch;
+  uint32_t fnext;  // earliest tick at which a pending fetch needs the member (hop, arrival or timeout); NEVER: none
   int32_t pingIdx, remoteIdx;
   uint32_t sel[8];
   uint64_t evHash;
@@ -345,6 +346,7 @@ __device__ __forceinline__ void fetch_md(ML& L, uint32_t subj, uint32_t st, uint
   f[5] = L.k + d.md_t;
   f[6] = L.k + d.lat;
   f[7] = NONE32;
+  L.fnext = min(L.fnext, min(f[5], f[6]));
   if (g >= 0) grp(L, g)[4]++;
 }
 
@@ -707,7 +709,7 @@ __device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t
       }
     }
   }
-  if (dead && d.npath[m] == 0 && d.nfetch[m] == 0) {
+  if (dead && d.npath[m] == 0 && (d.nfetch[m] == 0 || d.fnext[m] > k)) {
     d.tround[m] = 0;
     return false;
   }
@@ -742,6 +744,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   L.nsub = d.nsub[m];
   L.npath = d.npath[m];
   L.nfetch = d.nfetch[m];
+  L.fnext = d.fnext[m];
   L.pingIdx = d.pingIdx[m];
   L.remoteIdx = d.remoteIdx[m];
   for (int i = 0; i < 8; ++i) L.sel[i] = d.sel[(size_t)m * 8 + i];
@@ -762,6 +765,15 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   L.trk = d.trk + li * TRK;
   L.ntrk = 0;
   L.trk_on = false;
+  // SWIM_EXP & 16 (timing experiment): shader cycles per phase summed over members, ctr[8..12]
+  const bool prof = (d.exp & 16) != 0;
+  unsigned long long tp = prof ? clock64() : 0;
+  auto lap = [&](int slot) {
+    if (!prof) return;
+    const unsigned long long t = clock64();
+    atomicAdd(&d.ctr[8 + slot], t - tp);
+    tp = t;
+  };
 
   // ---- P0 host requests: updateIncarnation (MembershipProtocolImpl.java:178-190), then leaveCluster (:197-206) ----
   const uint32_t preq = dead ? 0u : d.pending_inc[m];
@@ -884,6 +896,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
     L.trk_on = false;
   }
 
+  lap(0);  // P0 + P1
   // ---- P2 FD: remote hops of pending pings, then PING_ACK arrivals in cid order ----
   if (L.npath) {
     uint32_t arr[PATHCAP];
@@ -975,60 +988,78 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   }
 
   // ---- P3 metadata: response hops at the subject, then GET_METADATA_RESP arrivals in cid order ----
-  if (L.nfetch) {
-    for (uint32_t q = 0; q < L.nfetch; ++q) {  // onMetadataRequest at the subject (MetadataStoreImpl.java:202-241)
+  // One pass over the pending fetches (kept in cid order), only when one of them is due: the response hops due now
+  // (onMetadataRequest at the subject, MetadataStoreImpl.java:202-241) and the responses arriving now, compacted in
+  // place. A hop reads nothing an arrival writes (its loss draw is keyed by the message, SEMANTICS.md §2), so one pass
+  // runs both. A dead issuer keeps only its pending hops (their responses still count as sent at the live subject).
+  if (L.nfetch && L.fnext <= k) {
+    uint32_t w = 0, fn = NEVER;
+    const uint32_t nf = L.nfetch;  // no fetch is issued in P3
+    for (uint32_t q = 0; q < nf; ++q) {
       uint32_t* f = L.fetch + (size_t)q * FREC;
-      uint32_t stage = f[3] >> 24;
-      if (stage == 1 && f[6] == k) {
-        uint32_t subj = f[1];
+      uint4 lo = *(const uint4*)f, hi = *(const uint4*)(f + 4);  // cnt subj inc w3 | g deadline hop meta
+      uint32_t stage = lo.w >> 24;
+      bool keep = true, mod = false;
+      if (stage == 1 && hi.z == k) {
+        mod = true;
+        const uint32_t subj = lo.y;
         if (dead_at(d, subj, k)) {
-          f[3] &= 0x00FFFFFFu;
+          lo.w &= 0x00FFFFFFu;
         } else {
           L.c[C_M]++;
-          if (lost_msg(d, K_GMD_RESP, subj, m, k, m, f[0])) {
+          if (lost_msg(d, K_GMD_RESP, subj, m, k, m, lo.x)) {
             L.c[C_LOST]++;
-            f[3] &= 0x00FFFFFFu;
+            lo.w &= 0x00FFFFFFu;
           } else {
-            f[3] = (f[3] & 0x00FFFFFFu) | (2u << 24);
-            f[6] = k + d.lat;
-            f[7] = d.md_version[subj];
+            lo.w = (lo.w & 0x00FFFFFFu) | (2u << 24);
+            hi.z = k + d.lat;
+            hi.w = d.md_version[subj];
           }
         }
+        keep = !dead || (lo.w >> 24) == 1;
+      } else if (stage == 2 && hi.z == k) {
+        keep = false;
+        if (!dead) {  // doOnSuccess (:563-567, :576-581): updateMetadata then sink.next
+          const uint32_t subj = lo.y, inc = lo.z, w3 = lo.w, meta = hi.w;
+          const int g = (int)hi.x;
+          const uint32_t st = w3 & 0xFF, reason = (w3 >> 8) & 0xFF, added = (w3 >> 16) & 0xFF;
+          uint64_t v = row_ld(L, subj);
+          uint32_t oldm = known_meta(L, subj, v);
+          L.ra[subj] = aux32(v | META_BIT);
+          const uint32_t u = d.md_uidx[subj];
+          if (u != NONE32) d.md_ver[lidx(d, m) * MDU + u] = meta;
+          if (added)
+            emit_event(L, 0, subj, NONE32, meta);
+          else
+            emit_event(L, 2, subj, oldm, meta);
+          if (g >= 0) grp(L, g)[4]--;
+          finish(L, g, false);
+          do_finally(L, subj, st, inc, reason);
+        }
+      } else if (dead) {
+        keep = stage == 1;
+      }
+      if (keep) {
+        if (w != q || mod) {
+          uint32_t* o = L.fetch + (size_t)w * FREC;
+          *(uint4*)o = lo;
+          *(uint4*)(o + 4) = hi;
+        }
+        w++;
+        const uint32_t ns = lo.w >> 24;  // the next due event (P5 recomputes it after its own pass)
+        fn = min(fn, dead ? (ns == 1 ? hi.z : NEVER) : (ns != 0 ? min(hi.y, hi.z) : hi.y));
       }
     }
-    uint32_t q = 0;
-    while (!dead && q < L.nfetch) {
-      uint32_t* f = L.fetch + (size_t)q * FREC;
-      if ((f[3] >> 24) == 2 && f[6] == k) {
-        uint32_t cnt = f[0], subj = f[1], inc = f[2], w3 = f[3], meta = f[7];
-        int g = (int)f[4];
-        (void)cnt;
-        for (uint32_t r = q + 1; r < L.nfetch; ++r)
-          for (uint32_t x = 0; x < FREC; ++x) L.fetch[(size_t)(r - 1) * FREC + x] = L.fetch[(size_t)r * FREC + x];
-        L.nfetch--;
-        uint32_t st = w3 & 0xFF, reason = (w3 >> 8) & 0xFF, added = (w3 >> 16) & 0xFF;
-        // doOnSuccess (:563-567, :576-581): updateMetadata then sink.next
-        uint64_t v = row_ld(L, subj);
-        uint32_t oldm = known_meta(L, subj, v);
-        L.ra[subj] = aux32(v | META_BIT);
-        const uint32_t u = d.md_uidx[subj];
-        if (u != NONE32) d.md_ver[lidx(d, m) * MDU + u] = meta;
-        if (added)
-          emit_event(L, 0, subj, NONE32, meta);
-        else
-          emit_event(L, 2, subj, oldm, meta);
-        if (g >= 0) grp(L, g)[4]--;
-        finish(L, g, false);
-        do_finally(L, subj, st, inc, reason);
-      } else {
-        ++q;
-      }
-    }
+    L.nfetch = w;
+    L.fnext = fn;
   }
 
+  lap(1);  // P2 + P3
   if (dead) {
     d.tround[m] = 0;
     d.npath[m] = L.npath;
+    d.nfetch[m] = L.nfetch;
+    d.fnext[m] = L.fnext;
     d.next_evt[m] = NEVER;
     for (int i = 0; i < 8; ++i) cnt[i] += L.c[i];
     return;
@@ -1055,6 +1086,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
     }
   }
 
+  lap(2);  // P4
   // ---- P5 timers ----
   if (L.nsub) {  // FD subscription timeouts in (cid, subscription) order
     uint32_t dcnt[SUBCAP], dkind[SUBCAP], dtgt[SUBCAP], nd = 0, w = 0;
@@ -1088,23 +1120,29 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
         on_fd_event(L, dtgt[q], ST_SUSPECT);  // ping-req timeout (:204-212)
     }
   }
-  if (L.nfetch) {  // metadata timeouts: onErrorResume(TimeoutException) swallows the event (:568,582)
-    uint32_t q = 0;
-    while (q < L.nfetch) {
+  if (L.nfetch && L.fnext <= k) {  // metadata timeouts: onErrorResume(TimeoutException) swallows the event (:568,582)
+    uint32_t w = 0, fn = NEVER;
+    const uint32_t nf = L.nfetch;  // no fetch is issued in P5
+    for (uint32_t q = 0; q < nf; ++q) {
       uint32_t* f = L.fetch + (size_t)q * FREC;
-      if (f[5] == k) {
-        uint32_t subj = f[1], inc = f[2], w3 = f[3];
-        int g = (int)f[4];
-        for (uint32_t r = q + 1; r < L.nfetch; ++r)
-          for (uint32_t x = 0; x < FREC; ++x) L.fetch[(size_t)(r - 1) * FREC + x] = L.fetch[(size_t)r * FREC + x];
-        L.nfetch--;
+      const uint4 lo = *(const uint4*)f, hi = *(const uint4*)(f + 4);
+      if (hi.y == k) {
+        const int g = (int)hi.x;
         if (g >= 0) grp(L, g)[4]--;
         finish(L, g, false);
-        do_finally(L, subj, w3 & 0xFF, inc, (w3 >> 8) & 0xFF);
-      } else {
-        ++q;
+        do_finally(L, lo.y, lo.w & 0xFF, lo.z, (lo.w >> 8) & 0xFF);
+        continue;
       }
+      fn = min(fn, (lo.w >> 24) != 0 ? min(hi.y, hi.z) : hi.y);
+      if (w != q) {
+        uint32_t* o = L.fetch + (size_t)w * FREC;
+        *(uint4*)o = lo;
+        *(uint4*)(o + 4) = hi;
+      }
+      w++;
     }
+    L.nfetch = w;
+    L.fnext = fn;
   }
   if ((L.initFlags & INIT_ACTIVE) && !(L.initFlags & INIT_RECEIVED) && k == L.initDeadline) {
     L.initFlags &= ~INIT_ACTIVE;  // .timeout(syncTimeout) (:241) -> doFinally -> schedulePeriodicSync
@@ -1130,6 +1168,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
     L.timerMin = nmin;
   }
 
+  lap(3);  // P5
   // ---- P6 periodic tasks (schedulePeriodically) ----
   if (k == L.nextPing) {
     L.nextPing += mc_ping_t(d, m);
@@ -1144,14 +1183,11 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
     do_sync(L);
   }
 
+  lap(4);  // P6
   uint32_t nev = NEVER;
   for (uint32_t q = 0; q < L.npath; ++q) nev = min(nev, L.paths[(size_t)q * 5 + 2]);
   for (uint32_t q = 0; q < L.nsub; ++q) nev = min(nev, L.subs[(size_t)q * 4 + 3]);
-  for (uint32_t q = 0; q < L.nfetch; ++q) {
-    const uint32_t* f = L.fetch + (size_t)q * FREC;
-    nev = min(nev, f[5]);
-    if ((f[3] >> 24) != 0) nev = min(nev, f[6]);
-  }
+  nev = min(nev, L.fnext);
   d.next_evt[m] = nev;
   d.tround[m] = L.tround;
   d.tsize[m] = L.tsize;
@@ -1175,6 +1211,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   d.nsub[m] = L.nsub;
   d.npath[m] = L.npath;
   d.nfetch[m] = L.nfetch;
+  d.fnext[m] = L.fnext;
   d.pingIdx[m] = L.pingIdx;
   d.remoteIdx[m] = L.remoteIdx;
   for (int i = 0; i < 8; ++i) d.sel[(size_t)m * 8 + i] = L.sel[i];

@@ -63,6 +63,7 @@ class SimConfig:
     latency_ticks: int = 1
     record_events: bool = False
     profile: bool = False
+    profile_all: bool = False  # SWIM_FLAG_PROFILE_ALL: every k_sync_diff launch timed (+ member / gossip kernels)
     gossip_slot_cap: int = 0
     pending_fetch_cap: int = 0
     event_cap: int = 0
@@ -94,7 +95,8 @@ class SimConfig:
         a.mode = self.mode
         a.churn_per_period = self.churn_per_period
         a.n_dormant = self.n_dormant
-        a.flags = (_abi.FLAG_RECORD_EVENTS if self.record_events else 0) | (_abi.FLAG_PROFILE if self.profile else 0)
+        a.flags = (_abi.FLAG_RECORD_EVENTS if self.record_events else 0) | (_abi.FLAG_PROFILE if self.profile or self.profile_all else 0) \
+            | (_abi.FLAG_PROFILE_ALL if self.profile_all else 0)
         seeds = list(dict.fromkeys(c.seedMembers))
         if len(seeds) > 16:
             raise ValueError("at most 16 seed members")

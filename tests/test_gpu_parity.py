@@ -387,3 +387,31 @@ def test_fast_config_blocks_restart_lockstep(oracle, engine):
         c.join(4, [0])
         c.join(5, [6])  # 6 never starts
     run_lockstep(o, e, 600, 50, "restart as 4, lonely 5")
+
+
+@pytest.mark.parametrize("profile_all", [False, True])
+def test_sampled_diff_accounting(oracle, engine, profile_all):
+    """swim_counters diff_ns / diff_launches / diff_msgs cover the same launches (SWIM_FLAG_PROFILE samples ticks
+    k % 5 == 0 on one GPU, PROFILE_ALL times all of them): with every launch timed, the payloads the timed launches
+    streamed are exactly the payloads merged; sampled, they are the merges of the sampled ticks (the oracle's
+    per-tick merge counts, tick by tick)."""
+    import dataclasses
+    cfg = SimConfig(n_members=600, cluster=ClusterConfig(syncInterval=1000))
+    e = SimulatedCluster(engine, dataclasses.replace(cfg, profile=True, profile_all=profile_all))
+    o = SimulatedCluster(oracle, cfg)
+    e.step(7)  # the timed window starts mid-call (a call's first tick launches its own diff)
+    o.step(7)
+    b, want = e.counters(), 0
+    for _ in range(3):
+        e.step(20)
+        for _ in range(20):
+            t, before = o.tick, o.counters()["sync_merges"]
+            o.step(1)
+            if profile_all or t % 5 == 0:
+                want += o.counters()["sync_merges"] - before
+    c = e.counters()
+    assert c["sync_merges"] == o.counters()["sync_merges"]
+    assert c["diff_launches"] - b["diff_launches"] == (60 if profile_all else 12)
+    assert c["diff_msgs"] - b["diff_msgs"] == want
+    assert c["diff_ns"] > b["diff_ns"]
+    e.close()

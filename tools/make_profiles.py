@@ -18,12 +18,21 @@ prof = ROOT / "profiles"
 
 def values(path):
     rows = list(csv.DictReader(open(path)))
-    v = [float(r["Counter_Value"]) for r in rows if "k_sync_diff" in r["Kernel_Name"]]
-    return [x for x in v if x > 1000.0]  # steady-state launches (the first ticks carry no SYNC payloads)
+    return [float(r["Counter_Value"]) for r in rows if "k_sync_diff" in r["Kernel_Name"]]
 
 
-fetch = values(next((src / "pmc_fetch").rglob("*counter_collection.csv")))
-write = values(next((src / "pmc_write").rglob("*counter_collection.csv")))
+def pass_totals(d):
+    """the bench line of a PMC pass: its run_totals price the same launches the pass counted"""
+    for line in (src / f"{d}.log").read_text().splitlines():
+        if line.startswith("{") and "run_totals" in line:
+            return json.loads(line)["run_totals"]
+    return None
+
+
+fetch_all = values(next((src / "pmc_fetch").rglob("*counter_collection.csv")))
+write_all = values(next((src / "pmc_write").rglob("*counter_collection.csv")))
+fetch = [x for x in fetch_all if x > 1000.0]  # steady-state launches (the first ticks carry no SYNC payloads)
+write = [x for x in write_all if x > 1000.0]
 stats = next((src / "trace").rglob("*kernel_stats.csv"))
 avg_us = None
 for r in csv.DictReader(open(stats)):
@@ -32,6 +41,14 @@ for r in csv.DictReader(open(stats)):
 bench = json.loads((src / "bench.json").read_text())
 n = bench["config"]["members"]
 fm, wm = statistics.median(fetch), statistics.median(write)
+# like-for-like: every k_sync_diff launch of the two PMC passes against the algorithmic bytes of those same launches
+# (8 B x N x the payloads merged over each pass's whole run, warm-up included)
+tf, tw = pass_totals("pmc_fetch"), pass_totals("pmc_write")
+ratio = None
+if tf and tw:
+    measured = 2 * sum(fetch_all) * 1024 + sum(write_all) * 1024  # one FETCH pass + one WRITE pass (same schedule)
+    algo = 8.0 * n * (tf["sync_merges"] + tw["sync_merges"]) / 2
+    ratio = measured / algo
 out = {
     "round": int(tag[1:]),
     "members": n,
@@ -42,6 +59,7 @@ out = {
     "gfx950_fetch_correction": "FETCH_SIZE x2 (MI355X_MICROARCH.md HBM section: wide coalesced reads are tallied at half)",
     "bytes_per_launch": 2 * fm * 1024 + wm * 1024,
     "algorithmic_bytes_per_launch": bench["roofline"]["algorithmic_bytes_per_launch"],
+    "traffic_over_algorithmic_same_launches": ratio,
     "rocprof_avg_duration_us": avg_us,
     "bench_hip_event_avg_us": bench["roofline"]["avg_launch_us"],
     "source_files": [f"{tag}_pmc_fetch_size_sync_diff.csv", f"{tag}_pmc_write_size_sync_diff.csv",
