@@ -42,13 +42,15 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=30, help="timed FD periods")
     p.add_argument("--warmup", type=int, default=3, help="untimed FD periods")
-    p.add_argument("--workload", choices=["c3", "c2", "c5"], default="c3",
-                   help="c3 (default, the headline): 100k full views; c2: 10k full views with 5%% loss; "
-                        "c5: rumor-only (SWIM_MODE_RUMOR) with 1%% churn per period")
+    p.add_argument("--workload", choices=["c3", "c3dyn", "c2", "c5"], default="c3",
+                   help="c3 (default, the headline): 100k full views; c3dyn: the same with membership evolution "
+                        "(--updates incarnation bumps per period, MembershipProtocolImpl.updateIncarnation); "
+                        "c2: 10k full views with 5%% loss; c5: rumor-only (SWIM_MODE_RUMOR) with 1%% churn per period")
+    p.add_argument("--updates", type=int, default=1, help="c3dyn: updateIncarnation calls per period")
     p.add_argument("--members", type=int, default=None, help="default: 100k (c3, c5), 10k (c2)")
     p.add_argument("--loss", type=int, default=None, help="default: 5 (c2), 0 otherwise")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-members", type=int, default=10_000)
+    p.add_argument("--cpu-members", type=int, default=None, help="default: the workload's size if host RAM allows")
     p.add_argument("--cpu-periods", type=int, default=120)
     p.add_argument("--transport", choices=["rccl", "host"], default="rccl", help="N>1 shard exchange")
     p.add_argument("--no-events", action="store_true", help="no per-kernel HIP events (roofline unavailable)")
@@ -72,6 +74,16 @@ def traffic_from_profiles(n_members):
     return None
 
 
+def mem_available():
+    try:
+        for line in open("/proc/meminfo"):
+            if line.startswith("MemAvailable:"):
+                return int(line.split()[1]) * 1024
+    except OSError:
+        pass
+    return 0
+
+
 def workload_config(a, SimConfig, _abi, members, **kw):
     if a.workload == "c5":
         return SimConfig(n_members=members, mode=_abi.MODE_RUMOR, churn_per_period=max(1, members // 100), **kw)
@@ -84,9 +96,17 @@ def _oracle_rate(a, lib, members, periods, threads):
     c = SimulatedCluster(lib, workload_config(a, SimConfig, _abi, members))
     if a.loss:
         c.set_default_loss(a.loss)
-    c.run_periods(1)
+    rng = __import__("random").Random(0x5EED)
+
+    def run(n):
+        for _ in range(n):
+            for _ in range(a.updates if a.workload == "c3dyn" else 0):
+                c.update_incarnation(rng.randrange(members))
+            c.run_periods(1)
+
+    run(1)
     t0 = time.perf_counter()
-    c.run_periods(periods)
+    run(periods)
     dt = time.perf_counter() - t0
     c.close()
     return members * periods / dt, dt
@@ -102,22 +122,29 @@ def cpu_baseline(a, members, periods):
         subprocess.check_call(["make", "-s", "-C", str(ROOT / "oracle")])
     lib = _abi.load(lib_path)
     cores = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count() or 1))
-    one, dt1 = _oracle_rate(a, lib, members, max(1, periods // 4), 1)
+    one_members = min(members, 10_000)  # one core: the setup alone is O(N^2) single-threaded work
+    one, dt1 = _oracle_rate(a, lib, one_members, max(1, min(periods, 120) // 4), 1)
     allc, dtn = _oracle_rate(a, lib, members, periods, cores)
     os.environ.pop("SWIMREF_THREADS", None)
-    note = {"c3": "per-member work grows ~linearly with N (SYNC payloads); the full 100k size is not sampled here: "
-                  "the oracle holds ~20 B per member pair (~200 GB of host RAM at 100k) and its preconverged setup "
-                  "alone takes minutes (one-off measurement: profiles/r02_cpu_baseline_c3_100k.json)",
+    full = "the headline size" if members == a.members else (
+        f"reduced N: the oracle holds ~20 B per member pair ({20 * a.members ** 2 / 1e9:.0f} GB of host RAM at "
+        f"{a.members}), more than this host had available")
+    note = {"c3": f"{full}; per-member work grows ~linearly with N (SYNC payloads)",
+            "c3dyn": f"{full}; {a.updates} updateIncarnation per period as on the GPU",
             "c2": "per-member gossip load grows ~N (SYNC re-spread storm), so at 10k it is far slower per member·period",
             "c5": "per-member rumor load grows ~N at 1 % churn, so at full N it is slower per member·period"}[a.workload]
     return {"value": allc, "unit": "member·periods/s", "cores": cores, "kind": "port",
-            "single_core_value": one,
-            "sample": f"oracle/swimref.cpp, {members} members (same {a.workload.upper()} shape, reduced N), {periods} "
-                      f"periods after 1 warm-up period on {cores} worker threads ({dtn:.1f} s), and {max(1, periods // 4)} "
-                      f"periods on one ({dt1:.1f} s); {note}"}
+            "single_core_value": one, "single_core_members": one_members,
+            "sample": f"oracle/swimref.cpp, {members} members (same {a.workload.upper()} shape), {periods} "
+                      f"periods after 1 warm-up period on {cores} worker threads ({dtn:.1f} s), and "
+                      f"{max(1, min(periods, 120) // 4)} periods at {one_members} members on one core ({dt1:.1f} s); "
+                      f"{note}"}
 
 
 def workload_name(a, n):
+    if a.workload == "c3dyn":
+        return (f"C3 with membership evolution: {n} members, full views, preconverged, {a.updates} "
+                f"updateIncarnation per period (gossip, SYNC re-spread, UPDATED events, metadata fetches)")
     if a.workload == "c3":
         return BASELINE_WORKLOAD if (n == 100_000 and not a.loss) else f"{n} members, full views, loss {a.loss}%"
     if a.workload == "c2":
@@ -162,7 +189,18 @@ def main():
         c = swimhip.cluster(cfg)
     if a.loss:
         c.set_default_loss(a.loss)
-    c.run_periods(a.warmup)
+    rng = __import__("random").Random(0x5EED)
+
+    def run(periods):
+        if a.workload != "c3dyn":
+            c.run_periods(periods)
+            return
+        for _ in range(periods):  # members chosen on the host: every rank makes the same calls
+            for _ in range(a.updates):
+                c.update_incarnation(rng.randrange(a.members))
+            c.run_periods(1)
+
+    run(a.warmup)
     base = c.counters()
 
     def barrier():
@@ -173,7 +211,7 @@ def main():
 
     barrier()
     t0 = time.perf_counter()
-    c.run_periods(a.steps)
+    run(a.steps)
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
@@ -227,19 +265,27 @@ def main():
             "run_totals": {"sync_merges": ctr["sync_merges"], "ticks": ctr["tick"]},
             "exchange_ms_per_step": d["exchange_ns"] * 1e-6 / a.steps,
         }
-        if a.workload != "c3":  # the gossip plane dominates: whole-step algorithmic bytes against HBM
+        if a.workload not in ("c3",):  # the gossip plane dominates: whole-step algorithmic bytes against HBM
             line["metric"] = f"member·periods/sec, {a.workload.upper()} workload (not the headline)"
             line["roofline"] = {"bound": "hbm", "kernel": "whole step (k_gossip_send dominates)",
                                 "achieved": B / dt / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                 "frac": B / dt / 1e9 / HBM_PEAK_GBPS, "traffic": None}
             line["kernel_time_share"] = {}
         if not a.no_cpu_baseline and world == 1:
-            cm, cp = {"c3": (a.cpu_members, a.cpu_periods), "c2": (600, 40), "c5": (2000, 24)}[a.workload]
+            c.close()  # the engine's host buffers go before the oracle's tables
+            c = None
+            cm, cp = {"c3": (a.cpu_members, a.cpu_periods), "c3dyn": (a.cpu_members, a.cpu_periods),
+                      "c2": (600, 40), "c5": (2000, 24)}[a.workload]
+            if a.workload in ("c3", "c3dyn") and a.cpu_members is None:
+                # the headline size when the host can hold the oracle's ~20 B per member pair (with 25 % slack),
+                # 2 periods (~2 s each on 16 threads after ~1 min of setup); else 10k members, 120 periods
+                cm, cp = (n, 2) if mem_available() > 25 * n * n else (10_000, 120)
             line["cpu_baseline"] = cpu_baseline(a, cm, cp)
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)
-    c.close()
+    if c is not None:
+        c.close()
     if dist is not None:
         dist.destroy_process_group()
 

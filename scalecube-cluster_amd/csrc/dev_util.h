@@ -95,6 +95,18 @@ __device__ __forceinline__ uint32_t link_loss(const Dev& d, int ep, uint32_t src
   return d.ep_loss[ep];
 }
 
+// the same with the settings epoch of tick k already looked up (epoch_at once per thread, not per message)
+__device__ __forceinline__ bool lost_msg_ep(const Dev& d, int ep, uint32_t kind, uint32_t src, uint32_t dst,
+                                            uint32_t k, uint32_t aux, uint32_t id) {
+  if (ep < 0) {
+    set_err(d, E_EPOCH);
+    return true;
+  }
+  uint32_t loss = link_loss(d, ep, src, dst, k);
+  if (loss == 0) return false;
+  if (loss >= 100) return true;
+  return loss_roll(d.seed_lo, d.seed_hi, kind, src, dst, k, aux, id) < loss;
+}
 __device__ __forceinline__ bool lost_msg(const Dev& d, uint32_t kind, uint32_t src, uint32_t dst, uint32_t k,
                                          uint32_t aux, uint32_t id) {
   int ep = epoch_at(d, k);
@@ -108,9 +120,8 @@ __device__ __forceinline__ bool lost_msg(const Dev& d, uint32_t kind, uint32_t s
   return loss_roll(d.seed_lo, d.seed_hi, kind, src, dst, k, aux, id) < loss;
 }
 
-__device__ __forceinline__ bool lost_gossip(const Dev& d, uint32_t src, uint32_t dst, uint32_t k, uint32_t slot,
-                                            uint64_t gid) {
-  int ep = epoch_at(d, k);
+__device__ __forceinline__ bool lost_gossip_ep(const Dev& d, int ep, uint32_t src, uint32_t dst, uint32_t k,
+                                               uint32_t slot, uint64_t gid) {
   if (ep < 0) {
     set_err(d, E_EPOCH);
     return true;
@@ -121,6 +132,10 @@ __device__ __forceinline__ bool lost_gossip(const Dev& d, uint32_t src, uint32_t
   u32x4 r = philox(src, k ^ ((slot >> 2) << 31), (uint32_t)(gid >> 32), (uint32_t)gid, d.seed_lo ^ SALT_LOSS_GOSSIP,
                    d.seed_hi);
   return next_int(pick(r, slot & 3), 100) < loss;
+}
+__device__ __forceinline__ bool lost_gossip(const Dev& d, uint32_t src, uint32_t dst, uint32_t k, uint32_t slot,
+                                            uint64_t gid) {
+  return lost_gossip_ep(d, epoch_at(d, k), src, dst, k, slot, gid);
 }
 
 // gPeriod of member x before its gossip task at tick c = number of its gossip rounds at ticks < c

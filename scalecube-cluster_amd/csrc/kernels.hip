@@ -707,7 +707,7 @@ __global__ void k_gossip_contacts(Dev d, uint32_t k) {
 // one counted send of gossip g from m to its round target t = T[m][s] (isInfected already checked): the receipt is
 // potential unless t holds g past this tick; a loss draw, then the first sender of (g, t) queues the delivery
 __device__ __forceinline__ void send_tail(const Dev& d, uint32_t g, uint32_t m, uint32_t s, uint32_t t, uint32_t k,
-                                          uint64_t gid, uint32_t* Sg) {
+                                          uint64_t gid, uint32_t* Sg, int ep) {
   if (d.dbg_send) {
     uint32_t di = atomicAdd(d.dbg_send_n, 1u);
     if (di < d.dbg_send_cap) {
@@ -722,7 +722,7 @@ __device__ __forceinline__ void send_tail(const Dev& d, uint32_t g, uint32_t m, 
   uint32_t et = Sg[t];
   // potential unless t holds g and does not sweep it in its own round this tick (a delivery would re-create it)
   if (s_held(et) && !(s_ctick(et) < d.swthr[t])) return;
-  if (lost_gossip(d, m, t, k, s, gid)) return;
+  if (lost_gossip_ep(d, ep, m, t, k, s, gid)) return;
   uint32_t old = atomicOr(&Sg[t], S_PENDING);
   if (!(old & S_PENDING)) {
     uint32_t di = wave_append(d.deliv_n);
@@ -854,6 +854,7 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
   __shared__ unsigned long long red[4];
   const uint32_t na = *nactive, nr = *d.rn, ngroups = (na + 63) / 64;
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const int ep = epoch_at(d, k);
   unsigned long long sends = 0;
   uint32_t st[4] = {0, 0, 0, 0};  // SWIM_EXP & 4: items with window bits, contact-loop bits, replays, first-receipt candidates
   for (uint32_t w = blockIdx.x * 4 + wave; w < nr * d.F; w += gridDim.x * 4) {  // wave-uniform item
@@ -915,7 +916,7 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
         if (j < total) {
           const uint32_t g = active[(size_t)(q0 + own) * 64 + nth_bit(word, r)];
           if (d.exp & 4) st[3]++;
-          send_tail(d, g, m, s, t, k, d.slot_gid[g], d.S + (size_t)g * d.N);
+          send_tail(d, g, m, s, t, k, d.slot_gid[g], d.S + (size_t)g * d.N, ep);
         }
       }
     }
@@ -938,6 +939,7 @@ __global__ void __launch_bounds__(256) k_gossip_replay(const Dev* __restrict__ d
   const Dev& d = *dp;
   __shared__ unsigned long long red[4];
   const uint32_t n = min(*d.rp_n, d.RPCAP);
+  const int ep = epoch_at(d, k);
   unsigned long long sends = 0;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint64_t v = d.rp[i];
@@ -948,7 +950,7 @@ __global__ void __launch_bounds__(256) k_gossip_replay(const Dev* __restrict__ d
     if (ci >= d.slot_ctick[g] && ci + d.lat >= c && blocked_pair_cached(d, m, t, g, gid, k, c, d.cev + (size_t)ms * CEVW))
       continue;
     sends++;
-    send_tail(d, g, m, s, t, k, gid, Sg);
+    send_tail(d, g, m, s, t, k, gid, Sg, ep);
   }
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   for (uint32_t o = 32; o > 0; o >>= 1) sends += __shfl_xor(sends, o);
@@ -964,6 +966,7 @@ __global__ void __launch_bounds__(256) k_gossip_replay(const Dev* __restrict__ d
 __global__ void __launch_bounds__(64) k_gossip_send_slow(const Dev* __restrict__ dp, uint32_t k) {
   const Dev& d = *dp;
   const uint32_t n = min(*d.slow_n, d.SLOWCAP);
+  const int ep = epoch_at(d, k);
   unsigned long long sends = 0;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint64_t v = d.slow[i];
@@ -973,7 +976,7 @@ __global__ void __launch_bounds__(64) k_gossip_send_slow(const Dev* __restrict__
     const uint64_t gid = d.slot_gid[g];
     if (blocked_pair(d, m, t, g, gid, k, c)) continue;  // isInfected (:247)
     sends++;
-    send_tail(d, g, m, s, t, k, gid, Sg);
+    send_tail(d, g, m, s, t, k, gid, Sg, ep);
   }
   if (sends) atomicAdd(&d.ctr[C_G], sends);
 }

@@ -21,6 +21,7 @@ struct ML {
   uint32_t m, k, N;
   uint32_t tsize, fdLen, gLen, fdPeriod, gPeriod, gCounter, nextPing, nextGossip, nextSync, cidCnt, syncSeq, evSeq,
       held, timerMin, initFlags, initDeadline, initCidBase, initN, nsub, npath, nfetch;
+  int ep;          // NetworkEmulator settings epoch of tick k (epoch_at, looked up once)
   uint32_t fnext;  // earliest tick at which a pending fetch needs the member (hop, arrival or timeout); NEVER: none
   int32_t pingIdx, remoteIdx;
   uint32_t sel[8];
@@ -95,7 +96,7 @@ __device__ __forceinline__ bool send_sync(ML& L, uint32_t kind, uint32_t dst, ui
   const Dev& d = *L.d;
   uint32_t seq = L.syncSeq++;
   L.c[C_M]++;
-  if (lost_msg(d, kind, L.m, dst, L.k, L.m, seq)) {
+  if (lost_msg_ep(d, L.ep, kind, L.m, dst, L.k, L.m, seq)) {
     L.c[C_LOST]++;
     return false;
   }
@@ -327,7 +328,7 @@ __device__ __forceinline__ void fetch_md(ML& L, uint32_t subj, uint32_t st, uint
   const Dev& d = *L.d;
   uint32_t cnt = L.cidCnt++;
   L.c[C_M]++;
-  if (lost_msg(d, K_GMD_REQ, L.m, subj, L.k, L.m, cnt)) {
+  if (lost_msg_ep(d, L.ep, K_GMD_REQ, L.m, subj, L.k, L.m, cnt)) {
     L.c[C_LOST]++;
     if (g >= 0) grp(L, g)[5] |= GF_ERROR;
     do_finally(L, subj, st, inc, reason);
@@ -487,7 +488,7 @@ __device__ __forceinline__ void ping_req_step(ML& L, uint32_t target, uint32_t c
   for (uint32_t q = 0; q < nh; ++q) {
     uint32_t h = helpers[q];
     L.c[C_M]++;
-    if (lost_msg(d, K_PING_REQ, L.m, h, L.k, L.m, cnt)) {
+    if (lost_msg_ep(d, L.ep, K_PING_REQ, L.m, h, L.k, L.m, cnt)) {
       L.c[C_LOST]++;
       on_fd_event(L, target, ST_SUSPECT);
       continue;
@@ -509,7 +510,7 @@ __device__ __forceinline__ void do_ping(ML& L) {
   uint32_t target = L.fdl[L.pingIdx++];
   uint32_t cnt = L.cidCnt++;
   L.c[C_M]++;
-  if (lost_msg(d, K_PING, L.m, target, L.k, L.m, cnt)) {
+  if (lost_msg_ep(d, L.ep, K_PING, L.m, target, L.k, L.m, cnt)) {
     L.c[C_LOST]++;
     ping_req_step(L, target, cnt);
     return;
@@ -745,6 +746,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   L.npath = d.npath[m];
   L.nfetch = d.nfetch[m];
   L.fnext = d.fnext[m];
+  L.ep = epoch_at(d, k);
   L.pingIdx = d.pingIdx[m];
   L.remoteIdx = d.remoteIdx[m];
   for (int i = 0; i < 8; ++i) L.sel[i] = d.sel[(size_t)m * 8 + i];
@@ -916,7 +918,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
             keep = false;
           } else {
             L.c[C_M]++;
-            if (lost_msg(d, K_PING_ACK, a, m, k, m, cnt)) {
+            if (lost_msg_ep(d, L.ep, K_PING_ACK, a, m, k, m, cnt)) {
               L.c[C_LOST]++;
               keep = false;
             } else {
@@ -932,11 +934,11 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
             L.c[C_M]++;
             bool lost;
             if (st == 1)  // onPingReq (:258-284): transit PING helper -> target
-              lost = lost_msg(d, K_PING, a, b, k, m, cnt);
+              lost = lost_msg_ep(d, L.ep, K_PING, a, b, k, m, cnt);
             else if (st == 2)  // onPing at the target: PING_ACK target -> helper
-              lost = lost_msg(d, K_PING_ACK, b, a, k, m, cnt);
+              lost = lost_msg_ep(d, L.ep, K_PING_ACK, b, a, k, m, cnt);
             else  // onTransitPingAck (:290-315): PING_ACK helper -> issuer
-              lost = lost_msg(d, K_PING_ACK, a, m, k, m, cnt);
+              lost = lost_msg_ep(d, L.ep, K_PING_ACK, a, m, k, m, cnt);
             if (lost) {
               L.c[C_LOST]++;
               keep = false;
@@ -1007,7 +1009,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
           lo.w &= 0x00FFFFFFu;
         } else {
           L.c[C_M]++;
-          if (lost_msg(d, K_GMD_RESP, subj, m, k, m, lo.x)) {
+          if (lost_msg_ep(d, L.ep, K_GMD_RESP, subj, m, k, m, lo.x)) {
             L.c[C_LOST]++;
             lo.w &= 0x00FFFFFFu;
           } else {
@@ -1074,15 +1076,34 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
       d.rc_cnt[m] = 0;  // the next receipt routing counts from zero
       d.rc_fill[m] = 0;
     }
-    for (uint32_t q = 0; q < n; ++q) {
-      uint32_t g = d.rc_slot[off + q];
-      uint64_t key = d.slot_key[g];
-      if (d.slot_subj[g] == USER_SUBJ) {  // sink.next -> ClusterImpl.listenGossips (:213-216), not membership
-        emit_event(L, 3, (uint32_t)(d.slot_gid[g] >> 32), (uint32_t)key, (uint32_t)(key >> 32));
-        continue;
+    // batches of PB receipts: their slot words and the rows they touch are loaded together (independent loads in
+    // flight at once), then the updates run in order; update_membership re-reads the row (cache-hot), so a batch
+    // that touches one subject twice still sees its own earlier write
+    constexpr uint32_t PB = 8;
+    for (uint32_t q0 = 0; q0 < n; q0 += PB) {
+      const uint32_t nb = min(PB, n - q0);
+      uint32_t gs[PB], subj[PB];
+      uint64_t key[PB];
+#pragma unroll
+      for (uint32_t i = 0; i < PB; ++i) gs[i] = i < nb ? d.rc_slot[off + q0 + i] : 0u;
+#pragma unroll
+      for (uint32_t i = 0; i < PB; ++i) {
+        subj[i] = i < nb ? d.slot_subj[gs[i]] : USER_SUBJ;
+        key[i] = i < nb ? d.slot_key[gs[i]] : 0ull;
       }
-      L.c[C_R]++;
-      update_membership(L, d.slot_subj[g], rec_status(key), rec_inc(key), R_GOSSIP, -1);
+      uint32_t warm = 0;
+#pragma unroll
+      for (uint32_t i = 0; i < PB; ++i)
+        if (subj[i] != USER_SUBJ) warm += L.rk[subj[i]] + L.ra[subj[i]];
+      asm volatile("" ::"v"(warm));  // keep the warming loads
+      for (uint32_t i = 0; i < nb; ++i) {
+        if (subj[i] == USER_SUBJ) {  // sink.next -> ClusterImpl.listenGossips (:213-216), not membership
+          emit_event(L, 3, (uint32_t)(d.slot_gid[gs[i]] >> 32), (uint32_t)key[i], (uint32_t)(key[i] >> 32));
+          continue;
+        }
+        L.c[C_R]++;
+        update_membership(L, subj[i], rec_status(key[i]), rec_inc(key[i]), R_GOSSIP, -1);
+      }
     }
   }
 
