@@ -229,7 +229,7 @@ struct Member {
   void start(uint64_t k);
   void send(Msg&& m, uint64_t k, bool gossip = false);
   bool send_sync(uint8_t kind, uint32_t dst, uint32_t cid_iss, uint32_t cid_cnt, uint64_t k);
-  void emit_event(uint32_t type, uint32_t subj, uint32_t oldm, uint32_t newm, uint64_t k);
+  void emit_event(uint32_t type, uint32_t subj, uint32_t oldm, uint32_t newm, uint64_t k, uint32_t pad = 0);
   void on_member_event(uint32_t type, uint32_t subj);
   void spread(uint32_t subj, Rec rec, uint64_t payload = 0);
   void update_membership(uint32_t subj, Rec r1, int reason, int group, uint64_t k);
@@ -367,14 +367,20 @@ bool Member::send_sync(uint8_t kind, uint32_t dst, uint32_t cid_iss, uint32_t ci
 }
 
 // sink.next(MembershipEvent) (:548-584) -> user stream, FailureDetectorImpl.onMemberEvent, GossipProtocolImpl.onMemberEvent
-void Member::emit_event(uint32_t type, uint32_t subj, uint32_t oldm, uint32_t newm, uint64_t k) {
+// pad: the gossip counter of a GOSSIP event (its id is (subject, pad)). RUMOR mode hashes the events as a sum
+// (SEMANTICS.md §9: slot shards each emit a member's events for their own gossips), FULL mode as a chain.
+void Member::emit_event(uint32_t type, uint32_t subj, uint32_t oldm, uint32_t newm, uint64_t k, uint32_t pad) {
   Sim& s = *sim;
   uint32_t seq = evSeq++;
-  evHash = hpair(evHash, ((uint64_t)k << 32) | ((uint64_t)type << 30) | subj);
-  evHash = hpair(evHash, ((uint64_t)oldm << 32) | newm);
+  if (s.cfg.mode == SWIM_MODE_RUMOR) {
+    evHash += hpair(hpair(((uint64_t)k << 32) | ((uint64_t)type << 30) | subj, ((uint64_t)oldm << 32) | newm), pad);
+  } else {
+    evHash = hpair(evHash, ((uint64_t)k << 32) | ((uint64_t)type << 30) | subj);
+    evHash = hpair(evHash, ((uint64_t)oldm << 32) | newm);
+  }
   tl_lane->ctr.events++;
   if (s.cfg.flags & SWIM_FLAG_RECORD_EVENTS) {
-    swim_event e{(uint32_t)k, id, seq, type, subj, oldm, newm, 0};
+    swim_event e{(uint32_t)k, id, seq, type, subj, oldm, newm, pad};
     tl_lane->events.push_back(e);
   }
   on_member_event(type, subj);
@@ -893,7 +899,8 @@ void Member::process(uint64_t k, std::vector<Msg>& inbox) {
       g.infPeriod = gPeriod;
       gossips.emplace(m->gid, std::move(g));
       if (m->g_subj == USER_SUBJ) {  // sink.next -> ClusterImpl.listenGossips (:213-216); membership filters it out
-        emit_event(SWIM_EV_GOSSIP, (uint32_t)(m->gid >> 32), (uint32_t)m->g_payload, (uint32_t)(m->g_payload >> 32), k);
+        emit_event(SWIM_EV_GOSSIP, (uint32_t)(m->gid >> 32), (uint32_t)m->g_payload, (uint32_t)(m->g_payload >> 32), k,
+                   (uint32_t)m->gid);
       } else {
         tl_lane->ctr.record_compares++;
         update_membership(m->g_subj, m->g_rec, R_GOSSIP, -1, k);  // onMembershipGossip (:401-408)

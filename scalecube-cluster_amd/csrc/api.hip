@@ -202,6 +202,13 @@ int build(swim_handle* h) {
   d.NS = (c.n_members + 7u) & ~7u;
   d.W = h->spec.world ? h->spec.world : 1u;
   d.rank = h->spec.rank;
+  d.XW = 1;
+  if (d.W > 1 && c.mode == SWIM_MODE_RUMOR) {  // slot sharding (engine.h): every shard runs every member
+    d.XW = d.W;
+    d.xrank = d.rank;
+    d.W = 1;
+    d.rank = 0;
+  }
   d.lo = shard_lo(d.N, d.W, d.rank);
   d.hi = shard_lo(d.N, d.W, d.rank + 1);
   d.NL = d.hi - d.lo;
@@ -292,6 +299,14 @@ int build(swim_handle* h) {
   A(d.m_next, 2ull * d.MSGCAP) A(d.m_head, 2 * N) A(d.deaths, 2ull * DEATHCAP) A(d.deaths_n, 2) A(d.next_evt, N) A(d.mdone, 1) A(d.trk, NL * TRK) A(d.pending_inc, N) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
   A(d.pool, d.POOLCAP) A(d.pool_used, 1)
   A(d.ev, (uint64_t)d.EVCAP * 8) A(d.ev_n, 1) A(d.ctr, C_NCTR) A(d.err, 8)
+  if (d.XW > 1) {
+    A(d.held_delta, N)
+    HIPCK(hipMemsetAsync(d.held_delta, 0, 4 * N, h->stream));
+    if (h->spec.transport == SWIM_TRANSPORT_HOST) {
+      h->hsend.resize(4ull * N * d.XW);
+      h->hrecv.resize(4ull * N * d.XW);
+    }
+  }
   if (getenv("SWIM_SEND_LOG")) {  // debugging aid: every counted gossip send
     d.dbg_send_cap = (uint32_t)atoi(getenv("SWIM_SEND_LOG"));
     A(d.dbg_send, 5ull * d.dbg_send_cap) A(d.dbg_send_n, 1)
@@ -490,6 +505,50 @@ int exchange(swim_handle* h, uint8_t* send, uint8_t* recv, uint64_t cap, unsigne
   return SWIM_OK;
 }
 
+// slot sharding: sum the shards' gossip-count deltas of this tick and apply them (k_held_add). RCCL: one in-place
+// all-reduce on the stream. HOST: every shard sends its delta vector to every peer and sums what it receives.
+int held_allreduce(swim_handle* h) {
+  Dev& d = h->d;
+  hipStream_t st = h->stream;
+  auto t0 = std::chrono::steady_clock::now();
+  if (h->spec.transport == SWIM_TRANSPORT_RCCL) {
+    if (ncclAllReduce(d.held_delta, d.held_delta, d.N, ncclInt32, ncclSum, h->comm, st) != ncclSuccess) {
+      h->err = "ncclAllReduce (gossip counts) failed";
+      return SWIM_EDEVICE;
+    }
+    launch_held_add(d, d.held_delta, st);
+  } else {
+    const uint64_t bytes = 4ull * d.N;
+    HIPCK(hipMemcpyAsync(h->hsend.data(), d.held_delta, bytes, hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    for (uint32_t q = 1; q < d.XW; ++q) std::memcpy(h->hsend.data() + q * bytes, h->hsend.data(), bytes);
+    uint64_t sb[64], rb[64];
+    for (uint32_t q = 0; q < d.XW; ++q) sb[q] = q == d.xrank ? 0 : bytes, rb[q] = 0;
+    if (h->spec.exchange(h->spec.ctx, h->hsend.data(), sb, h->hrecv.data(), h->hrecv.size(), rb) != 0) {
+      h->err = "host exchange callback failed";
+      return SWIM_EDEVICE;
+    }
+    std::vector<int32_t> sum((size_t)d.N);
+    std::memcpy(sum.data(), h->hsend.data(), bytes);
+    uint64_t off = 0;
+    for (uint32_t p = 0; p < d.XW; ++p) {
+      const uint64_t n = rb[p] & XCNT_MASK;
+      if (n != (p == d.xrank ? 0 : bytes)) {
+        h->err = "gossip-count exchange: unexpected block size";
+        return SWIM_EDEVICE;
+      }
+      const int32_t* v = (const int32_t*)(h->hrecv.data() + off);
+      for (uint32_t m = 0; m < n / 4; ++m) sum[m] += v[m];
+      off += n;
+    }
+    HIPCK(hipMemcpyAsync(d.held_delta, sum.data(), bytes, hipMemcpyHostToDevice, st));
+    launch_held_add(d, d.held_delta, st);
+    HIPCK(hipStreamSynchronize(st));
+  }
+  h->xchg_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return SWIM_OK;
+}
+
 int create(const swim_config* cfg, const swim_shard_spec* spec, swim_handle** out) {
   if (!cfg || !out) return SWIM_EINVAL;
   *out = nullptr;
@@ -571,6 +630,8 @@ struct Group {
   };
   std::vector<End> ends;
   std::vector<swim_event> events;
+  bool slots = false;             // slot-sharded (RUMOR mode): every shard runs every member, gossips are split
+  std::vector<uint32_t> evcount;  // slot-sharded: events per observer drained so far (the merged seq)
 };
 
 namespace {
@@ -676,6 +737,8 @@ int create_group(const swim_config* cfg, swim_handle** out) {
     g->lo.push_back(s->d.lo);
     g->hi.push_back(s->d.hi);
   }
+  g->slots = g->shards[0]->d.XW > 1;
+  g->evcount.assign(g->slots ? cfg->n_members : 0, 0);
   h->d = g->shards[0]->d;  // constants only (N, ping_t, ...): the group handle itself launches nothing
   *out = h;
   return SWIM_OK;
@@ -867,6 +930,10 @@ int swim_step(swim_handle* h, uint32_t n) {
       } else if (te && te->all) {
         HIPCK(hipEventRecord((hipEvent_t)te->ev[4], h->stream));
         HIPCK(hipEventRecord((hipEvent_t)te->ev[5], h->stream));
+      }
+      if (d.XW > 1) {  // slot sharding: the members' gossip counts, every tick (collective)
+        int xr;
+        if ((xr = held_allreduce(h)) != SWIM_OK) return xr;
       }
     } else {
       int xr;
@@ -1132,9 +1199,15 @@ int swim_state_hash(swim_handle* h, uint64_t* out, size_t cap) {
   if (h->grp) {  // each shard fills its observers' words and leaves the others zero
     std::vector<uint64_t> part(6ull * h->d.N);
     std::fill(out, out + 6ull * h->d.N, 0ull);
+    const bool slots = h->grp->slots;
+    bool first = true;
     return group_all(h, [&](swim_handle* s) {
       const int rc = swim_state_hash(s, part.data(), part.size());
-      for (size_t i = 0; rc == SWIM_OK && i < part.size(); ++i) out[i] += part[i];
+      // slot-sharded: row, lists and scalars are replicated (taken once); the event and held-gossip words are
+      // sums over each shard's own gossips (SEMANTICS.md §9)
+      for (size_t i = 0; rc == SWIM_OK && i < part.size(); ++i)
+        if (!slots || first || i % 6 == 3 || i % 6 == 4) out[i] += part[i];
+      first = false;
       return rc;
     });
   }
@@ -1167,6 +1240,24 @@ int swim_read_lists(swim_handle* h, uint32_t obs, uint32_t* fd, uint32_t* fd_len
 }
 
 int swim_read_gossips(swim_handle* h, uint32_t obs, uint64_t* ids, uint32_t* inf, size_t cap, size_t* n_out) {
+  if (h && h->grp && h->grp->slots) {  // slot-sharded: the union of every shard's own gossips, in id order
+    if (!n_out || obs >= h->d.N) return SWIM_EINVAL;
+    std::vector<std::pair<uint64_t, uint32_t>> all;
+    std::vector<uint64_t> i2(cap);
+    std::vector<uint32_t> f2(cap);
+    const int rc = group_all(h, [&](swim_handle* s) {
+      size_t n = 0;
+      const int r = swim_read_gossips(s, obs, i2.data(), f2.data(), cap, &n);
+      for (size_t i = 0; r == SWIM_OK && i < n; ++i) all.emplace_back(i2[i], f2[i]);
+      return r;
+    });
+    if (rc != SWIM_OK) return rc;
+    std::sort(all.begin(), all.end());
+    if (all.size() > cap) return SWIM_ECAPACITY;
+    for (size_t i = 0; i < all.size(); ++i) ids[i] = all[i].first, inf[i] = all[i].second;
+    *n_out = all.size();
+    return SWIM_OK;
+  }
   GROUP_OWNER(obs, swim_read_gossips(s, obs, ids, inf, cap, n_out));
   if (!h || obs >= h->d.N || !n_out || !owns(h, obs)) return SWIM_EINVAL;
   HIPCK(hipStreamSynchronize(h->stream));
@@ -1217,11 +1308,20 @@ int swim_drain_events(swim_handle* h, swim_event* out, size_t cap, size_t* n_out
       return SWIM_OK;
     });
     if (rc != SWIM_OK) return rc;
-    std::stable_sort(ev.begin(), ev.end(), [](const swim_event& a, const swim_event& b) {
-      if (a.tick != b.tick) return a.tick < b.tick;
-      if (a.observer != b.observer) return a.observer < b.observer;
-      return a.seq < b.seq;
-    });
+    if (h->grp->slots) {  // one observer's events of a tick come from several shards: P4's gossip-id order, renumbered
+      std::stable_sort(ev.begin(), ev.end(), [](const swim_event& a, const swim_event& b) {
+        if (a.tick != b.tick) return a.tick < b.tick;
+        if (a.observer != b.observer) return a.observer < b.observer;
+        return a.subject != b.subject ? a.subject < b.subject : a.pad < b.pad;
+      });
+      for (swim_event& e : ev) e.seq = h->grp->evcount[e.observer]++;
+    } else {
+      std::stable_sort(ev.begin(), ev.end(), [](const swim_event& a, const swim_event& b) {
+        if (a.tick != b.tick) return a.tick < b.tick;
+        if (a.observer != b.observer) return a.observer < b.observer;
+        return a.seq < b.seq;
+      });
+    }
     const size_t k = std::min(cap, ev.size());
     std::copy(ev.begin(), ev.begin() + (long)k, out);
     ev.erase(ev.begin(), ev.begin() + (long)k);

@@ -217,7 +217,20 @@ struct Dev {
   unsigned long long* xi_host;   // host-mapped [2W]: send and receive count words of the last exchange
   uint32_t* xdone;  // [W] finished k_pack_a_chunks blocks per peer column (the last one writes the inline block)
   uint32_t inl;     // RCCL transport: exchange A's inline blocks are written by k_pack_a_chunks
+
+  // ---- slot sharding (RUMOR mode with W > 1) ----
+  // Every shard runs all N members (their scalar state is replicated and evolves identically) but holds only the
+  // gossips it owns (slot_mine): their holder table, sends, first receipts and sweeps stay on that shard. The only
+  // cross-shard state is each member's gossip count (doSpreadGossip returns early without gossips): the shards'
+  // per-tick receipt / sweep deltas are summed with one all-reduce. Kernels see W = 1; XW / xrank name the slot shard.
+  uint32_t XW, xrank;
+  int32_t* held_delta;  // [N] this tick's change of the member's gossip count from this shard's slots
 };
+
+// the slot shard that owns gossip gid (slot sharding; always this shard otherwise)
+__host__ __device__ __forceinline__ bool slot_mine(const Dev& d, uint64_t gid) {
+  return d.XW <= 1 || (uint32_t)(mix64(gid ^ 0x510750A4D5ull) % d.XW) == d.xrank;
+}
 
 // local index of an observer owned by this shard
 __host__ __device__ __forceinline__ size_t lidx(const Dev& d, uint32_t m) { return (size_t)(m - d.lo); }
@@ -260,5 +273,6 @@ void launch_churn(const Dev& d, uint32_t k, void* stream);
 void launch_md_column(const Dev& d, uint32_t m, uint32_t u, void* stream);
 void launch_join(const Dev& d, uint32_t m, uint32_t k, const uint32_t* seeds, uint32_t n, void* stream);  // RUMOR mode, at ticks k % ping_t == 0
 void launch_hash(const Dev& d, uint64_t* out, uint32_t now, void* stream);
+void launch_held_add(const Dev& d, const int32_t* sum, void* stream);
 
 }  // namespace swim

@@ -775,7 +775,10 @@ __global__ void __launch_bounds__(256) k_gossip_scan(const Dev* __restrict__ dp,
       if (infP + sp >= per) wb |= 1ull << j;  // selectGossipsToSend window (:246)
       if (per > infP + sweep_after(sp)) {     // sweepGossips (:283-308)
         atomicOr(&d.S[(size_t)g * d.N + m], S_SWEPT);
-        atomicSub(&d.held[m], 1u);
+        if (d.XW > 1)
+          atomicSub(&d.held_delta[m], 1);
+        else
+          atomicSub(&d.held[m], 1u);
         atomicSub(&d.slot_holders[g], 1);
         on_sweep(d, g, m, k);
         if (d.W > 1) {  // applied on the other shards from exchange B
@@ -1024,7 +1027,10 @@ __global__ void k_gossip_apply(Dev d, uint32_t k) {
     if (s_ever(e)) hist_push(d, d.slot_gid[g], t, s_ctick(e));  // rebirth after a sweep (:176-180)
     uint32_t ne = ((k + d.lat + 1u) & S_TICK_MASK) | (s_ever(e) ? S_REBORN : 0u);
     *p = ne;
-    atomicAdd(&d.held[t], 1u);
+    if (d.XW > 1)
+      atomicAdd(&d.held_delta[t], 1);
+    else
+      atomicAdd(&d.held[t], 1u);
     atomicAdd(&d.slot_holders[g], 1);
     if (t < d.lo || t >= d.hi) continue;  // P4 of another shard's member
     if (!receipt_matters(d, t, g, k + d.lat)) {  // counted as a record compare in P4, nothing else
@@ -1113,6 +1119,17 @@ __global__ void __launch_bounds__(256) k_hash(Dev d, uint64_t* out, uint32_t now
 
 
 __global__ void k_tick_end(Dev d, uint32_t k) { tick_end(d, k); }
+
+// slot sharding: the all-reduced gossip-count deltas of this tick
+__global__ void k_held_add(Dev d, const int32_t* sum) {
+  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= d.N) return;
+  d.held[m] = (uint32_t)((int32_t)d.held[m] + sum[m]);
+  d.held_delta[m] = 0;
+}
+void launch_held_add(const Dev& d, const int32_t* sum, void* stream) {
+  hipLaunchKernelGGL(k_held_add, dim3((d.N + 255) / 256), dim3(256), 0, (hipStream_t)stream, d, sum);
+}
 
 // ------------------------------------------------------------------------------------------------------------
 // host launchers

@@ -162,11 +162,18 @@ __device__ __forceinline__ void on_member_event(ML& L, uint32_t type, uint32_t s
   }
 }
 
-__device__ __forceinline__ void emit_event(ML& L, uint32_t type, uint32_t subj, uint32_t oldm, uint32_t newm) {
+// pad: the gossip counter of a GOSSIP event (its id is (subject, pad)), 0 otherwise. RUMOR mode hashes the events
+// as a sum (SEMANTICS.md §9), so slot shards that each emit a member's events for their own gossips add up.
+__device__ __forceinline__ void emit_event(ML& L, uint32_t type, uint32_t subj, uint32_t oldm, uint32_t newm,
+                                           uint32_t pad = 0) {
   const Dev& d = *L.d;
   uint32_t seq = L.evSeq++;
-  L.evHash = hpair(L.evHash, ((uint64_t)L.k << 32) | ((uint64_t)type << 30) | subj);
-  L.evHash = hpair(L.evHash, ((uint64_t)oldm << 32) | newm);
+  if (d.mode == 1u) {  // SWIM_MODE_RUMOR
+    L.evHash += hpair(hpair(((uint64_t)L.k << 32) | ((uint64_t)type << 30) | subj, ((uint64_t)oldm << 32) | newm), pad);
+  } else {
+    L.evHash = hpair(L.evHash, ((uint64_t)L.k << 32) | ((uint64_t)type << 30) | subj);
+    L.evHash = hpair(L.evHash, ((uint64_t)oldm << 32) | newm);
+  }
   L.c[C_E]++;
   if (d.flags & 1u) {
     uint32_t i = atomicAdd(d.ev_n, 1u);
@@ -179,7 +186,7 @@ __device__ __forceinline__ void emit_event(ML& L, uint32_t type, uint32_t subj, 
       e[4] = subj;
       e[5] = oldm;
       e[6] = newm;
-      e[7] = 0;
+      e[7] = pad;
     } else {
       set_err(d, E_EVENTS);
     }
@@ -224,9 +231,11 @@ __device__ __forceinline__ bool new_slot(const Dev& d, uint32_t m, uint32_t k, u
 // GossipProtocolImpl.spread -> createAndPutGossip (:124-128,163-169): a membership gossip held by this member
 __device__ __forceinline__ void spread(ML& L, uint32_t subj, uint32_t st, uint32_t inc) {
   uint64_t gid = ((uint64_t)L.m << 32) | L.gCounter++;
-  if (!new_slot(*L.d, L.m, L.k, gid, subj, rec_key(st, inc))) return;
+  if (slot_mine(*L.d, gid)) {  // slot sharding: only the owning shard stores it; every shard counts it as held
+    if (!new_slot(*L.d, L.m, L.k, gid, subj, rec_key(st, inc))) return;
+    L.c[C_GCREATED]++;
+  }
   L.held++;
-  L.c[C_GCREATED]++;
 }
 
 // Cluster.spreadGossip (ClusterImpl.java:208-211) queued by swim_spread_gossip: user gossips of this shard's live
@@ -239,9 +248,11 @@ __global__ void k_user_gossips(Dev d, uint32_t k, const uint64_t* q, uint32_t n)
     const uint32_t m = (uint32_t)q[2 * i];
     if (m < d.lo || m >= d.hi || dead_at(d, m, k)) continue;
     const uint64_t gid = ((uint64_t)m << 32) | d.gCounter[m]++;
-    if (!new_slot(d, m, k, gid, USER_SUBJ, q[2 * i + 1])) continue;
+    if (slot_mine(d, gid)) {  // slot sharding: only the owning shard stores it; every shard counts it as held
+      if (!new_slot(d, m, k, gid, USER_SUBJ, q[2 * i + 1])) continue;
+      created++;
+    }
     d.held[m]++;
-    created++;
   }
   if (created) atomicAdd(&d.ctr[C_GCREATED], created);
 }
@@ -1098,7 +1109,8 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
       asm volatile("" ::"v"(warm));  // keep the warming loads
       for (uint32_t i = 0; i < nb; ++i) {
         if (subj[i] == USER_SUBJ) {  // sink.next -> ClusterImpl.listenGossips (:213-216), not membership
-          emit_event(L, 3, (uint32_t)(d.slot_gid[gs[i]] >> 32), (uint32_t)key[i], (uint32_t)(key[i] >> 32));
+          const uint64_t gid = d.slot_gid[gs[i]];
+          emit_event(L, 3, (uint32_t)(gid >> 32), (uint32_t)key[i], (uint32_t)(key[i] >> 32), (uint32_t)gid);
           continue;
         }
         L.c[C_R]++;

@@ -10,7 +10,7 @@ It mirrors the outward surface of the reference's per-member stack:
 The failure behaviour follows the C ABI: any negative return raises SwimError carrying swim_last_error().
 """
 import ctypes as C
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import List, Optional
 
 import numpy as np
@@ -32,6 +32,8 @@ class MembershipEvent:
     member: int
     oldMetadata: Optional[int]
     newMetadata: Optional[int]
+    # GOSSIP events: the gossip's counter (its id is (member, gossipCounter)); not part of equality
+    gossipCounter: int = field(default=0, compare=False, repr=False)
 
     def isAdded(self):
         return self.type == "ADDED"
@@ -246,7 +248,7 @@ class SimulatedCluster:
                 e = buf[i]
                 if e.type == _abi.EV_GOSSIP:  # payload words, not metadata versions
                     out.append(MembershipEvent(e.tick, e.observer, e.seq, "GOSSIP", e.subject, int(e.old_meta),
-                                               int(e.new_meta)))
+                                               int(e.new_meta), int(e.pad)))
                 else:
                     out.append(MembershipEvent(e.tick, e.observer, e.seq, _TYPES[e.type], e.subject,
                                                _meta(e.old_meta), _meta(e.new_meta)))

@@ -10,6 +10,7 @@ the SYNC / SYNC_ACK payloads addressed to each other's observers
 The readback methods of SimulatedCluster report this shard's observers only; gather_* helpers merge them.
 """
 import ctypes as C
+import dataclasses
 import threading
 
 import numpy as np
@@ -182,6 +183,9 @@ class ThreadShardGroup:
     def __init__(self, lib, cfg: SimConfig, world, chunk_cap=0):
         self.n = cfg.n_members
         self.world = world
+        # RUMOR mode shards the gossips instead of the observers: every shard runs every member
+        self.slots = cfg.mode == _abi.MODE_RUMOR
+        self._evcount = {}
         self.ex = ThreadExchange(world)
         self.shards = [ShardedCluster(lib, cfg, r, world, _abi.TRANSPORT_HOST, self.ex.endpoint(r), chunk_cap=chunk_cap)
                        for r in range(world)]
@@ -279,7 +283,13 @@ class ThreadShardGroup:
     def state_hash(self):
         h = self.shards[0].state_hash().copy()
         for s in self.shards[1:]:
-            h += s.state_hash()  # disjoint observer rows; the rest are zero
+            if self.slots:  # replicated row / lists / scalars; events and held gossips are per-shard sums
+                part = s.state_hash().reshape(-1, _abi.HASH_WORDS)
+                hv = h.reshape(-1, _abi.HASH_WORDS)
+                hv[:, 3] += part[:, 3]
+                hv[:, 4] += part[:, 4]
+            else:
+                h += s.state_hash()  # disjoint observer rows; the rest are zero
         return h
 
     def counters(self):
@@ -288,8 +298,17 @@ class ThreadShardGroup:
 
     def events(self):
         ev = [e for s in self.shards for e in s.events()]
-        ev.sort(key=lambda e: (e.tick, e.observer, e.seq))
-        return ev
+        if not self.slots:
+            ev.sort(key=lambda e: (e.tick, e.observer, e.seq))
+            return ev
+        # slot-sharded: an observer's events of one tick come from several shards; P4 order is the gossip id
+        ev.sort(key=lambda e: (e.tick, e.observer, e.member, e.gossipCounter))
+        out = []
+        for e in ev:
+            seq = self._evcount.get(e.observer, 0)
+            self._evcount[e.observer] = seq + 1
+            out.append(dataclasses.replace(e, seq=seq))
+        return out
 
     def row(self, m):
         return self._owner(m).row(m)
@@ -298,6 +317,8 @@ class ThreadShardGroup:
         return self._owner(m).lists(m)
 
     def gossips(self, m):
+        if self.slots:
+            return sorted(g for s in self.shards for g in s.gossips(m))
         return self._owner(m).gossips(m)
 
     def close(self):

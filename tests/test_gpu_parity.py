@@ -298,6 +298,29 @@ def test_rumor_mode_sharded(oracle, engine):
     e.close()
 
 
+@pytest.mark.parametrize("world", [3, 4])
+def test_rumor_mode_slot_sharded_faults(oracle, engine, world):
+    """RUMOR mode shards the gossips, not the observers: every shard runs all members and keeps
+    the gossips it owns; the members' gossip counts are all-reduced every tick. Loss, a user gossip and crashes;
+    events merged across shards in P4's gossip-id order."""
+    from swimhip.shard import ThreadShardGroup
+    cfg = SimConfig(n_members=300, mode=_abi.MODE_RUMOR, churn_per_period=5, record_events=True)
+    o, e = SimulatedCluster(oracle, cfg), ThreadShardGroup(engine, cfg, world)
+    for c in (o, e):
+        c.set_default_loss(10)
+    run_lockstep(o, e, 120, 20, f"rumor slot shards W={world}")
+    for c in (o, e):
+        c.spread_gossip(17, 99)
+        c.kill(40)
+        c.kill(41)
+    run_lockstep(o, e, 150, 30, f"rumor slot shards + user gossip + kills W={world}")
+    for m in (3, 150, 299):
+        assert o.gossips(m) == e.gossips(m)
+    cs = [s.counters()["gossips_created"] for s in e.shards]
+    assert all(c > 0 for c in cs) and sum(cs) == o.counters()["gossips_created"]  # every shard owns a share
+    e.close()
+
+
 def test_joins_and_restarts(oracle, engine):
     """ClusterImpl.join0 of late processes (MembershipProtocolTest.testLimitedSeedMembers / testRestartFailedMembers
     shapes): dormant members join with their own seeds, crashed members are replaced by new ids, under 10 % loss."""
