@@ -54,6 +54,11 @@ def parse():
     p.add_argument("--cpu-periods", type=int, default=120)
     p.add_argument("--transport", choices=["rccl", "host"], default="rccl", help="N>1 shard exchange")
     p.add_argument("--no-events", action="store_true", help="no per-kernel HIP events (roofline unavailable)")
+    p.add_argument("--rehearse-shard", type=int, default=0, metavar="W",
+                   help="c5 only: run rank 0 of W slot shards on this GPU alone, the other shards' gossip-count "
+                        "deltas taken as zero (a per-shard timing rehearsal of the W-GPU run, not its results)")
+    p.add_argument("--slots", type=int, default=0, help="gossip slots per shard (0: the engine's default)")
+    p.add_argument("--churn", type=int, default=0, help="c5: churn rumors per period (default: 1 %% of the members)")
     p.add_argument("--rehearse-one-gpu", action="store_true",
                    help="N>1 on a single GPU (functional rehearsal only): every rank uses device 0 and gets its own "
                         "NCCL_HOSTID, so RCCL connects the ranks through its socket transport")
@@ -85,8 +90,11 @@ def mem_available():
 
 
 def workload_config(a, SimConfig, _abi, members, **kw):
+    if a.slots:
+        kw["gossip_slot_cap"] = a.slots
     if a.workload == "c5":
-        return SimConfig(n_members=members, mode=_abi.MODE_RUMOR, churn_per_period=max(1, members // 100), **kw)
+        return SimConfig(n_members=members, mode=_abi.MODE_RUMOR, churn_per_period=a.churn or max(1, members // 100),
+                         **kw)
     return SimConfig(n_members=members, **kw)
 
 
@@ -149,7 +157,11 @@ def workload_name(a, n):
         return BASELINE_WORKLOAD if (n == 100_000 and not a.loss) else f"{n} members, full views, loss {a.loss}%"
     if a.workload == "c2":
         return f"C2: {n} members, full views, preconverged, loss {a.loss}%"
-    return f"C5 (reduced N): {n} members, rumor-only, {max(1, n // 100)} churn rumors per period, loss {a.loss}%"
+    what = "C5" if n >= 1_000_000 else "C5 (reduced N)"
+    shard = (f"; rank 0 of {a.rehearse_shard} slot shards alone (the other shards' gossip-count deltas zero: a "
+             f"per-shard timing rehearsal, not the {a.rehearse_shard}-GPU result)") if a.rehearse_shard > 1 else ""
+    return (f"{what}: {n} members, rumor-only, {a.churn or max(1, n // 100)} churn rumors per period, loss "
+            f"{a.loss}%{shard}")
 
 
 def main():
@@ -173,7 +185,14 @@ def main():
     if a.loss is None:
         a.loss = 5 if a.workload == "c2" else 0
     cfg = workload_config(a, SimConfig, _abi, a.members, device=local, profile=not a.no_events)
-    if world > 1:
+    if a.rehearse_shard > 1:
+        if a.workload != "c5" or world != 1:
+            raise SystemExit("--rehearse-shard needs --workload c5 on one GPU")
+        from swimhip.shard import LoneExchange, ShardedCluster
+        os.environ["SWIM_LONE_SHARD"] = "1"  # the engine skips the (simulated) exchange altogether
+        lib = swimhip.engine()
+        c = ShardedCluster(lib, cfg, 0, a.rehearse_shard, _abi.TRANSPORT_HOST, exchange=LoneExchange(a.rehearse_shard))
+    elif world > 1:
         import torch.distributed as dist
         from swimhip.shard import GlooExchange, ShardedCluster, rccl_unique_id
         dist.init_process_group("gloo")
@@ -271,6 +290,9 @@ def main():
                                 "achieved": B / dt / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                 "frac": B / dt / 1e9 / HBM_PEAK_GBPS, "traffic": None}
             line["kernel_time_share"] = {}
+        if a.rehearse_shard > 1:
+            line["metric"] = "member·periods/sec of ONE slot shard, C5 rehearsal (not the headline)"
+            line["config"]["parallelism"] = f"slot shard 0 of {a.rehearse_shard} (peers simulated)"
         if not a.no_cpu_baseline and world == 1:
             c.close()  # the engine's host buffers go before the oracle's tables
             c = None

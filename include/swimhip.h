@@ -62,6 +62,8 @@ extern "C" {
 #define SWIM_FLAG_PROFILE 2u       /* time a SAMPLE of the k_sync_diff launches with HIP events on the engine stream:
                                       one GPU: the launches of ticks k % 5 == 0; sharded or with PROFILE_ALL: every
                                       launch (swim_counters diff_ns / diff_launches / diff_msgs cover the same set) */
+#define SWIM_FLAG_IMPLICIT_VIEWS 8u /* RUMOR mode: the (unchanging) tables and lists are computed, not stored; always
+                                      on above 65536 members (C5: 10^6 members would need 8 TB of tables) */
 #define SWIM_FLAG_PROFILE_ALL 4u   /* also time k_member_tick and k_gossip_send (member_ns, gossip_ns); ~10 % slower */
 
 typedef struct swim_config {

@@ -62,6 +62,9 @@ struct swim_handle {
   hipEvent_t ev_member = nullptr;
   bool no_skip = getenv("SWIM_NO_GOSSIP_SKIP") != nullptr;  // debugging aid: always run the gossip data plane
   bool no_pipe = getenv("SWIM_NO_PIPELINE") != nullptr;    // debugging aid: no early SYNC diff of the next tick
+  // timing aid (bench.py --rehearse-shard): a slot shard alone, its peers' gossip-count deltas taken as zero without
+  // any exchange (not the W-shard simulation's results)
+  bool lone = getenv("SWIM_LONE_SHARD") != nullptr;
   Group* grp = nullptr;  // n_gpus > 1: every call is forwarded to the shards (d holds shard 0's constants only)
 };
 
@@ -231,6 +234,8 @@ int build(swim_handle* h) {
   d.n_dormant = c.n_dormant;
   d.churn = c.mode == SWIM_MODE_RUMOR ? c.churn_per_period : 0u;
   d.flags = c.flags;
+  d.implicit = c.mode == SWIM_MODE_RUMOR && (c.n_members > 65536 || (c.flags & SWIM_FLAG_IMPLICIT_VIEWS)) ? 1u : 0u;
+  d.fastp4 = c.mode == SWIM_MODE_RUMOR && !(c.flags & SWIM_FLAG_RECORD_EVENTS) ? 1u : 0u;
   d.exp = getenv("SWIM_EXP") ? (uint32_t)atoi(getenv("SWIM_EXP")) : 0u;  // timing experiments: wrong results
   // seeds: LinkedHashSet of valid ids (MembershipProtocolImpl.java:160-166); self is skipped per member
   for (uint32_t i = 0; i < c.n_seeds; ++i) {
@@ -246,6 +251,7 @@ int build(swim_handle* h) {
   d.LCAP = d.N + (c.list_slack ? c.list_slack : 64);
   d.FCAP = c.pending_fetch_cap ? c.pending_fetch_cap : 256;
   d.GRCAP = c.init_mode == SWIM_INIT_COLD_JOIN ? std::min<uint32_t>(d.N + 16, 1024) : 32;
+  if (d.implicit) d.FCAP = d.GRCAP = 1;  // RUMOR mode: no metadata fetch, no SYNC reply group
   uint32_t maxSpread = d.repeatMult * (32u - (uint32_t)__builtin_clz(d.LCAP + 1));
   d.LOGW = 8;
   while (d.LOGW < 4 * (maxSpread + 2)) d.LOGW <<= 1;  // rounds kept for the infectedFrom replay
@@ -271,8 +277,21 @@ int build(swim_handle* h) {
   d.RCAP = d.DCAP;
   d.SLOWCAP = d.DCAP;
   d.RPCAP = d.DCAP;
+  if (d.implicit) {
+    // C5: every period's rumors start at one tick, so their epidemics peak together: on one of 8 slot shards a tick
+    // can deliver ~7·10^8 first receipts (8 B each). Their GOSSIP events skip the receipt routing (fastp4), and
+    // infectedFrom replays are rare at this size.
+    d.DCAP = 1u << 30;
+    d.RCAP = d.fastp4 ? 1u << 22 : 1u << 28;
+    d.SLOWCAP = d.RPCAP = 1u << 26;
+  }
   // copy-on-write snapshots and pinned payload copies (pin_msg) per tick: up to 256 MB per buffer, at least 64 rows
   d.ARENA_ROWS = (uint32_t)std::min<uint64_t>(d.MSGCAP, std::max<uint64_t>(64, (256ull << 20) / (4ull * d.NS)));
+  if (d.implicit) {  // no SYNC traffic: minimal message buffers
+    d.MSGCAP = 1024;
+    d.ARENA_ROWS = 1;
+    d.POOLCAP = 1024;
+  }
 
   int rc;
 #define A(p, n)                                   \
@@ -285,7 +304,8 @@ int build(swim_handle* h) {
   A(d.initFlags, N) A(d.initDeadline, N) A(d.initCidBase, N) A(d.initN, N) A(d.firstGossip, N) A(d.nsub, N)
   A(d.npath, N) A(d.nfetch, N) A(d.fnext, N) A(d.pingIdx, N) A(d.remoteIdx, N) A(d.sel, N * 8) A(d.evHash, N)
   const uint64_t NL = d.NL;  // per-observer arrays: this shard's rows only
-  A(d.rowk, NL * d.NS) A(d.rowa, NL * d.NS) A(d.fdl, NL * d.LCAP) A(d.gl, NL * d.LCAP)
+  const uint64_t NV = d.implicit ? 1 : NL;  // implicit views: no table or list is stored
+  A(d.rowk, NV * d.NS) A(d.rowa, NV * d.NS) A(d.fdl, NV * d.LCAP) A(d.gl, NV * d.LCAP)
   A(d.subs, NL * SUBCAP * 4) A(d.paths, NL * PATHCAP * 5) A(d.fetch, NL * d.FCAP * FREC) A(d.groups, NL * d.GRCAP * GREC)
   A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.slow, d.SLOWCAP) A(d.slow_n, 1) A(d.rp, d.RPCAP) A(d.rp_n, 1) A(d.rlist, N) A(d.rn, 1) A(d.start_tick, N) A(d.jseed_n, N) A(d.jseeds, 16 * N) A(d.md_uidx, N) A(d.mcfg, 4 * N) A(d.md_ver, NL * MDU) A(d.churn_q, 2ull * d.churn) A(d.cin, N * d.F) A(d.swthr, N) A(d.HB, (uint64_t)d.QW * N) A(d.WB, (uint64_t)d.QW * N) A(d.HBq, (uint64_t)d.QW * N) A(d.WBq, (uint64_t)d.QW * N) A(d.cev, N * d.F * CEVW)
   A(d.log_tick, N * d.LOGW) A(d.log_spread, N * d.LOGW) A(d.log_cnt, N * d.LOGW) A(d.log_tg, N * d.LOGW * d.F)
@@ -299,6 +319,11 @@ int build(swim_handle* h) {
   A(d.m_next, 2ull * d.MSGCAP) A(d.m_head, 2 * N) A(d.deaths, 2ull * DEATHCAP) A(d.deaths_n, 2) A(d.next_evt, N) A(d.mdone, 1) A(d.trk, NL * TRK) A(d.pending_inc, N) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
   A(d.pool, d.POOLCAP) A(d.pool_used, 1)
   A(d.ev, (uint64_t)d.EVCAP * 8) A(d.ev_n, 1) A(d.ctr, C_NCTR) A(d.err, 8)
+  if (d.fastp4) {
+    A(d.evp_hash, N) A(d.evp_n, N)
+    HIPCK(hipMemsetAsync(d.evp_hash, 0, 8 * N, h->stream));
+    HIPCK(hipMemsetAsync(d.evp_n, 0, 4 * N, h->stream));
+  }
   if (d.XW > 1) {
     A(d.held_delta, N)
     HIPCK(hipMemsetAsync(d.held_delta, 0, 4 * N, h->stream));
@@ -511,7 +536,9 @@ int held_allreduce(swim_handle* h) {
   Dev& d = h->d;
   hipStream_t st = h->stream;
   auto t0 = std::chrono::steady_clock::now();
-  if (h->spec.transport == SWIM_TRANSPORT_RCCL) {
+  if (h->lone) {
+    launch_held_add(d, d.held_delta, st);
+  } else if (h->spec.transport == SWIM_TRANSPORT_RCCL) {
     if (ncclAllReduce(d.held_delta, d.held_delta, d.N, ncclInt32, ncclSum, h->comm, st) != ncclSuccess) {
       h->err = "ncclAllReduce (gossip counts) failed";
       return SWIM_EDEVICE;
@@ -1030,6 +1057,7 @@ int swim_spread_gossip(swim_handle* h, uint32_t m, uint64_t payload) {
 int swim_update_metadata(swim_handle* h, uint32_t m) {
   GROUP_ALL(swim_update_metadata(s, m));
   if (!h || m >= h->d.N) return SWIM_EINVAL;
+  if (h->d.implicit) return SWIM_EUNSUPPORTED;  // implicit views: the tables are not stored
   uint32_t dt = 0, ver = 0;
   HIPCK(hipStreamSynchronize(h->stream));
   HIPCK(hipMemcpy(&dt, h->d.dead_tick + m, 4, hipMemcpyDeviceToHost));
@@ -1053,6 +1081,7 @@ int swim_update_metadata(swim_handle* h, uint32_t m) {
 int swim_update_incarnation(swim_handle* h, uint32_t m) {
   GROUP_ALL(swim_update_incarnation(s, m));
   if (!h || m >= h->d.N) return SWIM_EINVAL;
+  if (h->d.implicit) return SWIM_EUNSUPPORTED;  // implicit views: the tables are not stored
   if (!owns(h, m)) return SWIM_OK;  // the owning shard bumps it; the others learn it from its gossip
   uint32_t req = 0, dt = 0;
   HIPCK(hipStreamSynchronize(h->stream));
@@ -1069,6 +1098,7 @@ int swim_update_incarnation(swim_handle* h, uint32_t m) {
 int swim_leave(swim_handle* h, uint32_t m) {
   GROUP_ALL(swim_leave(s, m));
   if (!h || m >= h->d.N) return SWIM_EINVAL;
+  if (h->d.implicit) return SWIM_EUNSUPPORTED;  // implicit views: the tables are not stored
   HIPCK(hipStreamSynchronize(h->stream));
   uint32_t dt = 0, req = 0;
   HIPCK(hipMemcpy(&dt, h->d.dead_tick + m, 4, hipMemcpyDeviceToHost));
@@ -1176,6 +1206,10 @@ int swim_read_row(swim_handle* h, uint32_t obs, uint64_t* out, size_t cap) {
   GROUP_OWNER(obs, swim_read_row(s, obs, out, cap));
   if (!h || obs >= h->d.N || cap < h->d.N || !owns(h, obs)) return SWIM_EINVAL;
   HIPCK(hipStreamSynchronize(h->stream));
+  if (h->d.implicit) {  // RUMOR mode: every row is the PRECONVERGED row
+    for (uint32_t s = 0; s < h->d.N; ++s) out[s] = PRE_REC;
+    return SWIM_OK;
+  }
   std::vector<uint32_t> k(h->d.N), a(h->d.N);  // the two planes, joined into logical records (swim_common.h)
   HIPCK(hipMemcpy(k.data(), h->d.rowk + lidx(h->d, obs) * h->d.NS, 4ull * h->d.N, hipMemcpyDeviceToHost));
   HIPCK(hipMemcpy(a.data(), h->d.rowa + lidx(h->d, obs) * h->d.NS, 4ull * h->d.N, hipMemcpyDeviceToHost));
@@ -1230,8 +1264,14 @@ int swim_read_lists(swim_handle* h, uint32_t obs, uint32_t* fd, uint32_t* fd_len
   HIPCK(hipMemcpy(&fl, h->d.fdLen + obs, 4, hipMemcpyDeviceToHost));
   HIPCK(hipMemcpy(&glen, h->d.gLen + obs, 4, hipMemcpyDeviceToHost));
   if (fl > cap || glen > cap) return SWIM_EINVAL;
-  HIPCK(hipMemcpy(fd, h->d.fdl + lidx(h->d, obs) * h->d.LCAP, 4ull * fl, hipMemcpyDeviceToHost));
-  HIPCK(hipMemcpy(gl, h->d.gl + lidx(h->d, obs) * h->d.LCAP, 4ull * glen, hipMemcpyDeviceToHost));
+  if (h->d.implicit) {  // RUMOR mode: the PRECONVERGED permutations (list_at)
+    const FeistelPerm P0 = list_perm(h->d, obs, 0), P1 = list_perm(h->d, obs, 1);
+    for (uint32_t p = 0; p < fl; ++p) fd[p] = list_at(P0, obs, p);
+    for (uint32_t p = 0; p < glen; ++p) gl[p] = list_at(P1, obs, p);
+  } else {
+    HIPCK(hipMemcpy(fd, h->d.fdl + lidx(h->d, obs) * h->d.LCAP, 4ull * fl, hipMemcpyDeviceToHost));
+    HIPCK(hipMemcpy(gl, h->d.gl + lidx(h->d, obs) * h->d.LCAP, 4ull * glen, hipMemcpyDeviceToHost));
+  }
   HIPCK(hipMemcpy(&cursors[0], h->d.pingIdx + obs, 4, hipMemcpyDeviceToHost));
   HIPCK(hipMemcpy(&cursors[1], h->d.remoteIdx + obs, 4, hipMemcpyDeviceToHost));
   *fd_len = fl;

@@ -225,7 +225,32 @@ struct Dev {
   // per-tick receipt / sweep deltas are summed with one all-reduce. Kernels see W = 1; XW / xrank name the slot shard.
   uint32_t XW, xrank;
   int32_t* held_delta;  // [N] this tick's change of the member's gossip count from this shard's slots
+
+  // ---- RUMOR mode at scale ----
+  // implicit: no table or list is stored; a row is the PRECONVERGED row and list position p of observer m is
+  // list_at (the Feistel permutation k_init_lists would have written). Tables and lists never change in RUMOR mode;
+  // a gossip-list wrap would need a reshuffle and raises E_LIST.
+  // fastp4 (RUMOR, events not recorded): the GOSSIP events of first receipts are hashed (an order-independent sum)
+  // and counted where the receipts are applied, into evp_*, and folded into the member at P4 of the next tick: no
+  // receipt routing.
+  uint32_t implicit, fastp4;
+  unsigned long long* evp_hash;  // [N]
+  uint32_t* evp_n;               // [N]
 };
+
+// PRECONVERGED list w (0: pingMembers, 1: remoteMembers) of observer m: position p holds the other member of rank
+// feistel(p) (SEMANTICS.md §3; k_init_lists, and computed on the fly with implicit views)
+__host__ __device__ __forceinline__ FeistelPerm list_perm(const Dev& d, uint32_t m, uint32_t w) {
+  uint32_t k[4];
+  for (uint32_t r = 0; r < 4; ++r) k[r] = philox(m, 16 + 4 * w + r, 0, 0, d.seed_lo ^ SALT_INIT, d.seed_hi).x;
+  return make_perm(d.N - 1, k[0], k[1], k[2], k[3]);
+}
+__host__ __device__ __forceinline__ uint32_t list_at(const FeistelPerm& P, uint32_t m, uint32_t p) {
+  const uint32_t j = feistel(P, p);
+  return j < m ? j : j + 1;
+}
+// the PRECONVERGED record every row holds in RUMOR mode (k_init_rows)
+constexpr uint64_t PRE_REC = ((uint64_t)ST_ALIVE << 32) | META_BIT;
 
 // the slot shard that owns gossip gid (slot sharding; always this shard otherwise)
 __host__ __device__ __forceinline__ bool slot_mine(const Dev& d, uint64_t gid) {

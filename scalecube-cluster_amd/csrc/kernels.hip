@@ -67,6 +67,7 @@ __global__ void k_init_members(Dev d) {
 
 // one block per observer row (grid-strided): both planes are written with coalesced 4-B stores
 __global__ void k_init_rows(Dev d) {
+  if (d.implicit) return;
   const uint64_t full = rec_key(ST_ALIVE, 0) | META_BIT;
   for (uint32_t li = blockIdx.x; li < d.NL; li += gridDim.x) {
     uint32_t m = d.lo + li;
@@ -85,7 +86,7 @@ __global__ void k_init_rows(Dev d) {
 
 // PRECONVERGED lists: position p of observer m holds the other member of rank feistel_m(p) (SEMANTICS.md §3)
 __global__ void k_init_lists(Dev d) {
-  if (d.init_mode != 1 || d.N < 2) return;
+  if (d.init_mode != 1 || d.N < 2 || d.implicit) return;
   uint32_t n = d.N - 1;
   for (uint32_t m = d.lo + blockIdx.x; m < d.hi; m += gridDim.x) {
     for (uint32_t w = 0; w < 2; ++w) {
@@ -1033,6 +1034,14 @@ __global__ void k_gossip_apply(Dev d, uint32_t k) {
       atomicAdd(&d.held[t], 1u);
     atomicAdd(&d.slot_holders[g], 1);
     if (t < d.lo || t >= d.hi) continue;  // P4 of another shard's member
+    if (d.fastp4 && d.slot_subj[g] == USER_SUBJ) {  // RUMOR mode: the GOSSIP event of P4 (k + lat), hashed now
+      const uint64_t gid = d.slot_gid[g], key = d.slot_key[g];
+      const uint64_t ev = ((uint64_t)(k + d.lat) << 32) | (3ull << 30) | (uint32_t)(gid >> 32);
+      const uint64_t meta = ((uint64_t)(uint32_t)key << 32) | (key >> 32);  // (oldMeta, newMeta) = payload (lo, hi)
+      atomicAdd(&d.evp_hash[t], (unsigned long long)hpair(hpair(ev, meta), (uint32_t)gid));
+      atomicAdd(&d.evp_n[t], 1u);
+      continue;
+    }
     if (!receipt_matters(d, t, g, k + d.lat)) {  // counted as a record compare in P4, nothing else
       atomicAdd(&d.rc_ndrop[t], 1u);
       continue;
@@ -1080,13 +1089,20 @@ __global__ void __launch_bounds__(256) k_hash(Dev d, uint64_t* out, uint32_t now
   unsigned long long hr = 0, hf = 0, hg = 0, hgs = 0;
   const uint32_t* rk = d.rowk + lidx(d, m) * d.NS;
   const uint32_t* ra = d.rowa + lidx(d, m) * d.NS;
-  for (uint32_t s = threadIdx.x; s < d.N; s += blockDim.x) {
-    const uint32_t k = rk[s];
-    if ((k & 3u) != ST_ABSENT) hr += hpair(s, rec_join(k, ra[s]));
-  }
   uint32_t fl = d.fdLen[m], gl = d.gLen[m];
-  for (uint32_t p = threadIdx.x; p < fl; p += blockDim.x) hf += hpair((uint64_t)p | (1ull << 40), d.fdl[lidx(d, m) * d.LCAP + p]);
-  for (uint32_t p = threadIdx.x; p < gl; p += blockDim.x) hg += hpair((uint64_t)p | (2ull << 40), d.gl[lidx(d, m) * d.LCAP + p]);
+  if (d.implicit) {  // the PRECONVERGED row and lists, computed (engine.h list_at)
+    const FeistelPerm P0 = list_perm(d, m, 0), P1 = list_perm(d, m, 1);
+    for (uint32_t s = threadIdx.x; s < d.N; s += blockDim.x) hr += hpair(s, PRE_REC);
+    for (uint32_t p = threadIdx.x; p < fl; p += blockDim.x) hf += hpair((uint64_t)p | (1ull << 40), list_at(P0, m, p));
+    for (uint32_t p = threadIdx.x; p < gl; p += blockDim.x) hg += hpair((uint64_t)p | (2ull << 40), list_at(P1, m, p));
+  } else {
+    for (uint32_t s = threadIdx.x; s < d.N; s += blockDim.x) {
+      const uint32_t k = rk[s];
+      if ((k & 3u) != ST_ABSENT) hr += hpair(s, rec_join(k, ra[s]));
+    }
+    for (uint32_t p = threadIdx.x; p < fl; p += blockDim.x) hf += hpair((uint64_t)p | (1ull << 40), d.fdl[lidx(d, m) * d.LCAP + p]);
+    for (uint32_t p = threadIdx.x; p < gl; p += blockDim.x) hg += hpair((uint64_t)p | (2ull << 40), d.gl[lidx(d, m) * d.LCAP + p]);
+  }
   const bool dead = d.dead_tick[m] != NEVER;  // a crashed member keeps no gossips (SEMANTICS.md §1)
   for (uint32_t g = threadIdx.x; g < d.SLOTS && !dead; g += blockDim.x) {
     if (!d.slot_used[g]) continue;

@@ -539,7 +539,21 @@ __device__ __forceinline__ void do_spread_gossip(ML& L) {
   uint32_t F = d.F;
   uint32_t* T = d.T + (size_t)L.m * F;
   uint32_t cnt;
-  if (L.gLen < F) {
+  if (d.implicit) {  // RUMOR at scale: the PRECONVERGED permutation, read where a stored list would be (engine.h)
+    const FeistelPerm P = list_perm(d, L.m, 1);
+    if (L.gLen < F) {
+      for (uint32_t i = 0; i < L.gLen; ++i) T[i] = list_at(P, L.m, i);
+      cnt = L.gLen;
+    } else {
+      if (L.remoteIdx < 0 || (uint32_t)L.remoteIdx + F > L.gLen) {
+        set_err(d, E_LIST);  // the reshuffle of a wrapped cursor needs a stored list (N / F rounds: never at C5)
+        L.remoteIdx = 0;
+      }
+      for (uint32_t i = 0; i < F; ++i) T[i] = list_at(P, L.m, L.remoteIdx + i);
+      L.remoteIdx += (int32_t)F;
+      cnt = F;
+    }
+  } else if (L.gLen < F) {
     for (uint32_t i = 0; i < L.gLen; ++i) T[i] = L.gl[i];
     cnt = L.gLen;
   } else {
@@ -683,7 +697,8 @@ __device__ __forceinline__ void merge_payload(ML& L, uint32_t mi, uint32_t reaso
 // control path of k_member_tick this tick, and its work class: 1 = a ping is due and nothing else, 2 = only
 // request-state events (ping hops, ack arrivals, timeouts), 3 = both, 0 = anything else (SYNC receipt, gossip
 // receipts or round, timers, host requests, start).
-__device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t k, uint32_t& cls, uint32_t& drops) {
+__device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t k, uint32_t& cls, uint32_t& drops,
+                                              uint32_t& evs) {
   // A dead member does nothing itself, but the remote hops of its in-flight requests still run at the live
   // responders (their sends fail against the dead issuer), so those hops are still evaluated for the counters.
   // every word is loaded up front (no short-circuit chain of dependent loads); the SoA loads coalesce per wave
@@ -694,6 +709,18 @@ __device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t
   const bool dead = k >= dt;
   cls = 0;
   drops = 0;
+  if (d.fastp4) {  // RUMOR mode: P4's GOSSIP events of this tick, hashed and counted when they were applied
+    const uint32_t pn = d.evp_n[m];
+    if (pn) {
+      if (!dead) {  // a member crashed since holds no P4 (its receipts are dropped, as rc_cnt below)
+        d.evHash[m] += d.evp_hash[m];
+        d.evSeq[m] += pn;
+        evs = pn;
+      }
+      d.evp_hash[m] = 0;
+      d.evp_n[m] = 0;
+    }
+  }
   if (nd) {  // receipts that could not change the row: P4's record compares (none for a dead member)
     d.rc_ndrop[m] = 0;
     if (!dead) drops = nd;
@@ -1264,13 +1291,14 @@ __global__ void __launch_bounds__(256) k_member_tick(const Dev* __restrict__ dp,
   __shared__ uint32_t wc[4][4];  // [wave][class] busy members
   __shared__ uint32_t list[256];
   const uint32_t m = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t cls = 0, drops = 0;
-  const bool busy = m < d.hi && member_triage(d, m, k, cls, drops);
-  {  // the triage's record compares, one atomic per wave
-    uint32_t v = drops;
+  uint32_t cls = 0, drops = 0, evs = 0;
+  const bool busy = m < d.hi && member_triage(d, m, k, cls, drops, evs);
+  {  // the triage's record compares and folded RUMOR events, one atomic each per wave
+    uint32_t v = drops, e = evs;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o), e += __shfl_xor(e, o);
     if ((threadIdx.x & 63) == 0 && v) atomicAdd(&d.ctr[C_R], (unsigned long long)v);
+    if ((threadIdx.x & 63) == 0 && e) atomicAdd(&d.ctr[C_E], (unsigned long long)e);
   }
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t b0 = __ballot(busy && cls == 0), b1 = __ballot(busy && cls == 1), b2 = __ballot(busy && cls == 2),

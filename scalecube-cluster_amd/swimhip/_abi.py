@@ -18,6 +18,7 @@ MODE_FULL, MODE_RUMOR = 0, 1
 FLAG_RECORD_EVENTS = 1
 FLAG_PROFILE = 2
 FLAG_PROFILE_ALL = 4
+FLAG_IMPLICIT_VIEWS = 8
 
 EV_ADDED, EV_REMOVED, EV_UPDATED, EV_GOSSIP = 0, 1, 2, 3
 META_NONE = 0xFFFFFFFF

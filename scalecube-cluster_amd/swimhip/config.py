@@ -63,7 +63,8 @@ class SimConfig:
     latency_ticks: int = 1
     record_events: bool = False
     profile: bool = False
-    profile_all: bool = False  # SWIM_FLAG_PROFILE_ALL: every k_sync_diff launch timed (+ member / gossip kernels)
+    profile_all: bool = False
+    implicit_views: bool = False  # SWIM_FLAG_IMPLICIT_VIEWS (RUMOR mode): tables / lists computed, not stored  # SWIM_FLAG_PROFILE_ALL: every k_sync_diff launch timed (+ member / gossip kernels)
     gossip_slot_cap: int = 0
     pending_fetch_cap: int = 0
     event_cap: int = 0
@@ -96,7 +97,8 @@ class SimConfig:
         a.churn_per_period = self.churn_per_period
         a.n_dormant = self.n_dormant
         a.flags = (_abi.FLAG_RECORD_EVENTS if self.record_events else 0) | (_abi.FLAG_PROFILE if self.profile or self.profile_all else 0) \
-            | (_abi.FLAG_PROFILE_ALL if self.profile_all else 0)
+            | (_abi.FLAG_PROFILE_ALL if self.profile_all else 0) \
+            | (_abi.FLAG_IMPLICIT_VIEWS if self.implicit_views else 0)
         seeds = list(dict.fromkeys(c.seedMembers))
         if len(seeds) > 16:
             raise ValueError("at most 16 seed members")

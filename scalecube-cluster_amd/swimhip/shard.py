@@ -92,6 +92,27 @@ class GlooExchange(_HostExchange):
             rb[p] = rwords[p]
 
 
+class LoneExchange(_HostExchange):
+    """A timing rehearsal of one shard without its peers: every peer "sends" a block of the size this rank sends it,
+    all zeros. For slot shards (RUMOR mode) that is a zero gossip-count delta from every other shard, so the shard
+    runs its full per-tick work; the results are not the W-shard simulation's (bench.py --rehearse-shard)."""
+
+    def __init__(self, world):
+        super().__init__()
+        self.world = world
+
+    def _run(self, send, sb, recv, cap, rb):
+        total = 0
+        for p in range(self.world):
+            n = int(sb[p]) & COUNT_MASK
+            rb[p] = int(sb[p])
+            total += n
+        if total > cap:
+            raise RuntimeError("receive capacity")
+        if total:
+            C.memset(recv, 0, total)
+
+
 class ThreadExchange:
     """W shards in one process: rank r's callback deposits its blocks, waits for every rank, takes its own."""
 

@@ -438,3 +438,40 @@ def test_sampled_diff_accounting(oracle, engine, profile_all):
     assert c["diff_msgs"] - b["diff_msgs"] == want
     assert c["diff_ns"] > b["diff_ns"]
     e.close()
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_rumor_mode_at_scale_paths(oracle, engine, world):
+    """The C5 code paths at test size: implicit views (the PRECONVERGED row and Feistel lists computed, not stored;
+    SWIM_FLAG_IMPLICIT_VIEWS, forced here, always on above 65536 members) and, with events not recorded, the GOSSIP
+    events hashed and counted where first receipts are applied (no receipt routing). Single GPU and 3 slot shards."""
+    import dataclasses
+    from swimhip.shard import ThreadShardGroup
+    cfg = SimConfig(n_members=2000, mode=_abi.MODE_RUMOR, churn_per_period=20)
+    o = SimulatedCluster(oracle, cfg)
+    ecfg = dataclasses.replace(cfg, implicit_views=True)
+    e = SimulatedCluster(engine, ecfg) if world == 1 else ThreadShardGroup(engine, ecfg, world)
+    for c in (o, e):
+        c.set_default_loss(5)
+    run_lockstep(o, e, 200, 50, f"rumor implicit views W={world}", events=False)
+    for c in (o, e):
+        c.kill(7)
+    run_lockstep(o, e, 100, 50, f"rumor implicit views + kill W={world}", events=False)
+    for m in (0, 1999):
+        assert o.lists(m)[1].tolist() == e.lists(m)[1].tolist()
+        assert np.array_equal(o.row(m), e.row(m))
+    assert e.counters()["events"] == o.counters()["events"] > 0
+    e.close()
+
+
+def test_c5_shard_fits_one_gpu(engine):
+    """C5 (10^6 members, RUMOR, 1 % churn on 8 GPUs): rank 0 of 8 slot shards at full size fits one MI355X. Tables
+    and lists are implicit; the holder table holds this shard's ~1/8 of the ~2.7·10^5 live rumors (40 000 slots)."""
+    from swimhip.shard import ShardedCluster, ThreadExchange
+    cfg = SimConfig(n_members=1_000_000, mode=_abi.MODE_RUMOR, churn_per_period=10_000, gossip_slot_cap=40_000)
+    c = ShardedCluster(engine, cfg, 0, 8, _abi.TRANSPORT_HOST, exchange=ThreadExchange(8).endpoint(0))
+    try:
+        nbytes = c.counters()["device_bytes"]
+    finally:
+        c.close()
+    assert nbytes < 250e9, nbytes
