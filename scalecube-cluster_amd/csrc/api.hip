@@ -275,8 +275,13 @@ int build(swim_handle* h) {
   d.EVCAP = c.event_cap ? c.event_cap : (1u << 20);
   d.DCAP = (uint32_t)std::min<uint64_t>(1ull << 27, std::max<uint64_t>(1ull << 16, N * 16384));
   d.RCAP = d.DCAP;
-  d.SLOWCAP = d.DCAP;
-  d.RPCAP = d.DCAP;
+  // infectedFrom replays: in a small cluster most pairs have a logged contact, so under a DEAD-gossip storm nearly
+  // every send is replayed (C4 at 2 000 members: ~4·10^7 per tick)
+  d.SLOWCAP = d.RPCAP = std::max<uint32_t>(d.DCAP, 1u << 26);
+  if (const char* dc = getenv("SWIM_DELIV_CAP")) {  // experiments (tools/exp_c4.py): first receipts per tick
+    d.DCAP = d.RCAP = (uint32_t)std::min<uint64_t>(1ull << 30, strtoull(dc, nullptr, 0));
+    d.SLOWCAP = d.RPCAP = std::max(d.SLOWCAP, d.DCAP);
+  }
   if (d.implicit) {
     // C5: every period's rumors start at one tick, so their epidemics peak together: on one of 8 slot shards a tick
     // can deliver ~7·10^8 first receipts (8 B each). Their GOSSIP events skip the receipt routing (fastp4), and

@@ -13,7 +13,7 @@ import pytest
 GOLDEN = Path(__file__).resolve().parent / "golden"
 sys.path.insert(0, str(GOLDEN))
 
-from scenarios import SCENARIOS, record  # noqa: E402
+from scenarios import SCENARIOS, SLOW_ON_ORACLE, record  # noqa: E402
 
 from swimhip.cluster import SimulatedCluster  # noqa: E402
 
@@ -30,7 +30,7 @@ def check(rec, want, who):
         assert rec["events"] == want["events"], f"{who}: {want['scenario']} event list differs"
 
 
-@pytest.mark.parametrize("name", list(SCENARIOS))
+@pytest.mark.parametrize("name", [n for n in SCENARIOS if n not in SLOW_ON_ORACLE])
 def test_oracle_matches_golden(oracle, name):
     cfg, _ = SCENARIOS[name]()
     c = SimulatedCluster(oracle, cfg)
@@ -48,7 +48,8 @@ def test_engine_matches_golden(engine, name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,world", [("c1", 2), ("c2_small", 3), ("c4_small", 2), ("c3_small", 4), ("c5_small", 3)])
+@pytest.mark.parametrize("name,world", [("c1", 2), ("c2_small", 3), ("c4_small", 2), ("c3_small", 4), ("c5_small", 3),
+                                        ("c4_mid", 2)])
 def test_sharded_engine_matches_golden(engine, name, world):
     from swimhip.shard import ThreadShardGroup
     cfg, _ = SCENARIOS[name]()

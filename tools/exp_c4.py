@@ -6,20 +6,24 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT / "scalecube-cluster_amd"))
+import os  # noqa: E402
+
+os.environ.setdefault("SWIM_DELIV_CAP", str(1 << 28))  # the DEAD-gossip storm delivers ~10^8 first receipts a tick
 import swimhip  # noqa: E402
 from swimhip import ClusterConfig, SimConfig  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
 heal = int(sys.argv[2]) if len(sys.argv) > 2 else 200
 end = int(sys.argv[3]) if len(sys.argv) > 3 else 320
-slots = int(sys.argv[4]) if len(sys.argv) > 4 else 1 << 20  # the DEAD-gossip storm needs far more than 64 per member
-c = swimhip.cluster(SimConfig(n_members=n, cluster=ClusterConfig(seedMembers=[0]), gossip_slot_cap=slots))
+slots = int(sys.argv[4]) if len(sys.argv) > 4 else 1 << 22  # the DEAD-gossip storm needs far more than 64 per member
+c = swimhip.cluster(SimConfig(n_members=n, cluster=ClusterConfig(seedMembers=[0]), gossip_slot_cap=slots,
+                              pending_fetch_cap=16384, list_slack=4096))  # the heal re-adds a whole side at once
 c.partition([0] * (n // 2) + [1] * (n - n // 2))
 p, t_all = 0, time.perf_counter()
 while p < end:
     if p == heal:
         c.unblock_all()
-    step = min(20, (heal if p < heal else end) - p)
+    step = min(10, (heal if p < heal else end) - p)
     t0 = time.perf_counter()
     c.run_periods(step)
     c.sync()

@@ -1,10 +1,10 @@
-# C4-shaped runs (partition healed at period 200, to period 320) at reduced N, to size a C4 bench line
-set -e
+# C4-shaped runs at reduced N (partition healed at period 200, run to period 320): wall time per 10 periods and the
+# storm counters; each size under its own time limit
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/c4
+O=gpurun_out/${1:-c4}
 mkdir -p $O
-timeout -k 10 300 python -u tools/exp_c4.py 2000 > $O/c4_2000.log 2>&1 || { tail -5 $O/c4_2000.log; exit 1; }
-tail -4 $O/c4_2000.log
-timeout -k 10 400 python -u tools/exp_c4.py 5000 > $O/c4_5000.log 2>&1 || { tail -5 $O/c4_5000.log; exit 1; }
-tail -4 $O/c4_5000.log
+for n in ${2:-1000 2000}; do
+  timeout -k 10 ${3:-400} python -u tools/exp_c4.py $n > $O/c4_$n.log 2>&1
+  echo "N=$n rc=$?"; tail -3 $O/c4_$n.log
+done
