@@ -256,7 +256,14 @@ int build(swim_handle* h) {
   d.LOGW = 8;
   while (d.LOGW < 4 * (maxSpread + 2)) d.LOGW <<= 1;  // rounds kept for the infectedFrom replay
   d.LOOKBACK = d.LOGW * d.gossip_t;
-  d.HCAP = 1u << 20;
+  // incarnation history of reborn (gossip, member) pairs: storms in small clusters (C4's heal) rebirth a large
+  // share of the holder states; sized from the holder table, 2^20 .. 2^24 entries (88 B each)
+  {
+    const uint64_t slots_est = c.gossip_slot_cap ? c.gossip_slot_cap : 64 * N;
+    uint64_t want = slots_est * N / 8, hc = 1u << 20;
+    while (hc < want && hc < (1u << 24)) hc <<= 1;
+    d.HCAP = (uint32_t)hc;
+  }
   // default: 64 slots per member, at most 32 GB of holder table (C2's SYNC re-spread storm keeps ~10^5 gossips alive)
   uint64_t slots = c.gossip_slot_cap ? c.gossip_slot_cap
                                      : std::min<uint64_t>(1ull << 22, std::max<uint64_t>(1024, std::min<uint64_t>(64 * N, (32ull << 30) / (4 * N))));

@@ -441,7 +441,7 @@ __device__ void hist_push(const Dev& d, uint64_t gid, uint32_t member, uint32_t 
     e[2] = (uint64_t)member | ((uint64_t)(n + 1) << 32);
     return;
   }
-  atomicOr(d.err, E_REBORN);
+  if (atomicOr(d.err, E_REBORN) == 0) d.err[1] = 1;  // info 1: the history table is full (HCAP)
 }
 
 // creation tick of member's incarnation of g that existed at tick tau (NEVER if none)
@@ -464,7 +464,8 @@ __device__ uint32_t inc_at(const Dev& d, uint32_t member, uint32_t g, uint64_t g
       if (cc[i] < oldest) oldest = cc[i];
       if (cc[i] <= tau && (best == NEVER || cc[i] > best)) best = cc[i];
     }
-    if (best == NEVER && n > HKEEP && tau < oldest) atomicOr(d.err, E_REBORN);  // an incarnation the ring dropped
+    if (best == NEVER && n > HKEEP && tau < oldest && atomicOr(d.err, E_REBORN) == 0)
+      d.err[1] = 2;  // info 2: an incarnation the ring dropped (more than HKEEP rebirths)
     return best;
   }
   return NEVER;

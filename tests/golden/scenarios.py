@@ -37,7 +37,8 @@ def _c4_mid():  # C4-shaped at 200 members: suspicion timeouts (40 periods) star
     # time on 8 threads, SWIMREF_THREADS=8 python tests/golden/make_golden.py c4_mid); the CPU suite does not replay it
     n = 200
     g = [0] * (n // 2) + [1] * (n // 2)
-    return SimConfig(n_members=n, cluster=ClusterConfig(seedMembers=[0]), gossip_slot_cap=1 << 18), [
+    return SimConfig(n_members=n, cluster=ClusterConfig(seedMembers=[0]), gossip_slot_cap=1 << 18, pending_fetch_cap=4096,
+                     list_slack=4096), [
         ("partition", g), ("periods", 45), ("unblock", None), ("periods", 30)]
 
 
