@@ -24,6 +24,8 @@ using namespace swim;
 
 struct Group;  // swim_config.n_gpus > 1: one handle over several row-sharded shard handles (below)
 
+constexpr size_t GUARD = 4096;  // SWIM_GUARD: guard bytes on each side of every device allocation
+
 struct swim_handle {
   swim_config cfg;
   Dev d;
@@ -31,6 +33,7 @@ struct swim_handle {
   uint64_t tick = 0;
   std::string err;
   std::vector<void*> allocs;
+  std::vector<std::pair<char*, size_t>> guards;  // SWIM_GUARD: (allocation, bytes inside the guards)
   std::vector<swim_event> host_events;
   // settings-epoch ring mirrored on the host
   uint32_t ep_from[MAX_EPOCHS], ep_loss[MAX_EPOCHS], ep_part[MAX_EPOCHS];
@@ -83,12 +86,20 @@ template <class T>
 int dalloc(swim_handle* h, T** p, size_t count) {
   size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
   void* q = nullptr;
-  hipError_t e = hipMalloc(&q, bytes);
+  // debugging aid (SWIM_GUARD): GUARD bytes of 0x5A before and after every allocation, checked after every step
+  const bool guard = getenv("SWIM_GUARD") != nullptr;
+  hipError_t e = hipMalloc(&q, bytes + (guard ? 2 * GUARD : 0));
   if (e != hipSuccess) {
     h->err = "hipMalloc(" + std::to_string(bytes) + ") failed: " + hipGetErrorString(e);
     return SWIM_ENOMEM;
   }
   h->allocs.push_back(q);
+  if (guard) {
+    hipMemsetAsync(q, 0x5A, GUARD, h->stream);
+    hipMemsetAsync((char*)q + GUARD + bytes, 0x5A, GUARD, h->stream);
+    h->guards.push_back({(char*)q, bytes});
+    q = (char*)q + GUARD;
+  }
   h->bytes += bytes;
   // debugging aids: poison fresh allocations (all, or only allocation #SWIM_POISON_ONLY) to catch never-written state
   const char* po = getenv("SWIM_POISON_ONLY");
@@ -108,6 +119,21 @@ int check_err(swim_handle* h) {
   if (e != hipSuccess) {
     h->err = std::string("device failure: ") + hipGetErrorString(e);
     return SWIM_EDEVICE;
+  }
+  for (size_t i = 0; i < h->guards.size(); ++i) {  // SWIM_GUARD
+    std::vector<unsigned char> g(2 * GUARD);
+    const auto& a = h->guards[i];
+    if (hipMemcpy(g.data(), a.first, GUARD, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(g.data() + GUARD, a.first + GUARD + a.second, GUARD, hipMemcpyDeviceToHost) != hipSuccess)
+      return SWIM_EDEVICE;
+    for (size_t j = 0; j < 2 * GUARD; ++j)
+      if (g[j] != 0x5A) {
+        h->err = "guard of allocation #" + std::to_string(i) + " (" + std::to_string(a.second) + " B) overwritten at " +
+                 (j < GUARD ? "-" + std::to_string(GUARD - j) : "+" + std::to_string(j - GUARD)) + " value " +
+                 std::to_string(g[j]);
+        fprintf(stderr, "%s\n", h->err.c_str());
+        return SWIM_EDEVICE;
+      }
   }
   uint32_t eb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (hipMemcpy(eb, h->d.err, sizeof(eb), hipMemcpyDeviceToHost) != hipSuccess) return SWIM_EDEVICE;
