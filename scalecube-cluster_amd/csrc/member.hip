@@ -666,30 +666,60 @@ __device__ __forceinline__ void merge_payload(ML& L, uint32_t mi, uint32_t reaso
   L.c[C_R] += mm.psize;
   L.c[C_SYNCMERGE]++;
   const uint32_t nt = L.ntrk;
-  if (nt > TRK) {  // rare: many subjects changed earlier in this tick; exact full walk
-    for (uint32_t s = 0; s < L.N; ++s) merge_record(L, s, payload_key_at(d, mm, b, s), reason, g);
-    return;
-  }
-  if (mm.ncand == 0 && nt == 0) return;  // steady state: nothing differs, skip the chunk walk
-  for (uint32_t i = 1; i < nt; ++i)  // the tracked subjects in ascending order (insertion sort, at most TRK)
-    for (uint32_t j = i; j > 0 && L.trk[j - 1] > L.trk[j]; --j) {
-      const uint32_t t = L.trk[j];
-      L.trk[j] = L.trk[j - 1];
-      L.trk[j - 1] = t;
+  const bool full = nt > TRK;  // rare: many subjects changed earlier in this tick; exact full walk
+  if (!full && mm.ncand == 0 && nt == 0) return;  // steady state: nothing differs, skip the chunk walk
+  if (!full)
+    for (uint32_t i = 1; i < nt; ++i)  // the tracked subjects in ascending order (insertion sort, at most TRK)
+      for (uint32_t j = i; j > 0 && L.trk[j - 1] > L.trk[j]; --j) {
+        const uint32_t t = L.trk[j];
+        L.trk[j] = L.trk[j - 1];
+        L.trk[j - 1] = t;
+      }
+  // One walk with a single merge site: update_membership is large, and each inlined copy of it costs instruction
+  // cache in every wave of this kernel. The next record comes from the full payload, or else from the candidate pool
+  // and the tracked subjects merged in subject order (a tracked candidate takes the pool's record).
+  uint32_t ti = 0, c = 0, e = 0, n = 0, off = 0, s = 0;
+  bool pool = !full && mm.ncand != 0;
+  for (;;) {
+    uint32_t subj, k1;
+    if (full) {
+      if (s >= L.N) break;
+      subj = s;
+      k1 = payload_key_at(d, mm, b, s);
+      ++s;
+    } else {
+      while (pool && e == n) {
+        if (c == d.NCHUNK) {
+          pool = false;
+          break;
+        }
+        const uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NCHUNK + c) * 2;
+        off = cm[0];
+        n = cm[1];
+        e = 0;
+        ++c;
+      }
+      uint64_t prec = 0;
+      uint32_t ps = NEVER;
+      if (pool) {
+        prec = d.pool[(size_t)off + e];
+        ps = (uint32_t)(prec >> 34);
+      }
+      const uint32_t ts = ti < nt ? L.trk[ti] : NEVER;
+      if (ps == NEVER && ts == NEVER) break;
+      if (ts < ps) {
+        subj = ts;
+        k1 = payload_key_at(d, mm, b, ts);
+        ++ti;
+      } else {
+        subj = ps;
+        k1 = key32(prec & KEY_MASK);
+        ++e;
+        if (ts == ps) ++ti;
+      }
     }
-  uint32_t ti = 0;
-  for (uint32_t c = 0; c < d.NCHUNK && mm.ncand; ++c) {
-    const uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NCHUNK + c) * 2;
-    uint32_t off = cm[0], n = cm[1];
-    for (uint32_t e = 0; e < n; ++e) {
-      uint64_t rec = d.pool[(size_t)off + e];
-      uint32_t subj = (uint32_t)(rec >> 34);
-      for (; ti < nt && L.trk[ti] < subj; ++ti) merge_record(L, L.trk[ti], payload_key_at(d, mm, b, L.trk[ti]), reason, g);
-      if (ti < nt && L.trk[ti] == subj) ++ti;  // a candidate: its record is the pool's
-      merge_record(L, subj, key32(rec & KEY_MASK), reason, g);
-    }
+    merge_record(L, subj, k1, reason, g);
   }
-  for (; ti < nt; ++ti) merge_record(L, L.trk[ti], payload_key_at(d, mm, b, L.trk[ti]), reason, g);
 }
 
 // Triage (k_member_triage): the idle fast path. Most members have nothing due in most ticks (a ping every 10 ticks,
@@ -913,24 +943,27 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
       }
       SyncMsg mm = d.msgs[pb][mi];
       if (mc_group(d, mm.src) != mc_group(d, m)) continue;  // checkSyncGroup (:320-321,431-437): another group's data
+      // one merge_payload / finish site for the three cases (each inlined copy is large)
+      int g = -1;
+      uint32_t reason = R_SYNC;
+      bool grouped = false;
       if (mm.kind == K_SYNC) {
-        int g = alloc_group(L, 0, mm.src, mm.cid_iss, mm.cid_cnt);
-        merge_payload(L, mi, R_SYNC, g);
-        if (g >= 0) {
-          grp(L, g)[5] |= GF_SEALED;
-          finish(L, g, false);
-        }
+        g = alloc_group(L, 0, mm.src, mm.cid_iss, mm.cid_cnt);
+        grouped = true;
       } else if (mm.cid_iss == NONE32) {
-        merge_payload(L, mi, R_SYNC, -1);
       } else if (mm.cid_iss == m && (L.initFlags & INIT_ACTIVE) && !(L.initFlags & INIT_RECEIVED) &&
                  mm.cid_cnt >= L.initCidBase && mm.cid_cnt < L.initCidBase + L.initN) {
         L.initFlags |= INIT_RECEIVED;  // mergeDelayError(...).take(1) (:239-243)
-        int g = alloc_group(L, 1, NONE32, NONE32, 0);
-        merge_payload(L, mi, R_INITIAL, g);
-        if (g >= 0) {
-          grp(L, g)[5] |= GF_SEALED;
-          finish(L, g, false);
-        }
+        g = alloc_group(L, 1, NONE32, NONE32, 0);
+        reason = R_INITIAL;
+        grouped = true;
+      } else {
+        continue;  // a SYNC_ACK of another initial sync or of an expired one (:326-328)
+      }
+      merge_payload(L, mi, reason, g);
+      if (grouped && g >= 0) {
+        grp(L, g)[5] |= GF_SEALED;
+        finish(L, g, false);
       }
     }
     L.trk_on = false;
