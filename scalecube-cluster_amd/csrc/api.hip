@@ -430,6 +430,8 @@ int build(swim_handle* h) {
   HIPCK(hipMemsetAsync(d.dead_rx, 0, 4 * N, h->stream));
   HIPCK(hipMemsetAsync(d.leaving, 0, 4 * N, h->stream));
   HIPCK(hipMemsetAsync(d.m_head, 0xFF, 2 * N * 4, h->stream));
+  HIPCK(hipMemsetAsync(d.msgs[0], 0xFF, (size_t)d.MSGCAP * sizeof(SyncMsg), h->stream));  // pin = NEVER (send_sync)
+  HIPCK(hipMemsetAsync(d.msgs[1], 0xFF, (size_t)d.MSGCAP * sizeof(SyncMsg), h->stream));
   if (d.W > 1) {
     HIPCK(hipMemsetAsync(d.xn, 0, 32, h->stream));
     HIPCK(hipMemsetAsync(d.rq_n, 0, 4ull * d.W, h->stream));

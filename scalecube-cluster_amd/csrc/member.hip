@@ -117,13 +117,17 @@ __device__ __forceinline__ bool send_sync(ML& L, uint32_t kind, uint32_t dst, ui
   mm.psize = L.tsize;
   mm.ncand = 0;
   mm.pad = L.pend;  // chained so that a later row write can redirect the payload to a snapshot (cow)
-  mm.pin = NEVER;
-  d.msgs[b][i] = mm;
+  // every field but `pin`: pin_msg of another sender may set that one by atomics in this same tick (from another
+  // XCD, whose L2 is not this one's), so this sender never stores it. It is NEVER already: the receiver of the
+  // slot's previous message reset it after use (P1 below), or the buffer's initialisation did. Without a store to it
+  // no release fence is needed (one per send cost an L2 write-back and invalidate: ~14 us per tick at C3).
+  SyncMsg* q = &d.msgs[b][i];
+  q->src = mm.src, q->dst = mm.dst, q->kind = mm.kind, q->seq = mm.seq, q->cid_iss = mm.cid_iss;
+  q->cid_cnt = mm.cid_cnt, q->payload = mm.payload, q->psize = mm.psize, q->ncand = mm.ncand, q->pad = mm.pad;
   L.pend = i;
   // the receiver's inbound list for the next tick (sharded handles build it when the exchange commits the list);
-  // a receiver with several payloads gets them pinned (pin_msg). The fence publishes the record before its index.
+  // a receiver with several payloads gets them pinned (pin_msg)
   if (d.W == 1) {
-    __threadfence();
     const uint32_t old = atomicExch(&d.m_head[(size_t)b * d.N + dst], i);
     d.m_next[(size_t)b * d.MSGCAP + i] = old;
     if (old != NEVER) {
@@ -758,7 +762,11 @@ __device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t
   if (dead) {
     d.rc_cnt[m] = 0;
     d.rc_fill[m] = 0;
-    if (k > 0) d.m_head[(size_t)((k - 1) & 1) * d.N + m] = NEVER;
+    if (k > 0 && mh != NEVER) {  // dropped payloads: their pins go back to NEVER (send_sync)
+      const uint32_t pb = (k - 1) & 1;
+      for (uint32_t q = mh; q != NEVER; q = d.m_next[(size_t)pb * d.MSGCAP + q]) d.msgs[pb][q].pin = NEVER;
+      d.m_head[(size_t)pb * d.N + m] = NEVER;
+    }
   } else {
     const bool busy = (k > 0 && mh != NEVER) | (rc != 0) | (pi != 0) | (ne <= k) | (tm <= k) | (k == np) | (k == ns) |
                       ((inf & INIT_ACTIVE) != 0) | (k == st);
@@ -967,6 +975,8 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
       }
     }
     L.trk_on = false;
+    if (n > 1 || more)  // the pins of this tick's payloads go back to NEVER for the slots' next use (send_sync)
+      for (uint32_t q = head; q != NEVER; q = mnext[q]) d.msgs[pb][q].pin = NEVER;
   }
 
   lap(0);  // P0 + P1
