@@ -31,6 +31,18 @@ __device__ __forceinline__ bool last_block(uint32_t* ctr, uint32_t nblocks) {
   return last;
 }
 
+// ticket only, no release / acquire: for a last block that reads nothing the other blocks stored with plain stores
+// (k_member_tick: tick_flag reads free_top by an atomic load). A release per block writes back its XCD's L2, which
+// the waves still running there then pay for.
+__device__ __forceinline__ bool last_block_ticket(uint32_t* ctr, uint32_t nblocks) {
+  __shared__ bool last;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblocks - 1u;
+  __syncthreads();
+  return last;
+}
+
 // 16-B row loads
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint4 ld_c4(const uint32_t* p) { return *(const uint4*)p; }
@@ -253,7 +265,7 @@ __device__ __forceinline__ void tick_flag(const Dev& d, uint32_t k) {
   *d.deliv_n = 0;
   *d.rc_n = 0;
   d.deaths_n[(k + 1) & 1] = 0;
-  d.hflag[0] = (uint32_t)((int32_t)d.SPR - *d.free_top);
+  d.hflag[0] = (uint32_t)((int32_t)d.SPR - __hip_atomic_load(d.free_top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   __threadfence_system();
 }
 

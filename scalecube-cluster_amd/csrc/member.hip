@@ -1381,7 +1381,7 @@ __global__ void __launch_bounds__(256) k_member_tick(const Dev* __restrict__ dp,
     }
   }
   if (!flag) return;
-  if (!last_block(d.mdone, gridDim.x) || threadIdx.x != 0) return;
+  if (!last_block_ticket(d.mdone, gridDim.x) || threadIdx.x != 0) return;
   *d.mdone = 0;
   tick_flag(d, k);
 }
