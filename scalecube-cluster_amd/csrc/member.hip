@@ -64,7 +64,12 @@ __device__ __forceinline__ void cow(ML& L) {
     return;
   }
   uint32_t* dst = d.arena[b] + (size_t)r * d.NS;
-  for (uint32_t s = 0; s < d.NS; ++s) dst[s] = L.rk[s];  // keys only, with the zero padding k_sync_diff reads up to NS
+  // keys only, with the zero padding k_sync_diff reads up to NS; one lane copies N words, so 16-B accesses with many
+  // in flight (rows are 32-B aligned, NS a multiple of 8)
+  const uint4* src4 = (const uint4*)L.rk;
+  uint4* dst4 = (uint4*)dst;
+#pragma unroll 16
+  for (uint32_t s = 0; s < d.NS / 4; ++s) dst4[s] = src4[s];
   if (L.rd)
     for (uint32_t w = 0; w < d.MW; ++w) d.arena_dirty[b][(size_t)r * d.MW + w] = L.rd[w];
   for (uint32_t i = L.pend; i != NEVER; i = d.msgs[b][i].pad) d.msgs[b][i].payload = r;
@@ -1253,10 +1258,16 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   }
   if (L.timerMin <= k) {  // suspicion timeouts (:608-618), ascending subject; lazy minimum
     uint32_t nmin = NEVER;
-    for (uint32_t s = 0; s < L.N; ++s) {
-      const uint32_t a = L.ra[s];  // the aux plane alone holds the deadline
+    // one lane scans the whole aux plane: 16-B loads, four subjects each (rows are 32-B aligned); processing
+    // subject s writes only entry s, so the loaded words of the later subjects stay current
+    for (uint32_t s4 = 0; s4 < L.N; s4 += 4) {
+     const uint4 a4 = *(const uint4*)(L.ra + s4);
+     const uint32_t av[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+     for (uint32_t j = 0; j < 4; ++j) {
+      const uint32_t s = s4 + j, a = av[j];  // the aux plane alone holds the deadline
       uint32_t dl = rec_timer((uint64_t)a << 34);
-      if (dl == 0) continue;
+      if (dl == 0 || s >= L.N) continue;
       const uint64_t v = rec_join(L.rk[s], a);
       if (dl == k) {
         L.ra[s] = aux32(rec_with_timer(v, 0));
@@ -1267,6 +1278,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
       } else if (dl < nmin) {
         nmin = dl;
       }
+     }
     }
     L.timerMin = nmin;
   }
