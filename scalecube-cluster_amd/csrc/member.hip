@@ -35,6 +35,11 @@ struct ML {
   uint32_t* trk;  // subjects whose key changed in this tick's P1 (several payloads only); ntrk > TRK: overflowed
   uint32_t ntrk;
   bool trk_on;
+  // deferred copy-on-write (cow): open snapshots of this member (indices into the block's list cw) and its undo log
+  uint4* cw;       // block list (LDS): member, arena row, first log entry, log length at the end of the body
+  uint32_t* cw_n;  // LDS counter of cw
+  uint32_t* ulog;  // this member's log: (subject, key before the write) per row write while a snapshot is open
+  uint32_t ncreq, nlog;  // open snapshots (their cw entries carry this member's id), logged writes
 
 };
 
@@ -53,7 +58,40 @@ __device__ __forceinline__ void shuffle_list(ML& L, uint32_t* v, uint32_t n, uin
   }
 }
 
-// copy-on-write of the live row for SYNC payloads sent earlier in this tick
+// copy-on-write of the live row for SYNC payloads sent earlier in this tick. The payloads take an
+// arena row; the copy itself is deferred to the end of k_member_tick, where the member's whole block copies the row
+// (coalesced) and then undoes, newest first, the writes the member logged after this point (row_put). One lane
+// copying N words would hold the whole kernel (~3 ms per tick at 100k members when a SYNC sender also merges a
+// gossip in the same tick). Past CREQ open snapshots, ULOG logged writes or CWMAX snapshots per block, the copy is
+// made here, by this lane (cow_now).
+__device__ __forceinline__ void copy_row_to(ML& L, uint32_t r) {
+  const Dev& d = *L.d;
+  const uint32_t b = L.k & 1;
+  const uint4* src4 = (const uint4*)L.rk;  // keys only, with the zero padding k_sync_diff reads up to NS
+  uint4* dst4 = (uint4*)(d.arena[b] + (size_t)r * d.NS);
+#pragma unroll 16
+  for (uint32_t s = 0; s < d.NS / 4; ++s) dst4[s] = src4[s];
+  if (L.rd)
+    for (uint32_t w = 0; w < d.MW; ++w) d.arena_dirty[b][(size_t)r * d.MW + w] = L.rd[w];
+}
+
+// the open snapshots, now: live row, then the logged writes since each one opened undone newest first
+__device__ __forceinline__ void cow_now(ML& L) {
+  const Dev& d = *L.d;
+  const uint32_t b = L.k & 1;
+  const uint32_t n = min(*L.cw_n, CWMAX);
+  for (uint32_t q = 0; q < n; ++q) {
+    uint4& e = L.cw[q];
+    if (e.x != L.m) continue;  // another member's (entries are NEVER until written)
+    copy_row_to(L, e.y);
+    uint32_t* dst = d.arena[b] + (size_t)e.y * d.NS;
+    for (uint32_t j = L.nlog; j-- > e.z;) dst[L.ulog[2 * j]] = L.ulog[2 * j + 1];
+    e.x = NEVER;  // done: the block epilogue skips it
+  }
+  L.ncreq = 0;
+  L.nlog = 0;
+}
+
 __device__ __forceinline__ void cow(ML& L) {
   const Dev& d = *L.d;
   uint32_t b = L.k & 1;
@@ -63,17 +101,16 @@ __device__ __forceinline__ void cow(ML& L) {
     L.pend = NEVER;
     return;
   }
-  uint32_t* dst = d.arena[b] + (size_t)r * d.NS;
-  // keys only, with the zero padding k_sync_diff reads up to NS; one lane copies N words, so 16-B accesses with many
-  // in flight (rows are 32-B aligned, NS a multiple of 8)
-  const uint4* src4 = (const uint4*)L.rk;
-  uint4* dst4 = (uint4*)dst;
-#pragma unroll 16
-  for (uint32_t s = 0; s < d.NS / 4; ++s) dst4[s] = src4[s];
-  if (L.rd)
-    for (uint32_t w = 0; w < d.MW; ++w) d.arena_dirty[b][(size_t)r * d.MW + w] = L.rd[w];
   for (uint32_t i = L.pend; i != NEVER; i = d.msgs[b][i].pad) d.msgs[b][i].payload = r;
   L.pend = NEVER;
+  if (L.ncreq == CREQ) cow_now(L);  // rare: many send-then-write rounds in one tick
+  const uint32_t idx = atomicAdd(L.cw_n, 1u);  // LDS
+  if (idx >= CWMAX) {  // the block's list is full: this snapshot now, by this lane
+    copy_row_to(L, r);
+    return;
+  }
+  L.cw[idx] = make_uint4(L.m, r, L.nlog, 0u);
+  L.ncreq++;
 }
 
 __device__ __forceinline__ uint64_t row_ld(const ML& L, uint32_t s) { return rec_join(L.rk[s], L.ra[s]); }
@@ -83,6 +120,14 @@ __device__ __forceinline__ void row_put(ML& L, uint32_t s, uint64_t v) {
   const uint32_t k = key32(v);
   if (rec_inc(v) >= INC_LIMIT) set_err(*L.d, E_INC);
   if (L.pend != NEVER && L.rk[s] != k) cow(L);
+  if (L.ncreq && L.rk[s] != k) {  // an open snapshot: log the key this write replaces
+    if (L.nlog == ULOG) cow_now(L);
+    else {
+      L.ulog[2 * L.nlog] = s;
+      L.ulog[2 * L.nlog + 1] = L.rk[s];
+      L.nlog++;
+    }
+  }
   if (L.trk_on && L.rk[s] != k && L.ntrk <= TRK) {  // merge_payload re-checks it against the later payloads
     bool seen = false;
     for (uint32_t i = 0; i < L.ntrk; ++i) seen |= L.trk[i] == s;
@@ -798,7 +843,8 @@ __device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t
   return true;
 }
 
-__device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint32_t k, unsigned long long (&cnt)[8]) {
+__device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint32_t k, unsigned long long (&cnt)[8],
+                                                 uint4* cw, uint32_t* cw_n) {
   const bool dead = dead_at(d, m, k);
   ML L;
   L.d = &d;
@@ -848,6 +894,11 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   L.trk = d.trk + li * TRK;
   L.ntrk = 0;
   L.trk_on = false;
+  L.cw = cw;
+  L.cw_n = cw_n;
+  L.ulog = d.ulog + li * ULOG * 2;
+  L.ncreq = 0;
+  L.nlog = 0;
   // SWIM_EXP & 16 (timing experiment): shader cycles per phase summed over members, ctr[8..12]
   const bool prof = (d.exp & 16) != 0;
   unsigned long long tp = prof ? clock64() : 0;
@@ -1303,6 +1354,9 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   for (uint32_t q = 0; q < L.npath; ++q) nev = min(nev, L.paths[(size_t)q * 5 + 2]);
   for (uint32_t q = 0; q < L.nsub; ++q) nev = min(nev, L.subs[(size_t)q * 4 + 3]);
   nev = min(nev, L.fnext);
+  if (L.ncreq)  // the log length the block epilogue undoes from
+    for (uint32_t q = 0, n = min(*L.cw_n, CWMAX); q < n; ++q)
+      if (L.cw[q].x == m) L.cw[q].w = L.nlog;
   d.next_evt[m] = nev;
   d.tround[m] = L.tround;
   d.tsize[m] = L.tsize;
@@ -1345,6 +1399,10 @@ __global__ void __launch_bounds__(256) k_member_tick(const Dev* __restrict__ dp,
   const Dev& d = *dp;  // global, not kernarg: taking its address must not copy ~1 KB into per-lane scratch
   __shared__ uint32_t wc[4][4];  // [wave][class] busy members
   __shared__ uint32_t list[256];
+  __shared__ uint4 cw[CWMAX];  // deferred copy-on-write snapshots of this block's members (cow)
+  __shared__ uint32_t cw_n;
+  if (threadIdx.x == 0) cw_n = 0;
+  if (threadIdx.x < CWMAX) cw[threadIdx.x].x = NEVER;  // no member until written (cow scans by member)
   const uint32_t m = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t cls = 0, drops = 0, evs = 0;
   const bool busy = m < d.hi && member_triage(d, m, k, cls, drops, evs);
@@ -1380,7 +1438,7 @@ __global__ void __launch_bounds__(256) k_member_tick(const Dev* __restrict__ dp,
   const uint32_t me = list[threadIdx.x];
   if (__ballot(me != NEVER)) {  // waves with no busy member skip to the end
     unsigned long long cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (me != NEVER) member_tick_body(d, me, k, cnt);
+    if (me != NEVER) member_tick_body(d, me, k, cnt, cw, &cw_n);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       unsigned long long v = cnt[i];
@@ -1391,6 +1449,29 @@ __global__ void __launch_bounds__(256) k_member_tick(const Dev* __restrict__ dp,
       }
       if (lane == 0 && v) atomicAdd(&d.ctr[i], v);
     }
+  }
+  // deferred copy-on-write: the block copies each snapshot's row (final for this tick: only its member writes it),
+  // then one lane undoes the member's logged writes since the snapshot opened, newest first
+  __syncthreads();
+  const uint32_t ncw = min(cw_n, CWMAX);
+  for (uint32_t q = 0; q < ncw; ++q) {
+    const uint4 e = cw[q];
+    if (e.x == NEVER) continue;  // made by its lane already (cow_now)
+    const uint32_t b = k & 1;
+    const size_t li = lidx(d, e.x);
+    const uint4* src4 = (const uint4*)(d.rowk + li * d.NS);
+    uint4* dst4 = (uint4*)(d.arena[b] + (size_t)e.y * d.NS);
+    for (uint32_t s = threadIdx.x; s < d.NS / 4; s += blockDim.x) dst4[s] = src4[s];
+    if (d.W > 1)
+      for (uint32_t w = threadIdx.x; w < d.MW; w += blockDim.x)
+        d.arena_dirty[b][(size_t)e.y * d.MW + w] = d.rdirty[li * d.MW + w];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t* dst = d.arena[b] + (size_t)e.y * d.NS;
+      const uint32_t* lg = d.ulog + li * ULOG * 2;
+      for (uint32_t j = e.w; j-- > e.z;) dst[lg[2 * j]] = lg[2 * j + 1];
+    }
+    __syncthreads();
   }
   if (!flag) return;
   if (!last_block_ticket(d.mdone, gridDim.x) || threadIdx.x != 0) return;
