@@ -708,8 +708,10 @@ __global__ void k_gossip_contacts(Dev d, uint32_t k) {
 
 // one counted send of gossip g from m to its round target t = T[m][s] (isInfected already checked): the receipt is
 // potential unless t holds g past this tick; a loss draw, then the first sender of (g, t) queues the delivery
+// potential: the caller already knows t does not hold g past this tick (k_gossip_send's candidates come from
+// WB & ~HB[t], and HB is exactly that test: nothing changes S between k_gossip_scan and the sends but PENDING bits)
 __device__ __forceinline__ void send_tail(const Dev& d, uint32_t g, uint32_t m, uint32_t s, uint32_t t, uint32_t k,
-                                          uint64_t gid, uint32_t* Sg, int ep) {
+                                          uint64_t gid, uint32_t* Sg, int ep, bool potential = false) {
   if (d.dbg_send) {
     uint32_t di = atomicAdd(d.dbg_send_n, 1u);
     if (di < d.dbg_send_cap) {
@@ -721,9 +723,11 @@ __device__ __forceinline__ void send_tail(const Dev& d, uint32_t g, uint32_t m, 
       r[4] = t;
     }
   }
-  uint32_t et = Sg[t];
-  // potential unless t holds g and does not sweep it in its own round this tick (a delivery would re-create it)
-  if (s_held(et) && !(s_ctick(et) < d.swthr[t])) return;
+  if (!potential) {
+    const uint32_t et = Sg[t];
+    // potential unless t holds g and does not sweep it in its own round this tick (a delivery would re-create it)
+    if (s_held(et) && !(s_ctick(et) < d.swthr[t])) return;
+  }
   if (lost_gossip_ep(d, ep, m, t, k, s, gid)) return;
   uint32_t old = atomicOr(&Sg[t], S_PENDING);
   if (!(old & S_PENDING)) {
@@ -921,7 +925,7 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
         if (j < total) {
           const uint32_t g = active[(size_t)(q0 + own) * 64 + nth_bit(word, r)];
           if (d.exp & 4) st[3]++;
-          send_tail(d, g, m, s, t, k, d.slot_gid[g], d.S + (size_t)g * d.N, ep);
+          send_tail(d, g, m, s, t, k, d.slot_gid[g], d.S + (size_t)g * d.N, ep, d.dbg_send == nullptr);
         }
       }
     }
