@@ -1433,12 +1433,14 @@ __global__ void __launch_bounds__(256) k_member_tick(const Dev* __restrict__ dp,
   const uint32_t start = all <= 256 ? aligned : dense;  // classes on wave boundaries when they fit, else packed
   for (uint32_t j = 0; j < w; ++j) before += wc[j][cls];
   const uint64_t bal = cls == 0 ? b0 : cls == 1 ? b1 : cls == 2 ? b2 : b3;
-  if (busy) list[start + before + __popcll(bal & ((1ull << lane) - 1ull))] = m;
+  if (busy) list[start + before + __popcll(bal & ((1ull << lane) - 1ull))] = m | (cls << 30);  // m < 2^30
   __syncthreads();
-  const uint32_t me = list[threadIdx.x];
+  const uint32_t ent = list[threadIdx.x], me = ent == NEVER ? NEVER : (ent & 0x3FFFFFFFu), mcls = ent >> 30;
+  // SWIM_EXP & 32 / 64 (timing experiments, wrong results): skip the bodies of class 0 / of classes 1-3
   if (__ballot(me != NEVER)) {  // waves with no busy member skip to the end
     unsigned long long cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (me != NEVER) member_tick_body(d, me, k, cnt, cw, &cw_n);
+    const bool skip = ((d.exp & 32) && mcls == 0) || ((d.exp & 64) && mcls != 0);
+    if (me != NEVER && !skip) member_tick_body(d, me, k, cnt, cw, &cw_n);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       unsigned long long v = cnt[i];
