@@ -770,31 +770,37 @@ __global__ void __launch_bounds__(256) k_gossip_scan(const Dev* __restrict__ dp,
       fg = d.firstGossip[m];
     }
     unsigned long long hb = 0, wb = 0;
-    for (uint32_t j = 0; j < gn; ++j) {
+    for (uint32_t j = 0; j < gn; ++j) {  // every lane of the wave runs the same slot g (its ballot below)
       const uint32_t g = active[q * 64 + j];
       const uint32_t e = d.S[(size_t)g * d.N + m];
-      if (!s_held(e)) continue;
-      const uint32_t c = s_ctick(e);
-      if (!(c < thr)) hb |= 1ull << j;
-      if (!rnd) continue;
-      const uint32_t infP = (fg == NEVER || c <= fg) ? 0u : (c - fg + d.gossip_t - 1) / d.gossip_t;  // rounds_before
-      if (infP + sp >= per) wb |= 1ull << j;  // selectGossipsToSend window (:246)
-      if (per > infP + sweep_after(sp)) {     // sweepGossips (:283-308)
+      bool sweep = false;
+      if (s_held(e)) {
+        const uint32_t c = s_ctick(e);
+        if (!(c < thr)) hb |= 1ull << j;
+        if (rnd) {
+          const uint32_t infP = (fg == NEVER || c <= fg) ? 0u : (c - fg + d.gossip_t - 1) / d.gossip_t;  // rounds_before
+          if (infP + sp >= per) wb |= 1ull << j;  // selectGossipsToSend window (:246)
+          sweep = per > infP + sweep_after(sp);   // sweepGossips (:283-308)
+        }
+      }
+      if (sweep) {
         atomicOr(&d.S[(size_t)g * d.N + m], S_SWEPT);
         if (d.XW > 1)
           atomicSub(&d.held_delta[m], 1);
         else
           atomicSub(&d.held[m], 1u);
-        atomicSub(&d.slot_holders[g], 1);
         on_sweep(d, g, m, k);
         if (d.W > 1) {  // applied on the other shards from exchange B
-          uint32_t i = atomicAdd(&d.xn[2], 1u);
+          uint32_t i = wave_append(&d.xn[2]);
           if (i < d.SWCAP)
             d.sw_rec[i] = ((uint64_t)g << 32) | m;
           else
             atomicOr(d.err, E_XCAP);
         }
       }
+      // the slot's holder count, once per wave (64 lanes of one slot would serialise on its address)
+      const unsigned long long sm = __ballot(sweep);
+      if (sm && __lane_id() == (uint32_t)(__ffsll((long long)sm) - 1)) atomicSub(&d.slot_holders[g], (int)__popcll(sm));
     }
     d.HBq[(size_t)q * d.N + m] = hb;  // group-major here (coalesced); k_mask_transpose makes the member-major rows
     d.WBq[(size_t)q * d.N + m] = wb;
@@ -1018,44 +1024,66 @@ __global__ void k_stamp_dead(Dev d, uint32_t k) {
   }
 }
 
-// first receipts (onGossipReq :176-180): create the holder state at tick k + lat and queue the record for P4
+// first receipts (onGossipReq :176-180): create the holder state at tick k + lat and queue the record for P4.
+// Deliveries come in runs of one target (a send-kernel wave appends one (sender, target) pair's receipts together), so
+// the target's counters are added once per run of equal targets in the wave instead of once per lane (one address
+// per wave serialised at L2). The loop is wave-uniform so that every lane reaches the run reduction.
 __global__ void k_gossip_apply(Dev d, uint32_t k) {
-  uint32_t n = *d.deliv_n < d.DCAP ? *d.deliv_n : d.DCAP;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    uint64_t v = d.deliv[i];
-    uint32_t g = (uint32_t)(v >> 32), t = (uint32_t)v;
-    uint32_t* p = d.S + (size_t)g * d.N + t;
-    uint32_t e = *p & ~S_PENDING;
-    if (s_held(e)) {
-      *p = e;
-      continue;
+  const uint32_t n = *d.deliv_n < d.DCAP ? *d.deliv_n : d.DCAP;
+  const uint32_t lane = __lane_id(), stride = gridDim.x * blockDim.x;
+  for (uint32_t i0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0 < n; i0 += stride) {
+    const uint32_t i = i0 + lane;
+    const bool act = i < n;
+    uint32_t g = 0, t = NEVER, created = 0, dropped = 0;
+    if (act) {
+      const uint64_t v = d.deliv[i];
+      g = (uint32_t)(v >> 32);
+      t = (uint32_t)v;
+      uint32_t* p = d.S + (size_t)g * d.N + t;
+      const uint32_t e = *p & ~S_PENDING;
+      if (s_held(e)) {
+        *p = e;
+      } else {
+        if (s_ever(e)) hist_push(d, d.slot_gid[g], t, s_ctick(e));  // rebirth after a sweep (:176-180)
+        *p = ((k + d.lat + 1u) & S_TICK_MASK) | (s_ever(e) ? S_REBORN : 0u);
+        created = 1;
+        atomicAdd(&d.slot_holders[g], 1);
+        if (t >= d.lo && t < d.hi) {  // else P4 of another shard's member
+          if (d.fastp4 && d.slot_subj[g] == USER_SUBJ) {  // RUMOR mode: the GOSSIP event of P4 (k + lat), hashed now
+            const uint64_t gid = d.slot_gid[g], key = d.slot_key[g];
+            const uint64_t ev = ((uint64_t)(k + d.lat) << 32) | (3ull << 30) | (uint32_t)(gid >> 32);
+            const uint64_t meta = ((uint64_t)(uint32_t)key << 32) | (key >> 32);  // (oldMeta, newMeta) = payload (lo, hi)
+            atomicAdd(&d.evp_hash[t], (unsigned long long)hpair(hpair(ev, meta), (uint32_t)gid));
+            atomicAdd(&d.evp_n[t], 1u);
+          } else if (!receipt_matters(d, t, g, k + d.lat)) {  // counted as a record compare in P4, nothing else
+            dropped = 1;
+          } else {
+            uint32_t ri = wave_append(d.rc_n);
+            if (ri < d.RCAP)
+              d.rc_raw[ri] = ((uint64_t)t << 32) | g;
+            else
+              atomicOr(d.err, E_RECEIPTS);
+          }
+        }
+      }
     }
-    if (s_ever(e)) hist_push(d, d.slot_gid[g], t, s_ctick(e));  // rebirth after a sweep (:176-180)
-    uint32_t ne = ((k + d.lat + 1u) & S_TICK_MASK) | (s_ever(e) ? S_REBORN : 0u);
-    *p = ne;
-    if (d.XW > 1)
-      atomicAdd(&d.held_delta[t], 1);
-    else
-      atomicAdd(&d.held[t], 1u);
-    atomicAdd(&d.slot_holders[g], 1);
-    if (t < d.lo || t >= d.hi) continue;  // P4 of another shard's member
-    if (d.fastp4 && d.slot_subj[g] == USER_SUBJ) {  // RUMOR mode: the GOSSIP event of P4 (k + lat), hashed now
-      const uint64_t gid = d.slot_gid[g], key = d.slot_key[g];
-      const uint64_t ev = ((uint64_t)(k + d.lat) << 32) | (3ull << 30) | (uint32_t)(gid >> 32);
-      const uint64_t meta = ((uint64_t)(uint32_t)key << 32) | (key >> 32);  // (oldMeta, newMeta) = payload (lo, hi)
-      atomicAdd(&d.evp_hash[t], (unsigned long long)hpair(hpair(ev, meta), (uint32_t)gid));
-      atomicAdd(&d.evp_n[t], 1u);
-      continue;
+    // runs of equal targets among the wave's lanes (lanes past n carry NEVER and nothing)
+    const uint32_t tp = __shfl_up(t, 1);
+    const unsigned long long heads = __ballot(lane == 0 || tp != t);
+    const unsigned long long cm = __ballot(created != 0), dm = __ballot(dropped != 0);
+    if (act && ((heads >> lane) & 1ull)) {
+      const unsigned long long above = heads & ~((2ull << lane) - 1ull);  // heads after this lane (lane < 63)
+      const uint32_t end = lane == 63 || !above ? 64u : (uint32_t)(__ffsll((long long)above) - 1);
+      const unsigned long long run = (end == 64 ? ~0ull : ((1ull << end) - 1ull)) & ~((1ull << lane) - 1ull);
+      const uint32_t nc = (uint32_t)__popcll(cm & run), nd = (uint32_t)__popcll(dm & run);
+      if (nc) {
+        if (d.XW > 1)
+          atomicAdd(&d.held_delta[t], (int)nc);
+        else
+          atomicAdd(&d.held[t], nc);
+      }
+      if (nd) atomicAdd(&d.rc_ndrop[t], nd);
     }
-    if (!receipt_matters(d, t, g, k + d.lat)) {  // counted as a record compare in P4, nothing else
-      atomicAdd(&d.rc_ndrop[t], 1u);
-      continue;
-    }
-    uint32_t ri = wave_append(d.rc_n);
-    if (ri < d.RCAP)
-      d.rc_raw[ri] = ((uint64_t)t << 32) | g;
-    else
-      atomicOr(d.err, E_RECEIPTS);
   }
 }
 
