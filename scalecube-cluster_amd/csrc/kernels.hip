@@ -872,15 +872,21 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
   const int ep = epoch_at(d, k);
   unsigned long long sends = 0;
   uint32_t st[4] = {0, 0, 0, 0};  // SWIM_EXP & 4: items with window bits, contact-loop bits, replays, first-receipt candidates
-  for (uint32_t w = blockIdx.x * 4 + wave; w < nr * d.F; w += gridDim.x * 4) {  // wave-uniform item
-    const uint32_t ri = w / d.F, s = w % d.F;
+  // wave-uniform work unit = (round member, target slot, chunk of 64 slot groups): a pair with many gossips in its
+  // window is spread over several waves instead of holding one wave for all its chunks (the kernel waits for the
+  // longest wave)
+  const uint32_t nch = (ngroups + 63) / 64;
+  const uint64_t units = (uint64_t)nr * d.F * nch;
+  for (uint64_t w = blockIdx.x * 4 + wave; w < units; w += gridDim.x * 4) {
+    const uint32_t item = (uint32_t)(w / nch), ch = (uint32_t)(w % nch);
+    const uint32_t ri = item / d.F, s = item % d.F;
     const uint32_t m = d.rlist[ri];
     if (s >= d.tcnt[m]) continue;
     const size_t ms = (size_t)m * d.F + s;
     const uint32_t t = d.T[ms], ci = d.cin[ms];
     const unsigned long long* wrow = d.WB + (size_t)m * d.QW;
     const unsigned long long* hrow = d.HB + (size_t)t * d.QW;
-    for (uint32_t q0 = 0; q0 < ngroups; q0 += 64) {
+    for (uint32_t q0 = ch * 64; q0 < ngroups && q0 < ch * 64 + 64; q0 += 64) {  // one chunk
       const uint32_t q = q0 + lane;
       const unsigned long long wb = q < ngroups ? wrow[q] : 0ull;
       if (__ballot(wb != 0ull) == 0ull) continue;
