@@ -354,7 +354,7 @@ int build(swim_handle* h) {
   A(d.rc_slot, d.RCAP) A(d.rc_ndrop, N) A(d.dead_rx, N) A(d.leaving, N) A(d.rc_key, d.RCAP) A(d.rc_slot2, d.RCAP) A(d.rc_key2, d.RCAP) A(d.active, d.SLOTS) A(d.nactive, 1) A(d.hist, (uint64_t)d.HCAP * HREC)
   A(d.msgs[0], d.MSGCAP) A(d.msgs[1], d.MSGCAP) A(d.nmsg, 2) A(d.arena[0], (uint64_t)d.ARENA_ROWS * d.NS)
   A(d.arena[1], (uint64_t)d.ARENA_ROWS * d.NS) A(d.arena_used, 2)
-  A(d.m_next, 2ull * d.MSGCAP) A(d.m_head, 2 * N) A(d.deaths, 2ull * DEATHCAP) A(d.deaths_n, 2) A(d.next_evt, N) A(d.mdone, 1) A(d.trk, NL * TRK) A(d.ulog, NL * ULOG * 2) A(d.pending_inc, N) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
+  A(d.m_next, 2ull * d.MSGCAP) A(d.m_head, 2 * N) A(d.deaths, 2ull * DEATHCAP) A(d.deaths_n, 2) A(d.next_evt, N) A(d.mdone, 1) A(d.trk, NL * TRK) A(d.ulog, NL * ULOG * 2) A(d.spq, NL * SPQ * 8) A(d.pending_inc, N) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
   A(d.pool, d.POOLCAP) A(d.pool_used, 1)
   A(d.ev, (uint64_t)d.EVCAP * 8) A(d.ev_n, 1) A(d.ctr, C_NCTR) A(d.err, 8)
   if (d.fastp4) {
@@ -1014,11 +1014,17 @@ int swim_step(swim_handle* h, uint32_t n) {
     h->tick++;
   }
   int rc = check_err(h);
-  if (rc == SWIM_OK && (d.exp & 16)) {  // timing experiments: member-kernel shader cycles per phase since the last step
+  if (rc == SWIM_OK && (d.exp & (16 | 128))) {  // timing experiments: member-kernel shader cycles per phase since the last step (16: sum over members, 128: max)
     unsigned long long c[5];
     HIPCK(hipMemcpy(c, d.ctr + 8, sizeof(c), hipMemcpyDeviceToHost));
     HIPCK(hipMemset(d.ctr + 8, 0, sizeof(c)));
     fprintf(stderr, "exp: member cycles P0+P1 %llu P2+P3 %llu P4 %llu P5 %llu P6 %llu\n", c[0], c[1], c[2], c[3], c[4]);
+    if (d.exp & 128) {
+      unsigned long long w[2];
+      HIPCK(hipMemcpy(w, d.ctr + 14, sizeof(w), hipMemcpyDeviceToHost));
+      HIPCK(hipMemset(d.ctr + 14, 0, sizeof(w)));
+      fprintf(stderr, "exp: SYNC full walks %llu, largest candidate count %llu\n", w[0], w[1]);
+    }
   }
   if (rc == SWIM_OK && (d.exp & 4)) {  // timing experiments: gossip-send work counters since the last step
     unsigned long long c[5];

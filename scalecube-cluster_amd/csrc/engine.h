@@ -24,6 +24,7 @@ constexpr uint32_t TRK = 16;   // subjects written in one tick's P1 that are re-
 // deferred copy-on-write (member.hip cow): row writes logged per member and tick while a snapshot is open, open
 // snapshots per member, deferred snapshots per k_member_tick block
 constexpr uint32_t ULOG = 64, CREQ = 4, CWMAX = 32;
+constexpr uint32_t SPQ = 32;  // gossips a member creates in one tick before their slots are taken together
 
 // S entry flags (gossip slot x member)
 constexpr uint32_t S_PENDING = 1u << 29, S_SWEPT = 1u << 30, S_REBORN = 1u << 31;
@@ -176,6 +177,7 @@ struct Dev {
   uint32_t* mdone;  // finished k_member_tick blocks this tick (the last one runs the end-of-tick resets)
   uint32_t* trk;    // [NL][TRK] per receiver: subjects its row changed earlier in this tick's P1 (member.hip)
   uint32_t* ulog;   // [NL][ULOG][2] per member: (subject, old key) of its row writes this tick after a SYNC send
+  uint32_t* spq;    // [NL][SPQ][8] per member: gossips created this tick, waiting for their slots (member.hip)
   uint32_t* chunk_meta;                      // [MSGCAP][NCHUNK][2] (pool offset, count)
   uint64_t* pool;                            // candidate (subject << 34 | key)
   uint32_t* pool_used;

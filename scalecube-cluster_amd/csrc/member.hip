@@ -40,6 +40,8 @@ struct ML {
   uint32_t* cw_n;  // LDS counter of cw
   uint32_t* ulog;  // this member's log: (subject, key before the write) per row write while a snapshot is open
   uint32_t ncreq, nlog;  // open snapshots (their cw entries carry this member's id), logged writes
+  uint32_t* spq;  // gossips created this tick that wait for their slots (flush_spreads): [SPQ][8] gid, subj, key
+  uint32_t nsp;
 
 };
 
@@ -248,14 +250,9 @@ __device__ __forceinline__ void emit_event(ML& L, uint32_t type, uint32_t subj, 
   on_member_event(L, type, subj);
 }
 
-// createAndPutGossip (GossipProtocolImpl.java:163-169): a new global gossip slot held by member m since tick k
-__device__ __forceinline__ bool new_slot(const Dev& d, uint32_t m, uint32_t k, uint64_t gid, uint32_t subj, uint64_t key) {
-  int pos = atomicSub(d.free_top, 1) - 1;
-  if (pos < 0) {
-    set_err(d, E_SLOTS);
-    return false;
-  }
-  uint32_t g = d.free_list[pos];
+// createAndPutGossip (GossipProtocolImpl.java:163-169): gossip slot g becomes a new gossip held by member m since tick k
+__device__ __forceinline__ void slot_init(const Dev& d, uint32_t g, uint32_t m, uint32_t k, uint64_t gid, uint32_t subj,
+                                          uint64_t key) {
   d.slot_gid[g] = gid;
   d.slot_subj[g] = subj;
   d.slot_ctick[g] = k;
@@ -267,7 +264,7 @@ __device__ __forceinline__ bool new_slot(const Dev& d, uint32_t m, uint32_t k, u
     uint32_t i = atomicAdd(&d.xn[0], 1u);
     if (i >= d.NSCAP) {
       set_err(d, E_XCAP);
-      return true;
+      return;
     }
     uint32_t* r = d.ns_rec + (size_t)i * NSW;
     r[0] = g;
@@ -279,15 +276,49 @@ __device__ __forceinline__ bool new_slot(const Dev& d, uint32_t m, uint32_t k, u
     r[6] = (uint32_t)(key >> 32);
     r[7] = m;
   }
+}
+
+// one slot off the free stack (k_user_gossips; members batch theirs, flush_spreads)
+__device__ __forceinline__ bool new_slot(const Dev& d, uint32_t m, uint32_t k, uint64_t gid, uint32_t subj, uint64_t key) {
+  int pos = atomicSub(d.free_top, 1) - 1;
+  if (pos < 0) {
+    set_err(d, E_SLOTS);
+    return false;
+  }
+  slot_init(d, d.free_list[pos], m, k, gid, subj, key);
   return true;
 }
 
-// GossipProtocolImpl.spread -> createAndPutGossip (:124-128,163-169): a membership gossip held by this member
+// the member's queued gossips of this tick get their slots with one atomic on the free stack: a member that re-spreads
+// hundreds of SYNC records in one tick (C2) would otherwise wait for one round trip on that hot word per gossip
+__device__ __forceinline__ void flush_spreads(ML& L) {
+  const uint32_t n = L.nsp;
+  if (n == 0) return;
+  L.nsp = 0;
+  const Dev& d = *L.d;
+  const int base = atomicSub(d.free_top, (int)n) - (int)n;
+  for (uint32_t i = 0; i < n; ++i) {
+    const int pos = base + (int)i;
+    if (pos < 0) {
+      set_err(d, E_SLOTS);
+      continue;
+    }
+    const uint4 e0 = *(const uint4*)(L.spq + 8 * i), e1 = *(const uint4*)(L.spq + 8 * i + 4);
+    slot_init(d, d.free_list[pos], L.m, L.k, ((uint64_t)e0.y << 32) | e0.x, e0.z, ((uint64_t)e1.x << 32) | e0.w);
+    L.c[C_GCREATED]++;
+  }
+}
+
+// GossipProtocolImpl.spread -> createAndPutGossip (:124-128,163-169): a membership gossip held by this member; its
+// slot is taken at the end of the member's tick (flush_spreads: slot ids are not observable)
 __device__ __forceinline__ void spread(ML& L, uint32_t subj, uint32_t st, uint32_t inc) {
   uint64_t gid = ((uint64_t)L.m << 32) | L.gCounter++;
   if (slot_mine(*L.d, gid)) {  // slot sharding: only the owning shard stores it; every shard counts it as held
-    if (!new_slot(*L.d, L.m, L.k, gid, subj, rec_key(st, inc))) return;
-    L.c[C_GCREATED]++;
+    if (L.nsp == SPQ) flush_spreads(L);
+    const uint64_t key = rec_key(st, inc);
+    *(uint4*)(L.spq + 8 * L.nsp) = make_uint4((uint32_t)gid, (uint32_t)(gid >> 32), subj, (uint32_t)key);
+    *(uint4*)(L.spq + 8 * L.nsp + 4) = make_uint4((uint32_t)(key >> 32), 0u, 0u, 0u);
+    L.nsp++;
   }
   L.held++;
 }
@@ -721,6 +752,10 @@ __device__ __forceinline__ void merge_payload(ML& L, uint32_t mi, uint32_t reaso
   L.c[C_SYNCMERGE]++;
   const uint32_t nt = L.ntrk;
   const bool full = nt > TRK;  // rare: many subjects changed earlier in this tick; exact full walk
+  if (d.exp & 128) {  // timing experiments: full walks, largest candidate count
+    if (full) atomicAdd(&d.ctr[14], 1ull);
+    atomicMax(&d.ctr[15], (unsigned long long)mm.ncand);
+  }
   if (!full && mm.ncand == 0 && nt == 0) return;  // steady state: nothing differs, skip the chunk walk
   if (!full)
     for (uint32_t i = 1; i < nt; ++i)  // the tracked subjects in ascending order (insertion sort, at most TRK)
@@ -899,13 +934,19 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   L.ulog = d.ulog + li * ULOG * 2;
   L.ncreq = 0;
   L.nlog = 0;
+  L.spq = d.spq + li * SPQ * 8;
+  L.nsp = 0;
   // SWIM_EXP & 16 (timing experiment): shader cycles per phase summed over members, ctr[8..12]
-  const bool prof = (d.exp & 16) != 0;
+  // SWIM_EXP & 128: the largest per-member cycles of each phase instead (which phase makes the longest lane)
+  const bool prof = (d.exp & (16 | 128)) != 0;
   unsigned long long tp = prof ? clock64() : 0;
   auto lap = [&](int slot) {
     if (!prof) return;
     const unsigned long long t = clock64();
-    atomicAdd(&d.ctr[8 + slot], t - tp);
+    if (d.exp & 16)
+      atomicAdd(&d.ctr[8 + slot], t - tp);
+    else
+      atomicMax(&d.ctr[8 + slot], t - tp);
     tp = t;
   };
 
@@ -1350,6 +1391,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   }
 
   lap(4);  // P6
+  flush_spreads(L);
   uint32_t nev = NEVER;
   for (uint32_t q = 0; q < L.npath; ++q) nev = min(nev, L.paths[(size_t)q * 5 + 2]);
   for (uint32_t q = 0; q < L.nsub; ++q) nev = min(nev, L.subs[(size_t)q * 4 + 3]);
