@@ -769,9 +769,22 @@ __device__ __forceinline__ void merge_payload(ML& L, uint32_t mi, uint32_t reaso
   // and the tracked subjects merged in subject order (a tracked candidate takes the pool's record).
   uint32_t ti = 0, c = 0, e = 0, n = 0, off = 0, s = 0;
   bool pool = !full && mm.ncand != 0;
+  // the full walk skips runs where the payload equals the live row, 4 subjects per 16-B compare, when the payload is
+  // an arena row (its snapshot or pinned copy); a lane walking N subjects one by one held C2's member kernel
+  const uint32_t* prow = nullptr;
+  if (full && !(mm.payload != NEVER && (mm.payload & PAY_RX))) {
+    const uint32_t r = mm.payload == NEVER ? mm.pin : mm.payload;
+    if (r != NEVER) prow = d.arena[b] + (size_t)r * d.NS;
+  }
   for (;;) {
     uint32_t subj, k1;
     if (full) {
+      if (prow)
+        while (s + 4 <= L.N && (s & 3u) == 0u) {
+          const uint4 p4 = *(const uint4*)(prow + s), r4 = *(const uint4*)(L.rk + s);
+          if (p4.x != r4.x || p4.y != r4.y || p4.z != r4.z || p4.w != r4.w) break;
+          s += 4;
+        }
       if (s >= L.N) break;
       subj = s;
       k1 = payload_key_at(d, mm, b, s);
