@@ -779,6 +779,19 @@ __device__ __forceinline__ void merge_payload(ML& L, uint32_t mi, uint32_t reaso
   for (;;) {
     uint32_t subj, k1;
     if (full) {
+      if (prow) {
+        // 16 subjects per step with all eight loads in flight, then 4 at a time near the next difference
+        while (s + 16 <= L.N && (s & 3u) == 0u) {
+          uint32_t diff = 0;
+#pragma unroll
+          for (uint32_t q = 0; q < 4; ++q) {
+            const uint4 p4 = *(const uint4*)(prow + s + 4 * q), r4 = *(const uint4*)(L.rk + s + 4 * q);
+            diff |= (p4.x ^ r4.x) | (p4.y ^ r4.y) | (p4.z ^ r4.z) | (p4.w ^ r4.w);
+          }
+          if (diff) break;
+          s += 16;
+        }
+      }
       if (prow)
         while (s + 4 <= L.N && (s & 3u) == 0u) {
           const uint4 p4 = *(const uint4*)(prow + s), r4 = *(const uint4*)(L.rk + s);
