@@ -758,31 +758,43 @@ __global__ void __launch_bounds__(256) k_gossip_scan(const Dev* __restrict__ dp,
   const uint32_t na = *nactive, ngroups = (na + 63) / 64;
   const uint32_t mchunks = (d.N + 255) / 256;
   for (uint32_t w = blockIdx.x; w < ngroups * mchunks; w += gridDim.x) {
-    const uint32_t q = w / mchunks, m = (w % mchunks) * 256 + threadIdx.x;
-    if (m >= d.N) continue;
-    const uint32_t gn = min(64u, na - q * 64);
+    const uint32_t q = w / mchunks, m0 = (w % mchunks) * 256 + threadIdx.x;
+    const bool act = m0 < d.N;  // lanes past N take part in the wave OR below with nothing to sweep
+    const uint32_t m = act ? m0 : d.N - 1;
+    const uint32_t gn = act ? min(64u, na - q * 64) : 0u;
     const uint32_t thr = d.swthr[m];
-    const bool rnd = d.tround[m] && m >= d.lo && m < d.hi;  // this shard's round members send and sweep
+    const bool rnd = act && d.tround[m] && m >= d.lo && m < d.hi;  // this shard's round members send and sweep
     uint32_t per = 0, sp = 0, fg = NEVER;
     if (rnd) {
       per = d.tperiod[m];
       sp = d.tspread[m];
       fg = d.firstGossip[m];
     }
-    unsigned long long hb = 0, wb = 0;
-    for (uint32_t j = 0; j < gn; ++j) {  // every lane of the wave runs the same slot g (its ballot below)
-      const uint32_t g = active[q * 64 + j];
-      const uint32_t e = d.S[(size_t)g * d.N + m];
-      bool sweep = false;
+    // pass 1 has no side effects, so the 64 holder-word loads pipeline; the sweeps (rare) run after it, per slot
+    // that any lane of the wave sweeps
+    unsigned long long hb = 0, wb = 0, swm = 0;
+#pragma unroll 8
+    for (uint32_t j = 0; j < gn; ++j) {
+      const uint32_t e = d.S[(size_t)active[q * 64 + j] * d.N + m];
       if (s_held(e)) {
         const uint32_t c = s_ctick(e);
         if (!(c < thr)) hb |= 1ull << j;
         if (rnd) {
           const uint32_t infP = (fg == NEVER || c <= fg) ? 0u : (c - fg + d.gossip_t - 1) / d.gossip_t;  // rounds_before
-          if (infP + sp >= per) wb |= 1ull << j;  // selectGossipsToSend window (:246)
-          sweep = per > infP + sweep_after(sp);   // sweepGossips (:283-308)
+          if (infP + sp >= per) wb |= 1ull << j;               // selectGossipsToSend window (:246)
+          if (per > infP + sweep_after(sp)) swm |= 1ull << j;  // sweepGossips (:283-308)
         }
       }
+    }
+    unsigned long long any = swm;  // the slots any lane of this wave sweeps (wave-uniform loop below)
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+      const uint32_t lo = __shfl_xor((uint32_t)any, o), hi = __shfl_xor((uint32_t)(any >> 32), o);
+      any |= ((unsigned long long)hi << 32) | lo;
+    }
+    for (; any; any &= any - 1) {
+      const uint32_t j = (uint32_t)(__ffsll((long long)any) - 1), g = active[q * 64 + j];
+      const bool sweep = (swm >> j) & 1ull;
       if (sweep) {
         atomicOr(&d.S[(size_t)g * d.N + m], S_SWEPT);
         if (d.XW > 1)
@@ -802,6 +814,7 @@ __global__ void __launch_bounds__(256) k_gossip_scan(const Dev* __restrict__ dp,
       const unsigned long long sm = __ballot(sweep);
       if (sm && __lane_id() == (uint32_t)(__ffsll((long long)sm) - 1)) atomicSub(&d.slot_holders[g], (int)__popcll(sm));
     }
+    if (!act) continue;
     d.HBq[(size_t)q * d.N + m] = hb;  // group-major here (coalesced); k_mask_transpose makes the member-major rows
     d.WBq[(size_t)q * d.N + m] = wb;
   }
