@@ -190,21 +190,39 @@ __device__ __forceinline__ bool send_sync(ML& L, uint32_t kind, uint32_t dst, ui
   return true;
 }
 
+// ArrayList.remove(Object) on one lane: find subj, then shift the tail down by one in blocks of 8 (the loads of a
+// block are independent of the stores before it, so they are in flight together instead of one load per element)
+__device__ __forceinline__ bool list_remove(uint32_t* a, uint32_t len, uint32_t subj) {
+  uint32_t i = 0;
+  for (; i + 8 <= len; i += 8) {
+    uint32_t v[8];
+#pragma unroll
+    for (uint32_t t = 0; t < 8; ++t) v[t] = a[i + t];
+    bool hit = false;
+#pragma unroll
+    for (uint32_t t = 0; t < 8; ++t) hit |= v[t] == subj;
+    if (hit) break;
+  }
+  for (; i < len && a[i] != subj; ++i) {
+  }
+  if (i >= len) return false;
+  uint32_t j = i + 1;
+  for (; j + 8 <= len; j += 8) {
+    uint32_t v[8];
+#pragma unroll
+    for (uint32_t t = 0; t < 8; ++t) v[t] = a[j + t];
+#pragma unroll
+    for (uint32_t t = 0; t < 8; ++t) a[j + t - 1] = v[t];
+  }
+  for (; j < len; ++j) a[j - 1] = a[j];
+  return true;
+}
+
 __device__ __forceinline__ void on_member_event(ML& L, uint32_t type, uint32_t subj) {
   const Dev& d = *L.d;
   if (type == 1) {  // REMOVED: FailureDetectorImpl.onMemberEvent (:321-325), GossipProtocolImpl (:187-189)
-    for (uint32_t i = 0; i < L.fdLen; ++i)
-      if (L.fdl[i] == subj) {
-        for (uint32_t j = i + 1; j < L.fdLen; ++j) L.fdl[j - 1] = L.fdl[j];
-        L.fdLen--;
-        break;
-      }
-    for (uint32_t i = 0; i < L.gLen; ++i)
-      if (L.gl[i] == subj) {
-        for (uint32_t j = i + 1; j < L.gLen; ++j) L.gl[j - 1] = L.gl[j];
-        L.gLen--;
-        break;
-      }
+    if (list_remove(L.fdl, L.fdLen, subj)) L.fdLen--;
+    if (list_remove(L.gl, L.gLen, subj)) L.gLen--;
   } else if (type == 0) {  // ADDED: insert at nextInt(size) (:326-331); append (:190-192)
     if (L.fdLen >= d.LCAP || L.gLen >= d.LCAP) {
       set_err(d, E_LIST);
