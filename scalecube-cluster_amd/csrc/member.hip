@@ -229,7 +229,15 @@ __device__ __forceinline__ void on_member_event(ML& L, uint32_t type, uint32_t s
       return;
     }
     uint32_t idx = L.fdLen > 0 ? next_int(draw(L, S_FD_INSERT), L.fdLen) : 0;
-    for (uint32_t j = L.fdLen; j > idx; --j) L.fdl[j] = L.fdl[j - 1];
+    uint32_t j = L.fdLen;  // ArrayList.add(index, e): the tail moves up by one, in blocks of 8 from the top
+    for (; j >= idx + 8; j -= 8) {
+      uint32_t v[8];
+#pragma unroll
+      for (uint32_t t = 0; t < 8; ++t) v[t] = L.fdl[j - 8 + t];
+#pragma unroll
+      for (uint32_t t = 0; t < 8; ++t) L.fdl[j - 7 + t] = v[t];
+    }
+    for (; j > idx; --j) L.fdl[j] = L.fdl[j - 1];
     L.fdl[idx] = subj;
     L.fdLen++;
     L.gl[L.gLen++] = subj;
