@@ -91,7 +91,8 @@ typedef struct swim_config {
   uint32_t gossip_slot_cap;   /* concurrent gossip ids */
   uint32_t pending_fetch_cap; /* concurrent metadata fetches per member */
   uint32_t event_cap;         /* buffered event records */
-  uint32_t n_gpus;            /* 1 for now */
+  uint32_t n_gpus;            /* > 1: one handle row-sharded over n_gpus devices of this process (RCCL between them;
+                                 host exchange when the process sees fewer devices), DESIGN.md §6 */
   uint32_t device;            /* first HIP device */
   uint32_t list_slack;        /* FD / gossip list entries beyond N (duplicates after reordered ADDED / REMOVED) */
   uint32_t churn_per_period;  /* SWIM_MODE_RUMOR: churn events (one rumor each) drawn at the start of every FD period */

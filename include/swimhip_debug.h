@@ -1,0 +1,50 @@
+/*
+ * swimhip_debug.h — test surface of libswimhip (not part of the simulation API; the CPU oracle has no such paths).
+ *
+ * The engine keeps its hot per-tick state in fixed-capacity fast structures and falls back to an exact slow path
+ * when one is full. Those fallbacks must give the same bits as the fast path, so tests force them:
+ * the environment variable SWIM_CAPS, read by swim_create, lowers the capacities, e.g.
+ *   SWIM_CAPS="trk=1,ulog=2,creq=1,cwmax=1,cev=1,mq=1,sort=2"
+ *   trk    subjects tracked per receiver and tick for later SYNC payloads (more: whole-row walk),
+ *          MembershipProtocolImpl.syncMembership (:456-467) with several payloads in one tick
+ *   ulog   row writes logged after a SYNC send of the same tick (more: the lane copies its open snapshots),
+ *          prepareSyncDataMsg (:446-454) snapshot semantics
+ *   creq   copy-on-write snapshots open per member and tick (more: the lane copies them)
+ *   cwmax  deferred snapshots per k_member_tick block (more: the lane copies the row)
+ *   cev    cached contact events per (sender, target) pair (more: k_gossip_send_slow scans both round logs),
+ *          GossipProtocolImpl.selectGossipsToSend isInfected (:239-250)
+ *   mq     inbound SYNC messages of one tick sorted in registers (more: selection by list walks), onMessage (:320-331)
+ *   sort   first receipts of one member and tick sorted in LDS at once (more: sorted runs merged), P4 order
+ * With SWIM_CAPS (or SWIM_FALLBACKS=1) set, the handle counts how often each fallback fired.
+ */
+#ifndef SWIMHIP_DEBUG_H
+#define SWIMHIP_DEBUG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "swimhip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* indices into swim_debug_fallbacks' output */
+#define SWIM_FB_TRK_WALK 0u    /* whole-row SYNC walks (trk) */
+#define SWIM_FB_ULOG 1u        /* snapshot copies forced by a full undo log (ulog) */
+#define SWIM_FB_CREQ 2u        /* snapshot copies forced by too many open snapshots (creq) */
+#define SWIM_FB_CWMAX 3u       /* lane row copies, block list full (cwmax) */
+#define SWIM_FB_CEV_SLOW 4u    /* gossip sends replayed from a full log scan (cev) */
+#define SWIM_FB_REPLAY 5u      /* gossip sends replayed from the contact cache (pairs with a logged contact) */
+#define SWIM_FB_MQ 6u          /* receivers with more than mq inbound SYNC messages in one tick */
+#define SWIM_FB_SORT_MERGE 7u  /* receipt segments sorted as runs and merged (sort) */
+#define SWIM_FB_COUNT 8u
+
+/* counts of the fallbacks fired since create, n <= 16 entries (summed over shards); SWIM_EUNSUPPORTED when the
+ * handle was created without SWIM_CAPS / SWIM_FALLBACKS */
+int swim_debug_fallbacks(swim_handle* h, uint64_t* out, size_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -18,6 +18,7 @@
 #include "../../include/swimhip.h"
 #include "../../include/swimhip_shard.h"
 #include "../../include/swimhip_wire.h"
+#include "../../include/swimhip_debug.h"
 #include "engine.h"
 
 using namespace swim;
@@ -263,6 +264,37 @@ int build(swim_handle* h) {
   d.implicit = c.mode == SWIM_MODE_RUMOR && (c.n_members > 65536 || (c.flags & SWIM_FLAG_IMPLICIT_VIEWS)) ? 1u : 0u;
   d.fastp4 = c.mode == SWIM_MODE_RUMOR && !(c.flags & SWIM_FLAG_RECORD_EVENTS) ? 1u : 0u;
   d.exp = getenv("SWIM_EXP") ? (uint32_t)atoi(getenv("SWIM_EXP")) : 0u;  // timing experiments: wrong results
+  // fast-structure capacities (include/swimhip_debug.h): SWIM_CAPS="trk=1,ulog=2,creq=1,cwmax=1,cev=1,mq=1,sort=2"
+  // lowers them so that the exact fallbacks run; results stay bit-exact, only slower
+  d.trk_cap = TRK, d.ulog_cap = ULOG, d.creq_cap = CREQ, d.cwmax_cap = CWMAX, d.cev_cap = CEV, d.mq_cap = MQ;
+  d.sort_cap = SORT_MAX;
+  const char* caps = getenv("SWIM_CAPS");
+  if (caps) {
+    std::string s(caps);
+    size_t p = 0;
+    while (p < s.size()) {
+      size_t e = s.find(',', p);
+      if (e == std::string::npos) e = s.size();
+      const std::string kv = s.substr(p, e - p);
+      p = e + 1;
+      const size_t eq = kv.find('=');
+      if (eq == std::string::npos) continue;
+      const std::string k = kv.substr(0, eq);
+      const uint32_t v = (uint32_t)strtoul(kv.c_str() + eq + 1, nullptr, 0);
+      auto clampv = [&](uint32_t lo, uint32_t hi) { return std::max(lo, std::min(hi, v)); };
+      if (k == "trk") d.trk_cap = clampv(0, TRK);
+      else if (k == "ulog") d.ulog_cap = clampv(0, ULOG);
+      else if (k == "creq") d.creq_cap = clampv(1, CREQ);
+      else if (k == "cwmax") d.cwmax_cap = clampv(0, CWMAX);
+      else if (k == "cev") d.cev_cap = clampv(0, CEV);
+      else if (k == "mq") d.mq_cap = clampv(1, MQ);
+      else if (k == "sort") {
+        uint32_t r = 2;
+        while (r * 2 <= clampv(2, SORT_MAX)) r *= 2;  // a power of two (bitonic runs)
+        d.sort_cap = r;
+      }
+    }
+  }
   // seeds: LinkedHashSet of valid ids (MembershipProtocolImpl.java:160-166); self is skipped per member
   for (uint32_t i = 0; i < c.n_seeds; ++i) {
     uint32_t s = c.seeds[i];
@@ -282,12 +314,19 @@ int build(swim_handle* h) {
   d.LOGW = 8;
   while (d.LOGW < 4 * (maxSpread + 2)) d.LOGW <<= 1;  // rounds kept for the infectedFrom replay
   d.LOOKBACK = d.LOGW * d.gossip_t;
-  // incarnation history of reborn (gossip, member) pairs: storms in small clusters (C4's heal) rebirth a large
-  // share of the holder states; sized from the holder table, 2^20 .. 2^24 entries (88 B each)
+  // incarnation history of reborn (gossip, member) pairs (88 B per entry). 2^20 entries (92 MB) by default; a run
+  // that asks for a large slot table (a storm: C4's heal rebirths a large share of the holder states) gets one
+  // entry per 8 holder states, up to 2^24; SWIM_HIST_CAP overrides (a full table raises E_REBORN, info 1)
   {
-    const uint64_t slots_est = c.gossip_slot_cap ? c.gossip_slot_cap : 64 * N;
-    uint64_t want = slots_est * N / 8, hc = 1u << 20;
-    while (hc < want && hc < (1u << 24)) hc <<= 1;
+    uint64_t hc = 1u << 20;
+    if (c.gossip_slot_cap) {
+      const uint64_t want = (uint64_t)c.gossip_slot_cap * N / 8;
+      while (hc < want && hc < (1u << 24)) hc <<= 1;
+    }
+    if (const char* e = getenv("SWIM_HIST_CAP")) {
+      hc = 1024;
+      while (hc < strtoull(e, nullptr, 0) && hc < (1u << 26)) hc <<= 1;
+    }
     d.HCAP = (uint32_t)hc;
   }
   // default: 64 slots per member, at most 32 GB of holder table (C2's SYNC re-spread storm keeps ~10^5 gossips alive)
@@ -345,7 +384,7 @@ int build(swim_handle* h) {
   const uint64_t NV = d.implicit ? 1 : NL;  // implicit views: no table or list is stored
   A(d.rowk, NV * d.NS) A(d.rowa, NV * d.NS) A(d.fdl, NV * d.LCAP) A(d.gl, NV * d.LCAP)
   A(d.subs, NL * SUBCAP * 4) A(d.paths, NL * PATHCAP * 5) A(d.fetch, NL * d.FCAP * FREC) A(d.groups, NL * d.GRCAP * GREC)
-  A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.slow, d.SLOWCAP) A(d.slow_n, 1) A(d.rp, d.RPCAP) A(d.rp_n, 1) A(d.rlist, N) A(d.rn, 1) A(d.start_tick, N) A(d.jseed_n, N) A(d.jseeds, 16 * N) A(d.md_uidx, N) A(d.mcfg, 4 * N) A(d.md_ver, NL * MDU) A(d.churn_q, 2ull * d.churn) A(d.cin, N * d.F) A(d.swthr, N) A(d.HB, (uint64_t)d.QW * N) A(d.WB, (uint64_t)d.QW * N) A(d.HBq, (uint64_t)d.QW * N) A(d.WBq, (uint64_t)d.QW * N) A(d.cev, N * d.F * CEVW)
+  A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.slow, d.SLOWCAP) A(d.slow_n, 1) A(d.rp, d.RPCAP) A(d.rp_n, 1) A(d.rlist, N) A(d.rn, 1) A(d.start_tick, N) A(d.jseed_n, N) A(d.jseeds, 16 * N) A(d.md_uidx, N) A(d.mcfg, 4 * N) A(d.md_ver, NL * MDU) A(d.churn_q, 2ull * d.churn) A(d.ucnt, N) A(d.cin, N * d.F) A(d.swthr, N) A(d.HB, (uint64_t)d.QW * N) A(d.WB, (uint64_t)d.QW * N) A(d.HBq, (uint64_t)d.QW * N) A(d.WBq, (uint64_t)d.QW * N) A(d.cev, N * d.F * CEVW)
   A(d.log_tick, N * d.LOGW) A(d.log_spread, N * d.LOGW) A(d.log_cnt, N * d.LOGW) A(d.log_tg, N * d.LOGW * d.F)
   A(d.log_pos, N) A(d.spchg, N)
   A(d.slot_gid, d.SLOTS) A(d.slot_subj, d.SLOTS) A(d.slot_ctick, d.SLOTS) A(d.slot_key, d.SLOTS) A(d.slot_holders, d.SLOTS)
@@ -369,6 +408,10 @@ int build(swim_handle* h) {
       h->hsend.resize(4ull * N * d.XW);
       h->hrecv.resize(4ull * N * d.XW);
     }
+  }
+  if (getenv("SWIM_CAPS") || getenv("SWIM_FALLBACKS")) {  // count the capacity fallbacks (swim_debug_fallbacks)
+    A(d.fb, FB_N)
+    HIPCK(hipMemsetAsync(d.fb, 0, 8 * FB_N, h->stream));
   }
   if (getenv("SWIM_SEND_LOG")) {  // debugging aid: every counted gossip send
     d.dbg_send_cap = (uint32_t)atoi(getenv("SWIM_SEND_LOG"));
@@ -418,6 +461,7 @@ int build(swim_handle* h) {
   HIPCK(hipMemsetAsync(d.nmsg, 0, 8, h->stream));
   HIPCK(hipMemsetAsync(d.arena_used, 0, 8, h->stream));
   HIPCK(hipMemsetAsync(d.tcnt, 0, N * 4, h->stream));
+  HIPCK(hipMemsetAsync(d.ucnt, 0, N * 4, h->stream));
   HIPCK(hipMemsetAsync(d.pool_used, 0, 4, h->stream));
   HIPCK(hipMemsetAsync(d.deaths_n, 0, 8, h->stream));
   HIPCK(hipMemsetAsync(d.mdone, 0, 4, h->stream));
@@ -1175,6 +1219,10 @@ int swim_set_member_config(swim_handle* h, uint32_t m, const swim_member_config*
     // the PRECONVERGED schedule phase under the member's own interval (k_init_members, SEMANTICS.md §3)
     const uint32_t np = 1u + philox(m, 1, 0, 0, d.seed_lo ^ SALT_INIT, d.seed_hi).x % pt;
     HIPCK(h2d(h->stream, d.nextPing + m, &np, 4));
+  } else if (h->cfg.init_mode == SWIM_INIT_COLD_JOIN && !dormant) {
+    // an initial member starts at tick 0 (start0): its first ping follows its own pingInterval (a dormant member's
+    // is set by k_join at its start tick)
+    HIPCK(h2d(h->stream, d.nextPing + m, &pt, 4));
   }
   if (!d.permember) {  // the kernels read mcfg from now on (Dev is passed by value and through d.self)
     d.permember = 1;
@@ -1383,6 +1431,9 @@ int swim_drain_events(swim_handle* h, swim_event* out, size_t cap, size_t* n_out
   if (!h || !n_out) return SWIM_EINVAL;
   if (h->grp) {  // every shard's events, merged in (tick, observer, seq) order
     auto& ev = h->grp->events;
+    // events left over from an earlier call (cap smaller than what was buffered) are already sorted and numbered;
+    // only this call's events, all of later ticks, are sorted and numbered here
+    const size_t old = ev.size();
     std::vector<swim_event> buf(65536);
     const int rc = group_all(h, [&](swim_handle* s) {
       size_t n = 0;
@@ -1395,14 +1446,14 @@ int swim_drain_events(swim_handle* h, swim_event* out, size_t cap, size_t* n_out
     });
     if (rc != SWIM_OK) return rc;
     if (h->grp->slots) {  // one observer's events of a tick come from several shards: P4's gossip-id order, renumbered
-      std::stable_sort(ev.begin(), ev.end(), [](const swim_event& a, const swim_event& b) {
+      std::stable_sort(ev.begin() + (long)old, ev.end(), [](const swim_event& a, const swim_event& b) {
         if (a.tick != b.tick) return a.tick < b.tick;
         if (a.observer != b.observer) return a.observer < b.observer;
         return a.subject != b.subject ? a.subject < b.subject : a.pad < b.pad;
       });
-      for (swim_event& e : ev) e.seq = h->grp->evcount[e.observer]++;
+      for (size_t i = old; i < ev.size(); ++i) ev[i].seq = h->grp->evcount[ev[i].observer]++;
     } else {
-      std::stable_sort(ev.begin(), ev.end(), [](const swim_event& a, const swim_event& b) {
+      std::stable_sort(ev.begin() + (long)old, ev.end(), [](const swim_event& a, const swim_event& b) {
         if (a.tick != b.tick) return a.tick < b.tick;
         if (a.observer != b.observer) return a.observer < b.observer;
         return a.seq < b.seq;
@@ -1476,6 +1527,23 @@ int swim_counters_get(swim_handle* h, swim_counters* out) {
 }
 
 const char* swim_last_error(swim_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+int swim_debug_fallbacks(swim_handle* h, uint64_t* out, size_t n) {
+  if (!h || !out || n > FB_N) return SWIM_EINVAL;
+  std::fill(out, out + n, 0ull);
+  if (h->grp) {  // summed over the shards
+    std::vector<uint64_t> part(n);
+    return group_all(h, [&](swim_handle* s) {
+      const int rc = swim_debug_fallbacks(s, part.data(), n);
+      for (size_t i = 0; rc == SWIM_OK && i < n; ++i) out[i] += part[i];
+      return rc;
+    });
+  }
+  if (!h->d.fb) return SWIM_EUNSUPPORTED;  // not counted (SWIM_CAPS / SWIM_FALLBACKS unset at create)
+  HIPCK(hipStreamSynchronize(h->stream));
+  HIPCK(hipMemcpy(out, h->d.fb, 8 * n, hipMemcpyDeviceToHost));
+  return SWIM_OK;
+}
 
 // debugging aid (not part of the ABI header): the gossip send log of SWIM_SEND_LOG (tick, sender, gid lo/hi, target)
 int swimdbg_send_log(swim_handle* h, uint32_t* out, size_t cap, size_t* n) {

@@ -8,6 +8,11 @@ namespace swim {
 
 __device__ __forceinline__ void set_err(const Dev& d, uint32_t bit) { atomicOr(d.err, bit); }
 
+// a capacity fallback fired (engine.h Fb), when the handle counts them
+__device__ __forceinline__ void fb_add(const Dev& d, uint32_t i, unsigned long long n = 1) {
+  if (d.fb && n) atomicAdd(&d.fb[i], n);
+}
+
 // The workgroup that finishes last on `ctr` (nblocks workgroups) sees every other workgroup's plain stores. The
 // hand-off of MI355X_MICROARCH.md / cdna_hip_programming.md §6 Guideline 16 (counter form): every wave drains its
 // stores, then one lane releases at agent scope (write-back of its XCD's L2) and draws a ticket; the last one acquires

@@ -25,6 +25,8 @@ constexpr uint32_t TRK = 16;   // subjects written in one tick's P1 that are re-
 // snapshots per member, deferred snapshots per k_member_tick block
 constexpr uint32_t ULOG = 64, CREQ = 4, CWMAX = 32;
 constexpr uint32_t SPQ = 32;  // gossips a member creates in one tick before their slots are taken together
+constexpr uint32_t MQ = 16;   // inbound SYNC messages of one tick sorted in registers (more: selected by list walks)
+constexpr uint32_t SORT_MAX = 4096;  // receipts of one member and tick sorted in LDS at once (more: runs + merges)
 
 // S entry flags (gossip slot x member)
 constexpr uint32_t S_PENDING = 1u << 29, S_SWEPT = 1u << 30, S_REBORN = 1u << 31;
@@ -59,6 +61,20 @@ constexpr uint32_t XINL = 16384;  // RCCL: bytes per peer moved by the fixed-siz
 // counters (swim_counters order after .tick)
 enum Ctr { C_R = 0, C_W, C_M, C_G, C_E, C_LOST, C_GCREATED, C_SYNCMERGE, C_DIFFMSG = 13, C_NCTR = 16 };  // 8..12: SWIM_EXP & 4
 
+// capacity fallbacks that fired (include/swimhip_debug.h; counted only when Dev::fb is allocated: SWIM_CAPS or
+// SWIM_FALLBACKS set at create). Each one is an exact slow path taken when a fixed-capacity fast structure is full.
+enum Fb {
+  FB_TRK_WALK = 0,  // merge_payload compared a later payload against the whole row (more than trk_cap tracked subjects)
+  FB_ULOG,          // cow_now: a member's undo log was full (ulog_cap), its open snapshots copied by its lane
+  FB_CREQ,          // cow_now: a member had creq_cap snapshots open
+  FB_CWMAX,         // copy_row_to: the block's deferred snapshot list was full (cwmax_cap), the lane copied the row
+  FB_CEV_SLOW,      // k_gossip_send_slow: sends of a pair whose contact list overflowed the cache (cev_cap)
+  FB_REPLAY,        // k_gossip_replay: sends of a pair with a cached contact (isInfected replay)
+  FB_MQ,            // P1: more than mq_cap inbound SYNC messages, selected in key order by list walks
+  FB_SORT_MERGE,    // k_seg_sort: a receipt segment above sort_cap sorted in runs and merged
+  FB_N = 16
+};
+
 struct SyncMsg {
   uint32_t src, dst, kind, seq, cid_iss, cid_cnt;
   uint32_t payload;  // NEVER = sender's live row, else arena row index
@@ -87,6 +103,7 @@ struct Dev {
   uint32_t* md_ver;   // [NL][MDU] metadata version each observer stores for those members (the others: 0 if known)
   uint32_t mode, churn;  // SWIM_MODE_RUMOR: gossip layer only, churn rumors per FD period (SEMANTICS.md §9)
   uint64_t* churn_q;     // [churn][2] (origin, payload) of this period's rumors
+  uint32_t* ucnt;        // [N] scratch of the user-gossip queue: its entries per member (zero between launches)
   uint32_t seeds[16];
   uint32_t LCAP, FCAP, GRCAP, LOGW, SLOTS, MSGCAP, NCHUNK, POOLCAP, EVCAP, DCAP, RCAP, ARENA_ROWS, LOOKBACK, HCAP;
 
@@ -193,6 +210,10 @@ struct Dev {
   uint32_t* dbg_send_n;
   uint32_t dbg_send_cap;
   uint32_t exp;  // timing experiments only (SWIM_EXP): 1 = no infectedFrom replay, 2 = no per-target work
+  // runtime capacities of the fast structures (<= the compile-time sizes TRK, ULOG, CREQ, CWMAX, CEV, MQ, SORT_MAX);
+  // SWIM_CAPS lowers them so that tests drive every exact fallback path (include/swimhip_debug.h)
+  uint32_t trk_cap, ulog_cap, creq_cap, cwmax_cap, cev_cap, mq_cap, sort_cap;
+  unsigned long long* fb;  // [FB_N] fallback counters, or null (not counted)
 
   // ---- row sharding (W > 1) ----
   // This shard owns observers [lo, hi): their rows, lists, subscriptions, paths, fetches and groups are stored

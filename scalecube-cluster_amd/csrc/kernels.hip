@@ -190,7 +190,7 @@ __global__ void k_scan_add(uint32_t* out, const uint32_t* part, uint32_t n) {
 // up to SORT_MAX entries are sorted bitonically in LDS; larger ones (a member receiving thousands of new gossips in
 // one tick, C2-style storms) sort SORT_MAX runs in LDS and then merge run pairs through the scratch arrays, each
 // element finding its output position by a binary search in the partner run (merge path, no atomics).
-constexpr uint32_t SORT_MAX = 4096;
+// (SORT_MAX: engine.h; the runtime run length is Dev::sort_cap <= SORT_MAX)
 __device__ void lds_bitonic(uint64_t* K, uint32_t* V, const uint64_t* key, const uint32_t* val, uint32_t n,
                             uint64_t* okey, uint32_t* oval) {
   uint32_t p2 = 1;
@@ -240,7 +240,7 @@ __device__ __forceinline__ uint32_t lower_rank(const uint64_t* r, uint32_t n, ui
 
 __global__ void __launch_bounds__(256) k_seg_sort(uint64_t* key, uint32_t* val, uint64_t* tkey, uint32_t* tval,
                                                   const uint32_t* off, const uint32_t* cnt, uint32_t nseg,
-                                                  const uint32_t* nitems) {
+                                                  const uint32_t* nitems, uint32_t run, unsigned long long* fb) {
   __shared__ uint64_t K[SORT_MAX];
   __shared__ uint32_t V[SORT_MAX];
   if (*nitems == 0) return;  // nothing was routed this tick
@@ -248,15 +248,16 @@ __global__ void __launch_bounds__(256) k_seg_sort(uint64_t* key, uint32_t* val, 
     const uint32_t n = cnt[sgi];
     if (n <= 1) continue;
     const uint32_t o = off[sgi];
-    if (n <= SORT_MAX) {
+    if (n <= run) {
       lds_bitonic(K, V, key + o, val + o, n, key + o, val + o);
       continue;
     }
-    for (uint32_t c = 0; c < n; c += SORT_MAX)
-      lds_bitonic(K, V, key + o + c, val + o + c, min(SORT_MAX, n - c), key + o + c, val + o + c);
+    if (fb && threadIdx.x == 0) atomicAdd(&fb[FB_SORT_MERGE], 1ull);
+    for (uint32_t c = 0; c < n; c += run)
+      lds_bitonic(K, V, key + o + c, val + o + c, min(run, n - c), key + o + c, val + o + c);
     uint64_t *sk = key + o, *dk = tkey + o;
     uint32_t *sv = val + o, *dv = tval + o;
-    for (uint32_t w = SORT_MAX; w < n; w <<= 1) {
+    for (uint32_t w = run; w < n; w <<= 1) {
       for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
         const uint32_t base = i / (2 * w) * (2 * w), mid = min(base + w, n), end = min(base + 2 * w, n);
         const uint64_t x = sk[i];
@@ -677,7 +678,8 @@ __global__ void k_gossip_contacts(Dev d, uint32_t k) {
       Contact ev[CEV];
       uint32_t oldest[2];
       uint32_t* rec = d.cev + (size_t)i * CEVW;
-      const uint32_t n = collect_contacts<CEV>(d, m, t, k, 0, ev, oldest);
+      uint32_t n = collect_contacts<CEV>(d, m, t, k, 0, ev, oldest);
+      if (n > d.cev_cap) n = CEV + 1;  // SWIM_CAPS: a smaller cache overflows into k_gossip_send_slow
       rec[0] = n;
       rec[1] = oldest[0];
       rec[2] = oldest[1];
@@ -906,6 +908,7 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
       if (d.exp & 4) st[0] += wb != 0ull;
       const uint32_t* ga = active + (size_t)q * 64;
       if (ci == CIN_SLOW) {  // overflowed contact list: the full replay runs in k_gossip_send_slow
+        fb_add(d, FB_CEV_SLOW, __popcll(wb));  // each lane its own group's slots
         uint32_t i = wave_reserve(d.slow_n, (uint32_t)__popcll(wb));
         for (unsigned long long b = wb; b; b &= b - 1, ++i) {
           if (i < d.SLOWCAP)
@@ -918,6 +921,7 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
       if (ci != NEVER) {  // a cached contact t -> m: every slot of the pair goes to k_gossip_replay (isInfected :247)
         const uint32_t nb = (uint32_t)__popcll(wb);
         if (d.exp & 4) st[1] += nb;
+        fb_add(d, FB_REPLAY, nb);  // each lane its own group's slots
         uint32_t i = wave_reserve(d.rp_n, nb);
         for (unsigned long long b = wb; b; b &= b - 1, ++i) {
           if (i < d.RPCAP)
@@ -1268,7 +1272,7 @@ static void launch_receipt_routing(const Dev& d, hipStream_t st) {
   hipLaunchKernelGGL(k_scatter_rc, dim3(256), dim3(256), 0, st, d, d.rc_raw, d.rc_n, d.RCAP, d.rc_off, d.rc_fill,
                      d.rc_slot, d.rc_key);
   hipLaunchKernelGGL(k_seg_sort, dim3(1024), dim3(256), 0, st, d.rc_key, d.rc_slot, d.rc_key2, d.rc_slot2, d.rc_off,
-                     d.rc_cnt, d.N, d.rc_n);
+                     d.rc_cnt, d.N, d.rc_n, d.sort_cap, d.fb);
 }
 
 void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {

@@ -81,7 +81,7 @@ __device__ __forceinline__ void copy_row_to(ML& L, uint32_t r) {
 __device__ __forceinline__ void cow_now(ML& L) {
   const Dev& d = *L.d;
   const uint32_t b = L.k & 1;
-  const uint32_t n = min(*L.cw_n, CWMAX);
+  const uint32_t n = min(*L.cw_n, d.cwmax_cap);
   for (uint32_t q = 0; q < n; ++q) {
     uint4& e = L.cw[q];
     if (e.x != L.m) continue;  // another member's (entries are NEVER until written)
@@ -105,9 +105,13 @@ __device__ __forceinline__ void cow(ML& L) {
   }
   for (uint32_t i = L.pend; i != NEVER; i = d.msgs[b][i].pad) d.msgs[b][i].payload = r;
   L.pend = NEVER;
-  if (L.ncreq == CREQ) cow_now(L);  // rare: many send-then-write rounds in one tick
+  if (L.ncreq == d.creq_cap) {  // rare: many send-then-write rounds in one tick
+    fb_add(d, FB_CREQ);
+    cow_now(L);
+  }
   const uint32_t idx = atomicAdd(L.cw_n, 1u);  // LDS
-  if (idx >= CWMAX) {  // the block's list is full: this snapshot now, by this lane
+  if (idx >= d.cwmax_cap) {  // the block's list is full: this snapshot now, by this lane
+    fb_add(d, FB_CWMAX);
     copy_row_to(L, r);
     return;
   }
@@ -123,18 +127,21 @@ __device__ __forceinline__ void row_put(ML& L, uint32_t s, uint64_t v) {
   if (rec_inc(v) >= INC_LIMIT) set_err(*L.d, E_INC);
   if (L.pend != NEVER && L.rk[s] != k) cow(L);
   if (L.ncreq && L.rk[s] != k) {  // an open snapshot: log the key this write replaces
-    if (L.nlog == ULOG) cow_now(L);
-    else {
+    if (L.nlog == L.d->ulog_cap) {
+      fb_add(*L.d, FB_ULOG);
+      cow_now(L);
+    } else {
       L.ulog[2 * L.nlog] = s;
       L.ulog[2 * L.nlog + 1] = L.rk[s];
       L.nlog++;
     }
   }
-  if (L.trk_on && L.rk[s] != k && L.ntrk <= TRK) {  // merge_payload re-checks it against the later payloads
+  const uint32_t tcap = L.d->trk_cap;
+  if (L.trk_on && L.rk[s] != k && L.ntrk <= tcap) {  // merge_payload re-checks it against the later payloads
     bool seen = false;
     for (uint32_t i = 0; i < L.ntrk; ++i) seen |= L.trk[i] == s;
     if (!seen) {
-      if (L.ntrk < TRK) L.trk[L.ntrk] = s;
+      if (L.ntrk < tcap) L.trk[L.ntrk] = s;
       L.ntrk++;
     }
   }
@@ -304,17 +311,6 @@ __device__ __forceinline__ void slot_init(const Dev& d, uint32_t g, uint32_t m, 
   }
 }
 
-// one slot off the free stack (k_user_gossips; members batch theirs, flush_spreads)
-__device__ __forceinline__ bool new_slot(const Dev& d, uint32_t m, uint32_t k, uint64_t gid, uint32_t subj, uint64_t key) {
-  int pos = atomicSub(d.free_top, 1) - 1;
-  if (pos < 0) {
-    set_err(d, E_SLOTS);
-    return false;
-  }
-  slot_init(d, d.free_list[pos], m, k, gid, subj, key);
-  return true;
-}
-
 // the member's queued gossips of this tick get their slots with one atomic on the free stack: a member that re-spreads
 // hundreds of SYNC records in one tick (C2) would otherwise wait for one round trip on that hot word per gossip
 __device__ __forceinline__ void flush_spreads(ML& L) {
@@ -350,22 +346,67 @@ __device__ __forceinline__ void spread(ML& L, uint32_t subj, uint32_t st, uint32
 }
 
 // Cluster.spreadGossip (ClusterImpl.java:208-211) queued by swim_spread_gossip: user gossips of this shard's live
-// members, in call order, at P0 of tick k (before the member kernel loads gCounter / held). One thread: the order
-// of the gossip counters of one member must follow the calls.
-__global__ void k_user_gossips(Dev d, uint32_t k, const uint64_t* q, uint32_t n) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  unsigned long long created = 0;
-  for (uint32_t i = 0; i < n; ++i) {
-    const uint32_t m = (uint32_t)q[2 * i];
-    if (m < d.lo || m >= d.hi || dead_at(d, m, k)) continue;
-    const uint64_t gid = ((uint64_t)m << 32) | d.gCounter[m]++;
-    if (slot_mine(d, gid)) {  // slot sharding: only the owning shard stores it; every shard counts it as held
-      if (!new_slot(d, m, k, gid, USER_SUBJ, q[2 * i + 1])) continue;
-      created++;
-    }
-    d.held[m]++;
+// members, in call order, at P0 of tick k (before the member kernel loads gCounter / held). Only the order of one
+// member's calls is observable (its gossip counters follow them, GossipProtocolImpl.generateGossipId :207-209), so
+// the queue runs one thread per entry in three passes: count the entries per member, create each gossip with
+// counter gCounter[m] + (its rank among the member's entries), then advance the member's counter and gossip count
+// once. Slot ids are not observable; a wave takes its slots with one atomic on the free stack.
+__device__ __forceinline__ bool ug_live(const Dev& d, uint32_t m, uint32_t k) {
+  return m >= d.lo && m < d.hi && !dead_at(d, m, k);
+}
+__global__ void k_ug_count(Dev d, uint32_t k, const uint64_t* q, uint32_t n, uint32_t* ucnt) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t m = (uint32_t)q[2 * i];
+  if (ug_live(d, m, k)) atomicAdd(&ucnt[m], 1u);
+}
+// rank of entry i among the queue entries of member m before it (members with one entry: 0, no scan)
+__device__ __forceinline__ uint32_t ug_rank(const uint64_t* q, uint32_t i, uint32_t m, uint32_t cnt) {
+  if (cnt <= 1) return 0;
+  uint32_t r = 0;
+  for (uint32_t j = 0; j < i; ++j) r += (uint32_t)q[2 * j] == m;
+  return r;
+}
+__global__ void __launch_bounds__(256) k_ug_create(Dev d, uint32_t k, const uint64_t* q, uint32_t n, const uint32_t* ucnt) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t m = i < n ? (uint32_t)q[2 * i] : 0u;
+  bool mine = false;
+  uint64_t gid = 0;
+  if (i < n && ug_live(d, m, k)) {
+    gid = ((uint64_t)m << 32) | (d.gCounter[m] + ug_rank(q, i, m, ucnt[m]));
+    mine = slot_mine(d, gid);  // slot sharding: only the owning shard stores it; every shard counts it as held
   }
-  if (created) atomicAdd(&d.ctr[C_GCREATED], created);
+  const uint64_t bm = __ballot(mine);
+  const uint32_t lane = __lane_id(), nb = (uint32_t)__popcll(bm);
+  int top = 0;
+  if (lane == 0 && nb) top = atomicSub(d.free_top, (int)nb);
+  top = __shfl(top, 0);
+  if (mine) {
+    const int pos = top - (int)nb + (int)__popcll(bm & ((1ull << lane) - 1ull));
+    if (pos < 0)
+      set_err(d, E_SLOTS);
+    else
+      slot_init(d, d.free_list[pos], m, k, gid, USER_SUBJ, q[2 * i + 1]);
+  }
+  if (lane == 0 && nb) atomicAdd(&d.ctr[C_GCREATED], (unsigned long long)nb);
+}
+__global__ void k_ug_finish(Dev d, uint32_t k, const uint64_t* q, uint32_t n, uint32_t* ucnt) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t m = (uint32_t)q[2 * i];
+  if (!ug_live(d, m, k)) return;
+  const uint32_t c = ucnt[m];
+  if (ug_rank(q, i, m, c) != 0) return;  // the member's first entry advances it once
+  d.gCounter[m] += c;
+  d.held[m] += c;
+  ucnt[m] = 0;
+}
+void launch_ug(const Dev& d, uint32_t k, const uint64_t* q, uint32_t n, hipStream_t st) {
+  if (n == 0) return;
+  const dim3 g((n + 255) / 256), b(256);
+  hipLaunchKernelGGL(k_ug_count, g, b, 0, st, d, k, q, n, d.ucnt);
+  hipLaunchKernelGGL(k_ug_create, g, b, 0, st, d, k, q, n, d.ucnt);
+  hipLaunchKernelGGL(k_ug_finish, g, b, 0, st, d, k, q, n, d.ucnt);
 }
 
 // RUMOR-mode churn of period p = k / ping_t (SEMANTICS.md §9): event i picks the churned member v and an origin
@@ -384,11 +425,11 @@ __global__ void k_churn(Dev d, uint32_t k) {
 
 void launch_churn(const Dev& d, uint32_t k, void* stream) {
   hipLaunchKernelGGL(k_churn, dim3((d.churn + 255) / 256), dim3(256), 0, (hipStream_t)stream, d, k);
-  hipLaunchKernelGGL(k_user_gossips, dim3(1), dim3(64), 0, (hipStream_t)stream, d, k, d.churn_q, d.churn);
+  launch_ug(d, k, d.churn_q, d.churn, (hipStream_t)stream);
 }
 
 void launch_user_gossips(const Dev& d, uint32_t k, const uint64_t* q, uint32_t n, void* stream) {
-  hipLaunchKernelGGL(k_user_gossips, dim3(1), dim3(64), 0, (hipStream_t)stream, d, k, q, n);
+  launch_ug(d, k, q, n, (hipStream_t)stream);
 }
 
 // the metadata version this observer stores for subj (MetadataStoreImpl.membersMetadata), NONE32 if unknown
@@ -777,7 +818,8 @@ __device__ __forceinline__ void merge_payload(ML& L, uint32_t mi, uint32_t reaso
   L.c[C_R] += mm.psize;
   L.c[C_SYNCMERGE]++;
   const uint32_t nt = L.ntrk;
-  const bool full = nt > TRK;  // rare: many subjects changed earlier in this tick; exact full walk
+  const bool full = nt > d.trk_cap;  // rare: many subjects changed earlier in this tick; exact full walk
+  if (full) fb_add(d, FB_TRK_WALK);
   if (d.exp & 128) {  // timing experiments: full walks, largest candidate count
     if (full) atomicAdd(&d.ctr[14], 1ull);
     atomicMax(&d.ctr[15], (unsigned long long)mm.ncand);
@@ -1057,13 +1099,13 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
     const uint32_t pb = (k - 1) & 1;
     const uint32_t head = d.m_head[(size_t)pb * d.N + m];
     d.m_head[(size_t)pb * d.N + m] = NEVER;
-    constexpr uint32_t MQ = 16;
     uint64_t key[MQ];
     uint32_t idx[MQ], n = 0;
     bool more = false;
     for (uint32_t q = head; q != NEVER; q = mnext[q]) {
-      if (n == MQ) {
+      if (n == d.mq_cap) {
         more = true;
+        fb_add(d, FB_MQ);
         break;
       }
       const SyncMsg& mq = d.msgs[pb][q];
@@ -1449,7 +1491,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   for (uint32_t q = 0; q < L.nsub; ++q) nev = min(nev, L.subs[(size_t)q * 4 + 3]);
   nev = min(nev, L.fnext);
   if (L.ncreq)  // the log length the block epilogue undoes from
-    for (uint32_t q = 0, n = min(*L.cw_n, CWMAX); q < n; ++q)
+    for (uint32_t q = 0, n = min(*L.cw_n, d.cwmax_cap); q < n; ++q)
       if (L.cw[q].x == m) L.cw[q].w = L.nlog;
   d.next_evt[m] = nev;
   d.tround[m] = L.tround;
@@ -1549,7 +1591,7 @@ __global__ void __launch_bounds__(256) k_member_tick(const Dev* __restrict__ dp,
   // deferred copy-on-write: the block copies each snapshot's row (final for this tick: only its member writes it),
   // then one lane undoes the member's logged writes since the snapshot opened, newest first
   __syncthreads();
-  const uint32_t ncw = min(cw_n, CWMAX);
+  const uint32_t ncw = min(cw_n, d.cwmax_cap);
   for (uint32_t q = 0; q < ncw; ++q) {
     const uint4 e = cw[q];
     if (e.x == NEVER) continue;  // made by its lane already (cow_now)

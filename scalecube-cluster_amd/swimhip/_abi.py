@@ -192,6 +192,24 @@ def selftest_eval(lib, op, rows, device=0):
     return [tuple(cout[i * wout:(i + 1) * wout]) for i in range(len(rows))]
 
 
+# include/swimhip_debug.h (capacity-fallback counters; libswimhip only, with SWIM_CAPS / SWIM_FALLBACKS at create)
+FB_NAMES = ["trk_walk", "ulog", "creq", "cwmax", "cev_slow", "replay", "mq", "sort_merge"]
+DEBUG_SIGNATURES = {
+    "swim_debug_fallbacks": (C.c_int, [_H, C.POINTER(C.c_uint64), C.c_size_t]),
+}
+
+
+def debug_fallbacks(lib, handle):
+    """{name: count} of the capacity fallbacks the handle took (include/swimhip_debug.h)."""
+    fn = lib.swim_debug_fallbacks
+    fn.restype, fn.argtypes = DEBUG_SIGNATURES["swim_debug_fallbacks"]
+    out = (C.c_uint64 * len(FB_NAMES))()
+    rc = fn(handle, out, len(FB_NAMES))
+    if rc != 0:
+        raise RuntimeError(f"swim_debug_fallbacks rc={rc}")
+    return dict(zip(FB_NAMES, (int(x) for x in out)))
+
+
 # include/swimhip_wire.h (wire-format export; libswimhip only)
 class SwimWireRecord(C.Structure):
     _fields_ = [("member", C.c_uint32), ("status", C.c_uint32), ("incarnation", C.c_uint32)]

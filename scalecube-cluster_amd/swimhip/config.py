@@ -63,8 +63,8 @@ class SimConfig:
     latency_ticks: int = 1
     record_events: bool = False
     profile: bool = False
-    profile_all: bool = False
-    implicit_views: bool = False  # SWIM_FLAG_IMPLICIT_VIEWS (RUMOR mode): tables / lists computed, not stored  # SWIM_FLAG_PROFILE_ALL: every k_sync_diff launch timed (+ member / gossip kernels)
+    profile_all: bool = False  # SWIM_FLAG_PROFILE_ALL: every k_sync_diff launch timed (+ member / gossip kernels)
+    implicit_views: bool = False  # SWIM_FLAG_IMPLICIT_VIEWS (RUMOR mode): tables / lists computed, not stored
     gossip_slot_cap: int = 0
     pending_fetch_cap: int = 0
     event_cap: int = 0

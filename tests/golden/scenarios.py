@@ -42,6 +42,20 @@ def _c4_mid():  # C4-shaped at 200 members: suspicion timeouts (40 periods) star
         ("partition", g), ("periods", 45), ("unblock", None), ("periods", 30)]
 
 
+def _c2_mid():  # C2-shaped at 2 000 members: 5 % loss on every link; refutations re-spread by SYNC build the gossip
+    # storm the bench line measures at 10k. Recorded once (SWIMREF_THREADS=8 python tests/golden/make_golden.py c2_mid)
+    return SimConfig(n_members=2000, record_events=True), [("loss", 5), ("periods", 14)]
+
+
+def _c4_long():  # C4's full schedule at 300 members: partition from period 0, healed at period 200 (as configs[3]),
+    # run 40 periods past the heal: suspicion timeouts, the DEAD-gossip storm, then SYNC recovery. Recorded once
+    n = 300
+    g = [0] * (n // 2) + [1] * (n // 2)
+    return SimConfig(n_members=n, cluster=ClusterConfig(seedMembers=[0]), gossip_slot_cap=1 << 19, pending_fetch_cap=4096,
+                     list_slack=4096), [
+        ("partition", g), ("periods", 200), ("unblock", None), ("periods", 40)]
+
+
 def _c3_small():  # C3-shaped: steady state SYNC / SYNC_ACK anti-entropy, no loss
     return SimConfig(n_members=1000), [("periods", 35)]
 
@@ -51,8 +65,8 @@ def _c5_small():  # C5-shaped: rumor-only dissemination with 1 % churn per perio
 
 
 SCENARIOS = {"c1": _c1, "c2_small": _c2_small, "c4_small": _c4_small, "c3_small": _c3_small, "c5_small": _c5_small,
-             "c4_mid": _c4_mid}
-SLOW_ON_ORACLE = {"c4_mid"}  # recorded once; replaying it on the oracle takes minutes
+             "c4_mid": _c4_mid, "c2_mid": _c2_mid, "c4_long": _c4_long}
+SLOW_ON_ORACLE = {"c4_mid", "c2_mid", "c4_long"}  # recorded once; replaying it on the oracle takes minutes
 FULL_EVENTS = {"c1"}
 
 

@@ -14,6 +14,7 @@ HEADER = Path(__file__).resolve().parent.parent / "include" / "swimhip.h"
 SHARD_HEADER = Path(__file__).resolve().parent.parent / "include" / "swimhip_shard.h"
 SELFTEST_HEADER = Path(__file__).resolve().parent.parent / "include" / "swimhip_selftest.h"
 WIRE_HEADER = Path(__file__).resolve().parent.parent / "include" / "swimhip_wire.h"
+DEBUG_HEADER = Path(__file__).resolve().parent.parent / "include" / "swimhip_debug.h"
 
 
 def declared_symbols(header=HEADER):
@@ -37,6 +38,13 @@ def test_selftest_header_and_ctypes_agree():
     assert set(declared_symbols(SELFTEST_HEADER)) == set(_abi.SELFTEST_SIGNATURES)
 
 
+def test_debug_header_and_ctypes_agree():
+    assert set(declared_symbols(DEBUG_HEADER)) == set(_abi.DEBUG_SIGNATURES)
+    text = DEBUG_HEADER.read_text()
+    for i, name in enumerate(_abi.FB_NAMES):  # index constants match the Python names
+        assert re.search(rf"#define SWIM_FB_{name.upper()}\s+{i}u", text), name
+
+
 def test_oracle_exports_every_symbol(oracle):
     for name in declared_symbols() + declared_symbols(SELFTEST_HEADER):
         assert hasattr(oracle, name), name
@@ -47,7 +55,7 @@ def test_engine_library_exports_every_symbol():
         pytest.skip("libswimhip.so not built (run __graft_entry__.build())")
     lib = _abi.load(LIB_PATH)  # loading initialises no device
     for name in (declared_symbols() + declared_symbols(SHARD_HEADER) + declared_symbols(SELFTEST_HEADER)
-                 + declared_symbols(WIRE_HEADER)):
+                 + declared_symbols(WIRE_HEADER) + declared_symbols(DEBUG_HEADER)):
         assert hasattr(lib, name), name
     assert lib.swim_abi_version() == 1
     # pure helpers run on the host side of the library

@@ -77,3 +77,17 @@ def test_rumor_mode(oracle, engine):
         c.set_default_loss(10)
     run_lockstep(o, e, 150, 50, "rumor n_gpus=2")
     e.close()
+
+
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_drain_small_cap(oracle, engine, gpus):
+    """swim_drain_events with a cap far below the buffered count: every call returns the next events in order and
+    the per-observer seq numbers neither skip nor repeat (slot-sharded RUMOR group: they are renumbered once)."""
+    cfg = SimConfig(n_members=120, mode=_abi.MODE_RUMOR, churn_per_period=4, record_events=True)
+    o, e = pair(oracle, engine, cfg, gpus)
+    for part in range(3):
+        o.step(40)
+        e.step(40)
+        eo, ee = o.events(), e.events(cap=7)  # several small drains per call, leftovers carried between them
+        assert eo == ee, f"part {part}: {len(eo)} oracle vs {len(ee)} engine events"
+    e.close()

@@ -93,14 +93,16 @@ def test_sync_same_tick_resurrection(oracle, engine, monkeypatch, shards):
     e.close()
 
 
-@pytest.mark.parametrize("shards", [1, 2])
-def test_member_configs(oracle, engine, shards):
+@pytest.mark.parametrize("shards,cold", [(1, False), (2, False), (1, True), (2, True)])
+def test_member_configs(oracle, engine, shards, cold):
     """Members with their own ClusterConfig (swim_set_member_config): FD timings and ping-req counts per member
     (FailureDetectorTest.testTrustedDespiteDifferentPingTimings, :150-178; the member's suspicion timeout follows its
     own pingInterval, MembershipProtocolImpl.java:597-606) and two syncGroups whose SYNC data the other side ignores
-    (checkSyncGroup, :431-437), under loss and with a crash; bit-exact with the oracle."""
+    (checkSyncGroup, :431-437), under loss and with a crash; bit-exact with the oracle. `cold`: every member joins at
+    tick 0 through the seeds (start0), so its first ping follows its own pingInterval."""
     n = 60
-    cfg = SimConfig(n_members=n, cluster=ClusterConfig(seedMembers=[0, 55], syncInterval=3000), record_events=True)
+    cfg = SimConfig(n_members=n, cluster=ClusterConfig(seedMembers=[0, 55], syncInterval=3000), record_events=True,
+                    init_mode=_abi.INIT_COLD_JOIN if cold else _abi.INIT_PRECONVERGED)
     o = SimulatedCluster(oracle, cfg)
     if shards == 1:
         e = SimulatedCluster(engine, cfg)
