@@ -97,7 +97,8 @@ typedef struct swim_config {
   uint32_t list_slack;        /* FD / gossip list entries beyond N (duplicates after reordered ADDED / REMOVED) */
   uint32_t churn_per_period;  /* SWIM_MODE_RUMOR: churn events (one rumor each) drawn at the start of every FD period */
   uint32_t n_dormant;         /* COLD_JOIN: the last n_dormant members are not started; each starts on swim_join */
-  uint32_t reserved[4];
+  uint32_t gossip_ring_cap;   /* gossips one member can hold at once (its receipt ring; rounded up to a power of two) */
+  uint32_t reserved[3];
 } swim_config;
 
 /* One member's own configuration where it differs from the handle's config. The reference builds every member from its own

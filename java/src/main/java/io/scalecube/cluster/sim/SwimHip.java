@@ -58,7 +58,8 @@ public final class SwimHip implements AutoCloseable {
           JAVA_INT.withName("list_slack"),
           JAVA_INT.withName("churn_per_period"),
           JAVA_INT.withName("n_dormant"),
-          MemoryLayout.sequenceLayout(4, JAVA_INT).withName("reserved"),
+          JAVA_INT.withName("gossip_ring_cap"),
+          MemoryLayout.sequenceLayout(3, JAVA_INT).withName("reserved"),
           MemoryLayout.paddingLayout(4));
 
   /** swim_member_config: 32 bytes. */

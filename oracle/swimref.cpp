@@ -180,7 +180,14 @@ struct Member {
     Rec rec;
     uint64_t payload = 0;
     uint64_t infPeriod;
-    std::set<uint32_t> infected;
+    // infectedFrom (GossipState.java:8-38) as a sorted vector: the same set semantics in ~4 B per sender (a
+    // std::set costs ~40 B per node; C2-shaped runs hold ~10^8 (member, gossip) states with tens of senders each)
+    std::vector<uint32_t> infected;
+    bool is_infected(uint32_t t) const { return std::binary_search(infected.begin(), infected.end(), t); }
+    void add_infected(uint32_t t) {
+      auto it = std::lower_bound(infected.begin(), infected.end(), t);
+      if (it == infected.end() || *it != t) infected.insert(it, t);
+    }
   };
   std::map<uint64_t, GState> gossips;
 
@@ -651,7 +658,7 @@ void Member::do_spread_gossip(uint64_t k) {
     for (auto& kv : gossips) {
       GState& g = kv.second;
       if (g.infPeriod + sp < period) continue;
-      if (g.infected.count(t)) continue;
+      if (g.is_infected(t)) continue;
       tl_lane->ctr.gossip_messages++;
       const bool lost = s.lost_gossip(id, t, k, slot, kv.first);
       if (s.send_log) fprintf(s.send_log, "S %llu %u %llu %u %d\n", (unsigned long long)k, id, (unsigned long long)kv.first, t, lost ? 1 : 0);
@@ -906,7 +913,7 @@ void Member::process(uint64_t k, std::vector<Msg>& inbox) {
         update_membership(m->g_subj, m->g_rec, R_GOSSIP, -1, k);  // onMembershipGossip (:401-408)
       }
     }
-    gossips[m->gid].infected.insert(m->src);
+    gossips[m->gid].add_infected(m->src);
   }
   // ---- P5 timers ----
   {

@@ -337,14 +337,33 @@ int build(swim_handle* h) {
   // 100k members and W = 8 a full range per shard would be a 275 GB holder table on every GPU
   const uint64_t share = d.W == 1 ? slots : std::max<uint64_t>(1024, (2 * slots + d.W - 1) / d.W);
   d.SPR = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(slots, share), (1ull << 22) / d.W);
+  d.SPR = (d.SPR + 63u) & ~63u;  // whole 64-slot groups per shard (holder bit rows)
   d.SLOTS = d.SPR * d.W;
-  d.QW = d.SLOTS / 64 + 1;
+  d.QW = d.SLOTS / 64;
+  // a gossip's holders have all swept it within 2 (spread + 1) + 2 of their rounds after their receipt
+  // (sweepGossips :283-308, spread <= maxSpread): its slot is recycled after that (slot_exp)
+  d.EXPB = (2u * maxSpread + 4u) * d.gossip_t;
+  if (2u * maxSpread + 4u >= 500u) {  // receipt-ring entries keep the infection period modulo 1024 (gossip.hip)
+    h->err = "gossipRepeatMult x ceilLog2(members) too large (at most 248)";
+    return SWIM_EINVAL;
+  }
+  // receipt ring per member: at least as many entries as the member can hold gossips; default the slot table's
+  // size up to a 48 GB total (C2 holds ~3·10^5 per member), swim_config.gossip_ring_cap overrides
+  {
+    uint64_t want = c.gossip_ring_cap ? c.gossip_ring_cap
+                                      : std::min<uint64_t>(d.SLOTS, std::max<uint64_t>(1024, (48ull << 30) / (4 * N)));
+    uint64_t bc = 64;
+    while (bc < want && bc < (1ull << 31)) bc <<= 1;
+    if (!c.gossip_ring_cap && bc > want && bc / 2 >= 1024 && bc > d.SLOTS) bc /= 2;
+    d.BCAP = (uint32_t)bc;
+  }
   uint64_t mc = N / d.sync_t * 4 + N / d.ping_t + 1024;
   if (c.init_mode == SWIM_INIT_COLD_JOIN) mc = std::max<uint64_t>(mc, N + 1024);
   d.MSGCAP = (uint32_t)mc;
   d.NCHUNK = (uint32_t)((d.NS + CH - 1) / CH);
   d.POOLCAP = (uint32_t)std::min<uint64_t>(1ull << 26, std::max<uint64_t>(1ull << 20, N * 64));
   d.EVCAP = c.event_cap ? c.event_cap : (1u << 20);
+  // first receipts per tick: routed to P4 (RCAP), shipped to the other row shards (DCAP)
   d.DCAP = (uint32_t)std::min<uint64_t>(1ull << 27, std::max<uint64_t>(1ull << 16, N * 16384));
   d.RCAP = d.DCAP;
   // infectedFrom replays: in a small cluster most pairs have a logged contact, so under a DEAD-gossip storm nearly
@@ -384,16 +403,19 @@ int build(swim_handle* h) {
   const uint64_t NV = d.implicit ? 1 : NL;  // implicit views: no table or list is stored
   A(d.rowk, NV * d.NS) A(d.rowa, NV * d.NS) A(d.fdl, NV * d.LCAP) A(d.gl, NV * d.LCAP)
   A(d.subs, NL * SUBCAP * 4) A(d.paths, NL * PATHCAP * 5) A(d.fetch, NL * d.FCAP * FREC) A(d.groups, NL * d.GRCAP * GREC)
-  A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.slow, d.SLOWCAP) A(d.slow_n, 1) A(d.rp, d.RPCAP) A(d.rp_n, 1) A(d.rlist, N) A(d.rn, 1) A(d.start_tick, N) A(d.jseed_n, N) A(d.jseeds, 16 * N) A(d.md_uidx, N) A(d.mcfg, 4 * N) A(d.md_ver, NL * MDU) A(d.churn_q, 2ull * d.churn) A(d.ucnt, N) A(d.cin, N * d.F) A(d.swthr, N) A(d.HB, (uint64_t)d.QW * N) A(d.WB, (uint64_t)d.QW * N) A(d.HBq, (uint64_t)d.QW * N) A(d.WBq, (uint64_t)d.QW * N) A(d.cev, N * d.F * CEVW)
+  A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.slow, d.SLOWCAP) A(d.slow_n, 1) A(d.rp, d.RPCAP) A(d.rp_n, 1) A(d.start_tick, N) A(d.jseed_n, N) A(d.jseeds, 16 * N) A(d.md_uidx, N) A(d.mcfg, 4 * N) A(d.md_ver, NL * MDU) A(d.churn_q, 2ull * d.churn) A(d.ucnt, N) A(d.cin, N * d.F) A(d.HB, (uint64_t)d.QW * N) A(d.WB, (uint64_t)d.QW * N) A(d.cev, N * d.F * CEVW)
+  A(d.rg, (uint64_t)d.BCAP * N) A(d.rhead, N) A(d.rwin, N) A(d.rseen, N) A(d.rtail, N) A(d.rwl, N) A(d.nrwl, 1)
+  A(d.rsend, N) A(d.rwnew, N) A(d.GU, d.QW) A(d.DM, d.QW) A(d.agroup, d.QW) A(d.nagroup, 2)
+  A(d.tin_cnt, N) A(d.tin_off, N) A(d.tin_fill, N) A(d.tin, N * d.F) A(d.tlist, N) A(d.ntl, 1) A(d.rt0, N)
   A(d.log_tick, N * d.LOGW) A(d.log_spread, N * d.LOGW) A(d.log_cnt, N * d.LOGW) A(d.log_tg, N * d.LOGW * d.F)
   A(d.log_pos, N) A(d.spchg, N)
-  A(d.slot_gid, d.SLOTS) A(d.slot_subj, d.SLOTS) A(d.slot_ctick, d.SLOTS) A(d.slot_key, d.SLOTS) A(d.slot_holders, d.SLOTS)
+  A(d.slot_gid, d.SLOTS) A(d.slot_subj, d.SLOTS) A(d.slot_ctick, d.SLOTS) A(d.slot_key, d.SLOTS) A(d.slot_exp, d.SLOTS)
   A(d.slot_used, d.SLOTS) A(d.S, (uint64_t)d.SLOTS * N) A(d.free_list, d.SLOTS) A(d.free_top, 1)
-  A(d.deliv, d.DCAP) A(d.deliv_n, 1) A(d.rc_raw, d.RCAP) A(d.rc_n, 1) A(d.rc_cnt, N) A(d.rc_off, N) A(d.rc_fill, N) A(d.scan_part, 1024)
-  A(d.rc_slot, d.RCAP) A(d.rc_ndrop, N) A(d.dead_rx, N) A(d.leaving, N) A(d.rc_key, d.RCAP) A(d.rc_slot2, d.RCAP) A(d.rc_key2, d.RCAP) A(d.active, d.SLOTS) A(d.nactive, 1) A(d.hist, (uint64_t)d.HCAP * HREC)
+  A(d.xd, d.W > 1 ? d.DCAP : 1) A(d.xd_n, 1) A(d.rc_raw, d.RCAP) A(d.rc_n, 1) A(d.rc_cnt, N) A(d.rc_off, N) A(d.rc_fill, N) A(d.scan_part, 1024)
+  A(d.rc_slot, d.RCAP) A(d.rc_ndrop, N) A(d.dead_rx, N) A(d.leaving, N) A(d.rc_key, d.RCAP) A(d.rc_slot2, d.RCAP) A(d.rc_key2, d.RCAP) A(d.fexp, d.SLOTS) A(d.nfexp, 1) A(d.hist, (uint64_t)d.HCAP * HREC)
   A(d.msgs[0], d.MSGCAP) A(d.msgs[1], d.MSGCAP) A(d.nmsg, 2) A(d.arena[0], (uint64_t)d.ARENA_ROWS * d.NS)
   A(d.arena[1], (uint64_t)d.ARENA_ROWS * d.NS) A(d.arena_used, 2)
-  A(d.m_next, 2ull * d.MSGCAP) A(d.m_head, 2 * N) A(d.deaths, 2ull * DEATHCAP) A(d.deaths_n, 2) A(d.next_evt, N) A(d.mdone, 1) A(d.trk, NL * TRK) A(d.ulog, NL * ULOG * 2) A(d.spq, NL * SPQ * 8) A(d.pending_inc, N) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
+  A(d.m_next, 2ull * d.MSGCAP) A(d.m_head, 2 * N) A(d.next_evt, N) A(d.mdone, 1) A(d.trk, NL * TRK) A(d.ulog, NL * ULOG * 2) A(d.spq, NL * SPQ * 8) A(d.pending_inc, N) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
   A(d.pool, d.POOLCAP) A(d.pool_used, 1)
   A(d.ev, (uint64_t)d.EVCAP * 8) A(d.ev_n, 1) A(d.ctr, C_NCTR) A(d.err, 8)
   if (d.fastp4) {
@@ -422,18 +444,17 @@ int build(swim_handle* h) {
     d.MW = (d.NCHUNK + 63) / 64;
     d.NSCAP = 1u << 16;
     d.RRCAP = d.NL;
-    d.SWCAP = 1u << 20;
     d.RQCAP = d.MSGCAP;
     d.RXCAP = d.MSGCAP;
     d.CHCAP = h->spec.chunk_cap ? h->spec.chunk_cap : (uint32_t)std::min<uint64_t>(4096, (uint64_t)d.MSGCAP * d.NCHUNK);
     uint64_t se = sizeof(SyncMsg) + 8 + 8ull * d.MW;
     d.XA_PEER = ((32 + 4ull * NSW * d.NSCAP + 4ull * RRW * d.RRCAP + se * d.RQCAP + 511) & ~255ull) +
                 (uint64_t)d.CHCAP * CH * 4;
-    d.XB_PEER = 16 + 8ull * std::min<uint64_t>((uint64_t)d.DCAP + d.SWCAP, 1ull << 25);
+    d.XB_PEER = 16 + 8ull * std::min<uint64_t>((uint64_t)d.DCAP, 1ull << 25);
     A(d.rdirty, (uint64_t)NL * d.MW) A(d.arena_dirty[0], (uint64_t)d.ARENA_ROWS * d.MW)
     A(d.arena_dirty[1], (uint64_t)d.ARENA_ROWS * d.MW)
     A(d.base_row, d.NS) A(d.xn, 8) A(d.ns_rec, (uint64_t)d.NSCAP * NSW) A(d.rr_rec, (uint64_t)d.RRCAP * RRW)
-    A(d.sw_rec, d.SWCAP) A(d.rq_n, d.W) A(d.rq_list, (uint64_t)d.W * d.RQCAP)
+    A(d.rq_n, d.W) A(d.rq_list, (uint64_t)d.W * d.RQCAP)
     A(d.rq_mask, (uint64_t)d.W * d.RQCAP * d.MW) A(d.rq_cnt, (uint64_t)d.W * d.RQCAP) A(d.rq_base, (uint64_t)d.W * d.RQCAP)
     A(d.mtmp, d.MSGCAP) A(d.rx_mask, (uint64_t)d.RXCAP * d.MW) A(d.rx_off, d.RXCAP)
     A(d.xa_send, d.W * d.XA_PEER) A(d.xa_recv, d.W * d.XA_PEER) A(d.xb_send, d.W * d.XB_PEER)
@@ -454,6 +475,11 @@ int build(swim_handle* h) {
   }
 #undef A
   HIPCK(hipMemsetAsync(d.S, 0, (size_t)d.SLOTS * N * 4, h->stream));
+  HIPCK(hipMemsetAsync(d.HB, 0, (size_t)d.QW * N * 8, h->stream));
+  HIPCK(hipMemsetAsync(d.WB, 0, (size_t)d.QW * N * 8, h->stream));
+  HIPCK(hipMemsetAsync(d.GU, 0, (size_t)d.QW * 8, h->stream));
+  HIPCK(hipMemsetAsync(d.DM, 0, (size_t)d.QW * 8, h->stream));
+  HIPCK(hipMemsetAsync(d.nagroup, 0, 8, h->stream));
   HIPCK(hipMemsetAsync(d.ctr, 0, C_NCTR * 8, h->stream));
   HIPCK(hipMemsetAsync(d.hist, 0, (size_t)d.HCAP * HREC * 8, h->stream));
   HIPCK(hipMemsetAsync(d.err, 0, 32, h->stream));
@@ -463,12 +489,10 @@ int build(swim_handle* h) {
   HIPCK(hipMemsetAsync(d.tcnt, 0, N * 4, h->stream));
   HIPCK(hipMemsetAsync(d.ucnt, 0, N * 4, h->stream));
   HIPCK(hipMemsetAsync(d.pool_used, 0, 4, h->stream));
-  HIPCK(hipMemsetAsync(d.deaths_n, 0, 8, h->stream));
   HIPCK(hipMemsetAsync(d.mdone, 0, 4, h->stream));
   HIPCK(hipMemsetAsync(d.link_n, 0, 4, h->stream));
   HIPCK(hipMemsetAsync(d.link_key, 0, 8ull * LKCAP, h->stream));
-  HIPCK(hipMemsetAsync(d.nactive, 0, 4, h->stream));
-  HIPCK(hipMemsetAsync(d.deliv_n, 0, 4, h->stream));
+  HIPCK(hipMemsetAsync(d.xd_n, 0, 4, h->stream));
   HIPCK(hipMemsetAsync(d.rc_n, 0, 4, h->stream));
   HIPCK(hipMemsetAsync(d.rc_ndrop, 0, 4 * N, h->stream));
   HIPCK(hipMemsetAsync(d.dead_rx, 0, 4 * N, h->stream));
@@ -1110,7 +1134,7 @@ int swim_kill(swim_handle* h, uint32_t m) {
   if (!h || m >= h->d.N) return SWIM_EINVAL;
   uint32_t t = (uint32_t)h->tick;
   HIPCK(hipMemcpyAsync(h->d.dead_tick + m, &t, 4, hipMemcpyHostToDevice, h->stream));
-  launch_kill(h->d, m, h->stream);
+  // (the crashed member's holder state stays as it is: it never sends again, sends to it fail, and its slots expire)
   return check_err(h);
 }
 

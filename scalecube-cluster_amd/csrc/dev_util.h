@@ -219,22 +219,49 @@ __device__ __forceinline__ uint32_t suspicion_ticks(const Dev& d, uint32_t size,
 }
 
 // member m swept gossip slot g at tick k: if g is m's own leave notification, leaveCluster completes and
-// ClusterImpl.doShutdown stops the member (ClusterImpl.java:305-313, GossipProtocolImpl.java:296-306); it is dead
-// from tick k + 1 and its held gossips stop counting as held at the start of that tick's gossip plane
+// ClusterImpl.doShutdown stops the member (ClusterImpl.java:305-313, GossipProtocolImpl.java:296-306): it is dead
+// from tick k + 1
 __device__ __forceinline__ void on_sweep(const Dev& d, uint32_t g, uint32_t m, uint32_t k) {
   if ((uint32_t)(d.slot_gid[g] >> 32) != m || d.slot_subj[g] != m || rec_status(d.slot_key[g]) != ST_DEAD) return;
   d.dead_tick[m] = k + 1u;
-  const uint32_t b = k & 1u;
-  const uint32_t i = atomicAdd(&d.deaths_n[b], 1u);
-  if (i < DEATHCAP)
-    d.deaths[(size_t)b * DEATHCAP + i] = m;
-  else
-    atomicOr(d.err, E_DEATHS);
 }
 
+// S entries: creation tick + 1 (0 = never held), SWEPT, REBORN
 __device__ __forceinline__ uint32_t s_ctick(uint32_t e) { return (e & S_TICK_MASK) - 1u; }
 __device__ __forceinline__ bool s_ever(uint32_t e) { return (e & S_TICK_MASK) != 0; }
 __device__ __forceinline__ bool s_held(uint32_t e) { return (e & S_TICK_MASK) != 0 && !(e & S_SWEPT); }
+
+// ---- gossip holder state (gossip.hip) ----
+// ring entries: slot (22 bits) | infection period & 1023 << 22. At a round every entry's period lies in
+// [P - 2 spreadMax - 3, P] (swim_create bounds spreadMax), so the low 10 bits identify it.
+constexpr uint32_t RG_SLOT = (1u << 22) - 1u;
+__device__ __forceinline__ uint32_t rg_entry(uint32_t g, uint32_t infp) { return g | ((infp & 1023u) << 22); }
+__device__ __forceinline__ int64_t rg_period(uint32_t e, uint32_t P) {
+  const int32_t rel = (int32_t)(((e >> 22) - (P & 1023u) + 512u) & 1023u) - 512;
+  return (int64_t)P + rel;
+}
+__device__ __forceinline__ uint32_t* ring(const Dev& d, uint32_t m) { return d.rg + (size_t)m * d.BCAP; }
+__device__ __forceinline__ unsigned long long* hrow(const Dev& d, uint32_t m) { return d.HB + (size_t)m * d.QW; }
+__device__ __forceinline__ unsigned long long* wrow(const Dev& d, uint32_t m) { return d.WB + (size_t)m * d.QW; }
+
+// createAndPutGossip (GossipProtocolImpl.java:163-169) at member m, tick k: the slot's table entries and the
+// creator's holder state. The caller reserved ring position `pos` of m.
+__device__ __forceinline__ void slot_create(const Dev& d, uint32_t g, uint32_t m, uint32_t k, uint64_t gid, uint32_t subj, uint64_t key,
+                            uint32_t pos) {
+  d.slot_gid[g] = gid;
+  d.slot_subj[g] = subj;
+  d.slot_ctick[g] = k;
+  d.slot_key[g] = key;
+  d.slot_exp[g] = k + d.EXPB;
+  d.slot_used[g] = 1;
+  const unsigned long long bit = 1ull << (g & 63u);
+  atomicOr(&d.GU[g >> 6], bit);
+  if (subj != USER_SUBJ && rec_status(key) == ST_DEAD) atomicOr(&d.DM[g >> 6], bit);
+  d.S[(size_t)g * d.N + m] = (k + 1u) & S_TICK_MASK;
+  atomicOr(&hrow(d, m)[g >> 6], bit);
+  ring(d, m)[pos & (d.BCAP - 1)] = rg_entry(g, rounds_before(d, m, k));
+  if (pos + 1u - d.rhead[m] > d.BCAP) set_err(d, E_RING);
+}
 
 // end of a sharded tick (W > 1): the same resets, plus the exchange counters (one block)
 __device__ __forceinline__ void tick_end(const Dev& d, uint32_t k) {
@@ -251,10 +278,7 @@ __device__ __forceinline__ void tick_end(const Dev& d, uint32_t k) {
     d.nmsg[nb] = 0;
     d.arena_used[nb] = 0;
     *d.pool_used = 0;
-    *d.nactive = 0;
-    *d.deliv_n = 0;
     *d.rc_n = 0;
-    d.deaths_n[(k + 1) & 1] = 0;
   }
 }
 
@@ -266,10 +290,7 @@ __device__ __forceinline__ void tick_flag(const Dev& d, uint32_t k) {
   d.nmsg[nb] = 0;
   d.arena_used[nb] = 0;
   *d.pool_used = 0;
-  *d.nactive = 0;
-  *d.deliv_n = 0;
   *d.rc_n = 0;
-  d.deaths_n[(k + 1) & 1] = 0;
   d.hflag[0] = (uint32_t)((int32_t)d.SPR - __hip_atomic_load(d.free_top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   __threadfence_system();
 }

@@ -29,7 +29,7 @@ constexpr uint32_t MQ = 16;   // inbound SYNC messages of one tick sorted in reg
 constexpr uint32_t SORT_MAX = 4096;  // receipts of one member and tick sorted in LDS at once (more: runs + merges)
 
 // S entry flags (gossip slot x member)
-constexpr uint32_t S_PENDING = 1u << 29, S_SWEPT = 1u << 30, S_REBORN = 1u << 31;
+constexpr uint32_t S_SWEPT = 1u << 30, S_REBORN = 1u << 31;
 constexpr uint32_t S_TICK_MASK = (1u << 29) - 1u;
 
 // device error bits
@@ -38,10 +38,10 @@ constexpr uint32_t E_SLOTS = 1, E_FETCH = 2, E_SUBS = 4, E_PATHS = 8, E_GROUPS =
                    E_REBORN = 4096, E_LOGWIN = 8192, E_EPOCH = 16384, E_EVENTS = 32768, E_SORTCAP = 65536,
                    E_XCAP = 1u << 17, E_LINKHIST = 1u << 18, E_DEATHS = 1u << 19,
                    E_INC = 1u << 20,  // an incarnation >= 2^30 would not fit the key plane (swim_common.h)
-                   E_PIN = 1u << 21;  // a later SYNC payload of a receiver's tick had no readable copy (pin)
+                   E_PIN = 1u << 21,  // a later SYNC payload of a receiver's tick had no readable copy (pin)
+                   E_RING = 1u << 22;  // a member held more gossips than its receipt ring (gossip_ring_cap)
 // per-link NetworkEmulator settings (setLinkSettings / block / unblock): hash of (src, dst) -> change history
 constexpr uint32_t LKCAP = 4096, LKH = 8;  // keys, history entries per key
-constexpr uint32_t DEATHCAP = 4096;        // completed leaves per tick
 constexpr uint32_t CIN_SLOW = 0xFFFFFFFEu;
 constexpr uint32_t MDU = 64;  // members with updated metadata per handle
 constexpr uint32_t CEV = 6, CEVW = 4 + 2 * CEV;  // cached contact events per (sender, target): n, oldest[2], events
@@ -141,31 +141,51 @@ struct Dev {
   uint64_t* slow;  // [SLOWCAP] (slot << 32 | m * F + s) sends deferred to k_gossip_send_slow
   uint32_t* slow_n;
   uint32_t SLOWCAP;
-  uint32_t *rlist, *rn;  // [N] members with a gossip round this tick (built by k_gossip_contacts)
   uint32_t* cin;    // [N][F] latest cached contact t -> m of (m, T[m][s]); NEVER: none, CIN_SLOW: list overflowed
-  uint32_t* swthr;  // [N] round sweep bound of this tick (k_round_info)
-  unsigned long long *HB, *WB;  // [N][QW] per member and 64-slot group (member-major): held past this tick / in a
-                                // round window
-  uint32_t QW;                  // words per member row of HB / WB = SLOTS / 64 + 1
-  unsigned long long *HBq, *WBq;  // [QW][N] the same masks group-major, as k_gossip_scan writes them
   uint64_t* rp;  // [RPCAP] (slot << 32 | m * F + s): sends of pairs with a cached contact, for k_gossip_replay
   uint32_t* rp_n;
   uint32_t RPCAP;
   uint32_t* cev;  // [N][F][CEVW] contact events of (m, T[m][s]) cached by k_gossip_contacts when tcontact is set
   uint32_t *log_tick, *log_spread, *log_cnt, *log_tg, *log_pos;  // [N][LOGW], tg [N][LOGW][F], pos [N]
 
+  // ---- holder state (gossip.hip) ----
+  // Bit planes indexed by slot id, member-major: HB = held (GossipProtocolImpl.gossips contains the id), kept up to
+  // date by every creation, first receipt and sweep; WB = inside the member's spread window as of its latest round
+  // (selectGossipsToSend :239-250), rebuilt incrementally at each of its rounds. QW = SLOTS / 64 words per row.
+  unsigned long long *HB, *WB;  // [N][QW]
+  uint32_t QW;
+  // The member's held gossips in receipt order: a ring of (slot | infection period & 1023 << 22) entries. The
+  // infection period (rounds before the receipt) never decreases along the ring, so the sweep (:283-308) removes a
+  // prefix and the window is a suffix; a round only walks the entries whose status changes.
+  uint32_t* rg;                                 // [N][BCAP]
+  uint32_t *rhead, *rwin, *rseen, *rtail;       // [N] positions: first held, first in WB, first not yet in WB, end
+  uint32_t BCAP;                                // ring entries per member (power of two)
+  uint32_t* rwl;                                // [N] round members whose ring needs work this tick
+  uint32_t* nrwl;
+  uint32_t *rsend, *rwnew;                      // [N] planned sweep end / window start (k_round_plan)
+  // groups of 64 slot ids with a slot in use (GU), and with a DEAD membership record (DM: first receipts of those
+  // stamp dead_rx); the active groups of a tick in ascending order
+  unsigned long long *GU, *DM;                  // [QW]
+  uint32_t *agroup, *nagroup;                   // [QW], [2] = count, span (last active group + 1)
+  // this tick's (sender, target) pairs by target: a target's senders are processed together, so first receipts
+  // are deduplicated without atomics (target-major send)
+  uint32_t *tin_cnt, *tin_off, *tin_fill, *tin;  // [N], [N], [N], [N * F] = m * F + s
+  uint32_t *tlist, *ntl;                         // targets with senders this tick
+  uint32_t* rt0;                                 // [N] a target's ring end before this tick's receipts
+  uint32_t EXPB;  // ticks after its latest creation or receipt by which every holder has swept a gossip (slot_exp)
+
   // ---- gossip slots ----
   uint64_t* slot_gid;
   uint32_t* slot_subj;
   uint32_t* slot_ctick;  // creation tick of the gossip (origin's spread)
   uint64_t* slot_key;  // inc | status<<32 (status may be DEAD)
-  int32_t* slot_holders;
+  uint32_t* slot_exp;  // tick from which no member holds the gossip any more: the slot is recycled (k_gossip_free)
   uint32_t* slot_used;
-  uint32_t* S;  // [SLOTS][N]
+  uint32_t* S;  // [SLOTS][N] creation tick + 1 | SWEPT | REBORN of each member's latest incarnation (replay, hashes)
   uint32_t* free_list;
   int32_t* free_top;
-  uint64_t* deliv;  // (slot << 32) | member
-  uint32_t* deliv_n;
+  uint64_t* xd;  // W > 1: (slot << 32) | target, this shard's first receipts of the tick (exchange B)
+  uint32_t* xd_n;
   // receipts produced at tick k, consumed in P4 of tick k+1
   uint64_t* rc_raw;  // (member << 32) | slot
   uint32_t* rc_n;
@@ -178,7 +198,8 @@ struct Dev {
   uint64_t* rc_key;   // [RCAP] gossip id sort key
   uint32_t* rc_slot2;  // [RCAP] merge scratch of k_seg_sort (segments above SORT_MAX)
   uint64_t* rc_key2;
-  uint32_t *active, *nactive;  // slots in use at the start of the gossip phase
+  uint32_t* fexp;   // [SLOTS] slots recycled at the end of this tick (k_gossip_free)
+  uint32_t* nfexp;
   uint64_t* hist;  // [HCAP][HREC] incarnation history: tag, gid, member | n << 32, HKEEP x u32 creation ticks
 
   // ---- SYNC messages (double-buffered by tick parity) ----
@@ -189,7 +210,6 @@ struct Dev {
   uint32_t* m_next; // [2][MSGCAP] next message of msgs[b] to the same destination
   uint32_t* m_head; // [2][N] first message of msgs[b] to each destination, NEVER if none (reset by the consumer)
   uint32_t* pending_inc; // [N] host requests for the next tick's P0: bits 2.. updateIncarnation calls, bit 1 leaveCluster
-  uint32_t *deaths, *deaths_n;  // [2][DEATHCAP], [2]: members whose leave completed at tick k (parity k & 1)
   uint32_t* next_evt; // [N] earliest tick at which a pending path / subscription / fetch needs the member
   uint32_t* mdone;  // finished k_member_tick blocks this tick (the last one runs the end-of-tick resets)
   uint32_t* trk;    // [NL][TRK] per receiver: subjects its row changed earlier in this tick's P1 (member.hip)
@@ -220,7 +240,7 @@ struct Dev {
   // at local index m - lo. Everything in the gossip plane (slots, S, round logs, hist) is replicated and kept
   // identical on every shard by applying the union of every shard's gossip records each tick.
   uint32_t W, rank, lo, hi, NL, SPR, MW;  // SPR: gossip slots owned per shard; MW: u64 words per chunk mask
-  uint32_t NSCAP, RRCAP, SWCAP, RQCAP, RXCAP, CHCAP;
+  uint32_t NSCAP, RRCAP, RQCAP, RXCAP, CHCAP;
   uint64_t XA_PEER, XB_PEER;  // bytes per peer region of the two exchange buffers
   uint64_t* rdirty;    // [NL][MW] per own observer: the 2048-record chunks of its key plane ever written with a key
                        // that differs from base_row (conservative: never cleared); a payload ships exactly these
@@ -229,7 +249,6 @@ struct Dev {
   uint32_t* xn;        // [8] 0 new slots, 1 round records, 2 sweeps, 4 inbound msgs (mtmp), 5 rx payloads
   uint32_t* ns_rec;    // [NSCAP][NSW] gossips created on this shard this tick
   uint32_t* rr_rec;    // [RRCAP][RRW] gossip rounds of this shard's members this tick
-  uint64_t* sw_rec;    // [SWCAP] (slot << 32 | member) sweeps by this shard's members this tick
   uint32_t* rq_n;      // [W] SYNC messages to each shard this tick
   uint32_t* rq_list;   // [W][RQCAP] their indices in msgs[b]
   uint64_t* rq_mask;   // [W * RQCAP][MW] chunks of the payload that differ from base_row
@@ -319,7 +338,6 @@ void launch_tick_c(const Dev& d, uint32_t k, void* stream, bool gossip);
 void launch_inline_out(const Dev& d, const uint8_t* send, uint64_t cap, const unsigned long long* scnt, void* stream);
 void launch_inline_in(const Dev& d, uint8_t* recv, uint64_t cap, const unsigned long long* scnt, unsigned long long* rcnt,
                       void* stream);
-void launch_kill(const Dev& d, uint32_t member, void* stream);
 void launch_user_gossips(const Dev& d, uint32_t k, const uint64_t* q, uint32_t n, void* stream);
 void launch_churn(const Dev& d, uint32_t k, void* stream);
 void launch_md_column(const Dev& d, uint32_t m, uint32_t u, void* stream);

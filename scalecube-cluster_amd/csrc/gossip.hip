@@ -1,0 +1,850 @@
+// gossip.hip — the gossip data plane: GossipProtocolImpl.doSpreadGossip (:139-157), selectGossipsToSend (:239-250),
+// onGossipReq (:171-183) and sweepGossips (:283-308) for every member at once.
+//
+// Holder state. Per member, the held gossips are a bit row HB over slot ids and a ring of (slot, infection period)
+// entries in receipt order. The infection period of an entry is the member's gossip period at its receipt
+// (GossipState.infectionPeriod), so it never decreases along the ring: a round's sweep (period > infP + 2(spread+1))
+// removes a prefix and the spread window (infP + spread >= period) is a suffix. The window bit row WB is rebuilt
+// at each of the member's rounds from the ring entries whose status changed since its previous round (swept, left
+// the window, re-entered it after the spread grew, or received since), so a round costs the entries it moves, not a
+// scan of the slot table.
+//
+// Target-major sends. All senders of one target in a tick are evaluated by the same lane for each 64-slot group:
+// the first receipts of the target are OR-ed in a register (no per-receipt atomics for deduplication), the sends are
+// counted by popcount, and the target's held bits and receipt ring are updated by the lane that owns them. Loss is
+// drawn per message only where the link is lossy (NetworkLinkSettings.evaluateLoss, SEMANTICS.md §2) and only for
+// messages that can still be a first receipt.
+//
+// infectedFrom. The reference keeps a set per (holder, gossip); here `y ∈ infectedFrom_x(g)` is recomputed only for
+// pairs with a logged contact (replay below). Slots are recycled at a bound after their latest creation or receipt
+// by which every holder has swept them (slot_exp), so no holder count is kept.
+#include "dev_util.h"
+
+namespace swim {
+
+// ------------------------------------------------------------------------------------------------------------
+// infectedFrom without storing it. `y ∈ infectedFrom_x(g)` at x's round at tick tau holds iff y delivered g to x by
+// a send in one of y's logged rounds t2 with c_x <= t2 + lat <= tau, where c_x is the creation tick of x's current
+// state for g. Whether such a send was delivered depends, one level down, on whether x had delivered g to y earlier
+// (then y skips x), and so on. The dependency only runs over the contact events between the pair (x's rounds that
+// targeted y, y's rounds that targeted x). Those are replayed in tick order as a small dynamic program.
+struct Contact {
+  uint32_t tick, slot, spread, dir;  // dir 0: y -> x, 1: x -> y
+};
+
+// incarnation history of (gid, member): creation ticks of swept incarnations (rebirths are rare)
+__device__ __forceinline__ uint64_t hist_tag(uint64_t gid, uint32_t member) {
+  return mix64(gid ^ ((uint64_t)member * 0x9E3779B97F4A7C15ull)) | 1ull;
+}
+
+__device__ void hist_push(const Dev& d, uint64_t gid, uint32_t member, uint32_t cprev) {
+  uint64_t tag = hist_tag(gid, member);
+  uint32_t mask = d.HCAP - 1;
+  for (uint32_t p = 0; p < d.HCAP; ++p) {
+    unsigned long long* e = (unsigned long long*)(d.hist + (size_t)((tag + p) & mask) * HREC);
+    unsigned long long old = atomicCAS(e, 0ull, (unsigned long long)tag);
+    if (old != 0ull && old != tag) continue;
+    if (old == 0ull) {
+      e[1] = gid;
+      e[2] = member;
+    }
+    uint32_t n = (uint32_t)(e[2] >> 32);  // total rebirths so far; the ring keeps the latest HKEEP
+    uint32_t* c = (uint32_t*)(e + 3);
+    c[n % HKEEP] = cprev;
+    e[2] = (uint64_t)member | ((uint64_t)(n + 1) << 32);
+    return;
+  }
+  if (atomicOr(d.err, E_REBORN) == 0) d.err[1] = 1;  // info 1: the history table is full (HCAP)
+}
+
+// creation tick of member's incarnation of g that existed at tick tau (NEVER if none)
+__device__ uint32_t inc_at(const Dev& d, uint32_t member, uint32_t g, uint64_t gid, uint32_t tau) {
+  uint32_t e = d.S[(size_t)g * d.N + member];
+  if (!s_ever(e)) return NEVER;
+  uint32_t c = s_ctick(e);
+  if (c <= tau) return c;
+  if (!(e & S_REBORN)) return NEVER;
+  uint64_t tag = hist_tag(gid, member);
+  uint32_t mask = d.HCAP - 1;
+  for (uint32_t p = 0; p < d.HCAP; ++p) {
+    const uint64_t* h = d.hist + (size_t)((tag + p) & mask) * HREC;
+    if (h[0] == 0) break;
+    if (h[0] != tag || h[1] != gid || (uint32_t)h[2] != member) continue;
+    uint32_t n = (uint32_t)(h[2] >> 32), best = NEVER, oldest = NEVER;
+    const uint32_t* cc = (const uint32_t*)(h + 3);
+    uint32_t kept = n < HKEEP ? n : HKEEP;
+    for (uint32_t i = 0; i < kept; ++i) {
+      if (cc[i] < oldest) oldest = cc[i];
+      if (cc[i] <= tau && (best == NEVER || cc[i] > best)) best = cc[i];
+    }
+    if (best == NEVER && n > HKEEP && tau < oldest && atomicOr(d.err, E_REBORN) == 0)
+      d.err[1] = 2;  // info 2: an incarnation the ring dropped (more than HKEEP rebirths)
+    return best;
+  }
+  return NEVER;
+}
+
+// Was x's incarnation of a gossip created at tick cs swept (sweepGossips :283-308) in one of x's rounds at ticks
+// [cs, t)? The window check alone is not enough: the spread is recomputed from the gossip list every round, so a
+// list that shrinks (members removed during a partition) and grows back reopens the window of a gossip already swept.
+// The ring holds every round in that range: the window at t bounds t - cs to ~spread rounds, LOGW >= 4 (spread + 2).
+// The ring is walked from the newest round back to cs (ring order is tick order), so the cost is the rounds since cs.
+// While x's spread has not changed since cs (spchg: tick of x's latest round whose spread differs from the round
+// before), the sweep condition is monotone in the round, so only the latest round before t needs a check.
+__device__ bool swept_before(const Dev& d, uint32_t x, uint32_t cs, uint32_t t) {
+  const uint32_t infP = rounds_before(d, x, cs);
+  const uint32_t pos = d.log_pos[x], n = min(pos, d.LOGW);
+  const bool steady = d.spchg[x] <= cs;
+  for (uint32_t e = 1; e <= n; ++e) {
+    const size_t li = (size_t)x * d.LOGW + (pos - e) % d.LOGW;
+    const uint32_t tr = d.log_tick[li];
+    if (tr == NEVER || tr >= t) continue;
+    if (tr < cs) break;
+    if (rounds_before(d, x, tr) > infP + sweep_after(d.log_spread[li])) return true;
+    if (steady) break;
+  }
+  return false;
+}
+
+// The replay over the sorted contact events of the pair (x, y) for gossip g (see the comment above Contact).
+// oldest[0]: oldest tick in y's log, oldest[1]: in x's log (0 if that ring never wrapped).
+template <uint32_t CM>
+__device__ __forceinline__ bool replay_pair(const Dev& d, uint32_t x, uint32_t y, uint32_t g, uint64_t gid,
+                                            uint32_t tau, uint32_t cx, const Contact* ev, uint32_t n,
+                                            const uint32_t* oldest) {
+  const uint32_t lat = d.lat;
+  // Find which deliveries can matter: into x from cx on (the answer), and into a sender from its incarnation start
+  // for every relevant event (its isInfected check). The fixpoint runs over at most CM events. The ring must cover
+  // those ranges.
+  uint32_t lo_in[2] = {cx, NEVER};  // [0]: deliveries into x, [1]: deliveries into y
+  uint32_t cinc[CM];
+  for (uint32_t i = 0; i < n; ++i) cinc[i] = NEVER - 1;  // not computed yet
+  for (int pass = 0; pass < 8; ++pass) {
+    bool changed = false;
+    for (int i = (int)n - 1; i >= 0; --i) {
+      const Contact& c = ev[i];
+      uint32_t rin = c.dir == 0 ? 0 : 1;  // receiver index into lo_in
+      if (lo_in[rin] == NEVER || c.tick + lat < lo_in[rin]) continue;
+      if (cinc[i] == NEVER - 1) cinc[i] = inc_at(d, c.dir == 0 ? y : x, g, gid, c.tick);
+      uint32_t cs = cinc[i];
+      uint32_t snd = c.dir == 0 ? y : x;
+      if (cs == NEVER || rounds_before(d, snd, cs) + c.spread < rounds_before(d, snd, c.tick)) continue;
+      if (swept_before(d, snd, cs, c.tick)) continue;
+      uint32_t sin = 1 - rin;
+      if (lo_in[sin] == NEVER || cs < lo_in[sin]) {
+        lo_in[sin] = cs;
+        changed = true;
+      }
+    }
+    if (!changed) break;
+  }
+  // deliveries into x come from y's log (oldest[0]); into y from x's log (oldest[1])
+  // (oldest 0: that ring never wrapped, so it holds every round since tick 0)
+  if ((lo_in[0] != NEVER && oldest[0] && lo_in[0] < oldest[0] + lat) ||
+      (lo_in[1] != NEVER && oldest[1] && lo_in[1] < oldest[1] + lat)) {
+    if (atomicOr(d.err, E_LOGWIN) == 0) {
+      d.err[1] = tau;
+      d.err[2] = lo_in[0];
+      d.err[3] = lo_in[1];
+      d.err[4] = oldest[0];
+      d.err[5] = oldest[1];
+    }
+  }
+  uint32_t del[2][CM];
+  uint32_t nd[2] = {0, 0};
+  for (uint32_t i = 0; i < n; ++i) {
+    const Contact& c = ev[i];
+    uint32_t snd = c.dir == 0 ? y : x;
+    // the sender held g at that round (its incarnation then), inside its spread window (selectGossipsToSend :246)
+    uint32_t cs = cinc[i] != NEVER - 1 ? cinc[i] : inc_at(d, snd, g, gid, c.tick);
+    if (cs == NEVER) continue;
+    if (rounds_before(d, snd, cs) + c.spread < rounds_before(d, snd, c.tick)) continue;
+    if (swept_before(d, snd, cs, c.tick)) continue;  // x no longer held it
+    // the receiver delivered g to the sender during that incarnation: infectedFrom (isInfected :247)
+    uint32_t od = 1 - c.dir;  // opposite direction
+    bool blocked = false;
+    for (uint32_t q = 0; q < nd[od] && !blocked; ++q) blocked = del[od][q] + lat >= cs && del[od][q] + lat <= c.tick;
+    if (blocked) continue;
+    if (lost_gossip(d, snd, c.dir == 0 ? x : y, c.tick, c.slot, gid)) continue;
+    del[c.dir][nd[c.dir]++] = c.tick;
+  }
+  for (uint32_t q = 0; q < nd[0]; ++q)
+    if (del[0][q] + lat >= cx) return true;
+  return false;
+}
+
+// contact events of the pair (x, y) in both logs up to tick tau - lat, in tick order; n = CM + 1 on overflow
+template <uint32_t CM>
+__device__ __forceinline__ uint32_t collect_contacts(const Dev& d, uint32_t x, uint32_t y, uint32_t tau, uint32_t born,
+                                                     Contact* ev, uint32_t* oldest) {
+  uint32_t n = 0;
+  for (int side = 0; side < 2; ++side) {
+    uint32_t from = side == 0 ? y : x, to = side == 0 ? x : y;
+    bool wrapped = d.log_pos[from] > d.LOGW;
+    uint32_t old = NEVER;
+    for (uint32_t e = 0; e < d.LOGW; ++e) {
+      size_t li = (size_t)from * d.LOGW + e;
+      uint32_t t2 = d.log_tick[li];
+      if (t2 == NEVER) continue;
+      if (t2 < old) old = t2;
+      if (t2 + d.lat > tau || t2 < born) continue;
+      uint32_t cnt = d.log_cnt[li];
+      for (uint32_t s2 = 0; s2 < cnt; ++s2)
+        if (d.log_tg[li * d.F + s2] == to) {
+          if (n == CM) return CM + 1;
+          uint32_t j = n++;
+          while (j > 0 && ev[j - 1].tick > t2) {
+            ev[j] = ev[j - 1];
+            --j;
+          }
+          ev[j] = Contact{t2, s2, d.log_spread[li], (uint32_t)side};
+        }
+    }
+    oldest[side] = wrapped ? old : 0;
+  }
+  return n;
+}
+
+// isInfected replay from a full scan of both logs (used when the cached contact list of the pair overflowed)
+__device__ __noinline__ bool blocked_pair(const Dev& d, uint32_t x, uint32_t y, uint32_t g, uint64_t gid,
+                                          uint32_t tau, uint32_t cx) {
+  constexpr uint32_t CMAX = 512;  // contact events between one pair inside the log window (small clusters: many)
+  Contact ev[CMAX];
+  uint32_t oldest[2];
+  const uint32_t n = collect_contacts<CMAX>(d, x, y, tau, d.slot_ctick[g], ev, oldest);
+  if (n > CMAX) {
+    atomicOr(d.err, E_CONTACTS);
+    return false;
+  }
+  return replay_pair<CMAX>(d, x, y, g, gid, tau, cx, ev, n, oldest);
+}
+
+// isInfected replay from the pair's contact list cached by k_gossip_contacts (gossip-independent; the creation
+// tick of g filters it: nobody could send g before it existed)
+__device__ __forceinline__ bool blocked_pair_cached(const Dev& d, uint32_t x, uint32_t y, uint32_t g, uint64_t gid,
+                                                    uint32_t tau, uint32_t cx, const uint32_t* rec) {
+  const uint32_t nall = rec[0];  // <= CEV: overflowed pairs go to k_gossip_send_slow
+  const uint32_t born = d.slot_ctick[g];
+  // only a delivery y -> x at or after x's incarnation start cx can put y in infectedFrom_x (most cached contacts
+  // are older than the gossip)
+  bool relevant = false;
+  for (uint32_t i = 0; i < nall; ++i) {
+    const uint32_t t2 = rec[4 + 2 * i];
+    relevant |= ((rec[5 + 2 * i] >> 8) & 1u) == 0 && t2 >= born && t2 + d.lat >= cx;
+  }
+  if (!relevant) return false;
+  Contact ev[CEV];
+  uint32_t n = 0;
+  for (uint32_t i = 0; i < nall; ++i) {
+    const uint32_t t2 = rec[4 + 2 * i], w = rec[5 + 2 * i];
+    if (t2 < born) continue;
+    ev[n++] = Contact{t2, w & 0xFFu, w >> 16, (w >> 8) & 1u};
+  }
+  const uint32_t oldest[2] = {rec[1], rec[2]};
+  return replay_pair<CEV>(d, x, y, g, gid, tau, cx, ev, n, oldest);
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// 1. the active 64-slot groups of this tick in ascending order (one block: a block-wide scan over the group words),
+// and the per-tick list counters
+__global__ void __launch_bounds__(1024) k_gossip_groups(Dev d) {
+  __shared__ uint32_t sh[1024];
+  __shared__ uint32_t base;
+  if (threadIdx.x == 0) {
+    base = 0;
+    *d.slow_n = *d.rp_n = *d.nrwl = *d.ntl = *d.xd_n = *d.nfexp = 0;
+  }
+  __syncthreads();
+  for (uint32_t q0 = 0; q0 < d.QW; q0 += 1024) {
+    const uint32_t q = q0 + threadIdx.x;
+    const uint32_t f = q < d.QW && d.GU[q] != 0ull ? 1u : 0u;
+    sh[threadIdx.x] = f;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {
+      const uint32_t v = threadIdx.x >= o ? sh[threadIdx.x - o] : 0u;
+      __syncthreads();
+      sh[threadIdx.x] += v;
+      __syncthreads();
+    }
+    if (f) d.agroup[base + sh[threadIdx.x] - 1] = q;
+    __syncthreads();
+    if (threadIdx.x == 0) base += sh[1023];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    d.nagroup[0] = base;
+    d.nagroup[1] = base ? d.agroup[base - 1] + 1 : 0;  // span of the holder rows touched this tick
+  }
+}
+
+// 2. per member with a gossip round this tick (every member on every shard: the holder state is replicated): where
+// its sweep ends and its window starts in the ring (binary searches: the infection periods are sorted), and whether
+// the round changes anything; the (sender, target) pairs of this shard's targets are counted per target
+__global__ void k_round_plan(Dev d, uint32_t k) {
+  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= d.N || !d.tround[m]) return;
+  const uint32_t cnt = d.tcnt[m];
+  for (uint32_t s = 0; s < cnt; ++s) {
+    const uint32_t t = d.T[(size_t)m * d.F + s];
+    if (t >= d.lo && t < d.hi) atomicAdd(&d.tin_cnt[t], 1u);
+  }
+  const uint32_t P = d.tperiod[m], sp = d.tspread[m];
+  const int64_t slo = (int64_t)P - (int64_t)sweep_after(sp), wlo = (int64_t)P - (int64_t)sp;
+  const uint32_t h = d.rhead[m], tl = d.rtail[m];
+  const uint32_t* R = ring(d, m);
+  const uint32_t mask = d.BCAP - 1;
+  uint32_t lo = 0, hi = tl - h;  // offsets from h
+  while (lo < hi) {  // first entry not swept: sweepGossips (:283-308) removes infP < P - 2 (spread + 1)
+    const uint32_t mid = lo + (hi - lo) / 2;
+    if (rg_period(R[(h + mid) & mask], P) < slo)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  const uint32_t send = h + lo;
+  hi = tl - h;
+  while (lo < hi) {  // first entry inside the window: selectGossipsToSend (:246) keeps infP + spread >= P
+    const uint32_t mid = lo + (hi - lo) / 2;
+    if (rg_period(R[(h + mid) & mask], P) < wlo)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  const uint32_t wnew = h + lo;
+  if (send != h || wnew != d.rwin[m] || d.rseen[m] != tl) {
+    d.rsend[m] = send;
+    d.rwnew[m] = wnew;
+    d.rwl[wave_append(d.nrwl)] = m;
+  }
+}
+
+// 3. senders of each target in one contiguous list (counting sort over this tick's pairs); the targets with senders;
+// each target's ring end before this tick's receipts
+__global__ void k_tin_scatter(Dev d) {
+  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= d.N || !d.tround[m]) return;
+  const uint32_t cnt = d.tcnt[m];
+  for (uint32_t s = 0; s < cnt; ++s) {
+    const uint32_t ms = m * d.F + s, t = d.T[ms];
+    if (t < d.lo || t >= d.hi) continue;
+    const uint32_t j = atomicAdd(&d.tin_fill[t], 1u);
+    d.tin[d.tin_off[t] + j] = ms;
+    if (j == 0) {
+      d.rt0[t] = d.rtail[t];
+      d.tlist[atomicAdd(d.ntl, 1u)] = t;
+    }
+  }
+}
+
+// 4. the rounds' holder-state changes (sweepGossips :283-308 and the window of selectGossipsToSend :239-250), one
+// workgroup per round member with work. Ring ranges (positions; see k_round_plan):
+//   [h, send)                      swept: HB cleared, S marked SWEPT, the gossip count drops
+//   [max(w0, h), min(seen, wnew))  out of the window: WB cleared (includes the swept entries that were in it)
+//   [wnew, max(w0, h))             back in the window (the spread grew): WB set
+//   [max(seen, wnew), tail)        received or created since the member's previous round: WB set
+// Few changes: one global atomic per entry. Many: the member's HB / WB rows are staged through LDS in chunks of
+// RCW words, so every word is read and written once per chunk.
+constexpr uint32_t RCW = 4096;
+__device__ __forceinline__ void rr_bits(const Dev& d, uint32_t m, uint32_t a, uint32_t b, uint32_t op,
+                                        unsigned long long* lh, unsigned long long* lw, uint32_t c0, uint32_t c1) {
+  const uint32_t* R = ring(d, m);
+  const uint32_t mask = d.BCAP - 1;
+  for (uint32_t p = a + threadIdx.x; p - a < b - a; p += blockDim.x) {
+    const uint32_t g = R[p & mask] & RG_SLOT, q = g >> 6;
+    const unsigned long long bit = 1ull << (g & 63u);
+    if (lh) {  // LDS chunk [c0, c1) of the rows
+      if (q < c0 || q >= c1) continue;
+      if (op == 0) atomicAnd(&lh[q - c0], ~bit);
+      else if (op == 1) atomicAnd(&lw[q - c0], ~bit);
+      else atomicOr(&lw[q - c0], bit);
+    } else {
+      if (op == 0) atomicAnd(&hrow(d, m)[q], ~bit);
+      else if (op == 1) atomicAnd(&wrow(d, m)[q], ~bit);
+      else atomicOr(&wrow(d, m)[q], bit);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_round_apply(const Dev* __restrict__ dp, uint32_t k) {
+  const Dev& d = *dp;
+  __shared__ unsigned long long lh[RCW], lw[RCW];
+  __shared__ uint32_t swept;
+  const uint32_t n = *d.nrwl, span = d.nagroup[1];
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const uint32_t m = d.rwl[i];
+    const uint32_t h = d.rhead[m], send = d.rsend[m], wnew = d.rwnew[m], tl = d.rtail[m], seen = d.rseen[m];
+    const uint32_t w0 = (int32_t)(d.rwin[m] - h) > 0 ? d.rwin[m] : h;
+    const uint32_t r2 = (int32_t)(seen - wnew) < 0 ? seen : wnew;  // min(seen, wnew)
+    const uint32_t r4 = (int32_t)(seen - wnew) > 0 ? seen : wnew;  // max(seen, wnew)
+    const uint32_t r3 = (int32_t)(w0 - wnew) > 0 ? w0 : wnew;      // end of the re-entry range
+    // side effects of the sweeps, once (sweepGossips :283-308; on_sweep: a completed leave)
+    if (threadIdx.x == 0) swept = 0;
+    __syncthreads();
+    {
+      const uint32_t* R = ring(d, m);
+      uint32_t c = 0;
+      for (uint32_t p = h + threadIdx.x; p - h < send - h; p += blockDim.x) {
+        const uint32_t g = R[p & (d.BCAP - 1)] & RG_SLOT;
+        d.S[(size_t)g * d.N + m] |= S_SWEPT;
+        on_sweep(d, g, m, k);
+        ++c;
+      }
+      if (c) atomicAdd(&swept, c);
+    }
+    const uint32_t nch = (send - h) + ((int32_t)(r2 - w0) > 0 ? r2 - w0 : 0u) + (r3 - wnew) + (tl - r4);
+    if (nch <= 512 || span == 0) {  // few changes: atomics on the rows
+      rr_bits(d, m, h, send, 0, nullptr, nullptr, 0, 0);
+      if ((int32_t)(r2 - w0) > 0) rr_bits(d, m, w0, r2, 1, nullptr, nullptr, 0, 0);
+      rr_bits(d, m, wnew, r3, 2, nullptr, nullptr, 0, 0);
+      rr_bits(d, m, r4, tl, 2, nullptr, nullptr, 0, 0);
+    } else {
+      for (uint32_t c0 = 0; c0 < span; c0 += RCW) {
+        const uint32_t c1 = min(span, c0 + RCW);
+        unsigned long long* H = hrow(d, m) + c0;
+        unsigned long long* Wr = wrow(d, m) + c0;
+        for (uint32_t j = threadIdx.x; j < c1 - c0; j += blockDim.x) {
+          lh[j] = H[j];
+          lw[j] = Wr[j];
+        }
+        __syncthreads();
+        rr_bits(d, m, h, send, 0, lh, lw, c0, c1);
+        if ((int32_t)(r2 - w0) > 0) rr_bits(d, m, w0, r2, 1, lh, lw, c0, c1);
+        rr_bits(d, m, wnew, r3, 2, lh, lw, c0, c1);
+        rr_bits(d, m, r4, tl, 2, lh, lw, c0, c1);
+        __syncthreads();
+        for (uint32_t j = threadIdx.x; j < c1 - c0; j += blockDim.x) {
+          H[j] = lh[j];
+          Wr[j] = lw[j];
+        }
+        __syncthreads();
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      d.rhead[m] = send;
+      d.rwin[m] = wnew;
+      d.rseen[m] = tl;
+      if (swept) {
+        if (d.XW > 1)
+          atomicSub(&d.held_delta[m], (int)swept);
+        else
+          atomicSub(&d.held[m], swept);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// 5. contact lists: did target t = T[m][s] choose m in a logged round inside the look-back window? If so, cache the
+// pair's contact events in both directions (independent of the gossip) for blocked_pair_cached. One thread per
+// (sender, target) pair of this shard's targets.
+__global__ void k_gossip_contacts(Dev d, uint32_t k) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t np = d.tin_off[d.N - 1] + d.tin_cnt[d.N - 1];  // exclusive scan: the total is the last offset + count
+  if (p >= np) return;
+  const uint32_t i = d.tin[p], m = i / d.F, t = d.T[i];
+  uint32_t flag = 0;
+  for (uint32_t e = 0; e < d.LOGW && !flag; ++e) {
+    size_t lo = (size_t)t * d.LOGW + e;
+    uint32_t t2 = d.log_tick[lo];
+    if (t2 == NEVER || t2 >= k) continue;
+    uint32_t n = d.log_cnt[lo];
+    for (uint32_t s2 = 0; s2 < n; ++s2)
+      if (d.log_tg[lo * d.F + s2] == m) flag = 1;
+  }
+  d.tcontact[i] = flag;
+  if (!flag) {
+    d.cin[i] = NEVER;
+    return;
+  }
+  Contact ev[CEV];
+  uint32_t oldest[2];
+  uint32_t* rec = d.cev + (size_t)i * CEVW;
+  uint32_t n = collect_contacts<CEV>(d, m, t, k, 0, ev, oldest);
+  if (n > d.cev_cap) n = CEV + 1;  // SWIM_CAPS: a smaller cache overflows into k_gossip_send_slow
+  rec[0] = n;
+  rec[1] = oldest[0];
+  rec[2] = oldest[1];
+  uint32_t last_in = NEVER;  // latest t -> m contact (NEVER: none); overflow is flagged by n alone
+  if (n <= CEV)
+    for (uint32_t j = 0; j < n; ++j) {
+      rec[4 + 2 * j] = ev[j].tick;
+      rec[5 + 2 * j] = ev[j].slot | (ev[j].dir << 8) | (ev[j].spread << 16);
+      if (ev[j].dir == 0) last_in = ev[j].tick;  // events are in tick order
+    }
+  rec[3] = last_in;
+  // a gossip inside m's window this round was created after tick k - (spread + 1) * gossip_t, so a contact t -> m
+  // at or before that tick - lat can never put t in infectedFrom_m of any gossip m sends now
+  const int64_t horizon = (int64_t)k - (int64_t)(d.tspread[m] + 1u) * d.gossip_t;
+  if (n > CEV)
+    d.cin[i] = CIN_SLOW;
+  else
+    d.cin[i] = last_in == NEVER || (int64_t)last_in + d.lat <= horizon ? NEVER : last_in;
+}
+
+// a first receipt of (g, t) at this tick (one lane owns it): the receiver-side bookkeeping that does not depend on
+// the other receipts of the tick happens at once (held bit, ring entry, DEAD-record stamp, exchange record)
+__device__ __forceinline__ void receipt_mark(const Dev& d, uint32_t g, uint32_t t, uint32_t k, uint32_t pos) {
+  ring(d, t)[pos & (d.BCAP - 1)] = rg_entry(g, rounds_before(d, t, k + d.lat));
+  if (pos + 1u - d.rhead[t] > d.BCAP) set_err(d, E_RING);
+}
+
+// 6. target-major sends (the fast path). Work item = (target t, active group q); the lanes of a wave take 64
+// consecutive items (64 groups of one target when there are that many). For each sender (m, s) of t: its window word
+// (sends = popcount), and the first-receipt candidates WB & ~HB[t] (t does not hold them past this tick: the rounds'
+// sweeps ran in k_round_apply), each surviving its loss draw (NetworkEmulator.tryFail, NetworkLinkSettings
+// .evaluateLoss: SEMANTICS.md §2). A receipt needs one surviving send from any sender; draws of candidates another
+// sender already delivered are skipped (they change nothing). Pairs with a cached contact go to k_gossip_replay and
+// pairs whose contact list overflowed to k_gossip_send_slow (isInfected, :247).
+__global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp, uint32_t k) {
+  const Dev& d = *dp;
+  __shared__ unsigned long long red[4];
+  const uint32_t nag = d.nagroup[0], ntl = *d.ntl;
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint64_t items = (uint64_t)ntl * nag;
+  const int ep = epoch_at(d, k);
+  unsigned long long sends = 0;
+  uint32_t st[4] = {0, 0, 0, 0};  // SWIM_EXP & 4: items with window bits, contact-path bits, -, candidates
+  for (uint64_t i0 = ((uint64_t)blockIdx.x * 4 + wave) * 64; i0 < items; i0 += (uint64_t)gridDim.x * 256) {
+    const uint64_t i = i0 + lane;
+    const bool act = i < items;
+    uint32_t t = NEVER, q = 0;
+    unsigned long long nb = 0, h = 0;
+    if (act) {
+      t = d.tlist[(uint32_t)(i / nag)];
+      q = d.agroup[(uint32_t)(i % nag)];
+      h = hrow(d, t)[q];
+      const uint32_t o = d.tin_off[t], ns = d.tin_cnt[t];
+      for (uint32_t p = 0; p < ns; ++p) {
+        const uint32_t ms = d.tin[o + p], m = ms / d.F, s = ms - m * d.F;
+        const unsigned long long w = wrow(d, m)[q];
+        if (!w) continue;
+        if (d.exp & 4) st[0]++;
+        const uint32_t ci = d.cin[ms];
+        if (ci != NEVER) {  // a logged contact: every slot of the pair is replayed (slow path past the cache)
+          const uint32_t c = (uint32_t)__popcll(w);
+          if (d.exp & 4) st[1] += c;
+          const bool slow = ci == CIN_SLOW;
+          fb_add(d, slow ? FB_CEV_SLOW : FB_REPLAY, c);
+          uint32_t j = atomicAdd(slow ? d.slow_n : d.rp_n, c);
+          for (unsigned long long b = w; b; b &= b - 1, ++j) {
+            const uint64_t v = ((uint64_t)(q * 64u + (uint32_t)(__ffsll((long long)b) - 1)) << 32) | ms;
+            if (j < (slow ? d.SLOWCAP : d.RPCAP))
+              (slow ? d.slow : d.rp)[j] = v;
+            else
+              set_err(d, E_CONTACTS);
+          }
+          continue;
+        }
+        sends += __popcll(w);
+        if (d.dbg_send) {  // debugging aid: every counted send
+          for (unsigned long long b = w; b; b &= b - 1) {
+            const uint32_t di = atomicAdd(d.dbg_send_n, 1u);
+            if (di >= d.dbg_send_cap) break;
+            const uint64_t gid = d.slot_gid[q * 64u + (uint32_t)(__ffsll((long long)b) - 1)];
+            uint32_t* r = d.dbg_send + (size_t)di * 5;
+            r[0] = k, r[1] = m, r[2] = (uint32_t)gid, r[3] = (uint32_t)(gid >> 32), r[4] = t;
+          }
+        }
+        const unsigned long long cand = w & ~h & ~nb;
+        if (!cand) continue;
+        if (d.exp & 4) st[3] += (uint32_t)__popcll(cand);
+        if (ep < 0) {
+          set_err(d, E_EPOCH);
+          continue;
+        }
+        const uint32_t pct = link_loss(d, ep, m, t, k);
+        if (pct == 0) {
+          nb |= cand;
+        } else if (pct < 100) {
+          for (unsigned long long b = cand; b; b &= b - 1) {
+            const uint32_t j = (uint32_t)(__ffsll((long long)b) - 1);
+            const uint64_t gid = d.slot_gid[q * 64u + j];
+            const u32x4 r = philox(m, k ^ ((s >> 2) << 31), (uint32_t)(gid >> 32), (uint32_t)gid,
+                                   d.seed_lo ^ SALT_LOSS_GOSSIP, d.seed_hi);  // lost_gossip_ep's draw
+            if (!(next_int(pick(r, s & 3), 100) < pct)) nb |= 1ull << j;
+          }
+        }
+      }
+    }
+    // the target's receipt ring: one reservation per run of lanes with the same target
+    const uint32_t c = (uint32_t)__popcll(nb);
+    uint32_t incl = c;
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+      const uint32_t v = __shfl_up(incl, o);
+      if (lane >= o) incl += v;
+    }
+    const uint32_t tp = __shfl_up(t, 1);
+    const unsigned long long heads = __ballot(lane == 0 || tp != t);
+    const uint32_t head = 63u - (uint32_t)__clzll(heads & ((2ull << lane) - 1ull));  // this lane's run head
+    const unsigned long long above = heads & ~((2ull << lane) - 1ull);
+    const uint32_t last = above ? (uint32_t)(__ffsll((long long)above) - 2) : 63u;  // the run's last lane
+    const uint32_t excl_head = __shfl(incl, (int)head) - __shfl(c, (int)head);
+    const uint32_t run_total = __shfl(incl, (int)last) - excl_head;
+    uint32_t base = 0;
+    if (lane == head && act && run_total) base = atomicAdd(&d.rtail[t], run_total);
+    base = __shfl(base, (int)head) + (incl - c - excl_head);
+    if (act && nb) {
+      hrow(d, t)[q] = h | nb;  // the lane owns (t, q) in this kernel: later receipts of the tick see it held
+      if (nb & d.DM[q]) d.dead_rx[t] = k + d.lat;  // a DEAD membership record arrives in P4 of k + lat
+      uint32_t pos = base;
+      for (unsigned long long b = nb; b; b &= b - 1, ++pos) {
+        const uint32_t g = q * 64u + (uint32_t)(__ffsll((long long)b) - 1);
+        receipt_mark(d, g, t, k, pos);
+        if (d.W > 1) {  // replicated on the other shards from exchange B
+          const uint32_t xi = atomicAdd(d.xd_n, 1u);
+          if (xi < d.DCAP)
+            d.xd[xi] = ((uint64_t)g << 32) | t;
+          else
+            set_err(d, E_DELIV);
+        }
+      }
+    }
+  }
+  if (d.exp & 4)
+    for (int q2 = 0; q2 < 4; ++q2)
+      if (st[q2]) atomicAdd(&d.ctr[8 + q2], (unsigned long long)st[q2]);
+  for (uint32_t o = 32; o > 0; o >>= 1) sends += __shfl_xor(sends, o);
+  if (lane == 0) red[wave] = sends;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long tot = red[0] + red[1] + red[2] + red[3];
+    if (tot) atomicAdd(&d.ctr[C_G], tot);
+  }
+}
+
+// one send of the replay / slow paths, after its isInfected check: a first receipt unless t holds g past this tick
+// (or received it already this tick: the held bit), subject to the loss draw; the held bit deduplicates by atomics
+__device__ __forceinline__ void deliver_one(const Dev& d, uint32_t g, uint32_t m, uint32_t s, uint32_t t, uint32_t k,
+                                            uint64_t gid, int ep) {
+  if (d.dbg_send) {
+    uint32_t di = atomicAdd(d.dbg_send_n, 1u);
+    if (di < d.dbg_send_cap) {
+      uint32_t* r = d.dbg_send + (size_t)di * 5;
+      r[0] = k, r[1] = m, r[2] = (uint32_t)gid, r[3] = (uint32_t)(gid >> 32), r[4] = t;
+    }
+  }
+  unsigned long long* hw = hrow(d, t) + (g >> 6);
+  const unsigned long long bit = 1ull << (g & 63u);
+  if (*hw & bit) return;
+  if (lost_gossip_ep(d, ep, m, t, k, s, gid)) return;
+  if (atomicOr(hw, bit) & bit) return;
+  if (d.DM[g >> 6] & bit) d.dead_rx[t] = k + d.lat;
+  receipt_mark(d, g, t, k, atomicAdd(&d.rtail[t], 1u));
+  if (d.W > 1) {
+    const uint32_t xi = atomicAdd(d.xd_n, 1u);
+    if (xi < d.DCAP)
+      d.xd[xi] = ((uint64_t)g << 32) | t;
+    else
+      set_err(d, E_DELIV);
+  }
+}
+
+// 7a. sends of pairs with a cached contact, one thread per (slot, sender, target): the isInfected replay runs only
+// where the contact can matter (t -> m at or after m's incarnation start and after the gossip existed), then the send
+__global__ void __launch_bounds__(256) k_gossip_replay(const Dev* __restrict__ dp, uint32_t k) {
+  const Dev& d = *dp;
+  __shared__ unsigned long long red[4];
+  const uint32_t n = min(*d.rp_n, d.RPCAP);
+  const int ep = epoch_at(d, k);
+  unsigned long long sends = 0;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint64_t v = d.rp[i];
+    const uint32_t g = (uint32_t)(v >> 32), ms = (uint32_t)v, m = ms / d.F, s = ms % d.F;
+    const uint32_t t = d.T[ms], c = s_ctick(d.S[(size_t)g * d.N + m]), ci = d.cin[ms];
+    const uint64_t gid = d.slot_gid[g];
+    if (ci >= d.slot_ctick[g] && ci + d.lat >= c && blocked_pair_cached(d, m, t, g, gid, k, c, d.cev + (size_t)ms * CEVW))
+      continue;
+    sends++;
+    deliver_one(d, g, m, s, t, k, gid, ep);
+  }
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  for (uint32_t o = 32; o > 0; o >>= 1) sends += __shfl_xor(sends, o);
+  if (lane == 0) red[wave] = sends;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long tot = red[0] + red[1] + red[2] + red[3];
+    if (tot) atomicAdd(&d.ctr[C_G], tot);
+  }
+}
+
+// 7b. sends whose pair had more contact events than the cache holds (small clusters): full log scan + replay
+__global__ void __launch_bounds__(64) k_gossip_send_slow(const Dev* __restrict__ dp, uint32_t k) {
+  const Dev& d = *dp;
+  const uint32_t n = min(*d.slow_n, d.SLOWCAP);
+  const int ep = epoch_at(d, k);
+  unsigned long long sends = 0;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint64_t v = d.slow[i];
+    const uint32_t g = (uint32_t)(v >> 32), ms = (uint32_t)v, m = ms / d.F, s = ms % d.F;
+    const uint32_t t = d.T[ms], c = s_ctick(d.S[(size_t)g * d.N + m]);
+    const uint64_t gid = d.slot_gid[g];
+    if (blocked_pair(d, m, t, g, gid, k, c)) continue;  // isInfected (:247)
+    sends++;
+    deliver_one(d, g, m, s, t, k, gid, ep);
+  }
+  if (sends) atomicAdd(&d.ctr[C_G], sends);
+}
+
+// P4 pre-filter (onMembershipGossip -> updateMembership, MembershipProtocolImpl.java:401-408,475-485). A first
+// receipt is routed to P4 of tick k4 unless it provably cannot change t's row there: its record does not override
+// the row as it stands now (= at the start of tick k4), the row is present, and the row cannot be removed before the
+// receipt in that tick. Present rows only move up the isOverrides order except through a removal, so a record that
+// does not override the start row overrides no later one. A removal needs a DEAD record: in P4 another receipt
+// (dead_rx[t] = k4, stamped by the delivering send), or in P1 a leaver's own record in SYNC data (leaving[subject]);
+// after one the row is absent or re-added at any incarnation (an absent row accepts any ALIVE,
+// MembershipRecord.java:67-69), so every receipt is kept then. An absent start row keeps every receipt (the row may
+// become present earlier in the tick). User gossips are always routed (each one emits a GOSSIP event).
+__device__ __forceinline__ bool receipt_matters(const Dev& d, uint32_t t, uint32_t g, uint32_t k4) {
+  const uint32_t subj = d.slot_subj[g];
+  if (subj == USER_SUBJ || (d.exp & 8)) return true;  // SWIM_EXP & 8: route every receipt (debugging aid)
+  const uint64_t key = d.slot_key[g];
+  const uint32_t r0 = d.rowk[lidx(d, t) * d.NS + subj], s1 = rec_status(key);
+  if ((r0 & 3u) == ST_ABSENT || overrides(s1, rec_inc(key), r0 & 3u, r0 >> 2)) return true;
+  return d.dead_rx[t] == k4 || d.leaving[subj];
+}
+
+// the holder-table entry of a first receipt (onGossipReq :176-180): the incarnation created at tick k + lat; a
+// rebirth after a sweep keeps the swept incarnation's creation tick in the history (infectedFrom replay)
+__device__ __forceinline__ void receipt_create(const Dev& d, uint32_t g, uint32_t t, uint32_t k) {
+  uint32_t* p = d.S + (size_t)g * d.N + t;
+  const uint32_t e = *p;
+  if (s_ever(e)) hist_push(d, d.slot_gid[g], t, s_ctick(e));
+  *p = ((k + d.lat + 1u) & S_TICK_MASK) | (s_ever(e) ? S_REBORN : 0u);
+  d.slot_exp[g] = k + d.lat + d.EXPB;  // every holder sweeps it by then (all receipts of a tick store the same value)
+}
+
+// 8. first receipts of this shard's targets, one wave per target: the entries its ring gained this tick. Holder
+// table, expiry, gossip count, then membership: records that can change the row are queued for P4 of k + lat in
+// gossip-id order (receipt routing), the others are counted as record compares; RUMOR mode hashes the GOSSIP events
+// here (fastp4). The senders' lists are reset for the next tick.
+__global__ void __launch_bounds__(256) k_gossip_apply(const Dev* __restrict__ dp, uint32_t k) {
+  const Dev& d = *dp;
+  const uint32_t lane = threadIdx.x & 63u, ntl = *d.ntl;
+  for (uint32_t ti = blockIdx.x * 4 + (threadIdx.x >> 6); ti < ntl; ti += gridDim.x * 4) {
+    const uint32_t t = d.tlist[ti], a = d.rt0[t], b = d.rtail[t];
+    const uint32_t* R = ring(d, t);
+    uint32_t drops = 0;
+    unsigned long long eh = 0;
+    for (uint32_t p = a + lane; p - a < b - a; p += 64) {
+      const uint32_t g = R[p & (d.BCAP - 1)] & RG_SLOT;
+      receipt_create(d, g, t, k);
+      if (d.fastp4 && d.slot_subj[g] == USER_SUBJ) {  // RUMOR mode: the GOSSIP event of P4 (k + lat), hashed now
+        const uint64_t gid = d.slot_gid[g], key = d.slot_key[g];
+        const uint64_t ev = ((uint64_t)(k + d.lat) << 32) | (3ull << 30) | (uint32_t)(gid >> 32);
+        const uint64_t meta = ((uint64_t)(uint32_t)key << 32) | (key >> 32);  // (oldMeta, newMeta) = payload (lo, hi)
+        eh += hpair(hpair(ev, meta), (uint32_t)gid);
+      } else if (!receipt_matters(d, t, g, k + d.lat)) {  // counted as a record compare in P4, nothing else
+        drops++;
+      } else {
+        const uint32_t ri = wave_append(d.rc_n);
+        if (ri < d.RCAP)
+          d.rc_raw[ri] = ((uint64_t)t << 32) | g;
+        else
+          set_err(d, E_RECEIPTS);
+      }
+    }
+    for (uint32_t o = 32; o > 0; o >>= 1) {
+      drops += __shfl_xor(drops, o);
+      const uint32_t lo = __shfl_xor((uint32_t)eh, o), hi = __shfl_xor((uint32_t)(eh >> 32), o);
+      eh += ((unsigned long long)hi << 32) | lo;
+    }
+    if (lane == 0) {
+      const uint32_t nr = b - a;
+      if (nr) {
+        if (d.XW > 1)
+          atomicAdd(&d.held_delta[t], (int)nr);
+        else
+          atomicAdd(&d.held[t], nr);
+      }
+      if (drops) atomicAdd(&d.rc_ndrop[t], drops);
+      if (d.fastp4 && nr) {
+        atomicAdd(&d.evp_hash[t], eh);
+        atomicAdd(&d.evp_n[t], nr);
+      }
+      d.tin_cnt[t] = 0;
+      d.tin_fill[t] = 0;
+    }
+  }
+}
+
+// 9. slots every holder has swept (slot_exp): nobody can send them again. Pass 1 lists them and clears their
+// group bits; pass 2 clears each one's holder-table row (a block per slot) and returns it to its owner shard's free list.
+__global__ void k_gossip_expire(Dev d, uint32_t k) {
+  const uint32_t nag = d.nagroup[0];
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nag * 64u) return;
+  const uint32_t q = d.agroup[i >> 6], g = q * 64u + (i & 63u);
+  if (!((d.GU[q] >> (g & 63u)) & 1ull) || d.slot_exp[g] > k) return;
+  const unsigned long long bit = 1ull << (g & 63u);
+  atomicAnd(&d.GU[q], ~bit);
+  atomicAnd(&d.DM[q], ~bit);
+  d.fexp[wave_append(d.nfexp)] = g;
+}
+__global__ void __launch_bounds__(256) k_gossip_free(Dev d) {
+  const uint32_t n = *d.nfexp;
+  for (uint32_t a = blockIdx.x; a < n; a += gridDim.x) {
+    const uint32_t g = d.fexp[a];
+    uint32_t* Sg = d.S + (size_t)g * d.N;
+    for (uint32_t s = threadIdx.x; s < d.N; s += blockDim.x) Sg[s] = 0;
+    if (threadIdx.x == 0) {
+      d.slot_used[g] = 0;
+      if (g / d.SPR == d.rank) d.free_list[atomicAdd(d.free_top, 1)] = g;  // back to the owning shard's free list
+    }
+  }
+}
+
+// W > 1: peers' first receipts into this shard's replicated holder state (the owning shard did the membership part)
+__global__ void k_unpack_b(Dev d, uint32_t k) {
+  const uint32_t p = blockIdx.y;
+  if (p == d.rank || (d.xb_rcnt[p] & XCNT_MASK) < 16) return;
+  const uint8_t* R = d.xb_recv + (size_t)p * d.XB_PEER;
+  const uint32_t nd = ((const uint32_t*)R)[0];
+  const uint64_t* V = (const uint64_t*)(R + 16);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nd; i += gridDim.x * blockDim.x) {
+    const uint32_t g = (uint32_t)(V[i] >> 32), t = (uint32_t)V[i];
+    atomicOr(&hrow(d, t)[g >> 6], 1ull << (g & 63u));
+    receipt_mark(d, g, t, k, atomicAdd(&d.rtail[t], 1u));
+    receipt_create(d, g, t, k);
+    atomicAdd(&d.held[t], 1u);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// host launchers
+static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+void launch_scan(const uint32_t* in, uint32_t* out, uint32_t* part, uint32_t n, hipStream_t st);  // kernels.hip
+void launch_receipt_routing(const Dev& d, hipStream_t st);                                         // kernels.hip
+
+constexpr uint32_t SEND_GRID = 4096;  // 16 blocks per CU, grid-stride
+
+// the sends of this tick and the holder-state changes they need, up to the first receipts (the sharded tick
+// exchanges them before launch_gossip_apply)
+void launch_gossip_send(const Dev& d, uint32_t k, hipStream_t st, const TickEvents* prof) {
+  hipLaunchKernelGGL(k_gossip_groups, dim3(1), dim3(1024), 0, st, d);
+  hipLaunchKernelGGL(k_round_plan, dim3(cdiv(d.N, 256)), dim3(256), 0, st, d, k);
+  launch_scan(d.tin_cnt, d.tin_off, d.scan_part, d.N, st);
+  hipLaunchKernelGGL(k_tin_scatter, dim3(cdiv(d.N, 256)), dim3(256), 0, st, d);
+  hipLaunchKernelGGL(k_round_apply, dim3(4096), dim3(256), 0, st, d.self, k);
+  hipLaunchKernelGGL(k_gossip_contacts, dim3(cdiv((uint64_t)d.N * d.F, 256)), dim3(256), 0, st, d, k);
+  if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[4], st);
+  hipLaunchKernelGGL(k_gossip_send, dim3(SEND_GRID), dim3(256), 0, st, d.self, k);
+  hipLaunchKernelGGL(k_gossip_send_slow, dim3(64), dim3(64), 0, st, d.self, k);  // rare; ~14 KB of stack per lane
+  hipLaunchKernelGGL(k_gossip_replay, dim3(2048), dim3(256), 0, st, d.self, k);
+  if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[5], st);
+}
+
+// the receivers' side of this tick's first receipts, P4 routing and slot recycling
+void launch_gossip_apply(const Dev& d, uint32_t k, hipStream_t st) {
+  hipLaunchKernelGGL(k_gossip_apply, dim3(2048), dim3(256), 0, st, d.self, k);
+  launch_receipt_routing(d, st);
+  hipLaunchKernelGGL(k_gossip_expire, dim3(cdiv((uint64_t)d.QW * 64, 256)), dim3(256), 0, st, d, k);
+  hipLaunchKernelGGL(k_gossip_free, dim3(1024), dim3(256), 0, st, d);
+}
+
+void launch_unpack_b(const Dev& d, uint32_t k, hipStream_t st) {
+  hipLaunchKernelGGL(k_unpack_b, dim3(64, d.W), dim3(256), 0, st, d, k);
+}
+
+}  // namespace swim

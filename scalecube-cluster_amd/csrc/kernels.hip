@@ -1,4 +1,5 @@
-// kernels.hip — initialisation, message routing, the SYNC-payload diff, the gossip data plane, kill and state hashes.
+// kernels.hip — initialisation, receipt routing, the SYNC-payload diff, state hashes and the tick launchers (the
+// gossip data plane is in gossip.hip).
 #include <hip/hip_runtime.h>
 
 #include "dev_util.h"
@@ -12,8 +13,6 @@ __global__ void k_pack_a(Dev d, uint32_t b);
 __global__ void k_pack_a_chunks(Dev d, uint32_t b);
 __global__ void k_unpack_a(Dev d, uint32_t k, uint32_t end);
 __global__ void k_pack_b(Dev d);
-__global__ void k_unpack_b_sweeps(Dev d, uint32_t k);
-__global__ void k_unpack_b_deliv(Dev d, uint32_t k);
 __global__ void k_round_reset(Dev d);
 
 // ------------------------------------------------------------------------------------------------------------
@@ -60,6 +59,8 @@ __global__ void k_init_members(Dev d) {
   d.m_head[m] = d.m_head[d.N + m] = NEVER;
   d.next_evt[m] = NEVER;
   d.pending_inc[m] = 0;
+  d.rhead[m] = d.rwin[m] = d.rseen[m] = d.rtail[m] = 0;  // empty receipt ring (gossip.hip)
+  d.tin_cnt[m] = d.tin_fill[m] = 0;
   if (m >= d.lo && m < d.hi)
     for (uint32_t g = 0; g < d.GRCAP; ++g) d.groups[(lidx(d, m) * d.GRCAP + g) * GREC + 5] = 0;
   for (uint32_t e = 0; e < d.LOGW; ++e) d.log_tick[(size_t)m * d.LOGW + e] = NEVER;
@@ -105,7 +106,7 @@ __global__ void k_init_slots(Dev d) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= d.SLOTS) return;
   d.slot_used[g] = 0;
-  d.slot_holders[g] = 0;
+  d.slot_exp[g] = NEVER;
   // each shard allocates only from its own slot range [rank SPR, (rank+1) SPR), so slot ids are global
   if (g < d.SPR) d.free_list[g] = d.rank * d.SPR + d.SPR - 1 - g;
 }
@@ -408,735 +409,6 @@ __global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b, uint32_t t
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// gossip data plane (GossipProtocolImpl.java:139-308 for all members at once)
-//
-// infectedFrom is never stored. `y ∈ infectedFrom_x(g)` at x's round at tick tau holds iff y delivered g to x by a
-// send in one of y's logged rounds t2 with c_x <= t2 + lat <= tau, where c_x is the creation tick of x's current
-// state for g. Whether such a send was delivered depends, one level down, on whether x had delivered g to y
-// earlier (then y skips x), and so on. The dependency only runs over the contact events between the pair
-// (x's rounds that targeted y, y's rounds that targeted x). Those are replayed in tick order as a small dynamic
-// program, so there is no recursion.
-struct Contact {
-  uint32_t tick, slot, spread, dir;  // dir 0: y -> x, 1: x -> y
-};
-
-// incarnation history of (gid, member): creation ticks of swept incarnations (rebirths are rare)
-__device__ __forceinline__ uint64_t hist_tag(uint64_t gid, uint32_t member) {
-  return mix64(gid ^ ((uint64_t)member * 0x9E3779B97F4A7C15ull)) | 1ull;
-}
-
-__device__ void hist_push(const Dev& d, uint64_t gid, uint32_t member, uint32_t cprev) {
-  uint64_t tag = hist_tag(gid, member);
-  uint32_t mask = d.HCAP - 1;
-  for (uint32_t p = 0; p < d.HCAP; ++p) {
-    unsigned long long* e = (unsigned long long*)(d.hist + (size_t)((tag + p) & mask) * HREC);
-    unsigned long long old = atomicCAS(e, 0ull, (unsigned long long)tag);
-    if (old != 0ull && old != tag) continue;
-    if (old == 0ull) {
-      e[1] = gid;
-      e[2] = member;
-    }
-    uint32_t n = (uint32_t)(e[2] >> 32);  // total rebirths so far; the ring keeps the latest 6
-    uint32_t* c = (uint32_t*)(e + 3);
-    c[n % HKEEP] = cprev;
-    e[2] = (uint64_t)member | ((uint64_t)(n + 1) << 32);
-    return;
-  }
-  if (atomicOr(d.err, E_REBORN) == 0) d.err[1] = 1;  // info 1: the history table is full (HCAP)
-}
-
-// creation tick of member's incarnation of g that existed at tick tau (NEVER if none)
-__device__ uint32_t inc_at(const Dev& d, uint32_t member, uint32_t g, uint64_t gid, uint32_t tau) {
-  uint32_t e = d.S[(size_t)g * d.N + member];
-  if (!s_ever(e)) return NEVER;
-  uint32_t c = s_ctick(e);
-  if (c <= tau) return c;
-  if (!(e & S_REBORN)) return NEVER;
-  uint64_t tag = hist_tag(gid, member);
-  uint32_t mask = d.HCAP - 1;
-  for (uint32_t p = 0; p < d.HCAP; ++p) {
-    const uint64_t* h = d.hist + (size_t)((tag + p) & mask) * HREC;
-    if (h[0] == 0) break;
-    if (h[0] != tag || h[1] != gid || (uint32_t)h[2] != member) continue;
-    uint32_t n = (uint32_t)(h[2] >> 32), best = NEVER, oldest = NEVER;
-    const uint32_t* cc = (const uint32_t*)(h + 3);
-    uint32_t kept = n < HKEEP ? n : HKEEP;
-    for (uint32_t i = 0; i < kept; ++i) {
-      if (cc[i] < oldest) oldest = cc[i];
-      if (cc[i] <= tau && (best == NEVER || cc[i] > best)) best = cc[i];
-    }
-    if (best == NEVER && n > HKEEP && tau < oldest && atomicOr(d.err, E_REBORN) == 0)
-      d.err[1] = 2;  // info 2: an incarnation the ring dropped (more than HKEEP rebirths)
-    return best;
-  }
-  return NEVER;
-}
-
-// Was x's incarnation of a gossip created at tick cs swept (sweepGossips :283-308) in one of x's rounds at ticks
-// [cs, t)? The window check alone is not enough: the spread is recomputed from the gossip list every round, so a
-// list that shrinks (members removed during a partition) and grows back reopens the window of a gossip already swept.
-// The ring holds every round in that range: the window at t bounds t - cs to ~spread rounds, LOGW >= 4 (spread + 2).
-// The ring is walked from the newest round back to cs (ring order is tick order), so the cost is the rounds since cs.
-// While x's spread has not changed since cs (spchg: tick of x's latest round whose spread differs from the round
-// before), the sweep condition is monotone in the round, so only the latest round before t needs a check.
-__device__ bool swept_before(const Dev& d, uint32_t x, uint32_t cs, uint32_t t) {
-  const uint32_t infP = rounds_before(d, x, cs);
-  const uint32_t pos = d.log_pos[x], n = min(pos, d.LOGW);
-  const bool steady = d.spchg[x] <= cs;
-  for (uint32_t e = 1; e <= n; ++e) {
-    const size_t li = (size_t)x * d.LOGW + (pos - e) % d.LOGW;
-    const uint32_t tr = d.log_tick[li];
-    if (tr == NEVER || tr >= t) continue;
-    if (tr < cs) break;
-    if (rounds_before(d, x, tr) > infP + sweep_after(d.log_spread[li])) return true;
-    if (steady) break;
-  }
-  return false;
-}
-
-// The replay over the sorted contact events of the pair (x, y) for gossip g (see the comment above Contact).
-// oldest[0]: oldest tick in y's log, oldest[1]: in x's log (0 if that ring never wrapped).
-template <uint32_t CM>
-__device__ __forceinline__ bool replay_pair(const Dev& d, uint32_t x, uint32_t y, uint32_t g, uint64_t gid,
-                                            uint32_t tau, uint32_t cx, const Contact* ev, uint32_t n,
-                                            const uint32_t* oldest) {
-  const uint32_t lat = d.lat;
-  // Find which deliveries can matter: into x from cx on (the answer), and into a sender from its incarnation start
-  // for every relevant event (its isInfected check). The fixpoint runs over at most CM events. The ring must cover
-  // those ranges.
-  uint32_t lo_in[2] = {cx, NEVER};  // [0]: deliveries into x, [1]: deliveries into y
-  uint32_t cinc[CM];
-  for (uint32_t i = 0; i < n; ++i) cinc[i] = NEVER - 1;  // not computed yet
-  for (int pass = 0; pass < 8; ++pass) {
-    bool changed = false;
-    for (int i = (int)n - 1; i >= 0; --i) {
-      const Contact& c = ev[i];
-      uint32_t rin = c.dir == 0 ? 0 : 1;  // receiver index into lo_in
-      if (lo_in[rin] == NEVER || c.tick + lat < lo_in[rin]) continue;
-      if (cinc[i] == NEVER - 1) cinc[i] = inc_at(d, c.dir == 0 ? y : x, g, gid, c.tick);
-      uint32_t cs = cinc[i];
-      uint32_t snd = c.dir == 0 ? y : x;
-      if (cs == NEVER || rounds_before(d, snd, cs) + c.spread < rounds_before(d, snd, c.tick)) continue;
-      if (swept_before(d, snd, cs, c.tick)) continue;
-      uint32_t sin = 1 - rin;
-      if (lo_in[sin] == NEVER || cs < lo_in[sin]) {
-        lo_in[sin] = cs;
-        changed = true;
-      }
-    }
-    if (!changed) break;
-  }
-  // deliveries into x come from y's log (oldest[0]); into y from x's log (oldest[1])
-  // (oldest 0: that ring never wrapped, so it holds every round since tick 0)
-  if ((lo_in[0] != NEVER && oldest[0] && lo_in[0] < oldest[0] + lat) ||
-      (lo_in[1] != NEVER && oldest[1] && lo_in[1] < oldest[1] + lat)) {
-    if (atomicOr(d.err, E_LOGWIN) == 0) {
-      d.err[1] = tau;
-      d.err[2] = lo_in[0];
-      d.err[3] = lo_in[1];
-      d.err[4] = oldest[0];
-      d.err[5] = oldest[1];
-    }
-  }
-  uint32_t del[2][CM];
-  uint32_t nd[2] = {0, 0};
-  for (uint32_t i = 0; i < n; ++i) {
-    const Contact& c = ev[i];
-    uint32_t snd = c.dir == 0 ? y : x;
-    // the sender held g at that round (its incarnation then), inside its spread window (selectGossipsToSend :246)
-    uint32_t cs = cinc[i] != NEVER - 1 ? cinc[i] : inc_at(d, snd, g, gid, c.tick);
-    if (cs == NEVER) continue;
-    if (rounds_before(d, snd, cs) + c.spread < rounds_before(d, snd, c.tick)) continue;
-    if (swept_before(d, snd, cs, c.tick)) continue;  // x no longer held it
-    // the receiver delivered g to the sender during that incarnation: infectedFrom (isInfected :247)
-    uint32_t od = 1 - c.dir;  // opposite direction
-    bool blocked = false;
-    for (uint32_t q = 0; q < nd[od] && !blocked; ++q) blocked = del[od][q] + lat >= cs && del[od][q] + lat <= c.tick;
-    if (blocked) continue;
-    if (lost_gossip(d, snd, c.dir == 0 ? x : y, c.tick, c.slot, gid)) continue;
-    del[c.dir][nd[c.dir]++] = c.tick;
-  }
-  for (uint32_t q = 0; q < nd[0]; ++q)
-    if (del[0][q] + lat >= cx) return true;
-  return false;
-}
-
-// contact events of the pair (x, y) in both logs up to tick tau - lat, in tick order; n = CM + 1 on overflow
-template <uint32_t CM>
-__device__ __forceinline__ uint32_t collect_contacts(const Dev& d, uint32_t x, uint32_t y, uint32_t tau, uint32_t born,
-                                                     Contact* ev, uint32_t* oldest) {
-  uint32_t n = 0;
-  for (int side = 0; side < 2; ++side) {
-    uint32_t from = side == 0 ? y : x, to = side == 0 ? x : y;
-    bool wrapped = d.log_pos[from] > d.LOGW;
-    uint32_t old = NEVER;
-    for (uint32_t e = 0; e < d.LOGW; ++e) {
-      size_t li = (size_t)from * d.LOGW + e;
-      uint32_t t2 = d.log_tick[li];
-      if (t2 == NEVER) continue;
-      if (t2 < old) old = t2;
-      if (t2 + d.lat > tau || t2 < born) continue;
-      uint32_t cnt = d.log_cnt[li];
-      for (uint32_t s2 = 0; s2 < cnt; ++s2)
-        if (d.log_tg[li * d.F + s2] == to) {
-          if (n == CM) return CM + 1;
-          uint32_t j = n++;
-          while (j > 0 && ev[j - 1].tick > t2) {
-            ev[j] = ev[j - 1];
-            --j;
-          }
-          ev[j] = Contact{t2, s2, d.log_spread[li], (uint32_t)side};
-        }
-    }
-    oldest[side] = wrapped ? old : 0;
-  }
-  return n;
-}
-
-// isInfected replay from a full scan of both logs (used when the cached contact list of the pair overflowed)
-__device__ __noinline__ bool blocked_pair(const Dev& d, uint32_t x, uint32_t y, uint32_t g, uint64_t gid,
-                                          uint32_t tau, uint32_t cx) {
-  constexpr uint32_t CMAX = 512;  // contact events between one pair inside the log window (small clusters: many)
-  Contact ev[CMAX];
-  uint32_t oldest[2];
-  const uint32_t n = collect_contacts<CMAX>(d, x, y, tau, d.slot_ctick[g], ev, oldest);
-  if (n > CMAX) {
-    atomicOr(d.err, E_CONTACTS);
-    return false;
-  }
-  return replay_pair<CMAX>(d, x, y, g, gid, tau, cx, ev, n, oldest);
-}
-
-// isInfected replay from the pair's contact list cached by k_gossip_contacts (gossip-independent; the creation
-// tick of g filters it: nobody could send g before it existed)
-__device__ __forceinline__ bool blocked_pair_cached(const Dev& d, uint32_t x, uint32_t y, uint32_t g, uint64_t gid,
-                                                    uint32_t tau, uint32_t cx, const uint32_t* rec) {
-  const uint32_t nall = rec[0];  // <= CEV: overflowed pairs go to k_gossip_send_slow
-  const uint32_t born = d.slot_ctick[g];
-  // only a delivery y -> x at or after x's incarnation start cx can put y in infectedFrom_x (most cached contacts
-  // are older than the gossip)
-  bool relevant = false;
-  for (uint32_t i = 0; i < nall; ++i) {
-    const uint32_t t2 = rec[4 + 2 * i];
-    relevant |= ((rec[5 + 2 * i] >> 8) & 1u) == 0 && t2 >= born && t2 + d.lat >= cx;
-  }
-  if (!relevant) return false;
-  Contact ev[CEV];
-  uint32_t n = 0;
-  for (uint32_t i = 0; i < nall; ++i) {
-    const uint32_t t2 = rec[4 + 2 * i], w = rec[5 + 2 * i];
-    if (t2 < born) continue;
-    ev[n++] = Contact{t2, w & 0xFFu, w >> 16, (w >> 8) & 1u};
-  }
-  const uint32_t oldest[2] = {rec[1], rec[2]};
-  return replay_pair<CEV>(d, x, y, g, gid, tau, cx, ev, n, oldest);
-}
-
-__global__ void k_gossip_active(Dev d, uint32_t k, uint32_t* active, uint32_t* nactive) {
-  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g == 0) *d.slow_n = *d.rn = *d.rp_n = 0;  // deferred sends, round members and replays of this tick
-  if (g >= d.SLOTS || !d.slot_used[g]) return;
-  // members stopped after their leave completed at tick k - 1 hold nothing any more (as k_kill)
-  const uint32_t pb = (k - 1) & 1u, nd = k > 0 ? min(d.deaths_n[pb], DEATHCAP) : 0u;
-  for (uint32_t i = 0; i < nd; ++i)
-    if (s_held(d.S[(size_t)g * d.N + d.deaths[(size_t)pb * DEATHCAP + i]])) atomicSub(&d.slot_holders[g], 1);
-  active[atomicAdd(nactive, 1u)] = g;
-}
-
-// per member (all N, every shard): swthr = creation-tick bound of the gossips it sweeps in its round this tick
-// (sweepGossips :283-308): sweeps g iff rounds_before(c) < P = period - 2 (spread + 1) iff c < swthr; 0 = sweeps none
-__global__ void k_round_info(Dev d) {
-  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= d.N) return;
-  uint32_t thr = 0;
-  if (d.tround[m]) {
-    const int64_t P = (int64_t)d.tperiod[m] - (int64_t)sweep_after(d.tspread[m]);
-    const uint32_t f = d.firstGossip[m];
-    if (P >= 1) thr = f == NEVER ? NEVER : (uint32_t)min<int64_t>((int64_t)NEVER, (int64_t)f + (P - 1) * d.gossip_t + 1);
-  }
-  d.swthr[m] = thr;
-}
-
-// contact lists: did target t = T[m][s] choose m in a logged round inside the look-back window? If so, cache the
-// pair's contact events in both directions (independent of the gossip) for blocked_pair_cached
-__global__ void k_gossip_contacts(Dev d, uint32_t k) {
-  uint32_t i = d.lo * d.F + blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= d.hi * d.F) return;
-  uint32_t m = i / d.F, s = i % d.F;
-  uint32_t flag = 0;
-  if (d.tround[m] && s < d.tcnt[m]) {
-    uint32_t t = d.T[i];
-    for (uint32_t e = 0; e < d.LOGW && !flag; ++e) {
-      size_t lo = (size_t)t * d.LOGW + e;
-      uint32_t t2 = d.log_tick[lo];
-      if (t2 == NEVER || t2 >= k) continue;
-      uint32_t n = d.log_cnt[lo];
-      for (uint32_t s2 = 0; s2 < n; ++s2)
-        if (d.log_tg[lo * d.F + s2] == m) flag = 1;
-    }
-    if (flag) {
-      Contact ev[CEV];
-      uint32_t oldest[2];
-      uint32_t* rec = d.cev + (size_t)i * CEVW;
-      uint32_t n = collect_contacts<CEV>(d, m, t, k, 0, ev, oldest);
-      if (n > d.cev_cap) n = CEV + 1;  // SWIM_CAPS: a smaller cache overflows into k_gossip_send_slow
-      rec[0] = n;
-      rec[1] = oldest[0];
-      rec[2] = oldest[1];
-      uint32_t last_in = NEVER;  // latest y -> x contact (NEVER: none); overflow is flagged by n alone
-      if (n <= CEV)
-        for (uint32_t j = 0; j < n; ++j) {
-          rec[4 + 2 * j] = ev[j].tick;
-          rec[5 + 2 * j] = ev[j].slot | (ev[j].dir << 8) | (ev[j].spread << 16);
-          if (ev[j].dir == 0) last_in = ev[j].tick;  // events are in tick order
-        }
-      rec[3] = last_in;
-      // a gossip inside m's window this round was created after tick k - (spread + 1) * gossip_t, so a contact
-      // t -> m at or before that tick - lat can never put t in infectedFrom_m of any gossip m sends now
-      const int64_t horizon = (int64_t)k - (int64_t)(d.tspread[m] + 1u) * d.gossip_t;
-      if (n > CEV)
-        d.cin[i] = CIN_SLOW;
-      else
-        d.cin[i] = last_in == NEVER || (int64_t)last_in + d.lat <= horizon ? NEVER : last_in;
-    }
-  }
-  d.tcontact[i] = flag;
-  if (!flag) d.cin[i] = NEVER;
-  if (s == 0 && d.tround[m]) {  // compact list of this tick's round members (k_gossip_send iterates over it)
-    uint32_t r = wave_append(d.rn);
-    d.rlist[r] = m;
-  }
-}
-
-// one counted send of gossip g from m to its round target t = T[m][s] (isInfected already checked): the receipt is
-// potential unless t holds g past this tick; a loss draw, then the first sender of (g, t) queues the delivery
-// potential: the caller already knows t does not hold g past this tick (k_gossip_send's candidates come from
-// WB & ~HB[t], and HB is exactly that test: nothing changes S between k_gossip_scan and the sends but PENDING bits)
-__device__ __forceinline__ void send_tail(const Dev& d, uint32_t g, uint32_t m, uint32_t s, uint32_t t, uint32_t k,
-                                          uint64_t gid, uint32_t* Sg, int ep, bool potential = false) {
-  if (d.dbg_send) {
-    uint32_t di = atomicAdd(d.dbg_send_n, 1u);
-    if (di < d.dbg_send_cap) {
-      uint32_t* r = d.dbg_send + (size_t)di * 5;
-      r[0] = k;
-      r[1] = m;
-      r[2] = (uint32_t)gid;
-      r[3] = (uint32_t)(gid >> 32);
-      r[4] = t;
-    }
-  }
-  if (!potential) {
-    const uint32_t et = Sg[t];
-    // potential unless t holds g and does not sweep it in its own round this tick (a delivery would re-create it)
-    if (s_held(et) && !(s_ctick(et) < d.swthr[t])) return;
-  }
-  if (lost_gossip_ep(d, ep, m, t, k, s, gid)) return;
-  uint32_t old = atomicOr(&Sg[t], S_PENDING);
-  if (!(old & S_PENDING)) {
-    uint32_t di = wave_append(d.deliv_n);
-    if (di < d.DCAP)
-      d.deliv[di] = ((uint64_t)g << 32) | t;
-    else
-      atomicOr(d.err, E_DELIV);
-  }
-}
-
-// The gossip round is bit-parallel over groups of 64 active slots (active[64 q .. 64 q + 63] = group q). Both masks
-// are member-major, [member][QW] words, so a sender reads its window mask and its target's held mask as contiguous
-// rows:
-//   k_gossip_scan  streams the holder table once per tick, coalesced (lane = member), and writes per (member, group)
-//                  two 64-bit masks: HB = slots the member holds past this tick (held and not sweeping them in its
-//                  round: swthr), WB = slots a round member holds inside its spread window (selectGossipsToSend
-//                  :239-250). It also performs the round members' sweeps (sweepGossips :283-308). A block covers 256
-//                  members x QT groups and transposes the masks through LDS, so every row segment is one 128-B store.
-//   k_gossip_send  one wave per (round member m, target slot s), lanes over the groups: each load of WB[m][q] and
-//                  HB[t][q] is a 512-B contiguous segment. t gets WB minus the slots t is in infectedFrom of
-//                  (isInfected, cached contact replay, only where a contact can matter); the count is a popcount,
-//                  and the first-receipt candidates are WB & ~HB[t].
-// A pair whose contact list overflowed is deferred to k_gossip_send_slow (the full replay needs a large stack).
-__global__ void __launch_bounds__(256) k_gossip_scan(const Dev* __restrict__ dp, uint32_t k, const uint32_t* active,
-                                                     const uint32_t* nactive) {
-  const Dev& d = *dp;
-  const uint32_t na = *nactive, ngroups = (na + 63) / 64;
-  const uint32_t mchunks = (d.N + 255) / 256;
-  for (uint32_t w = blockIdx.x; w < ngroups * mchunks; w += gridDim.x) {
-    const uint32_t q = w / mchunks, m0 = (w % mchunks) * 256 + threadIdx.x;
-    const bool act = m0 < d.N;  // lanes past N take part in the wave OR below with nothing to sweep
-    const uint32_t m = act ? m0 : d.N - 1;
-    const uint32_t gn = act ? min(64u, na - q * 64) : 0u;
-    const uint32_t thr = d.swthr[m];
-    const bool rnd = act && d.tround[m] && m >= d.lo && m < d.hi;  // this shard's round members send and sweep
-    uint32_t per = 0, sp = 0, fg = NEVER;
-    if (rnd) {
-      per = d.tperiod[m];
-      sp = d.tspread[m];
-      fg = d.firstGossip[m];
-    }
-    // pass 1 has no side effects, so the 64 holder-word loads pipeline; the sweeps (rare) run after it, per slot
-    // that any lane of the wave sweeps
-    unsigned long long hb = 0, wb = 0, swm = 0;
-#pragma unroll 8
-    for (uint32_t j = 0; j < gn; ++j) {
-      const uint32_t e = d.S[(size_t)active[q * 64 + j] * d.N + m];
-      if (s_held(e)) {
-        const uint32_t c = s_ctick(e);
-        if (!(c < thr)) hb |= 1ull << j;
-        if (rnd) {
-          const uint32_t infP = (fg == NEVER || c <= fg) ? 0u : (c - fg + d.gossip_t - 1) / d.gossip_t;  // rounds_before
-          if (infP + sp >= per) wb |= 1ull << j;               // selectGossipsToSend window (:246)
-          if (per > infP + sweep_after(sp)) swm |= 1ull << j;  // sweepGossips (:283-308)
-        }
-      }
-    }
-    unsigned long long any = swm;  // the slots any lane of this wave sweeps (wave-uniform loop below)
-#pragma unroll
-    for (uint32_t o = 1; o < 64; o <<= 1) {
-      const uint32_t lo = __shfl_xor((uint32_t)any, o), hi = __shfl_xor((uint32_t)(any >> 32), o);
-      any |= ((unsigned long long)hi << 32) | lo;
-    }
-    for (; any; any &= any - 1) {
-      const uint32_t j = (uint32_t)(__ffsll((long long)any) - 1), g = active[q * 64 + j];
-      const bool sweep = (swm >> j) & 1ull;
-      if (sweep) {
-        atomicOr(&d.S[(size_t)g * d.N + m], S_SWEPT);
-        if (d.XW > 1)
-          atomicSub(&d.held_delta[m], 1);
-        else
-          atomicSub(&d.held[m], 1u);
-        on_sweep(d, g, m, k);
-        if (d.W > 1) {  // applied on the other shards from exchange B
-          uint32_t i = wave_append(&d.xn[2]);
-          if (i < d.SWCAP)
-            d.sw_rec[i] = ((uint64_t)g << 32) | m;
-          else
-            atomicOr(d.err, E_XCAP);
-        }
-      }
-      // the slot's holder count, once per wave (64 lanes of one slot would serialise on its address)
-      const unsigned long long sm = __ballot(sweep);
-      if (sm && __lane_id() == (uint32_t)(__ffsll((long long)sm) - 1)) atomicSub(&d.slot_holders[g], (int)__popcll(sm));
-    }
-    if (!act) continue;
-    d.HBq[(size_t)q * d.N + m] = hb;  // group-major here (coalesced); k_mask_transpose makes the member-major rows
-    d.WBq[(size_t)q * d.N + m] = wb;
-  }
-}
-
-// [q][N] -> [N][QW] for both masks, 64 x 64 word tiles through LDS (512-B contiguous reads and writes)
-__global__ void __launch_bounds__(256) k_mask_transpose(const Dev* __restrict__ dp, const uint32_t* nactive) {
-  const Dev& d = *dp;
-  __shared__ unsigned long long tile[2][64][65];
-  const uint32_t ngroups = (*nactive + 63) / 64, qt = (ngroups + 63) / 64, mt = (d.N + 63) / 64;
-  const uint32_t lane = threadIdx.x & 63, row0 = threadIdx.x >> 6;  // 4 rows per pass
-  for (uint32_t w = blockIdx.x; w < qt * mt; w += gridDim.x) {
-    const uint32_t q0 = (w / mt) * 64, m0 = (w % mt) * 64;
-    for (uint32_t r = row0; r < 64; r += 4) {  // rows q0 + r, columns m0 + lane
-      const uint32_t q = q0 + r, m = m0 + lane;
-      const bool in = q < ngroups && m < d.N;
-      tile[0][r][lane] = in ? d.HBq[(size_t)q * d.N + m] : 0ull;
-      tile[1][r][lane] = in ? d.WBq[(size_t)q * d.N + m] : 0ull;
-    }
-    __syncthreads();
-    for (uint32_t r = row0; r < 64; r += 4) {  // rows m0 + r, columns q0 + lane
-      const uint32_t m = m0 + r, q = q0 + lane;
-      if (m < d.N && q < ngroups) {
-        d.HB[(size_t)m * d.QW + q] = tile[0][lane][r];
-        d.WB[(size_t)m * d.QW + q] = tile[1][lane][r];
-      }
-    }
-    __syncthreads();
-  }
-}
-
-// the r-th (from 0) set bit of w
-__device__ __forceinline__ uint32_t nth_bit(unsigned long long w, uint32_t r) {
-  uint32_t pos = 0;
-#pragma unroll
-  for (uint32_t half = 32; half > 0; half >>= 1) {
-    const uint32_t c = (uint32_t)__popcll(w & ((1ull << half) - 1ull));
-    if (r >= c) {
-      r -= c;
-      w >>= half;
-      pos += half;
-    }
-  }
-  return pos;
-}
-
-// reserve n entries per lane on a wave-shared counter with one atomic (every lane of the wave must call it)
-__device__ __forceinline__ uint32_t wave_reserve(uint32_t* ctr, uint32_t n) {
-  const uint32_t lane = __lane_id();
-  uint32_t incl = n;
-#pragma unroll
-  for (uint32_t o = 1; o < 64; o <<= 1) {
-    const uint32_t v = __shfl_up(incl, o);
-    if (lane >= o) incl += v;
-  }
-  const uint32_t total = __shfl(incl, 63);
-  uint32_t base = 0;
-  if (lane == 0 && total) base = atomicAdd(ctr, total);
-  return __shfl(base, 0) + incl - n;
-}
-
-__global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp, uint32_t k, const uint32_t* active,
-                                                     const uint32_t* nactive) {
-  const Dev& d = *dp;
-  __shared__ unsigned long long red[4];
-  const uint32_t na = *nactive, nr = *d.rn, ngroups = (na + 63) / 64;
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  const int ep = epoch_at(d, k);
-  unsigned long long sends = 0;
-  uint32_t st[4] = {0, 0, 0, 0};  // SWIM_EXP & 4: items with window bits, contact-loop bits, replays, first-receipt candidates
-  // wave-uniform work unit = (round member, target slot, chunk of 64 slot groups): a pair with many gossips in its
-  // window is spread over several waves instead of holding one wave for all its chunks (the kernel waits for the
-  // longest wave)
-  const uint32_t nch = (ngroups + 63) / 64;
-  const uint64_t units = (uint64_t)nr * d.F * nch;
-  for (uint64_t w = blockIdx.x * 4 + wave; w < units; w += gridDim.x * 4) {
-    const uint32_t item = (uint32_t)(w / nch), ch = (uint32_t)(w % nch);
-    const uint32_t ri = item / d.F, s = item % d.F;
-    const uint32_t m = d.rlist[ri];
-    if (s >= d.tcnt[m]) continue;
-    const size_t ms = (size_t)m * d.F + s;
-    const uint32_t t = d.T[ms], ci = d.cin[ms];
-    const unsigned long long* wrow = d.WB + (size_t)m * d.QW;
-    const unsigned long long* hrow = d.HB + (size_t)t * d.QW;
-    for (uint32_t q0 = ch * 64; q0 < ngroups && q0 < ch * 64 + 64; q0 += 64) {  // one chunk
-      const uint32_t q = q0 + lane;
-      const unsigned long long wb = q < ngroups ? wrow[q] : 0ull;
-      if (__ballot(wb != 0ull) == 0ull) continue;
-      if (d.exp & 4) st[0] += wb != 0ull;
-      const uint32_t* ga = active + (size_t)q * 64;
-      if (ci == CIN_SLOW) {  // overflowed contact list: the full replay runs in k_gossip_send_slow
-        fb_add(d, FB_CEV_SLOW, __popcll(wb));  // each lane its own group's slots
-        uint32_t i = wave_reserve(d.slow_n, (uint32_t)__popcll(wb));
-        for (unsigned long long b = wb; b; b &= b - 1, ++i) {
-          if (i < d.SLOWCAP)
-            d.slow[i] = ((uint64_t)ga[__ffsll(b) - 1] << 32) | (uint32_t)ms;
-          else
-            atomicOr(d.err, E_CONTACTS);
-        }
-        continue;
-      }
-      if (ci != NEVER) {  // a cached contact t -> m: every slot of the pair goes to k_gossip_replay (isInfected :247)
-        const uint32_t nb = (uint32_t)__popcll(wb);
-        if (d.exp & 4) st[1] += nb;
-        fb_add(d, FB_REPLAY, nb);  // each lane its own group's slots
-        uint32_t i = wave_reserve(d.rp_n, nb);
-        for (unsigned long long b = wb; b; b &= b - 1, ++i) {
-          if (i < d.RPCAP)
-            d.rp[i] = ((uint64_t)ga[__ffsll(b) - 1] << 32) | (uint32_t)ms;
-          else
-            atomicOr(d.err, E_CONTACTS);
-        }
-        continue;
-      }
-      sends += __popcll(wb);
-      const unsigned long long cand = d.dbg_send ? wb : wb & ~(q < ngroups ? hrow[q] : 0ull);
-      // the wave's candidates are spread over its lanes (a few groups hold most of them: new gossips take recently
-      // freed slots): lane p takes candidates p, p + 64, ... of the wave's list in (group, slot) order
-      const uint32_t c = (uint32_t)__popcll(cand);
-      uint32_t incl = c;
-#pragma unroll
-      for (uint32_t o = 1; o < 64; o <<= 1) {
-        const uint32_t v = __shfl_up(incl, o);
-        if (lane >= o) incl += v;
-      }
-      const uint32_t total = __shfl(incl, 63);
-      for (uint32_t b0 = 0; b0 < total; b0 += 64) {  // wave-uniform: every lane takes part in the shuffles
-        const uint32_t j = b0 + lane;
-        uint32_t own = 0;  // the lane whose word holds candidate j: the number of lanes with incl <= j
-#pragma unroll
-        for (uint32_t step = 32; step > 0; step >>= 1)
-          if (__shfl(incl, (int)(own + step - 1)) <= j) own += step;
-        const unsigned long long word = __shfl(cand, (int)own);
-        const uint32_t r = j - (__shfl(incl, (int)own) - (uint32_t)__popcll(word));
-        if (j < total) {
-          const uint32_t g = active[(size_t)(q0 + own) * 64 + nth_bit(word, r)];
-          if (d.exp & 4) st[3]++;
-          send_tail(d, g, m, s, t, k, d.slot_gid[g], d.S + (size_t)g * d.N, ep, d.dbg_send == nullptr);
-        }
-      }
-    }
-  }
-  if (d.exp & 4)
-    for (int q2 = 0; q2 < 4; ++q2)
-      if (st[q2]) atomicAdd(&d.ctr[8 + q2], (unsigned long long)st[q2]);
-  for (uint32_t o = 32; o > 0; o >>= 1) sends += __shfl_xor(sends, o);
-  if (lane == 0) red[wave] = sends;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned long long tot = red[0] + red[1] + red[2] + red[3];
-    if (tot) atomicAdd(&d.ctr[C_G], tot);
-  }
-}
-
-// sends of pairs with a cached contact, one thread per (slot, sender, target): the isInfected replay runs only where
-// the contact can matter (t -> m at or after m's incarnation start and after the gossip existed), then the send
-__global__ void __launch_bounds__(256) k_gossip_replay(const Dev* __restrict__ dp, uint32_t k) {
-  const Dev& d = *dp;
-  __shared__ unsigned long long red[4];
-  const uint32_t n = min(*d.rp_n, d.RPCAP);
-  const int ep = epoch_at(d, k);
-  unsigned long long sends = 0;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint64_t v = d.rp[i];
-    const uint32_t g = (uint32_t)(v >> 32), ms = (uint32_t)v, m = ms / d.F, s = ms % d.F;
-    uint32_t* Sg = d.S + (size_t)g * d.N;
-    const uint32_t t = d.T[ms], c = s_ctick(Sg[m]), ci = d.cin[ms];
-    const uint64_t gid = d.slot_gid[g];
-    if (ci >= d.slot_ctick[g] && ci + d.lat >= c && blocked_pair_cached(d, m, t, g, gid, k, c, d.cev + (size_t)ms * CEVW))
-      continue;
-    sends++;
-    send_tail(d, g, m, s, t, k, gid, Sg, ep);
-  }
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  for (uint32_t o = 32; o > 0; o >>= 1) sends += __shfl_xor(sends, o);
-  if (lane == 0) red[wave] = sends;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned long long tot = red[0] + red[1] + red[2] + red[3];
-    if (tot) atomicAdd(&d.ctr[C_G], tot);
-  }
-}
-
-// deferred sends whose pair had more contact events than the cache holds (small clusters): full log scan + replay
-__global__ void __launch_bounds__(64) k_gossip_send_slow(const Dev* __restrict__ dp, uint32_t k) {
-  const Dev& d = *dp;
-  const uint32_t n = min(*d.slow_n, d.SLOWCAP);
-  const int ep = epoch_at(d, k);
-  unsigned long long sends = 0;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint64_t v = d.slow[i];
-    const uint32_t g = (uint32_t)(v >> 32), ms = (uint32_t)v, m = ms / d.F, s = ms % d.F;
-    uint32_t* Sg = d.S + (size_t)g * d.N;
-    const uint32_t t = d.T[ms], c = s_ctick(Sg[m]);
-    const uint64_t gid = d.slot_gid[g];
-    if (blocked_pair(d, m, t, g, gid, k, c)) continue;  // isInfected (:247)
-    sends++;
-    send_tail(d, g, m, s, t, k, gid, Sg, ep);
-  }
-  if (sends) atomicAdd(&d.ctr[C_G], sends);
-}
-
-// P4 pre-filter (onMembershipGossip -> updateMembership, MembershipProtocolImpl.java:401-408,475-485). A first
-// receipt is routed to P4 of tick k4 unless it provably cannot change t's row there: its record does not override
-// the row as it stands now (= at the start of tick k4), the row is present, and the row cannot be removed before the
-// receipt in that tick. Present rows only move up the isOverrides order except through a removal, so a record that
-// does not override the start row overrides no later one. A removal needs a DEAD record: in P4 another receipt
-// (k_stamp_dead set dead_rx[t] = k4), or in P1 a leaver's own record in SYNC data (leaving[subject]); after one the
-// row is absent or re-added at any incarnation (an absent row accepts any ALIVE, MembershipRecord.java:67-69), so
-// every receipt is kept then. An absent start row keeps every receipt (the row may become present earlier in the
-// tick). User gossips are always routed (each one emits a GOSSIP event).
-__device__ __forceinline__ bool receipt_matters(const Dev& d, uint32_t t, uint32_t g, uint32_t k4) {
-  const uint32_t subj = d.slot_subj[g];
-  if (subj == USER_SUBJ || (d.exp & 8)) return true;  // SWIM_EXP & 8: route every receipt (debugging aid)
-  const uint64_t key = d.slot_key[g];
-  const uint32_t r0 = d.rowk[lidx(d, t) * d.NS + subj], s1 = rec_status(key);
-  if ((r0 & 3u) == ST_ABSENT || overrides(s1, rec_inc(key), r0 & 3u, r0 >> 2)) return true;
-  return d.dead_rx[t] == k4 || d.leaving[subj];
-}
-
-// the deliveries of DEAD membership records: their targets receive one in P4 of tick k + lat (receipt_matters)
-__global__ void k_stamp_dead(Dev d, uint32_t k) {
-  const uint32_t n = *d.deliv_n < d.DCAP ? *d.deliv_n : d.DCAP;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint64_t v = d.deliv[i];
-    const uint32_t g = (uint32_t)(v >> 32), t = (uint32_t)v;
-    if (rec_status(d.slot_key[g]) == ST_DEAD && d.slot_subj[g] != USER_SUBJ) d.dead_rx[t] = k + d.lat;
-  }
-}
-
-// first receipts (onGossipReq :176-180): create the holder state at tick k + lat and queue the record for P4.
-// Deliveries come in runs of one target (a send-kernel wave appends one (sender, target) pair's receipts together), so
-// the target's counters are added once per run of equal targets in the wave instead of once per lane (one address
-// per wave serialised at L2). The loop is wave-uniform so that every lane reaches the run reduction.
-__global__ void k_gossip_apply(Dev d, uint32_t k) {
-  const uint32_t n = *d.deliv_n < d.DCAP ? *d.deliv_n : d.DCAP;
-  const uint32_t lane = __lane_id(), stride = gridDim.x * blockDim.x;
-  for (uint32_t i0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0 < n; i0 += stride) {
-    const uint32_t i = i0 + lane;
-    const bool act = i < n;
-    uint32_t g = 0, t = NEVER, created = 0, dropped = 0;
-    if (act) {
-      const uint64_t v = d.deliv[i];
-      g = (uint32_t)(v >> 32);
-      t = (uint32_t)v;
-      uint32_t* p = d.S + (size_t)g * d.N + t;
-      const uint32_t e = *p & ~S_PENDING;
-      if (s_held(e)) {
-        *p = e;
-      } else {
-        if (s_ever(e)) hist_push(d, d.slot_gid[g], t, s_ctick(e));  // rebirth after a sweep (:176-180)
-        *p = ((k + d.lat + 1u) & S_TICK_MASK) | (s_ever(e) ? S_REBORN : 0u);
-        created = 1;
-        atomicAdd(&d.slot_holders[g], 1);
-        if (t >= d.lo && t < d.hi) {  // else P4 of another shard's member
-          if (d.fastp4 && d.slot_subj[g] == USER_SUBJ) {  // RUMOR mode: the GOSSIP event of P4 (k + lat), hashed now
-            const uint64_t gid = d.slot_gid[g], key = d.slot_key[g];
-            const uint64_t ev = ((uint64_t)(k + d.lat) << 32) | (3ull << 30) | (uint32_t)(gid >> 32);
-            const uint64_t meta = ((uint64_t)(uint32_t)key << 32) | (key >> 32);  // (oldMeta, newMeta) = payload (lo, hi)
-            atomicAdd(&d.evp_hash[t], (unsigned long long)hpair(hpair(ev, meta), (uint32_t)gid));
-            atomicAdd(&d.evp_n[t], 1u);
-          } else if (!receipt_matters(d, t, g, k + d.lat)) {  // counted as a record compare in P4, nothing else
-            dropped = 1;
-          } else {
-            uint32_t ri = wave_append(d.rc_n);
-            if (ri < d.RCAP)
-              d.rc_raw[ri] = ((uint64_t)t << 32) | g;
-            else
-              atomicOr(d.err, E_RECEIPTS);
-          }
-        }
-      }
-    }
-    // runs of equal targets among the wave's lanes (lanes past n carry NEVER and nothing)
-    const uint32_t tp = __shfl_up(t, 1);
-    const unsigned long long heads = __ballot(lane == 0 || tp != t);
-    const unsigned long long cm = __ballot(created != 0), dm = __ballot(dropped != 0);
-    if (act && ((heads >> lane) & 1ull)) {
-      const unsigned long long above = heads & ~((2ull << lane) - 1ull);  // heads after this lane (lane < 63)
-      const uint32_t end = lane == 63 || !above ? 64u : (uint32_t)(__ffsll((long long)above) - 1);
-      const unsigned long long run = (end == 64 ? ~0ull : ((1ull << end) - 1ull)) & ~((1ull << lane) - 1ull);
-      const uint32_t nc = (uint32_t)__popcll(cm & run), nd = (uint32_t)__popcll(dm & run);
-      if (nc) {
-        if (d.XW > 1)
-          atomicAdd(&d.held_delta[t], (int)nc);
-        else
-          atomicAdd(&d.held[t], nc);
-      }
-      if (nd) atomicAdd(&d.rc_ndrop[t], nd);
-    }
-  }
-}
-
-// a slot nobody holds can never be sent again: clear its holder row and recycle it
-__global__ void __launch_bounds__(256) k_gossip_free(Dev d, const uint32_t* active, const uint32_t* nactive) {
-  uint32_t na = *nactive;
-  for (uint32_t a = blockIdx.x; a < na; a += gridDim.x) {
-    uint32_t g = active[a];
-    if (d.slot_holders[g] > 0) continue;
-    uint32_t* Sg = d.S + (size_t)g * d.N;
-    for (uint32_t s = threadIdx.x; s < d.N; s += blockDim.x) Sg[s] = 0;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      d.slot_used[g] = 0;
-      if (g / d.SPR == d.rank) {  // back to the owning shard's free list
-        int pos = atomicAdd(d.free_top, 1);
-        d.free_list[pos] = g;
-      }
-    }
-  }
-}
-
-// swim_kill: the member stops holding gossips (it can never send them again)
-__global__ void k_kill(Dev d, uint32_t m) {
-  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= d.SLOTS || !d.slot_used[g]) return;
-  if (s_held(d.S[(size_t)g * d.N + m])) atomicSub(&d.slot_holders[g], 1);
-}
-
-// ------------------------------------------------------------------------------------------------------------
 // state hashes (SEMANTICS.md §8), one block per member
 __global__ void __launch_bounds__(256) k_hash(Dev d, uint64_t* out, uint32_t now) {
   __shared__ unsigned long long red[4][256];
@@ -1240,46 +512,43 @@ void launch_member(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[3], st);
 }
 
-static void launch_receipt_routing(const Dev& d, hipStream_t st);
-
-constexpr uint32_t SEND_GRID = 4096;  // 16 blocks per CU, grid-stride
+// gossip.hip
+void launch_gossip_send(const Dev& d, uint32_t k, hipStream_t st, const TickEvents* prof);
+void launch_gossip_apply(const Dev& d, uint32_t k, hipStream_t st);
+void launch_unpack_b(const Dev& d, uint32_t k, hipStream_t st);
 
 void launch_gossip(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_gossip_active, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, st, d, k, d.active, d.nactive);
-  hipLaunchKernelGGL(k_round_info, dim3(cdiv(d.N, 256)), dim3(256), 0, st, d);
-  hipLaunchKernelGGL(k_gossip_contacts, dim3(cdiv((uint64_t)d.NL * d.F, 256)), dim3(256), 0, st, d, k);
-  if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[4], st);
-  hipLaunchKernelGGL(k_gossip_scan, dim3(SEND_GRID), dim3(256), 0, st, d.self, k, d.active, d.nactive);
-  hipLaunchKernelGGL(k_mask_transpose, dim3(SEND_GRID), dim3(256), 0, st, d.self, d.nactive);
-  hipLaunchKernelGGL(k_gossip_send, dim3(SEND_GRID), dim3(256), 0, st, d.self, k, d.active, d.nactive);
-  hipLaunchKernelGGL(k_gossip_send_slow, dim3(64), dim3(64), 0, st, d.self, k);  // rare; ~14 KB of stack per lane
-  hipLaunchKernelGGL(k_gossip_replay, dim3(2048), dim3(256), 0, st, d.self, k);
-  if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[5], st);
-  hipLaunchKernelGGL(k_stamp_dead, dim3(1024), dim3(256), 0, st, d, k);
-  hipLaunchKernelGGL(k_gossip_apply, dim3(1024), dim3(256), 0, st, d, k);
-  launch_receipt_routing(d, st);
-  hipLaunchKernelGGL(k_gossip_free, dim3(1024), dim3(256), 0, st, d, d.active, d.nactive);
+  launch_gossip_send(d, k, st, prof);
+  launch_gossip_apply(d, k, st);
 }
 
-// ---- sharded tick (W > 1): the same kernel sequence as launch_tick, cut at the two exchange points ----
-static void launch_receipt_routing(const Dev& d, hipStream_t st) {
+// exclusive scan of n counts (n <= 2^20)
+void launch_scan(const uint32_t* in, uint32_t* out, uint32_t* part, uint32_t n, hipStream_t st) {
+  uint32_t nb = cdiv(n, 1024);
+  hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(256), 0, st, in, out, part, n);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, st, part, nb);
+  hipLaunchKernelGGL(k_scan_add, dim3(cdiv(n, 256)), dim3(256), 0, st, out, part, n);
+}
+
+// receipts routed to P4: counting sort by member, then each member's receipts by gossip id
+void launch_receipt_routing(const Dev& d, hipStream_t st) {
   hipLaunchKernelGGL(k_count_rc, dim3(256), dim3(256), 0, st, d.rc_raw, d.rc_n, d.RCAP, d.rc_cnt);
-  uint32_t nb = cdiv(d.N, 1024);
-  hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(256), 0, st, d.rc_cnt, d.rc_off, d.scan_part, d.N);
-  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, st, d.scan_part, nb);
-  hipLaunchKernelGGL(k_scan_add, dim3(cdiv(d.N, 256)), dim3(256), 0, st, d.rc_off, d.scan_part, d.N);
+  launch_scan(d.rc_cnt, d.rc_off, d.scan_part, d.N, st);
   hipLaunchKernelGGL(k_scatter_rc, dim3(256), dim3(256), 0, st, d, d.rc_raw, d.rc_n, d.RCAP, d.rc_off, d.rc_fill,
                      d.rc_slot, d.rc_key);
   hipLaunchKernelGGL(k_seg_sort, dim3(1024), dim3(256), 0, st, d.rc_key, d.rc_slot, d.rc_key2, d.rc_slot2, d.rc_off,
                      d.rc_cnt, d.N, d.rc_n, d.sort_cap, d.fb);
 }
 
+// sharded tick (W > 1): A = SYNC diff + member control + pack exchange A; B = unpack A, the rounds' holder-state
+// changes and this shard's targets' sends, pack exchange B (their first receipts); C = peers' first receipts into the
+// replicated holder state, this shard's receipts, routing, slot recycling
 void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
   hipStream_t st = (hipStream_t)stream;
-  uint32_t b = k & 1, pb = (k - 1) & 1;
+  uint32_t b = k & 1;
   if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
-  if (k > 0) launch_sync_diff(d, pb, st, prof ? 1u : 0u);
+  if (k > 0) launch_sync_diff(d, (k - 1) & 1, st, prof ? 1u : 0u);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[2], st);
   hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k, 0u);
@@ -1297,28 +566,15 @@ void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
     if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[5], st);
     return;
   }
-  hipLaunchKernelGGL(k_gossip_active, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, st, d, k, d.active, d.nactive);
-  hipLaunchKernelGGL(k_round_info, dim3(cdiv(d.N, 256)), dim3(256), 0, st, d);
-  hipLaunchKernelGGL(k_gossip_contacts, dim3(cdiv((uint64_t)d.NL * d.F, 256)), dim3(256), 0, st, d, k);
-  if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[4], st);
-  hipLaunchKernelGGL(k_gossip_scan, dim3(SEND_GRID), dim3(256), 0, st, d.self, k, d.active, d.nactive);
-  hipLaunchKernelGGL(k_mask_transpose, dim3(SEND_GRID), dim3(256), 0, st, d.self, d.nactive);
-  hipLaunchKernelGGL(k_gossip_send, dim3(SEND_GRID), dim3(256), 0, st, d.self, k, d.active, d.nactive);
-  hipLaunchKernelGGL(k_gossip_send_slow, dim3(64), dim3(64), 0, st, d.self, k);  // rare; ~14 KB of stack per lane
-  hipLaunchKernelGGL(k_gossip_replay, dim3(2048), dim3(256), 0, st, d.self, k);
-  if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[5], st);
+  launch_gossip_send(d, k, st, prof);
   hipLaunchKernelGGL(k_pack_b, dim3(64, d.W), dim3(256), 0, st, d);
 }
 
 void launch_tick_c(const Dev& d, uint32_t k, void* stream, bool gossip) {
   hipStream_t st = (hipStream_t)stream;
   if (!gossip) return;  // k_unpack_a closed the tick
-  hipLaunchKernelGGL(k_unpack_b_sweeps, dim3(64, d.W), dim3(256), 0, st, d, k);
-  hipLaunchKernelGGL(k_unpack_b_deliv, dim3(64, d.W), dim3(256), 0, st, d, k);
-  hipLaunchKernelGGL(k_stamp_dead, dim3(1024), dim3(256), 0, st, d, k);
-  hipLaunchKernelGGL(k_gossip_apply, dim3(1024), dim3(256), 0, st, d, k);
-  launch_receipt_routing(d, st);
-  hipLaunchKernelGGL(k_gossip_free, dim3(1024), dim3(256), 0, st, d, d.active, d.nactive);
+  launch_unpack_b(d, k, st);
+  launch_gossip_apply(d, k, st);
   hipLaunchKernelGGL(k_round_reset, dim3(16, d.W), dim3(256), 0, st, d);
   hipLaunchKernelGGL(k_tick_end, dim3(1), dim3(64), 0, st, d, k);
 }
@@ -1355,9 +611,6 @@ void launch_join(const Dev& d, uint32_t m, uint32_t k, const uint32_t* seeds, ui
   hipLaunchKernelGGL(k_join, dim3(1), dim3(64), 0, (hipStream_t)stream, d, m, k, js, n);
 }
 
-void launch_kill(const Dev& d, uint32_t member, void* stream) {
-  hipLaunchKernelGGL(k_kill, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, (hipStream_t)stream, d, member);
-}
 
 void launch_hash(const Dev& d, uint64_t* out, uint32_t now, void* stream) {
   hipLaunchKernelGGL(k_hash, dim3(d.NL), dim3(256), 0, (hipStream_t)stream, d, out, now);

@@ -283,17 +283,13 @@ __device__ __forceinline__ void emit_event(ML& L, uint32_t type, uint32_t subj, 
   on_member_event(L, type, subj);
 }
 
-// createAndPutGossip (GossipProtocolImpl.java:163-169): gossip slot g becomes a new gossip held by member m since tick k
+// createAndPutGossip (GossipProtocolImpl.java:163-169): gossip slot g becomes a new gossip held by member m since tick
+// k (slot_create: slot tables and the creator's holder state, ring position pos); with row shards it is replicated on
+// the other shards from exchange A
 __device__ __forceinline__ void slot_init(const Dev& d, uint32_t g, uint32_t m, uint32_t k, uint64_t gid, uint32_t subj,
-                                          uint64_t key) {
-  d.slot_gid[g] = gid;
-  d.slot_subj[g] = subj;
-  d.slot_ctick[g] = k;
-  d.slot_key[g] = key;
-  d.slot_holders[g] = 1;
-  d.slot_used[g] = 1;
-  d.S[(size_t)g * d.N + m] = (k + 1u) & S_TICK_MASK;
-  if (d.W > 1) {  // replicated on the other shards from exchange A
+                                          uint64_t key, uint32_t pos) {
+  slot_create(d, g, m, k, gid, subj, key, pos);
+  if (d.W > 1) {
     uint32_t i = atomicAdd(&d.xn[0], 1u);
     if (i >= d.NSCAP) {
       set_err(d, E_XCAP);
@@ -319,6 +315,7 @@ __device__ __forceinline__ void flush_spreads(ML& L) {
   L.nsp = 0;
   const Dev& d = *L.d;
   const int base = atomicSub(d.free_top, (int)n) - (int)n;
+  uint32_t rt = d.rtail[L.m];  // only this lane appends to the member's ring in this kernel
   for (uint32_t i = 0; i < n; ++i) {
     const int pos = base + (int)i;
     if (pos < 0) {
@@ -326,9 +323,10 @@ __device__ __forceinline__ void flush_spreads(ML& L) {
       continue;
     }
     const uint4 e0 = *(const uint4*)(L.spq + 8 * i), e1 = *(const uint4*)(L.spq + 8 * i + 4);
-    slot_init(d, d.free_list[pos], L.m, L.k, ((uint64_t)e0.y << 32) | e0.x, e0.z, ((uint64_t)e1.x << 32) | e0.w);
+    slot_init(d, d.free_list[pos], L.m, L.k, ((uint64_t)e0.y << 32) | e0.x, e0.z, ((uint64_t)e1.x << 32) | e0.w, rt++);
     L.c[C_GCREATED]++;
   }
+  d.rtail[L.m] = rt;
 }
 
 // GossipProtocolImpl.spread -> createAndPutGossip (:124-128,163-169): a membership gossip held by this member; its
@@ -360,11 +358,17 @@ __global__ void k_ug_count(Dev d, uint32_t k, const uint64_t* q, uint32_t n, uin
   const uint32_t m = (uint32_t)q[2 * i];
   if (ug_live(d, m, k)) atomicAdd(&ucnt[m], 1u);
 }
-// rank of entry i among the queue entries of member m before it (members with one entry: 0, no scan)
-__device__ __forceinline__ uint32_t ug_rank(const uint64_t* q, uint32_t i, uint32_t m, uint32_t cnt) {
-  if (cnt <= 1) return 0;
-  uint32_t r = 0;
-  for (uint32_t j = 0; j < i; ++j) r += (uint32_t)q[2 * j] == m;
+// rank of entry i among the queue entries of member m before it (members with one entry: 0, no scan), and among
+// those whose gossip this (slot) shard stores (its ring position); gc0 = the member's gossip counter before the queue
+struct UgRank {
+  uint32_t all, mine;
+};
+__device__ __forceinline__ UgRank ug_rank(const Dev& d, const uint64_t* q, uint32_t i, uint32_t m, uint32_t cnt,
+                                          uint32_t gc0) {
+  UgRank r{0, 0};
+  if (cnt <= 1) return r;
+  for (uint32_t j = 0; j < i; ++j)
+    if ((uint32_t)q[2 * j] == m) r.mine += slot_mine(d, ((uint64_t)m << 32) | (gc0 + r.all++)) ? 1u : 0u;
   return r;
 }
 __global__ void __launch_bounds__(256) k_ug_create(Dev d, uint32_t k, const uint64_t* q, uint32_t n, const uint32_t* ucnt) {
@@ -372,8 +376,10 @@ __global__ void __launch_bounds__(256) k_ug_create(Dev d, uint32_t k, const uint
   const uint32_t m = i < n ? (uint32_t)q[2 * i] : 0u;
   bool mine = false;
   uint64_t gid = 0;
+  UgRank rk{0, 0};
   if (i < n && ug_live(d, m, k)) {
-    gid = ((uint64_t)m << 32) | (d.gCounter[m] + ug_rank(q, i, m, ucnt[m]));
+    rk = ug_rank(d, q, i, m, ucnt[m], d.gCounter[m]);
+    gid = ((uint64_t)m << 32) | (d.gCounter[m] + rk.all);
     mine = slot_mine(d, gid);  // slot sharding: only the owning shard stores it; every shard counts it as held
   }
   const uint64_t bm = __ballot(mine);
@@ -385,8 +391,8 @@ __global__ void __launch_bounds__(256) k_ug_create(Dev d, uint32_t k, const uint
     const int pos = top - (int)nb + (int)__popcll(bm & ((1ull << lane) - 1ull));
     if (pos < 0)
       set_err(d, E_SLOTS);
-    else
-      slot_init(d, d.free_list[pos], m, k, gid, USER_SUBJ, q[2 * i + 1]);
+    else  // ring position: the member's stored gossips of this queue take consecutive positions in call order
+      slot_init(d, d.free_list[pos], m, k, gid, USER_SUBJ, q[2 * i + 1], d.rtail[m] + rk.mine);
   }
   if (lane == 0 && nb) atomicAdd(&d.ctr[C_GCREATED], (unsigned long long)nb);
 }
@@ -395,10 +401,13 @@ __global__ void k_ug_finish(Dev d, uint32_t k, const uint64_t* q, uint32_t n, ui
   if (i >= n) return;
   const uint32_t m = (uint32_t)q[2 * i];
   if (!ug_live(d, m, k)) return;
-  const uint32_t c = ucnt[m];
-  if (ug_rank(q, i, m, c) != 0) return;  // the member's first entry advances it once
-  d.gCounter[m] += c;
+  const uint32_t c = ucnt[m], gc0 = d.gCounter[m];
+  if (c > 1 && ug_rank(d, q, i, m, c, gc0).all != 0) return;  // the member's first entry advances it once
+  uint32_t mine = 0;  // ring entries this shard appended for the member
+  for (uint32_t r = 0; r < c; ++r) mine += slot_mine(d, ((uint64_t)m << 32) | (gc0 + r)) ? 1u : 0u;
+  d.gCounter[m] = gc0 + c;
   d.held[m] += c;
+  d.rtail[m] += mine;
   ucnt[m] = 0;
 }
 void launch_ug(const Dev& d, uint32_t k, const uint64_t* q, uint32_t n, hipStream_t st) {

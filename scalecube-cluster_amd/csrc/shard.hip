@@ -1,20 +1,21 @@
 // shard.hip — row-sharded observers: packing and unpacking of the two per-tick exchanges.
 //
 // Each shard owns the observers [lo, hi) and runs their protocol control (k_member_tick) and their SYNC merges.
-// The gossip plane stays replicated: every shard keeps the whole slot table, S, the round logs and the
-// incarnation history, and applies the union of every shard's gossip records, so the data-plane kernels read
-// any member's gossip state locally.
+// The gossip plane stays replicated: every shard keeps the whole slot table, holder state (S, HB / WB, receipt rings),
+// the round logs and the incarnation history, and applies the union of every shard's gossip records, so the
+// data-plane kernels read any member's gossip state locally. The sends of a tick are split by target shard.
 //
 //   exchange A (after k_member_tick): gossips created this tick, gossip rounds this tick (targets, spread, period),
 //     and the SYNC / SYNC_ACK messages addressed to the peer's observers. A SYNC payload (the sender's row at send
 //     time, MembershipProtocolImpl.prepareSyncDataMsg :446-454) ships as a 2048-record chunk mask against the
 //     replicated baseline row plus the chunks that differ, so a converged row costs a few bytes on xGMI.
-//   exchange B (after k_gossip_send): first receipts (slot, target) and sweeps (slot, member) of this shard's senders.
+//   exchange B (after the sends): first receipts (slot, target) of this shard's targets. Every shard runs every
+//     member's round (sweeps and windows) on its replicated holder state, so sweeps need no exchange.
 //
 // Peer regions have a fixed capacity; a region that would overflow raises E_XCAP instead of being truncated.
 // Region A: u32 hdr[8] = {nslot, nround, nsync, nchunk, data_off, 0, 0, 0}; slot records; round records;
 //           sync entries {SyncMsg, u32 chunk base, u32 pad, u64 mask[MW]}; chunk data at data_off (256-B aligned).
-// Region B: u32 hdr[4] = {ndeliv, nsweep, 0, 0}; u64 deliveries; u64 sweeps.
+// Region B: u32 hdr[4] = {nreceipt, 0, 0, 0}; u64 receipts.
 #include "dev_util.h"
 
 namespace swim {
@@ -188,14 +189,9 @@ __global__ void __launch_bounds__(256) k_unpack_a(Dev d, uint32_t k, uint32_t en
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
     for (uint32_t i = tid; i < nslot; i += nth) {  // spread -> createAndPutGossip at the origin (member.hip)
       const uint32_t* r = S + (size_t)i * NSW;
-      uint32_t g = r[0], origin = r[7];
-      d.slot_gid[g] = (uint64_t)r[1] | ((uint64_t)r[2] << 32);
-      d.slot_subj[g] = r[3];
-      d.slot_ctick[g] = r[4];
-      d.slot_key[g] = (uint64_t)r[5] | ((uint64_t)r[6] << 32);
-      d.slot_holders[g] = 1;
-      d.slot_used[g] = 1;
-      d.S[(size_t)g * d.N + origin] = (r[4] + 1u) & S_TICK_MASK;
+      const uint32_t g = r[0], origin = r[7];
+      slot_create(d, g, origin, r[4], (uint64_t)r[1] | ((uint64_t)r[2] << 32), r[3], (uint64_t)r[5] | ((uint64_t)r[6] << 32),
+                  atomicAdd(&d.rtail[origin], 1u));
       atomicAdd(&d.held[origin], 1u);
     }
     for (uint32_t i = tid; i < nround; i += nth) {  // do_spread_gossip at the sender (member.hip)
@@ -243,60 +239,25 @@ __global__ void __launch_bounds__(256) k_unpack_a(Dev d, uint32_t k, uint32_t en
   }
 }
 
+// this shard's first receipts of the tick (its targets' senders ran here): every peer applies them to its replicated
+// holder state (gossip.hip k_unpack_b)
 __global__ void __launch_bounds__(256) k_pack_b(Dev d) {
   const uint32_t q = blockIdx.y;
   if (q == d.rank) return;
   uint8_t* R = d.xb_send + (size_t)q * d.XB_PEER;
-  uint32_t nd = min(*d.deliv_n, d.DCAP), ns = min(d.xn[2], d.SWCAP);
-  if (16 + 8ull * (nd + ns) > d.XB_PEER) {
+  uint32_t nd = min(*d.xd_n, d.DCAP);
+  if (16 + 8ull * nd > d.XB_PEER) {
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(d.err, E_XCAP);
-    nd = ns = 0;
+    nd = 0;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     uint32_t* H = (uint32_t*)R;
     H[0] = nd;
-    H[1] = ns;
-    H[2] = H[3] = 0;
-    d.xb_scnt[q] = 16 + 8ull * (nd + ns);
+    H[1] = H[2] = H[3] = 0;
+    d.xb_scnt[q] = 16 + 8ull * nd;
   }
   uint64_t* V = (uint64_t*)(R + 16);
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nd + ns; i += gridDim.x * blockDim.x)
-    V[i] = i < nd ? d.deliv[i] : d.sw_rec[i - nd];
-}
-
-// peers' sweeps first (sweepGossips :283-308), so that a delivery to a member that swept g this tick re-creates it
-__global__ void k_unpack_b_sweeps(Dev d, uint32_t k) {
-  const uint32_t p = blockIdx.y;
-  if (p == d.rank || (d.xb_rcnt[p] & XCNT_MASK) < 16) return;
-  const uint8_t* R = d.xb_recv + (size_t)p * d.XB_PEER;
-  const uint32_t nd = ((const uint32_t*)R)[0], ns = ((const uint32_t*)R)[1];
-  const uint64_t* V = (const uint64_t*)(R + 16) + nd;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += gridDim.x * blockDim.x) {
-    uint32_t g = (uint32_t)(V[i] >> 32), m = (uint32_t)V[i];
-    atomicOr(&d.S[(size_t)g * d.N + m], S_SWEPT);
-    atomicSub(&d.held[m], 1u);
-    atomicSub(&d.slot_holders[g], 1);
-    on_sweep(d, g, m, k);
-  }
-}
-
-// peers' first receipts join this shard's delivery list, deduplicated by the PENDING bit like local ones
-__global__ void k_unpack_b_deliv(Dev d, uint32_t k) {
-  const uint32_t p = blockIdx.y;
-  if (p == d.rank || (d.xb_rcnt[p] & XCNT_MASK) < 16) return;
-  const uint8_t* R = d.xb_recv + (size_t)p * d.XB_PEER;
-  const uint32_t nd = ((const uint32_t*)R)[0];
-  const uint64_t* V = (const uint64_t*)(R + 16);
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nd; i += gridDim.x * blockDim.x) {
-    uint64_t v = V[i];
-    uint32_t old = atomicOr(&d.S[(size_t)(v >> 32) * d.N + (uint32_t)v], S_PENDING);
-    if (old & S_PENDING) continue;
-    uint32_t di = atomicAdd(d.deliv_n, 1u);
-    if (di < d.DCAP)
-      d.deliv[di] = v;
-    else
-      atomicOr(d.err, E_DELIV);
-  }
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nd; i += gridDim.x * blockDim.x) V[i] = d.xd[i];
 }
 
 // the peers' members are out of their gossip round again

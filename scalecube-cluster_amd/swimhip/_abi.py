@@ -55,7 +55,8 @@ class SwimConfig(C.Structure):
         ("list_slack", C.c_uint32),
         ("churn_per_period", C.c_uint32),
         ("n_dormant", C.c_uint32),
-        ("reserved", C.c_uint32 * 4),
+        ("gossip_ring_cap", C.c_uint32),
+        ("reserved", C.c_uint32 * 3),
     ]
 
 

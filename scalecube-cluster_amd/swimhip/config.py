@@ -66,6 +66,7 @@ class SimConfig:
     profile_all: bool = False  # SWIM_FLAG_PROFILE_ALL: every k_sync_diff launch timed (+ member / gossip kernels)
     implicit_views: bool = False  # SWIM_FLAG_IMPLICIT_VIEWS (RUMOR mode): tables / lists computed, not stored
     gossip_slot_cap: int = 0
+    gossip_ring_cap: int = 0  # gossips one member can hold at once (0: the engine's default)
     pending_fetch_cap: int = 0
     event_cap: int = 0
     list_slack: int = 0
@@ -106,6 +107,7 @@ class SimConfig:
         for i, s in enumerate(seeds):
             a.seeds[i] = s
         a.gossip_slot_cap = self.gossip_slot_cap
+        a.gossip_ring_cap = self.gossip_ring_cap
         a.pending_fetch_cap = self.pending_fetch_cap
         a.event_cap = self.event_cap
         a.n_gpus = self.n_gpus

@@ -6,7 +6,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/${1:-r3a}
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider \
   -k "fallback or tiny_caps or member_configs or drain_small or user_gossip or rumor or cold_join_inbound or contact_replay" \
   > $O/new_tests.log 2>&1
 timeout -k 10 900 python -u -m pytest tests/test_gpu_scale_props.py -x -v --timeout 850 --timeout-method thread \
