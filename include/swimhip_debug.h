@@ -15,6 +15,8 @@
  *          GossipProtocolImpl.selectGossipsToSend isInfected (:239-250)
  *   mq     inbound SYNC messages of one tick sorted in registers (more: selection by list walks), onMessage (:320-331)
  *   sort   first receipts of one member and tick sorted in LDS at once (more: sorted runs merged), P4 order
+ *   rx     contact pairs per tick whose replay is limited to the gossips received before the contact (more: the
+ *          whole window is replayed), GossipProtocolImpl isInfected (:247)
  * With SWIM_CAPS (or SWIM_FALLBACKS=1) set, the handle counts how often each fallback fired.
  */
 #ifndef SWIMHIP_DEBUG_H
@@ -38,7 +40,9 @@ extern "C" {
 #define SWIM_FB_REPLAY 5u      /* gossip sends replayed from the contact cache (pairs with a logged contact) */
 #define SWIM_FB_MQ 6u          /* receivers with more than mq inbound SYNC messages in one tick */
 #define SWIM_FB_SORT_MERGE 7u  /* receipt segments sorted as runs and merged (sort) */
-#define SWIM_FB_COUNT 8u
+#define SWIM_FB_RX_ALL 8u      /* contact pairs that replayed their whole window (rx: rows of window gossips received
+                                  before the contact, per tick) */
+#define SWIM_FB_COUNT 9u
 
 /* counts of the fallbacks fired since create, n <= 16 entries (summed over shards); SWIM_EUNSUPPORTED when the
  * handle was created without SWIM_CAPS / SWIM_FALLBACKS */

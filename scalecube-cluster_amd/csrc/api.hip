@@ -268,6 +268,7 @@ int build(swim_handle* h) {
   // lowers them so that the exact fallbacks run; results stay bit-exact, only slower
   d.trk_cap = TRK, d.ulog_cap = ULOG, d.creq_cap = CREQ, d.cwmax_cap = CWMAX, d.cev_cap = CEV, d.mq_cap = MQ;
   d.sort_cap = SORT_MAX;
+  uint32_t rx_cap = NEVER;
   const char* caps = getenv("SWIM_CAPS");
   if (caps) {
     std::string s(caps);
@@ -288,6 +289,7 @@ int build(swim_handle* h) {
       else if (k == "cwmax") d.cwmax_cap = clampv(0, CWMAX);
       else if (k == "cev") d.cev_cap = clampv(0, CEV);
       else if (k == "mq") d.mq_cap = clampv(1, MQ);
+      else if (k == "rx") rx_cap = v;
       else if (k == "sort") {
         uint32_t r = 2;
         while (r * 2 <= clampv(2, SORT_MAX)) r *= 2;  // a power of two (bitonic runs)
@@ -347,14 +349,15 @@ int build(swim_handle* h) {
     h->err = "gossipRepeatMult x ceilLog2(members) too large (at most 248)";
     return SWIM_EINVAL;
   }
-  // receipt ring per member: at least as many entries as the member can hold gossips; default the slot table's
-  // size up to a 48 GB total (C2 holds ~3·10^5 per member), swim_config.gossip_ring_cap overrides
+  // receipt ring per member: at least as many entries as the member can hold gossips; by default the slot table's
+  // size, within about 16-24 GB in all (C2 holds ~3·10^5 gossips per member at 10k members), and
+  // swim_config.gossip_ring_cap overrides (a full ring raises E_RING)
   {
-    uint64_t want = c.gossip_ring_cap ? c.gossip_ring_cap
-                                      : std::min<uint64_t>(d.SLOTS, std::max<uint64_t>(1024, (48ull << 30) / (4 * N)));
+    const uint64_t want = c.gossip_ring_cap ? c.gossip_ring_cap
+                                            : std::min<uint64_t>(d.SLOTS, std::max<uint64_t>(4096, (16ull << 30) / (4 * N)));
     uint64_t bc = 64;
     while (bc < want && bc < (1ull << 31)) bc <<= 1;
-    if (!c.gossip_ring_cap && bc > want && bc / 2 >= 1024 && bc > d.SLOTS) bc /= 2;
+    if (!c.gossip_ring_cap && bc > 4096 && bc * N * 4 > (24ull << 30)) bc >>= 1;
     d.BCAP = (uint32_t)bc;
   }
   uint64_t mc = N / d.sync_t * 4 + N / d.ping_t + 1024;
@@ -407,6 +410,9 @@ int build(swim_handle* h) {
   A(d.rg, (uint64_t)d.BCAP * N) A(d.rhead, N) A(d.rwin, N) A(d.rseen, N) A(d.rtail, N) A(d.rwl, N) A(d.nrwl, 1)
   A(d.rsend, N) A(d.rwnew, N) A(d.GU, d.QW) A(d.DM, d.QW) A(d.agroup, d.QW) A(d.nagroup, 2)
   A(d.tin_cnt, N) A(d.tin_off, N) A(d.tin_fill, N) A(d.tin, N * d.F) A(d.tlist, N) A(d.ntl, 1) A(d.rt0, N)
+  d.CRCAP = (uint32_t)std::max<uint64_t>(64, std::min<uint64_t>(4096, (512ull << 20) / (8ull * d.QW)));
+  if (rx_cap != NEVER) d.CRCAP = rx_cap;  // SWIM_CAPS rx=...: contact pairs past it replay their whole window
+  A(d.crow, N * d.F) A(d.RX, (uint64_t)d.CRCAP * d.QW) A(d.rxl, 3ull * d.CRCAP) A(d.nrx, 1) A(d.cfl, N * d.F) A(d.ncfl, 1)
   A(d.log_tick, N * d.LOGW) A(d.log_spread, N * d.LOGW) A(d.log_cnt, N * d.LOGW) A(d.log_tg, N * d.LOGW * d.F)
   A(d.log_pos, N) A(d.spchg, N)
   A(d.slot_gid, d.SLOTS) A(d.slot_subj, d.SLOTS) A(d.slot_ctick, d.SLOTS) A(d.slot_key, d.SLOTS) A(d.slot_exp, d.SLOTS)

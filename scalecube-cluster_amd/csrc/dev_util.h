@@ -169,6 +169,22 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* ctr) {
   return base + rank;
 }
 
+// reserve n entries per lane on a shared counter with ONE atomic per wave; every lane of the wave must call it
+// (inactive work passes n = 0). Returns the lane's first index.
+__device__ __forceinline__ uint32_t wave_reserve(uint32_t* ctr, uint32_t n) {
+  const uint32_t lane = __lane_id();
+  uint32_t incl = n;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  const uint32_t total = __shfl(incl, 63);
+  uint32_t base = 0;
+  if (lane == 0 && total) base = atomicAdd(ctr, total);
+  return __shfl(base, 0) + incl - n;
+}
+
 // A receiver with several SYNC / SYNC_ACK payloads in one tick reads the later ones' records for the subjects an
 // earlier one changed (member.hip, merge_payload), after their senders may have written their live rows again:
 // such a live-row payload gets an arena row that k_sync_diff fills with its keys. A lost CAS race wastes a row.

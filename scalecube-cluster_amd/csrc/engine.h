@@ -43,6 +43,7 @@ constexpr uint32_t E_SLOTS = 1, E_FETCH = 2, E_SUBS = 4, E_PATHS = 8, E_GROUPS =
 // per-link NetworkEmulator settings (setLinkSettings / block / unblock): hash of (src, dst) -> change history
 constexpr uint32_t LKCAP = 4096, LKH = 8;  // keys, history entries per key
 constexpr uint32_t CIN_SLOW = 0xFFFFFFFEu;
+constexpr uint32_t RX_ALL = 0xFFFFFFFFu;
 constexpr uint32_t MDU = 64;  // members with updated metadata per handle
 constexpr uint32_t CEV = 6, CEVW = 4 + 2 * CEV;  // cached contact events per (sender, target): n, oldest[2], events
 // gossip incarnation history entry: 3 header words + HKEEP creation ticks of swept incarnations (small clusters
@@ -72,6 +73,7 @@ enum Fb {
   FB_REPLAY,        // k_gossip_replay: sends of a pair with a cached contact (isInfected replay)
   FB_MQ,            // P1: more than mq_cap inbound SYNC messages, selected in key order by list walks
   FB_SORT_MERGE,    // k_seg_sort: a receipt segment above sort_cap sorted in runs and merged
+  FB_RX_ALL,        // a contact pair without an RX row (more than rx_cap this tick): its whole window replayed
   FB_N = 16
 };
 
@@ -172,6 +174,13 @@ struct Dev {
   uint32_t *tin_cnt, *tin_off, *tin_fill, *tin;  // [N], [N], [N], [N * F] = m * F + s
   uint32_t *tlist, *ntl;                         // targets with senders this tick
   uint32_t* rt0;                                 // [N] a target's ring end before this tick's receipts
+  // pairs with a logged contact: only the sender's window gossips received no later than the latest contact can
+  // have the target in infectedFrom (replayed); the rest are sent normally. RX row r marks the former for one pair.
+  uint32_t* crow;                                // [N * F] RX row of the pair (m, s), RX_ALL: every window gossip
+  unsigned long long* RX;                        // [CRCAP][QW]
+  uint32_t* rxl;                                 // [CRCAP][3] (m * F + s, first, end ring position)
+  uint32_t *nrx, CRCAP;
+  uint32_t *cfl, *ncfl;                          // [N * F] pairs with a logged contact this tick (k_contact_cache)
   uint32_t EXPB;  // ticks after its latest creation or receipt by which every holder has swept a gossip (slot_exp)
 
   // ---- gossip slots ----

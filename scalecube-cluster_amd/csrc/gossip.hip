@@ -252,7 +252,7 @@ __global__ void __launch_bounds__(1024) k_gossip_groups(Dev d) {
   __shared__ uint32_t base;
   if (threadIdx.x == 0) {
     base = 0;
-    *d.slow_n = *d.rp_n = *d.nrwl = *d.ntl = *d.xd_n = *d.nfexp = 0;
+    *d.slow_n = *d.rp_n = *d.nrwl = *d.ntl = *d.xd_n = *d.nfexp = *d.nrx = *d.ncfl = 0;
   }
   __syncthreads();
   for (uint32_t q0 = 0; q0 < d.QW; q0 += 1024) {
@@ -336,20 +336,35 @@ __global__ void k_tin_scatter(Dev d) {
   }
 }
 
-// 4. the rounds' holder-state changes (sweepGossips :283-308 and the window of selectGossipsToSend :239-250), one
-// workgroup per round member with work. Ring ranges (positions; see k_round_plan):
+// 4. the rounds' holder-state changes (sweepGossips :283-308 and the window of selectGossipsToSend :239-250), a
+// wavefront (rows up to RCS words) or a workgroup (larger rows) per round member with work. Ring ranges (positions;
+// see k_round_plan):
 //   [h, send)                      swept: HB cleared, S marked SWEPT, the gossip count drops
 //   [max(w0, h), min(seen, wnew))  out of the window: WB cleared (includes the swept entries that were in it)
 //   [wnew, max(w0, h))             back in the window (the spread grew): WB set
 //   [max(seen, wnew), tail)        received or created since the member's previous round: WB set
-// Few changes: one global atomic per entry. Many: the member's HB / WB rows are staged through LDS in chunks of
-// RCW words, so every word is read and written once per chunk.
-constexpr uint32_t RCW = 4096;
+// Few changes (<= 64): one global atomic per entry. More: the member's HB / WB rows are staged through LDS in chunks
+// of RCW words, so every word is read and written once per chunk and the bits change by LDS atomics.
+constexpr uint32_t RCW = 4096;  // words per row chunk, block per member (large rows)
+constexpr uint32_t RCS = 1024;  // words per row, wave per member (rows of up to 65 536 slots)
+
+// a cooperative group of threads: one workgroup (BLOCK) or one wavefront
+template <bool BLOCK>
+__device__ __forceinline__ void grp_sync() {
+  if (BLOCK) {
+    __syncthreads();
+  } else {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 __device__ __forceinline__ void rr_bits(const Dev& d, uint32_t m, uint32_t a, uint32_t b, uint32_t op,
-                                        unsigned long long* lh, unsigned long long* lw, uint32_t c0, uint32_t c1) {
+                                        unsigned long long* lh, unsigned long long* lw, uint32_t c0, uint32_t c1,
+                                        uint32_t tid, uint32_t nth) {
   const uint32_t* R = ring(d, m);
   const uint32_t mask = d.BCAP - 1;
-  for (uint32_t p = a + threadIdx.x; p - a < b - a; p += blockDim.x) {
+  for (uint32_t p = a + tid; p - a < b - a; p += nth) {
     const uint32_t g = R[p & mask] & RG_SLOT, q = g >> 6;
     const unsigned long long bit = 1ull << (g & 63u);
     if (lh) {  // LDS chunk [c0, c1) of the rows
@@ -365,98 +380,89 @@ __device__ __forceinline__ void rr_bits(const Dev& d, uint32_t m, uint32_t a, ui
   }
 }
 
-__global__ void __launch_bounds__(256) k_round_apply(const Dev* __restrict__ dp, uint32_t k) {
+// one round member's ring ranges (see above) by a group of nth threads; lh / lw: LDS rows of cw words
+template <bool BLOCK>
+__device__ void round_member(const Dev& d, uint32_t m, uint32_t k, unsigned long long* lh, unsigned long long* lw,
+                             uint32_t cw, uint32_t span, uint32_t tid, uint32_t nth) {
+  const uint32_t h = d.rhead[m], send = d.rsend[m], wnew = d.rwnew[m], tl = d.rtail[m], seen = d.rseen[m];
+  const uint32_t w0 = (int32_t)(d.rwin[m] - h) > 0 ? d.rwin[m] : h;
+  const uint32_t r2 = (int32_t)(seen - wnew) < 0 ? seen : wnew;  // min(seen, wnew)
+  const uint32_t r4 = (int32_t)(seen - wnew) > 0 ? seen : wnew;  // max(seen, wnew)
+  const uint32_t r3 = (int32_t)(w0 - wnew) > 0 ? w0 : wnew;      // end of the re-entry range
+  // side effects of the sweeps (sweepGossips :283-308; on_sweep: a completed leave)
+  const uint32_t* R = ring(d, m);
+  for (uint32_t p = h + tid; p - h < send - h; p += nth) {
+    const uint32_t g = R[p & (d.BCAP - 1)] & RG_SLOT;
+    d.S[(size_t)g * d.N + m] |= S_SWEPT;
+    on_sweep(d, g, m, k);
+  }
+  const uint32_t nch = (send - h) + ((int32_t)(r2 - w0) > 0 ? r2 - w0 : 0u) + (r3 - wnew) + (tl - r4);
+  if (nch <= 64 || span == 0) {  // few changes: atomics on the rows
+    rr_bits(d, m, h, send, 0, nullptr, nullptr, 0, 0, tid, nth);
+    if ((int32_t)(r2 - w0) > 0) rr_bits(d, m, w0, r2, 1, nullptr, nullptr, 0, 0, tid, nth);
+    rr_bits(d, m, wnew, r3, 2, nullptr, nullptr, 0, 0, tid, nth);
+    rr_bits(d, m, r4, tl, 2, nullptr, nullptr, 0, 0, tid, nth);
+  } else {
+    for (uint32_t c0 = 0; c0 < span; c0 += cw) {
+      const uint32_t c1 = min(span, c0 + cw);
+      unsigned long long* H = hrow(d, m) + c0;
+      unsigned long long* Wr = wrow(d, m) + c0;
+      for (uint32_t j = tid; j < c1 - c0; j += nth) {
+        lh[j] = H[j];
+        lw[j] = Wr[j];
+      }
+      grp_sync<BLOCK>();
+      rr_bits(d, m, h, send, 0, lh, lw, c0, c1, tid, nth);
+      if ((int32_t)(r2 - w0) > 0) rr_bits(d, m, w0, r2, 1, lh, lw, c0, c1, tid, nth);
+      rr_bits(d, m, wnew, r3, 2, lh, lw, c0, c1, tid, nth);
+      rr_bits(d, m, r4, tl, 2, lh, lw, c0, c1, tid, nth);
+      grp_sync<BLOCK>();
+      for (uint32_t j = tid; j < c1 - c0; j += nth) {
+        H[j] = lh[j];
+        Wr[j] = lw[j];
+      }
+      grp_sync<BLOCK>();
+    }
+  }
+  if (tid == 0) {
+    d.rhead[m] = send;
+    d.rwin[m] = wnew;
+    d.rseen[m] = tl;
+    if (send != h) {
+      if (d.XW > 1)
+        atomicSub(&d.held_delta[m], (int)(send - h));
+      else
+        atomicSub(&d.held[m], send - h);
+    }
+  }
+}
+
+// rows of up to RCS words: one wavefront per round member (16 KB of LDS each, four per workgroup)
+__global__ void __launch_bounds__(256) k_round_apply_w(const Dev* __restrict__ dp, uint32_t k) {
+  const Dev& d = *dp;
+  __shared__ unsigned long long lh[4][RCS], lw[4][RCS];
+  const uint32_t n = *d.nrwl, span = d.nagroup[1], wave = threadIdx.x >> 6;
+  if (span > RCS) return;  // k_round_apply_b
+  for (uint32_t i = blockIdx.x * 4 + wave; i < n; i += gridDim.x * 4)
+    round_member<false>(d, d.rwl[i], k, lh[wave], lw[wave], RCS, span, threadIdx.x & 63u, 64u);
+}
+
+// larger rows: one workgroup per round member, the rows staged in chunks of RCW words
+__global__ void __launch_bounds__(256) k_round_apply_b(const Dev* __restrict__ dp, uint32_t k) {
   const Dev& d = *dp;
   __shared__ unsigned long long lh[RCW], lw[RCW];
-  __shared__ uint32_t swept;
   const uint32_t n = *d.nrwl, span = d.nagroup[1];
+  if (span <= RCS) return;  // k_round_apply_w
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-    const uint32_t m = d.rwl[i];
-    const uint32_t h = d.rhead[m], send = d.rsend[m], wnew = d.rwnew[m], tl = d.rtail[m], seen = d.rseen[m];
-    const uint32_t w0 = (int32_t)(d.rwin[m] - h) > 0 ? d.rwin[m] : h;
-    const uint32_t r2 = (int32_t)(seen - wnew) < 0 ? seen : wnew;  // min(seen, wnew)
-    const uint32_t r4 = (int32_t)(seen - wnew) > 0 ? seen : wnew;  // max(seen, wnew)
-    const uint32_t r3 = (int32_t)(w0 - wnew) > 0 ? w0 : wnew;      // end of the re-entry range
-    // side effects of the sweeps, once (sweepGossips :283-308; on_sweep: a completed leave)
-    if (threadIdx.x == 0) swept = 0;
-    __syncthreads();
-    {
-      const uint32_t* R = ring(d, m);
-      uint32_t c = 0;
-      for (uint32_t p = h + threadIdx.x; p - h < send - h; p += blockDim.x) {
-        const uint32_t g = R[p & (d.BCAP - 1)] & RG_SLOT;
-        d.S[(size_t)g * d.N + m] |= S_SWEPT;
-        on_sweep(d, g, m, k);
-        ++c;
-      }
-      if (c) atomicAdd(&swept, c);
-    }
-    const uint32_t nch = (send - h) + ((int32_t)(r2 - w0) > 0 ? r2 - w0 : 0u) + (r3 - wnew) + (tl - r4);
-    if (nch <= 512 || span == 0) {  // few changes: atomics on the rows
-      rr_bits(d, m, h, send, 0, nullptr, nullptr, 0, 0);
-      if ((int32_t)(r2 - w0) > 0) rr_bits(d, m, w0, r2, 1, nullptr, nullptr, 0, 0);
-      rr_bits(d, m, wnew, r3, 2, nullptr, nullptr, 0, 0);
-      rr_bits(d, m, r4, tl, 2, nullptr, nullptr, 0, 0);
-    } else {
-      for (uint32_t c0 = 0; c0 < span; c0 += RCW) {
-        const uint32_t c1 = min(span, c0 + RCW);
-        unsigned long long* H = hrow(d, m) + c0;
-        unsigned long long* Wr = wrow(d, m) + c0;
-        for (uint32_t j = threadIdx.x; j < c1 - c0; j += blockDim.x) {
-          lh[j] = H[j];
-          lw[j] = Wr[j];
-        }
-        __syncthreads();
-        rr_bits(d, m, h, send, 0, lh, lw, c0, c1);
-        if ((int32_t)(r2 - w0) > 0) rr_bits(d, m, w0, r2, 1, lh, lw, c0, c1);
-        rr_bits(d, m, wnew, r3, 2, lh, lw, c0, c1);
-        rr_bits(d, m, r4, tl, 2, lh, lw, c0, c1);
-        __syncthreads();
-        for (uint32_t j = threadIdx.x; j < c1 - c0; j += blockDim.x) {
-          H[j] = lh[j];
-          Wr[j] = lw[j];
-        }
-        __syncthreads();
-      }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      d.rhead[m] = send;
-      d.rwin[m] = wnew;
-      d.rseen[m] = tl;
-      if (swept) {
-        if (d.XW > 1)
-          atomicSub(&d.held_delta[m], (int)swept);
-        else
-          atomicSub(&d.held[m], swept);
-      }
-    }
+    round_member<true>(d, d.rwl[i], k, lh, lw, RCW, span, threadIdx.x, blockDim.x);
     __syncthreads();
   }
 }
 
 // 5. contact lists: did target t = T[m][s] choose m in a logged round inside the look-back window? If so, cache the
-// pair's contact events in both directions (independent of the gossip) for blocked_pair_cached. One thread per
-// (sender, target) pair of this shard's targets.
-__global__ void k_gossip_contacts(Dev d, uint32_t k) {
-  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t np = d.tin_off[d.N - 1] + d.tin_cnt[d.N - 1];  // exclusive scan: the total is the last offset + count
-  if (p >= np) return;
-  const uint32_t i = d.tin[p], m = i / d.F, t = d.T[i];
-  uint32_t flag = 0;
-  for (uint32_t e = 0; e < d.LOGW && !flag; ++e) {
-    size_t lo = (size_t)t * d.LOGW + e;
-    uint32_t t2 = d.log_tick[lo];
-    if (t2 == NEVER || t2 >= k) continue;
-    uint32_t n = d.log_cnt[lo];
-    for (uint32_t s2 = 0; s2 < n; ++s2)
-      if (d.log_tg[lo * d.F + s2] == m) flag = 1;
-  }
-  d.tcontact[i] = flag;
-  if (!flag) {
-    d.cin[i] = NEVER;
-    return;
-  }
+// pair's contact events in both directions (independent of the gossip) for blocked_pair_cached. One wave per target
+// of this shard: its lanes read the target's round log once (coalesced) and test every sender of the target against it.
+__device__ void contact_cache(const Dev& d, uint32_t i, uint32_t m, uint32_t t, uint32_t k) {
   Contact ev[CEV];
   uint32_t oldest[2];
   uint32_t* rec = d.cev + (size_t)i * CEVW;
@@ -476,10 +482,100 @@ __global__ void k_gossip_contacts(Dev d, uint32_t k) {
   // a gossip inside m's window this round was created after tick k - (spread + 1) * gossip_t, so a contact t -> m
   // at or before that tick - lat can never put t in infectedFrom_m of any gossip m sends now
   const int64_t horizon = (int64_t)k - (int64_t)(d.tspread[m] + 1u) * d.gossip_t;
+  uint32_t ci;
   if (n > CEV)
-    d.cin[i] = CIN_SLOW;
+    ci = CIN_SLOW;
   else
-    d.cin[i] = last_in == NEVER || (int64_t)last_in + d.lat <= horizon ? NEVER : last_in;
+    ci = last_in == NEVER || (int64_t)last_in + d.lat <= horizon ? NEVER : last_in;
+  d.crow[i] = RX_ALL;
+  if (ci != NEVER && ci != CIN_SLOW) {
+    // Only gossips m received at or before the latest contact t -> m arrived (last_in + lat) can have t in
+    // infectedFrom_m. Their infection periods are at most B1 = rounds_before(last_in + lat + 1); the window entries
+    // of m's ring with a period above B1 were received later (sorted ring: a suffix) and are sent normally.
+    const uint32_t P = d.tperiod[m], B1 = rounds_before(d, m, last_in + d.lat + 1u);
+    const uint32_t* R = ring(d, m);
+    const uint32_t w0 = d.rwin[m], tl = d.rseen[m];  // the window as k_round_apply left it for this round
+    uint32_t lo = 0, hi = tl - w0;
+    while (lo < hi) {
+      const uint32_t mid = lo + (hi - lo) / 2;
+      if (rg_period(R[(w0 + mid) & (d.BCAP - 1)], P) <= (int64_t)B1)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    if (lo == 0) {
+      ci = NEVER;  // every window gossip arrived after the contact: no replay at all
+    } else if (lo < tl - w0) {
+      const uint32_t r = atomicAdd(d.nrx, 1u);
+      if (r < d.CRCAP) {
+        d.crow[i] = r;
+        d.rxl[3 * r] = i;
+        d.rxl[3 * r + 1] = w0;
+        d.rxl[3 * r + 2] = w0 + lo;
+      } else {
+        fb_add(d, FB_RX_ALL);
+      }
+    }
+  }
+  d.cin[i] = ci;
+}
+
+// the RX rows of this tick's contact pairs: bit g set for the window gossips received no later than the contact (one
+// workgroup per row, staged through LDS in chunks of RCW words)
+constexpr uint32_t RXW = 8192;
+__global__ void __launch_bounds__(256) k_rx_build(const Dev* __restrict__ dp) {
+  const Dev& d = *dp;
+  __shared__ unsigned long long lr[RXW];
+  const uint32_t n = min(*d.nrx, d.CRCAP), span = d.nagroup[1];
+  for (uint32_t r = blockIdx.x; r < n; r += gridDim.x) {
+    const uint32_t m = d.rxl[3 * r] / d.F, a = d.rxl[3 * r + 1], b = d.rxl[3 * r + 2];
+    const uint32_t* R = ring(d, m);
+    unsigned long long* row = d.RX + (size_t)r * d.QW;
+    for (uint32_t c0 = 0; c0 < span; c0 += RXW) {
+      const uint32_t c1 = min(span, c0 + RXW);
+      for (uint32_t j = threadIdx.x; j < c1 - c0; j += blockDim.x) lr[j] = 0ull;
+      __syncthreads();
+      for (uint32_t p = a + threadIdx.x; p - a < b - a; p += blockDim.x) {
+        const uint32_t g = R[p & (d.BCAP - 1)] & RG_SLOT, q = g >> 6;
+        if (q >= c0 && q < c1) atomicOr(&lr[q - c0], 1ull << (g & 63u));
+      }
+      __syncthreads();
+      for (uint32_t j = threadIdx.x; j < c1 - c0; j += blockDim.x) row[c0 + j] = lr[j];
+      __syncthreads();
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_gossip_contacts(Dev d, uint32_t k) {
+  const uint32_t lane = threadIdx.x & 63u, ntl = *d.ntl;
+  for (uint32_t ti = blockIdx.x * 4 + (threadIdx.x >> 6); ti < ntl; ti += gridDim.x * 4) {
+    const uint32_t t = d.tlist[ti], o = d.tin_off[t], ns = d.tin_cnt[t];
+    for (uint32_t p = 0; p < ns; ++p) {
+      const uint32_t i = d.tin[o + p], m = i / d.F;
+      bool hit = false;
+      for (uint32_t e = lane; e < d.LOGW && !hit; e += 64) {
+        const size_t lo = (size_t)t * d.LOGW + e;
+        const uint32_t t2 = d.log_tick[lo];
+        if (t2 == NEVER || t2 >= k) continue;
+        const uint32_t n = d.log_cnt[lo];
+        for (uint32_t s2 = 0; s2 < n; ++s2) hit |= d.log_tg[lo * d.F + s2] == m;
+      }
+      const bool flag = __ballot(hit) != 0ull;
+      if (lane != 0) continue;
+      d.tcontact[i] = flag ? 1u : 0u;
+      d.cin[i] = NEVER;
+      if (flag) d.cfl[atomicAdd(d.ncfl, 1u)] = i;  // its contact events are cached by k_contact_cache
+    }
+  }
+}
+
+// the flagged pairs' contact caches, one thread each (two log scans per pair: in parallel, not behind a wave's lane 0)
+__global__ void k_contact_cache(Dev d, uint32_t k) {
+  const uint32_t n = *d.ncfl;
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+    const uint32_t i = d.cfl[j];
+    contact_cache(d, i, i / d.F, d.T[i], k);
+  }
 }
 
 // a first receipt of (g, t) at this tick (one lane owns it): the receiver-side bookkeeping that does not depend on
@@ -508,62 +604,80 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
   for (uint64_t i0 = ((uint64_t)blockIdx.x * 4 + wave) * 64; i0 < items; i0 += (uint64_t)gridDim.x * 256) {
     const uint64_t i = i0 + lane;
     const bool act = i < items;
-    uint32_t t = NEVER, q = 0;
+    uint32_t t = NEVER, q = 0, o = 0, ns = 0;
     unsigned long long nb = 0, h = 0;
     if (act) {
       t = d.tlist[(uint32_t)(i / nag)];
       q = d.agroup[(uint32_t)(i % nag)];
       h = hrow(d, t)[q];
-      const uint32_t o = d.tin_off[t], ns = d.tin_cnt[t];
-      for (uint32_t p = 0; p < ns; ++p) {
-        const uint32_t ms = d.tin[o + p], m = ms / d.F, s = ms - m * d.F;
-        const unsigned long long w = wrow(d, m)[q];
-        if (!w) continue;
-        if (d.exp & 4) st[0]++;
-        const uint32_t ci = d.cin[ms];
-        if (ci != NEVER) {  // a logged contact: every slot of the pair is replayed (slow path past the cache)
-          const uint32_t c = (uint32_t)__popcll(w);
-          if (d.exp & 4) st[1] += c;
-          const bool slow = ci == CIN_SLOW;
-          fb_add(d, slow ? FB_CEV_SLOW : FB_REPLAY, c);
-          uint32_t j = atomicAdd(slow ? d.slow_n : d.rp_n, c);
-          for (unsigned long long b = w; b; b &= b - 1, ++j) {
-            const uint64_t v = ((uint64_t)(q * 64u + (uint32_t)(__ffsll((long long)b) - 1)) << 32) | ms;
-            if (j < (slow ? d.SLOWCAP : d.RPCAP))
-              (slow ? d.slow : d.rp)[j] = v;
-            else
-              set_err(d, E_CONTACTS);
-          }
-          continue;
+      o = d.tin_off[t];
+      ns = d.tin_cnt[t];
+    }
+    // the senders loop is wave-uniform (lanes past their own target's senders idle), so the replay lists take one
+    // atomic per wave
+    uint32_t nsw = ns;
+#pragma unroll
+    for (uint32_t x = 32; x > 0; x >>= 1) nsw = max(nsw, (uint32_t)__shfl_xor(nsw, x));
+    for (uint32_t p = 0; p < nsw; ++p) {
+      uint32_t ms = 0, m = 0, s = 0, ci = NEVER;
+      unsigned long long w = 0, wr = 0;
+      if (p < ns) {
+        ms = d.tin[o + p];
+        m = ms / d.F;
+        s = ms - m * d.F;
+        w = wrow(d, m)[q];
+        if (w) ci = d.cin[ms];
+        if (ci != NEVER) {  // a logged contact: the gossips that can have t in infectedFrom are replayed
+          const uint32_t r = ci == CIN_SLOW ? RX_ALL : d.crow[ms];
+          wr = r == RX_ALL ? w : w & d.RX[(size_t)r * d.QW + q];
+          w &= ~wr;
         }
-        sends += __popcll(w);
-        if (d.dbg_send) {  // debugging aid: every counted send
-          for (unsigned long long b = w; b; b &= b - 1) {
-            const uint32_t di = atomicAdd(d.dbg_send_n, 1u);
-            if (di >= d.dbg_send_cap) break;
-            const uint64_t gid = d.slot_gid[q * 64u + (uint32_t)(__ffsll((long long)b) - 1)];
-            uint32_t* r = d.dbg_send + (size_t)di * 5;
-            r[0] = k, r[1] = m, r[2] = (uint32_t)gid, r[3] = (uint32_t)(gid >> 32), r[4] = t;
-          }
+      }
+      if ((w | wr) && (d.exp & 4)) st[0]++;
+      // (the slow path past the contact cache replays from a full scan of both round logs)
+      const bool slow = ci == CIN_SLOW;
+      if (__ballot(wr != 0ull)) {
+        const uint32_t c = (uint32_t)__popcll(wr);
+        if (d.exp & 4) st[1] += c;
+        fb_add(d, slow ? FB_CEV_SLOW : FB_REPLAY, c);
+        uint32_t jr = wave_reserve(d.rp_n, slow ? 0u : c), js = wave_reserve(d.slow_n, slow ? c : 0u);
+        uint32_t j = slow ? js : jr;
+        for (unsigned long long b = wr; b; b &= b - 1, ++j) {
+          const uint64_t v = ((uint64_t)(q * 64u + (uint32_t)(__ffsll((long long)b) - 1)) << 32) | ms;
+          if (j < (slow ? d.SLOWCAP : d.RPCAP))
+            (slow ? d.slow : d.rp)[j] = v;
+          else
+            set_err(d, E_CONTACTS);
         }
-        const unsigned long long cand = w & ~h & ~nb;
-        if (!cand) continue;
-        if (d.exp & 4) st[3] += (uint32_t)__popcll(cand);
-        if (ep < 0) {
-          set_err(d, E_EPOCH);
-          continue;
+      }
+      if (!w) continue;
+      sends += __popcll(w);
+      if (d.dbg_send) {  // debugging aid: every counted send
+        for (unsigned long long b = w; b; b &= b - 1) {
+          const uint32_t di = atomicAdd(d.dbg_send_n, 1u);
+          if (di >= d.dbg_send_cap) break;
+          const uint64_t gid = d.slot_gid[q * 64u + (uint32_t)(__ffsll((long long)b) - 1)];
+          uint32_t* r = d.dbg_send + (size_t)di * 5;
+          r[0] = k, r[1] = m, r[2] = (uint32_t)gid, r[3] = (uint32_t)(gid >> 32), r[4] = t;
         }
-        const uint32_t pct = link_loss(d, ep, m, t, k);
-        if (pct == 0) {
-          nb |= cand;
-        } else if (pct < 100) {
-          for (unsigned long long b = cand; b; b &= b - 1) {
-            const uint32_t j = (uint32_t)(__ffsll((long long)b) - 1);
-            const uint64_t gid = d.slot_gid[q * 64u + j];
-            const u32x4 r = philox(m, k ^ ((s >> 2) << 31), (uint32_t)(gid >> 32), (uint32_t)gid,
-                                   d.seed_lo ^ SALT_LOSS_GOSSIP, d.seed_hi);  // lost_gossip_ep's draw
-            if (!(next_int(pick(r, s & 3), 100) < pct)) nb |= 1ull << j;
-          }
+      }
+      const unsigned long long cand = w & ~h & ~nb;
+      if (!cand) continue;
+      if (d.exp & 4) st[3] += (uint32_t)__popcll(cand);
+      if (ep < 0) {
+        set_err(d, E_EPOCH);
+        continue;
+      }
+      const uint32_t pct = link_loss(d, ep, m, t, k);
+      if (pct == 0) {
+        nb |= cand;
+      } else if (pct < 100) {
+        for (unsigned long long b = cand; b; b &= b - 1) {
+          const uint32_t j = (uint32_t)(__ffsll((long long)b) - 1);
+          const uint64_t gid = d.slot_gid[q * 64u + j];
+          const u32x4 r = philox(m, k ^ ((s >> 2) << 31), (uint32_t)(gid >> 32), (uint32_t)gid,
+                                 d.seed_lo ^ SALT_LOSS_GOSSIP, d.seed_hi);  // lost_gossip_ep's draw
+          if (!(next_int(pick(r, s & 3), 100) < pct)) nb |= 1ull << j;
         }
       }
     }
@@ -588,14 +702,17 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
     if (act && nb) {
       hrow(d, t)[q] = h | nb;  // the lane owns (t, q) in this kernel: later receipts of the tick see it held
       if (nb & d.DM[q]) d.dead_rx[t] = k + d.lat;  // a DEAD membership record arrives in P4 of k + lat
+      // the receipts' ring entries (receipt_mark, with the loop-invariant parts hoisted)
+      const uint32_t tag = rounds_before(d, t, k + d.lat) << 22, mask = d.BCAP - 1;
+      uint32_t* Rt = ring(d, t);
+      if (base + c - d.rhead[t] > d.BCAP) set_err(d, E_RING);
       uint32_t pos = base;
-      for (unsigned long long b = nb; b; b &= b - 1, ++pos) {
-        const uint32_t g = q * 64u + (uint32_t)(__ffsll((long long)b) - 1);
-        receipt_mark(d, g, t, k, pos);
-        if (d.W > 1) {  // replicated on the other shards from exchange B
-          const uint32_t xi = atomicAdd(d.xd_n, 1u);
+      for (unsigned long long b = nb; b; b &= b - 1, ++pos) Rt[pos & mask] = (q * 64u + (uint32_t)(__ffsll((long long)b) - 1)) | tag;
+      if (d.W > 1) {  // replicated on the other shards from exchange B
+        uint32_t xi = atomicAdd(d.xd_n, c);
+        for (unsigned long long b = nb; b; b &= b - 1, ++xi) {
           if (xi < d.DCAP)
-            d.xd[xi] = ((uint64_t)g << 32) | t;
+            d.xd[xi] = ((uint64_t)(q * 64u + (uint32_t)(__ffsll((long long)b) - 1)) << 32) | t;
           else
             set_err(d, E_DELIV);
         }
@@ -727,20 +844,31 @@ __global__ void __launch_bounds__(256) k_gossip_apply(const Dev* __restrict__ dp
     const uint32_t* R = ring(d, t);
     uint32_t drops = 0;
     unsigned long long eh = 0;
-    for (uint32_t p = a + lane; p - a < b - a; p += 64) {
-      const uint32_t g = R[p & (d.BCAP - 1)] & RG_SLOT;
-      receipt_create(d, g, t, k);
-      if (d.fastp4 && d.slot_subj[g] == USER_SUBJ) {  // RUMOR mode: the GOSSIP event of P4 (k + lat), hashed now
-        const uint64_t gid = d.slot_gid[g], key = d.slot_key[g];
-        const uint64_t ev = ((uint64_t)(k + d.lat) << 32) | (3ull << 30) | (uint32_t)(gid >> 32);
-        const uint64_t meta = ((uint64_t)(uint32_t)key << 32) | (key >> 32);  // (oldMeta, newMeta) = payload (lo, hi)
-        eh += hpair(hpair(ev, meta), (uint32_t)gid);
-      } else if (!receipt_matters(d, t, g, k + d.lat)) {  // counted as a record compare in P4, nothing else
-        drops++;
-      } else {
-        const uint32_t ri = wave_append(d.rc_n);
+    // batches of 64 entries per lane: which ones are routed to P4 is kept as a bit per entry, then the wave reserves
+    // their places in the routing list with one atomic (a per-entry append would serialise on rc_n)
+    for (uint32_t p0 = a; p0 - a < b - a; p0 += 64u * 64u) {
+      unsigned long long routed = 0;
+      for (uint32_t it = 0; it < 64; ++it) {
+        const uint32_t p = p0 + it * 64u + lane;
+        if (p - a >= b - a) break;
+        const uint32_t g = R[p & (d.BCAP - 1)] & RG_SLOT;
+        receipt_create(d, g, t, k);
+        if (d.fastp4 && d.slot_subj[g] == USER_SUBJ) {  // RUMOR mode: the GOSSIP event of P4 (k + lat), hashed now
+          const uint64_t gid = d.slot_gid[g], key = d.slot_key[g];
+          const uint64_t ev = ((uint64_t)(k + d.lat) << 32) | (3ull << 30) | (uint32_t)(gid >> 32);
+          const uint64_t meta = ((uint64_t)(uint32_t)key << 32) | (key >> 32);  // (oldMeta, newMeta) = payload (lo, hi)
+          eh += hpair(hpair(ev, meta), (uint32_t)gid);
+        } else if (!receipt_matters(d, t, g, k + d.lat)) {  // counted as a record compare in P4, nothing else
+          drops++;
+        } else {
+          routed |= 1ull << it;
+        }
+      }
+      uint32_t ri = wave_reserve(d.rc_n, (uint32_t)__popcll(routed));
+      for (; routed; routed &= routed - 1, ++ri) {
+        const uint32_t p = p0 + (uint32_t)(__ffsll((long long)routed) - 1) * 64u + lane;
         if (ri < d.RCAP)
-          d.rc_raw[ri] = ((uint64_t)t << 32) | g;
+          d.rc_raw[ri] = ((uint64_t)t << 32) | (R[p & (d.BCAP - 1)] & RG_SLOT);
         else
           set_err(d, E_RECEIPTS);
       }
@@ -826,8 +954,11 @@ void launch_gossip_send(const Dev& d, uint32_t k, hipStream_t st, const TickEven
   hipLaunchKernelGGL(k_round_plan, dim3(cdiv(d.N, 256)), dim3(256), 0, st, d, k);
   launch_scan(d.tin_cnt, d.tin_off, d.scan_part, d.N, st);
   hipLaunchKernelGGL(k_tin_scatter, dim3(cdiv(d.N, 256)), dim3(256), 0, st, d);
-  hipLaunchKernelGGL(k_round_apply, dim3(4096), dim3(256), 0, st, d.self, k);
-  hipLaunchKernelGGL(k_gossip_contacts, dim3(cdiv((uint64_t)d.N * d.F, 256)), dim3(256), 0, st, d, k);
+  hipLaunchKernelGGL(k_round_apply_w, dim3(4096), dim3(256), 0, st, d.self, k);
+  hipLaunchKernelGGL(k_round_apply_b, dim3(2048), dim3(256), 0, st, d.self, k);
+  hipLaunchKernelGGL(k_gossip_contacts, dim3(2048), dim3(256), 0, st, d, k);
+  hipLaunchKernelGGL(k_contact_cache, dim3(256), dim3(64), 0, st, d, k);
+  hipLaunchKernelGGL(k_rx_build, dim3(512), dim3(256), 0, st, d.self);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[4], st);
   hipLaunchKernelGGL(k_gossip_send, dim3(SEND_GRID), dim3(256), 0, st, d.self, k);
   hipLaunchKernelGGL(k_gossip_send_slow, dim3(64), dim3(64), 0, st, d.self, k);  // rare; ~14 KB of stack per lane

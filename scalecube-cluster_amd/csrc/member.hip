@@ -160,7 +160,9 @@ __device__ __forceinline__ bool send_sync(ML& L, uint32_t kind, uint32_t dst, ui
     return false;
   }
   uint32_t b = L.k & 1;
-  uint32_t i = atomicAdd(&d.nmsg[b], 1u);
+  // one atomic per wave for the lanes sending here together: ~1 300 SYNC / SYNC_ACK sends per tick at C3 on one
+  // counter would otherwise serialise at its L2 channel (~90 per µs)
+  uint32_t i = wave_append(&d.nmsg[b]);
   if (i >= d.MSGCAP) {
     set_err(d, E_MSGS);
     return true;

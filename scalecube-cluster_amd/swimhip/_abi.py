@@ -194,7 +194,7 @@ def selftest_eval(lib, op, rows, device=0):
 
 
 # include/swimhip_debug.h (capacity-fallback counters; libswimhip only, with SWIM_CAPS / SWIM_FALLBACKS at create)
-FB_NAMES = ["trk_walk", "ulog", "creq", "cwmax", "cev_slow", "replay", "mq", "sort_merge"]
+FB_NAMES = ["trk_walk", "ulog", "creq", "cwmax", "cev_slow", "replay", "mq", "sort_merge", "rx_all"]
 DEBUG_SIGNATURES = {
     "swim_debug_fallbacks": (C.c_int, [_H, C.POINTER(C.c_uint64), C.c_size_t]),
 }

@@ -17,7 +17,7 @@ from test_gpu_fuzz import play, schedule
 
 pytestmark = pytest.mark.gpu
 
-TINY = "trk=1,ulog=1,creq=1,cwmax=1,cev=1,mq=1,sort=2"
+TINY = "trk=1,ulog=1,creq=1,cwmax=1,cev=1,mq=1,sort=2,rx=1"
 
 
 def _engine(engine, cfg, monkeypatch, caps=TINY, shards=1):
@@ -65,7 +65,7 @@ def test_tiny_caps_fallbacks_all_fire(oracle, engine, monkeypatch):
         for k, v in _fallbacks(engine, e).items():
             total[k] = total.get(k, 0) + v
         e.close()
-    for k in ("trk_walk", "ulog", "creq", "cwmax", "cev_slow", "mq", "sort_merge"):
+    for k in ("trk_walk", "ulog", "creq", "cwmax", "cev_slow", "mq", "sort_merge", "rx_all"):
         assert total[k] > 0, (k, total)
 
 
