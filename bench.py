@@ -263,7 +263,9 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "u32",  # record keys: inc << 2 | status (30-bit incarnation, SEMANTICS.md §8), u32 list entries
+            # record keys are u32 `inc << 2 | status`: incarnations are capped at 2^30 - 1 (Java int: 2^31 - 1), past
+            # which the engine raises SWIM_ECAPACITY (SEMANTICS.md §8); list entries are u32 member ids
+            "dtype": "u32 (record key inc<<2|status: 30-bit incarnation cap)",
             "data": "synthetic (PRECONVERGED full views, seeded Philox selector)",
             "config": {"workload": workload_name(a, n),
                        "members": n, "periods_per_step": 1, "ticks_per_period": ticks_per_period,

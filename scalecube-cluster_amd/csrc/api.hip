@@ -66,6 +66,8 @@ struct swim_handle {
   hipEvent_t ev_member = nullptr;
   bool no_skip = getenv("SWIM_NO_GOSSIP_SKIP") != nullptr;  // debugging aid: always run the gossip data plane
   bool no_pipe = getenv("SWIM_NO_PIPELINE") != nullptr;    // debugging aid: no early SYNC diff of the next tick
+  bool no_spec = getenv("SWIM_NO_SPECULATION") != nullptr;  // debugging aid: a host wait after every member kernel
+  bool gossip_idle = false;  // W == 1: no gossip slot was in use after the latest member kernel
   // timing aid (bench.py --rehearse-shard): a slot shard alone, its peers' gossip-count deltas taken as zero without
   // any exchange (not the W-shard simulation's results)
   bool lone = getenv("SWIM_LONE_SHARD") != nullptr;
@@ -421,9 +423,10 @@ int build(swim_handle* h) {
   A(d.rc_slot, d.RCAP) A(d.rc_ndrop, N) A(d.dead_rx, N) A(d.leaving, N) A(d.rc_key, d.RCAP) A(d.rc_slot2, d.RCAP) A(d.rc_key2, d.RCAP) A(d.fexp, d.SLOTS) A(d.nfexp, 1) A(d.hist, (uint64_t)d.HCAP * HREC)
   A(d.msgs[0], d.MSGCAP) A(d.msgs[1], d.MSGCAP) A(d.nmsg, 2) A(d.arena[0], (uint64_t)d.ARENA_ROWS * d.NS)
   A(d.arena[1], (uint64_t)d.ARENA_ROWS * d.NS) A(d.arena_used, 2)
-  A(d.m_next, 2ull * d.MSGCAP) A(d.m_head, 2 * N) A(d.next_evt, N) A(d.mdone, 1) A(d.trk, NL * TRK) A(d.ulog, NL * ULOG * 2) A(d.spq, NL * SPQ * 8) A(d.pending_inc, N) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
+  A(d.m_next, 2ull * d.MSGCAP) A(d.m_head, 2 * N) A(d.next_evt, N) A(d.mdone, 2) A(d.trk, NL * TRK) A(d.ulog, NL * ULOG * 2) A(d.spq, NL * SPQ * 8) A(d.pending_inc, N) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
   A(d.pool, d.POOLCAP) A(d.pool_used, 1)
   A(d.ev, (uint64_t)d.EVCAP * 8) A(d.ev_n, 1) A(d.ctr, C_NCTR) A(d.err, 8)
+  if (d.exp & 512) A(d.wt, (uint64_t)(NL + 255) / 256 * 4 * 4)
   if (d.fastp4) {
     A(d.evp_hash, N) A(d.evp_n, N)
     HIPCK(hipMemsetAsync(d.evp_hash, 0, 8 * N, h->stream));
@@ -495,7 +498,8 @@ int build(swim_handle* h) {
   HIPCK(hipMemsetAsync(d.tcnt, 0, N * 4, h->stream));
   HIPCK(hipMemsetAsync(d.ucnt, 0, N * 4, h->stream));
   HIPCK(hipMemsetAsync(d.pool_used, 0, 4, h->stream));
-  HIPCK(hipMemsetAsync(d.mdone, 0, 4, h->stream));
+  HIPCK(hipMemsetAsync(d.mdone, 0, 8, h->stream));
+  d.halt = d.mdone + 1;
   HIPCK(hipMemsetAsync(d.link_n, 0, 4, h->stream));
   HIPCK(hipMemsetAsync(d.link_key, 0, 8ull * LKCAP, h->stream));
   HIPCK(hipMemsetAsync(d.xd_n, 0, 4, h->stream));
@@ -1041,7 +1045,8 @@ int swim_step(swim_handle* h, uint32_t n) {
   auto timed = [&](uint64_t kk) {
     return profile && ((h->cfg.flags & SWIM_FLAG_PROFILE_ALL) || d.W > 1 || kk % DIFF_SAMPLE == 0);
   };
-  for (uint32_t i = 0; i < n; ++i) {
+  bool need_diff = true;  // W == 1: SYNC diff(k) not queued yet (it is queued with the previous tick when it can be)
+  for (uint32_t i = 0; i < n;) {
     const TickEvents* te = timed(h->tick) ? &h->prof[i] : nullptr;
     const uint32_t k = (uint32_t)h->tick;
     // P0 gossip creations before the member kernel: RUMOR-mode churn rumors, then the user gossips queued by the host
@@ -1058,15 +1063,51 @@ int swim_step(swim_handle* h, uint32_t n) {
       HIPCK(hipStreamSynchronize(h->stream));  // the host queue is reused after this
       h->ugq.clear();
     }
+    if (d.W == 1 && h->gossip_idle && i + 1 < n && d.XW == 1 && !d.churn && !h->no_pipe && !h->no_skip &&
+        !h->no_spec) {
+      // Speculative batch: while no gossip slot is in use the host need not look at the flag after every member
+      // kernel. The rest of the call is queued as diff / member pairs with no host wait; the member kernel after which
+      // a slot is in use raises d.halt, every later launch of the batch returns at once, and the host resumes after
+      // that tick with the gossip plane.
+      for (uint32_t j = i; j < n; ++j) {
+        const uint32_t kj = k + (j - i);
+        if (need_diff) launch_diff(d, kj, h->stream, timed(kj) ? &h->prof[j] : nullptr, true);
+        launch_member(d, kj, h->stream, timed(kj) ? &h->prof[j] : nullptr, true);
+        need_diff = j + 1 == n;
+        if (!need_diff) launch_diff(d, kj + 1, h->stream, timed(kj + 1ull) ? &h->prof[j + 1] : nullptr, true);
+      }
+      HIPCK(hipMemcpyAsync((void*)(h->hflag + 1), d.halt, 4, hipMemcpyDeviceToHost, h->stream));
+      HIPCK(hipStreamSynchronize(h->stream));
+      const uint32_t hk = h->hflag[1];
+      if (hk == 0) {  // the whole batch ran
+        h->tick += n - i;
+        i = n;
+        continue;
+      }
+      const uint32_t kh = hk - 1u;  // member(kh) ran; the launches after it returned at once
+      if (kh < k || kh >= k + (n - i)) return fail(h, SWIM_EDEVICE, "speculative batch: bad halt tick");
+      HIPCK(hipMemsetAsync(d.halt, 0, 4, h->stream));
+      const uint32_t ih = i + (kh - k);
+      launch_gossip(d, kh, h->stream, timed(kh) ? &h->prof[ih] : nullptr);
+      h->gossip_idle = false;
+      need_diff = true;  // diff(kh + 1) returned at once
+      h->tick = kh + 1ull;
+      i = ih + 1;
+      continue;
+    }
     if (d.W == 1) {
       // SYNC diff(k) was queued in the previous iteration, except for the first tick of this call
-      if (i == 0 || h->no_pipe) launch_diff(d, k, h->stream, te);
+      if (need_diff) launch_diff(d, k, h->stream, te);
       launch_member(d, k, h->stream, te);
-      HIPCK(hipEventRecord(h->ev_member, h->stream));
+      const bool nosync = (d.exp & 256) != 0;  // timing experiment: no per-tick event (gossip plane never launched)
+      if (!nosync) HIPCK(hipEventRecord(h->ev_member, h->stream));
       const bool pipe = i + 1 < n && !h->no_pipe;
       if (pipe) launch_diff(d, k + 1, h->stream, timed(k + 1ull) ? &h->prof[i + 1] : nullptr);  // overlaps the wait
-      HIPCK(hipEventSynchronize(h->ev_member));  // (a spin wait measured the same here: diff(k+1) hides the wake-up)
-      if (h->hflag[0] != 0 || h->no_skip) {
+      need_diff = !pipe;
+      if (!nosync) HIPCK(hipEventSynchronize(h->ev_member));  // (a spin wait measured the same here: diff(k+1) hides the wake-up)
+      h->gossip_idle = !nosync && h->hflag[0] == 0;
+      if (nosync) {
+      } else if (h->hflag[0] != 0 || h->no_skip) {
         launch_gossip(d, k, h->stream, te);
       } else if (te && te->all) {
         HIPCK(hipEventRecord((hipEvent_t)te->ev[4], h->stream));
@@ -1086,6 +1127,7 @@ int swim_step(swim_handle* h, uint32_t n) {
       launch_tick_c(d, k, h->stream, gossip);
     }
     h->tick++;
+    ++i;
   }
   int rc = check_err(h);
   if (rc == SWIM_OK && (d.exp & (16 | 128))) {  // timing experiments: member-kernel shader cycles per phase since the last step (16: sum over members, 128: max)
@@ -1098,6 +1140,30 @@ int swim_step(swim_handle* h, uint32_t n) {
       HIPCK(hipMemcpy(w, d.ctr + 14, sizeof(w), hipMemcpyDeviceToHost));
       HIPCK(hipMemset(d.ctr + 14, 0, sizeof(w)));
       fprintf(stderr, "exp: SYNC full walks %llu, largest candidate count %llu\n", w[0], w[1]);
+    }
+  }
+  if (rc == SWIM_OK && (d.exp & 512)) {  // timing experiment: per-wave wall clock of the latest member kernel
+    const size_t nw = (size_t)(d.NL + 255) / 256 * 4;
+    std::vector<unsigned long long> w(nw * 4);
+    HIPCK(hipMemcpy(w.data(), d.wt, w.size() * 8, hipMemcpyDeviceToHost));
+    const unsigned long long M = (1ull << 48) - 1;
+    unsigned long long t0 = ~0ull, tend = 0;
+    for (size_t i = 0; i < nw; ++i) t0 = std::min(t0, w[4 * i]), tend = std::max(tend, w[4 * i + 3]);
+    std::vector<size_t> ord(nw);
+    for (size_t i = 0; i < nw; ++i) ord[i] = i;
+    std::sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return w[4 * a + 3] > w[4 * b + 3]; });
+    double sst = 0, str = 0, sbd = 0, scw = 0;
+    for (size_t i = 0; i < nw; ++i) {
+      sst += (double)(w[4 * i] - t0), str += (double)((w[4 * i + 1] & M) - w[4 * i]);
+      sbd += (double)(w[4 * i + 2] - (w[4 * i + 1] & M)), scw += (double)(w[4 * i + 3] - w[4 * i + 2]);
+    }
+    fprintf(stderr, "exp512: span %.2f us; mean per wave (us): start %.2f triage %.2f body %.2f cow %.2f\n",
+            (tend - t0) / 100.0, sst / nw / 100.0, str / nw / 100.0, sbd / nw / 100.0, scw / nw / 100.0);
+    for (size_t r = 0; r < 8 && r < nw; ++r) {
+      const size_t i = ord[r];
+      fprintf(stderr, "exp512: wave %zu start %.2f triage %.2f body %.2f cow %.2f classes %llx busy %llu\n", i,
+              (w[4 * i] - t0) / 100.0, ((w[4 * i + 1] & M) - w[4 * i]) / 100.0, (w[4 * i + 2] - (w[4 * i + 1] & M)) / 100.0,
+              (w[4 * i + 3] - w[4 * i + 2]) / 100.0, w[4 * i + 1] >> 56, (w[4 * i + 1] >> 48) & 255);
     }
   }
   if (rc == SWIM_OK && (d.exp & 4)) {  // timing experiments: gossip-send work counters since the last step

@@ -301,14 +301,22 @@ __device__ __forceinline__ void tick_end(const Dev& d, uint32_t k) {
 // end of k_member_tick (W == 1, the last block, one thread): reset the per-tick counters the gossip plane of this tick and the SYNC diff and
 // member control of the next tick append to, and tell the host whether any gossip slot is in use (if none, the
 // gossip data plane of this tick has nothing to send, deliver, route or recycle and is not launched)
-__device__ __forceinline__ void tick_flag(const Dev& d, uint32_t k) {
+// In a speculative batch the host reads nothing until the batch ends: a gossip plane needed raises d.halt instead
+// (no system-scope fence: that writes back the XCD's L2 at the end of every tick)
+__device__ __forceinline__ void tick_flag(const Dev& d, uint32_t k, bool spec) {
   uint32_t nb = (k + 1) & 1;
   d.nmsg[nb] = 0;
   d.arena_used[nb] = 0;
   *d.pool_used = 0;
   *d.rc_n = 0;
-  d.hflag[0] = (uint32_t)((int32_t)d.SPR - __hip_atomic_load(d.free_top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  __threadfence_system();
+  const uint32_t used =
+      (uint32_t)((int32_t)d.SPR - __hip_atomic_load(d.free_top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  d.hflag[0] = used;
+  if (!spec) {
+    __threadfence_system();
+  } else if (used) {
+    *d.halt = k + 1u;
+  }
 }
 
 }  // namespace swim

@@ -221,6 +221,9 @@ struct Dev {
   uint32_t* pending_inc; // [N] host requests for the next tick's P0: bits 2.. updateIncarnation calls, bit 1 leaveCluster
   uint32_t* next_evt; // [N] earliest tick at which a pending path / subscription / fetch needs the member
   uint32_t* mdone;  // finished k_member_tick blocks this tick (the last one runs the end-of-tick resets)
+  // speculative batches (W == 1, gossip plane idle): tick + 1 of the member kernel after which the gossip plane was
+  // needed (0: none); every later k_sync_diff / k_member_tick launch of the batch returns at once
+  uint32_t* halt;
   uint32_t* trk;    // [NL][TRK] per receiver: subjects its row changed earlier in this tick's P1 (member.hip)
   uint32_t* ulog;   // [NL][ULOG][2] per member: (subject, old key) of its row writes this tick after a SYNC send
   uint32_t* spq;    // [NL][SPQ][8] per member: gossips created this tick, waiting for their slots (member.hip)
@@ -232,6 +235,7 @@ struct Dev {
   uint32_t* ev;  // [EVCAP][8] swim_event
   uint32_t* ev_n;
   unsigned long long* ctr;  // [C_NCTR]
+  unsigned long long* wt;   // SWIM_EXP & 512: per-wave timestamps of the latest k_member_tick [waves][4]
   uint32_t* err;            // [8] bits, info...
   const Dev* self;          // device-resident copy of this struct (kernels index it through a pointer)
   uint32_t* hflag;          // host-mapped: [0] gossip slots in use after this tick's member control (W == 1)
@@ -335,8 +339,9 @@ struct TickEvents {
 void launch_init(const Dev& d, void* stream);
 // single GPU, per tick k: launch_diff(k) (k > 0), launch_member(k) (+ host flag), then launch_gossip(k) if the flag
 // says a gossip slot is in use; launch_diff(k+1) may be queued before launch_gossip(k)
-void launch_diff(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr);
-void launch_member(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr);
+// spec: a launch of a speculative batch (it returns at once once d.halt is set)
+void launch_diff(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr, bool spec = false);
+void launch_member(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr, bool spec = false);
 void launch_gossip(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr);
 // sharded tick (W > 1): A = SYNC diff + member control + pack exchange A; B = unpack A, gossip sends, pack
 // exchange B; C = unpack B, apply receipts, routing, slot recycling. The host runs the exchanges in between and

@@ -339,7 +339,8 @@ __device__ __forceinline__ void diff_fetch(const Dev& d, uint32_t b, uint32_t w,
 // adds payloads received from other shards (baseline row + shipped chunks); the single-GPU instance has only local
 // rows and snapshots.
 template <bool SHARDED>
-__global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b, uint32_t timed) {
+__global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b, uint32_t timed, uint32_t spec) {
+  if (spec && *(volatile uint32_t*)d.halt) return;  // a speculative batch halted at an earlier tick
   __shared__ uint32_t scan[256];
   __shared__ uint32_t base;
   uint32_t nmsg = d.nmsg[b] < d.MSGCAP ? d.nmsg[b] : d.MSGCAP;
@@ -489,26 +490,26 @@ void launch_init(const Dev& d, void* stream) {
 }
 
 // timed: this launch is bracketed by profiling events; it adds its message count to ctr[C_DIFFMSG]
-static void launch_sync_diff(const Dev& d, uint32_t b, hipStream_t st, uint32_t timed) {
+static void launch_sync_diff(const Dev& d, uint32_t b, hipStream_t st, uint32_t timed, uint32_t spec = 0) {
   if (d.W > 1)
-    hipLaunchKernelGGL(k_sync_diff<true>, dim3(2048), dim3(256), 0, st, d, b, timed);
+    hipLaunchKernelGGL(k_sync_diff<true>, dim3(2048), dim3(256), 0, st, d, b, timed, 0u);
   else
-    hipLaunchKernelGGL(k_sync_diff<false>, dim3(2048), dim3(256), 0, st, d, b, timed);
+    hipLaunchKernelGGL(k_sync_diff<false>, dim3(2048), dim3(256), 0, st, d, b, timed, spec);
 }
 
 // single GPU: the tick is cut in three so that the host can hold back the gossip data plane when no slot is in
 // use; the SYNC diff of tick k+1 does not depend on the gossip plane of tick k and is queued in between
-void launch_diff(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
+void launch_diff(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool spec) {
   hipStream_t st = (hipStream_t)stream;
   if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
-  if (k > 0) launch_sync_diff(d, (k - 1) & 1, st, prof ? 1u : 0u);
+  if (k > 0) launch_sync_diff(d, (k - 1) & 1, st, prof ? 1u : 0u, spec ? 1u : 0u);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
 }
 
-void launch_member(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
+void launch_member(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool spec) {
   hipStream_t st = (hipStream_t)stream;
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[2], st);
-  hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k, 1u);  // + k_tick_flag's work
+  hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k, spec ? 3u : 1u);  // + tick_flag
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[3], st);
 }
 

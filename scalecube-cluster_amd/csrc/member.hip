@@ -1541,9 +1541,15 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
 // control path for them: a wave holds one kind of work, so it does not serialise the latency chains of a ping, a
 // ping hop and an ack arrival, and no wave runs mostly idle lanes. Counters are summed across the wave first: 10^4
 // pingers per tick adding to one word would serialise on that address. With `flag` (W == 1) the block that finishes
-// last runs the end-of-tick resets and raises the host flag.
+// last runs the end-of-tick resets and raises the host flag. flag: 1 = W == 1 (end-of-tick work), 2 = a launch of a
+// speculative batch.
 __global__ void __launch_bounds__(256) k_member_tick(const Dev* __restrict__ dp, uint32_t k, uint32_t flag) {
   const Dev& d = *dp;  // global, not kernarg: taking its address must not copy ~1 KB into per-lane scratch
+  if ((flag & 2u) && *(volatile uint32_t*)d.halt) return;  // a speculative batch halted at an earlier tick
+  // SWIM_EXP & 512 (timing experiment): wall clock of each wave at entry, after triage, after its bodies, at exit
+  const bool wtime = (d.exp & 512) != 0;
+  unsigned long long* wt = wtime ? d.wt + ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 4 : nullptr;
+  if (wtime && (threadIdx.x & 63) == 0) wt[0] = wall_clock64();
   __shared__ uint32_t wc[4][4];  // [wave][class] busy members
   __shared__ uint32_t list[256];
   __shared__ uint4 cw[CWMAX];  // deferred copy-on-write snapshots of this block's members (cow)
@@ -1583,6 +1589,12 @@ __global__ void __launch_bounds__(256) k_member_tick(const Dev* __restrict__ dp,
   if (busy) list[start + before + __popcll(bal & ((1ull << lane) - 1ull))] = m | (cls << 30);  // m < 2^30
   __syncthreads();
   const uint32_t ent = list[threadIdx.x], me = ent == NEVER ? NEVER : (ent & 0x3FFFFFFFu), mcls = ent >> 30;
+  if (wtime) {  // [1]: after triage, with the wave's class mix in the top byte
+    const uint64_t cm = (__ballot(me != NEVER && mcls == 0) ? 1ull : 0ull) | (__ballot(me != NEVER && mcls == 1) ? 2ull : 0ull) |
+                        (__ballot(me != NEVER && mcls == 2) ? 4ull : 0ull) | (__ballot(me != NEVER && mcls == 3) ? 8ull : 0ull);
+    const uint32_t nb = (uint32_t)__popcll(__ballot(me != NEVER));
+    if ((threadIdx.x & 63) == 0) wt[1] = wall_clock64() | (cm << 56) | ((uint64_t)nb << 48);
+  }
   // SWIM_EXP & 32 / 64 (timing experiments, wrong results): skip the bodies of class 0 / of classes 1-3
   if (__ballot(me != NEVER)) {  // waves with no busy member skip to the end
     unsigned long long cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1599,6 +1611,7 @@ __global__ void __launch_bounds__(256) k_member_tick(const Dev* __restrict__ dp,
       if (lane == 0 && v) atomicAdd(&d.ctr[i], v);
     }
   }
+  if (wtime && (threadIdx.x & 63) == 0) wt[2] = wall_clock64();
   // deferred copy-on-write: the block copies each snapshot's row (final for this tick: only its member writes it),
   // then one lane undoes the member's logged writes since the snapshot opened, newest first
   __syncthreads();
@@ -1622,10 +1635,11 @@ __global__ void __launch_bounds__(256) k_member_tick(const Dev* __restrict__ dp,
     }
     __syncthreads();
   }
-  if (!flag) return;
+  if (wtime && (threadIdx.x & 63) == 0) wt[3] = wall_clock64();
+  if (!(flag & 1u)) return;
   if (!last_block_ticket(d.mdone, gridDim.x) || threadIdx.x != 0) return;
   *d.mdone = 0;
-  tick_flag(d, k);
+  tick_flag(d, k, (flag & 2u) != 0);
 }
 
 }  // namespace swim

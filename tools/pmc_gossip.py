@@ -1,0 +1,62 @@
+"""Per-tick HBM bytes and L2 atomics of the gossip data plane from three rocprofv3 --pmc passes (FETCH_SIZE with the
+gfx950 x2 correction, WRITE_SIZE, TCC_ATOMIC_sum; MI355X_MICROARCH.md HBM section), averaged over the last <timed ticks>
+member-kernel dispatches (= ticks) and the dispatches after the first of them. Usage: python tools/pmc_gossip.py <dir> <workload> <timed ticks> [out.json]
+<dir> holds pmc_<workload>_<counter>/run_counter_collection.csv"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+
+def per_kernel(path, last):
+    """counter sums per kernel over the dispatches of the last `last` ticks (the timed periods of the bench run)"""
+    rows = list(csv.DictReader(open(path)))
+    for r in rows:
+        r["name"] = r["Kernel_Name"].split("(")[0].replace("swim::", "").replace("void ", "").split("<")[0]
+    ticks = sorted({int(r["Dispatch_Id"]) for r in rows if r["name"] == "k_member_tick"})
+    first = ticks[-last] if last and len(ticks) >= last else 0
+    tot, disp = defaultdict(float), defaultdict(set)
+    for r in rows:
+        if int(r["Dispatch_Id"]) < first:
+            continue
+        tot[r["name"]] += float(r["Counter_Value"])
+        disp[r["name"]].add(r["Dispatch_Id"])
+    return tot, {k: len(v) for k, v in disp.items()}
+
+
+def main():
+    d, w, last = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    f, nd = per_kernel(f"{d}/pmc_{w}_FETCH_SIZE/run_counter_collection.csv", last)
+    wr, _ = per_kernel(f"{d}/pmc_{w}_WRITE_SIZE/run_counter_collection.csv", last)
+    try:
+        at, _ = per_kernel(f"{d}/pmc_{w}_TCC_ATOMIC_sum/run_counter_collection.csv", last)
+    except FileNotFoundError:
+        at = {}
+    ticks = nd.get("k_member_tick", 1)
+    out = {"ticks": ticks, "kernels": {}}
+    for k in sorted(f, key=lambda k: -(2 * f[k] + wr.get(k, 0))):
+        out["kernels"][k] = {"dispatches": nd[k], "hbm_bytes_per_tick": (2 * f[k] + wr.get(k, 0)) * 1024 / ticks,
+                             "fetch_bytes_per_tick_x2": 2 * f[k] * 1024 / ticks,
+                             "write_bytes_per_tick": wr.get(k, 0) * 1024 / ticks,
+                             "l2_atomics_per_tick": at.get(k, 0) / ticks}
+    gk = [k for k in out["kernels"] if k != "k_member_tick"]
+    out["gossip_plane_hbm_bytes_per_tick"] = sum(out["kernels"][k]["hbm_bytes_per_tick"] for k in gk)
+    out["gossip_plane_l2_atomics_per_tick"] = sum(out["kernels"][k]["l2_atomics_per_tick"] for k in gk)
+    # the same ticks' op counters from the bench line of the FETCH_SIZE pass: SURVEY.md §8d algorithmic bytes
+    # B = 8R + 8W + 32M + 0.375G + 24E (4-B record keys) against the measured HBM bytes of the whole step
+    line = [json.loads(x) for x in open(f"{d}/pmc_{w}_FETCH_SIZE.log") if x.startswith("{")]
+    if line:
+        c, ticks = line[-1]["counters"], line[-1]["steps"] * line[-1]["config"]["ticks_per_period"]
+        B = 8 * c["record_compares"] + 8 * c["row_writes"] + 32 * c["messages"] + 0.375 * c["gossip_messages"] + 24 * c["events"]
+        out["algorithmic_bytes_per_tick"] = B / ticks
+        out["counters_per_tick"] = {k: v / ticks for k, v in c.items()}
+        allb = sum(v["hbm_bytes_per_tick"] for v in out["kernels"].values())
+        out["hbm_bytes_per_tick_all_kernels"] = allb
+        out["wasted_traffic_ratio"] = allb / (B / ticks) if B else None
+    print(json.dumps(out, indent=1))
+    if len(sys.argv) > 4:
+        json.dump(out, open(sys.argv[4], "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
