@@ -65,6 +65,8 @@ extern "C" {
 #define SWIM_FLAG_IMPLICIT_VIEWS 8u /* RUMOR mode: the (unchanging) tables and lists are computed, not stored; always
                                       on above 65536 members (C5: 10^6 members would need 8 TB of tables) */
 #define SWIM_FLAG_PROFILE_ALL 4u   /* also time k_member_tick and k_gossip_send (member_ns, gossip_ns); ~10 % slower */
+#define SWIM_FLAG_EMULATOR_COUNTERS 16u /* keep every member's NetworkEmulator sent / lost counters
+                                           (swim_emulator_counters; the oracle always keeps them) */
 
 typedef struct swim_config {
   uint32_t n_members;
@@ -98,7 +100,10 @@ typedef struct swim_config {
   uint32_t churn_per_period;  /* SWIM_MODE_RUMOR: churn events (one rumor each) drawn at the start of every FD period */
   uint32_t n_dormant;         /* COLD_JOIN: the last n_dormant members are not started; each starts on swim_join */
   uint32_t gossip_ring_cap;   /* gossips one member can hold at once (its receipt ring; rounded up to a power of two) */
-  uint32_t reserved[3];
+  uint32_t delay_cap_ms;      /* the largest mean link delay the handle will be given (swim_set_*link_settings); it sizes
+                                 the engine's delay queues and replay window. 0: delays that reach a tick are refused
+                                 by the engine (the oracle ignores it) */
+  uint32_t reserved[2];
 } swim_config;
 
 /* One member's own configuration where it differs from the handle's config. The reference builds every member from its own
@@ -174,6 +179,18 @@ int swim_unblock_all(swim_handle* h); /* also clears every per-link setting (Net
 int swim_set_link_loss(swim_handle* h, uint32_t src, uint32_t dst, uint32_t loss_percent);
 /* NetworkEmulator.unblock(destination) on member src's emulator (:158-175): back to the default settings */
 int swim_unblock_link(swim_handle* h, uint32_t src, uint32_t dst);
+/* NetworkEmulator.setDefaultLinkSettings(loss, meanDelay) (:113-125) and setLinkSettings(destination, loss, meanDelay)
+ * on member src's emulator (:97-111): loss as above plus a mean delay in ms. A message that is not lost is delayed
+ * exponentially (NetworkLinkSettings.evaluateDelay :64-74) and delivered floor(delay / tick_ms) ticks after its
+ * normal tick (SEMANTICS.md §2). mean_delay_ms <= 11 * tick_ms (larger means reach delays of 256 ticks: SWIM_EINVAL).
+ * swim_set_default_loss keeps the default mean delay; swim_set_link_loss sets a link's mean delay to 0. */
+int swim_set_default_link_settings(swim_handle* h, uint32_t loss_percent, uint32_t mean_delay_ms);
+int swim_set_link_settings(swim_handle* h, uint32_t src, uint32_t dst, uint32_t loss_percent, uint32_t mean_delay_ms);
+/* every member's NetworkEmulator counters (totalMessageSentCount / totalMessageLostCount, NetworkEmulator.java:200-222):
+ * out[2m] = sent, out[2m + 1] = lost, cap >= 2 * n_members. tryFail and tryDelay each count a send, so a delivered
+ * message counts 2 and a lost one 1 (+1 lost); sends to a dead member fail before the emulator and are not counted.
+ * The engine needs SWIM_FLAG_EMULATOR_COUNTERS (else SWIM_EUNSUPPORTED). */
+int swim_emulator_counters(swim_handle* h, uint64_t* out, size_t cap);
 /* MembershipProtocolImpl.updateIncarnation (:178-190): the member bumps its own incarnation and spreads it, at the
  * start (P0) of the next tick; what ClusterImpl.updateMetadata does after storing new metadata */
 int swim_update_incarnation(swim_handle* h, uint32_t member);

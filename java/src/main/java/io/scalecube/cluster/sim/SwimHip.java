@@ -59,7 +59,8 @@ public final class SwimHip implements AutoCloseable {
           JAVA_INT.withName("churn_per_period"),
           JAVA_INT.withName("n_dormant"),
           JAVA_INT.withName("gossip_ring_cap"),
-          MemoryLayout.sequenceLayout(3, JAVA_INT).withName("reserved"),
+          JAVA_INT.withName("delay_cap_ms"),
+          MemoryLayout.sequenceLayout(2, JAVA_INT).withName("reserved"),
           MemoryLayout.paddingLayout(4));
 
   /** swim_member_config: 32 bytes. */
@@ -101,6 +102,12 @@ public final class SwimHip implements AutoCloseable {
       fn("swim_set_link_loss", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT, JAVA_INT, JAVA_INT));
   private static final MethodHandle UNBLOCK =
       fn("swim_unblock_link", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT, JAVA_INT));
+  private static final MethodHandle DEFAULT_LINK =
+      fn("swim_set_default_link_settings", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT, JAVA_INT));
+  private static final MethodHandle LINK =
+      fn("swim_set_link_settings", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT, JAVA_INT, JAVA_INT, JAVA_INT));
+  private static final MethodHandle EMU =
+      fn("swim_emulator_counters", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG));
   private static final MethodHandle UNBLOCK_ALL = fn("swim_unblock_all", FunctionDescriptor.of(JAVA_INT, ADDRESS));
   private static final MethodHandle PARTITION =
       fn("swim_set_partition", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS));
@@ -239,6 +246,35 @@ public final class SwimHip implements AutoCloseable {
   public void setLinkLoss(int src, int dst, int pct) {
     try {
       call((int) LINK_LOSS.invokeExact(handle, src, dst, pct));
+    } catch (Throwable t) {
+      throw rethrow(t);
+    }
+  }
+
+  /** NetworkEmulator.setDefaultLinkSettings(loss, meanDelay) on every member (NetworkEmulator.java:113-125). */
+  public void setDefaultLinkSettings(int pct, int meanDelayMs) {
+    try {
+      call((int) DEFAULT_LINK.invokeExact(handle, pct, meanDelayMs));
+    } catch (Throwable t) {
+      throw rethrow(t);
+    }
+  }
+
+  /** member src's NetworkEmulator.setLinkSettings(dst, loss, meanDelay) (NetworkEmulator.java:97-111). */
+  public void setLinkSettings(int src, int dst, int pct, int meanDelayMs) {
+    try {
+      call((int) LINK.invokeExact(handle, src, dst, pct, meanDelayMs));
+    } catch (Throwable t) {
+      throw rethrow(t);
+    }
+  }
+
+  /** every member's (totalMessageSentCount, totalMessageLostCount), NetworkEmulator.java:200-222. */
+  public long[] emulatorCounters() {
+    try (Arena a = Arena.ofConfined()) {
+      MemorySegment out = a.allocate(JAVA_LONG, 2L * members);
+      call((int) EMU.invokeExact(handle, out, 2L * members));
+      return out.toArray(JAVA_LONG);
     } catch (Throwable t) {
       throw rethrow(t);
     }

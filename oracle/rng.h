@@ -40,6 +40,8 @@ enum Salt : uint32_t {
   SALT_LOSS_BASE = 0x4C4F5300u,  // + message kind
   SALT_LOSS_GOSSIP = 0x474F5353u,
   SALT_CHURN = 0x43485552u,  // RUMOR mode churn draws (SEMANTICS.md §9)
+  SALT_DELAY_BASE = 0x444C5900u,  // + message kind: NetworkLinkSettings.evaluateDelay draws (SEMANTICS.md §2)
+  SALT_DELAY_GOSSIP = 0x444C5947u,
 };
 
 inline uint32_t next_int(uint32_t x, uint32_t bound) { return (uint32_t)(((uint64_t)x * bound) >> 32); }

@@ -17,6 +17,7 @@
 // is pinned by its closed forms. Event ordering and timing are pinned only by SEMANTICS.md, which makes parity for
 // them "spec-pinned", not reference-pinned.
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <condition_variable>
 #include <functional>
@@ -74,6 +75,7 @@ struct Msg {
   uint32_t cid_iss = NONE, cid_cnt = 0;                  // correlation id (issuer, counter)
   uint32_t pd_from = NONE, pd_to = NONE, pd_orig = NONE;  // PingData (fdetector/PingData.java:6-50)
   uint32_t seq = 0;                                       // syncSeq for SYNC / SYNC_ACK
+  uint32_t extra = 0;                                     // delay ticks past lat (NetworkEmulator.tryDelay)
   std::shared_ptr<Payload> payload;                       // SyncData (membership/SyncData.java:11-41)
   uint32_t md_subject = NONE, md_meta = NONE;             // GetMetadataRequest / Response
   uint64_t gid = 0;                                       // gossip id (origin << 32 | counter)
@@ -170,6 +172,9 @@ struct Member {
   std::vector<Sub> subs;  // pending requestResponse subscriptions
   uint64_t subOrder = 0;
 
+  // this member's NetworkEmulator counters (totalMessageSentCount / totalMessageLostCount, NetworkEmulator.java:200-222)
+  uint64_t emSent = 0, emLost = 0;
+
   // GossipProtocolImpl state (:47-53), GossipState.java:8-38
   std::vector<uint32_t> remote;
   int64_t remoteIdx = -1;
@@ -261,14 +266,18 @@ struct Sim {
   uint32_t ping_t = 0, pingTimeout_t = 0, gossip_t = 0, sync_t = 0, syncTimeout_t = 0, md_t = 0, lat = 1;
   uint32_t seed_lo = 0, seed_hi = 0;
   uint64_t tick = 0;
-  uint32_t loss = 0;
+  struct Link {
+    uint32_t loss, delay;  // NetworkLinkSettings (NetworkLinkSettings.java:15-38): loss %, mean delay ms
+  };
+  uint32_t loss = 0, delay = 0;  // defaultLinkSettings (NetworkEmulator.java:113-125)
   bool partitioned = false;
   std::vector<uint32_t> group;
-  std::map<uint64_t, uint32_t> custom;  // NetworkEmulator.customLinkSettings: (src << 32 | dst) -> loss %
+  std::map<uint64_t, Link> custom;  // NetworkEmulator.customLinkSettings: (src << 32 | dst) -> settings
+  std::map<uint32_t, std::vector<uint32_t>> dly_thr;  // mean delay ms -> delay thresholds (delay_table)
   std::vector<uint32_t> leaving_done;   // members whose leave completed this tick: stopped from the next tick
   std::vector<Member> members;
   std::vector<uint32_t> md_version;  // each member's own metadata version (GET_METADATA_RESP payload)
-  std::vector<std::vector<Msg>> inflight;  // ring indexed by delivery tick % (lat+1)
+  std::vector<std::vector<Msg>> inflight;  // ring indexed by delivery tick % (lat + 256): delays stay below 256 ticks
   std::vector<swim_event> events;
   swim_counters ctr;
   std::string err;
@@ -291,14 +300,41 @@ struct Sim {
   // NetworkEmulator.tryFail (transport/.../NetworkEmulator.java:231-248) + NetworkLinkSettings.evaluateLoss (:54-57)
   // getLinkSettings (:57-59): the custom setting of src's emulator for dst, else the default; a partition is the
   // DEAD custom setting on every cross-group link. Returns the loss percent (100 for a dead destination).
-  uint32_t link_loss(uint32_t src, uint32_t dst) const {
-    if (!members[dst].alive) return 100;
+  Link link(uint32_t src, uint32_t dst) const {
     if (!custom.empty()) {
       auto it = custom.find(((uint64_t)src << 32) | dst);
       if (it != custom.end()) return it->second;
     }
-    if (partitioned && group[src] != group[dst]) return 100;
-    return loss;
+    if (partitioned && group[src] != group[dst]) return Link{100, 0};  // block(): DEAD_LINK_SETTINGS (:24-26)
+    return Link{loss, delay};
+  }
+  uint32_t link_loss(uint32_t src, uint32_t dst) const {
+    if (!members[dst].alive) return 100;
+    return link(src, dst).loss;
+  }
+  // NetworkLinkSettings.evaluateDelay (:64-74): y = -ln(1 - u) * D ms, truncated to ms (longValue) and delivered
+  // floor(y / tick_ms) ticks past lat. floor(y / T) >= j  <=>  u >= 1 - exp(-jT/D), so with u = x / 2^32 the extra ticks
+  // are the number of thresholds ceil(2^32 (1 - exp(-jT/D))), j = 1.., that x reaches (SEMANTICS.md §2)
+  static bool delay_table(uint32_t D, uint32_t T, std::vector<uint32_t>* out) {
+    out->clear();
+    for (uint32_t j = 1; j <= 256; ++j) {
+      const double th = std::ceil((1.0 - std::exp(-(double)j * (double)T / (double)D)) * 4294967296.0);
+      if (th > 4294967295.0) return true;
+      if (j == 256) return false;  // a delay of 256 ticks or more is reachable: mean delay too long
+      out->push_back((uint32_t)th);
+    }
+    return true;
+  }
+  uint32_t delay_ticks(uint32_t D, uint32_t x) const {
+    const std::vector<uint32_t>& t = dly_thr.at(D);
+    return (uint32_t)(std::upper_bound(t.begin(), t.end(), x) - t.begin());
+  }
+  bool add_delay(uint32_t D) {  // host thread only (settings calls): worker threads only read the tables
+    if (D == 0 || dly_thr.count(D)) return true;
+    std::vector<uint32_t> t;
+    if (!delay_table(D, cfg.tick_ms, &t)) return false;
+    dly_thr[D] = std::move(t);
+    return true;
   }
   bool lost(uint8_t kind, uint32_t src, uint32_t dst, uint64_t k, uint32_t aux, uint32_t id) const {
     const uint32_t loss = link_loss(src, dst);
@@ -311,6 +347,11 @@ struct Sim {
     P4 r = philox4x32_10(src, dst, (uint32_t)k, id, seed_lo ^ (SALT_LOSS_BASE + kind), seed_hi ^ (aux * 0x9E3779B9u));
     return next_int(r.v[0], 100);
   }
+  // NetworkEmulator.tryFail + tryDelay (NetworkEmulator.java:231-272) of one message src -> dst: -1 if the send
+  // fails, else its delay ticks past lat; counts on src's emulator unless the destination refuses the connection
+  // (a dead member: TransportImpl.send fails in connect, before the emulator)
+  int xmit(uint8_t kind, uint32_t src, uint32_t dst, uint64_t k, uint32_t aux, uint32_t id, Member& em) const;
+  int xmit_gossip(uint32_t src, uint32_t dst, uint64_t k, uint32_t slot, uint64_t gid, Member& em) const;
   bool lost_gossip(uint32_t src, uint32_t dst, uint64_t k, uint32_t slot, uint64_t gid) const {
     const uint32_t loss = link_loss(src, dst);
     if (loss == 0) return false;
@@ -324,6 +365,34 @@ struct Sim {
   }
   void run_tick();
 };
+
+int Sim::xmit(uint8_t kind, uint32_t src, uint32_t dst, uint64_t k, uint32_t aux, uint32_t id, Member& em) const {
+  if (!members[dst].alive) return -1;
+  const Link L = link(src, dst);
+  em.emSent++;  // tryFail
+  if (L.loss >= 100 || (L.loss > 0 && loss_roll(kind, src, dst, k, aux, id) < L.loss)) {
+    em.emLost++;
+    return -1;
+  }
+  em.emSent++;  // tryDelay
+  if (L.delay == 0) return 0;
+  P4 r = philox4x32_10(src, dst, (uint32_t)k, id, seed_lo ^ (SALT_DELAY_BASE + kind), seed_hi ^ (aux * 0x9E3779B9u));
+  return (int)delay_ticks(L.delay, r.v[0]);
+}
+int Sim::xmit_gossip(uint32_t src, uint32_t dst, uint64_t k, uint32_t slot, uint64_t gid, Member& em) const {
+  if (!members[dst].alive) return -1;
+  const Link L = link(src, dst);
+  em.emSent++;
+  if (L.loss >= 100 || (L.loss > 0 && lost_gossip(src, dst, k, slot, gid))) {
+    em.emLost++;
+    return -1;
+  }
+  em.emSent++;
+  if (L.delay == 0) return 0;
+  P4 r = philox4x32_10(src, (uint32_t)k ^ ((slot >> 2) << 31), (uint32_t)(gid >> 32), (uint32_t)gid,
+                       seed_lo ^ SALT_DELAY_GOSSIP, seed_hi);
+  return (int)delay_ticks(L.delay, r.v[slot & 3]);
+}
 
 // ---------------------------------------------------------------------------------------------------------------
 // selector (SEMANTICS.md §2)
@@ -345,7 +414,7 @@ void Member::send(Msg&& m, uint64_t k, bool gossip) {
   Sim& s = *sim;
   (void)s;
   (void)k;
-  tl_lane->out.push_back(std::move(m));  // merged into inflight[(k + lat) % (lat + 1)] after the tick
+  tl_lane->out.push_back(std::move(m));  // merged into inflight[k + lat + m.extra] after the tick
 }
 
 // prepareSyncDataMsg (:446-454) + transport.send; returns false when the send failed
@@ -353,11 +422,13 @@ bool Member::send_sync(uint8_t kind, uint32_t dst, uint32_t cid_iss, uint32_t ci
   Sim& s = *sim;
   uint32_t seq = syncSeq++;
   tl_lane->ctr.messages++;
-  if (s.lost(kind, id, dst, k, id, seq)) {
+  const int e = s.xmit(kind, id, dst, k, id, seq, *this);
+  if (e < 0) {
     tl_lane->ctr.messages_lost++;
     return false;
   }
   Msg m;
+  m.extra = (uint32_t)e;
   m.kind = kind;
   m.src = id;
   m.dst = dst;
@@ -503,13 +574,15 @@ void Member::fetch(uint32_t subj, Rec r1, int reason, bool added, int group, uin
   Sim& s = *sim;
   uint32_t cnt = cidCnt++;
   tl_lane->ctr.messages++;
-  if (s.lost(K_GMD_REQ, id, subj, k, id, cnt)) {  // requestResponse send error -> sink.error
+  const int e = s.xmit(K_GMD_REQ, id, subj, k, id, cnt, *this);
+  if (e < 0) {  // requestResponse send error -> sink.error
     tl_lane->ctr.messages_lost++;
     if (group >= 0) groups[group].error = true;  // error propagates to whenDelayError
     do_finally(subj, r1, reason);
     return;
   }
   Msg m;
+  m.extra = (uint32_t)e;
   m.kind = K_GMD_REQ;
   m.src = id;
   m.dst = subj;
@@ -576,12 +649,14 @@ void Member::ping_req_step(uint32_t target, uint32_t cnt, uint64_t k) {
   }
   for (uint32_t h : helpers) {
     tl_lane->ctr.messages++;
-    if (s.lost(K_PING_REQ, id, h, k, id, cnt)) {
+    const int e = s.xmit(K_PING_REQ, id, h, k, id, cnt, *this);
+    if (e < 0) {
       tl_lane->ctr.messages_lost++;
       on_fd_event(target, SUSPECT, k);
       continue;
     }
     Msg m;
+    m.extra = (uint32_t)e;
     m.kind = K_PING_REQ;
     m.src = id;
     m.dst = h;
@@ -617,12 +692,14 @@ void Member::do_ping(uint64_t k) {
   uint32_t target = ping[(size_t)pingIdx++];
   uint32_t cnt = cidCnt++;
   tl_lane->ctr.messages++;
-  if (s.lost(K_PING, id, target, k, id, cnt)) {
+  const int e = s.xmit(K_PING, id, target, k, id, cnt, *this);
+  if (e < 0) {
     tl_lane->ctr.messages_lost++;
     ping_req_step(target, cnt, k);
     return;
   }
   Msg m;
+  m.extra = (uint32_t)e;
   m.kind = K_PING;
   m.src = id;
   m.dst = target;
@@ -660,10 +737,11 @@ void Member::do_spread_gossip(uint64_t k) {
       if (g.infPeriod + sp < period) continue;
       if (g.is_infected(t)) continue;
       tl_lane->ctr.gossip_messages++;
-      const bool lost = s.lost_gossip(id, t, k, slot, kv.first);
-      if (s.send_log) fprintf(s.send_log, "S %llu %u %llu %u %d\n", (unsigned long long)k, id, (unsigned long long)kv.first, t, lost ? 1 : 0);
-      if (lost) continue;  // gossip losses are not counted (SEMANTICS.md §8)
+      const int e = s.xmit_gossip(id, t, k, slot, kv.first, *this);
+      if (s.send_log) fprintf(s.send_log, "S %llu %u %llu %u %d\n", (unsigned long long)k, id, (unsigned long long)kv.first, t, e < 0 ? 1 : 0);
+      if (e < 0) continue;  // gossip losses are not counted (SEMANTICS.md §8)
       Msg m;
+      m.extra = (uint32_t)e;
       m.kind = K_GOSSIP;
       m.src = id;
       m.dst = t;
@@ -800,22 +878,26 @@ void Member::process(uint64_t k, std::vector<Msg>& inbox) {
     if (m->kind == K_PING) {  // onPing (:230-255)
       if (m->pd_to != id) continue;
       tl_lane->ctr.messages++;
-      if (s.lost(K_PING_ACK, id, m->pd_from, k, m->cid_iss, m->cid_cnt)) {
+      const int e = s.xmit(K_PING_ACK, id, m->pd_from, k, m->cid_iss, m->cid_cnt, *this);
+      if (e < 0) {
         tl_lane->ctr.messages_lost++;
         continue;
       }
       Msg a = *m;
+      a.extra = (uint32_t)e;
       a.kind = K_PING_ACK;
       a.src = id;
       a.dst = m->pd_from;
       send(std::move(a), k);
     } else if (m->kind == K_PING_REQ) {  // onPingReq (:258-284): transit ping
       tl_lane->ctr.messages++;
-      if (s.lost(K_PING, id, m->pd_to, k, m->cid_iss, m->cid_cnt)) {
+      const int e = s.xmit(K_PING, id, m->pd_to, k, m->cid_iss, m->cid_cnt, *this);
+      if (e < 0) {
         tl_lane->ctr.messages_lost++;
         continue;
       }
       Msg p;
+      p.extra = (uint32_t)e;
       p.kind = K_PING;
       p.src = id;
       p.dst = m->pd_to;
@@ -827,11 +909,13 @@ void Member::process(uint64_t k, std::vector<Msg>& inbox) {
       send(std::move(p), k);
     } else if (m->pd_orig != NONE) {  // onTransitPingAck (:290-315)
       tl_lane->ctr.messages++;
-      if (s.lost(K_PING_ACK, id, m->pd_orig, k, m->cid_iss, m->cid_cnt)) {
+      const int e = s.xmit(K_PING_ACK, id, m->pd_orig, k, m->cid_iss, m->cid_cnt, *this);
+      if (e < 0) {
         tl_lane->ctr.messages_lost++;
         continue;
       }
       Msg a;
+      a.extra = (uint32_t)e;
       a.kind = K_PING_ACK;
       a.src = id;
       a.dst = m->pd_orig;
@@ -850,11 +934,13 @@ void Member::process(uint64_t k, std::vector<Msg>& inbox) {
     if (m->kind == K_GMD_REQ) {
       if (m->md_subject != id) continue;
       tl_lane->ctr.messages++;
-      if (s.lost(K_GMD_RESP, id, m->src, k, m->cid_iss, m->cid_cnt)) {
+      const int e = s.xmit(K_GMD_RESP, id, m->src, k, m->cid_iss, m->cid_cnt, *this);
+      if (e < 0) {
         tl_lane->ctr.messages_lost++;
         continue;
       }
       Msg r;
+      r.extra = (uint32_t)e;
       r.kind = K_GMD_RESP;
       r.src = id;
       r.dst = m->src;
@@ -978,7 +1064,7 @@ void Member::process(uint64_t k, std::vector<Msg>& inbox) {
 void Sim::run_tick() {
   uint64_t k = tick;
   std::vector<Msg> arrived;
-  arrived.swap(inflight[k % (lat + 1)]);
+  arrived.swap(inflight[k % inflight.size()]);
   std::vector<std::vector<Msg>> inbox(N);
   for (auto& m : arrived) inbox[m.dst].push_back(std::move(m));
   const int T = threads;
@@ -1017,9 +1103,8 @@ void Sim::run_tick() {
     pool->run(work);
   else
     work(0);
-  auto& slot = inflight[(k + lat) % (lat + 1)];
   for (auto& l : lanes) {  // member order: the lanes hold contiguous member ranges
-    for (auto& m : l.out) slot.push_back(std::move(m));
+    for (auto& m : l.out) inflight[(k + lat + m.extra) % inflight.size()].push_back(std::move(m));
     events.insert(events.end(), l.events.begin(), l.events.end());
     leaving_done.insert(leaving_done.end(), l.leaving.begin(), l.leaving.end());
     ctr.record_compares += l.ctr.record_compares;
@@ -1115,7 +1200,7 @@ __attribute__((visibility("default"))) int swim_create(const swim_config* cfg, s
   s.seed_lo = (uint32_t)c.seed;
   s.seed_hi = (uint32_t)(c.seed >> 32);
   std::memset(&s.ctr, 0, sizeof(s.ctr));
-  s.inflight.assign(s.lat + 1, {});
+  s.inflight.assign(s.lat + 256, {});
   s.group.assign(s.N, 0);
   s.md_version.assign(s.N, 0);
   s.members.resize(s.N);
@@ -1283,7 +1368,27 @@ __attribute__((visibility("default"))) int swim_unblock_all(swim_handle* h) {
 }
 __attribute__((visibility("default"))) int swim_set_link_loss(swim_handle* h, uint32_t src, uint32_t dst, uint32_t pct) {
   if (!h || src >= h->sim.N || dst >= h->sim.N || pct > 100) return SWIM_EINVAL;
-  h->sim.custom[((uint64_t)src << 32) | dst] = pct;  // setLinkSettings / block (:97-150)
+  h->sim.custom[((uint64_t)src << 32) | dst] = Sim::Link{pct, 0};  // setLinkSettings(dst, pct, 0) / block (:97-150)
+  return SWIM_OK;
+}
+__attribute__((visibility("default"))) int swim_set_link_settings(swim_handle* h, uint32_t src, uint32_t dst, uint32_t pct,
+                                                                  uint32_t delay_ms) {
+  if (!h || src >= h->sim.N || dst >= h->sim.N || pct > 100 || !h->sim.add_delay(delay_ms)) return SWIM_EINVAL;
+  h->sim.custom[((uint64_t)src << 32) | dst] = Sim::Link{pct, delay_ms};  // setLinkSettings (:97-111)
+  return SWIM_OK;
+}
+__attribute__((visibility("default"))) int swim_set_default_link_settings(swim_handle* h, uint32_t pct, uint32_t delay_ms) {
+  if (!h || pct > 100 || !h->sim.add_delay(delay_ms)) return SWIM_EINVAL;
+  h->sim.loss = pct;  // setDefaultLinkSettings (:113-125)
+  h->sim.delay = delay_ms;
+  return SWIM_OK;
+}
+__attribute__((visibility("default"))) int swim_emulator_counters(swim_handle* h, uint64_t* out, size_t cap) {
+  if (!h || !out || cap < 2ull * h->sim.N) return SWIM_EINVAL;
+  for (uint32_t m = 0; m < h->sim.N; ++m) {
+    out[2 * m] = h->sim.members[m].emSent;
+    out[2 * m + 1] = h->sim.members[m].emLost;
+  }
   return SWIM_OK;
 }
 __attribute__((visibility("default"))) int swim_unblock_link(swim_handle* h, uint32_t src, uint32_t dst) {

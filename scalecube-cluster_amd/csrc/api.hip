@@ -37,9 +37,11 @@ struct swim_handle {
   std::vector<std::pair<char*, size_t>> guards;  // SWIM_GUARD: (allocation, bytes inside the guards)
   std::vector<swim_event> host_events;
   // settings-epoch ring mirrored on the host
-  uint32_t ep_from[MAX_EPOCHS], ep_loss[MAX_EPOCHS], ep_part[MAX_EPOCHS];
+  uint32_t ep_from[MAX_EPOCHS], ep_loss[MAX_EPOCHS], ep_part[MAX_EPOCHS], ep_delay[MAX_EPOCHS];
   int cur_ep = 0;
   uint32_t loss = 0;
+  uint32_t delay_idx = 0;                 // default mean delay (index into delays)
+  std::vector<uint32_t> delays{0};        // mean delay ms of each delay index (0: none)
   bool partitioned = false;
   std::vector<uint32_t> group;
   // per-link NetworkEmulator settings: current custom settings and each link's change history (mirrored to HBM)
@@ -68,6 +70,7 @@ struct swim_handle {
   bool no_pipe = getenv("SWIM_NO_PIPELINE") != nullptr;    // debugging aid: no early SYNC diff of the next tick
   bool no_spec = getenv("SWIM_NO_SPECULATION") != nullptr;  // debugging aid: a host wait after every member kernel
   bool gossip_idle = false;  // W == 1: no gossip slot was in use after the latest member kernel
+  int wclk_khz = 100000;     // device wall clock (wall_clock64) rate
   // timing aid (bench.py --rehearse-shard): a slot shard alone, its peers' gossip-count deltas taken as zero without
   // any exchange (not the W-shard simulation's results)
   bool lone = getenv("SWIM_LONE_SHARD") != nullptr;
@@ -109,6 +112,20 @@ int dalloc(swim_handle* h, T** p, size_t count) {
   if (getenv("SWIM_POISON") || (po && atoi(po) == (int)h->allocs.size() - 1)) hipMemsetAsync(q, 0xA5, bytes, h->stream);
   *p = (T*)q;
   return SWIM_OK;
+}
+
+// NetworkLinkSettings.evaluateDelay (:64-74) quantised to ticks (SEMANTICS.md §2): thresholds on the 32-bit delay draw
+// x, the extra ticks are the number of thresholds x reaches. false: a delay of 256 ticks or more is reachable.
+bool delay_table(uint32_t D, uint32_t T, std::vector<uint32_t>* out) {
+  out->clear();
+  if (D == 0) return true;
+  for (uint32_t j = 1; j <= 256; ++j) {
+    const double th = std::ceil((1.0 - std::exp(-(double)j * (double)T / (double)D)) * 4294967296.0);
+    if (th > 4294967295.0) return true;
+    if (j == 256) return false;
+    out->push_back((uint32_t)th);
+  }
+  return true;
 }
 
 bool to_ticks(uint32_t ms, uint32_t tick, uint32_t* out) {
@@ -167,6 +184,8 @@ int push_epoch(swim_handle* h) {
   h->ep_from[e] = (uint32_t)h->tick;
   h->ep_loss[e] = h->loss;
   h->ep_part[e] = h->partitioned ? 1u : 0u;
+  h->ep_delay[e] = h->delay_idx;
+  HIPCK(h2d(h->stream, h->d.ep_delay + e, &h->ep_delay[e], 4));
   HIPCK(h2d(h->stream, h->d.ep_from + e, &h->ep_from[e], 4));
   HIPCK(h2d(h->stream, h->d.ep_loss + e, &h->ep_loss[e], 4));
   HIPCK(h2d(h->stream, h->d.ep_part + e, &h->ep_part[e], 4));
@@ -315,8 +334,22 @@ int build(swim_handle* h) {
   d.GRCAP = c.init_mode == SWIM_INIT_COLD_JOIN ? std::min<uint32_t>(d.N + 16, 1024) : 32;
   if (d.implicit) d.FCAP = d.GRCAP = 1;  // RUMOR mode: no metadata fetch, no SYNC reply group
   uint32_t maxSpread = d.repeatMult * (32u - (uint32_t)__builtin_clz(d.LCAP + 1));
+  // link delays (swim_config.delay_cap_ms): the longest delay in ticks past lat
+  {
+    std::vector<uint32_t> t;
+    if (!delay_table(c.delay_cap_ms, c.tick_ms, &t)) {
+      h->err = "delay_cap_ms above 11 x tick_ms";
+      return SWIM_EINVAL;
+    }
+    d.EMAX = (uint32_t)t.size();
+    if (d.EMAX && d.W > 1) {
+      h->err = "link delays on a row-sharded handle";
+      return SWIM_EUNSUPPORTED;
+    }
+  }
   d.LOGW = 8;
-  while (d.LOGW < 4 * (maxSpread + 2)) d.LOGW <<= 1;  // rounds kept for the infectedFrom replay
+  // rounds kept for the infectedFrom replay (a delayed send arrives up to EMAX ticks after its round)
+  while (d.LOGW < 4 * (maxSpread + 2) + 2 * ((d.EMAX + d.gossip_t - 1) / d.gossip_t + 1)) d.LOGW <<= 1;
   d.LOOKBACK = d.LOGW * d.gossip_t;
   // incarnation history of reborn (gossip, member) pairs (88 B per entry). 2^20 entries (92 MB) by default; a run
   // that asks for a large slot table (a storm: C4's heal rebirths a large share of the holder states) gets one
@@ -398,7 +431,8 @@ int build(swim_handle* h) {
 #define A(p, n)                                   \
   if ((rc = dalloc(h, &(p), (size_t)(n))) != 0) return rc;
   A(d.link_n, 1) A(d.link_key, LKCAP) A(d.link_hist, (uint64_t)LKCAP * LKH * 2)
-  A(d.dead_tick, N) A(d.ep_from, MAX_EPOCHS) A(d.ep_loss, MAX_EPOCHS) A(d.ep_part, MAX_EPOCHS)
+  A(d.dead_tick, N) A(d.ep_from, MAX_EPOCHS) A(d.ep_loss, MAX_EPOCHS) A(d.ep_part, MAX_EPOCHS) A(d.ep_delay, MAX_EPOCHS)
+  A(d.dly_thr, DTAB * 256) A(d.dly_len, DTAB)
   A(d.ep_group, MAX_EPOCHS * N) A(d.md_version, N)
   A(d.tsize, N) A(d.fdLen, N) A(d.gLen, N) A(d.fdPeriod, N) A(d.gPeriod, N) A(d.gCounter, N) A(d.nextPing, N)
   A(d.nextGossip, N) A(d.nextSync, N) A(d.cidCnt, N) A(d.syncSeq, N) A(d.evSeq, N) A(d.held, N) A(d.timerMin, N)
@@ -425,8 +459,26 @@ int build(swim_handle* h) {
   A(d.arena[1], (uint64_t)d.ARENA_ROWS * d.NS) A(d.arena_used, 2)
   A(d.m_next, 2ull * d.MSGCAP) A(d.m_head, 2 * N) A(d.next_evt, N) A(d.mdone, 2) A(d.trk, NL * TRK) A(d.ulog, NL * ULOG * 2) A(d.spq, NL * SPQ * 8) A(d.pending_inc, N) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
   A(d.pool, d.POOLCAP) A(d.pool_used, 1)
-  A(d.ev, (uint64_t)d.EVCAP * 8) A(d.ev_n, 1) A(d.ctr, C_NCTR) A(d.err, 8)
-  if (d.exp & 512) A(d.wt, (uint64_t)(NL + 255) / 256 * 4 * 4)
+  A(d.ev, (uint64_t)d.EVCAP * 8) A(d.ev_n, 1) A(d.ctr, C_NCTR) A(d.err, 8) A(d.dts, 4)
+  if (c.flags & SWIM_FLAG_EMULATOR_COUNTERS) {
+    A(d.em, 2 * N)
+    HIPCK(hipMemsetAsync(d.em, 0, 16 * N, h->stream));
+  }
+  if (d.EMAX) {  // delayed gossip receipts by delivery tick; delayed SYNC / SYNC_ACK messages with their payloads
+    d.DQCAP = (uint32_t)std::min<uint64_t>(1ull << 22, std::max<uint64_t>(1ull << 16, (1ull << 30) / (8ull * (d.EMAX + 2))));
+    A(d.dq, (uint64_t)(d.EMAX + 2) * d.DQCAP) A(d.dq_n, d.EMAX + 2) A(d.dmark, N)
+    HIPCK(hipMemsetAsync(d.dq_n, 0, 4ull * (d.EMAX + 2), h->stream));
+    HIPCK(hipMemsetAsync(d.dmark, 0, 4 * N, h->stream));
+    d.DSCAP = (uint32_t)std::max<uint64_t>(64, std::min<uint64_t>(4096, (256ull << 20) / (4ull * d.NS)));
+    A(d.ds_msg, d.DSCAP) A(d.ds_row, (uint64_t)d.DSCAP * d.NS) A(d.ds_used, d.DSCAP) A(d.ds_free, d.DSCAP) A(d.ds_top, 1)
+    HIPCK(hipMemsetAsync(d.ds_used, 0, 4ull * d.DSCAP, h->stream));
+    std::vector<uint32_t> fl(d.DSCAP);
+    for (uint32_t i = 0; i < d.DSCAP; ++i) fl[i] = i;
+    const int32_t top = (int32_t)d.DSCAP;
+    HIPCK(h2d(h->stream, d.ds_free, fl.data(), 4ull * d.DSCAP));
+    HIPCK(h2d(h->stream, d.ds_top, &top, 4));
+  }
+  if (d.exp & 512) A(d.wt, (uint64_t)(NL + 255) / 256 * 4 * 16)
   if (d.fastp4) {
     A(d.evp_hash, N) A(d.evp_n, N)
     HIPCK(hipMemsetAsync(d.evp_hash, 0, 8 * N, h->stream));
@@ -499,6 +551,14 @@ int build(swim_handle* h) {
   HIPCK(hipMemsetAsync(d.ucnt, 0, N * 4, h->stream));
   HIPCK(hipMemsetAsync(d.pool_used, 0, 4, h->stream));
   HIPCK(hipMemsetAsync(d.mdone, 0, 8, h->stream));
+  {
+    const unsigned long long dts0[4] = {~0ull, 0ull, 0ull, 0ull};
+    HIPCK(hipMemcpyAsync(d.dts, dts0, sizeof(dts0), hipMemcpyHostToDevice, h->stream));
+    HIPCK(hipStreamSynchronize(h->stream));
+    if (hipDeviceGetAttribute(&h->wclk_khz, hipDeviceAttributeWallClockRate, (int)h->cfg.device) != hipSuccess ||
+        h->wclk_khz <= 0)
+      h->wclk_khz = 100000;
+  }
   d.halt = d.mdone + 1;
   HIPCK(hipMemsetAsync(d.link_n, 0, 4, h->stream));
   HIPCK(hipMemsetAsync(d.link_key, 0, 8ull * LKCAP, h->stream));
@@ -1064,7 +1124,7 @@ int swim_step(swim_handle* h, uint32_t n) {
       h->ugq.clear();
     }
     if (d.W == 1 && h->gossip_idle && i + 1 < n && d.XW == 1 && !d.churn && !h->no_pipe && !h->no_skip &&
-        !h->no_spec) {
+        !h->no_spec && !(h->cfg.flags & SWIM_FLAG_PROFILE_ALL)) {  // (PROFILE_ALL times every tick's gossip plane)
       // Speculative batch: while no gossip slot is in use the host need not look at the flag after every member
       // kernel. The rest of the call is queued as diff / member pairs with no host wait; the member kernel after which
       // a slot is in use raises d.halt, every later launch of the batch returns at once, and the host resumes after
@@ -1144,8 +1204,10 @@ int swim_step(swim_handle* h, uint32_t n) {
   }
   if (rc == SWIM_OK && (d.exp & 512)) {  // timing experiment: per-wave wall clock of the latest member kernel
     const size_t nw = (size_t)(d.NL + 255) / 256 * 4;
-    std::vector<unsigned long long> w(nw * 4);
-    HIPCK(hipMemcpy(w.data(), d.wt, w.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<unsigned long long> w16(nw * 16), w(nw * 4);
+    HIPCK(hipMemcpy(w16.data(), d.wt, w16.size() * 8, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < nw; ++i)
+      for (int j = 0; j < 4; ++j) w[4 * i + j] = w16[16 * i + j];
     const unsigned long long M = (1ull << 48) - 1;
     unsigned long long t0 = ~0ull, tend = 0;
     for (size_t i = 0; i < nw; ++i) t0 = std::min(t0, w[4 * i]), tend = std::max(tend, w[4 * i + 3]);
@@ -1164,6 +1226,16 @@ int swim_step(swim_handle* h, uint32_t n) {
       fprintf(stderr, "exp512: wave %zu start %.2f triage %.2f body %.2f cow %.2f classes %llx busy %llu\n", i,
               (w[4 * i] - t0) / 100.0, ((w[4 * i + 1] & M) - w[4 * i]) / 100.0, (w[4 * i + 2] - (w[4 * i + 1] & M)) / 100.0,
               (w[4 * i + 3] - w[4 * i + 2]) / 100.0, w[4 * i + 1] >> 56, (w[4 * i + 1] >> 48) & 255);
+      if (w[4 * i + 1] >> 56) {  // phase groups of its busy lanes: P0+P1, P2+P3, P4, P5, P6
+        unsigned long long prev = w[4 * i + 1] & M;
+        fprintf(stderr, "exp512:   phases");
+        for (int j = 0; j < 5; ++j) {
+          const unsigned long long t = w16[16 * i + 4 + j];
+          fprintf(stderr, " %.2f", t >= prev ? (t - prev) / 100.0 : -1.0);
+          if (t >= prev) prev = t;
+        }
+        fprintf(stderr, "\n");
+      }
     }
   }
   if (rc == SWIM_OK && (d.exp & 4)) {  // timing experiments: gossip-send work counters since the last step
@@ -1177,8 +1249,10 @@ int swim_step(swim_handle* h, uint32_t n) {
       float ms = 0;
       if (!timed(first + i)) continue;
       if (first + i > 0) {
-        HIPCK(hipEventElapsedTime(&ms, (hipEvent_t)h->prof[i].ev[0], (hipEvent_t)h->prof[i].ev[1]));
-        h->prof_ms[0] += ms;
+        if (d.W > 1 || h->prof[i].all) {
+          HIPCK(hipEventElapsedTime(&ms, (hipEvent_t)h->prof[i].ev[0], (hipEvent_t)h->prof[i].ev[1]));
+          h->prof_ms[0] += ms;
+        }  // (one GPU, sampled: the launch timed itself, dts)
         h->prof_diff_launches++;
       }
       if (!h->prof[i].all) continue;
@@ -1376,6 +1450,62 @@ int swim_set_link_loss(swim_handle* h, uint32_t src, uint32_t dst, uint32_t pct)
   if (!h || src >= h->d.N || dst >= h->d.N || pct > 100) return SWIM_EINVAL;
   link_change(h, link_key_of(src, dst), pct);
   return upload_links(h);
+}
+
+// the delay index of a mean delay (0: none, or a delay that never reaches a tick); registers its threshold table
+static int delay_index(swim_handle* h, uint32_t delay_ms, uint32_t* idx) {
+  std::vector<uint32_t> t;
+  if (!delay_table(delay_ms, h->cfg.tick_ms, &t)) return fail(h, SWIM_EINVAL, "mean delay above 11 x tick_ms");
+  *idx = 0;
+  if (t.empty()) return SWIM_OK;  // no message can be delayed past its tick
+  if (t.size() > h->d.EMAX || h->d.W > 1)
+    return fail(h, SWIM_EUNSUPPORTED, h->d.W > 1 ? "link delays on a row-sharded handle"
+                                                  : "mean delay above swim_config.delay_cap_ms");
+  for (uint32_t i = 1; i < (uint32_t)h->delays.size(); ++i)
+    if (h->delays[i] == delay_ms) {
+      *idx = i;
+      return SWIM_OK;
+    }
+  if (h->delays.size() >= DTAB) return fail(h, SWIM_ECAPACITY, "more than 15 distinct mean delays");
+  *idx = (uint32_t)h->delays.size();
+  h->delays.push_back(delay_ms);
+  const uint32_t len = (uint32_t)t.size();
+  HIPCK(h2d(h->stream, h->d.dly_thr + (size_t)*idx * 256, t.data(), 4ull * len));
+  HIPCK(h2d(h->stream, h->d.dly_len + *idx, &len, 4));
+  if (!h->d.dly_on) {  // from now on the gossip plane queues delayed receipts and SYNC messages are stored
+    h->d.dly_on = 1;
+    HIPCK(h2d(h->stream, (void*)h->d.self, &h->d, sizeof(Dev)));
+  }
+  return SWIM_OK;
+}
+
+int swim_set_default_link_settings(swim_handle* h, uint32_t pct, uint32_t delay_ms) {
+  GROUP_ALL(swim_set_default_link_settings(s, pct, delay_ms));
+  if (!h || pct > 100) return SWIM_EINVAL;
+  uint32_t idx;
+  int rc = delay_index(h, delay_ms, &idx);
+  if (rc) return rc;
+  h->delay_idx = idx;
+  return swim_set_default_loss(h, pct);  // a new settings epoch with both
+}
+
+int swim_set_link_settings(swim_handle* h, uint32_t src, uint32_t dst, uint32_t pct, uint32_t delay_ms) {
+  GROUP_ALL(swim_set_link_settings(s, src, dst, pct, delay_ms));
+  if (!h || src >= h->d.N || dst >= h->d.N || pct > 100) return SWIM_EINVAL;
+  uint32_t idx;
+  int rc = delay_index(h, delay_ms, &idx);
+  if (rc) return rc;
+  link_change(h, link_key_of(src, dst), pct | (idx << 8));
+  return upload_links(h);
+}
+
+int swim_emulator_counters(swim_handle* h, uint64_t* out, size_t cap) {
+  if (!h || !out || cap < 2ull * h->cfg.n_members) return SWIM_EINVAL;
+  if (h->grp) return fail(h, SWIM_EUNSUPPORTED, "emulator counters of a row-sharded handle");
+  if (!h->d.em) return fail(h, SWIM_EUNSUPPORTED, "emulator counters need SWIM_FLAG_EMULATOR_COUNTERS");
+  HIPCK(hipStreamSynchronize(h->stream));
+  HIPCK(hipMemcpy(out, h->d.em, 16ull * h->d.N, hipMemcpyDeviceToHost));
+  return SWIM_OK;
 }
 
 int swim_unblock_link(swim_handle* h, uint32_t src, uint32_t dst) {
@@ -1614,6 +1744,11 @@ int swim_counters_get(swim_handle* h, swim_counters* out) {
   out->sync_merges = c[C_SYNCMERGE];
   out->device_bytes = h->bytes;
   out->diff_ns = (uint64_t)(h->prof_ms[0] * 1e6);
+  if (h->d.W == 1) {  // sampled launches on one GPU time themselves by the wall clock (k_sync_diff, dts[3])
+    unsigned long long raw = 0;
+    HIPCK(hipMemcpy(&raw, h->d.dts + 3, 8, hipMemcpyDeviceToHost));
+    out->diff_ns += (uint64_t)((double)raw * 1e6 / (double)h->wclk_khz);
+  }
   out->member_ns = (uint64_t)(h->prof_ms[1] * 1e6);
   out->gossip_ns = (uint64_t)(h->prof_ms[2] * 1e6);
   out->diff_launches = h->prof_diff_launches;

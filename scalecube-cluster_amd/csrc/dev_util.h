@@ -99,17 +99,97 @@ __device__ __noinline__ int link_loss_at(const Dev& d, uint32_t src, uint32_t ds
   return -1;
 }
 
-// NetworkEmulator.tryFail (transport/.../NetworkEmulator.java:231-248) at the sender, evaluated for tick k: a dead
-// destination fails the send; then the link's custom setting if it has one (block = 100 %), else the partition
-// block and the default loss. Returns the loss percent to draw against, or 100 for a certain failure.
-__device__ __forceinline__ uint32_t link_loss(const Dev& d, int ep, uint32_t src, uint32_t dst, uint32_t k) {
-  if (dead_at(d, dst, k)) return 100;
+// NetworkEmulator.getLinkSettings (:57-59) of link src -> dst at tick k: its custom setting if it has one (block =
+// 100 %), else the partition block (DEAD_LINK_SETTINGS, no delay) and the default settings. Returns loss % | delay
+// index << 8.
+__device__ __forceinline__ uint32_t link_set(const Dev& d, int ep, uint32_t src, uint32_t dst, uint32_t k) {
   if (*d.link_n) {
     const int lp = link_loss_at(d, src, dst, k);
     if (lp >= 0) return (uint32_t)lp;
   }
   if (d.ep_part[ep] && d.ep_group[(size_t)ep * d.N + src] != d.ep_group[(size_t)ep * d.N + dst]) return 100;
-  return d.ep_loss[ep];
+  return d.ep_loss[ep] | (d.ep_delay[ep] << 8);
+}
+
+// NetworkEmulator.tryFail (transport/.../NetworkEmulator.java:231-248) at the sender, evaluated for tick k: a dead
+// destination fails the send; then the link's loss. Returns the loss percent to draw against, or 100 for a certain
+// failure.
+__device__ __forceinline__ uint32_t link_loss(const Dev& d, int ep, uint32_t src, uint32_t dst, uint32_t k) {
+  if (dead_at(d, dst, k)) return 100;
+  return link_set(d, ep, src, dst, k) & 0xFFu;
+}
+
+// the delay in ticks past lat of a message whose delay draw is x, on a link with delay index di (SEMANTICS.md §2)
+__device__ __forceinline__ uint32_t delay_ticks(const Dev& d, uint32_t di, uint32_t x) {
+  const uint32_t* t = d.dly_thr + (size_t)di * 256;
+  uint32_t lo = 0, hi = d.dly_len[di];
+  while (lo < hi) {  // thresholds ascend: count those <= x
+    const uint32_t mid = (lo + hi) >> 1;
+    if (t[mid] <= x)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+// this member's emulator counters (NetworkEmulator.java:200-222, 231-272): tryFail counts every send that reaches the
+// emulator, tryDelay every one that survived it
+__device__ __forceinline__ void em_count(const Dev& d, uint32_t src, uint32_t sent, uint32_t lost) {
+  if (!d.em) return;
+  if (sent) atomicAdd(&d.em[2 * src], 2ull * sent - lost);
+  if (lost) atomicAdd(&d.em[2 * src + 1], (unsigned long long)lost);
+}
+
+// tryFail + tryDelay of one non-gossip message: -1 if the send fails, else its delay in ticks past lat
+__device__ __forceinline__ int xmit_ep(const Dev& d, int ep, uint32_t kind, uint32_t src, uint32_t dst, uint32_t k,
+                                       uint32_t aux, uint32_t id) {
+  if (ep < 0) {
+    set_err(d, E_EPOCH);
+    return -1;
+  }
+  if (dead_at(d, dst, k)) return -1;  // connection refused: fails before the emulator, not counted
+  const uint32_t ls = link_set(d, ep, src, dst, k), loss = ls & 0xFFu, di = ls >> 8;
+  const bool lost = loss >= 100 || (loss > 0 && loss_roll(d.seed_lo, d.seed_hi, kind, src, dst, k, aux, id) < loss);
+  em_count(d, src, 1u, lost ? 1u : 0u);
+  if (lost) return -1;
+  if (di == 0) return 0;
+  return (int)delay_ticks(d, di, delay_draw(d.seed_lo, d.seed_hi, kind, src, dst, k, aux, id));
+}
+
+// the gossip-send draw words (LOSS_GOSSIP, DELAY_GOSSIP: SEMANTICS.md §2) of gossip gid sent by src to target slot s
+__device__ __forceinline__ uint32_t gossip_loss_word(const Dev& d, uint32_t src, uint32_t k, uint32_t s, uint64_t gid) {
+  return pick(philox(src, k ^ ((s >> 2) << 31), (uint32_t)(gid >> 32), (uint32_t)gid, d.seed_lo ^ SALT_LOSS_GOSSIP,
+                     d.seed_hi), s & 3);
+}
+__device__ __forceinline__ uint32_t gossip_delay(const Dev& d, uint32_t di, uint32_t src, uint32_t k, uint32_t s,
+                                                 uint64_t gid) {
+  if (di == 0) return 0;
+  return delay_ticks(d, di, pick(philox(src, k ^ ((s >> 2) << 31), (uint32_t)(gid >> 32), (uint32_t)gid,
+                                        d.seed_lo ^ SALT_DELAY_GOSSIP, d.seed_hi), s & 3));
+}
+
+// the arrival tick of a gossip send (delay only, not loss): tick + lat + its delay under the settings of that tick
+__device__ __forceinline__ uint32_t gossip_arrival(const Dev& d, uint32_t src, uint32_t dst, uint32_t tick, uint32_t s,
+                                                   uint64_t gid) {
+  const uint32_t a = tick + d.lat;
+  if (!d.dly_on) return a;
+  const int ep = epoch_at(d, tick);
+  if (ep < 0) return a;
+  return a + gossip_delay(d, link_set(d, ep, src, dst, tick) >> 8, src, tick, s, gid);
+}
+// the latest a send can arrive past tick + lat
+__device__ __forceinline__ uint32_t dmax(const Dev& d) { return d.dly_on ? d.EMAX : 0u; }
+
+// a first-receipt candidate delayed past the next tick: queued by its delivery tick (k_gossip_due delivers it then);
+// its slot lives until every holder it makes has swept it
+__device__ __forceinline__ void delay_push(const Dev& d, uint32_t g, uint32_t t, uint32_t due) {
+  const uint32_t b = due % (d.EMAX + 2u), j = atomicAdd(&d.dq_n[b], 1u);
+  if (j < d.DQCAP)
+    d.dq[(size_t)b * d.DQCAP + j] = ((uint64_t)g << 32) | t;
+  else
+    set_err(d, E_DELAYQ);
+  atomicMax(&d.slot_exp[g], due + d.EXPB);
 }
 
 // the same with the settings epoch of tick k already looked up (epoch_at once per thread, not per message)

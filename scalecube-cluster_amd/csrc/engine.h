@@ -18,6 +18,7 @@ namespace swim {
 
 constexpr uint32_t NEVER = 0xFFFFFFFFu;
 constexpr uint32_t MAX_EPOCHS = 8;
+constexpr uint32_t DTAB = 16;  // distinct mean delays per handle (delay index 0: none)
 constexpr uint32_t SUBCAP = 8, PATHCAP = 8, FREC = 8, GREC = 8;
 constexpr uint32_t CH = 2048;  // subjects per SYNC-diff work item (256 threads x 8)
 constexpr uint32_t TRK = 16;   // subjects written in one tick's P1 that are re-checked against later payloads
@@ -39,7 +40,9 @@ constexpr uint32_t E_SLOTS = 1, E_FETCH = 2, E_SUBS = 4, E_PATHS = 8, E_GROUPS =
                    E_XCAP = 1u << 17, E_LINKHIST = 1u << 18, E_DEATHS = 1u << 19,
                    E_INC = 1u << 20,  // an incarnation >= 2^30 would not fit the key plane (swim_common.h)
                    E_PIN = 1u << 21,  // a later SYNC payload of a receiver's tick had no readable copy (pin)
-                   E_RING = 1u << 22;  // a member held more gossips than its receipt ring (gossip_ring_cap)
+                   E_RING = 1u << 22,  // a member held more gossips than its receipt ring (gossip_ring_cap)
+                   E_DELAYQ = 1u << 23,  // more delayed first receipts due in one tick than the delay queue holds
+                   E_SYNCQ = 1u << 24;   // more delayed SYNC / SYNC_ACK messages in flight than the SYNC delay store holds
 // per-link NetworkEmulator settings (setLinkSettings / block / unblock): hash of (src, dst) -> change history
 constexpr uint32_t LKCAP = 4096, LKH = 8;  // keys, history entries per key
 constexpr uint32_t CIN_SLOW = 0xFFFFFFFEu;
@@ -49,7 +52,7 @@ constexpr uint32_t CEV = 6, CEVW = 4 + 2 * CEV;  // cached contact events per (s
 // gossip incarnation history entry: 3 header words + HKEEP creation ticks of swept incarnations (small clusters
 // under loss re-infect a member with the same gossip many times: each late sender restarts the chain)
 constexpr uint32_t HREC = 11, HKEEP = 16;
-constexpr uint32_t LK_NONE = 0xFFFFFFFFu, LK_TRUNC = 0x80000000u;
+constexpr uint32_t LK_NONE = 0xFFFFFFFFu, LK_TRUNC = 0x80000000u;  // link values: loss % | delay index << 8
 
 // row sharding: SyncMsg.payload values
 constexpr uint32_t PAY_RX = 0x40000000u;  // received from another shard: PAY_RX | rx index (dirty chunks + baseline)
@@ -87,7 +90,9 @@ struct SyncMsg {
   // several SYNC / SYNC_ACK payloads in one tick: the member kernel then reads later payloads' records directly (the
   // sender may write its live row meanwhile), for the subjects an earlier payload of that tick changed
   uint32_t pin;
+  uint32_t due;  // delayed message (kind has KF_DEFER): the tick of its P1 delivery
 };
+constexpr uint32_t KF_DEFER = 0x100u;  // SyncMsg.kind flag: delivered after the next tick (k_sync_defer stores it)
 
 struct Dev {
   // ---- configuration ----
@@ -114,6 +119,26 @@ struct Dev {
   uint32_t* ep_from;    // [MAX_EPOCHS] first tick of each settings epoch (NEVER = unused)
   uint32_t* ep_loss;    // [MAX_EPOCHS]
   uint32_t* ep_part;    // [MAX_EPOCHS] partition active
+  uint32_t* ep_delay;   // [MAX_EPOCHS] default mean delay (its delay index)
+  // NetworkLinkSettings.meanDelay (SEMANTICS.md §2): a link value is loss % | delay index << 8; each index has the
+  // thresholds on the 32-bit delay draw whose count the draw reaches is the message's delay in ticks past lat
+  uint32_t dly_on;      // a delay that reaches a tick was set (the gossip plane queues delayed first receipts)
+  uint32_t EMAX;        // largest delay in ticks past lat under swim_config.delay_cap_ms
+  uint32_t* dly_thr;    // [DTAB][256]
+  uint32_t* dly_len;    // [DTAB]
+  unsigned long long* em;  // [2N] SWIM_FLAG_EMULATOR_COUNTERS: every member's emulator (sent, lost); null otherwise
+  uint64_t* dq;         // [EMAX + 2][DQCAP] delayed first-receipt candidates (slot << 32 | target) by delivery tick
+  uint32_t* dq_n;       // [EMAX + 2]
+  uint32_t DQCAP;
+  uint32_t* dmark;      // [N] tick + 1 at which the target joined the tick's target list by a delayed receipt
+  // delayed SYNC / SYNC_ACK messages (KF_DEFER) between their send and the tick before their delivery: the record and
+  // the payload as it was sent (k_sync_defer), put back into the message buffer then (k_sync_redeliver)
+  uint32_t DSCAP;
+  SyncMsg* ds_msg;      // [DSCAP]
+  uint32_t* ds_row;     // [DSCAP][NS]
+  uint32_t* ds_used;    // [DSCAP]
+  uint32_t* ds_free;    // [DSCAP] free entries (a stack)
+  int32_t* ds_top;      // [1]
   uint32_t* ep_group;   // [MAX_EPOCHS][N]
   uint32_t* md_version; // [N]
   uint32_t* link_n;     // [1] keys in the link table (0: no per-link setting was ever made)
@@ -235,7 +260,8 @@ struct Dev {
   uint32_t* ev;  // [EVCAP][8] swim_event
   uint32_t* ev_n;
   unsigned long long* ctr;  // [C_NCTR]
-  unsigned long long* wt;   // SWIM_EXP & 512: per-wave timestamps of the latest k_member_tick [waves][4]
+  unsigned long long* dts;  // [4] timed k_sync_diff launches on one GPU: first start, last end, blocks done, summed wall-clock ticks
+  unsigned long long* wt;   // SWIM_EXP & 512: per-wave timestamps of the latest k_member_tick [waves][16]
   uint32_t* err;            // [8] bits, info...
   const Dev* self;          // device-resident copy of this struct (kernels index it through a pointer)
   uint32_t* hflag;          // host-mapped: [0] gossip slots in use after this tick's member control (W == 1)

@@ -124,7 +124,8 @@ __device__ __forceinline__ bool replay_pair(const Dev& d, uint32_t x, uint32_t y
     for (int i = (int)n - 1; i >= 0; --i) {
       const Contact& c = ev[i];
       uint32_t rin = c.dir == 0 ? 0 : 1;  // receiver index into lo_in
-      if (lo_in[rin] == NEVER || c.tick + lat < lo_in[rin]) continue;
+      if (lo_in[rin] == NEVER || c.tick + lat + dmax(d) < lo_in[rin]) continue;
+      if (d.dly_on && gossip_arrival(d, c.dir == 0 ? y : x, c.dir == 0 ? x : y, c.tick, c.slot, gid) < lo_in[rin]) continue;
       if (cinc[i] == NEVER - 1) cinc[i] = inc_at(d, c.dir == 0 ? y : x, g, gid, c.tick);
       uint32_t cs = cinc[i];
       uint32_t snd = c.dir == 0 ? y : x;
@@ -139,9 +140,10 @@ __device__ __forceinline__ bool replay_pair(const Dev& d, uint32_t x, uint32_t y
     if (!changed) break;
   }
   // deliveries into x come from y's log (oldest[0]); into y from x's log (oldest[1])
-  // (oldest 0: that ring never wrapped, so it holds every round since tick 0)
-  if ((lo_in[0] != NEVER && oldest[0] && lo_in[0] < oldest[0] + lat) ||
-      (lo_in[1] != NEVER && oldest[1] && lo_in[1] < oldest[1] + lat)) {
+  // (oldest 0: that ring never wrapped, so it holds every round since tick 0; a delayed send arrives up to dmax
+  // ticks later, so the log must reach that much further back)
+  if ((lo_in[0] != NEVER && oldest[0] && lo_in[0] < oldest[0] + lat + dmax(d)) ||
+      (lo_in[1] != NEVER && oldest[1] && lo_in[1] < oldest[1] + lat + dmax(d))) {
     if (atomicOr(d.err, E_LOGWIN) == 0) {
       d.err[1] = tau;
       d.err[2] = lo_in[0];
@@ -150,7 +152,7 @@ __device__ __forceinline__ bool replay_pair(const Dev& d, uint32_t x, uint32_t y
       d.err[5] = oldest[1];
     }
   }
-  uint32_t del[2][CM];
+  uint32_t del[2][CM];  // arrival ticks of the delivered sends, per direction
   uint32_t nd[2] = {0, 0};
   for (uint32_t i = 0; i < n; ++i) {
     const Contact& c = ev[i];
@@ -163,13 +165,14 @@ __device__ __forceinline__ bool replay_pair(const Dev& d, uint32_t x, uint32_t y
     // the receiver delivered g to the sender during that incarnation: infectedFrom (isInfected :247)
     uint32_t od = 1 - c.dir;  // opposite direction
     bool blocked = false;
-    for (uint32_t q = 0; q < nd[od] && !blocked; ++q) blocked = del[od][q] + lat >= cs && del[od][q] + lat <= c.tick;
+    for (uint32_t q = 0; q < nd[od] && !blocked; ++q) blocked = del[od][q] >= cs && del[od][q] <= c.tick;
     if (blocked) continue;
-    if (lost_gossip(d, snd, c.dir == 0 ? x : y, c.tick, c.slot, gid)) continue;
-    del[c.dir][nd[c.dir]++] = c.tick;
+    const uint32_t rcv = c.dir == 0 ? x : y;
+    if (lost_gossip(d, snd, rcv, c.tick, c.slot, gid)) continue;
+    del[c.dir][nd[c.dir]++] = d.dly_on ? gossip_arrival(d, snd, rcv, c.tick, c.slot, gid) : c.tick + lat;
   }
   for (uint32_t q = 0; q < nd[0]; ++q)
-    if (del[0][q] + lat >= cx) return true;
+    if (del[0][q] >= cx && del[0][q] <= tau) return true;
   return false;
 }
 
@@ -230,7 +233,7 @@ __device__ __forceinline__ bool blocked_pair_cached(const Dev& d, uint32_t x, ui
   bool relevant = false;
   for (uint32_t i = 0; i < nall; ++i) {
     const uint32_t t2 = rec[4 + 2 * i];
-    relevant |= ((rec[5 + 2 * i] >> 8) & 1u) == 0 && t2 >= born && t2 + d.lat >= cx;
+    relevant |= ((rec[5 + 2 * i] >> 8) & 1u) == 0 && t2 >= born && t2 + d.lat + dmax(d) >= cx;
   }
   if (!relevant) return false;
   Contact ev[CEV];
@@ -492,7 +495,7 @@ __device__ void contact_cache(const Dev& d, uint32_t i, uint32_t m, uint32_t t, 
     // Only gossips m received at or before the latest contact t -> m arrived (last_in + lat) can have t in
     // infectedFrom_m. Their infection periods are at most B1 = rounds_before(last_in + lat + 1); the window entries
     // of m's ring with a period above B1 were received later (sorted ring: a suffix) and are sent normally.
-    const uint32_t P = d.tperiod[m], B1 = rounds_before(d, m, last_in + d.lat + 1u);
+    const uint32_t P = d.tperiod[m], B1 = rounds_before(d, m, last_in + d.lat + dmax(d) + 1u);
     const uint32_t* R = ring(d, m);
     const uint32_t w0 = d.rwin[m], tl = d.rseen[m];  // the window as k_round_apply left it for this round
     uint32_t lo = 0, hi = tl - w0;
@@ -662,6 +665,37 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
         }
       }
       const unsigned long long cand = w & ~h & ~nb;
+      if (d.dly_on || d.em) {  // delays or emulator counters: the exact per-send path
+        if (ep < 0) {
+          set_err(d, E_EPOCH);
+          continue;
+        }
+        if (dead_at(d, t, k)) continue;  // refused before the emulator: nothing delivered or counted
+        const uint32_t ls = link_set(d, ep, m, t, k), pct = ls & 0xFFu, di = ls >> 8;
+        const unsigned long long drawn = d.em ? w : cand;  // the counters need every send's loss outcome
+        unsigned long long lostm = 0;
+        if (pct >= 100) {
+          lostm = drawn;
+        } else if (pct > 0) {
+          for (unsigned long long b = drawn; b; b &= b - 1) {
+            const uint32_t j = (uint32_t)(__ffsll((long long)b) - 1);
+            if (next_int(gossip_loss_word(d, m, k, s, d.slot_gid[q * 64u + j]), 100) < pct) lostm |= 1ull << j;
+          }
+        }
+        em_count(d, m, (uint32_t)__popcll(w), (uint32_t)__popcll(lostm & w));
+        unsigned long long ok = cand & ~lostm;
+        if (di)
+          for (unsigned long long b = ok; b; b &= b - 1) {
+            const uint32_t j = (uint32_t)(__ffsll((long long)b) - 1), g = q * 64u + j;
+            const uint32_t e = gossip_delay(d, di, m, k, s, d.slot_gid[g]);
+            if (e) {  // arrives after the next tick: queued (k_gossip_due)
+              ok &= ~(1ull << j);
+              delay_push(d, g, t, k + d.lat + e);
+            }
+          }
+        nb |= ok;
+        continue;
+      }
       if (!cand) continue;
       if (d.exp & 4) st[3] += (uint32_t)__popcll(cand);
       if (ep < 0) {
@@ -744,8 +778,27 @@ __device__ __forceinline__ void deliver_one(const Dev& d, uint32_t g, uint32_t m
   }
   unsigned long long* hw = hrow(d, t) + (g >> 6);
   const unsigned long long bit = 1ull << (g & 63u);
-  if (*hw & bit) return;
-  if (lost_gossip_ep(d, ep, m, t, k, s, gid)) return;
+  if (d.dly_on || d.em) {  // the exact per-send path (see k_gossip_send)
+    if (ep < 0) {
+      set_err(d, E_EPOCH);
+      return;
+    }
+    if (dead_at(d, t, k)) return;
+    const uint32_t ls = link_set(d, ep, m, t, k), pct = ls & 0xFFu, di = ls >> 8;
+    const bool held = (*hw & bit) != 0ull;
+    if (held && !d.em) return;
+    const bool lost = pct >= 100 || (pct > 0 && next_int(gossip_loss_word(d, m, k, s, gid), 100) < pct);
+    em_count(d, m, 1u, lost ? 1u : 0u);
+    if (held || lost) return;
+    const uint32_t e = gossip_delay(d, di, m, k, s, gid);
+    if (e) {
+      delay_push(d, g, t, k + d.lat + e);
+      return;
+    }
+  } else {
+    if (*hw & bit) return;
+    if (lost_gossip_ep(d, ep, m, t, k, s, gid)) return;
+  }
   if (atomicOr(hw, bit) & bit) return;
   if (d.DM[g >> 6] & bit) d.dead_rx[t] = k + d.lat;
   receipt_mark(d, g, t, k, atomicAdd(&d.rtail[t], 1u));
@@ -771,7 +824,8 @@ __global__ void __launch_bounds__(256) k_gossip_replay(const Dev* __restrict__ d
     const uint32_t g = (uint32_t)(v >> 32), ms = (uint32_t)v, m = ms / d.F, s = ms % d.F;
     const uint32_t t = d.T[ms], c = s_ctick(d.S[(size_t)g * d.N + m]), ci = d.cin[ms];
     const uint64_t gid = d.slot_gid[g];
-    if (ci >= d.slot_ctick[g] && ci + d.lat >= c && blocked_pair_cached(d, m, t, g, gid, k, c, d.cev + (size_t)ms * CEVW))
+    if (ci >= d.slot_ctick[g] && ci + d.lat + dmax(d) >= c &&
+        blocked_pair_cached(d, m, t, g, gid, k, c, d.cev + (size_t)ms * CEVW))
       continue;
     sends++;
     deliver_one(d, g, m, s, t, k, gid, ep);
@@ -804,6 +858,34 @@ __global__ void __launch_bounds__(64) k_gossip_send_slow(const Dev* __restrict__
   if (sends) atomicAdd(&d.ctr[C_G], sends);
 }
 
+// 7c. delayed first-receipt candidates due in P4 of k + lat (delay_push). Targets without senders this tick join the
+// target list first (their ring end before this tick's receipts: k_gossip_apply takes [rt0, rtail)), then each
+// candidate is a first receipt unless the target holds the gossip by now or is dead then.
+__global__ void k_gossip_due_mark(Dev d, uint32_t k) {
+  const uint32_t b = (k + d.lat) % (d.EMAX + 2u), n = min(d.dq_n[b], d.DQCAP);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t t = (uint32_t)d.dq[(size_t)b * d.DQCAP + i];
+    if (dead_at(d, t, k + d.lat) || d.tin_cnt[t]) continue;
+    if (atomicExch(&d.dmark[t], k + 1u) != k + 1u) {
+      d.rt0[t] = d.rtail[t];
+      d.tlist[atomicAdd(d.ntl, 1u)] = t;
+    }
+  }
+}
+__global__ void k_gossip_due(Dev d, uint32_t k) {
+  const uint32_t b = (k + d.lat) % (d.EMAX + 2u), n = min(d.dq_n[b], d.DQCAP);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint64_t v = d.dq[(size_t)b * d.DQCAP + i];
+    const uint32_t g = (uint32_t)(v >> 32), t = (uint32_t)v;
+    if (dead_at(d, t, k + d.lat)) continue;
+    const unsigned long long bit = 1ull << (g & 63u);
+    if (atomicOr(hrow(d, t) + (g >> 6), bit) & bit) continue;  // held, or made a receipt by another delivery
+    if (d.DM[g >> 6] & bit) d.dead_rx[t] = k + d.lat;
+    receipt_mark(d, g, t, k, atomicAdd(&d.rtail[t], 1u));
+  }
+}
+__global__ void k_dq_reset(Dev d, uint32_t k) { d.dq_n[(k + d.lat) % (d.EMAX + 2u)] = 0; }
+
 // P4 pre-filter (onMembershipGossip -> updateMembership, MembershipProtocolImpl.java:401-408,475-485). A first
 // receipt is routed to P4 of tick k4 unless it provably cannot change t's row there: its record does not override
 // the row as it stands now (= at the start of tick k4), the row is present, and the row cannot be removed before the
@@ -829,7 +911,10 @@ __device__ __forceinline__ void receipt_create(const Dev& d, uint32_t g, uint32_
   const uint32_t e = *p;
   if (s_ever(e)) hist_push(d, d.slot_gid[g], t, s_ctick(e));
   *p = ((k + d.lat + 1u) & S_TICK_MASK) | (s_ever(e) ? S_REBORN : 0u);
-  d.slot_exp[g] = k + d.lat + d.EXPB;  // every holder sweeps it by then (all receipts of a tick store the same value)
+  if (d.dly_on)  // a delayed first receipt still queued may have pushed it further (delay_push)
+    atomicMax(&d.slot_exp[g], k + d.lat + d.EXPB);
+  else
+    d.slot_exp[g] = k + d.lat + d.EXPB;  // every holder sweeps it by then (all receipts of a tick store the same value)
 }
 
 // 8. first receipts of this shard's targets, one wave per target: the entries its ring gained this tick. Holder
@@ -963,6 +1048,11 @@ void launch_gossip_send(const Dev& d, uint32_t k, hipStream_t st, const TickEven
   hipLaunchKernelGGL(k_gossip_send, dim3(SEND_GRID), dim3(256), 0, st, d.self, k);
   hipLaunchKernelGGL(k_gossip_send_slow, dim3(64), dim3(64), 0, st, d.self, k);  // rare; ~14 KB of stack per lane
   hipLaunchKernelGGL(k_gossip_replay, dim3(2048), dim3(256), 0, st, d.self, k);
+  if (d.dly_on) {
+    hipLaunchKernelGGL(k_gossip_due_mark, dim3(256), dim3(256), 0, st, d, k);
+    hipLaunchKernelGGL(k_gossip_due, dim3(256), dim3(256), 0, st, d, k);
+    hipLaunchKernelGGL(k_dq_reset, dim3(1), dim3(1), 0, st, d, k);
+  }
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[5], st);
 }
 

@@ -303,7 +303,9 @@ __device__ __forceinline__ void diff_fetch(const Dev& d, uint32_t b, uint32_t w,
   const uint32_t mi = w / d.NCHUNK, c = w % d.NCHUNK;
   const SyncMsg& mm = d.msgs[b][mi];
   const uint32_t s0 = c * CH + threadIdx.x * 8;
-  if (s0 >= d.NS) {  // NS is a multiple of 8: a 32-B group is wholly in or out; padding entries are 0 (absent)
+  // NS is a multiple of 8: a 32-B group is wholly in or out; padding entries are 0 (absent). A delayed message
+  // (KF_DEFER) is merged in a later tick: nothing to compare now
+  if (s0 >= d.NS || (mm.kind & KF_DEFER)) {
     x[0] = x[1] = x[2] = x[3] = make_uint4(0, 0, 0, 0);
     return;
   }
@@ -343,6 +345,10 @@ __global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b, uint32_t t
   if (spec && *(volatile uint32_t*)d.halt) return;  // a speculative batch halted at an earlier tick
   __shared__ uint32_t scan[256];
   __shared__ uint32_t base;
+  // timed (one GPU): the launch times itself, first block start to last block end (no event around it: a stream
+  // event writes back the L2 and opens a ~6 us gap)
+  const bool selftime = timed == 2u;
+  if (selftime && threadIdx.x == 0) atomicMin(&d.dts[0], (unsigned long long)wall_clock64());
   uint32_t nmsg = d.nmsg[b] < d.MSGCAP ? d.nmsg[b] : d.MSGCAP;
   if (timed && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&d.ctr[C_DIFFMSG], (unsigned long long)nmsg);
   uint32_t total = nmsg * d.NCHUNK;
@@ -406,6 +412,17 @@ __global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b, uint32_t t
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
+  }
+  if (selftime) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      atomicMax(&d.dts[1], (unsigned long long)wall_clock64());
+      if (atomicAdd(&d.dts[2], 1ull) == gridDim.x - 1u) {  // the last block: add the launch's span, reset
+        const unsigned long long t0 = atomicExch(&d.dts[0], ~0ull), t1 = atomicExch(&d.dts[1], 0ull);
+        atomicExch(&d.dts[2], 0ull);
+        atomicAdd(&d.dts[3], t1 - t0);
+      }
+    }
   }
 }
 
@@ -501,15 +518,91 @@ static void launch_sync_diff(const Dev& d, uint32_t b, hipStream_t st, uint32_t 
 // use; the SYNC diff of tick k+1 does not depend on the gossip plane of tick k and is queued in between
 void launch_diff(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool spec) {
   hipStream_t st = (hipStream_t)stream;
-  if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
-  if (k > 0) launch_sync_diff(d, (k - 1) & 1, st, prof ? 1u : 0u, spec ? 1u : 0u);
-  if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
+  // sampled: the launch times itself (timed = 2); PROFILE_ALL keeps the events
+  if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[0], st);
+  if (k > 0) launch_sync_diff(d, (k - 1) & 1, st, prof ? (prof->all ? 1u : 2u) : 0u, spec ? 1u : 0u);
+  if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[1], st);
+}
+
+// link delays: SYNC / SYNC_ACK messages due in the next tick back into this tick's buffer, then the delayed messages
+// of this tick into the store (k_sync_diff of the next tick skips them)
+__global__ void __launch_bounds__(256) k_sync_redeliver(Dev d, uint32_t k, uint32_t spec) {
+  if (spec && *(volatile uint32_t*)d.halt) return;
+  __shared__ uint32_t slot[2];
+  const uint32_t b = k & 1;
+  for (uint32_t e = blockIdx.x; e < d.DSCAP; e += gridDim.x) {
+    if (!d.ds_used[e] || d.ds_msg[e].due != k + 1u) continue;
+    if (threadIdx.x == 0) {
+      slot[0] = atomicAdd(&d.nmsg[b], 1u);
+      slot[1] = atomicAdd(&d.arena_used[b], 1u);
+      if (slot[0] >= d.MSGCAP) set_err(d, E_MSGS);
+      if (slot[1] >= d.ARENA_ROWS) set_err(d, E_ARENA);
+    }
+    __syncthreads();
+    const uint32_t i = slot[0], r = slot[1];
+    if (i < d.MSGCAP && r < d.ARENA_ROWS) {
+      const uint32_t* src = d.ds_row + (size_t)e * d.NS;
+      uint32_t* dst = d.arena[b] + (size_t)r * d.NS;
+      for (uint32_t s = threadIdx.x; s < d.NS; s += blockDim.x) dst[s] = src[s];
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        SyncMsg m = d.ds_msg[e];
+        m.kind &= ~KF_DEFER;
+        m.payload = r;
+        m.ncand = 0;
+        m.pad = NEVER;
+        m.pin = NEVER;
+        d.msgs[b][i] = m;
+        const uint32_t old = atomicExch(&d.m_head[(size_t)b * d.N + m.dst], i);
+        d.m_next[(size_t)b * d.MSGCAP + i] = old;
+        if (old != NEVER) {
+          pin_msg(d, b, i);
+          pin_msg(d, b, old);
+        }
+      }
+    }
+    if (threadIdx.x == 0) {
+      d.ds_used[e] = 0;
+      d.ds_free[atomicAdd(d.ds_top, 1)] = e;
+    }
+    __syncthreads();
+  }
+}
+__global__ void __launch_bounds__(256) k_sync_defer(Dev d, uint32_t k, uint32_t spec) {
+  if (spec && *(volatile uint32_t*)d.halt) return;
+  __shared__ int32_t slot;
+  const uint32_t b = k & 1, n = min(d.nmsg[b], d.MSGCAP);
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const SyncMsg mm = d.msgs[b][i];
+    if (!(mm.kind & KF_DEFER)) continue;
+    if (threadIdx.x == 0) {
+      const int32_t top = atomicSub(d.ds_top, 1) - 1;
+      slot = top >= 0 ? (int32_t)d.ds_free[top] : -1;
+      if (top < 0) set_err(d, E_SYNCQ);
+    }
+    __syncthreads();
+    const int32_t e = slot;
+    if (e >= 0) {  // the payload as sent: the sender's row at the end of the tick, or its copy-on-write snapshot
+      const uint32_t* src = mm.payload == NEVER ? d.rowk + lidx(d, mm.src) * d.NS : d.arena[b] + (size_t)mm.payload * d.NS;
+      uint32_t* dst = d.ds_row + (size_t)e * d.NS;
+      for (uint32_t s = threadIdx.x; s < d.NS; s += blockDim.x) dst[s] = src[s];
+      if (threadIdx.x == 0) {
+        d.ds_msg[e] = mm;
+        d.ds_used[e] = 1;
+      }
+    }
+    __syncthreads();
+  }
 }
 
 void launch_member(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool spec) {
   hipStream_t st = (hipStream_t)stream;
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[2], st);
   hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k, spec ? 3u : 1u);  // + tick_flag
+  if (d.dly_on) {
+    hipLaunchKernelGGL(k_sync_redeliver, dim3(256), dim3(256), 0, st, d, k, spec ? 1u : 0u);
+    hipLaunchKernelGGL(k_sync_defer, dim3(256), dim3(256), 0, st, d, k, spec ? 1u : 0u);
+  }
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[3], st);
 }
 

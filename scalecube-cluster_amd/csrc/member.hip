@@ -155,7 +155,8 @@ __device__ __forceinline__ bool send_sync(ML& L, uint32_t kind, uint32_t dst, ui
   const Dev& d = *L.d;
   uint32_t seq = L.syncSeq++;
   L.c[C_M]++;
-  if (lost_msg_ep(d, L.ep, kind, L.m, dst, L.k, L.m, seq)) {
+  const int e = xmit_ep(d, L.ep, kind, L.m, dst, L.k, L.m, seq);
+  if (e < 0) {
     L.c[C_LOST]++;
     return false;
   }
@@ -170,7 +171,7 @@ __device__ __forceinline__ bool send_sync(ML& L, uint32_t kind, uint32_t dst, ui
   SyncMsg mm;
   mm.src = L.m;
   mm.dst = dst;
-  mm.kind = kind;
+  mm.kind = kind | (e > 0 ? KF_DEFER : 0u);  // a delayed one is stored at the end of the tick (k_sync_defer)
   mm.seq = seq;
   mm.cid_iss = ciss;
   mm.cid_cnt = ccnt;
@@ -185,7 +186,9 @@ __device__ __forceinline__ bool send_sync(ML& L, uint32_t kind, uint32_t dst, ui
   SyncMsg* q = &d.msgs[b][i];
   q->src = mm.src, q->dst = mm.dst, q->kind = mm.kind, q->seq = mm.seq, q->cid_iss = mm.cid_iss;
   q->cid_cnt = mm.cid_cnt, q->payload = mm.payload, q->psize = mm.psize, q->ncand = mm.ncand, q->pad = mm.pad;
+  q->due = L.k + d.lat + (uint32_t)e;
   L.pend = i;
+  if (e > 0) return true;  // not linked to the receiver's inbound list before its delivery tick
   // the receiver's inbound list for the next tick (sharded handles build it when the exchange commits the list);
   // a receiver with several payloads gets them pinned (pin_msg)
   if (d.W == 1) {
@@ -452,6 +455,8 @@ __device__ __forceinline__ uint32_t known_meta(const ML& L, uint32_t subj, uint6
 }
 
 __device__ __forceinline__ uint32_t* grp(ML& L, int g) { return L.groups + (size_t)g * GREC; }
+// a fetch whose timeout fired while its request was still in flight (a delay): only its hops remain
+constexpr uint32_t FETCH_ORPHAN = 0xFFFFFFFEu;
 
 __device__ __forceinline__ void complete_group(ML& L, int g) {
   uint32_t* G = grp(L, g);
@@ -502,7 +507,8 @@ __device__ __forceinline__ void fetch_md(ML& L, uint32_t subj, uint32_t st, uint
   const Dev& d = *L.d;
   uint32_t cnt = L.cidCnt++;
   L.c[C_M]++;
-  if (lost_msg_ep(d, L.ep, K_GMD_REQ, L.m, subj, L.k, L.m, cnt)) {
+  const int e = xmit_ep(d, L.ep, K_GMD_REQ, L.m, subj, L.k, L.m, cnt);
+  if (e < 0) {
     L.c[C_LOST]++;
     if (g >= 0) grp(L, g)[5] |= GF_ERROR;
     do_finally(L, subj, st, inc, reason);
@@ -519,7 +525,7 @@ __device__ __forceinline__ void fetch_md(ML& L, uint32_t subj, uint32_t st, uint
   f[3] = st | (reason << 8) | (added << 16) | (1u << 24);  // stage 1: response hop pending
   f[4] = (uint32_t)g;
   f[5] = L.k + d.md_t;
-  f[6] = L.k + d.lat;
+  f[6] = L.k + d.lat + (uint32_t)e;
   f[7] = NONE32;
   L.fnext = min(L.fnext, min(f[5], f[6]));
   if (g >= 0) grp(L, g)[4]++;
@@ -662,13 +668,14 @@ __device__ __forceinline__ void ping_req_step(ML& L, uint32_t target, uint32_t c
   for (uint32_t q = 0; q < nh; ++q) {
     uint32_t h = helpers[q];
     L.c[C_M]++;
-    if (lost_msg_ep(d, L.ep, K_PING_REQ, L.m, h, L.k, L.m, cnt)) {
+    const int e = xmit_ep(d, L.ep, K_PING_REQ, L.m, h, L.k, L.m, cnt);
+    if (e < 0) {
       L.c[C_LOST]++;
       on_fd_event(L, target, ST_SUSPECT);
       continue;
     }
     add_sub(L, cnt, 1, target, L.k + (uint32_t)timeLeft);
-    add_path(L, cnt, P_REQ | 1, L.k + d.lat, h, target);
+    add_path(L, cnt, P_REQ | 1, L.k + d.lat + (uint32_t)e, h, target);
   }
 }
 
@@ -684,13 +691,14 @@ __device__ __forceinline__ void do_ping(ML& L) {
   uint32_t target = L.fdl[L.pingIdx++];
   uint32_t cnt = L.cidCnt++;
   L.c[C_M]++;
-  if (lost_msg_ep(d, L.ep, K_PING, L.m, target, L.k, L.m, cnt)) {
+  const int e = xmit_ep(d, L.ep, K_PING, L.m, target, L.k, L.m, cnt);
+  if (e < 0) {
     L.c[C_LOST]++;
     ping_req_step(L, target, cnt);
     return;
   }
   add_sub(L, cnt, 0, target, L.k + mc_timeout_t(d, L.m));
-  add_path(L, cnt, P_DIRECT | 1, L.k + d.lat, target, 0);
+  add_path(L, cnt, P_DIRECT | 1, L.k + d.lat + (uint32_t)e, target, 0);
 }
 
 // doSpreadGossip (GossipProtocolImpl.java:139-157) target selection (:252-273). The sends and the sweep run in
@@ -1045,7 +1053,10 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   // SWIM_EXP & 128: the largest per-member cycles of each phase instead (which phase makes the longest lane)
   const bool prof = (d.exp & (16 | 128)) != 0;
   unsigned long long tp = prof ? clock64() : 0;
+  // SWIM_EXP & 512: the wave's first busy lane stamps the wall clock after each phase group (wt[4 + slot])
+  const bool wlead = (d.exp & 512) && (threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)__ballot(1)) - 1);
   auto lap = [&](int slot) {
+    if (wlead) d.wt[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + 4 + slot] = wall_clock64();
     if (!prof) return;
     const unsigned long long t = clock64();
     if (d.exp & 16)
@@ -1201,12 +1212,13 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
             keep = false;
           } else {
             L.c[C_M]++;
-            if (lost_msg_ep(d, L.ep, K_PING_ACK, a, m, k, m, cnt)) {
+            const int e = xmit_ep(d, L.ep, K_PING_ACK, a, m, k, m, cnt);
+            if (e < 0) {
               L.c[C_LOST]++;
               keep = false;
             } else {
               stage = P_DIRECT | P_ARRIVE;
-              tk = k + d.lat;
+              tk = k + d.lat + (uint32_t)e;
             }
           }
         } else {  // ping-req chain: helper a, target b
@@ -1215,19 +1227,19 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
             keep = false;
           } else {
             L.c[C_M]++;
-            bool lost;
+            int e;
             if (st == 1)  // onPingReq (:258-284): transit PING helper -> target
-              lost = lost_msg_ep(d, L.ep, K_PING, a, b, k, m, cnt);
+              e = xmit_ep(d, L.ep, K_PING, a, b, k, m, cnt);
             else if (st == 2)  // onPing at the target: PING_ACK target -> helper
-              lost = lost_msg_ep(d, L.ep, K_PING_ACK, b, a, k, m, cnt);
+              e = xmit_ep(d, L.ep, K_PING_ACK, b, a, k, m, cnt);
             else  // onTransitPingAck (:290-315): PING_ACK helper -> issuer
-              lost = lost_msg_ep(d, L.ep, K_PING_ACK, a, m, k, m, cnt);
-            if (lost) {
+              e = xmit_ep(d, L.ep, K_PING_ACK, a, m, k, m, cnt);
+            if (e < 0) {
               L.c[C_LOST]++;
               keep = false;
             } else {
               stage = P_REQ | (st == 3 ? P_ARRIVE : st + 1);
-              tk = k + d.lat;
+              tk = k + d.lat + (uint32_t)e;
             }
           }
         }
@@ -1292,19 +1304,20 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
           lo.w &= 0x00FFFFFFu;
         } else {
           L.c[C_M]++;
-          if (lost_msg_ep(d, L.ep, K_GMD_RESP, subj, m, k, m, lo.x)) {
+          const int e = xmit_ep(d, L.ep, K_GMD_RESP, subj, m, k, m, lo.x);
+          if (e < 0) {
             L.c[C_LOST]++;
             lo.w &= 0x00FFFFFFu;
           } else {
             lo.w = (lo.w & 0x00FFFFFFu) | (2u << 24);
-            hi.z = k + d.lat;
+            hi.z = k + d.lat + (uint32_t)e;
             hi.w = d.md_version[subj];
           }
         }
-        keep = !dead || (lo.w >> 24) == 1;
+        keep = (!dead && hi.x != FETCH_ORPHAN) || (lo.w >> 24) == 1;
       } else if (stage == 2 && hi.z == k) {
         keep = false;
-        if (!dead) {  // doOnSuccess (:563-567, :576-581): updateMetadata then sink.next
+        if (!dead && hi.x != FETCH_ORPHAN) {  // doOnSuccess (:563-567, :576-581): updateMetadata then sink.next
           const uint32_t subj = lo.y, inc = lo.z, w3 = lo.w, meta = hi.w;
           const int g = (int)hi.x;
           const uint32_t st = w3 & 0xFF, reason = (w3 >> 8) & 0xFF, added = (w3 >> 16) & 0xFF;
@@ -1431,18 +1444,22 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
     for (uint32_t q = 0; q < nf; ++q) {
       uint32_t* f = L.fetch + (size_t)q * FREC;
       const uint4 lo = *(const uint4*)f, hi = *(const uint4*)(f + 4);
+      uint4 h2 = hi;
       if (hi.y == k) {
         const int g = (int)hi.x;
         if (g >= 0) grp(L, g)[4]--;
         finish(L, g, false);
         do_finally(L, lo.y, lo.w & 0xFF, lo.z, (lo.w >> 8) & 0xFF);
-        continue;
+        if ((lo.w >> 24) != 1) continue;
+        // the request is still in flight (delayed past the timeout): the subject still answers it, into nothing
+        h2.x = FETCH_ORPHAN;
+        h2.y = NEVER;
       }
-      fn = min(fn, (lo.w >> 24) != 0 ? min(hi.y, hi.z) : hi.y);
-      if (w != q) {
+      fn = min(fn, (lo.w >> 24) != 0 ? min(h2.y, h2.z) : h2.y);
+      if (w != q || h2.x != hi.x) {
         uint32_t* o = L.fetch + (size_t)w * FREC;
         *(uint4*)o = lo;
-        *(uint4*)(o + 4) = hi;
+        *(uint4*)(o + 4) = h2;
       }
       w++;
     }
@@ -1548,7 +1565,7 @@ __global__ void __launch_bounds__(256) k_member_tick(const Dev* __restrict__ dp,
   if ((flag & 2u) && *(volatile uint32_t*)d.halt) return;  // a speculative batch halted at an earlier tick
   // SWIM_EXP & 512 (timing experiment): wall clock of each wave at entry, after triage, after its bodies, at exit
   const bool wtime = (d.exp & 512) != 0;
-  unsigned long long* wt = wtime ? d.wt + ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 4 : nullptr;
+  unsigned long long* wt = wtime ? d.wt + ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 : nullptr;
   if (wtime && (threadIdx.x & 63) == 0) wt[0] = wall_clock64();
   __shared__ uint32_t wc[4][4];  // [wave][class] busy members
   __shared__ uint32_t list[256];

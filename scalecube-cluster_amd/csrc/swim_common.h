@@ -95,7 +95,8 @@ SW_HD u32x4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t 
 SW_HD uint32_t pick(const u32x4& r, uint32_t i) { return i == 0 ? r.x : i == 1 ? r.y : i == 2 ? r.z : r.w; }
 
 constexpr uint32_t SALT_SEL = 0x53454C31u, SALT_INIT = 0x494E4954u, SALT_LOSS_BASE = 0x4C4F5300u,
-                   SALT_LOSS_GOSSIP = 0x474F5353u, SALT_CHURN = 0x43485552u;
+                   SALT_LOSS_GOSSIP = 0x474F5353u, SALT_CHURN = 0x43485552u, SALT_DELAY_BASE = 0x444C5900u,
+                   SALT_DELAY_GOSSIP = 0x444C5947u;
 // message kinds (loss-key salts; SEMANTICS.md §2)
 constexpr uint32_t K_SYNC = 1, K_SYNC_ACK = 2, K_PING = 3, K_PING_REQ = 4, K_PING_ACK = 5, K_GMD_REQ = 6,
                    K_GMD_RESP = 7;
@@ -110,6 +111,12 @@ SW_HD uint32_t loss_roll(uint32_t seed_lo, uint32_t seed_hi, uint32_t kind, uint
                          uint32_t aux, uint32_t id) {
   const u32x4 r = philox(src, dst, k, id, seed_lo ^ (SALT_LOSS_BASE + kind), seed_hi ^ (aux * 0x9E3779B9u));
   return next_int(r.x, 100);
+}
+
+// NetworkLinkSettings.evaluateDelay (:64-74): the DELAY_<kind> draw of one message, same counter words as its loss draw
+SW_HD uint32_t delay_draw(uint32_t seed_lo, uint32_t seed_hi, uint32_t kind, uint32_t src, uint32_t dst, uint32_t k,
+                          uint32_t aux, uint32_t id) {
+  return philox(src, dst, k, id, seed_lo ^ (SALT_DELAY_BASE + kind), seed_hi ^ (aux * 0x9E3779B9u)).x;
 }
 
 SW_HD uint64_t mix64(uint64_t z) {

@@ -19,6 +19,7 @@ FLAG_RECORD_EVENTS = 1
 FLAG_PROFILE = 2
 FLAG_PROFILE_ALL = 4
 FLAG_IMPLICIT_VIEWS = 8
+FLAG_EMULATOR_COUNTERS = 16
 
 EV_ADDED, EV_REMOVED, EV_UPDATED, EV_GOSSIP = 0, 1, 2, 3
 META_NONE = 0xFFFFFFFF
@@ -56,7 +57,8 @@ class SwimConfig(C.Structure):
         ("churn_per_period", C.c_uint32),
         ("n_dormant", C.c_uint32),
         ("gossip_ring_cap", C.c_uint32),
-        ("reserved", C.c_uint32 * 3),
+        ("delay_cap_ms", C.c_uint32),
+        ("reserved", C.c_uint32 * 2),
     ]
 
 
@@ -123,6 +125,9 @@ SIGNATURES = {
     "swim_set_partition": (C.c_int, [_H, _U32P]),
     "swim_unblock_all": (C.c_int, [_H]),
     "swim_set_link_loss": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.c_uint32]),
+    "swim_set_default_link_settings": (C.c_int, [_H, C.c_uint32, C.c_uint32]),
+    "swim_set_link_settings": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
+    "swim_emulator_counters": (C.c_int, [_H, C.POINTER(C.c_uint64), C.c_size_t]),
     "swim_unblock_link": (C.c_int, [_H, C.c_uint32, C.c_uint32]),
     "swim_update_incarnation": (C.c_int, [_H, C.c_uint32]),
     "swim_update_metadata": (C.c_int, [_H, C.c_uint32]),

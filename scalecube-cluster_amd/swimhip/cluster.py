@@ -171,6 +171,21 @@ class SimulatedCluster:
         """NetworkEmulator.setLinkSettings on src's emulator for destination dst; 100 = block(dst)."""
         self._ck(self.lib.swim_set_link_loss(self._h, src, dst, pct), "swim_set_link_loss")
 
+    def set_default_link_settings(self, loss, mean_delay_ms):
+        """NetworkEmulator.setDefaultLinkSettings(lossPercent, meanDelay) (NetworkEmulator.java:113-125)."""
+        self._ck(self.lib.swim_set_default_link_settings(self._h, loss, mean_delay_ms), "swim_set_default_link_settings")
+
+    def set_link_settings(self, src, dst, loss, mean_delay_ms):
+        """NetworkEmulator.setLinkSettings(dst, lossPercent, meanDelay) on src's emulator (NetworkEmulator.java:97-111)."""
+        self._ck(self.lib.swim_set_link_settings(self._h, src, dst, loss, mean_delay_ms), "swim_set_link_settings")
+
+    def emulator_counters(self):
+        """Every member's (totalMessageSentCount, totalMessageLostCount) (NetworkEmulator.java:200-222), shape (n, 2)."""
+        out = np.zeros(2 * self.n, dtype=np.uint64)
+        self._ck(self.lib.swim_emulator_counters(self._h, out.ctypes.data_as(C.POINTER(C.c_uint64)), out.size),
+                 "swim_emulator_counters")
+        return out.reshape(self.n, 2)
+
     def block(self, src, *dsts):
         """NetworkEmulator.block(destinations) on src's emulator (NetworkEmulator.java:141-150)."""
         for dst in dsts:

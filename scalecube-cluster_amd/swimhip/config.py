@@ -65,8 +65,10 @@ class SimConfig:
     profile: bool = False
     profile_all: bool = False  # SWIM_FLAG_PROFILE_ALL: every k_sync_diff launch timed (+ member / gossip kernels)
     implicit_views: bool = False  # SWIM_FLAG_IMPLICIT_VIEWS (RUMOR mode): tables / lists computed, not stored
+    emulator_counters: bool = False  # SWIM_FLAG_EMULATOR_COUNTERS: per-member NetworkEmulator sent / lost counts
     gossip_slot_cap: int = 0
     gossip_ring_cap: int = 0  # gossips one member can hold at once (0: the engine's default)
+    delay_cap_ms: int = 0  # the largest mean link delay this handle will be given (sizes the engine's delay queues)
     pending_fetch_cap: int = 0
     event_cap: int = 0
     list_slack: int = 0
@@ -99,7 +101,8 @@ class SimConfig:
         a.n_dormant = self.n_dormant
         a.flags = (_abi.FLAG_RECORD_EVENTS if self.record_events else 0) | (_abi.FLAG_PROFILE if self.profile or self.profile_all else 0) \
             | (_abi.FLAG_PROFILE_ALL if self.profile_all else 0) \
-            | (_abi.FLAG_IMPLICIT_VIEWS if self.implicit_views else 0)
+            | (_abi.FLAG_IMPLICIT_VIEWS if self.implicit_views else 0) \
+            | (_abi.FLAG_EMULATOR_COUNTERS if self.emulator_counters else 0)
         seeds = list(dict.fromkeys(c.seedMembers))
         if len(seeds) > 16:
             raise ValueError("at most 16 seed members")
@@ -108,6 +111,7 @@ class SimConfig:
             a.seeds[i] = s
         a.gossip_slot_cap = self.gossip_slot_cap
         a.gossip_ring_cap = self.gossip_ring_cap
+        a.delay_cap_ms = self.delay_cap_ms
         a.pending_fetch_cap = self.pending_fetch_cap
         a.event_cap = self.event_cap
         a.n_gpus = self.n_gpus
