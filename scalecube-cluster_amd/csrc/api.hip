@@ -342,6 +342,7 @@ int build(swim_handle* h) {
       return SWIM_EINVAL;
     }
     d.EMAX = (uint32_t)t.size();
+    d.PCAP = c.delay_cap_ms ? PATHCAP_DELAY : PATHCAP;
     if (d.EMAX && d.W > 1) {
       h->err = "link delays on a row-sharded handle";
       return SWIM_EUNSUPPORTED;
@@ -441,7 +442,7 @@ int build(swim_handle* h) {
   const uint64_t NL = d.NL;  // per-observer arrays: this shard's rows only
   const uint64_t NV = d.implicit ? 1 : NL;  // implicit views: no table or list is stored
   A(d.rowk, NV * d.NS) A(d.rowa, NV * d.NS) A(d.fdl, NV * d.LCAP) A(d.gl, NV * d.LCAP)
-  A(d.subs, NL * SUBCAP * 4) A(d.paths, NL * PATHCAP * 5) A(d.fetch, NL * d.FCAP * FREC) A(d.groups, NL * d.GRCAP * GREC)
+  A(d.subs, NL * SUBCAP * 4) A(d.paths, NL * d.PCAP * 5) A(d.fetch, NL * d.FCAP * FREC) A(d.groups, NL * d.GRCAP * GREC)
   A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.slow, d.SLOWCAP) A(d.slow_n, 1) A(d.rp, d.RPCAP) A(d.rp_n, 1) A(d.start_tick, N) A(d.jseed_n, N) A(d.jseeds, 16 * N) A(d.md_uidx, N) A(d.mcfg, 4 * N) A(d.md_ver, NL * MDU) A(d.churn_q, 2ull * d.churn) A(d.ucnt, N) A(d.cin, N * d.F) A(d.HB, (uint64_t)d.QW * N) A(d.WB, (uint64_t)d.QW * N) A(d.cev, N * d.F * CEVW)
   A(d.rg, (uint64_t)d.BCAP * N) A(d.rhead, N) A(d.rwin, N) A(d.rseen, N) A(d.rtail, N) A(d.rwl, N) A(d.nrwl, 1)
   A(d.rsend, N) A(d.rwnew, N) A(d.GU, d.QW) A(d.DM, d.QW) A(d.agroup, d.QW) A(d.nagroup, 2)

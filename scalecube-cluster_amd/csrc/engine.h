@@ -20,6 +20,9 @@ constexpr uint32_t NEVER = 0xFFFFFFFFu;
 constexpr uint32_t MAX_EPOCHS = 8;
 constexpr uint32_t DTAB = 16;  // distinct mean delays per handle (delay index 0: none)
 constexpr uint32_t SUBCAP = 8, PATHCAP = 8, FREC = 8, GREC = 8;
+// pending virtual hops per member with link delays (swim_config.delay_cap_ms > 0): a delayed ping-req chain stays
+// open for up to 4 x (lat + EMAX) ticks, several FD periods, so more of them overlap (Dev::PCAP <= 32)
+constexpr uint32_t PATHCAP_DELAY = 32;
 constexpr uint32_t CH = 2048;  // subjects per SYNC-diff work item (256 threads x 8)
 constexpr uint32_t TRK = 16;   // subjects written in one tick's P1 that are re-checked against later payloads
 // deferred copy-on-write (member.hip cow): row writes logged per member and tick while a snapshot is open, open
@@ -158,7 +161,8 @@ struct Dev {
   uint32_t *fdl, *gl;  // [N][LCAP]
 
   uint32_t* subs;    // [N][SUBCAP][4]  cnt, kind, target, deadline
-  uint32_t* paths;   // [N][PATHCAP][5] cnt, stage, tick, a, b
+  uint32_t* paths;   // [N][PCAP][5] cnt, stage, tick, a, b
+  uint32_t PCAP;     // PATHCAP, or PATHCAP_DELAY when link delays are enabled
   uint32_t* fetch;   // [N][FCAP][FREC]
   uint32_t* groups;  // [N][GRCAP][GREC]  pending Mono.whenDelayError groups (SYNC replies, initial sync)
 

@@ -482,14 +482,15 @@ __device__ void contact_cache(const Dev& d, uint32_t i, uint32_t m, uint32_t t, 
       if (ev[j].dir == 0) last_in = ev[j].tick;  // events are in tick order
     }
   rec[3] = last_in;
-  // a gossip inside m's window this round was created after tick k - (spread + 1) * gossip_t, so a contact t -> m
-  // at or before that tick - lat can never put t in infectedFrom_m of any gossip m sends now
+  // a gossip inside m's window this round was received after tick k - (spread + 1) * gossip_t, so a contact t -> m
+  // that arrived at or before that tick (sent at most lat + dmax ticks earlier) can never put t in infectedFrom_m of
+  // any gossip m sends now
   const int64_t horizon = (int64_t)k - (int64_t)(d.tspread[m] + 1u) * d.gossip_t;
   uint32_t ci;
   if (n > CEV)
     ci = CIN_SLOW;
   else
-    ci = last_in == NEVER || (int64_t)last_in + d.lat <= horizon ? NEVER : last_in;
+    ci = last_in == NEVER || (int64_t)last_in + d.lat + dmax(d) <= horizon ? NEVER : last_in;
   d.crow[i] = RX_ALL;
   if (ci != NEVER && ci != CIN_SLOW) {
     // Only gossips m received at or before the latest contact t -> m arrived (last_in + lat) can have t in
@@ -672,7 +673,9 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
         }
         if (dead_at(d, t, k)) continue;  // refused before the emulator: nothing delivered or counted
         const uint32_t ls = link_set(d, ep, m, t, k), pct = ls & 0xFFu, di = ls >> 8;
-        const unsigned long long drawn = d.em ? w : cand;  // the counters need every send's loss outcome
+        // the counters need every send's loss outcome, and so does a delayed send to a holder: the target may sweep
+        // the gossip before it arrives, and then it is a first receipt again (onGossipReq :171-183 at arrival)
+        const unsigned long long drawn = (d.em || di) ? w : cand;
         unsigned long long lostm = 0;
         if (pct >= 100) {
           lostm = drawn;
@@ -684,11 +687,11 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
         }
         em_count(d, m, (uint32_t)__popcll(w), (uint32_t)__popcll(lostm & w));
         unsigned long long ok = cand & ~lostm;
-        if (di)
-          for (unsigned long long b = ok; b; b &= b - 1) {
+        if (di)  // every delivered send that arrives after the next tick is queued (k_gossip_due decides at arrival)
+          for (unsigned long long b = w & ~lostm; b; b &= b - 1) {
             const uint32_t j = (uint32_t)(__ffsll((long long)b) - 1), g = q * 64u + j;
             const uint32_t e = gossip_delay(d, di, m, k, s, d.slot_gid[g]);
-            if (e) {  // arrives after the next tick: queued (k_gossip_due)
+            if (e) {
               ok &= ~(1ull << j);
               delay_push(d, g, t, k + d.lat + e);
             }
@@ -786,15 +789,16 @@ __device__ __forceinline__ void deliver_one(const Dev& d, uint32_t g, uint32_t m
     if (dead_at(d, t, k)) return;
     const uint32_t ls = link_set(d, ep, m, t, k), pct = ls & 0xFFu, di = ls >> 8;
     const bool held = (*hw & bit) != 0ull;
-    if (held && !d.em) return;
+    if (held && !d.em && !di) return;
     const bool lost = pct >= 100 || (pct > 0 && next_int(gossip_loss_word(d, m, k, s, gid), 100) < pct);
     em_count(d, m, 1u, lost ? 1u : 0u);
-    if (held || lost) return;
+    if (lost) return;
     const uint32_t e = gossip_delay(d, di, m, k, s, gid);
-    if (e) {
+    if (e) {  // decided at arrival (a holder may have swept it by then): k_gossip_due
       delay_push(d, g, t, k + d.lat + e);
       return;
     }
+    if (held) return;
   } else {
     if (*hw & bit) return;
     if (lost_gossip_ep(d, ep, m, t, k, s, gid)) return;

@@ -606,7 +606,7 @@ __device__ __forceinline__ void add_sub(ML& L, uint32_t cnt, uint32_t kind, uint
   s[3] = deadline;
 }
 __device__ __forceinline__ void add_path(ML& L, uint32_t cnt, uint32_t stage, uint32_t tick, uint32_t a, uint32_t b) {
-  if (L.npath >= PATHCAP) {
+  if (L.npath >= L.d->PCAP) {
     set_err(*L.d, E_PATHS);
     return;
   }
@@ -1033,7 +1033,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   L.fdl = d.fdl + li * d.LCAP;
   L.gl = d.gl + li * d.LCAP;
   L.subs = d.subs + li * SUBCAP * 4;
-  L.paths = d.paths + li * PATHCAP * 5;
+  L.paths = d.paths + li * d.PCAP * 5;
   L.fetch = d.fetch + li * d.FCAP * FREC;
   L.groups = d.groups + li * d.GRCAP * GREC;
   for (int i = 0; i < 8; ++i) L.c[i] = 0;
@@ -1195,8 +1195,8 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   lap(0);  // P0 + P1
   // ---- P2 FD: remote hops of pending pings, then PING_ACK arrivals in cid order ----
   if (L.npath) {
-    uint32_t arr[PATHCAP];
-    uint32_t narr = 0;
+    // arrivals stay in the compacted list this pass, marked by their new index (at most PATHCAP_DELAY = 32 entries)
+    uint32_t arrmask = 0;
     uint32_t w = 0;
     for (uint32_t p = 0; p < L.npath; ++p) {
       uint32_t* P = L.paths + (size_t)p * 5;
@@ -1205,8 +1205,8 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
       if (tk == k) {
         uint32_t kind = stage & 0xF0, st = stage & 0xF;
         if (st == P_ARRIVE) {
-          if (!dead) arr[narr++] = cnt;
-          keep = false;
+          if (dead) keep = false;
+          else arrmask |= 1u << w;
         } else if (kind == P_DIRECT) {  // onPing at the target (:230-255): PING_ACK back to the issuer
           if (dead_at(d, a, k)) {
             keep = false;
@@ -1255,16 +1255,17 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
       }
     }
     L.npath = w;
-    // arrivals: every pending subscription on the cid takes the first PING_ACK (TransportImpl.java:205-232)
-    for (uint32_t i = 1; i < narr; ++i)
-      for (uint32_t j = i; j > 0 && arr[j - 1] > arr[j]; --j) {
-        uint32_t t = arr[j];
-        arr[j] = arr[j - 1];
-        arr[j - 1] = t;
+    // arrivals: every pending subscription on the cid takes the first PING_ACK (TransportImpl.java:205-232), in cid
+    // order; then the arrived entries leave the list
+    const uint32_t narr = __popc(arrmask);
+    for (uint32_t done = 0, last = 0; done < narr;) {
+      uint32_t cnt = NEVER;  // the smallest arrived cid above the last one handled
+      for (uint32_t q = 0; q < w; ++q) {
+        const uint32_t c = L.paths[(size_t)q * 5];
+        if (((arrmask >> q) & 1u) && (done == 0 || c > last) && c < cnt) cnt = c;
       }
-    for (uint32_t i = 0; i < narr; ++i) {
-      if (i && arr[i] == arr[i - 1]) continue;
-      uint32_t cnt = arr[i];
+      for (uint32_t q = 0; q < w; ++q) done += ((arrmask >> q) & 1u) && L.paths[(size_t)q * 5] == cnt;
+      last = cnt;
       uint32_t hit[SUBCAP], nh = 0, w2 = 0;
       for (uint32_t s = 0; s < L.nsub; ++s) {
         uint32_t* S4 = L.subs + (size_t)s * 4;
@@ -1281,6 +1282,16 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
       }
       L.nsub = w2;
       for (uint32_t q = 0; q < nh; ++q) on_fd_event(L, hit[q], ST_ALIVE);  // publishPingResult(ALIVE)
+    }
+    if (arrmask) {
+      uint32_t w3 = 0;
+      for (uint32_t p = 0; p < w; ++p)
+        if (!((arrmask >> p) & 1u)) {
+          if (w3 != p)
+            for (uint32_t q = 0; q < 5; ++q) L.paths[(size_t)w3 * 5 + q] = L.paths[(size_t)p * 5 + q];
+          w3++;
+        }
+      L.npath = w3;
     }
   }
 
