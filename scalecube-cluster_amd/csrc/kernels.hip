@@ -527,7 +527,12 @@ void launch_diff(const Dev& d, uint32_t k, void* stream, const TickEvents* prof,
 // link delays: SYNC / SYNC_ACK messages due in the next tick back into this tick's buffer, then the delayed messages
 // of this tick into the store (k_sync_diff of the next tick skips them)
 __global__ void __launch_bounds__(256) k_sync_redeliver(Dev d, uint32_t k, uint32_t spec) {
-  if (spec && *(volatile uint32_t*)d.halt) return;
+  // a speculative batch halted at an earlier tick (halt = k + 1: this tick's member kernel ran and raised it, and its
+  // delayed messages still move)
+  if (spec) {
+    const uint32_t hk = *(volatile uint32_t*)d.halt;
+    if (hk != 0 && hk <= k) return;
+  }
   __shared__ uint32_t slot[2];
   const uint32_t b = k & 1;
   for (uint32_t e = blockIdx.x; e < d.DSCAP; e += gridDim.x) {
@@ -569,7 +574,12 @@ __global__ void __launch_bounds__(256) k_sync_redeliver(Dev d, uint32_t k, uint3
   }
 }
 __global__ void __launch_bounds__(256) k_sync_defer(Dev d, uint32_t k, uint32_t spec) {
-  if (spec && *(volatile uint32_t*)d.halt) return;
+  // a speculative batch halted at an earlier tick (halt = k + 1: this tick's member kernel ran and raised it, and its
+  // delayed messages still move)
+  if (spec) {
+    const uint32_t hk = *(volatile uint32_t*)d.halt;
+    if (hk != 0 && hk <= k) return;
+  }
   __shared__ int32_t slot;
   const uint32_t b = k & 1, n = min(d.nmsg[b], d.MSGCAP);
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {

@@ -41,8 +41,9 @@ def test_gossip_protocol_grid(oracle, engine, n, loss, delay):
 def test_full_stack_delays(oracle, engine, delay):
     """Every message kind late: pings and acks past the ping timeout (ping-req then resolves on the late direct ack),
     SYNC / SYNC_ACK payloads stored as sent, metadata responses past their timeout (1100 ms mean: ~6 % of them)."""
+    # 1100 ms means: most FD rounds time out, so suspicion gossips pile up (more slots than the 64 per member default)
     cfg = SimConfig(n_members=40, cluster=ClusterConfig(syncInterval=3000, metadataTimeout=1000), record_events=True,
-                    emulator_counters=True, delay_cap_ms=1100)
+                    emulator_counters=True, delay_cap_ms=1100, gossip_slot_cap=8192)
     o, e = both(oracle, engine, cfg)
     for c in (o, e):
         c.set_default_link_settings(5, delay)
@@ -53,6 +54,7 @@ def test_full_stack_delays(oracle, engine, delay):
         c.update_metadata(11)
     run_lockstep(o, e, 400, 40, f"delay {delay} kill")
     same_emulators(o, e, f"delay {delay}")
+    print(f"delay {delay}: {o.counters()['gossips_created']} gossips created, {o.counters()['messages']} messages")
 
 
 def test_cold_join_with_delays(oracle, engine):

@@ -15,20 +15,20 @@ pytestmark = pytest.mark.gpu
 ROOT = Path(__file__).resolve().parent.parent
 
 
-@pytest.mark.parametrize("transport", ["host", "rccl"])
-def test_two_process_shards(transport, tmp_path):
+@pytest.mark.parametrize("transport,mode", [("host", "full"), ("rccl", "full"), ("rccl", "rumor")])
+def test_two_process_shards(transport, mode, tmp_path):
     import torch  # noqa: F401  (pages torch in once, before two workers import it at the same time)
     procs, logs = [], []
     for r in range(2):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT="29533" if transport == "rccl" else "29534", NCCL_HOSTID=f"swimhost{r}",
+                   MASTER_PORT={"rccl": "29533", "host": "29534"}[transport] if mode == "full" else "29535", NCCL_HOSTID=f"swimhost{r}",
                    NCCL_SOCKET_IFNAME="lo", GLOO_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1",
                    HSA_ENABLE_IPC_MODE_LEGACY="0")
         logdir = Path(os.environ.get("SWIM_TEST_LOGDIR", str(tmp_path)))
         logdir.mkdir(parents=True, exist_ok=True)
-        log = open(logdir / f"{transport}_rank{r}.log", "w")
+        log = open(logdir / f"{transport}_{mode}_rank{r}.log", "w")
         logs.append(log)
-        procs.append(subprocess.Popen([sys.executable, "-u", str(ROOT / "tests" / "shard_rccl_worker.py"), transport],
+        procs.append(subprocess.Popen([sys.executable, "-u", str(ROOT / "tests" / "shard_rccl_worker.py"), transport, mode],
                                       env=env, stdout=log, stderr=subprocess.STDOUT))
     t0 = time.time()
     timed_out = False
