@@ -70,7 +70,6 @@ struct swim_handle {
   bool no_pipe = getenv("SWIM_NO_PIPELINE") != nullptr;    // debugging aid: no early SYNC diff of the next tick
   bool no_spec = getenv("SWIM_NO_SPECULATION") != nullptr;  // debugging aid: a host wait after every member kernel
   bool gossip_idle = false;  // W == 1: no gossip slot was in use after the latest member kernel
-  int wclk_khz = 100000;     // device wall clock (wall_clock64) rate
   // timing aid (bench.py --rehearse-shard): a slot shard alone, its peers' gossip-count deltas taken as zero without
   // any exchange (not the W-shard simulation's results)
   bool lone = getenv("SWIM_LONE_SHARD") != nullptr;
@@ -460,7 +459,7 @@ int build(swim_handle* h) {
   A(d.arena[1], (uint64_t)d.ARENA_ROWS * d.NS) A(d.arena_used, 2)
   A(d.m_next, 2ull * d.MSGCAP) A(d.m_head, 2 * N) A(d.next_evt, N) A(d.mdone, 2) A(d.trk, NL * TRK) A(d.ulog, NL * ULOG * 2) A(d.spq, NL * SPQ * 8) A(d.pending_inc, N) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
   A(d.pool, d.POOLCAP) A(d.pool_used, 1)
-  A(d.ev, (uint64_t)d.EVCAP * 8) A(d.ev_n, 1) A(d.ctr, C_NCTR) A(d.err, 8) A(d.dts, 4)
+  A(d.ev, (uint64_t)d.EVCAP * 8) A(d.ev_n, 1) A(d.ctr, C_NCTR) A(d.err, 8)
   if (c.flags & SWIM_FLAG_EMULATOR_COUNTERS) {
     A(d.em, 2 * N)
     HIPCK(hipMemsetAsync(d.em, 0, 16 * N, h->stream));
@@ -552,14 +551,6 @@ int build(swim_handle* h) {
   HIPCK(hipMemsetAsync(d.ucnt, 0, N * 4, h->stream));
   HIPCK(hipMemsetAsync(d.pool_used, 0, 4, h->stream));
   HIPCK(hipMemsetAsync(d.mdone, 0, 8, h->stream));
-  {
-    const unsigned long long dts0[4] = {~0ull, 0ull, 0ull, 0ull};
-    HIPCK(hipMemcpyAsync(d.dts, dts0, sizeof(dts0), hipMemcpyHostToDevice, h->stream));
-    HIPCK(hipStreamSynchronize(h->stream));
-    if (hipDeviceGetAttribute(&h->wclk_khz, hipDeviceAttributeWallClockRate, (int)h->cfg.device) != hipSuccess ||
-        h->wclk_khz <= 0)
-      h->wclk_khz = 100000;
-  }
   d.halt = d.mdone + 1;
   HIPCK(hipMemsetAsync(d.link_n, 0, 4, h->stream));
   HIPCK(hipMemsetAsync(d.link_key, 0, 8ull * LKCAP, h->stream));
@@ -1250,10 +1241,8 @@ int swim_step(swim_handle* h, uint32_t n) {
       float ms = 0;
       if (!timed(first + i)) continue;
       if (first + i > 0) {
-        if (d.W > 1 || h->prof[i].all) {
-          HIPCK(hipEventElapsedTime(&ms, (hipEvent_t)h->prof[i].ev[0], (hipEvent_t)h->prof[i].ev[1]));
-          h->prof_ms[0] += ms;
-        }  // (one GPU, sampled: the launch timed itself, dts)
+        HIPCK(hipEventElapsedTime(&ms, (hipEvent_t)h->prof[i].ev[0], (hipEvent_t)h->prof[i].ev[1]));
+        h->prof_ms[0] += ms;
         h->prof_diff_launches++;
       }
       if (!h->prof[i].all) continue;
@@ -1745,11 +1734,6 @@ int swim_counters_get(swim_handle* h, swim_counters* out) {
   out->sync_merges = c[C_SYNCMERGE];
   out->device_bytes = h->bytes;
   out->diff_ns = (uint64_t)(h->prof_ms[0] * 1e6);
-  if (h->d.W == 1) {  // sampled launches on one GPU time themselves by the wall clock (k_sync_diff, dts[3])
-    unsigned long long raw = 0;
-    HIPCK(hipMemcpy(&raw, h->d.dts + 3, 8, hipMemcpyDeviceToHost));
-    out->diff_ns += (uint64_t)((double)raw * 1e6 / (double)h->wclk_khz);
-  }
   out->member_ns = (uint64_t)(h->prof_ms[1] * 1e6);
   out->gossip_ns = (uint64_t)(h->prof_ms[2] * 1e6);
   out->diff_launches = h->prof_diff_launches;

@@ -141,6 +141,13 @@ __device__ __forceinline__ void em_count(const Dev& d, uint32_t src, uint32_t se
   if (lost) atomicAdd(&d.em[2 * src + 1], (unsigned long long)lost);
 }
 
+// the delay draw of one non-gossip message on a link with delay index di > 0 (out of line: the member kernel inlines
+// xmit_ep at every FD / SYNC / metadata send, and the delay path only runs with link delays set)
+__device__ __noinline__ int xmit_delay(const Dev& d, uint32_t di, uint32_t kind, uint32_t src, uint32_t dst, uint32_t k,
+                                       uint32_t aux, uint32_t id) {
+  return (int)delay_ticks(d, di, delay_draw(d.seed_lo, d.seed_hi, kind, src, dst, k, aux, id));
+}
+
 // tryFail + tryDelay of one non-gossip message: -1 if the send fails, else its delay in ticks past lat
 __device__ __forceinline__ int xmit_ep(const Dev& d, int ep, uint32_t kind, uint32_t src, uint32_t dst, uint32_t k,
                                        uint32_t aux, uint32_t id) {
@@ -154,7 +161,7 @@ __device__ __forceinline__ int xmit_ep(const Dev& d, int ep, uint32_t kind, uint
   em_count(d, src, 1u, lost ? 1u : 0u);
   if (lost) return -1;
   if (di == 0) return 0;
-  return (int)delay_ticks(d, di, delay_draw(d.seed_lo, d.seed_hi, kind, src, dst, k, aux, id));
+  return xmit_delay(d, di, kind, src, dst, k, aux, id);
 }
 
 // the gossip-send draw words (LOSS_GOSSIP, DELAY_GOSSIP: SEMANTICS.md §2) of gossip gid sent by src to target slot s

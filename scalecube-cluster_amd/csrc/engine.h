@@ -264,7 +264,6 @@ struct Dev {
   uint32_t* ev;  // [EVCAP][8] swim_event
   uint32_t* ev_n;
   unsigned long long* ctr;  // [C_NCTR]
-  unsigned long long* dts;  // [4] timed k_sync_diff launches on one GPU: first start, last end, blocks done, summed wall-clock ticks
   unsigned long long* wt;   // SWIM_EXP & 512: per-wave timestamps of the latest k_member_tick [waves][16]
   uint32_t* err;            // [8] bits, info...
   const Dev* self;          // device-resident copy of this struct (kernels index it through a pointer)

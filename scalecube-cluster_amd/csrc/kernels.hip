@@ -345,10 +345,9 @@ __global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b, uint32_t t
   if (spec && *(volatile uint32_t*)d.halt) return;  // a speculative batch halted at an earlier tick
   __shared__ uint32_t scan[256];
   __shared__ uint32_t base;
-  // timed (one GPU): the launch times itself, first block start to last block end (no event around it: a stream
-  // event writes back the L2 and opens a ~6 us gap)
-  const bool selftime = timed == 2u;
-  if (selftime && threadIdx.x == 0) atomicMin(&d.dts[0], (unsigned long long)wall_clock64());
+  // (timed launches are bracketed by HIP events on the stream. A self-timing variant, first block start to last block
+  // end by wall clock and atomics, made every launch of this kernel 30 % slower by its mere presence in the code:
+  // 85 -> 112 us per launch at C3, profiles/r03_*)
   uint32_t nmsg = d.nmsg[b] < d.MSGCAP ? d.nmsg[b] : d.MSGCAP;
   if (timed && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&d.ctr[C_DIFFMSG], (unsigned long long)nmsg);
   uint32_t total = nmsg * d.NCHUNK;
@@ -412,17 +411,6 @@ __global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b, uint32_t t
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
-  }
-  if (selftime) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      atomicMax(&d.dts[1], (unsigned long long)wall_clock64());
-      if (atomicAdd(&d.dts[2], 1ull) == gridDim.x - 1u) {  // the last block: add the launch's span, reset
-        const unsigned long long t0 = atomicExch(&d.dts[0], ~0ull), t1 = atomicExch(&d.dts[1], 0ull);
-        atomicExch(&d.dts[2], 0ull);
-        atomicAdd(&d.dts[3], t1 - t0);
-      }
-    }
   }
 }
 
@@ -518,10 +506,9 @@ static void launch_sync_diff(const Dev& d, uint32_t b, hipStream_t st, uint32_t 
 // use; the SYNC diff of tick k+1 does not depend on the gossip plane of tick k and is queued in between
 void launch_diff(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool spec) {
   hipStream_t st = (hipStream_t)stream;
-  // sampled: the launch times itself (timed = 2); PROFILE_ALL keeps the events
-  if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[0], st);
-  if (k > 0) launch_sync_diff(d, (k - 1) & 1, st, prof ? (prof->all ? 1u : 2u) : 0u, spec ? 1u : 0u);
-  if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[1], st);
+  if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
+  if (k > 0) launch_sync_diff(d, (k - 1) & 1, st, prof ? 1u : 0u, spec ? 1u : 0u);
+  if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
 }
 
 // link delays: SYNC / SYNC_ACK messages due in the next tick back into this tick's buffer, then the delayed messages

@@ -1571,7 +1571,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
 // pingers per tick adding to one word would serialise on that address. With `flag` (W == 1) the block that finishes
 // last runs the end-of-tick resets and raises the host flag. flag: 1 = W == 1 (end-of-tick work), 2 = a launch of a
 // speculative batch.
-__global__ void __launch_bounds__(256) k_member_tick(const Dev* __restrict__ dp, uint32_t k, uint32_t flag) {
+__global__ void __launch_bounds__(256, 2) k_member_tick(const Dev* __restrict__ dp, uint32_t k, uint32_t flag) {
   const Dev& d = *dp;  // global, not kernarg: taking its address must not copy ~1 KB into per-lane scratch
   if ((flag & 2u) && *(volatile uint32_t*)d.halt) return;  // a speculative batch halted at an earlier tick
   // SWIM_EXP & 512 (timing experiment): wall clock of each wave at entry, after triage, after its bodies, at exit
