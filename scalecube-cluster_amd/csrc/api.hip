@@ -613,11 +613,59 @@ hipError_t spin_wait(hipEvent_t ev) {
   return e;
 }
 
+// RCCL, fixed-size part of an exchange: the inline all-to-all and its unpacking into the regions (k_inline_in also
+// publishes the count words to the host-mapped xi_host)
+int exchange_inline(swim_handle* h, uint8_t* recv, uint64_t cap, unsigned long long* scnt, unsigned long long* rcnt,
+                    bool spec) {
+  if (ncclAllToAll(h->d.xi_send, h->d.xi_recv, XINL, ncclUint8, h->comm, h->stream) != ncclSuccess) {
+    h->err = "ncclAllToAll (inline exchange) failed";
+    return SWIM_EDEVICE;
+  }
+  launch_inline_in(h->d, recv, cap, scnt, rcnt, h->stream, spec);
+  return SWIM_OK;
+}
+
+// RCCL, after the inline part has completed: the count words from xi_host (the gossip flag, the sizes) and a
+// send/recv group for the regions that did not fit inline
+int exchange_rest(swim_handle* h, uint8_t* send, uint8_t* recv, uint64_t cap) {
+  const uint32_t W = h->d.W, me = h->d.rank;
+  unsigned long long* hc = h->hcnt;
+  volatile unsigned long long* xh = h->d.xi_host;
+  for (uint32_t q = 0; q < 2 * W; ++q) hc[q] = xh[q];
+  h->xflag = false;
+  bool rest = false;
+  for (uint32_t q = 0; q < 2 * W; ++q) {
+    h->xflag |= (hc[q] & XFLAG_GOSSIP) != 0;
+    rest |= (hc[q] & XCNT_MASK) > XINL - 8;
+    if ((hc[q] & XCNT_MASK) > cap) {
+      h->err = "exchange block larger than its region";
+      return SWIM_ECAPACITY;
+    }
+  }
+  if (rest) {
+    bool ok = ncclGroupStart() == ncclSuccess;
+    for (uint32_t q = 0; q < W && ok; ++q) {
+      if (q == me) continue;
+      const uint64_t sb = hc[q] & XCNT_MASK, rb = hc[W + q] & XCNT_MASK;
+      if (sb > XINL - 8)
+        ok &= ncclSend(send + (size_t)q * cap + XINL - 8, sb - (XINL - 8), ncclUint8, (int)q, h->comm, h->stream) == ncclSuccess;
+      if (rb > XINL - 8)
+        ok &= ncclRecv(recv + (size_t)q * cap + XINL - 8, rb - (XINL - 8), ncclUint8, (int)q, h->comm, h->stream) == ncclSuccess;
+    }
+    ok &= ncclGroupEnd() == ncclSuccess;
+    if (!ok) {
+      h->err = "RCCL send/recv group failed";
+      return SWIM_EDEVICE;
+    }
+  }
+  return SWIM_OK;
+}
+
 // one all-to-all of per-peer byte blocks (fixed-capacity regions of `cap` bytes in send / recv, rank order).
 // The byte counts are device-resident (written by the pack kernels); the transport needs them on the host.
 int exchange(swim_handle* h, uint8_t* send, uint8_t* recv, uint64_t cap, unsigned long long* scnt,
              unsigned long long* rcnt, bool inline_packed) {
-  const uint32_t W = h->d.W, me = h->d.rank;
+  const uint32_t W = h->d.W;
   hipStream_t st = h->stream;
   unsigned long long* hc = h->hcnt;
   auto t0 = std::chrono::steady_clock::now();
@@ -625,41 +673,11 @@ int exchange(swim_handle* h, uint8_t* send, uint8_t* recv, uint64_t cap, unsigne
     // one fixed-size all-to-all (count word + the first XINL - 8 bytes of each region), one host read of the
     // count words through mapped memory, and a send/recv group only for regions that did not fit
     if (!inline_packed) launch_inline_out(h->d, send, cap, scnt, st);  // exchange A: k_pack_a_chunks wrote them
-    if (ncclAllToAll(h->d.xi_send, h->d.xi_recv, XINL, ncclUint8, h->comm, st) != ncclSuccess) {
-      h->err = "ncclAllToAll (inline exchange) failed";
-      return SWIM_EDEVICE;
-    }
-    launch_inline_in(h->d, recv, cap, scnt, rcnt, st);
+    int rc;
+    if ((rc = exchange_inline(h, recv, cap, scnt, rcnt, false)) != SWIM_OK) return rc;
     HIPCK(hipEventRecord(h->ev_member, st));
     HIPCK(spin_wait(h->ev_member));
-    volatile unsigned long long* xh = h->d.xi_host;
-    for (uint32_t q = 0; q < 2 * W; ++q) hc[q] = xh[q];
-    h->xflag = false;
-    bool rest = false;
-    for (uint32_t q = 0; q < 2 * W; ++q) {
-      h->xflag |= (hc[q] & XFLAG_GOSSIP) != 0;
-      rest |= (hc[q] & XCNT_MASK) > XINL - 8;
-      if ((hc[q] & XCNT_MASK) > cap) {
-        h->err = "exchange block larger than its region";
-        return SWIM_ECAPACITY;
-      }
-    }
-    if (rest) {
-      bool ok = ncclGroupStart() == ncclSuccess;
-      for (uint32_t q = 0; q < W && ok; ++q) {
-        if (q == me) continue;
-        const uint64_t sb = hc[q] & XCNT_MASK, rb = hc[W + q] & XCNT_MASK;
-        if (sb > XINL - 8)
-          ok &= ncclSend(send + (size_t)q * cap + XINL - 8, sb - (XINL - 8), ncclUint8, (int)q, h->comm, st) == ncclSuccess;
-        if (rb > XINL - 8)
-          ok &= ncclRecv(recv + (size_t)q * cap + XINL - 8, rb - (XINL - 8), ncclUint8, (int)q, h->comm, st) == ncclSuccess;
-      }
-      ok &= ncclGroupEnd() == ncclSuccess;
-      if (!ok) {
-        h->err = "RCCL send/recv group failed";
-        return SWIM_EDEVICE;
-      }
-    }
+    if ((rc = exchange_rest(h, send, recv, cap)) != SWIM_OK) return rc;
   } else {
     HIPCK(hipMemcpyAsync(hc, scnt, 8ull * W, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
@@ -1169,6 +1187,43 @@ int swim_step(swim_handle* h, uint32_t n) {
         int xr;
         if ((xr = held_allreduce(h)) != SWIM_OK) return xr;
       }
+    } else if (h->spec.transport == SWIM_TRANSPORT_RCCL && !h->xflag && i + 1 < n && !d.churn && !h->no_spec &&
+               !(h->cfg.flags & SWIM_FLAG_PROFILE_ALL)) {
+      // Speculative sharded batch: while no shard has a gossip slot in use and every exchange-A region fits its inline
+      // block, a tick needs nothing from the host. The rest of the call is queued as A / inline all-to-all / B with
+      // no host wait; the gate after the all-to-all of the first tick that needs the host (the same tick on every
+      // shard: the flags ride on the exchanged count words) raises d.halt, every later launch returns at once (the
+      // all-to-alls still run, carrying nothing anyone reads), and the host finishes that tick on the normal path.
+      int xr;
+      for (uint32_t j = i; j < n; ++j) {
+        const uint32_t kj = k + (j - i);
+        const TickEvents* tj = timed(kj) ? &h->prof[j] : nullptr;
+        launch_tick_a(d, kj, h->stream, tj, true);
+        if ((xr = exchange_inline(h, d.xa_recv, d.XA_PEER, d.xa_scnt, d.xa_rcnt, true)) != SWIM_OK) return xr;
+        launch_spec_gate(d, kj, h->stream);
+        launch_tick_b(d, kj, h->stream, tj, false, true);
+      }
+      HIPCK(hipMemcpyAsync((void*)(h->hflag + 1), d.halt, 4, hipMemcpyDeviceToHost, h->stream));
+      HIPCK(hipStreamSynchronize(h->stream));
+      const uint32_t hk = h->hflag[1];
+      if (hk == 0) {
+        h->tick += n - i;
+        i = n;
+        continue;
+      }
+      const uint32_t kh = hk - 1u;  // tick kh ran up to its inline exchange; the launches after that returned at once
+      if (kh < k || kh >= k + (n - i)) return fail(h, SWIM_EDEVICE, "speculative sharded batch: bad halt tick");
+      HIPCK(hipMemsetAsync(d.halt, 0, 4, h->stream));
+      const uint32_t ih = i + (kh - k);
+      const TickEvents* th = timed(kh) ? &h->prof[ih] : nullptr;
+      if ((xr = exchange_rest(h, d.xa_send, d.xa_recv, d.XA_PEER)) != SWIM_OK) return xr;
+      const bool gossip = h->xflag;
+      launch_tick_b(d, kh, h->stream, th, gossip);
+      if (gossip && (xr = exchange(h, d.xb_send, d.xb_recv, d.XB_PEER, d.xb_scnt, d.xb_rcnt, false)) != SWIM_OK) return xr;
+      launch_tick_c(d, kh, h->stream, gossip);
+      h->tick = kh + 1ull;
+      i = ih + 1;
+      continue;
     } else {
       int xr;
       launch_tick_a(d, k, h->stream, te);

@@ -367,6 +367,11 @@ __device__ __forceinline__ void slot_create(const Dev& d, uint32_t g, uint32_t m
 }
 
 // end of a sharded tick (W > 1): the same resets, plus the exchange counters (one block)
+// a launch of a speculative batch that halted at an earlier tick (or at this one, for the kernels after the gate)
+__device__ __forceinline__ bool spec_halted(const Dev& d, uint32_t spec) {
+  return spec && *(volatile uint32_t*)d.halt != 0u;
+}
+
 __device__ __forceinline__ void tick_end(const Dev& d, uint32_t k) {
   uint32_t t = threadIdx.x;
   if (t < 8) d.xn[t] = 0;

@@ -62,7 +62,8 @@ constexpr uint32_t PAY_RX = 0x40000000u;  // received from another shard: PAY_RX
 constexpr uint32_t RRW = 12;              // words per gossip-round record: m, cnt, spread, period, targets[8]
 constexpr uint32_t NSW = 8;               // words per new-gossip-slot record
 // exchange byte-count words: low 48 bits = bytes; bit 62 = the sender has gossip slots in use this tick
-constexpr unsigned long long XCNT_MASK = (1ull << 48) - 1, XFLAG_GOSSIP = 1ull << 62;
+// bit 61 = the sender has a region larger than the inline block for some peer (a send/recv group follows)
+constexpr unsigned long long XCNT_MASK = (1ull << 48) - 1, XFLAG_GOSSIP = 1ull << 62, XFLAG_OVER = 1ull << 61;
 constexpr uint32_t XINL = 16384;  // RCCL: bytes per peer moved by the fixed-size all-to-all (count word + region head)
 
 // counters (swim_counters order after .tick)
@@ -375,12 +376,16 @@ void launch_gossip(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
 // sharded tick (W > 1): A = SYNC diff + member control + pack exchange A; B = unpack A, gossip sends, pack
 // exchange B; C = unpack B, apply receipts, routing, slot recycling. The host runs the exchanges in between and
 // skips the gossip half (and exchange B) when no shard has a gossip slot in use.
-void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr);
-void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool gossip);
+// spec: a launch of a speculative sharded batch (RCCL, gossip plane idle): every kernel returns at once once d.halt is
+// set; launch_spec_gate (after exchange A's inline all-to-all) raises it at the first tick whose exchange needs the
+// host (a gossip slot in use on some shard, or a region past the inline block)
+void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr, bool spec = false);
+void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool gossip, bool spec = false);
+void launch_spec_gate(const Dev& d, uint32_t k, void* stream);
 void launch_tick_c(const Dev& d, uint32_t k, void* stream, bool gossip);
 void launch_inline_out(const Dev& d, const uint8_t* send, uint64_t cap, const unsigned long long* scnt, void* stream);
 void launch_inline_in(const Dev& d, uint8_t* recv, uint64_t cap, const unsigned long long* scnt, unsigned long long* rcnt,
-                      void* stream);
+                      void* stream, bool spec = false);
 void launch_user_gossips(const Dev& d, uint32_t k, const uint64_t* q, uint32_t n, void* stream);
 void launch_churn(const Dev& d, uint32_t k, void* stream);
 void launch_md_column(const Dev& d, uint32_t m, uint32_t u, void* stream);

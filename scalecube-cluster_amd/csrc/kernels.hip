@@ -8,10 +8,10 @@ namespace swim {
 
 __global__ void k_member_tick(const Dev* __restrict__ dp, uint32_t k, uint32_t flag);  // member.hip
 // shard.hip
-__global__ void k_sync_route(Dev d, uint32_t b);
-__global__ void k_pack_a(Dev d, uint32_t b);
-__global__ void k_pack_a_chunks(Dev d, uint32_t b);
-__global__ void k_unpack_a(Dev d, uint32_t k, uint32_t end);
+__global__ void k_sync_route(Dev d, uint32_t b, uint32_t spec);
+__global__ void k_pack_a(Dev d, uint32_t b, uint32_t spec);
+__global__ void k_pack_a_chunks(Dev d, uint32_t b, uint32_t spec);
+__global__ void k_unpack_a(Dev d, uint32_t k, uint32_t end, uint32_t spec);
 __global__ void k_pack_b(Dev d);
 __global__ void k_round_reset(Dev d);
 
@@ -497,7 +497,7 @@ void launch_init(const Dev& d, void* stream) {
 // timed: this launch is bracketed by profiling events; it adds its message count to ctr[C_DIFFMSG]
 static void launch_sync_diff(const Dev& d, uint32_t b, hipStream_t st, uint32_t timed, uint32_t spec = 0) {
   if (d.W > 1)
-    hipLaunchKernelGGL(k_sync_diff<true>, dim3(2048), dim3(256), 0, st, d, b, timed, 0u);
+    hipLaunchKernelGGL(k_sync_diff<true>, dim3(2048), dim3(256), 0, st, d, b, timed, spec);
   else
     hipLaunchKernelGGL(k_sync_diff<false>, dim3(2048), dim3(256), 0, st, d, b, timed, spec);
 }
@@ -635,23 +635,24 @@ void launch_receipt_routing(const Dev& d, hipStream_t st) {
 // sharded tick (W > 1): A = SYNC diff + member control + pack exchange A; B = unpack A, the rounds' holder-state
 // changes and this shard's targets' sends, pack exchange B (their first receipts); C = peers' first receipts into the
 // replicated holder state, this shard's receipts, routing, slot recycling
-void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* prof) {
+void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool spec) {
   hipStream_t st = (hipStream_t)stream;
   uint32_t b = k & 1;
+  const uint32_t sp = spec ? 1u : 0u;
   if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
-  if (k > 0) launch_sync_diff(d, (k - 1) & 1, st, prof ? 1u : 0u);
+  if (k > 0) launch_sync_diff(d, (k - 1) & 1, st, prof ? 1u : 0u, sp);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[2], st);
-  hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k, 0u);
+  hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k, spec ? 2u : 0u);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[3], st);
-  hipLaunchKernelGGL(k_sync_route, dim3(cdiv(d.MSGCAP, 256)), dim3(256), 0, st, d, b);
-  hipLaunchKernelGGL(k_pack_a, dim3(d.W), dim3(256), 0, st, d, b);
-  hipLaunchKernelGGL(k_pack_a_chunks, dim3(64, d.W), dim3(256), 0, st, d, b);
+  hipLaunchKernelGGL(k_sync_route, dim3(cdiv(d.MSGCAP, 256)), dim3(256), 0, st, d, b, sp);
+  hipLaunchKernelGGL(k_pack_a, dim3(d.W), dim3(256), 0, st, d, b, sp);
+  hipLaunchKernelGGL(k_pack_a_chunks, dim3(64, d.W), dim3(256), 0, st, d, b, sp);
 }
 
-void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool gossip) {
+void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool gossip, bool spec) {
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_unpack_a, dim3(32, d.W), dim3(256), 0, st, d, k, gossip ? 0u : 1u);
+  hipLaunchKernelGGL(k_unpack_a, dim3(32, d.W), dim3(256), 0, st, d, k, gossip ? 0u : 1u, spec ? 1u : 0u);
   if (!gossip) {  // no gossip slot in use on any shard: nothing to send, deliver or recycle; no exchange B
     if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[4], st);
     if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[5], st);

@@ -30,7 +30,8 @@ __device__ __forceinline__ const uint32_t* payload_row(const Dev& d, const SyncM
 
 // this tick's sends: local destinations go straight to the next tick's inbound list, the rest are queued per shard
 // with their payload's dirty-chunk mask (maintained at every key write, member.hip row_put; no scan of the payload)
-__global__ void k_sync_route(Dev d, uint32_t b) {
+__global__ void k_sync_route(Dev d, uint32_t b, uint32_t spec) {
+  if (spec_halted(d, spec)) return;
   uint32_t n = d.nmsg[b] < d.MSGCAP ? d.nmsg[b] : d.MSGCAP;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const SyncMsg& mm = d.msgs[b][i];
@@ -60,9 +61,9 @@ __global__ void k_sync_route(Dev d, uint32_t b) {
 }
 
 // region layout, records and SYNC headers for peer q (one block per peer)
-__global__ void __launch_bounds__(256) k_pack_a(Dev d, uint32_t b) {
+__global__ void __launch_bounds__(256) k_pack_a(Dev d, uint32_t b, uint32_t spec) {
   const uint32_t q = blockIdx.x;
-  if (q == d.rank) return;
+  if (q == d.rank || spec_halted(d, spec)) return;
   __shared__ uint32_t sh[8];
   uint8_t* R = d.xa_send + (size_t)q * d.XA_PEER;
   const uint64_t SE = sync_entry_bytes(d);
@@ -117,7 +118,8 @@ __global__ void __launch_bounds__(256) k_pack_a(Dev d, uint32_t b) {
 // copy the differing payload chunks (key plane) into peer q's region (16-B loads and stores, 8 keys per lane). With
 // RCCL, the last block of peer q's column then writes q's inline all-to-all block (count word + region head), so
 // exchange A needs no separate copy kernel.
-__global__ void __launch_bounds__(256) k_pack_a_chunks(Dev d, uint32_t b) {
+__global__ void __launch_bounds__(256) k_pack_a_chunks(Dev d, uint32_t b, uint32_t spec) {
+  if (spec_halted(d, spec)) return;
   const uint32_t q = blockIdx.y;
   if (q == d.rank) {  // the block to itself carries an empty region
     if (d.inl && blockIdx.x == 0 && threadIdx.x == 0) *(uint64_t*)(d.xi_send + (size_t)q * XINL) = 0ull;
@@ -145,7 +147,11 @@ __global__ void __launch_bounds__(256) k_pack_a_chunks(Dev d, uint32_t b) {
     }
   }
   if (!d.inl || !last_block(&d.xdone[q], gridDim.x)) return;
-  const unsigned long long w = d.xa_scnt[q];
+  // every peer learns whether this shard needs a send/recv group past the inline blocks this tick (k_pack_a wrote
+  // all the counts in an earlier launch), so a speculative batch halts at the same tick on every shard
+  bool over = false;
+  for (uint32_t r = 0; r < d.W; ++r) over |= (d.xa_scnt[r] & XCNT_MASK) > XINL - 8;
+  const unsigned long long w = d.xa_scnt[q] | (over ? XFLAG_OVER : 0ull);
   uint64_t* idst = (uint64_t*)(d.xi_send + (size_t)q * XINL);
   if (threadIdx.x == 0) idst[0] = w;
   const uint64_t n = min((uint64_t)(w & XCNT_MASK), (uint64_t)XINL - 8) / 8;  // regions are multiples of 8 B
@@ -176,7 +182,8 @@ __device__ void msgs_commit(const Dev& d, uint32_t b) {
 // replay peer p's gossip creations and rounds into the replicated gossip plane; queue its SYNC messages. The block
 // that finishes last commits the inbound list, and, when no shard has a gossip slot in use (`end`), closes the tick
 // (k_tick_end): the steady-state tick after exchange A is this one launch.
-__global__ void __launch_bounds__(256) k_unpack_a(Dev d, uint32_t k, uint32_t end) {
+__global__ void __launch_bounds__(256) k_unpack_a(Dev d, uint32_t k, uint32_t end, uint32_t spec) {
+  if (spec_halted(d, spec)) return;
   const uint32_t p = blockIdx.y;
   if (p != d.rank && (d.xa_rcnt[p] & XCNT_MASK) >= 32) {
     const uint8_t* R = d.xa_recv + (size_t)p * d.XA_PEER;
@@ -285,7 +292,8 @@ __global__ void __launch_bounds__(256) k_inline_out(const uint8_t* send, uint64_
 
 __global__ void __launch_bounds__(256) k_inline_in(const uint8_t* irecv, uint8_t* recv, uint64_t cap,
                                                    const unsigned long long* scnt, unsigned long long* rcnt,
-                                                   unsigned long long* host, uint32_t W) {
+                                                   unsigned long long* host, uint32_t W, const uint32_t* halt) {
+  if (halt && *(volatile const uint32_t*)halt) return;  // speculative batch: halted at an earlier tick
   const uint32_t p = blockIdx.x;
   const uint64_t* src = (const uint64_t*)(irecv + (size_t)p * XINL);
   const unsigned long long w = src[0];
@@ -305,9 +313,25 @@ void launch_inline_out(const Dev& d, const uint8_t* send, uint64_t cap, const un
 }
 
 void launch_inline_in(const Dev& d, uint8_t* recv, uint64_t cap, const unsigned long long* scnt, unsigned long long* rcnt,
-                      void* stream) {
+                      void* stream, bool spec) {
   hipLaunchKernelGGL(k_inline_in, dim3(d.W), dim3(256), 0, (hipStream_t)stream, d.xi_recv, recv, cap, scnt, rcnt,
-                     d.xi_host, d.W);
+                     d.xi_host, d.W, spec ? (const uint32_t*)d.halt : nullptr);
+}
+
+// speculative sharded batch, after exchange A's inline all-to-all of tick k: halt (d.halt = k + 1) if any shard has a
+// gossip slot in use or a region past its inline block. Every shard reads the same flags (its own and every peer's
+// count words), so all of them halt at the same tick and run its rest on the host path
+__global__ void k_spec_gate(Dev d, uint32_t k) {
+  if (threadIdx.x != 0 || *(volatile uint32_t*)d.halt) return;
+  unsigned long long f = 0;
+  for (uint32_t p = 0; p < d.W; ++p) {
+    f |= d.xa_rcnt[p] | d.xa_scnt[p];
+    if ((d.xa_scnt[p] & XCNT_MASK) > XINL - 8) f |= XFLAG_OVER;
+  }
+  if (f & (XFLAG_GOSSIP | XFLAG_OVER)) *d.halt = k + 1u;
+}
+void launch_spec_gate(const Dev& d, uint32_t k, void* stream) {
+  hipLaunchKernelGGL(k_spec_gate, dim3(1), dim3(64), 0, (hipStream_t)stream, d, k);
 }
 
 }  // namespace swim
