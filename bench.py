@@ -269,7 +269,8 @@ def main():
             "data": "synthetic (PRECONVERGED full views, seeded Philox selector)",
             "config": {"workload": workload_name(a, n),
                        "members": n, "periods_per_step": 1, "ticks_per_period": ticks_per_period,
-                       "parallelism": f"row-sharded x{world} ({a.transport})" if world > 1 else "single-gpu"},
+                       "parallelism": (f"{'slot' if a.workload == 'c5' else 'row'}-sharded x{world} ({a.transport})"
+                                       if world > 1 else "single-gpu")},
             "roofline": {"bound": "hbm", "kernel": "k_sync_diff", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                          "algorithmic_bytes_per_launch": bytes_per_launch,
