@@ -1289,7 +1289,8 @@ int swim_step(swim_handle* h, uint32_t n) {
     unsigned long long c[5];
     HIPCK(hipMemcpy(c, d.ctr + 8, sizeof(c), hipMemcpyDeviceToHost));
     HIPCK(hipMemset(d.ctr + 8, 0, sizeof(c)));
-    fprintf(stderr, "exp: items %llu contact-bits %llu replays %llu candidates %llu\n", c[0], c[1], c[2], c[3]);
+    fprintf(stderr, "exp: items %llu contact-bits %llu replayed %llu candidates %llu blocked %llu\n", c[0], c[1], c[2], c[3],
+            c[4]);
   }
   if (rc == SWIM_OK && profile) {
     for (uint32_t i = 0; i < n; ++i) {
@@ -1667,11 +1668,12 @@ int swim_read_gossips(swim_handle* h, uint32_t obs, uint64_t* ids, uint32_t* inf
   if (!h || obs >= h->d.N || !n_out || !owns(h, obs)) return SWIM_EINVAL;
   HIPCK(hipStreamSynchronize(h->stream));
   const Dev& d = h->d;
-  std::vector<uint32_t> used(d.SLOTS), col(d.SLOTS);
+  std::vector<uint32_t> used(d.SLOTS), col(d.SLOTS), born(d.SLOTS);
   std::vector<uint64_t> gid(d.SLOTS);
   HIPCK(hipMemcpy(used.data(), d.slot_used, 4ull * d.SLOTS, hipMemcpyDeviceToHost));
   HIPCK(hipMemcpy(gid.data(), d.slot_gid, 8ull * d.SLOTS, hipMemcpyDeviceToHost));
-  HIPCK(hipMemcpy2D(col.data(), 4, d.S + obs, 4ull * d.N, 4, d.SLOTS, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(born.data(), d.slot_ctick, 4ull * d.SLOTS, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(col.data(), d.S + (size_t)obs * d.SLOTS, 4ull * d.SLOTS, hipMemcpyDeviceToHost));  // member-major
   uint32_t first = 0, dt = 0;
   HIPCK(hipMemcpy(&first, d.firstGossip + obs, 4, hipMemcpyDeviceToHost));
   HIPCK(hipMemcpy(&dt, d.dead_tick + obs, 4, hipMemcpyDeviceToHost));
@@ -1684,6 +1686,7 @@ int swim_read_gossips(swim_handle* h, uint32_t obs, uint64_t* ids, uint32_t* inf
     uint32_t e = col[g];
     if (!used[g] || (e & S_TICK_MASK) == 0 || (e & S_SWEPT)) continue;
     uint32_t c = (e & S_TICK_MASK) - 1;
+    if (c < born[g]) continue;   // an earlier gossip of the recycled slot (s_get)
     if (c >= h->tick) continue;  // receipt of the next tick's P4
     uint32_t rb = (first == NEVER || c <= first) ? 0 : (c - first + d.gossip_t - 1) / d.gossip_t;
     out.emplace_back(gid[g], rb);

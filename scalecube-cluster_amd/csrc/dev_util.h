@@ -333,6 +333,16 @@ __device__ __forceinline__ void on_sweep(const Dev& d, uint32_t g, uint32_t m, u
 __device__ __forceinline__ uint32_t s_ctick(uint32_t e) { return (e & S_TICK_MASK) - 1u; }
 __device__ __forceinline__ bool s_ever(uint32_t e) { return (e & S_TICK_MASK) != 0; }
 __device__ __forceinline__ bool s_held(uint32_t e) { return (e & S_TICK_MASK) != 0 && !(e & S_SWEPT); }
+// S is member-major ([N][SLOTS]): one member's entries for the 64 slots of a group share two cache lines, so the
+// receipts of one target (k_gossip_apply) and the sweeps of one member touch few lines
+__device__ __forceinline__ size_t s_idx(const Dev& d, uint32_t g, uint32_t m) { return (size_t)m * d.SLOTS + g; }
+// member m's entry for slot g. A recycled slot's entries are not cleared (k_gossip_free): an entry created before
+// the slot's current gossip existed (slot_ctick) belongs to an earlier gossip of the slot and reads as never held.
+// (Every holder of the earlier gossip received it before its slot expired, EXPB > 0 ticks before the recycle.)
+__device__ __forceinline__ uint32_t s_get(const Dev& d, uint32_t g, uint32_t m) {
+  const uint32_t e = d.S[s_idx(d, g, m)];
+  return (e & S_TICK_MASK) != 0 && s_ctick(e) < d.slot_ctick[g] ? 0u : e;
+}
 
 // ---- gossip holder state (gossip.hip) ----
 // ring entries: slot (22 bits) | infection period & 1023 << 22. At a round every entry's period lies in
@@ -360,7 +370,7 @@ __device__ __forceinline__ void slot_create(const Dev& d, uint32_t g, uint32_t m
   const unsigned long long bit = 1ull << (g & 63u);
   atomicOr(&d.GU[g >> 6], bit);
   if (subj != USER_SUBJ && rec_status(key) == ST_DEAD) atomicOr(&d.DM[g >> 6], bit);
-  d.S[(size_t)g * d.N + m] = (k + 1u) & S_TICK_MASK;
+  d.S[s_idx(d, g, m)] = (k + 1u) & S_TICK_MASK;
   atomicOr(&hrow(d, m)[g >> 6], bit);
   ring(d, m)[pos & (d.BCAP - 1)] = rg_entry(g, rounds_before(d, m, k));
   if (pos + 1u - d.rhead[m] > d.BCAP) set_err(d, E_RING);

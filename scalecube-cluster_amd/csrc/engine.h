@@ -4,7 +4,7 @@
 //   rowk, rowa u32[N][NS] x 2      membership table: key plane (inc << 2 | status) and aux plane (metadata bit,
 //                                  suspicion deadline), swim_common.h
 //   fdl, gl    u32[N][LCAP]       FailureDetectorImpl.pingMembers / GossipProtocolImpl.remoteMembers
-//   S          u32[SLOTS][N]      gossip slot x holder: creation tick | PENDING | SWEPT | REBORN
+//   S          u32[N][SLOTS]      holder x gossip slot: creation tick + 1 | SWEPT | REBORN (stale past a recycle: s_get)
 //   logs       per member ring of the last LOGW gossip rounds: (tick, spread, targets[F])
 //   subs/paths/fetches/groups      fixed-capacity per-member request state (virtual remote hops)
 //   msgs       SYNC / SYNC_ACK records, double-buffered by tick parity; payload = the sender's live row
@@ -220,7 +220,8 @@ struct Dev {
   uint64_t* slot_key;  // inc | status<<32 (status may be DEAD)
   uint32_t* slot_exp;  // tick from which no member holds the gossip any more: the slot is recycled (k_gossip_free)
   uint32_t* slot_used;
-  uint32_t* S;  // [SLOTS][N] creation tick + 1 | SWEPT | REBORN of each member's latest incarnation (replay, hashes)
+  uint32_t* S;  // [N][SLOTS] creation tick + 1 | SWEPT | REBORN of each member's latest incarnation (replay, hashes);
+                // entries older than the slot's gossip (slot_ctick) are stale (s_get)
   uint32_t* free_list;
   int32_t* free_top;
   uint64_t* xd;  // W > 1: (slot << 32) | target, this shard's first receipts of the tick (exchange B)

@@ -59,7 +59,7 @@ __device__ void hist_push(const Dev& d, uint64_t gid, uint32_t member, uint32_t 
 
 // creation tick of member's incarnation of g that existed at tick tau (NEVER if none)
 __device__ uint32_t inc_at(const Dev& d, uint32_t member, uint32_t g, uint64_t gid, uint32_t tau) {
-  uint32_t e = d.S[(size_t)g * d.N + member];
+  uint32_t e = s_get(d, g, member);
   if (!s_ever(e)) return NEVER;
   uint32_t c = s_ctick(e);
   if (c <= tau) return c;
@@ -396,7 +396,7 @@ __device__ void round_member(const Dev& d, uint32_t m, uint32_t k, unsigned long
   const uint32_t* R = ring(d, m);
   for (uint32_t p = h + tid; p - h < send - h; p += nth) {
     const uint32_t g = R[p & (d.BCAP - 1)] & RG_SLOT;
-    d.S[(size_t)g * d.N + m] |= S_SWEPT;
+    d.S[s_idx(d, g, m)] |= S_SWEPT;
     on_sweep(d, g, m, k);
   }
   const uint32_t nch = (send - h) + ((int32_t)(r2 - w0) > 0 ? r2 - w0 : 0u) + (r3 - wnew) + (tl - r4);
@@ -826,11 +826,16 @@ __global__ void __launch_bounds__(256) k_gossip_replay(const Dev* __restrict__ d
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint64_t v = d.rp[i];
     const uint32_t g = (uint32_t)(v >> 32), ms = (uint32_t)v, m = ms / d.F, s = ms % d.F;
-    const uint32_t t = d.T[ms], c = s_ctick(d.S[(size_t)g * d.N + m]), ci = d.cin[ms];
+    const uint32_t t = d.T[ms], c = s_ctick(d.S[s_idx(d, g, m)]), ci = d.cin[ms];  // m holds g: a current entry
     const uint64_t gid = d.slot_gid[g];
-    if (ci >= d.slot_ctick[g] && ci + d.lat + dmax(d) >= c &&
-        blocked_pair_cached(d, m, t, g, gid, k, c, d.cev + (size_t)ms * CEVW))
+    const bool maybe = ci >= d.slot_ctick[g] && ci + d.lat + dmax(d) >= c;
+    if (d.exp & 4) {  // timing experiment: replay items that reach the contact replay, and those it blocks
+      if (maybe) atomicAdd(&d.ctr[10], 1ull);
+    }
+    if (maybe && blocked_pair_cached(d, m, t, g, gid, k, c, d.cev + (size_t)ms * CEVW)) {
+      if (d.exp & 4) atomicAdd(&d.ctr[12], 1ull);
       continue;
+    }
     sends++;
     deliver_one(d, g, m, s, t, k, gid, ep);
   }
@@ -853,7 +858,7 @@ __global__ void __launch_bounds__(64) k_gossip_send_slow(const Dev* __restrict__
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint64_t v = d.slow[i];
     const uint32_t g = (uint32_t)(v >> 32), ms = (uint32_t)v, m = ms / d.F, s = ms % d.F;
-    const uint32_t t = d.T[ms], c = s_ctick(d.S[(size_t)g * d.N + m]);
+    const uint32_t t = d.T[ms], c = s_ctick(d.S[s_idx(d, g, m)]);
     const uint64_t gid = d.slot_gid[g];
     if (blocked_pair(d, m, t, g, gid, k, c)) continue;  // isInfected (:247)
     sends++;
@@ -911,8 +916,8 @@ __device__ __forceinline__ bool receipt_matters(const Dev& d, uint32_t t, uint32
 // the holder-table entry of a first receipt (onGossipReq :176-180): the incarnation created at tick k + lat; a
 // rebirth after a sweep keeps the swept incarnation's creation tick in the history (infectedFrom replay)
 __device__ __forceinline__ void receipt_create(const Dev& d, uint32_t g, uint32_t t, uint32_t k) {
-  uint32_t* p = d.S + (size_t)g * d.N + t;
-  const uint32_t e = *p;
+  uint32_t* p = d.S + s_idx(d, g, t);
+  const uint32_t e = s_get(d, g, t);
   if (s_ever(e)) hist_push(d, d.slot_gid[g], t, s_ctick(e));
   *p = ((k + d.lat + 1u) & S_TICK_MASK) | (s_ever(e) ? S_REBORN : 0u);
   if (d.dly_on)  // a delayed first receipt still queued may have pushed it further (delay_push)
@@ -987,7 +992,8 @@ __global__ void __launch_bounds__(256) k_gossip_apply(const Dev* __restrict__ dp
 }
 
 // 9. slots every holder has swept (slot_exp): nobody can send them again. Pass 1 lists them and clears their
-// group bits; pass 2 clears each one's holder-table row (a block per slot) and returns it to its owner shard's free list.
+// group bits; pass 2 returns each one to its owner shard's free list. Their holder-table entries stay: they predate
+// the slot's next gossip, so s_get reads them as never held.
 __global__ void k_gossip_expire(Dev d, uint32_t k) {
   const uint32_t nag = d.nagroup[0];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1001,14 +1007,10 @@ __global__ void k_gossip_expire(Dev d, uint32_t k) {
 }
 __global__ void __launch_bounds__(256) k_gossip_free(Dev d) {
   const uint32_t n = *d.nfexp;
-  for (uint32_t a = blockIdx.x; a < n; a += gridDim.x) {
+  for (uint32_t a = blockIdx.x * blockDim.x + threadIdx.x; a < n; a += gridDim.x * blockDim.x) {
     const uint32_t g = d.fexp[a];
-    uint32_t* Sg = d.S + (size_t)g * d.N;
-    for (uint32_t s = threadIdx.x; s < d.N; s += blockDim.x) Sg[s] = 0;
-    if (threadIdx.x == 0) {
-      d.slot_used[g] = 0;
-      if (g / d.SPR == d.rank) d.free_list[atomicAdd(d.free_top, 1)] = g;  // back to the owning shard's free list
-    }
+    d.slot_used[g] = 0;
+    if (g / d.SPR == d.rank) d.free_list[atomicAdd(d.free_top, 1)] = g;  // back to the owning shard's free list
   }
 }
 

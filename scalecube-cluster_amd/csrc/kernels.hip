@@ -440,7 +440,7 @@ __global__ void __launch_bounds__(256) k_hash(Dev d, uint64_t* out, uint32_t now
   const bool dead = d.dead_tick[m] != NEVER;  // a crashed member keeps no gossips (SEMANTICS.md §1)
   for (uint32_t g = threadIdx.x; g < d.SLOTS && !dead; g += blockDim.x) {
     if (!d.slot_used[g]) continue;
-    uint32_t e = d.S[(size_t)g * d.N + m];
+    uint32_t e = s_get(d, g, m);
     // receipts applied at the end of tick now-1 belong to P4 of tick `now`: not yet visible
     if (s_held(e) && s_ctick(e) < now) hgs += hpair(d.slot_gid[g], rounds_before(d, m, s_ctick(e)));
   }

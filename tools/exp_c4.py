@@ -23,7 +23,7 @@ p, t_all = 0, time.perf_counter()
 while p < end:
     if p == heal:
         c.unblock_all()
-    step = min(10, (heal if p < heal else end) - p)
+    step = min(int(os.environ.get("C4_CHUNK", "10")), (heal if p < heal else end) - p)
     t0 = time.perf_counter()
     c.run_periods(step)
     c.sync()
