@@ -465,11 +465,63 @@ __global__ void __launch_bounds__(256) k_round_apply_b(const Dev* __restrict__ d
 // 5. contact lists: did target t = T[m][s] choose m in a logged round inside the look-back window? If so, cache the
 // pair's contact events in both directions (independent of the gossip) for blocked_pair_cached. One wave per target
 // of this shard: its lanes read the target's round log once (coalesced) and test every sender of the target against it.
-__device__ void contact_cache(const Dev& d, uint32_t i, uint32_t m, uint32_t t, uint32_t k) {
-  Contact ev[CEV];
-  uint32_t oldest[2];
+// The pair's contact events (collect_contacts for x = m, y = t), gathered by one wave: lanes test 64 log entries of
+// one side at a time, a wave prefix sum places the hits, and lane 0 orders them by (tick, side, target slot) as the
+// serial insertion does. n = CEV + 1 on overflow.
+__device__ uint32_t collect_contacts_wave(const Dev& d, uint32_t m, uint32_t t, uint32_t k, uint32_t lane, Contact* ev,
+                                          uint32_t* oldest) {
+  uint32_t n = 0;
+  for (uint32_t side = 0; side < 2; ++side) {
+    const uint32_t from = side == 0 ? t : m, to = side == 0 ? m : t;
+    uint32_t old = NEVER;
+    for (uint32_t e0 = 0; e0 < d.LOGW; e0 += 64) {
+      const uint32_t e = e0 + lane;
+      uint32_t hits = 0, t2 = NEVER, sp = 0;
+      if (e < d.LOGW) {
+        const size_t li = (size_t)from * d.LOGW + e;
+        t2 = d.log_tick[li];
+        if (t2 != NEVER) {
+          old = min(old, t2);
+          if (t2 + d.lat <= k) {
+            const uint32_t cnt = d.log_cnt[li];
+            for (uint32_t s2 = 0; s2 < cnt; ++s2) hits |= (d.log_tg[li * d.F + s2] == to ? 1u : 0u) << s2;
+            if (hits) sp = d.log_spread[li];
+          }
+        }
+      }
+      const uint32_t c = __popc(hits);
+      uint32_t incl = c;
+#pragma unroll
+      for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+      }
+      const uint32_t tot = __shfl(incl, 63);
+      if (n <= CEV && n + tot <= CEV)
+        for (uint32_t j = n + incl - c; hits; hits &= hits - 1, ++j) ev[j] = Contact{t2, (uint32_t)(__ffs(hits) - 1), sp, side};
+      n = min(n + tot, CEV + 1u);
+    }
+#pragma unroll
+    for (uint32_t o = 32; o > 0; o >>= 1) old = min(old, (uint32_t)__shfl_xor(old, o));
+    oldest[side] = d.log_pos[from] > d.LOGW ? old : 0u;
+  }
+  grp_sync<false>();  // the lanes' LDS writes, before lane 0 orders them
+  if (lane == 0 && n <= CEV)
+    for (uint32_t a = 1; a < n; ++a)  // insertion by (tick, side, slot): the order collect_contacts produces
+      for (uint32_t b = a; b > 0; --b) {
+        const Contact &p = ev[b - 1], &q = ev[b];
+        if (p.tick < q.tick || (p.tick == q.tick && (p.dir < q.dir || (p.dir == q.dir && p.slot <= q.slot)))) break;
+        const Contact tmp = ev[b];
+        ev[b] = ev[b - 1];
+        ev[b - 1] = tmp;
+      }
+  return n;
+}
+
+// lane 0 of the wave that gathered ev (collect_contacts_wave): the pair's cache record and its replay row
+__device__ void contact_cache(const Dev& d, uint32_t i, uint32_t m, uint32_t t, uint32_t k, const Contact* ev,
+                              uint32_t n, const uint32_t* oldest) {
   uint32_t* rec = d.cev + (size_t)i * CEVW;
-  uint32_t n = collect_contacts<CEV>(d, m, t, k, 0, ev, oldest);
   if (n > d.cev_cap) n = CEV + 1;  // SWIM_CAPS: a smaller cache overflows into k_gossip_send_slow
   rec[0] = n;
   rec[1] = oldest[0];
@@ -554,13 +606,18 @@ __global__ void __launch_bounds__(256) k_gossip_contacts(Dev d, uint32_t k) {
   const uint32_t lane = threadIdx.x & 63u, ntl = *d.ntl;
   for (uint32_t ti = blockIdx.x * 4 + (threadIdx.x >> 6); ti < ntl; ti += gridDim.x * 4) {
     const uint32_t t = d.tlist[ti], o = d.tin_off[t], ns = d.tin_cnt[t];
+    const uint32_t pos = d.log_pos[t], nlog = min(pos, d.LOGW);
     for (uint32_t p = 0; p < ns; ++p) {
       const uint32_t i = d.tin[o + p], m = i / d.F;
+      // Only a contact t -> m that arrived after m's window horizon can put t in infectedFrom_m (contact_cache): t's
+      // rounds since then, newest first. t logs at most one round per gossip interval, so they are its last R entries.
+      const int64_t cut = (int64_t)k - (int64_t)(d.tspread[m] + 1u) * d.gossip_t - d.lat - dmax(d);
+      const uint32_t R = min(nlog, d.tspread[m] + 2u + (d.lat + dmax(d) + d.gossip_t - 1u) / d.gossip_t);
       bool hit = false;
-      for (uint32_t e = lane; e < d.LOGW && !hit; e += 64) {
-        const size_t lo = (size_t)t * d.LOGW + e;
+      for (uint32_t e = lane; e < R && !hit; e += 64) {
+        const size_t lo = (size_t)t * d.LOGW + (pos - 1u - e) % d.LOGW;
         const uint32_t t2 = d.log_tick[lo];
-        if (t2 == NEVER || t2 >= k) continue;
+        if (t2 == NEVER || t2 >= k || (int64_t)t2 <= cut) continue;
         const uint32_t n = d.log_cnt[lo];
         for (uint32_t s2 = 0; s2 < n; ++s2) hit |= d.log_tg[lo * d.F + s2] == m;
       }
@@ -573,12 +630,16 @@ __global__ void __launch_bounds__(256) k_gossip_contacts(Dev d, uint32_t k) {
   }
 }
 
-// the flagged pairs' contact caches, one thread each (two log scans per pair: in parallel, not behind a wave's lane 0)
-__global__ void k_contact_cache(Dev d, uint32_t k) {
-  const uint32_t n = *d.ncfl;
-  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
-    const uint32_t i = d.cfl[j];
-    contact_cache(d, i, i / d.F, d.T[i], k);
+// the flagged pairs' contact caches, one wave each: its lanes scan the two round logs 64 entries at a time
+__global__ void __launch_bounds__(256) k_contact_cache(Dev d, uint32_t k) {
+  __shared__ Contact sev[4][CEV];
+  const uint32_t n = *d.ncfl, lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  for (uint32_t j = blockIdx.x * 4 + wave; j < n; j += gridDim.x * 4) {
+    const uint32_t i = d.cfl[j], m = i / d.F, t = d.T[i];
+    uint32_t oldest[2];
+    const uint32_t ne = collect_contacts_wave(d, m, t, k, lane, sev[wave], oldest);
+    if (lane == 0) contact_cache(d, i, m, t, k, sev[wave], ne, oldest);
+    grp_sync<false>();  // lane 0 is done with sev before the next pair's lanes write it
   }
 }
 
@@ -1048,7 +1109,7 @@ void launch_gossip_send(const Dev& d, uint32_t k, hipStream_t st, const TickEven
   hipLaunchKernelGGL(k_round_apply_w, dim3(4096), dim3(256), 0, st, d.self, k);
   hipLaunchKernelGGL(k_round_apply_b, dim3(2048), dim3(256), 0, st, d.self, k);
   hipLaunchKernelGGL(k_gossip_contacts, dim3(2048), dim3(256), 0, st, d, k);
-  hipLaunchKernelGGL(k_contact_cache, dim3(256), dim3(64), 0, st, d, k);
+  hipLaunchKernelGGL(k_contact_cache, dim3(1024), dim3(256), 0, st, d, k);
   hipLaunchKernelGGL(k_rx_build, dim3(512), dim3(256), 0, st, d.self);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[4], st);
   hipLaunchKernelGGL(k_gossip_send, dim3(SEND_GRID), dim3(256), 0, st, d.self, k);

@@ -6,6 +6,6 @@ export TMPDIR=/tmp
 O=gpurun_out/${1:-r3c4}
 mkdir -p $O
 for n in ${2:-2000 4000 8000}; do
-  C4_CHUNK=${4:-10} timeout -k 10 ${3:-500} python -u tools/exp_c4.py $n 200 320 > $O/c4_$n.log 2>&1 || { tail -5 $O/c4_$n.log; exit 1; }
+  C4_RING=${5:-0} C4_CHUNK=${4:-10} timeout -k 10 ${3:-500} python -u tools/exp_c4.py $n 200 320 > $O/c4_$n.log 2>&1 || { tail -5 $O/c4_$n.log; exit 1; }
   tail -2 $O/c4_$n.log
 done
