@@ -58,6 +58,7 @@ def parse():
                    help="c5 only: run rank 0 of W slot shards on this GPU alone, the other shards' gossip-count "
                         "deltas taken as zero (a per-shard timing rehearsal of the W-GPU run, not its results)")
     p.add_argument("--slots", type=int, default=0, help="gossip slots per shard (0: the engine's default)")
+    p.add_argument("--ring", type=int, default=0, help="receipt-ring entries per member (0: the engine's default)")
     p.add_argument("--churn", type=int, default=0, help="c5: churn rumors per period (default: 1 %% of the members)")
     p.add_argument("--rehearse-one-gpu", action="store_true",
                    help="N>1 on a single GPU (functional rehearsal only): every rank uses device 0 and gets its own "
@@ -92,6 +93,8 @@ def mem_available():
 def workload_config(a, SimConfig, _abi, members, **kw):
     if a.slots:
         kw["gossip_slot_cap"] = a.slots
+    if a.ring:
+        kw["gossip_ring_cap"] = a.ring
     if a.workload == "c5":
         return SimConfig(n_members=members, mode=_abi.MODE_RUMOR, churn_per_period=a.churn or max(1, members // 100),
                          **kw)

@@ -1286,11 +1286,13 @@ int swim_step(swim_handle* h, uint32_t n) {
     }
   }
   if (rc == SWIM_OK && (d.exp & 4)) {  // timing experiments: gossip-send work counters since the last step
-    unsigned long long c[5];
+    unsigned long long c[5], u[2];
     HIPCK(hipMemcpy(c, d.ctr + 8, sizeof(c), hipMemcpyDeviceToHost));
     HIPCK(hipMemset(d.ctr + 8, 0, sizeof(c)));
-    fprintf(stderr, "exp: items %llu contact-bits %llu replayed %llu candidates %llu blocked %llu\n", c[0], c[1], c[2], c[3],
-            c[4]);
+    HIPCK(hipMemcpy(u, d.ctr + C_XU, sizeof(u), hipMemcpyDeviceToHost));
+    HIPCK(hipMemset(d.ctr + C_XU, 0, sizeof(u)));
+    fprintf(stderr, "exp: items %llu contact-bits %llu replayed %llu candidates %llu blocked %llu target-group items %llu "
+            "sender words %llu\n", c[0], c[1], c[2], c[3], c[4], u[0], u[1]);
   }
   if (rc == SWIM_OK && profile) {
     for (uint32_t i = 0; i < n; ++i) {

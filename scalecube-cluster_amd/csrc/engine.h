@@ -67,7 +67,8 @@ constexpr unsigned long long XCNT_MASK = (1ull << 48) - 1, XFLAG_GOSSIP = 1ull <
 constexpr uint32_t XINL = 16384;  // RCCL: bytes per peer moved by the fixed-size all-to-all (count word + region head)
 
 // counters (swim_counters order after .tick)
-enum Ctr { C_R = 0, C_W, C_M, C_G, C_E, C_LOST, C_GCREATED, C_SYNCMERGE, C_DIFFMSG = 13, C_NCTR = 16 };  // 8..12: SWIM_EXP & 4
+// 8..12: SWIM_EXP & 4 (and 16..19: the gossip plane's work units per tick, for algorithmic bytes; tools/pmc_gossip.py)
+enum Ctr { C_R = 0, C_W, C_M, C_G, C_E, C_LOST, C_GCREATED, C_SYNCMERGE, C_DIFFMSG = 13, C_XU = 16, C_NCTR = 24 };
 
 // capacity fallbacks that fired (include/swimhip_debug.h; counted only when Dev::fb is allocated: SWIM_CAPS or
 // SWIM_FALLBACKS set at create). Each one is an exact slow path taken when a fixed-capacity fast structure is full.

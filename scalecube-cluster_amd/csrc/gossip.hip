@@ -664,6 +664,12 @@ __global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp,
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint64_t items = (uint64_t)ntl * nag;
   const int ep = epoch_at(d, k);
+  if ((d.exp & 4) && blockIdx.x == 0 && threadIdx.x == 0) {  // work units: (target, group) items, their sender words
+    uint64_t pairs = 0;
+    for (uint32_t i = 0; i < ntl; ++i) pairs += d.tin_cnt[d.tlist[i]];
+    atomicAdd(&d.ctr[C_XU], (unsigned long long)items);
+    atomicAdd(&d.ctr[C_XU + 1], (unsigned long long)pairs * nag);
+  }
   unsigned long long sends = 0;
   uint32_t st[4] = {0, 0, 0, 0};  // SWIM_EXP & 4: items with window bits, contact-path bits, -, candidates
   for (uint64_t i0 = ((uint64_t)blockIdx.x * 4 + wave) * 64; i0 < items; i0 += (uint64_t)gridDim.x * 256) {

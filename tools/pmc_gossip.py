@@ -53,6 +53,34 @@ def main():
         allb = sum(v["hbm_bytes_per_tick"] for v in out["kernels"].values())
         out["hbm_bytes_per_tick_all_kernels"] = allb
         out["wasted_traffic_ratio"] = allb / (B / ticks) if B else None
+    # k_gossip_send's algorithmic bytes from the same ticks' work units (SWIM_EXP=4 run of the same command, the
+    # workload is deterministic): an 8-B held word per (target, active group) item, an 8-B window word per sender of
+    # the item, a 4-B ring entry per first-receipt candidate. Atomic throughput from the kernel-trace averages.
+    try:
+        ex = [x for x in open(f"{d}/exp4_{w}.log") if x.startswith("exp: items")][-(last // 10 or 1):]
+        tok = lambda x, key: int(x.split(key)[1].split()[0])
+        n = len(ex) * 10  # one line per step (one period = 10 ticks)
+        items, words = sum(tok(x, "target-group items ") for x in ex) / n, sum(tok(x, "sender words ") for x in ex) / n
+        cand = sum(tok(x, "candidates ") for x in ex) / n
+        alg = 8 * items + 8 * words + 4 * cand
+        ks = out["kernels"].get("k_gossip_send")
+        if ks:
+            ks["algorithmic_bytes_per_tick"] = alg
+            ks["traffic_ratio"] = ks["hbm_bytes_per_tick"] / alg if alg else None
+            ks["work_units_per_tick"] = {"target_group_items": items, "sender_words": words, "candidates": cand}
+    except FileNotFoundError:
+        pass
+    try:
+        for r in csv.DictReader(open(f"{d}/trace_{w}/run_kernel_stats.csv")):
+            k = r["Name"].split("(")[0].replace("swim::", "").replace("void ", "").split("<")[0]
+            if k in out["kernels"]:
+                us = float(r["AverageNs"]) / 1e3
+                e = out["kernels"][k]
+                e["avg_us"] = us
+                e["achieved_GBps"] = e["hbm_bytes_per_tick"] / max(1, e["dispatches"] / ticks) / us / 1e3
+                e["l2_atomics_per_us"] = e["l2_atomics_per_tick"] / max(1, e["dispatches"] / ticks) / us
+    except FileNotFoundError:
+        pass
     print(json.dumps(out, indent=1))
     if len(sys.argv) > 4:
         json.dump(out, open(sys.argv[4], "w"), indent=1)
