@@ -17,6 +17,8 @@
  *   sort   first receipts of one member and tick sorted in LDS at once (more: sorted runs merged), P4 order
  *   rx     contact pairs per tick whose replay is limited to the gossips received before the contact (more: the
  *          whole window is replayed), GossipProtocolImpl isInfected (:247)
+ *   xinl   bytes per peer of the RCCL inline all-to-all of a sharded tick (more: a send/recv group; speculative
+ *          sharded batches halt on the overflow flag), every rank the same value
  * With SWIM_CAPS (or SWIM_FALLBACKS=1) set, the handle counts how often each fallback fired.
  */
 #ifndef SWIMHIP_DEBUG_H

@@ -287,6 +287,7 @@ int build(swim_handle* h) {
   // fast-structure capacities (include/swimhip_debug.h): SWIM_CAPS="trk=1,ulog=2,creq=1,cwmax=1,cev=1,mq=1,sort=2"
   // lowers them so that the exact fallbacks run; results stay bit-exact, only slower
   d.trk_cap = TRK, d.ulog_cap = ULOG, d.creq_cap = CREQ, d.cwmax_cap = CWMAX, d.cev_cap = CEV, d.mq_cap = MQ;
+  d.XI = XINL;
   d.sort_cap = SORT_MAX;
   uint32_t rx_cap = NEVER;
   const char* caps = getenv("SWIM_CAPS");
@@ -310,6 +311,7 @@ int build(swim_handle* h) {
       else if (k == "cev") d.cev_cap = clampv(0, CEV);
       else if (k == "mq") d.mq_cap = clampv(1, MQ);
       else if (k == "rx") rx_cap = v;
+      else if (k == "xinl") d.XI = std::max<uint32_t>(64, std::min<uint32_t>(XINL, v)) & ~7u;  // send/recv group past it
       else if (k == "sort") {
         uint32_t r = 2;
         while (r * 2 <= clampv(2, SORT_MAX)) r *= 2;  // a power of two (bitonic runs)
@@ -617,7 +619,7 @@ hipError_t spin_wait(hipEvent_t ev) {
 // publishes the count words to the host-mapped xi_host)
 int exchange_inline(swim_handle* h, uint8_t* recv, uint64_t cap, unsigned long long* scnt, unsigned long long* rcnt,
                     bool spec) {
-  if (ncclAllToAll(h->d.xi_send, h->d.xi_recv, XINL, ncclUint8, h->comm, h->stream) != ncclSuccess) {
+  if (ncclAllToAll(h->d.xi_send, h->d.xi_recv, h->d.XI, ncclUint8, h->comm, h->stream) != ncclSuccess) {
     h->err = "ncclAllToAll (inline exchange) failed";
     return SWIM_EDEVICE;
   }
@@ -636,7 +638,7 @@ int exchange_rest(swim_handle* h, uint8_t* send, uint8_t* recv, uint64_t cap) {
   bool rest = false;
   for (uint32_t q = 0; q < 2 * W; ++q) {
     h->xflag |= (hc[q] & XFLAG_GOSSIP) != 0;
-    rest |= (hc[q] & XCNT_MASK) > XINL - 8;
+    rest |= (hc[q] & XCNT_MASK) > h->d.XI - 8;
     if ((hc[q] & XCNT_MASK) > cap) {
       h->err = "exchange block larger than its region";
       return SWIM_ECAPACITY;
@@ -647,10 +649,9 @@ int exchange_rest(swim_handle* h, uint8_t* send, uint8_t* recv, uint64_t cap) {
     for (uint32_t q = 0; q < W && ok; ++q) {
       if (q == me) continue;
       const uint64_t sb = hc[q] & XCNT_MASK, rb = hc[W + q] & XCNT_MASK;
-      if (sb > XINL - 8)
-        ok &= ncclSend(send + (size_t)q * cap + XINL - 8, sb - (XINL - 8), ncclUint8, (int)q, h->comm, h->stream) == ncclSuccess;
-      if (rb > XINL - 8)
-        ok &= ncclRecv(recv + (size_t)q * cap + XINL - 8, rb - (XINL - 8), ncclUint8, (int)q, h->comm, h->stream) == ncclSuccess;
+      const uint64_t X = h->d.XI - 8;
+      if (sb > X) ok &= ncclSend(send + (size_t)q * cap + X, sb - X, ncclUint8, (int)q, h->comm, h->stream) == ncclSuccess;
+      if (rb > X) ok &= ncclRecv(recv + (size_t)q * cap + X, rb - X, ncclUint8, (int)q, h->comm, h->stream) == ncclSuccess;
     }
     ok &= ncclGroupEnd() == ncclSuccess;
     if (!ok) {

@@ -305,6 +305,7 @@ struct Dev {
   uint8_t *xa_send, *xa_recv, *xb_send, *xb_recv;  // [W][X*_PEER]
   unsigned long long *xa_scnt, *xa_rcnt, *xb_scnt, *xb_rcnt;  // [W] bytes per peer region
   uint8_t *xi_send, *xi_recv;    // [W][XINL] inline all-to-all blocks
+  uint32_t XI;                   // bytes per peer the inline all-to-all moves (XINL; SWIM_CAPS xinl= lowers it)
   unsigned long long* xi_host;   // host-mapped [2W]: send and receive count words of the last exchange
   uint32_t* xdone;  // [W] finished k_pack_a_chunks blocks per peer column (the last one writes the inline block)
   uint32_t inl;     // RCCL transport: exchange A's inline blocks are written by k_pack_a_chunks

@@ -122,7 +122,7 @@ __global__ void __launch_bounds__(256) k_pack_a_chunks(Dev d, uint32_t b, uint32
   if (spec_halted(d, spec)) return;
   const uint32_t q = blockIdx.y;
   if (q == d.rank) {  // the block to itself carries an empty region
-    if (d.inl && blockIdx.x == 0 && threadIdx.x == 0) *(uint64_t*)(d.xi_send + (size_t)q * XINL) = 0ull;
+    if (d.inl && blockIdx.x == 0 && threadIdx.x == 0) *(uint64_t*)(d.xi_send + (size_t)q * d.XI) = 0ull;
     return;
   }
   uint8_t* R = d.xa_send + (size_t)q * d.XA_PEER;
@@ -150,11 +150,11 @@ __global__ void __launch_bounds__(256) k_pack_a_chunks(Dev d, uint32_t b, uint32
   // every peer learns whether this shard needs a send/recv group past the inline blocks this tick (k_pack_a wrote
   // all the counts in an earlier launch), so a speculative batch halts at the same tick on every shard
   bool over = false;
-  for (uint32_t r = 0; r < d.W; ++r) over |= (d.xa_scnt[r] & XCNT_MASK) > XINL - 8;
+  for (uint32_t r = 0; r < d.W; ++r) over |= (d.xa_scnt[r] & XCNT_MASK) > d.XI - 8;
   const unsigned long long w = d.xa_scnt[q] | (over ? XFLAG_OVER : 0ull);
-  uint64_t* idst = (uint64_t*)(d.xi_send + (size_t)q * XINL);
+  uint64_t* idst = (uint64_t*)(d.xi_send + (size_t)q * d.XI);
   if (threadIdx.x == 0) idst[0] = w;
-  const uint64_t n = min((uint64_t)(w & XCNT_MASK), (uint64_t)XINL - 8) / 8;  // regions are multiples of 8 B
+  const uint64_t n = min((uint64_t)(w & XCNT_MASK), (uint64_t)d.XI - 8) / 8;  // regions are multiples of 8 B
   const uint64_t* isrc = (const uint64_t*)R;
   for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) idst[1 + i] = isrc[i];
 }
@@ -280,24 +280,25 @@ __global__ void k_round_reset(Dev d) {
 // RCCL exchange, fixed-size part: block q = the count word of region q followed by its first XINL - 8 bytes. The
 // all-to-all of these blocks needs no sizes on the host, and in the steady state carries the whole exchange.
 __global__ void __launch_bounds__(256) k_inline_out(const uint8_t* send, uint64_t cap, const unsigned long long* scnt,
-                                                    uint8_t* isend) {
+                                                    uint8_t* isend, uint32_t XI) {
   const uint32_t q = blockIdx.x;
   const unsigned long long w = scnt[q];
-  uint64_t* dst = (uint64_t*)(isend + (size_t)q * XINL);
+  uint64_t* dst = (uint64_t*)(isend + (size_t)q * XI);
   if (threadIdx.x == 0) dst[0] = w;
-  const uint64_t n = min((uint64_t)(w & XCNT_MASK), (uint64_t)XINL - 8) / 8;  // regions are multiples of 8 B
+  const uint64_t n = min((uint64_t)(w & XCNT_MASK), (uint64_t)XI - 8) / 8;  // regions are multiples of 8 B
   const uint64_t* src = (const uint64_t*)(send + (size_t)q * cap);
   for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) dst[1 + i] = src[i];
 }
 
 __global__ void __launch_bounds__(256) k_inline_in(const uint8_t* irecv, uint8_t* recv, uint64_t cap,
                                                    const unsigned long long* scnt, unsigned long long* rcnt,
-                                                   unsigned long long* host, uint32_t W, const uint32_t* halt) {
+                                                   unsigned long long* host, uint32_t W, const uint32_t* halt,
+                                                   uint32_t XI) {
   if (halt && *(volatile const uint32_t*)halt) return;  // speculative batch: halted at an earlier tick
   const uint32_t p = blockIdx.x;
-  const uint64_t* src = (const uint64_t*)(irecv + (size_t)p * XINL);
+  const uint64_t* src = (const uint64_t*)(irecv + (size_t)p * XI);
   const unsigned long long w = src[0];
-  const uint64_t n = min((uint64_t)(w & XCNT_MASK), (uint64_t)XINL - 8) / 8;
+  const uint64_t n = min((uint64_t)(w & XCNT_MASK), (uint64_t)XI - 8) / 8;
   uint64_t* dst = (uint64_t*)(recv + (size_t)p * cap);
   for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[1 + i];
   if (threadIdx.x == 0) {
@@ -309,13 +310,13 @@ __global__ void __launch_bounds__(256) k_inline_in(const uint8_t* irecv, uint8_t
 }
 
 void launch_inline_out(const Dev& d, const uint8_t* send, uint64_t cap, const unsigned long long* scnt, void* stream) {
-  hipLaunchKernelGGL(k_inline_out, dim3(d.W), dim3(256), 0, (hipStream_t)stream, send, cap, scnt, d.xi_send);
+  hipLaunchKernelGGL(k_inline_out, dim3(d.W), dim3(256), 0, (hipStream_t)stream, send, cap, scnt, d.xi_send, d.XI);
 }
 
 void launch_inline_in(const Dev& d, uint8_t* recv, uint64_t cap, const unsigned long long* scnt, unsigned long long* rcnt,
                       void* stream, bool spec) {
   hipLaunchKernelGGL(k_inline_in, dim3(d.W), dim3(256), 0, (hipStream_t)stream, d.xi_recv, recv, cap, scnt, rcnt,
-                     d.xi_host, d.W, spec ? (const uint32_t*)d.halt : nullptr);
+                     d.xi_host, d.W, spec ? (const uint32_t*)d.halt : nullptr, d.XI);
 }
 
 // speculative sharded batch, after exchange A's inline all-to-all of tick k: halt (d.halt = k + 1) if any shard has a
@@ -326,7 +327,7 @@ __global__ void k_spec_gate(Dev d, uint32_t k) {
   unsigned long long f = 0;
   for (uint32_t p = 0; p < d.W; ++p) {
     f |= d.xa_rcnt[p] | d.xa_scnt[p];
-    if ((d.xa_scnt[p] & XCNT_MASK) > XINL - 8) f |= XFLAG_OVER;
+    if ((d.xa_scnt[p] & XCNT_MASK) > d.XI - 8) f |= XFLAG_OVER;
   }
   if (f & (XFLAG_GOSSIP | XFLAG_OVER)) *d.halt = k + 1u;
 }

@@ -15,20 +15,25 @@ pytestmark = pytest.mark.gpu
 ROOT = Path(__file__).resolve().parent.parent
 
 
-@pytest.mark.parametrize("transport,mode", [("host", "full"), ("rccl", "full"), ("rccl", "rumor")])
+# "full-xinl": the inline all-to-all block cut to 256 B (SWIM_CAPS xinl=), so most exchange-A regions overflow it: the
+# speculative sharded batches halt on the overflow flag (XFLAG_OVER) and the host's send/recv group carries the rest
+@pytest.mark.parametrize("transport,mode", [("host", "full"), ("rccl", "full"), ("rccl", "rumor"), ("rccl", "full-xinl")])
 def test_two_process_shards(transport, mode, tmp_path):
     import torch  # noqa: F401  (pages torch in once, before two workers import it at the same time)
     procs, logs = [], []
     for r in range(2):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT={"rccl": "29533", "host": "29534"}[transport] if mode == "full" else "29535", NCCL_HOSTID=f"swimhost{r}",
+                   MASTER_PORT={"full": {"rccl": "29533", "host": "29534"}[transport], "rumor": "29535",
+                                            "full-xinl": "29536"}[mode], NCCL_HOSTID=f"swimhost{r}",
                    NCCL_SOCKET_IFNAME="lo", GLOO_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1",
                    HSA_ENABLE_IPC_MODE_LEGACY="0")
+        if mode == "full-xinl":
+            env["SWIM_CAPS"] = "xinl=256"
         logdir = Path(os.environ.get("SWIM_TEST_LOGDIR", str(tmp_path)))
         logdir.mkdir(parents=True, exist_ok=True)
         log = open(logdir / f"{transport}_{mode}_rank{r}.log", "w")
         logs.append(log)
-        procs.append(subprocess.Popen([sys.executable, "-u", str(ROOT / "tests" / "shard_rccl_worker.py"), transport, mode],
+        procs.append(subprocess.Popen([sys.executable, "-u", str(ROOT / "tests" / "shard_rccl_worker.py"), transport, mode.split("-")[0]],
                                       env=env, stdout=log, stderr=subprocess.STDOUT))
     t0 = time.time()
     timed_out = False
