@@ -66,6 +66,7 @@ struct swim_handle {
   volatile uint32_t* hflag = nullptr; // host-mapped flag word written by k_tick_flag (W == 1)
   unsigned long long* xi_host_h = nullptr;  // host side of Dev::xi_host
   hipEvent_t ev_member = nullptr;
+  uint64_t next_scrub = SCRUB;  // tick of the next k_s_scrub (16-bit holder entries, engine.h)
   bool no_skip = getenv("SWIM_NO_GOSSIP_SKIP") != nullptr;  // debugging aid: always run the gossip data plane
   bool no_pipe = getenv("SWIM_NO_PIPELINE") != nullptr;    // debugging aid: no early SYNC diff of the next tick
   bool no_spec = getenv("SWIM_NO_SPECULATION") != nullptr;  // debugging aid: a host wait after every member kernel
@@ -537,7 +538,7 @@ int build(swim_handle* h) {
     }
   }
 #undef A
-  HIPCK(hipMemsetAsync(d.S, 0, (size_t)d.SLOTS * N * 4, h->stream));
+  HIPCK(hipMemsetAsync(d.S, 0, (size_t)d.SLOTS * N * 2, h->stream));
   HIPCK(hipMemsetAsync(d.HB, 0, (size_t)d.QW * N * 8, h->stream));
   HIPCK(hipMemsetAsync(d.WB, 0, (size_t)d.QW * N * 8, h->stream));
   HIPCK(hipMemsetAsync(d.GU, 0, (size_t)d.QW * 8, h->stream));
@@ -1120,6 +1121,12 @@ int swim_step(swim_handle* h, uint32_t n) {
   for (uint32_t i = 0; i < n;) {
     const TickEvents* te = timed(h->tick) ? &h->prof[i] : nullptr;
     const uint32_t k = (uint32_t)h->tick;
+    if (h->tick >= h->next_scrub) {  // stale holder entries of recycled slots, before they can alias (engine.h)
+      launch_s_scrub(d, k, h->stream);
+      h->next_scrub = h->tick + SCRUB;
+    }
+    // a speculative batch ends at the next scrub tick
+    const uint32_t nb = (uint32_t)std::min<uint64_t>(n, i + (h->next_scrub - h->tick));
     // P0 gossip creations before the member kernel: RUMOR-mode churn rumors, then the user gossips queued by the host
     if (d.churn && k % d.ping_t == 0) launch_churn(d, k, h->stream);
     if (i == 0 && !h->ugq.empty()) {
@@ -1134,29 +1141,29 @@ int swim_step(swim_handle* h, uint32_t n) {
       HIPCK(hipStreamSynchronize(h->stream));  // the host queue is reused after this
       h->ugq.clear();
     }
-    if (d.W == 1 && h->gossip_idle && i + 1 < n && d.XW == 1 && !d.churn && !h->no_pipe && !h->no_skip &&
+    if (d.W == 1 && h->gossip_idle && i + 1 < nb && d.XW == 1 && !d.churn && !h->no_pipe && !h->no_skip &&
         !h->no_spec && !(h->cfg.flags & SWIM_FLAG_PROFILE_ALL)) {  // (PROFILE_ALL times every tick's gossip plane)
       // Speculative batch: while no gossip slot is in use the host need not look at the flag after every member
       // kernel. The rest of the call is queued as diff / member pairs with no host wait; the member kernel after which
       // a slot is in use raises d.halt, every later launch of the batch returns at once, and the host resumes after
       // that tick with the gossip plane.
-      for (uint32_t j = i; j < n; ++j) {
+      for (uint32_t j = i; j < nb; ++j) {
         const uint32_t kj = k + (j - i);
         if (need_diff) launch_diff(d, kj, h->stream, timed(kj) ? &h->prof[j] : nullptr, true);
         launch_member(d, kj, h->stream, timed(kj) ? &h->prof[j] : nullptr, true);
-        need_diff = j + 1 == n;
+        need_diff = j + 1 == nb;
         if (!need_diff) launch_diff(d, kj + 1, h->stream, timed(kj + 1ull) ? &h->prof[j + 1] : nullptr, true);
       }
       HIPCK(hipMemcpyAsync((void*)(h->hflag + 1), d.halt, 4, hipMemcpyDeviceToHost, h->stream));
       HIPCK(hipStreamSynchronize(h->stream));
       const uint32_t hk = h->hflag[1];
       if (hk == 0) {  // the whole batch ran
-        h->tick += n - i;
-        i = n;
+        h->tick += nb - i;
+        i = nb;
         continue;
       }
       const uint32_t kh = hk - 1u;  // member(kh) ran; the launches after it returned at once
-      if (kh < k || kh >= k + (n - i)) return fail(h, SWIM_EDEVICE, "speculative batch: bad halt tick");
+      if (kh < k || kh >= k + (nb - i)) return fail(h, SWIM_EDEVICE, "speculative batch: bad halt tick");
       HIPCK(hipMemsetAsync(d.halt, 0, 4, h->stream));
       const uint32_t ih = i + (kh - k);
       launch_gossip(d, kh, h->stream, timed(kh) ? &h->prof[ih] : nullptr);
@@ -1188,7 +1195,7 @@ int swim_step(swim_handle* h, uint32_t n) {
         int xr;
         if ((xr = held_allreduce(h)) != SWIM_OK) return xr;
       }
-    } else if (h->spec.transport == SWIM_TRANSPORT_RCCL && !h->xflag && i + 1 < n && !d.churn && !h->no_spec &&
+    } else if (h->spec.transport == SWIM_TRANSPORT_RCCL && !h->xflag && i + 1 < nb && !d.churn && !h->no_spec &&
                !(h->cfg.flags & SWIM_FLAG_PROFILE_ALL)) {
       // Speculative sharded batch: while no shard has a gossip slot in use and every exchange-A region fits its inline
       // block, a tick needs nothing from the host. The rest of the call is queued as A / inline all-to-all / B with
@@ -1196,7 +1203,7 @@ int swim_step(swim_handle* h, uint32_t n) {
       // shard: the flags ride on the exchanged count words) raises d.halt, every later launch returns at once (the
       // all-to-alls still run, carrying nothing anyone reads), and the host finishes that tick on the normal path.
       int xr;
-      for (uint32_t j = i; j < n; ++j) {
+      for (uint32_t j = i; j < nb; ++j) {
         const uint32_t kj = k + (j - i);
         const TickEvents* tj = timed(kj) ? &h->prof[j] : nullptr;
         launch_tick_a(d, kj, h->stream, tj, true);
@@ -1208,12 +1215,12 @@ int swim_step(swim_handle* h, uint32_t n) {
       HIPCK(hipStreamSynchronize(h->stream));
       const uint32_t hk = h->hflag[1];
       if (hk == 0) {
-        h->tick += n - i;
-        i = n;
+        h->tick += nb - i;
+        i = nb;
         continue;
       }
       const uint32_t kh = hk - 1u;  // tick kh ran up to its inline exchange; the launches after that returned at once
-      if (kh < k || kh >= k + (n - i)) return fail(h, SWIM_EDEVICE, "speculative sharded batch: bad halt tick");
+      if (kh < k || kh >= k + (nb - i)) return fail(h, SWIM_EDEVICE, "speculative sharded batch: bad halt tick");
       HIPCK(hipMemsetAsync(d.halt, 0, 4, h->stream));
       const uint32_t ih = i + (kh - k);
       const TickEvents* th = timed(kh) ? &h->prof[ih] : nullptr;
@@ -1671,12 +1678,13 @@ int swim_read_gossips(swim_handle* h, uint32_t obs, uint64_t* ids, uint32_t* inf
   if (!h || obs >= h->d.N || !n_out || !owns(h, obs)) return SWIM_EINVAL;
   HIPCK(hipStreamSynchronize(h->stream));
   const Dev& d = h->d;
-  std::vector<uint32_t> used(d.SLOTS), col(d.SLOTS), born(d.SLOTS);
+  std::vector<uint32_t> used(d.SLOTS), born(d.SLOTS);
+  std::vector<uint16_t> col(d.SLOTS);
   std::vector<uint64_t> gid(d.SLOTS);
   HIPCK(hipMemcpy(used.data(), d.slot_used, 4ull * d.SLOTS, hipMemcpyDeviceToHost));
   HIPCK(hipMemcpy(gid.data(), d.slot_gid, 8ull * d.SLOTS, hipMemcpyDeviceToHost));
   HIPCK(hipMemcpy(born.data(), d.slot_ctick, 4ull * d.SLOTS, hipMemcpyDeviceToHost));
-  HIPCK(hipMemcpy(col.data(), d.S + (size_t)obs * d.SLOTS, 4ull * d.SLOTS, hipMemcpyDeviceToHost));  // member-major
+  HIPCK(hipMemcpy(col.data(), d.S + (size_t)obs * d.SLOTS, 2ull * d.SLOTS, hipMemcpyDeviceToHost));  // member-major
   uint32_t first = 0, dt = 0;
   HIPCK(hipMemcpy(&first, d.firstGossip + obs, 4, hipMemcpyDeviceToHost));
   HIPCK(hipMemcpy(&dt, d.dead_tick + obs, 4, hipMemcpyDeviceToHost));
@@ -1686,9 +1694,9 @@ int swim_read_gossips(swim_handle* h, uint32_t obs, uint64_t* ids, uint32_t* inf
   }
   std::vector<std::pair<uint64_t, uint32_t>> out;
   for (uint32_t g = 0; g < d.SLOTS; ++g) {
-    uint32_t e = col[g];
-    if (!used[g] || (e & S_TICK_MASK) == 0 || (e & S_SWEPT)) continue;
-    uint32_t c = (e & S_TICK_MASK) - 1;
+    const uint16_t e = col[g];
+    if (!used[g] || !(e & S16_EVER) || (e & S16_SWEPT)) continue;
+    const uint32_t c = s16_tick(e, (uint32_t)h->tick + d.lat);
     if (c < born[g]) continue;   // an earlier gossip of the recycled slot (s_get)
     if (c >= h->tick) continue;  // receipt of the next tick's P4
     uint32_t rb = (first == NEVER || c <= first) ? 0 : (c - first + d.gossip_t - 1) / d.gossip_t;

@@ -336,12 +336,19 @@ __device__ __forceinline__ bool s_held(uint32_t e) { return (e & S_TICK_MASK) !=
 // S is member-major ([N][SLOTS]): one member's entries for the 64 slots of a group share two cache lines, so the
 // receipts of one target (k_gossip_apply) and the sweeps of one member touch few lines
 __device__ __forceinline__ size_t s_idx(const Dev& d, uint32_t g, uint32_t m) { return (size_t)m * d.SLOTS + g; }
-// member m's entry for slot g. A recycled slot's entries are not cleared (k_gossip_free): an entry created before
-// the slot's current gossip existed (slot_ctick) belongs to an earlier gossip of the slot and reads as never held.
-// (Every holder of the earlier gossip received it before its slot expired, EXPB > 0 ticks before the recycle.)
-__device__ __forceinline__ uint32_t s_get(const Dev& d, uint32_t g, uint32_t m) {
-  const uint32_t e = d.S[s_idx(d, g, m)];
-  return (e & S_TICK_MASK) != 0 && s_ctick(e) < d.slot_ctick[g] ? 0u : e;
+// member m's entry for slot g in the 32-bit form (creation tick + 1 | SWEPT | REBORN; 0 = never held). A recycled
+// slot's entries are not cleared at once (k_gossip_free, k_s_scrub): an entry created before the slot's current gossip
+// existed (slot_ctick) belongs to an earlier gossip of the slot and reads as never held. (Every holder of the earlier
+// gossip received it before its slot expired, EXPB > 0 ticks before the recycle.)
+__device__ __forceinline__ uint32_t s_get(const Dev& d, uint32_t g, uint32_t m, uint32_t ref) {
+  const uint16_t e = d.S[s_idx(d, g, m)];
+  if (!(e & S16_EVER)) return 0u;
+  const uint32_t c = s16_tick(e, ref);
+  if (c < d.slot_ctick[g]) return 0u;
+  return ((c + 1u) & S_TICK_MASK) | ((e & S16_SWEPT) ? S_SWEPT : 0u) | ((e & S16_REBORN) ? S_REBORN : 0u);
+}
+__device__ __forceinline__ void s_put(const Dev& d, uint32_t g, uint32_t m, uint32_t ctick, bool reborn) {
+  d.S[s_idx(d, g, m)] = (uint16_t)(S16_EVER | (ctick & S16_TICK) | (reborn ? S16_REBORN : 0u));
 }
 
 // ---- gossip holder state (gossip.hip) ----
@@ -370,7 +377,7 @@ __device__ __forceinline__ void slot_create(const Dev& d, uint32_t g, uint32_t m
   const unsigned long long bit = 1ull << (g & 63u);
   atomicOr(&d.GU[g >> 6], bit);
   if (subj != USER_SUBJ && rec_status(key) == ST_DEAD) atomicOr(&d.DM[g >> 6], bit);
-  d.S[s_idx(d, g, m)] = (k + 1u) & S_TICK_MASK;
+  s_put(d, g, m, k, false);
   atomicOr(&hrow(d, m)[g >> 6], bit);
   ring(d, m)[pos & (d.BCAP - 1)] = rg_entry(g, rounds_before(d, m, k));
   if (pos + 1u - d.rhead[m] > d.BCAP) set_err(d, E_RING);

@@ -32,9 +32,20 @@ constexpr uint32_t SPQ = 32;  // gossips a member creates in one tick before the
 constexpr uint32_t MQ = 16;   // inbound SYNC messages of one tick sorted in registers (more: selected by list walks)
 constexpr uint32_t SORT_MAX = 4096;  // receipts of one member and tick sorted in LDS at once (more: runs + merges)
 
-// S entry flags (gossip slot x member)
+// S entry flags (gossip slot x member), as s_get returns them
 constexpr uint32_t S_SWEPT = 1u << 30, S_REBORN = 1u << 31;
 constexpr uint32_t S_TICK_MASK = (1u << 29) - 1u;
+// stored S entries are 16 bits: REBORN | SWEPT | EVER | the creation tick's low 13 bits. s_get rebuilds the tick as the
+// latest one at or before the entry's newest possible tick (now + lat) with those bits, exact while every entry is
+// younger than 8192 ticks: a slot may live SLIFE ticks (E_SLIFE past it), and every SCRUB ticks k_s_scrub clears the
+// entries of recycled slots, so a stale entry is at most SLIFE + SCRUB < 8192 - lat ticks old
+constexpr uint16_t S16_REBORN = 1u << 15, S16_SWEPT = 1u << 14, S16_EVER = 1u << 13, S16_TICK = (1u << 13) - 1u;
+constexpr uint32_t SLIFE = 4096, SCRUB = 2048;
+// the creation tick of a stored entry: the latest tick at or before ref (the newest an entry can carry: now + lat)
+// with the stored low 13 bits
+__host__ __device__ __forceinline__ uint32_t s16_tick(uint16_t e, uint32_t ref) {
+  return ref - ((ref - (uint32_t)(e & S16_TICK)) & (uint32_t)S16_TICK);
+}
 
 // device error bits
 constexpr uint32_t E_SLOTS = 1, E_FETCH = 2, E_SUBS = 4, E_PATHS = 8, E_GROUPS = 16, E_MSGS = 32, E_ARENA = 64,
@@ -45,7 +56,8 @@ constexpr uint32_t E_SLOTS = 1, E_FETCH = 2, E_SUBS = 4, E_PATHS = 8, E_GROUPS =
                    E_PIN = 1u << 21,  // a later SYNC payload of a receiver's tick had no readable copy (pin)
                    E_RING = 1u << 22,  // a member held more gossips than its receipt ring (gossip_ring_cap)
                    E_DELAYQ = 1u << 23,  // more delayed first receipts due in one tick than the delay queue holds
-                   E_SYNCQ = 1u << 24;   // more delayed SYNC / SYNC_ACK messages in flight than the SYNC delay store holds
+                   E_SYNCQ = 1u << 24,   // more delayed SYNC / SYNC_ACK messages in flight than the SYNC delay store holds
+                   E_SLIFE = 1u << 25;   // a gossip slot stayed in use SLIFE ticks (its 16-bit holder entries could alias)
 // per-link NetworkEmulator settings (setLinkSettings / block / unblock): hash of (src, dst) -> change history
 constexpr uint32_t LKCAP = 4096, LKH = 8;  // keys, history entries per key
 constexpr uint32_t CIN_SLOW = 0xFFFFFFFEu;
@@ -221,8 +233,8 @@ struct Dev {
   uint64_t* slot_key;  // inc | status<<32 (status may be DEAD)
   uint32_t* slot_exp;  // tick from which no member holds the gossip any more: the slot is recycled (k_gossip_free)
   uint32_t* slot_used;
-  uint32_t* S;  // [N][SLOTS] creation tick + 1 | SWEPT | REBORN of each member's latest incarnation (replay, hashes);
-                // entries older than the slot's gossip (slot_ctick) are stale (s_get)
+  uint16_t* S;  // [N][SLOTS] creation tick (13 low bits) | EVER | SWEPT | REBORN of each member's latest incarnation
+                // (replay, hashes); entries older than the slot's gossip (slot_ctick) are stale (s_get)
   uint32_t* free_list;
   int32_t* free_top;
   uint64_t* xd;  // W > 1: (slot << 32) | target, this shard's first receipts of the tick (exchange B)
@@ -395,5 +407,6 @@ void launch_md_column(const Dev& d, uint32_t m, uint32_t u, void* stream);
 void launch_join(const Dev& d, uint32_t m, uint32_t k, const uint32_t* seeds, uint32_t n, void* stream);  // RUMOR mode, at ticks k % ping_t == 0
 void launch_hash(const Dev& d, uint64_t* out, uint32_t now, void* stream);
 void launch_held_add(const Dev& d, const int32_t* sum, void* stream);
+void launch_s_scrub(const Dev& d, uint32_t now, void* stream);  // every SCRUB ticks: stale S entries cleared
 
 }  // namespace swim

@@ -58,8 +58,8 @@ __device__ void hist_push(const Dev& d, uint64_t gid, uint32_t member, uint32_t 
 }
 
 // creation tick of member's incarnation of g that existed at tick tau (NEVER if none)
-__device__ uint32_t inc_at(const Dev& d, uint32_t member, uint32_t g, uint64_t gid, uint32_t tau) {
-  uint32_t e = s_get(d, g, member);
+__device__ uint32_t inc_at(const Dev& d, uint32_t member, uint32_t g, uint64_t gid, uint32_t tau, uint32_t ref) {
+  uint32_t e = s_get(d, g, member, ref);
   if (!s_ever(e)) return NEVER;
   uint32_t c = s_ctick(e);
   if (c <= tau) return c;
@@ -126,7 +126,7 @@ __device__ __forceinline__ bool replay_pair(const Dev& d, uint32_t x, uint32_t y
       uint32_t rin = c.dir == 0 ? 0 : 1;  // receiver index into lo_in
       if (lo_in[rin] == NEVER || c.tick + lat + dmax(d) < lo_in[rin]) continue;
       if (d.dly_on && gossip_arrival(d, c.dir == 0 ? y : x, c.dir == 0 ? x : y, c.tick, c.slot, gid) < lo_in[rin]) continue;
-      if (cinc[i] == NEVER - 1) cinc[i] = inc_at(d, c.dir == 0 ? y : x, g, gid, c.tick);
+      if (cinc[i] == NEVER - 1) cinc[i] = inc_at(d, c.dir == 0 ? y : x, g, gid, c.tick, tau + lat);
       uint32_t cs = cinc[i];
       uint32_t snd = c.dir == 0 ? y : x;
       if (cs == NEVER || rounds_before(d, snd, cs) + c.spread < rounds_before(d, snd, c.tick)) continue;
@@ -158,7 +158,7 @@ __device__ __forceinline__ bool replay_pair(const Dev& d, uint32_t x, uint32_t y
     const Contact& c = ev[i];
     uint32_t snd = c.dir == 0 ? y : x;
     // the sender held g at that round (its incarnation then), inside its spread window (selectGossipsToSend :246)
-    uint32_t cs = cinc[i] != NEVER - 1 ? cinc[i] : inc_at(d, snd, g, gid, c.tick);
+    uint32_t cs = cinc[i] != NEVER - 1 ? cinc[i] : inc_at(d, snd, g, gid, c.tick, tau + lat);
     if (cs == NEVER) continue;
     if (rounds_before(d, snd, cs) + c.spread < rounds_before(d, snd, c.tick)) continue;
     if (swept_before(d, snd, cs, c.tick)) continue;  // x no longer held it
@@ -396,7 +396,7 @@ __device__ void round_member(const Dev& d, uint32_t m, uint32_t k, unsigned long
   const uint32_t* R = ring(d, m);
   for (uint32_t p = h + tid; p - h < send - h; p += nth) {
     const uint32_t g = R[p & (d.BCAP - 1)] & RG_SLOT;
-    d.S[s_idx(d, g, m)] |= S_SWEPT;
+    d.S[s_idx(d, g, m)] |= S16_SWEPT;
     on_sweep(d, g, m, k);
   }
   const uint32_t nch = (send - h) + ((int32_t)(r2 - w0) > 0 ? r2 - w0 : 0u) + (r3 - wnew) + (tl - r4);
@@ -893,7 +893,7 @@ __global__ void __launch_bounds__(256) k_gossip_replay(const Dev* __restrict__ d
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint64_t v = d.rp[i];
     const uint32_t g = (uint32_t)(v >> 32), ms = (uint32_t)v, m = ms / d.F, s = ms % d.F;
-    const uint32_t t = d.T[ms], c = s_ctick(d.S[s_idx(d, g, m)]), ci = d.cin[ms];  // m holds g: a current entry
+    const uint32_t t = d.T[ms], c = s_ctick(s_get(d, g, m, k + d.lat)), ci = d.cin[ms];  // m holds g: a current entry
     const uint64_t gid = d.slot_gid[g];
     const bool maybe = ci >= d.slot_ctick[g] && ci + d.lat + dmax(d) >= c;
     if (d.exp & 4) {  // timing experiment: replay items that reach the contact replay, and those it blocks
@@ -925,7 +925,7 @@ __global__ void __launch_bounds__(64) k_gossip_send_slow(const Dev* __restrict__
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint64_t v = d.slow[i];
     const uint32_t g = (uint32_t)(v >> 32), ms = (uint32_t)v, m = ms / d.F, s = ms % d.F;
-    const uint32_t t = d.T[ms], c = s_ctick(d.S[s_idx(d, g, m)]);
+    const uint32_t t = d.T[ms], c = s_ctick(s_get(d, g, m, k + d.lat));
     const uint64_t gid = d.slot_gid[g];
     if (blocked_pair(d, m, t, g, gid, k, c)) continue;  // isInfected (:247)
     sends++;
@@ -983,10 +983,9 @@ __device__ __forceinline__ bool receipt_matters(const Dev& d, uint32_t t, uint32
 // the holder-table entry of a first receipt (onGossipReq :176-180): the incarnation created at tick k + lat; a
 // rebirth after a sweep keeps the swept incarnation's creation tick in the history (infectedFrom replay)
 __device__ __forceinline__ void receipt_create(const Dev& d, uint32_t g, uint32_t t, uint32_t k) {
-  uint32_t* p = d.S + s_idx(d, g, t);
-  const uint32_t e = s_get(d, g, t);
+  const uint32_t e = s_get(d, g, t, k + d.lat);
   if (s_ever(e)) hist_push(d, d.slot_gid[g], t, s_ctick(e));
-  *p = ((k + d.lat + 1u) & S_TICK_MASK) | (s_ever(e) ? S_REBORN : 0u);
+  s_put(d, g, t, k + d.lat, s_ever(e));
   if (d.dly_on)  // a delayed first receipt still queued may have pushed it further (delay_push)
     atomicMax(&d.slot_exp[g], k + d.lat + d.EXPB);
   else
@@ -1066,7 +1065,9 @@ __global__ void k_gossip_expire(Dev d, uint32_t k) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nag * 64u) return;
   const uint32_t q = d.agroup[i >> 6], g = q * 64u + (i & 63u);
-  if (!((d.GU[q] >> (g & 63u)) & 1ull) || d.slot_exp[g] > k) return;
+  if (!((d.GU[q] >> (g & 63u)) & 1ull)) return;
+  if (k - d.slot_ctick[g] > SLIFE) set_err(d, E_SLIFE);  // its 16-bit holder entries could alias (engine.h)
+  if (d.slot_exp[g] > k) return;
   const unsigned long long bit = 1ull << (g & 63u);
   atomicAnd(&d.GU[q], ~bit);
   atomicAnd(&d.DM[q], ~bit);

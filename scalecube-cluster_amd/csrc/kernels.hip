@@ -440,7 +440,7 @@ __global__ void __launch_bounds__(256) k_hash(Dev d, uint64_t* out, uint32_t now
   const bool dead = d.dead_tick[m] != NEVER;  // a crashed member keeps no gossips (SEMANTICS.md §1)
   for (uint32_t g = threadIdx.x; g < d.SLOTS && !dead; g += blockDim.x) {
     if (!d.slot_used[g]) continue;
-    uint32_t e = s_get(d, g, m);
+    uint32_t e = s_get(d, g, m, now + d.lat);
     // receipts applied at the end of tick now-1 belong to P4 of tick `now`: not yet visible
     if (s_held(e) && s_ctick(e) < now) hgs += hpair(d.slot_gid[g], rounds_before(d, m, s_ctick(e)));
   }
@@ -479,6 +479,35 @@ __global__ void k_held_add(Dev d, const int32_t* sum) {
 }
 void launch_held_add(const Dev& d, const int32_t* sum, void* stream) {
   hipLaunchKernelGGL(k_held_add, dim3((d.N + 255) / 256), dim3(256), 0, (hipStream_t)stream, d, sum);
+}
+
+// every SCRUB ticks (engine.h): the holder entries of recycled slots are cleared, 8 entries (16 B) per lane, so that
+// no stale entry outlives the 13-bit tick window of s_get. SLOTS is a multiple of 64: a lane's 8 entries share a member.
+__global__ void __launch_bounds__(256) k_s_scrub(Dev d, uint32_t now) {
+  const uint64_t nq = (uint64_t)d.N * d.SLOTS / 8;
+  const uint32_t ref = now + d.lat;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nq; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint4* p = (uint4*)d.S + i;
+    uint4 v = *p;
+    if ((v.x | v.y | v.z | v.w) == 0u) continue;
+    const uint32_t g0 = (uint32_t)((i * 8) % d.SLOTS);
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    bool changed = false;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint16_t e = (uint16_t)(w[j >> 1] >> ((j & 1) * 16));
+      if (!(e & S16_EVER)) continue;
+      const uint32_t g = g0 + j;
+      if (!d.slot_used[g] || s16_tick(e, ref) < d.slot_ctick[g]) {
+        w[j >> 1] &= ~(0xFFFFu << ((j & 1) * 16));
+        changed = true;
+      }
+    }
+    if (changed) *p = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+void launch_s_scrub(const Dev& d, uint32_t now, void* stream) {
+  hipLaunchKernelGGL(k_s_scrub, dim3(8192), dim3(256), 0, (hipStream_t)stream, d, now);
 }
 
 // ------------------------------------------------------------------------------------------------------------

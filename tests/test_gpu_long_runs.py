@@ -1,0 +1,36 @@
+"""Runs longer than the 13-bit tick window of the engine's 16-bit holder entries (engine.h S16_*, SCRUB, SLIFE): slots
+are recycled many times over 10^4 ticks, so stale entries of earlier gossips must read as never held (s_get) until the
+periodic scrub clears them. Bit-exact against the CPU oracle, which keeps full ticks (state hashes include every
+member's event-sequence hash)."""
+import pytest
+
+from swimhip import ClusterConfig, SimConfig, _abi
+
+from parity_util import pair, run_lockstep
+
+pytestmark = pytest.mark.gpu
+
+
+def test_rumor_long_run_slot_reuse(oracle, engine):
+    cfg = SimConfig(n_members=200, mode=_abi.MODE_RUMOR, churn_per_period=8, gossip_slot_cap=1024)
+    o, e = pair(oracle, engine, cfg)
+    for c in (o, e):
+        c.set_default_loss(5)
+    run_lockstep(o, e, 12_000, 2_000, "rumor, 12 000 ticks", events=False)
+    assert o.counters()["gossips_created"] > 4 * 1024  # every slot reused several times
+    e.close()
+    o.close()
+
+
+def test_full_long_run_slot_reuse(oracle, engine):
+    cfg = SimConfig(n_members=120, cluster=ClusterConfig(seedMembers=[0]), gossip_slot_cap=1024)
+    o, e = pair(oracle, engine, cfg)
+    for c in (o, e):
+        c.set_default_loss(10)
+    run_lockstep(o, e, 4_000, 1_000, "full, loss", events=False)
+    for c in (o, e):
+        c.kill(7)
+        c.update_incarnation(3)
+    run_lockstep(o, e, 6_000, 1_000, "full, kill + update", events=False)  # (per-member event hashes compared)
+    e.close()
+    o.close()
