@@ -29,6 +29,7 @@ constexpr uint32_t TRK = 16;   // subjects written in one tick's P1 that are re-
 // snapshots per member, deferred snapshots per k_member_tick block
 constexpr uint32_t ULOG = 64, CREQ = 4, CWMAX = 32;
 constexpr uint32_t SPQ = 32;  // gossips a member creates in one tick before their slots are taken together
+constexpr uint32_t KP = 64;   // FD-list inserts of one member's tick applied together (member.hip fd_flush)
 constexpr uint32_t MQ = 16;   // inbound SYNC messages of one tick sorted in registers (more: selected by list walks)
 constexpr uint32_t SORT_MAX = 4096;  // receipts of one member and tick sorted in LDS at once (more: runs + merges)
 
@@ -271,6 +272,7 @@ struct Dev {
   uint32_t* trk;    // [NL][TRK] per receiver: subjects its row changed earlier in this tick's P1 (member.hip)
   uint32_t* ulog;   // [NL][ULOG][2] per member: (subject, old key) of its row writes this tick after a SYNC send
   uint32_t* spq;    // [NL][SPQ][8] per member: gossips created this tick, waiting for their slots (member.hip)
+  uint32_t* fpend;  // [NL][KP][2] per member: this tick's pending FD-list inserts (subject, final position)
   uint32_t* chunk_meta;                      // [MSGCAP][NCHUNK][2] (pool offset, count)
   uint64_t* pool;                            // candidate (subject << 34 | key)
   uint32_t* pool_used;

@@ -42,6 +42,10 @@ struct ML {
   uint32_t ncreq, nlog;  // open snapshots (their cw entries carry this member's id), logged writes
   uint32_t* spq;  // gossips created this tick that wait for their slots (flush_spreads): [SPQ][8] gid, subj, key
   uint32_t nsp;
+  // ArrayList.add(index) inserts of this tick not applied to fdl yet (fd_flush), sorted by their final position;
+  // fdLen counts them
+  uint32_t* fpend;
+  uint32_t npend;
 
 };
 
@@ -230,9 +234,37 @@ __device__ __forceinline__ bool list_remove(uint32_t* a, uint32_t len, uint32_t 
   return true;
 }
 
+// The FD list with its pending inserts applied: one pass over the part of the list at or above the first insert,
+// instead of one tail shift per ArrayList.add(index, e). Entry p (ascending final positions f_0 < ... < f_{k-1}) ends
+// at f_p; the originals between f_p and f_{p+1} move up by p + 1, segment by segment from the top (8 loads in flight,
+// then 8 stores), so no original is overwritten before it is read.
+__device__ __noinline__ void fd_flush(uint32_t* a, const uint32_t* pend, uint32_t k, uint32_t len) {
+  for (int p = (int)k - 1; p >= 0; --p) {
+    const uint32_t fp = pend[2 * p + 1], fnext = (uint32_t)p + 1 < k ? pend[2 * p + 3] : len;
+    const uint32_t s = (uint32_t)p + 1, lo = fp + 1 - s, hi = fnext - s;  // originals [lo, hi) move to [lo + s, hi + s)
+    uint32_t j = hi;
+    for (; j >= lo + 8; j -= 8) {
+      uint32_t v[8];
+#pragma unroll
+      for (uint32_t t = 0; t < 8; ++t) v[t] = a[j - 8 + t];
+#pragma unroll
+      for (uint32_t t = 0; t < 8; ++t) a[j - 8 + t + s] = v[t];
+    }
+    for (; j > lo; --j) a[j - 1 + s] = a[j - 1];
+    a[fp] = pend[2 * p];
+  }
+}
+__device__ __forceinline__ void fd_ready(ML& L) {
+  if (L.npend) {
+    fd_flush(L.fdl, L.fpend, L.npend, L.fdLen);
+    L.npend = 0;
+  }
+}
+
 __device__ __forceinline__ void on_member_event(ML& L, uint32_t type, uint32_t subj) {
   const Dev& d = *L.d;
   if (type == 1) {  // REMOVED: FailureDetectorImpl.onMemberEvent (:321-325), GossipProtocolImpl (:187-189)
+    fd_ready(L);
     if (list_remove(L.fdl, L.fdLen, subj)) L.fdLen--;
     if (list_remove(L.gl, L.gLen, subj)) L.gLen--;
   } else if (type == 0) {  // ADDED: insert at nextInt(size) (:326-331); append (:190-192)
@@ -240,17 +272,17 @@ __device__ __forceinline__ void on_member_event(ML& L, uint32_t type, uint32_t s
       set_err(d, E_LIST);
       return;
     }
-    uint32_t idx = L.fdLen > 0 ? next_int(draw(L, S_FD_INSERT), L.fdLen) : 0;
-    uint32_t j = L.fdLen;  // ArrayList.add(index, e): the tail moves up by one, in blocks of 8 from the top
-    for (; j >= idx + 8; j -= 8) {
-      uint32_t v[8];
-#pragma unroll
-      for (uint32_t t = 0; t < 8; ++t) v[t] = L.fdl[j - 8 + t];
-#pragma unroll
-      for (uint32_t t = 0; t < 8; ++t) L.fdl[j - 7 + t] = v[t];
+    const uint32_t idx = L.fdLen > 0 ? next_int(draw(L, S_FD_INSERT), L.fdLen) : 0;
+    if (L.npend == KP) fd_ready(L);
+    // ArrayList.add(index, e), deferred: the pending inserts at or above idx move up by one, the new one takes idx
+    uint32_t j = L.npend;
+    for (; j > 0 && L.fpend[2 * j - 1] >= idx; --j) {
+      L.fpend[2 * j] = L.fpend[2 * j - 2];
+      L.fpend[2 * j + 1] = L.fpend[2 * j - 1] + 1u;
     }
-    for (; j > idx; --j) L.fdl[j] = L.fdl[j - 1];
-    L.fdl[idx] = subj;
+    L.fpend[2 * j] = subj;
+    L.fpend[2 * j + 1] = idx;
+    L.npend++;
     L.fdLen++;
     L.gl[L.gLen++] = subj;
   }
@@ -625,6 +657,7 @@ __device__ __forceinline__ void ping_req_step(ML& L, uint32_t target, uint32_t c
   uint32_t nh = 0;
   const uint32_t kreq = mc_kreq(d, L.m);
   if (kreq > 0) {
+    fd_ready(L);
     uint32_t pos = L.fdLen;
     for (uint32_t i = 0; i < L.fdLen; ++i)
       if (L.fdl[i] == target) {
@@ -684,6 +717,7 @@ __device__ __forceinline__ void do_ping(ML& L) {
   const Dev& d = *L.d;
   L.fdPeriod++;
   if (L.fdLen == 0) return;
+  fd_ready(L);
   if (L.pingIdx >= (int32_t)L.fdLen) {
     L.pingIdx = 0;
     shuffle_list(L, L.fdl, L.fdLen, S_FD_SHUFFLE);
@@ -1036,6 +1070,8 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   L.paths = d.paths + li * d.PCAP * 5;
   L.fetch = d.fetch + li * d.FCAP * FREC;
   L.groups = d.groups + li * d.GRCAP * GREC;
+  L.fpend = d.fpend + li * KP * 2;
+  L.npend = 0;
   for (int i = 0; i < 8; ++i) L.c[i] = 0;
   L.pend = NEVER;
   L.tround = 0;
@@ -1365,6 +1401,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
 
   lap(1);  // P2 + P3
   if (dead) {
+    fd_ready(L);
     d.tround[m] = 0;
     d.npath[m] = L.npath;
     d.nfetch[m] = L.nfetch;
@@ -1532,6 +1569,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   if (L.ncreq)  // the log length the block epilogue undoes from
     for (uint32_t q = 0, n = min(*L.cw_n, d.cwmax_cap); q < n; ++q)
       if (L.cw[q].x == m) L.cw[q].w = L.nlog;
+  fd_ready(L);
   d.next_evt[m] = nev;
   d.tround[m] = L.tround;
   d.tsize[m] = L.tsize;
