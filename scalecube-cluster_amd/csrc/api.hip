@@ -1208,7 +1208,6 @@ int swim_step(swim_handle* h, uint32_t n) {
         const TickEvents* tj = timed(kj) ? &h->prof[j] : nullptr;
         launch_tick_a(d, kj, h->stream, tj, true);
         if ((xr = exchange_inline(h, d.xa_recv, d.XA_PEER, d.xa_scnt, d.xa_rcnt, true)) != SWIM_OK) return xr;
-        launch_spec_gate(d, kj, h->stream);
         launch_tick_b(d, kj, h->stream, tj, false, true);
       }
       HIPCK(hipMemcpyAsync((void*)(h->hflag + 1), d.halt, 4, hipMemcpyDeviceToHost, h->stream));

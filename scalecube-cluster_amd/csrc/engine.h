@@ -394,11 +394,10 @@ void launch_gossip(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
 // exchange B; C = unpack B, apply receipts, routing, slot recycling. The host runs the exchanges in between and
 // skips the gossip half (and exchange B) when no shard has a gossip slot in use.
 // spec: a launch of a speculative sharded batch (RCCL, gossip plane idle): every kernel returns at once once d.halt is
-// set; launch_spec_gate (after exchange A's inline all-to-all) raises it at the first tick whose exchange needs the
-// host (a gossip slot in use on some shard, or a region past the inline block)
+// set; k_unpack_a (after exchange A's inline all-to-all) raises it at the first tick whose exchange needs the host (a
+// gossip slot in use on some shard, or a region past the inline block)
 void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr, bool spec = false);
 void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool gossip, bool spec = false);
-void launch_spec_gate(const Dev& d, uint32_t k, void* stream);
 void launch_tick_c(const Dev& d, uint32_t k, void* stream, bool gossip);
 void launch_inline_out(const Dev& d, const uint8_t* send, uint64_t cap, const unsigned long long* scnt, void* stream);
 void launch_inline_in(const Dev& d, uint8_t* recv, uint64_t cap, const unsigned long long* scnt, unsigned long long* rcnt,

@@ -182,8 +182,15 @@ __device__ void msgs_commit(const Dev& d, uint32_t b) {
 // replay peer p's gossip creations and rounds into the replicated gossip plane; queue its SYNC messages. The block
 // that finishes last commits the inbound list, and, when no shard has a gossip slot in use (`end`), closes the tick
 // (k_tick_end): the steady-state tick after exchange A is this one launch.
+__device__ __forceinline__ bool spec_gate(const Dev& d);
 __global__ void __launch_bounds__(256) k_unpack_a(Dev d, uint32_t k, uint32_t end, uint32_t spec) {
   if (spec_halted(d, spec)) return;
+  // the gate of a speculative batch, evaluated by every block from the same count words: all of them see the same
+  // answer, and one raises d.halt for the host
+  if (spec && spec_gate(d)) {
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *d.halt = k + 1u;
+    return;
+  }
   const uint32_t p = blockIdx.y;
   if (p != d.rank && (d.xa_rcnt[p] & XCNT_MASK) >= 32) {
     const uint8_t* R = d.xa_recv + (size_t)p * d.XA_PEER;
@@ -319,20 +326,16 @@ void launch_inline_in(const Dev& d, uint8_t* recv, uint64_t cap, const unsigned 
                      d.xi_host, d.W, spec ? (const uint32_t*)d.halt : nullptr, d.XI);
 }
 
-// speculative sharded batch, after exchange A's inline all-to-all of tick k: halt (d.halt = k + 1) if any shard has a
+// speculative sharded batch, after exchange A's inline all-to-all of a tick (k_unpack_a): halt if any shard has a
 // gossip slot in use or a region past its inline block. Every shard reads the same flags (its own and every peer's
 // count words), so all of them halt at the same tick and run its rest on the host path
-__global__ void k_spec_gate(Dev d, uint32_t k) {
-  if (threadIdx.x != 0 || *(volatile uint32_t*)d.halt) return;
+__device__ __forceinline__ bool spec_gate(const Dev& d) {
   unsigned long long f = 0;
   for (uint32_t p = 0; p < d.W; ++p) {
     f |= d.xa_rcnt[p] | d.xa_scnt[p];
     if ((d.xa_scnt[p] & XCNT_MASK) > d.XI - 8) f |= XFLAG_OVER;
   }
-  if (f & (XFLAG_GOSSIP | XFLAG_OVER)) *d.halt = k + 1u;
-}
-void launch_spec_gate(const Dev& d, uint32_t k, void* stream) {
-  hipLaunchKernelGGL(k_spec_gate, dim3(1), dim3(64), 0, (hipStream_t)stream, d, k);
+  return (f & (XFLAG_GOSSIP | XFLAG_OVER)) != 0;
 }
 
 }  // namespace swim
