@@ -16,5 +16,4 @@ for ww in c2:12 c5:25; do
     echo "$w $c done"
   done
 done
-timeout -k 10 600 python3 -u bench.py --workload c5 --members 1000000 --rehearse-shard 8 --steps 3 --warmup 25 --no-cpu-baseline > $O/c5_1M_shard.log 2>&1
-grep -o '"ms_per_step": [0-9.]*\|"device_bytes": [0-9]*' $O/c5_1M_shard.log
+# (the lone 10^6-member C5 shard is measured by tools/gpu_r3_c5m.sh)
