@@ -462,6 +462,13 @@ int build(swim_handle* h) {
   A(d.arena[1], (uint64_t)d.ARENA_ROWS * d.NS) A(d.arena_used, 2)
   A(d.m_next, 2ull * d.MSGCAP) A(d.m_head, 2 * N) A(d.next_evt, N) A(d.mdone, 2) A(d.trk, NL * TRK) A(d.ulog, NL * ULOG * 2) A(d.spq, NL * SPQ * 8) A(d.fpend, NL * KP * 2) A(d.pending_inc, N) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
   A(d.pool, d.POOLCAP) A(d.pool_used, 1)
+  // SYNC_ACK resolution (k_ack_resolve): one GPU; SWIM_NO_ACKRES streams every payload (measurements)
+  d.ackres = d.W == 1 && !d.implicit && !getenv("SWIM_NO_ACKRES") ? 1u : 0u;
+  if (d.ackres) {
+    A(d.tlog, 2 * NL * TL) A(d.tl_n, 2 * NL) A(d.tl_tick, 2 * NL) A(d.dlist, d.MSGCAP) A(d.ndl, 1)
+    HIPCK(hipMemsetAsync(d.tl_tick, 0xFF, 8 * NL, h->stream));
+    HIPCK(hipMemsetAsync(d.ndl, 0, 4, h->stream));
+  }
   A(d.ev, (uint64_t)d.EVCAP * 8) A(d.ev_n, 1) A(d.ctr, C_NCTR) A(d.err, 8)
   if (c.flags & SWIM_FLAG_EMULATOR_COUNTERS) {
     A(d.em, 2 * N)
@@ -1806,6 +1813,7 @@ int swim_counters_get(swim_handle* h, swim_counters* out) {
   out->gossip_ns = (uint64_t)(h->prof_ms[2] * 1e6);
   out->diff_launches = h->prof_diff_launches;
   out->diff_msgs = c[C_DIFFMSG];
+  out->ack_resolved = c[C_ACKRES];
   out->exchange_ns = (uint64_t)(h->xchg_ms * 1e6);
   return SWIM_OK;
 }

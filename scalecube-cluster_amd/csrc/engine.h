@@ -81,7 +81,7 @@ constexpr uint32_t XINL = 16384;  // RCCL: bytes per peer moved by the fixed-siz
 
 // counters (swim_counters order after .tick)
 // 8..12: SWIM_EXP & 4 (and 16..19: the gossip plane's work units per tick, for algorithmic bytes; tools/pmc_gossip.py)
-enum Ctr { C_R = 0, C_W, C_M, C_G, C_E, C_LOST, C_GCREATED, C_SYNCMERGE, C_DIFFMSG = 13, C_XU = 16, C_NCTR = 24 };
+enum Ctr { C_R = 0, C_W, C_M, C_G, C_E, C_LOST, C_GCREATED, C_SYNCMERGE, C_DIFFMSG = 13, C_XU = 16, C_ACKRES = 24, C_NCTR = 26 };
 
 // capacity fallbacks that fired (include/swimhip_debug.h; counted only when Dev::fb is allocated: SWIM_CAPS or
 // SWIM_FALLBACKS set at create). Each one is an exact slow path taken when a fixed-capacity fast structure is full.
@@ -109,8 +109,17 @@ struct SyncMsg {
   // sender may write its live row meanwhile), for the subjects an earlier payload of that tick changed
   uint32_t pin;
   uint32_t due;  // delayed message (kind has KF_DEFER): the tick of its P1 delivery
+  uint32_t tln;  // SYNC_ACK with KF_RES: the sender's tick write-log length when it sent (k_ack_resolve)
 };
 constexpr uint32_t KF_DEFER = 0x100u;  // SyncMsg.kind flag: delivered after the next tick (k_sync_defer stores it)
+// k_sync_diff: a SYNC payload lacks a record the receiver holds (its SYNC_ACK cannot be resolved from write logs)
+constexpr uint32_t KF_ABS = 0x200u;
+// a SYNC_ACK sent in the tick its SYNC was merged: k_ack_resolve derives its diff from the two write logs instead of
+// k_sync_diff streaming it (cleared there when it cannot)
+constexpr uint32_t KF_RES = 0x400u;
+constexpr uint32_t KF_LATE = 0x800u;  // a delayed message put back by k_sync_redeliver
+constexpr uint32_t KF_FLAGS = KF_DEFER | KF_ABS | KF_RES | KF_LATE;
+constexpr uint32_t TL = 16;  // per-member tick write log (ack resolution); past it the member's ACKs are streamed
 
 struct Dev {
   // ---- configuration ----
@@ -276,6 +285,15 @@ struct Dev {
   uint32_t* chunk_meta;                      // [MSGCAP][NCHUNK][2] (pool offset, count)
   uint64_t* pool;                            // candidate (subject << 34 | key)
   uint32_t* pool_used;
+  // SYNC_ACK resolution (W == 1): per member and tick parity, the subjects whose key its row changed in
+  // that tick plus the candidates of the payloads it merged (first TL of them), their count (> TL: overflowed) and the
+  // tick they belong to; the messages k_sync_diff streams this tick (the others are resolved)
+  uint32_t ackres;
+  uint32_t* tlog;     // [2][NL][TL]
+  uint32_t* tl_n;     // [2][NL]
+  uint32_t* tl_tick;  // [2][NL]
+  uint32_t* dlist;    // [MSGCAP]
+  uint32_t* ndl;
 
   // ---- outputs ----
   uint32_t* ev;  // [EVCAP][8] swim_event

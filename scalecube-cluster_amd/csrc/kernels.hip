@@ -299,8 +299,7 @@ __global__ void __launch_bounds__(256) k_seg_sort(uint64_t* key, uint32_t* val, 
 // is the sender's live row or its copy-on-write snapshot; for a payload received from another shard, the shipped
 // chunk if it differs from the baseline, else the baseline
 template <bool SHARDED>
-__device__ __forceinline__ void diff_fetch(const Dev& d, uint32_t b, uint32_t w, uint4 (&x)[4]) {
-  const uint32_t mi = w / d.NCHUNK, c = w % d.NCHUNK;
+__device__ __forceinline__ void diff_fetch(const Dev& d, uint32_t b, uint32_t mi, uint32_t c, uint4 (&x)[4]) {
   const SyncMsg& mm = d.msgs[b][mi];
   const uint32_t s0 = c * CH + threadIdx.x * 8;
   // NS is a multiple of 8: a 32-B group is wholly in or out; padding entries are 0 (absent). A delayed message
@@ -341,22 +340,35 @@ __device__ __forceinline__ void diff_fetch(const Dev& d, uint32_t b, uint32_t w,
 // adds payloads received from other shards (baseline row + shipped chunks); the single-GPU instance has only local
 // rows and snapshots.
 template <bool SHARDED>
-__global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b, uint32_t timed, uint32_t spec) {
+__global__ void __launch_bounds__(256) k_sync_diff(const Dev* __restrict__ dp, uint32_t b, uint32_t timed, uint32_t spec) {
+  const Dev& d = *dp;  // global, not kernarg (as k_member_tick): a by-value Dev of this size was copied to scratch
   if (spec && *(volatile uint32_t*)d.halt) return;  // a speculative batch halted at an earlier tick
   __shared__ uint32_t scan[256];
   __shared__ uint32_t base;
   // (timed launches are bracketed by HIP events on the stream. A self-timing variant, first block start to last block
   // end by wall clock and atomics, made every launch of this kernel 30 % slower by its mere presence in the code:
   // 85 -> 112 us per launch at C3, profiles/r03_*)
-  uint32_t nmsg = d.nmsg[b] < d.MSGCAP ? d.nmsg[b] : d.MSGCAP;
+  // with SYNC_ACK resolution, only the messages k_ack_resolve left in dlist
+  const bool dl = !SHARDED && d.ackres;
+  uint32_t nmsg = dl ? *(volatile uint32_t*)d.ndl : (d.nmsg[b] < d.MSGCAP ? d.nmsg[b] : d.MSGCAP);
   if (timed && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&d.ctr[C_DIFFMSG], (unsigned long long)nmsg);
   uint32_t total = nmsg * d.NCHUNK;
+  const uint32_t* dlp = dl ? d.dlist : nullptr;
+  const uint32_t nch = d.NCHUNK;
   uint4 cur[4];
-  if (blockIdx.x < total) diff_fetch<SHARDED>(d, b, blockIdx.x, cur);
+  uint32_t mcur = 0;
+  if (blockIdx.x < total) {
+    mcur = dlp ? dlp[blockIdx.x / nch] : blockIdx.x / nch;
+    diff_fetch<SHARDED>(d, b, mcur, blockIdx.x % nch, cur);
+  }
   for (uint32_t w = blockIdx.x; w < total; w += gridDim.x) {
     uint4 nxt[4];
-    if (w + gridDim.x < total) diff_fetch<SHARDED>(d, b, w + gridDim.x, nxt);
-    const uint32_t mi = w / d.NCHUNK, c = w % d.NCHUNK;
+    uint32_t mnxt = 0;
+    if (w + gridDim.x < total) {
+      mnxt = dlp ? dlp[(w + gridDim.x) / nch] : (w + gridDim.x) / nch;
+      diff_fetch<SHARDED>(d, b, mnxt, (w + gridDim.x) % nch, nxt);
+    }
+    const uint32_t mi = mcur, c = w % nch;
     const uint32_t s0 = c * CH + threadIdx.x * 8;
     const uint32_t pin = d.msgs[b][mi].pin;
     if (pin != NEVER && d.msgs[b][mi].payload == NEVER && s0 < d.NS) {  // a live-row payload read again later (pin_msg)
@@ -366,18 +378,21 @@ __global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b, uint32_t t
     }
     const uint32_t p[8] = {cur[0].x, cur[0].y, cur[0].z, cur[0].w, cur[1].x, cur[1].y, cur[1].z, cur[1].w};
     const uint32_t r[8] = {cur[2].x, cur[2].y, cur[2].z, cur[2].w, cur[3].x, cur[3].y, cur[3].z, cur[3].w};
-    uint32_t mask = 0;
+    uint32_t mask = 0, ab = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
+    for (int j = 0; j < 8; ++j) {
       if ((p[j] & 3u) != ST_ABSENT && p[j] != r[j]) mask |= 1u << j;
+      ab |= (uint32_t)((p[j] & 3u) == ST_ABSENT && (r[j] & 3u) != ST_ABSENT);
+    }
     uint32_t nc = __popc(mask);
-    if (!__syncthreads_or(nc)) {  // steady state: the whole 2048-subject item matches
+    if (!__syncthreads_or(nc | ab)) {  // steady state: the whole 2048-subject item matches
       if (threadIdx.x == 0) {
         uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NCHUNK + c) * 2;
         cm[0] = 0;
         cm[1] = 0;
       }
     } else {
+      if (dl && ab) atomicOr(&d.msgs[b][mi].kind, KF_ABS);  // (rare: a record the payload lacks)
       scan[threadIdx.x] = nc;
       __syncthreads();
       for (uint32_t o = 1; o < 256; o <<= 1) {
@@ -411,6 +426,86 @@ __global__ void __launch_bounds__(256) k_sync_diff(Dev d, uint32_t b, uint32_t t
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
+    mcur = mnxt;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// k_ack_resolve (W == 1): the SYNC_ACKs of tick k-1 whose diff follows from logs instead of a stream.
+// Member A's SYNC of tick k-2 carried A's row as of its send; B's diff at tick k-1 extracted D = {s : payload[s] !=
+// B's row[s]} (no record the payload lacked, else KF_ABS), B merged D and answered in the same tick with its row at
+// that moment. For any subject outside D, outside what B wrote in tick k-1 before the answer and outside what A
+// wrote in ticks k-2 and k-1, B's answer and A's row now both equal A's payload. So only the subjects of those three
+// logs (tl_add: every key change and every merged candidate) can differ; they are tested here, in subject order,
+// into the same pool / chunk_meta form k_sync_diff writes. A message that cannot be resolved this way (no KF_RES, a
+// log past TL, a pinned live-row payload, a delayed one) goes to dlist for k_sync_diff. One wave per message.
+__global__ void __launch_bounds__(256) k_ack_resolve(Dev d, uint32_t b, uint32_t k, uint32_t spec, uint32_t timed) {
+  if (spec && *(volatile uint32_t*)d.halt) return;
+  __shared__ uint32_t sv_[4][64], sc_[4][64];
+  volatile uint32_t* sv = sv_[threadIdx.x >> 6];  // this wave's lists (volatile: read across lanes)
+  volatile uint32_t* sc = sc_[threadIdx.x >> 6];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t nmsg = min(d.nmsg[b], d.MSGCAP);
+  for (uint32_t i = blockIdx.x * 4 + wv; i < nmsg; i += gridDim.x * 4) {  // wave-uniform
+    const SyncMsg& mm = d.msgs[b][i];
+    const uint32_t kind = mm.kind, src = mm.src, dst = mm.dst, tln = mm.tln, pay = mm.payload;
+    bool res = k >= 2 && (kind & KF_RES) && !(kind & KF_DEFER) && mm.pin == NEVER && tln <= TL;
+    uint32_t n0 = 0, n1 = 0;  // A's log entries of ticks k-2 and k-1
+    if (res) {
+      const size_t a0 = (size_t)(k & 1) * d.NL + dst, a1 = (size_t)((k - 1) & 1) * d.NL + dst;
+      n0 = d.tl_tick[a0] == k - 2 ? d.tl_n[a0] : 0u;
+      n1 = d.tl_tick[a1] == k - 1 ? d.tl_n[a1] : 0u;
+      res = n0 <= TL && n1 <= TL;
+    }
+    if (!res) {
+      if (lane == 0) d.dlist[atomicAdd(d.ndl, 1u)] = i;
+      continue;
+    }
+    // gather: B's prefix, then A's two ticks (at most 3 TL <= 64 subjects, one per lane)
+    uint32_t v = NEVER;
+    if (lane < tln) v = d.tlog[((size_t)((k - 1) & 1) * d.NL + src) * TL + lane];
+    else if (lane < tln + n0) v = d.tlog[((size_t)(k & 1) * d.NL + dst) * TL + (lane - tln)];
+    else if (lane < tln + n0 + n1) v = d.tlog[((size_t)((k - 1) & 1) * d.NL + dst) * TL + (lane - tln - n0)];
+    sv[lane] = v;
+    __builtin_amdgcn_wave_barrier();
+    bool first = v != NEVER;
+    for (uint32_t j = 0; j < lane; ++j) first &= sv[j] != v;
+    uint32_t key = 0;
+    bool cand = false;
+    if (first) {
+      key = pay == NEVER ? d.rowk[(size_t)src * d.NS + v] : d.arena[b][(size_t)pay * d.NS + v];
+      cand = (key & 3u) != ST_ABSENT && key != d.rowk[(size_t)dst * d.NS + v];
+    }
+    sc[lane] = cand ? v : NEVER;
+    __builtin_amdgcn_wave_barrier();
+    uint32_t pos = 0;
+    for (uint32_t j = 0; j < 64; ++j) pos += sc[j] < v;
+    const uint32_t total = (uint32_t)__popcll(__ballot(cand));
+    uint32_t off = 0;
+    if (lane == 0 && total) {
+      off = atomicAdd(d.pool_used, total);
+      if (off + total > d.POOLCAP) {
+        atomicOr(d.err, E_POOL);
+        off = NEVER;
+      }
+    }
+    off = __shfl(off, 0);
+    if (cand && off != NEVER) d.pool[(size_t)off + pos] = ((uint64_t)v << 34) | key34(key);
+    // per chunk: first candidate and count (the chunk walk of merge_payload)
+    for (uint32_t c = lane; c < d.NCHUNK; c += 64) {
+      uint32_t before = 0, in = 0;
+      for (uint32_t j = 0; j < 64; ++j) {
+        const uint32_t t = sc[j];
+        before += t < c * CH;
+        in += t != NEVER && t / CH == c;
+      }
+      uint32_t* cm = d.chunk_meta + ((size_t)i * d.NCHUNK + c) * 2;
+      cm[0] = off == NEVER ? 0u : off + before;
+      cm[1] = off == NEVER ? 0u : in;
+    }
+    if (lane == 0) d.msgs[b][i].ncand = off == NEVER ? 0u : total;
+    if (lane == 0 && timed) atomicAdd(&d.ctr[C_ACKRES], 1ull);
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -526,15 +621,17 @@ void launch_init(const Dev& d, void* stream) {
 // timed: this launch is bracketed by profiling events; it adds its message count to ctr[C_DIFFMSG]
 static void launch_sync_diff(const Dev& d, uint32_t b, hipStream_t st, uint32_t timed, uint32_t spec = 0) {
   if (d.W > 1)
-    hipLaunchKernelGGL(k_sync_diff<true>, dim3(2048), dim3(256), 0, st, d, b, timed, spec);
+    hipLaunchKernelGGL(k_sync_diff<true>, dim3(2048), dim3(256), 0, st, d.self, b, timed, spec);
   else
-    hipLaunchKernelGGL(k_sync_diff<false>, dim3(2048), dim3(256), 0, st, d, b, timed, spec);
+    hipLaunchKernelGGL(k_sync_diff<false>, dim3(2048), dim3(256), 0, st, d.self, b, timed, spec);
 }
 
 // single GPU: the tick is cut in three so that the host can hold back the gossip data plane when no slot is in
 // use; the SYNC diff of tick k+1 does not depend on the gossip plane of tick k and is queued in between
 void launch_diff(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool spec) {
   hipStream_t st = (hipStream_t)stream;
+  if (k > 0 && d.ackres)
+    hipLaunchKernelGGL(k_ack_resolve, dim3(256), dim3(256), 0, st, d, (k - 1) & 1, k, spec ? 1u : 0u, prof ? 1u : 0u);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
   if (k > 0) launch_sync_diff(d, (k - 1) & 1, st, prof ? 1u : 0u, spec ? 1u : 0u);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
@@ -568,7 +665,7 @@ __global__ void __launch_bounds__(256) k_sync_redeliver(Dev d, uint32_t k, uint3
       __syncthreads();
       if (threadIdx.x == 0) {
         SyncMsg m = d.ds_msg[e];
-        m.kind &= ~KF_DEFER;
+        m.kind = (m.kind & ~KF_DEFER) | KF_LATE;
         m.payload = r;
         m.ncand = 0;
         m.pad = NEVER;

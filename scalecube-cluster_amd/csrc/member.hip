@@ -46,8 +46,20 @@ struct ML {
   // fdLen counts them
   uint32_t* fpend;
   uint32_t npend;
-
+  // SYNC_ACK resolution (d.ackres): this tick's write log (Dev::tlog), its length (> TL: overflowed) and last entry;
+  // the group of the SYNC merged just now whose SYNC_ACK may be resolved (-1: none)
+  uint32_t* tl;
+  uint32_t ntl, tlast;
+  int rgrp;
 };
+
+// a subject whose key this member's row changed in this tick, or a candidate of a payload it merged (k_ack_resolve)
+__device__ __forceinline__ void tl_add(ML& L, uint32_t s) {
+  if (L.ntl && L.tlast == s) return;  // merge_record's candidate, then its row_put
+  if (L.ntl < TL) L.tl[L.ntl] = s;
+  if (L.ntl <= TL) L.ntl++;
+  L.tlast = s;
+}
 
 __device__ __forceinline__ uint32_t draw(ML& L, uint32_t stream) {
   uint32_t c = L.sel[stream]++;
@@ -149,13 +161,16 @@ __device__ __forceinline__ void row_put(ML& L, uint32_t s, uint64_t v) {
       L.ntrk++;
     }
   }
+  if (L.d->ackres && L.rk[s] != k) tl_add(L, s);
   L.rk[s] = k;
   if (L.rd && k != L.d->base_row[s]) L.rd[(s / CH) >> 6] |= 1ull << ((s / CH) & 63);
   L.ra[s] = aux32(v);
 }
 
 // prepareSyncDataMsg (MembershipProtocolImpl.java:446-454) + transport.send; false if the send failed
-__device__ __forceinline__ bool send_sync(ML& L, uint32_t kind, uint32_t dst, uint32_t ciss, uint32_t ccnt) {
+// res: a SYNC_ACK sent in the tick its SYNC was merged (k_ack_resolve may derive its diff from the write logs)
+__device__ __forceinline__ bool send_sync(ML& L, uint32_t kind, uint32_t dst, uint32_t ciss, uint32_t ccnt,
+                                          bool res = false) {
   const Dev& d = *L.d;
   uint32_t seq = L.syncSeq++;
   L.c[C_M]++;
@@ -175,7 +190,8 @@ __device__ __forceinline__ bool send_sync(ML& L, uint32_t kind, uint32_t dst, ui
   SyncMsg mm;
   mm.src = L.m;
   mm.dst = dst;
-  mm.kind = kind | (e > 0 ? KF_DEFER : 0u);  // a delayed one is stored at the end of the tick (k_sync_defer)
+  // a delayed one is stored at the end of the tick (k_sync_defer)
+  mm.kind = kind | (e > 0 ? KF_DEFER : (res && d.ackres && L.ntl <= TL ? KF_RES : 0u));
   mm.seq = seq;
   mm.cid_iss = ciss;
   mm.cid_cnt = ccnt;
@@ -191,6 +207,7 @@ __device__ __forceinline__ bool send_sync(ML& L, uint32_t kind, uint32_t dst, ui
   q->src = mm.src, q->dst = mm.dst, q->kind = mm.kind, q->seq = mm.seq, q->cid_iss = mm.cid_iss;
   q->cid_cnt = mm.cid_cnt, q->payload = mm.payload, q->psize = mm.psize, q->ncand = mm.ncand, q->pad = mm.pad;
   q->due = L.k + d.lat + (uint32_t)e;
+  q->tln = L.ntl;
   L.pend = i;
   if (e > 0) return true;  // not linked to the receiver's inbound list before its delivery tick
   // the receiver's inbound list for the next tick (sharded handles build it when the exchange commits the list);
@@ -496,7 +513,7 @@ __device__ __forceinline__ void complete_group(ML& L, int g) {
   G[5] = 0;
   if (kind == 0) {
     // onSync doOnSuccess (MembershipProtocolImpl.java:351-365): SYNC_ACK with the post-merge table
-    if (!(flags & GF_ERROR)) send_sync(L, K_SYNC_ACK, G[1], G[2], G[3]);
+    if (!(flags & GF_ERROR)) send_sync(L, K_SYNC_ACK, G[1], G[2], G[3], g == L.rgrp);
   } else {
     // start0 doFinally (:244-248): schedulePeriodicSync
     L.initFlags &= ~INIT_ACTIVE;
@@ -853,6 +870,7 @@ __device__ __forceinline__ void do_sync(ML& L) {
 // updateMembership (:462-464)
 __device__ __forceinline__ void merge_record(ML& L, uint32_t s, uint32_t k1, uint32_t reason, int g) {
   if ((k1 & 3u) == ST_ABSENT || k1 == L.rk[s]) return;
+  if (L.d->ackres) tl_add(L, s);
   const uint64_t key = key34(k1);
   update_membership(L, s, rec_status(key), rec_inc(key), reason, g);
 }
@@ -1085,6 +1103,10 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   L.nlog = 0;
   L.spq = d.spq + li * SPQ * 8;
   L.nsp = 0;
+  L.tl = d.ackres ? d.tlog + ((size_t)(k & 1) * d.NL + li) * TL : nullptr;
+  L.ntl = 0;
+  L.tlast = NEVER;
+  L.rgrp = -1;
   // SWIM_EXP & 16 (timing experiment): shader cycles per phase summed over members, ctr[8..12]
   // SWIM_EXP & 128: the largest per-member cycles of each phase instead (which phase makes the longest lane)
   const bool prof = (d.exp & (16 | 128)) != 0;
@@ -1199,6 +1221,8 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
         last = best;
       }
       SyncMsg mm = d.msgs[pb][mi];
+      const uint32_t mflags = mm.kind & KF_FLAGS;
+      mm.kind &= ~KF_FLAGS;
       if (mc_group(d, mm.src) != mc_group(d, m)) continue;  // checkSyncGroup (:320-321,431-437): another group's data
       // one merge_payload / finish site for the three cases (each inlined copy is large)
       int g = -1;
@@ -1220,7 +1244,10 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
       merge_payload(L, mi, reason, g);
       if (grouped && g >= 0) {
         grp(L, g)[5] |= GF_SEALED;
+        // its SYNC_ACK, if sent now, may be resolved unless the payload lacked records this row holds or came late
+        L.rgrp = (mm.kind == K_SYNC && !(mflags & (KF_ABS | KF_LATE))) ? g : -1;
         finish(L, g, false);
+        L.rgrp = -1;
       }
     }
     L.trk_on = false;
@@ -1407,6 +1434,10 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
     d.nfetch[m] = L.nfetch;
     d.fnext[m] = L.fnext;
     d.next_evt[m] = NEVER;
+    if (L.ntl) {
+      d.tl_n[(size_t)(k & 1) * d.NL + li] = L.ntl;
+      d.tl_tick[(size_t)(k & 1) * d.NL + li] = k;
+    }
     for (int i = 0; i < 8; ++i) cnt[i] += L.c[i];
     return;
   }
@@ -1598,6 +1629,10 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   d.remoteIdx[m] = L.remoteIdx;
   for (int i = 0; i < 8; ++i) d.sel[(size_t)m * 8 + i] = L.sel[i];
   d.evHash[m] = L.evHash;
+  if (L.ntl) {  // (no entry this tick: the stale tick stamp reads as an empty log)
+    d.tl_n[(size_t)(k & 1) * d.NL + li] = L.ntl;
+    d.tl_tick[(size_t)(k & 1) * d.NL + li] = k;
+  }
   for (int i = 0; i < 8; ++i) cnt[i] += L.c[i];
 }
 

@@ -103,6 +103,7 @@ class SwimCounters(C.Structure):
         ("diff_launches", C.c_uint64),
         ("exchange_ns", C.c_uint64),
         ("diff_msgs", C.c_uint64),
+        ("ack_resolved", C.c_uint64),
     ]
 
     def as_dict(self):

@@ -437,7 +437,9 @@ def test_sampled_diff_accounting(oracle, engine, profile_all):
     c = e.counters()
     assert c["sync_merges"] == o.counters()["sync_merges"]
     assert c["diff_launches"] - b["diff_launches"] == (60 if profile_all else 12)
-    assert c["diff_msgs"] - b["diff_msgs"] == want
+    # (SYNC_ACKs resolved from the write logs are merged without being streamed, k_ack_resolve)
+    assert c["diff_msgs"] + c["ack_resolved"] - b["diff_msgs"] - b["ack_resolved"] == want
+    assert c["ack_resolved"] > b["ack_resolved"]
     assert c["diff_ns"] > b["diff_ns"]
     e.close()
 
