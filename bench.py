@@ -287,7 +287,8 @@ def main():
             "device_bytes": ctr["device_bytes"],
             # since the handle was created (warm-up included): a profiler pass over the whole process prices its
             # k_sync_diff traffic against 8 B x N x these merges (tools/make_profiles.py)
-            "run_totals": {"sync_merges": ctr["sync_merges"], "ticks": ctr["tick"]},
+            "run_totals": {"sync_merges": ctr["sync_merges"], "ack_resolved": ctr.get("ack_resolved_total", 0),
+                           "ticks": ctr["tick"]},
             "exchange_ms_per_step": d["exchange_ns"] * 1e-6 / a.steps,
         }
         if a.workload not in ("c3",):  # the gossip plane dominates: whole-step algorithmic bytes against HBM

@@ -153,6 +153,7 @@ typedef struct swim_counters {
   uint64_t exchange_ns; /* sharded handles: host time spent in the per-tick shard exchanges */
   uint64_t diff_msgs;   /* SYNC / SYNC_ACK payloads streamed by the timed k_sync_diff launches (diff_launches) */
   uint64_t ack_resolved; /* SYNC_ACK payloads of those ticks resolved from write logs instead (one GPU; k_ack_resolve) */
+  uint64_t ack_resolved_total; /* the same over every tick (payloads streamed = those merged minus these) */
 } swim_counters;
 
 typedef struct swim_handle swim_handle;

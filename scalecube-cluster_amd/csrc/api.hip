@@ -1814,6 +1814,7 @@ int swim_counters_get(swim_handle* h, swim_counters* out) {
   out->diff_launches = h->prof_diff_launches;
   out->diff_msgs = c[C_DIFFMSG];
   out->ack_resolved = c[C_ACKRES];
+  out->ack_resolved_total = c[C_ACKRES_ALL];
   out->exchange_ns = (uint64_t)(h->xchg_ms * 1e6);
   return SWIM_OK;
 }

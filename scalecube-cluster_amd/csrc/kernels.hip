@@ -504,6 +504,7 @@ __global__ void __launch_bounds__(256) k_ack_resolve(Dev d, uint32_t b, uint32_t
       cm[1] = off == NEVER ? 0u : in;
     }
     if (lane == 0) d.msgs[b][i].ncand = off == NEVER ? 0u : total;
+    if (lane == 0) atomicAdd(&d.ctr[C_ACKRES_ALL], 1ull);
     if (lane == 0 && timed) atomicAdd(&d.ctr[C_ACKRES], 1ull);
     __builtin_amdgcn_wave_barrier();
   }
@@ -620,10 +621,12 @@ void launch_init(const Dev& d, void* stream) {
 
 // timed: this launch is bracketed by profiling events; it adds its message count to ctr[C_DIFFMSG]
 static void launch_sync_diff(const Dev& d, uint32_t b, hipStream_t st, uint32_t timed, uint32_t spec = 0) {
+  // 8 resident blocks per CU; SWIM_DIFF_GRID overrides it (measurements)
+  static const uint32_t grid = getenv("SWIM_DIFF_GRID") ? (uint32_t)atoi(getenv("SWIM_DIFF_GRID")) : 2048u;
   if (d.W > 1)
-    hipLaunchKernelGGL(k_sync_diff<true>, dim3(2048), dim3(256), 0, st, d.self, b, timed, spec);
+    hipLaunchKernelGGL(k_sync_diff<true>, dim3(grid), dim3(256), 0, st, d.self, b, timed, spec);
   else
-    hipLaunchKernelGGL(k_sync_diff<false>, dim3(2048), dim3(256), 0, st, d.self, b, timed, spec);
+    hipLaunchKernelGGL(k_sync_diff<false>, dim3(grid), dim3(256), 0, st, d.self, b, timed, spec);
 }
 
 // single GPU: the tick is cut in three so that the host can hold back the gossip data plane when no slot is in

@@ -42,12 +42,14 @@ bench = json.loads((src / "bench.json").read_text())
 n = bench["config"]["members"]
 fm, wm = statistics.median(fetch), statistics.median(write)
 # like-for-like: every k_sync_diff launch of the two PMC passes against the algorithmic bytes of those same launches
-# (8 B x N x the payloads merged over each pass's whole run, warm-up included)
+# (8 B x N x the payloads streamed over each pass's whole run, warm-up included)
 tf, tw = pass_totals("pmc_fetch"), pass_totals("pmc_write")
 ratio = None
 if tf and tw:
     measured = 2 * sum(fetch_all) * 1024 + sum(write_all) * 1024  # one FETCH pass + one WRITE pass (same schedule)
-    algo = 8.0 * n * (tf["sync_merges"] + tw["sync_merges"]) / 2
+    # (SYNC_ACKs resolved from write logs are merged without being streamed: k_ack_resolve)
+    streamed = lambda t: t["sync_merges"] - t.get("ack_resolved", 0)
+    algo = 8.0 * n * (streamed(tf) + streamed(tw)) / 2
     ratio = measured / algo
 out = {
     "round": int(tag[1:]),
