@@ -439,74 +439,113 @@ __global__ void __launch_bounds__(256) k_sync_diff(const Dev* __restrict__ dp, u
 // logs (tl_add: every key change and every merged candidate) can differ; they are tested here, in subject order,
 // into the same pool / chunk_meta form k_sync_diff writes. A message that cannot be resolved this way (no KF_RES, a
 // log past TL, a pinned live-row payload, a delayed one) goes to dlist for k_sync_diff. One wave per message.
-__global__ void __launch_bounds__(256) k_ack_resolve(Dev d, uint32_t b, uint32_t k, uint32_t spec, uint32_t timed) {
+// the fields k_ack_resolve reads, passed as kernel arguments: through Dev* every one of them was a dependent load of
+// its own before the loads that use it (the kernel is a chain of short dependent loads)
+struct ResArgs {
+  const uint32_t *halt, *nmsg, *tl_tick, *tl_n, *tlog, *rowk, *arena;
+  SyncMsg* msgs;
+  uint32_t *dlist, *ndl, *chunk_meta, *pool_used, *err;
+  uint64_t* pool;
+  unsigned long long* ctr;
+  uint32_t NL, NS, MSGCAP, NCHUNK, POOLCAP;
+};
+__global__ void __launch_bounds__(512) k_ack_resolve(ResArgs d, uint32_t k, uint32_t spec, uint32_t timed) {
   if (spec && *(volatile uint32_t*)d.halt) return;
-  __shared__ uint32_t sv_[4][64], sc_[4][64];
-  volatile uint32_t* sv = sv_[threadIdx.x >> 6];  // this wave's lists (volatile: read across lanes)
-  volatile uint32_t* sc = sc_[threadIdx.x >> 6];
+  __shared__ uint32_t sv_[8][64], sc_[8][64];
+  __shared__ uint32_t slist[8], nstream, nres, sbase;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint32_t nmsg = min(d.nmsg[b], d.MSGCAP);
-  for (uint32_t i = blockIdx.x * 4 + wv; i < nmsg; i += gridDim.x * 4) {  // wave-uniform
-    const SyncMsg& mm = d.msgs[b][i];
-    const uint32_t kind = mm.kind, src = mm.src, dst = mm.dst, tln = mm.tln, pay = mm.payload;
-    bool res = k >= 2 && (kind & KF_RES) && !(kind & KF_DEFER) && mm.pin == NEVER && tln <= TL;
-    uint32_t n0 = 0, n1 = 0;  // A's log entries of ticks k-2 and k-1
-    if (res) {
-      const size_t a0 = (size_t)(k & 1) * d.NL + dst, a1 = (size_t)((k - 1) & 1) * d.NL + dst;
-      n0 = d.tl_tick[a0] == k - 2 ? d.tl_n[a0] : 0u;
-      n1 = d.tl_tick[a1] == k - 1 ? d.tl_n[a1] : 0u;
-      res = n0 <= TL && n1 <= TL;
-    }
-    if (!res) {
-      if (lane == 0) d.dlist[atomicAdd(d.ndl, 1u)] = i;
-      continue;
-    }
-    // gather: B's prefix, then A's two ticks (at most 3 TL <= 64 subjects, one per lane)
-    uint32_t v = NEVER;
-    if (lane < tln) v = d.tlog[((size_t)((k - 1) & 1) * d.NL + src) * TL + lane];
-    else if (lane < tln + n0) v = d.tlog[((size_t)(k & 1) * d.NL + dst) * TL + (lane - tln)];
-    else if (lane < tln + n0 + n1) v = d.tlog[((size_t)((k - 1) & 1) * d.NL + dst) * TL + (lane - tln - n0)];
-    sv[lane] = v;
-    __builtin_amdgcn_wave_barrier();
-    bool first = v != NEVER;
-    for (uint32_t j = 0; j < lane; ++j) first &= sv[j] != v;
-    uint32_t key = 0;
-    bool cand = false;
-    if (first) {
-      key = pay == NEVER ? d.rowk[(size_t)src * d.NS + v] : d.arena[b][(size_t)pay * d.NS + v];
-      cand = (key & 3u) != ST_ABSENT && key != d.rowk[(size_t)dst * d.NS + v];
-    }
-    sc[lane] = cand ? v : NEVER;
-    __builtin_amdgcn_wave_barrier();
-    uint32_t pos = 0;
-    for (uint32_t j = 0; j < 64; ++j) pos += sc[j] < v;
-    const uint32_t total = (uint32_t)__popcll(__ballot(cand));
-    uint32_t off = 0;
-    if (lane == 0 && total) {
-      off = atomicAdd(d.pool_used, total);
-      if (off + total > d.POOLCAP) {
-        atomicOr(d.err, E_POOL);
-        off = NEVER;
+  volatile uint32_t* sv = sv_[wv];  // this wave's lists (volatile: read across lanes)
+  volatile uint32_t* sc = sc_[wv];
+  const uint32_t nmsg = min(*d.nmsg, d.MSGCAP);
+  // block-uniform loop, one message per wave; the stream list and the counters take one atomic per block (a few
+  // hundred waves adding to one address one by one took ~17 us per tick at C3)
+  for (uint32_t base = blockIdx.x * 8; base < nmsg; base += gridDim.x * 8) {
+    if (threadIdx.x == 0) nstream = nres = 0;
+    __syncthreads();
+    const uint32_t i = base + wv;
+    if (i < nmsg) {  // wave-uniform
+      const SyncMsg& mm = d.msgs[i];
+      const uint32_t kind = mm.kind, src = mm.src, dst = mm.dst, tln = mm.tln, pay = mm.payload;
+      bool res = k >= 2 && (kind & KF_RES) && !(kind & KF_DEFER) && mm.pin == NEVER && tln <= TL;
+      uint32_t n0 = 0, n1 = 0;  // A's log entries of ticks k-2 and k-1
+      if (res) {
+        const size_t a0 = (size_t)(k & 1) * d.NL + dst, a1 = (size_t)((k - 1) & 1) * d.NL + dst;
+        n0 = d.tl_tick[a0] == k - 2 ? d.tl_n[a0] : 0u;
+        n1 = d.tl_tick[a1] == k - 1 ? d.tl_n[a1] : 0u;
+        res = n0 <= TL && n1 <= TL;
+      }
+      const uint32_t nall = tln + n0 + n1;
+      if (!res) {
+        if (lane == 0) slist[atomicAdd(&nstream, 1u)] = i;
+      } else if (nall == 0) {  // nothing written on either side and nothing merged: nothing can differ
+        if (lane == 0) {
+          d.msgs[i].ncand = 0;
+          atomicAdd(&nres, 1u);
+        }
+      } else {
+        // gather: B's prefix, then A's two ticks (at most 3 TL <= 64 subjects, one per lane)
+        uint32_t v = NEVER;
+        if (lane < tln) v = d.tlog[((size_t)((k - 1) & 1) * d.NL + src) * TL + lane];
+        else if (lane < tln + n0) v = d.tlog[((size_t)(k & 1) * d.NL + dst) * TL + (lane - tln)];
+        else if (lane < tln + n0 + n1) v = d.tlog[((size_t)((k - 1) & 1) * d.NL + dst) * TL + (lane - tln - n0)];
+        sv[lane] = v;
+        __builtin_amdgcn_wave_barrier();
+        bool first = v != NEVER;
+        for (uint32_t j = 0; j < min(lane, nall); ++j) first &= sv[j] != v;
+        uint32_t key = 0;
+        bool cand = false;
+        if (first) {
+          key = pay == NEVER ? d.rowk[(size_t)src * d.NS + v] : d.arena[(size_t)pay * d.NS + v];
+          cand = (key & 3u) != ST_ABSENT && key != d.rowk[(size_t)dst * d.NS + v];
+        }
+        sc[lane] = cand ? v : NEVER;
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t cb = __ballot(cand);
+        const uint32_t total = (uint32_t)__popcll(cb);
+        uint32_t off = 0;
+        if (total) {  // (wave-uniform; none in the C3 steady state)
+          uint32_t pos = 0;
+          for (uint32_t j = 0; j < nall; ++j) pos += sc[j] < v;
+          if (lane == 0) {
+            off = atomicAdd(d.pool_used, total);
+            if (off + total > d.POOLCAP) {
+              atomicOr(d.err, E_POOL);
+              off = NEVER;
+            }
+          }
+          off = __shfl(off, 0);
+          if (cand && off != NEVER) d.pool[(size_t)off + pos] = ((uint64_t)v << 34) | key34(key);
+        }
+        // per chunk: first candidate and count (the chunk walk of merge_payload, which reads none of it when ncand is 0)
+        if (total && off != NEVER)
+          for (uint32_t c = lane; c < d.NCHUNK; c += 64) {
+            uint32_t before = 0, in = 0;
+            for (uint32_t j = 0; j < nall; ++j) {
+              const uint32_t t = sc[j];
+              before += t < c * CH;
+              in += t != NEVER && t / CH == c;
+            }
+            uint32_t* cm = d.chunk_meta + ((size_t)i * d.NCHUNK + c) * 2;
+            cm[0] = off + before;
+            cm[1] = in;
+          }
+        if (lane == 0) {
+          d.msgs[i].ncand = off == NEVER ? 0u : total;
+          atomicAdd(&nres, 1u);
+        }
       }
     }
-    off = __shfl(off, 0);
-    if (cand && off != NEVER) d.pool[(size_t)off + pos] = ((uint64_t)v << 34) | key34(key);
-    // per chunk: first candidate and count (the chunk walk of merge_payload)
-    for (uint32_t c = lane; c < d.NCHUNK; c += 64) {
-      uint32_t before = 0, in = 0;
-      for (uint32_t j = 0; j < 64; ++j) {
-        const uint32_t t = sc[j];
-        before += t < c * CH;
-        in += t != NEVER && t / CH == c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      if (nstream) sbase = atomicAdd(d.ndl, nstream);
+      if (nres) {
+        atomicAdd(&d.ctr[C_ACKRES_ALL], (unsigned long long)nres);
+        if (timed) atomicAdd(&d.ctr[C_ACKRES], (unsigned long long)nres);
       }
-      uint32_t* cm = d.chunk_meta + ((size_t)i * d.NCHUNK + c) * 2;
-      cm[0] = off == NEVER ? 0u : off + before;
-      cm[1] = off == NEVER ? 0u : in;
     }
-    if (lane == 0) d.msgs[b][i].ncand = off == NEVER ? 0u : total;
-    if (lane == 0) atomicAdd(&d.ctr[C_ACKRES_ALL], 1ull);
-    if (lane == 0 && timed) atomicAdd(&d.ctr[C_ACKRES], 1ull);
-    __builtin_amdgcn_wave_barrier();
+    __syncthreads();
+    if (threadIdx.x < nstream) d.dlist[sbase + threadIdx.x] = slist[threadIdx.x];
+    __syncthreads();  // (slist and the counts are reused)
   }
 }
 
@@ -633,8 +672,12 @@ static void launch_sync_diff(const Dev& d, uint32_t b, hipStream_t st, uint32_t 
 // use; the SYNC diff of tick k+1 does not depend on the gossip plane of tick k and is queued in between
 void launch_diff(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool spec) {
   hipStream_t st = (hipStream_t)stream;
-  if (k > 0 && d.ackres)
-    hipLaunchKernelGGL(k_ack_resolve, dim3(256), dim3(256), 0, st, d, (k - 1) & 1, k, spec ? 1u : 0u, prof ? 1u : 0u);
+  if (k > 0 && d.ackres) {
+    const uint32_t b = (k - 1) & 1;
+    const ResArgs ra{d.halt, d.nmsg + b, d.tl_tick, d.tl_n, d.tlog, d.rowk, d.arena[b], d.msgs[b], d.dlist, d.ndl,
+                     d.chunk_meta, d.pool_used, d.err, d.pool, d.ctr, d.NL, d.NS, d.MSGCAP, d.NCHUNK, d.POOLCAP};
+    hipLaunchKernelGGL(k_ack_resolve, dim3(128), dim3(512), 0, st, ra, k, spec ? 1u : 0u, prof ? 1u : 0u);
+  }
   if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
   if (k > 0) launch_sync_diff(d, (k - 1) & 1, st, prof ? 1u : 0u, spec ? 1u : 0u);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
