@@ -14,8 +14,8 @@ from parity_util import run_lockstep
 
 pytestmark = pytest.mark.gpu
 
-# SYNC every 3 ticks at 300 ms: many SYNC / SYNC_ACK pairs per tick, and receivers with several payloads
-FAST_SYNC = ClusterConfig(syncInterval=300)
+# SYNC every 10 ticks: many SYNC / SYNC_ACK pairs per tick, and receivers with several payloads
+FAST_SYNC = ClusterConfig(syncInterval=1000)
 
 
 def faults(c, phase):
@@ -33,7 +33,7 @@ def faults(c, phase):
 
 
 def test_ack_resolution_parity_under_faults(oracle, engine):
-    cfg = SimConfig(n_members=160, cluster=FAST_SYNC, delay_cap_ms=400)
+    cfg = SimConfig(n_members=160, cluster=FAST_SYNC, delay_cap_ms=400, gossip_slot_cap=1 << 16)
     o, e = SimulatedCluster(oracle, cfg), SimulatedCluster(engine, dataclasses.replace(cfg, profile_all=True))
     for phase in range(3):
         for c in (o, e):
@@ -48,7 +48,7 @@ def test_ack_resolution_parity_under_faults(oracle, engine):
 
 
 def test_ack_resolution_equals_streaming(engine):
-    cfg = SimConfig(n_members=400, cluster=FAST_SYNC)
+    cfg = SimConfig(n_members=400, cluster=FAST_SYNC, gossip_slot_cap=1 << 16)
     runs = []
     for off in (False, True):
         if off:
