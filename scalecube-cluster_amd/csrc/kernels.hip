@@ -299,9 +299,13 @@ __global__ void __launch_bounds__(256) k_seg_sort(uint64_t* key, uint32_t* val, 
 // is the sender's live row or its copy-on-write snapshot; for a payload received from another shard, the shipped
 // chunk if it differs from the baseline, else the baseline
 template <bool SHARDED>
-__device__ __forceinline__ void diff_fetch(const Dev& d, uint32_t b, uint32_t mi, uint32_t c, uint4 (&x)[4]) {
+// pinw: the arena row a live-row payload is copied into while it streams (pin_msg), else NEVER; loaded here with the
+// item's data so that no dependent load of the message waits at the top of the item's iteration
+__device__ __forceinline__ void diff_fetch(const Dev& d, uint32_t b, uint32_t mi, uint32_t c, uint4 (&x)[4],
+                                           uint32_t& pinw) {
   const SyncMsg& mm = d.msgs[b][mi];
   const uint32_t s0 = c * CH + threadIdx.x * 8;
+  pinw = NEVER;
   // NS is a multiple of 8: a 32-B group is wholly in or out; padding entries are 0 (absent). A delayed message
   // (KF_DEFER) is merged in a later tick: nothing to compare now
   if (s0 >= d.NS || (mm.kind & KF_DEFER)) {
@@ -310,6 +314,7 @@ __device__ __forceinline__ void diff_fetch(const Dev& d, uint32_t b, uint32_t mi
   }
   const uint32_t* p8;
   if (mm.payload == NEVER) {
+    pinw = mm.pin;
     p8 = d.rowk + lidx(d, mm.src) * d.NS + s0;
   } else if (SHARDED && (mm.payload & PAY_RX)) {
     const uint32_t ri = mm.payload & ~PAY_RX;
@@ -356,22 +361,22 @@ __global__ void __launch_bounds__(256) k_sync_diff(const Dev* __restrict__ dp, u
   const uint32_t* dlp = dl ? d.dlist : nullptr;
   const uint32_t nch = d.NCHUNK;
   uint4 cur[4];
-  uint32_t mcur = 0;
+  uint32_t mcur = 0, pcur = NEVER;
   if (blockIdx.x < total) {
     mcur = dlp ? dlp[blockIdx.x / nch] : blockIdx.x / nch;
-    diff_fetch<SHARDED>(d, b, mcur, blockIdx.x % nch, cur);
+    diff_fetch<SHARDED>(d, b, mcur, blockIdx.x % nch, cur, pcur);
   }
   for (uint32_t w = blockIdx.x; w < total; w += gridDim.x) {
     uint4 nxt[4];
-    uint32_t mnxt = 0;
+    uint32_t mnxt = 0, pnxt = NEVER;
     if (w + gridDim.x < total) {
       mnxt = dlp ? dlp[(w + gridDim.x) / nch] : (w + gridDim.x) / nch;
-      diff_fetch<SHARDED>(d, b, mnxt, (w + gridDim.x) % nch, nxt);
+      diff_fetch<SHARDED>(d, b, mnxt, (w + gridDim.x) % nch, nxt, pnxt);
     }
     const uint32_t mi = mcur, c = w % nch;
     const uint32_t s0 = c * CH + threadIdx.x * 8;
-    const uint32_t pin = d.msgs[b][mi].pin;
-    if (pin != NEVER && d.msgs[b][mi].payload == NEVER && s0 < d.NS) {  // a live-row payload read again later (pin_msg)
+    const uint32_t pin = pcur;
+    if (pin != NEVER && s0 < d.NS) {  // a live-row payload read again later (pin_msg)
       uint4* dst = (uint4*)(d.arena[b] + (size_t)pin * d.NS + s0);
       dst[0] = cur[0];
       dst[1] = cur[1];
@@ -427,6 +432,7 @@ __global__ void __launch_bounds__(256) k_sync_diff(const Dev* __restrict__ dp, u
 #pragma unroll
     for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
     mcur = mnxt;
+    pcur = pnxt;
   }
 }
 
