@@ -154,6 +154,7 @@ typedef struct swim_counters {
   uint64_t diff_msgs;   /* SYNC / SYNC_ACK payloads streamed by the timed k_sync_diff launches (diff_launches) */
   uint64_t ack_resolved; /* SYNC_ACK payloads of those ticks resolved from write logs instead (one GPU; k_ack_resolve) */
   uint64_t ack_resolved_total; /* the same over every tick (payloads streamed = those merged minus these) */
+  uint64_t diff_msgs_total;    /* SYNC / SYNC_ACK payloads streamed by every k_sync_diff launch (timed or not) */
 } swim_counters;
 
 typedef struct swim_handle swim_handle;

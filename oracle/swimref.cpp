@@ -1419,11 +1419,23 @@ __attribute__((visibility("default"))) int swim_read_row(swim_handle* h, uint32_
   return SWIM_OK;
 }
 
+static void state_hash_range(swim_handle* h, uint64_t* out, uint32_t lo, uint32_t hi);
 __attribute__((visibility("default"))) int swim_state_hash(swim_handle* h, uint64_t* out, size_t cap) {
   if (!h || cap < 6ull * h->sim.N) return SWIM_EINVAL;
   Sim& s = h->sim;
+  // read-only per member: SWIMREF_THREADS workers over member ranges (the full-size parity tests hash 10^5 rows)
+  const uint32_t nth = (uint32_t)std::max(1, std::min<int>(s.threads, (int)(s.N / 64) + 1));
+  std::vector<std::thread> th;
+  for (uint32_t t = 0; t < nth; ++t)
+    th.emplace_back([&, t] { state_hash_range(h, out, (uint32_t)((uint64_t)t * s.N / nth), (uint32_t)((uint64_t)(t + 1) * s.N / nth)); });
+  for (auto& x : th) x.join();
+  return SWIM_OK;
+}
+
+static void state_hash_range(swim_handle* h, uint64_t* out, uint32_t lo, uint32_t hi) {
+  Sim& s = h->sim;
   std::vector<uint64_t> row(s.N);
-  for (uint32_t m = 0; m < s.N; ++m) {
+  for (uint32_t m = lo; m < hi; ++m) {
     const Member& mb = s.members[m];
     swim_read_row(h, m, row.data(), s.N);
     uint64_t hr = 0;
@@ -1443,7 +1455,6 @@ __attribute__((visibility("default"))) int swim_state_hash(swim_handle* h, uint6
     out[6 * m + 4] = hgs;
     out[6 * m + 5] = misc;
   }
-  return SWIM_OK;
 }
 
 // include/swimhip_selftest.h: the oracle's own functions on caller inputs (the engine runs its device code)

@@ -387,6 +387,15 @@ int build(swim_handle* h) {
     h->err = "gossipRepeatMult x ceilLog2(members) too large (at most 248)";
     return SWIM_EINVAL;
   }
+  // 16-bit holder entries (engine.h S16_*): a gossip slot may stay in use SLIFE ticks. Its holders sweep it EXPB
+  // ticks after their receipt, and an epidemic's first receipts come within about maxSpread + 1 rounds of its
+  // creation, so a slot lives about (3 maxSpread + 6) gossip intervals. A config whose gossip interval is so many
+  // ticks that this reaches SLIFE is refused here instead of failing with E_SLIFE mid-run
+  if ((3ull * maxSpread + 6ull) * d.gossip_t >= SLIFE) {
+    h->err = "gossipInterval / tick_ms x (3 x gossipRepeatMult x ceilLog2(members) + 6) must stay below " +
+             std::to_string(SLIFE) + " ticks (the holder entries' tick window): use a coarser tick_ms";
+    return SWIM_EINVAL;
+  }
   // receipt ring per member: at least as many entries as the member can hold gossips; by default the slot table's
   // size, within about 16-24 GB in all (C2 holds ~3·10^5 gossips per member at 10k members), and
   // swim_config.gossip_ring_cap overrides (a full ring raises E_RING)
@@ -1815,6 +1824,7 @@ int swim_counters_get(swim_handle* h, swim_counters* out) {
   out->diff_msgs = c[C_DIFFMSG];
   out->ack_resolved = c[C_ACKRES];
   out->ack_resolved_total = c[C_ACKRES_ALL];
+  out->diff_msgs_total = c[C_DIFFMSG_ALL];
   out->exchange_ns = (uint64_t)(h->xchg_ms * 1e6);
   return SWIM_OK;
 }

@@ -81,7 +81,7 @@ constexpr uint32_t XINL = 16384;  // RCCL: bytes per peer moved by the fixed-siz
 
 // counters (swim_counters order after .tick)
 // 8..12: SWIM_EXP & 4 (and 16..19: the gossip plane's work units per tick, for algorithmic bytes; tools/pmc_gossip.py)
-enum Ctr { C_R = 0, C_W, C_M, C_G, C_E, C_LOST, C_GCREATED, C_SYNCMERGE, C_DIFFMSG = 13, C_XU = 16, C_ACKRES = 24, C_ACKRES_ALL = 25, C_NCTR = 26 };
+enum Ctr { C_R = 0, C_W, C_M, C_G, C_E, C_LOST, C_GCREATED, C_SYNCMERGE, C_DIFFMSG = 13, C_XU = 16, C_ACKRES = 24, C_ACKRES_ALL = 25, C_DIFFMSG_ALL = 26, C_NCTR = 27 };
 
 // capacity fallbacks that fired (include/swimhip_debug.h; counted only when Dev::fb is allocated: SWIM_CAPS or
 // SWIM_FALLBACKS set at create). Each one is an exact slow path taken when a fixed-capacity fast structure is full.

@@ -298,9 +298,9 @@ __global__ void __launch_bounds__(256) k_seg_sort(uint64_t* key, uint32_t* val, 
 // this lane's 8 payload keys and 8 receiver keys of work item w (message w / NCHUNK, chunk w % NCHUNK): the payload
 // is the sender's live row or its copy-on-write snapshot; for a payload received from another shard, the shipped
 // chunk if it differs from the baseline, else the baseline
-template <bool SHARDED>
 // pinw: the arena row a live-row payload is copied into while it streams (pin_msg), else NEVER; loaded here with the
 // item's data so that no dependent load of the message waits at the top of the item's iteration
+template <bool SHARDED>
 __device__ __forceinline__ void diff_fetch(const Dev& d, uint32_t b, uint32_t mi, uint32_t c, uint4 (&x)[4],
                                            uint32_t& pinw) {
   const SyncMsg& mm = d.msgs[b][mi];
@@ -356,7 +356,10 @@ __global__ void __launch_bounds__(256) k_sync_diff(const Dev* __restrict__ dp, u
   // with SYNC_ACK resolution, only the messages k_ack_resolve left in dlist
   const bool dl = !SHARDED && d.ackres;
   uint32_t nmsg = dl ? *(volatile uint32_t*)d.ndl : (d.nmsg[b] < d.MSGCAP ? d.nmsg[b] : d.MSGCAP);
-  if (timed && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&d.ctr[C_DIFFMSG], (unsigned long long)nmsg);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    atomicAdd(&d.ctr[C_DIFFMSG_ALL], (unsigned long long)nmsg);
+    if (timed) atomicAdd(&d.ctr[C_DIFFMSG], (unsigned long long)nmsg);
+  }
   uint32_t total = nmsg * d.NCHUNK;
   const uint32_t* dlp = dl ? d.dlist : nullptr;
   const uint32_t nch = d.NCHUNK;
@@ -666,8 +669,12 @@ void launch_init(const Dev& d, void* stream) {
 
 // timed: this launch is bracketed by profiling events; it adds its message count to ctr[C_DIFFMSG]
 static void launch_sync_diff(const Dev& d, uint32_t b, hipStream_t st, uint32_t timed, uint32_t spec = 0) {
-  // 8 resident blocks per CU; SWIM_DIFF_GRID overrides it (measurements)
-  static const uint32_t grid = getenv("SWIM_DIFF_GRID") ? (uint32_t)atoi(getenv("SWIM_DIFF_GRID")) : 2048u;
+  // 8 resident blocks per CU; SWIM_DIFF_GRID overrides it (measurements; a value that does not parse, or 0, keeps 2048)
+  static const uint32_t grid = [] {
+    const char* e = getenv("SWIM_DIFF_GRID");
+    const unsigned long v = e ? strtoul(e, nullptr, 0) : 0ul;
+    return v >= 1 && v <= (1ul << 20) ? (uint32_t)v : 2048u;
+  }();
   if (d.W > 1)
     hipLaunchKernelGGL(k_sync_diff<true>, dim3(grid), dim3(256), 0, st, d.self, b, timed, spec);
   else

@@ -105,6 +105,7 @@ class SwimCounters(C.Structure):
         ("diff_msgs", C.c_uint64),
         ("ack_resolved", C.c_uint64),
         ("ack_resolved_total", C.c_uint64),
+        ("diff_msgs_total", C.c_uint64),
     ]
 
     def as_dict(self):

@@ -56,6 +56,16 @@ def _c4_long():  # C4's full schedule at 300 members: partition from period 0, h
         ("partition", g), ("periods", 200), ("unblock", None), ("periods", 40)]
 
 
+def _c4_large():  # C4's full schedule (BASELINE configs[3]) at 1 000 members: partition from period 0, unblockAll at
+    # period 200, run to period 320 (4 SYNC rounds past the heal). Recorded once (SWIMREF_THREADS=8 python
+    # tests/golden/make_golden.py c4_large); replayed on 1 and 2 shards by the GPU suite
+    n = 1000
+    g = [0] * (n // 2) + [1] * (n // 2)
+    return SimConfig(n_members=n, cluster=ClusterConfig(seedMembers=[0]), gossip_slot_cap=1 << 19, pending_fetch_cap=4096,
+                     list_slack=4096), [
+        ("partition", g), ("periods", 200), ("unblock", None), ("periods", 120)]
+
+
 def _c3_small():  # C3-shaped: steady state SYNC / SYNC_ACK anti-entropy, no loss
     return SimConfig(n_members=1000), [("periods", 35)]
 
@@ -65,8 +75,8 @@ def _c5_small():  # C5-shaped: rumor-only dissemination with 1 % churn per perio
 
 
 SCENARIOS = {"c1": _c1, "c2_small": _c2_small, "c4_small": _c4_small, "c3_small": _c3_small, "c5_small": _c5_small,
-             "c4_mid": _c4_mid, "c2_mid": _c2_mid, "c4_long": _c4_long}
-SLOW_ON_ORACLE = {"c4_mid", "c2_mid", "c4_long"}  # recorded once; replaying it on the oracle takes minutes
+             "c4_mid": _c4_mid, "c2_mid": _c2_mid, "c4_long": _c4_long, "c4_large": _c4_large}
+SLOW_ON_ORACLE = {"c4_mid", "c2_mid", "c4_long", "c4_large"}  # recorded once; replaying it on the oracle takes minutes
 FULL_EVENTS = {"c1"}
 
 

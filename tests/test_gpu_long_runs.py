@@ -34,3 +34,24 @@ def test_full_long_run_slot_reuse(oracle, engine):
     run_lockstep(o, e, 6_000, 1_000, "full, kill + update", events=False)  # (per-member event hashes compared)
     e.close()
     o.close()
+
+
+def test_fine_tick_long_run(oracle, engine):
+    """A 10 ms tick (gossip interval = 20 ticks, so a slot's lifetime is ~2 000 ticks of the 4 096 its 16-bit holder
+    entries allow): slots recycled over 24 000 ticks, bit-exact."""
+    cfg = SimConfig(n_members=150, mode=_abi.MODE_RUMOR, churn_per_period=6, gossip_slot_cap=1024, tick_ms=10)
+    o, e = pair(oracle, engine, cfg)
+    for c in (o, e):
+        c.set_default_loss(5)
+    run_lockstep(o, e, 24_000, 4_000, "rumor, 10 ms ticks", events=False)
+    assert o.counters()["gossips_created"] > 1024  # every slot reused
+    e.close()
+    o.close()
+
+
+def test_tick_window_refused_at_create(engine):
+    """tick_ms = 1 with the default 200 ms gossip interval: a gossip would live ~20 000 ticks, past the holder entries'
+    4 096-tick window, so swim_create refuses the config instead of failing mid-run with E_SLIFE."""
+    from swimhip import SimulatedCluster
+    with pytest.raises(Exception, match=f"rc={_abi.SWIM_EINVAL}"):
+        SimulatedCluster(engine, SimConfig(n_members=100, tick_ms=1))

@@ -1,0 +1,60 @@
+# The one GPU runner (run through gpurun from the repository root): each argument is a step, run in order under its
+# own time limit; the first failing step ends the call (no GPU step runs after a fault, abort or time limit).
+#   suite[:EXPR]      -m gpu tests (optionally -k EXPR), log in $O/tests.log
+#   smoke             __graft_entry__.smoke()
+#   bench:W[:S[:WU]]  bench.py --workload W (c3 | c3dyn | c2 | c5), S steps, WU warm-up, no CPU baseline
+#   benchcpu          the default bench line with its CPU baseline (the driver's command)
+#   trace:W[:S[:WU]]  rocprofv3 kernel trace + stats of the same bench command, and its per-tick breakdown
+#   pmc:W:COUNTER     one rocprofv3 --pmc pass (one counter group) over a short bench run of workload W
+# Example:  gpurun --timeout 1200 -- 'bash tools/gpu_run.sh r4a suite:fullsize smoke bench:c3'
+set -e
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/$1
+shift
+mkdir -p $O
+for step in "$@"; do
+  IFS=: read -r what a b c <<< "$step"
+  echo "== $step $(date +%T)"
+  case $what in
+    suite)
+      k=()
+      [ -n "$a" ] && k=(-k "$a")
+      rc=0
+      timeout -k 10 1100 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread -p no:cacheprovider \
+        "${k[@]}" > $O/tests.log 2>&1 || rc=$?
+      tail -n 1 $O/tests.log
+      grep -E "^FAILED|^ERROR" $O/tests.log | head -30 || true
+      [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc  # 1 = test failures (listed above); anything else ends the call
+      ;;
+    smoke)
+      timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+      tail -1 $O/smoke.log
+      ;;
+    bench)
+      timeout -k 10 400 python -u bench.py --workload $a --steps ${b:-20} --warmup ${c:-3} --no-cpu-baseline \
+        > $O/bench_$a.log 2>&1
+      grep metric $O/bench_$a.log > $O/bench_$a.json
+      grep -o '"ms_per_step": [0-9.]*' $O/bench_$a.json
+      ;;
+    benchcpu)
+      timeout -k 10 600 python -u bench.py > $O/bench.log 2>&1
+      grep metric $O/bench.log > $O/bench.json
+      grep -o '"ms_per_step": [0-9.]*\|"frac": [0-9.]*' $O/bench.json
+      ;;
+    trace)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/t_$a -o run --output-format csv -- \
+        python3 bench.py --workload $a --steps ${b:-5} --warmup ${c:-3} --no-cpu-baseline > $O/trace_$a.log 2>&1
+      python3 tools/tick_breakdown.py $O/t_$a/run_kernel_trace.csv 10 | tail -3
+      ;;
+    pmc)
+      timeout -s KILL 300 rocprofv3 --pmc $b -d $O/pmc_${a}_$b -o run --output-format csv -- \
+        python3 bench.py --workload $a --steps 3 --warmup 1 --no-cpu-baseline > $O/pmc_${a}_$b.log 2>&1
+      ;;
+    *)
+      echo "unknown step $step"
+      exit 2
+      ;;
+  esac
+done
+echo "== done $(date +%T)"
