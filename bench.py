@@ -80,6 +80,18 @@ def traffic_from_profiles(n_members):
     return None
 
 
+def whole_step_pmc(workload, n_members):
+    """Whole-step HBM bytes per period from a committed PMC summary (tools/make_profiles.py wholestep), if present."""
+    f = ROOT / "profiles" / "pmc_whole_step.json"
+    try:
+        d = json.loads(f.read_text()).get(workload)
+        if d and d.get("members") == n_members:
+            return {"bytes": d["bytes_per_period"], "source": f"profiles/pmc_whole_step.json ({d['round']})"}
+    except Exception:
+        pass
+    return None
+
+
 def mem_available():
     try:
         for line in open("/proc/meminfo"):
@@ -253,8 +265,14 @@ def main():
         timed_msgs = d["diff_msgs"] if world == 1 else merges
         bytes_per_launch = 8.0 * n * timed_msgs / launches  # payload keys + receiver keys, 4 B each per subject
         achieved = (8.0 * n * timed_msgs) / diff_s / 1e9 if diff_s > 0 else 0.0
-        # whole-step algorithmic bytes, SURVEY.md §8d with 4-B record keys: B = 8R + 8W + 32M + 0.375G + 24E
-        B = 8 * d["record_compares"] + 8 * d["row_writes"] + 32 * d["messages"] + 0.375 * d["gossip_messages"] + 24 * d["events"]
+        # whole-step algorithmic bytes, SURVEY.md §8d with 4-B record keys (B = 8R + 8W + 32M + 0.375G + 24E), with R's
+        # SYNC part priced as the engine reads it: 8 B x N per payload k_sync_diff streamed, and for a SYNC_ACK
+        # resolved from write logs (k_ack_resolve) at most 3 x 16 subjects x 8 B; every other record compare at 8 B.
+        # (R counts the sender's table size per merged payload, N in these preconverged workloads.)
+        streamed, resolved = d["diff_msgs_total"], d["ack_resolved_total"]
+        r_other = max(0, d["record_compares"] - n * merges)
+        B = (8 * n * streamed + 8 * 48 * resolved + 8 * r_other + 8 * d["row_writes"] + 32 * d["messages"]
+             + 0.375 * d["gossip_messages"] + 24 * d["events"])
         line = {
             "metric": "member·periods/sec at 100k members (whole node); achieved HBM GB/s",
             "value": n * a.steps / dt,
@@ -278,12 +296,18 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                          "algorithmic_bytes_per_launch": bytes_per_launch,
                          "avg_launch_us": diff_s * 1e6 / launches,
-                         "traffic": traffic_from_profiles(n) if world == 1 else None},
+                         "traffic": traffic_from_profiles(n) if world == 1 else None,
+                         "traffic_source": "committed rocprofv3 PMC summary profiles/pmc_sync_diff_k32.json (FETCH_SIZE x 2 "
+                                           "+ WRITE_SIZE per launch), not measured in this run"},
             # the engine times a sample of the launches (every 5th tick on one GPU): average x launches per period
             "kernel_time_share": {"k_sync_diff": diff_s / launches * ticks_per_period * a.steps / dt},  # others: profiles/*kernel_stats*
             "whole_step_algorithmic_GBps": B / dt / 1e9,
+            "whole_step_algorithmic_bytes_per_period": B / a.steps,
+            # whole-step HBM bytes per period measured by rocprofv3 PMC (FETCH_SIZE x 2 + WRITE_SIZE over every kernel,
+            # the difference of two runs of different lengths): read from the committed profiles/, not this run
+            "whole_step_pmc_bytes_per_period_committed": whole_step_pmc(a.workload, n) if world == 1 else None,
             "counters": {k: d[k] for k in ("record_compares", "row_writes", "messages", "gossip_messages", "events",
-                                           "sync_merges")},
+                                           "sync_merges", "diff_msgs_total", "ack_resolved_total")},
             "device_bytes": ctr["device_bytes"],
             # since the handle was created (warm-up included): a profiler pass over the whole process prices its
             # k_sync_diff traffic against 8 B x N x these merges (tools/make_profiles.py)

@@ -471,10 +471,11 @@ int build(swim_handle* h) {
   A(d.arena[1], (uint64_t)d.ARENA_ROWS * d.NS) A(d.arena_used, 2)
   A(d.m_next, 2ull * d.MSGCAP) A(d.m_head, 2 * N) A(d.next_evt, N) A(d.mdone, 2) A(d.trk, NL * TRK) A(d.ulog, NL * ULOG * 2) A(d.spq, NL * SPQ * 8) A(d.fpend, NL * KP * 2) A(d.pending_inc, N) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
   A(d.pool, d.POOLCAP) A(d.pool_used, 1)
-  // SYNC_ACK resolution (k_ack_resolve): one GPU; SWIM_NO_ACKRES streams every payload (measurements)
-  d.ackres = d.W == 1 && !d.implicit && !getenv("SWIM_NO_ACKRES") ? 1u : 0u;
+  // SYNC_ACK resolution (k_ack_resolve); SWIM_NO_ACKRES streams every payload (measurements)
+  d.ackres = !d.implicit && !getenv("SWIM_NO_ACKRES") ? 1u : 0u;
   if (d.ackres) {
     A(d.tlog, 2 * NL * TL) A(d.tl_n, 2 * NL) A(d.tl_tick, 2 * NL) A(d.dlist, d.MSGCAP) A(d.ndl, 1)
+    if (d.W > 1) A(d.mlog, (uint64_t)d.MSGCAP * TL)
     HIPCK(hipMemsetAsync(d.tl_tick, 0xFF, 8 * NL, h->stream));
     HIPCK(hipMemsetAsync(d.ndl, 0, 4, h->stream));
   }
@@ -527,7 +528,7 @@ int build(swim_handle* h) {
     d.RQCAP = d.MSGCAP;
     d.RXCAP = d.MSGCAP;
     d.CHCAP = h->spec.chunk_cap ? h->spec.chunk_cap : (uint32_t)std::min<uint64_t>(4096, (uint64_t)d.MSGCAP * d.NCHUNK);
-    uint64_t se = sizeof(SyncMsg) + 8 + 8ull * d.MW;
+    uint64_t se = sync_entry_size(d.MW);
     d.XA_PEER = ((32 + 4ull * NSW * d.NSCAP + 4ull * RRW * d.RRCAP + se * d.RQCAP + 511) & ~255ull) +
                 (uint64_t)d.CHCAP * CH * 4;
     d.XB_PEER = 16 + 8ull * std::min<uint64_t>((uint64_t)d.DCAP, 1ull << 25);

@@ -404,6 +404,7 @@ __device__ __forceinline__ void tick_end(const Dev& d, uint32_t k) {
     d.arena_used[nb] = 0;
     *d.pool_used = 0;
     *d.rc_n = 0;
+    if (d.ackres) *d.ndl = 0;
   }
 }
 

@@ -120,6 +120,8 @@ constexpr uint32_t KF_RES = 0x400u;
 constexpr uint32_t KF_LATE = 0x800u;  // a delayed message put back by k_sync_redeliver
 constexpr uint32_t KF_FLAGS = KF_DEFER | KF_ABS | KF_RES | KF_LATE;
 constexpr uint32_t TL = 16;  // per-member tick write log (ack resolution); past it the member's ACKs are streamed
+// exchange A's SYNC entry: the message, its first chunk slot + pad, the chunk mask, the sender's write-log prefix
+__host__ __device__ __forceinline__ uint64_t sync_entry_size(uint32_t MW) { return sizeof(SyncMsg) + 8 + 8ull * MW + 4ull * TL; }
 
 struct Dev {
   // ---- configuration ----
@@ -294,6 +296,9 @@ struct Dev {
   uint32_t* tl_tick;  // [2][NL]
   uint32_t* dlist;    // [MSGCAP]
   uint32_t* ndl;
+  // W > 1: the sender's write-log prefix (SyncMsg.tln entries) of each message of the inbound list committed this tick,
+  // by its index there: copied by k_sync_route for this shard's senders and shipped in exchange A for the peers'
+  uint32_t* mlog;     // [MSGCAP][TL]
 
   // ---- outputs ----
   uint32_t* ev;  // [EVCAP][8] swim_event

@@ -354,7 +354,7 @@ __global__ void __launch_bounds__(256) k_sync_diff(const Dev* __restrict__ dp, u
   // end by wall clock and atomics, made every launch of this kernel 30 % slower by its mere presence in the code:
   // 85 -> 112 us per launch at C3, profiles/r03_*)
   // with SYNC_ACK resolution, only the messages k_ack_resolve left in dlist
-  const bool dl = !SHARDED && d.ackres;
+  const bool dl = d.ackres != 0;
   uint32_t nmsg = dl ? *(volatile uint32_t*)d.ndl : (d.nmsg[b] < d.MSGCAP ? d.nmsg[b] : d.MSGCAP);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     atomicAdd(&d.ctr[C_DIFFMSG_ALL], (unsigned long long)nmsg);
@@ -457,7 +457,26 @@ struct ResArgs {
   uint64_t* pool;
   unsigned long long* ctr;
   uint32_t NL, NS, MSGCAP, NCHUNK, POOLCAP;
+  // W > 1: this shard's first observer, the senders' log prefixes by message (Dev::mlog), and the received payloads
+  // (baseline row + shipped chunks, as diff_fetch reads them)
+  uint32_t lo, W, MW;
+  const uint32_t *mlog, *base_row;
+  const uint64_t *rx_mask, *rx_off;
+  const uint8_t* xa_recv;
 };
+
+// subject v of a message's payload: the sender's live row, its arena snapshot, or (W > 1) a payload received from
+// another shard (the shipped chunk if the chunk mask has it, else the baseline row)
+__device__ __forceinline__ uint32_t res_payload_key(const ResArgs& d, uint32_t pay, uint32_t src, uint32_t v) {
+  if (pay == NEVER) return d.rowk[(size_t)(src - d.lo) * d.NS + v];
+  if (!(pay & PAY_RX) || d.W == 1) return d.arena[(size_t)pay * d.NS + v];
+  const uint32_t ri = pay & ~PAY_RX, c = v / CH;
+  const uint64_t* mk = d.rx_mask + (size_t)ri * d.MW;
+  if (!((mk[c >> 6] >> (c & 63)) & 1ull)) return d.base_row[v];
+  uint32_t rank = __popcll(mk[c >> 6] & ((1ull << (c & 63)) - 1ull));
+  for (uint32_t q = 0; q < (c >> 6); ++q) rank += __popcll(mk[q]);
+  return ((const uint32_t*)(d.xa_recv + d.rx_off[ri]))[(size_t)rank * CH + v % CH];
+}
 __global__ void __launch_bounds__(512) k_ack_resolve(ResArgs d, uint32_t k, uint32_t spec, uint32_t timed) {
   if (spec && *(volatile uint32_t*)d.halt) return;
   __shared__ uint32_t sv_[8][64], sc_[8][64];
@@ -477,8 +496,9 @@ __global__ void __launch_bounds__(512) k_ack_resolve(ResArgs d, uint32_t k, uint
       const uint32_t kind = mm.kind, src = mm.src, dst = mm.dst, tln = mm.tln, pay = mm.payload;
       bool res = k >= 2 && (kind & KF_RES) && !(kind & KF_DEFER) && mm.pin == NEVER && tln <= TL;
       uint32_t n0 = 0, n1 = 0;  // A's log entries of ticks k-2 and k-1
+      const uint32_t ld = dst - d.lo;  // the requester: an observer of this shard
       if (res) {
-        const size_t a0 = (size_t)(k & 1) * d.NL + dst, a1 = (size_t)((k - 1) & 1) * d.NL + dst;
+        const size_t a0 = (size_t)(k & 1) * d.NL + ld, a1 = (size_t)((k - 1) & 1) * d.NL + ld;
         n0 = d.tl_tick[a0] == k - 2 ? d.tl_n[a0] : 0u;
         n1 = d.tl_tick[a1] == k - 1 ? d.tl_n[a1] : 0u;
         res = n0 <= TL && n1 <= TL;
@@ -494,9 +514,10 @@ __global__ void __launch_bounds__(512) k_ack_resolve(ResArgs d, uint32_t k, uint
       } else {
         // gather: B's prefix, then A's two ticks (at most 3 TL <= 64 subjects, one per lane)
         uint32_t v = NEVER;
-        if (lane < tln) v = d.tlog[((size_t)((k - 1) & 1) * d.NL + src) * TL + lane];
-        else if (lane < tln + n0) v = d.tlog[((size_t)(k & 1) * d.NL + dst) * TL + (lane - tln)];
-        else if (lane < tln + n0 + n1) v = d.tlog[((size_t)((k - 1) & 1) * d.NL + dst) * TL + (lane - tln - n0)];
+        if (lane < tln)  // W > 1: the prefix came with the message (the responder may live on another shard)
+          v = d.W > 1 ? d.mlog[(size_t)i * TL + lane] : d.tlog[((size_t)((k - 1) & 1) * d.NL + src) * TL + lane];
+        else if (lane < tln + n0) v = d.tlog[((size_t)(k & 1) * d.NL + ld) * TL + (lane - tln)];
+        else if (lane < tln + n0 + n1) v = d.tlog[((size_t)((k - 1) & 1) * d.NL + ld) * TL + (lane - tln - n0)];
         sv[lane] = v;
         __builtin_amdgcn_wave_barrier();
         bool first = v != NEVER;
@@ -504,8 +525,8 @@ __global__ void __launch_bounds__(512) k_ack_resolve(ResArgs d, uint32_t k, uint
         uint32_t key = 0;
         bool cand = false;
         if (first) {
-          key = pay == NEVER ? d.rowk[(size_t)src * d.NS + v] : d.arena[(size_t)pay * d.NS + v];
-          cand = (key & 3u) != ST_ABSENT && key != d.rowk[(size_t)dst * d.NS + v];
+          key = res_payload_key(d, pay, src, v);
+          cand = (key & 3u) != ST_ABSENT && key != d.rowk[(size_t)ld * d.NS + v];
         }
         sc[lane] = cand ? v : NEVER;
         __builtin_amdgcn_wave_barrier();
@@ -683,14 +704,19 @@ static void launch_sync_diff(const Dev& d, uint32_t b, hipStream_t st, uint32_t 
 
 // single GPU: the tick is cut in three so that the host can hold back the gossip data plane when no slot is in
 // use; the SYNC diff of tick k+1 does not depend on the gossip plane of tick k and is queued in between
+// SYNC_ACKs of tick k - 1 resolved from write logs (the rest go to the list k_sync_diff streams)
+static void launch_ack_resolve(const Dev& d, uint32_t k, hipStream_t st, bool spec, bool timed) {
+  if (k == 0 || !d.ackres) return;
+  const uint32_t b = (k - 1) & 1;
+  const ResArgs ra{d.halt, d.nmsg + b, d.tl_tick, d.tl_n, d.tlog, d.rowk, d.arena[b], d.msgs[b], d.dlist, d.ndl,
+                   d.chunk_meta, d.pool_used, d.err, d.pool, d.ctr, d.NL, d.NS, d.MSGCAP, d.NCHUNK, d.POOLCAP,
+                   d.lo, d.W, d.MW, d.mlog, d.base_row, d.rx_mask, d.rx_off, d.xa_recv};
+  hipLaunchKernelGGL(k_ack_resolve, dim3(128), dim3(512), 0, st, ra, k, spec ? 1u : 0u, timed ? 1u : 0u);
+}
+
 void launch_diff(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool spec) {
   hipStream_t st = (hipStream_t)stream;
-  if (k > 0 && d.ackres) {
-    const uint32_t b = (k - 1) & 1;
-    const ResArgs ra{d.halt, d.nmsg + b, d.tl_tick, d.tl_n, d.tlog, d.rowk, d.arena[b], d.msgs[b], d.dlist, d.ndl,
-                     d.chunk_meta, d.pool_used, d.err, d.pool, d.ctr, d.NL, d.NS, d.MSGCAP, d.NCHUNK, d.POOLCAP};
-    hipLaunchKernelGGL(k_ack_resolve, dim3(128), dim3(512), 0, st, ra, k, spec ? 1u : 0u, prof ? 1u : 0u);
-  }
+  launch_ack_resolve(d, k, st, spec, prof != nullptr);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
   if (k > 0) launch_sync_diff(d, (k - 1) & 1, st, prof ? 1u : 0u, spec ? 1u : 0u);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
@@ -824,6 +850,7 @@ void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   hipStream_t st = (hipStream_t)stream;
   uint32_t b = k & 1;
   const uint32_t sp = spec ? 1u : 0u;
+  launch_ack_resolve(d, k, st, spec, prof != nullptr);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
   if (k > 0) launch_sync_diff(d, (k - 1) & 1, st, prof ? 1u : 0u, sp);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);

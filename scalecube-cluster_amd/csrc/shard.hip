@@ -14,14 +14,23 @@
 //
 // Peer regions have a fixed capacity; a region that would overflow raises E_XCAP instead of being truncated.
 // Region A: u32 hdr[8] = {nslot, nround, nsync, nchunk, data_off, 0, 0, 0}; slot records; round records;
-//           sync entries {SyncMsg, u32 chunk base, u32 pad, u64 mask[MW]}; chunk data at data_off (256-B aligned).
+//           sync entries {SyncMsg, u32 chunk base, u32 pad, u64 mask[MW], u32 log[TL]}; chunk data at data_off
+//           (256-B aligned). log: a resolvable SYNC_ACK's responder write-log prefix (k_ack_resolve).
 // Region B: u32 hdr[4] = {nreceipt, 0, 0, 0}; u64 receipts.
 #include "dev_util.h"
 
 namespace swim {
 
 
-__device__ __forceinline__ uint64_t sync_entry_bytes(const Dev& d) { return sizeof(SyncMsg) + 8 + 8ull * d.MW; }
+__device__ __forceinline__ uint64_t sync_entry_bytes(const Dev& d) { return sync_entry_size(d.MW); }
+
+// SYNC_ACK resolution (k_ack_resolve): a resolvable SYNC_ACK's sender's write-log prefix of this tick (tick parity b),
+// the SyncMsg.tln subjects it wrote before answering; nothing for the other messages
+__device__ __forceinline__ void copy_log_prefix(const Dev& d, const SyncMsg& mm, uint32_t b, uint32_t* out) {
+  const uint32_t n = (mm.kind & KF_RES) && mm.tln <= TL ? mm.tln : 0u;
+  const uint32_t* src = d.tlog + ((size_t)b * d.NL + lidx(d, mm.src)) * TL;
+  for (uint32_t j = 0; j < n; ++j) out[j] = src[j];
+}
 
 // a payload's key plane: the sender's live row or its copy-on-write snapshot
 __device__ __forceinline__ const uint32_t* payload_row(const Dev& d, const SyncMsg& mm, uint32_t b) {
@@ -38,7 +47,10 @@ __global__ void k_sync_route(Dev d, uint32_t b, uint32_t spec) {
     uint32_t q = shard_of(d.N, d.W, mm.dst);
     if (q == d.rank) {
       uint32_t j = atomicAdd(&d.xn[4], 1u);
-      if (j < d.MSGCAP) d.mtmp[j] = mm;
+      if (j < d.MSGCAP) {
+        d.mtmp[j] = mm;
+        if (d.ackres) copy_log_prefix(d, mm, b, d.mlog + (size_t)j * TL);
+      }
       continue;
     }
     uint32_t j = atomicAdd(&d.rq_n[q], 1u);
@@ -112,6 +124,7 @@ __global__ void __launch_bounds__(256) k_pack_a(Dev d, uint32_t b, uint32_t spec
     ((uint32_t*)(p + sizeof(SyncMsg)))[1] = 0;
     uint64_t* mk = (uint64_t*)(p + sizeof(SyncMsg) + 8);
     for (uint32_t w = 0; w < d.MW; ++w) mk[w] = d.rq_mask[e * d.MW + w];
+    if (d.ackres) copy_log_prefix(d, d.msgs[b][d.rq_list[e]], b, (uint32_t*)(mk + d.MW));
   }
 }
 
@@ -239,6 +252,8 @@ __global__ void __launch_bounds__(256) k_unpack_a(Dev d, uint32_t k, uint32_t en
         continue;
       }
       for (uint32_t w = 0; w < d.MW; ++w) d.rx_mask[(size_t)ri * d.MW + w] = mk[w];
+      if (d.ackres && (mm.kind & KF_RES) && mm.tln <= TL)  // the responder's log prefix (k_ack_resolve)
+        for (uint32_t q = 0; q < mm.tln; ++q) d.mlog[(size_t)j * TL + q] = ((const uint32_t*)(mk + d.MW))[q];
       d.rx_off[ri] = (uint64_t)p * d.XA_PEER + data_off + (uint64_t)base * CH * 4;
       mm.payload = PAY_RX | ri;
       mm.ncand = 0;

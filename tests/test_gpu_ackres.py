@@ -71,3 +71,47 @@ def test_ack_resolution_equals_streaming(engine):
     assert ca["ack_resolved_total"] > 0 and cb["ack_resolved_total"] == 0
     for k in ("record_compares", "row_writes", "messages", "events", "sync_merges", "messages_lost"):
         assert ca[k] == cb[k], k
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ack_resolution_sharded_parity(oracle, engine, world):
+    """Row-sharded handles resolve SYNC_ACKs too: the responder's write-log prefix travels with the SYNC_ACK in exchange
+    A. Bit-exact against the oracle under loss, kills, incarnation and metadata updates and a leave."""
+    from swimhip.shard import ThreadShardGroup
+    cfg = SimConfig(n_members=160, cluster=FAST_SYNC, gossip_slot_cap=1 << 16)
+    o, e = SimulatedCluster(oracle, cfg), ThreadShardGroup(engine, cfg, world)
+    for phase in range(2):
+        for c in (o, e):
+            faults(c, phase)
+        run_lockstep(o, e, 120, 30, f"W={world} phase {phase}", events=False)
+    for c in (o, e):
+        c.leave(90)
+    run_lockstep(o, e, 120, 30, f"W={world} leave", events=False)
+    assert o.events() == e.events()
+    assert e.counters()["ack_resolved_total"] > 0
+    e.close()
+    o.close()
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_ack_resolution_sharded_steady_accounting(engine, world):
+    """C3-shaped steady state on W shards: the SYNC_ACKs are resolved (all but those whose receiver got several
+    payloads in one tick), so the shards' k_sync_diff launches stream little more than the SYNC payloads, and the state
+    equals the single-GPU run's."""
+    from swimhip.shard import ThreadShardGroup
+    cfg = SimConfig(n_members=3000, cluster=FAST_SYNC)
+    c = SimulatedCluster(engine, cfg) if world == 1 else ThreadShardGroup(engine, cfg, world)
+    c.run_periods(2)
+    base = c.counters()
+    c.run_periods(4)
+    ctr = c.counters()
+    d = {k: ctr[k] - base[k] for k in ("sync_merges", "ack_resolved_total", "diff_msgs_total")}
+    assert d["sync_merges"] > 0 and d["ack_resolved_total"] * 4 > d["sync_merges"], d
+    assert d["ack_resolved_total"] + d["diff_msgs_total"] == d["sync_merges"], d
+    h = c.state_hash()
+    c.close()
+    if world > 1:
+        ref = SimulatedCluster(engine, cfg)
+        ref.run_periods(6)
+        assert np.array_equal(ref.state_hash(), h)
+        ref.close()

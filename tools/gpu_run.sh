@@ -5,7 +5,7 @@
 #   bench:W[:S[:WU]]  bench.py --workload W (c3 | c3dyn | c2 | c5), S steps, WU warm-up, no CPU baseline
 #   benchcpu          the default bench line with its CPU baseline (the driver's command)
 #   trace:W[:S[:WU]]  rocprofv3 kernel trace + stats of the same bench command, and its per-tick breakdown
-#   pmc:W:COUNTER     one rocprofv3 --pmc pass (one counter group) over a short bench run of workload W
+#   pmc:W:COUNTER[:S] one rocprofv3 --pmc pass (one counter) over a bench run of workload W with S steps (default 3)
 # Example:  gpurun --timeout 1200 -- 'bash tools/gpu_run.sh r4a suite:fullsize smoke bench:c3'
 set -e
 cd $GRAFT_REPO_ROOT
@@ -21,7 +21,7 @@ for step in "$@"; do
       k=()
       [ -n "$a" ] && k=(-k "$a")
       rc=0
-      timeout -k 10 1100 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread -p no:cacheprovider \
+      timeout -k 10 1100 python -u -m pytest tests -m gpu -v --durations=25 --timeout 600 --timeout-method thread -p no:cacheprovider \
         "${k[@]}" > $O/tests.log 2>&1 || rc=$?
       tail -n 1 $O/tests.log
       grep -E "^FAILED|^ERROR" $O/tests.log | head -30 || true
@@ -48,8 +48,8 @@ for step in "$@"; do
       python3 tools/tick_breakdown.py $O/t_$a/run_kernel_trace.csv 10 | tail -3
       ;;
     pmc)
-      timeout -s KILL 300 rocprofv3 --pmc $b -d $O/pmc_${a}_$b -o run --output-format csv -- \
-        python3 bench.py --workload $a --steps 3 --warmup 1 --no-cpu-baseline > $O/pmc_${a}_$b.log 2>&1
+      timeout -s KILL 300 rocprofv3 --pmc $b -d $O/pmc_${a}_${b}_${c:-3} -o run --output-format csv -- \
+        python3 bench.py --workload $a --steps ${c:-3} --warmup 1 --no-cpu-baseline > $O/pmc_${a}_${b}_${c:-3}.log 2>&1
       ;;
     *)
       echo "unknown step $step"
