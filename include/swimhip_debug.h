@@ -19,6 +19,8 @@
  *          whole window is replayed), GossipProtocolImpl isInfected (:247)
  *   xinl   bytes per peer of the RCCL inline all-to-all of a sharded tick (more: a send/recv group; speculative
  *          sharded batches halt on the overflow flag), every rank the same value
+ *   rp     replay / slow-path gossip sends per tick (grow_caps enlarges the lists; SWIM_DELIV_CAP sets the routed
+ *          receipts per tick the same way)
  * With SWIM_CAPS (or SWIM_FALLBACKS=1) set, the handle counts how often each fallback fired.
  */
 #ifndef SWIMHIP_DEBUG_H
@@ -49,6 +51,17 @@ extern "C" {
 /* counts of the fallbacks fired since create, n <= 16 entries (summed over shards); SWIM_EUNSUPPORTED when the
  * handle was created without SWIM_CAPS / SWIM_FALLBACKS */
 int swim_debug_fallbacks(swim_handle* h, uint64_t* out, size_t n);
+
+/* the current sizes of the structures that grow between ticks (api.hip grow_caps), n <= 8 entries:
+ * gossip slots per shard, receipt-ring entries per member, routed receipts per tick, replay / slow-path sends per
+ * tick, incarnation-history entries, and how many growth steps ran. One GPU (a sharded handle: SWIM_EUNSUPPORTED). */
+#define SWIM_CAP_SLOTS 0u
+#define SWIM_CAP_RING 1u
+#define SWIM_CAP_RECEIPTS 2u
+#define SWIM_CAP_REPLAY 3u
+#define SWIM_CAP_HISTORY 4u
+#define SWIM_CAP_GROWTHS 5u
+int swim_debug_caps(swim_handle* h, uint64_t* out, size_t n);
 
 #ifdef __cplusplus
 }

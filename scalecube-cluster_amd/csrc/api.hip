@@ -71,6 +71,7 @@ struct swim_handle {
   bool no_pipe = getenv("SWIM_NO_PIPELINE") != nullptr;    // debugging aid: no early SYNC diff of the next tick
   bool no_spec = getenv("SWIM_NO_SPECULATION") != nullptr;  // debugging aid: a host wait after every member kernel
   bool gossip_idle = false;  // W == 1: no gossip slot was in use after the latest member kernel
+  uint64_t growths = 0;      // capacity growth steps so far (grow_caps)
   // timing aid (bench.py --rehearse-shard): a slot shard alone, its peers' gossip-count deltas taken as zero without
   // any exchange (not the W-shard simulation's results)
   bool lone = getenv("SWIM_LONE_SHARD") != nullptr;
@@ -111,6 +112,161 @@ int dalloc(swim_handle* h, T** p, size_t count) {
   const char* po = getenv("SWIM_POISON_ONLY");
   if (getenv("SWIM_POISON") || (po && atoi(po) == (int)h->allocs.size() - 1)) hipMemsetAsync(q, 0xA5, bytes, h->stream);
   *p = (T*)q;
+  return SWIM_OK;
+}
+
+hipError_t h2d(hipStream_t st, void* dst, const void* src, size_t bytes);
+
+// an allocation of dalloc given back (capacity growth replaced it)
+void dfree(swim_handle* h, void* p, size_t bytes) {
+  auto it = std::find(h->allocs.begin(), h->allocs.end(), p);
+  if (it == h->allocs.end()) return;
+  h->allocs.erase(it);
+  hipFree(p);
+  h->bytes -= bytes;
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Capacity growth (one GPU). The gossip slot table, the receipt rings and the per-tick receipt / replay lists start
+// at the config's size and grow between ticks before they can overflow: after each member kernel of a tick with the
+// gossip plane active, tick_flag has published the slots in use, the largest ring fill and the previous gossip plane's
+// list lengths (Dev::hflag). A structure past half (slots, rings) or a quarter (per-tick lists) of its capacity is
+// reallocated larger, within the free HBM, its contents moved: slot ids, ring positions and every held bit keep their
+// meaning, so the simulation is unchanged (slot ids are not observable). SWIM_NO_GROW: fixed sizes.
+int grow_caps(swim_handle* h) {
+  Dev& d = h->d;
+  if (!d.rfill) return SWIM_OK;
+  const volatile uint32_t* f = h->hflag;
+  const uint64_t used = f[0], fill = f[2], nrc = f[3], nrp = f[4], nsl = f[5], nhist = f[6];
+  const uint64_t N = d.N;
+  const bool gs = used > d.SPR / 2 && d.SPR < (1u << 22), gr = fill > d.BCAP / 2 && d.BCAP < (1u << 30);
+  const bool grc = nrc > d.RCAP / 4 && d.RCAP < (1u << 30), grp = (nrp > d.RPCAP / 4 || nsl > d.SLOWCAP / 4) && d.RPCAP < (1u << 30);
+  // the history scales with the holder states that can be reborn: the create-time rule (slots x members / 8, up to
+  // 2^24) for the grown slot table, or four times the entries in use
+  uint64_t hwant = d.HCAP;
+  if (nhist > d.HCAP / 2) hwant = 4 * nhist;
+  if (gs) hwant = std::max<uint64_t>(hwant, std::min<uint64_t>(1ull << 24, 2ull * d.SPR * N / 8));
+  uint64_t hcap2 = d.HCAP;
+  while (hcap2 < hwant && hcap2 < (1ull << 28)) hcap2 <<= 1;
+  const bool gh = hcap2 > d.HCAP;
+  if (!gs && !gr && !grc && !grp && !gh) return SWIM_OK;
+  HIPCK(hipStreamSynchronize(h->stream));
+  size_t fr = 0, tot = 0;
+  HIPCK(hipMemGetInfo(&fr, &tot));
+  const uint64_t reserve = 2ull << 30;
+  uint64_t budget = fr > reserve ? fr - reserve : 0;
+  hipStream_t st = h->stream;
+  int rc;
+  if (grc || grp) {  // per-tick lists: nothing in them between ticks, so no contents move
+    const uint64_t rcap = grc ? std::min<uint64_t>(1ull << 30, std::max<uint64_t>(4ull * nrc, 4ull * d.RCAP)) : d.RCAP;
+    const uint64_t pcap = grp ? std::min<uint64_t>(1ull << 30, 4ull * std::max<uint64_t>(d.RPCAP, std::max(nrp, nsl))) : d.RPCAP;
+    const uint64_t need = (rcap - d.RCAP) * 32 + (pcap - d.RPCAP) * 16;
+    if (need <= budget) {
+      budget -= need;
+      if (rcap != d.RCAP) {
+        dfree(h, d.rc_raw, 8ull * d.RCAP), dfree(h, d.rc_slot, 4ull * d.RCAP), dfree(h, d.rc_key, 8ull * d.RCAP);
+        dfree(h, d.rc_slot2, 4ull * d.RCAP), dfree(h, d.rc_key2, 8ull * d.RCAP);
+        d.RCAP = d.DCAP = (uint32_t)rcap;
+        if ((rc = dalloc(h, &d.rc_raw, rcap)) || (rc = dalloc(h, &d.rc_slot, rcap)) || (rc = dalloc(h, &d.rc_key, rcap)) ||
+            (rc = dalloc(h, &d.rc_slot2, rcap)) || (rc = dalloc(h, &d.rc_key2, rcap)))
+          return rc;
+      }
+      if (pcap != d.RPCAP) {
+        dfree(h, d.rp, 8ull * d.RPCAP), dfree(h, d.slow, 8ull * d.SLOWCAP);
+        d.RPCAP = d.SLOWCAP = (uint32_t)pcap;
+        if ((rc = dalloc(h, &d.rp, pcap)) || (rc = dalloc(h, &d.slow, pcap))) return rc;
+      }
+    }
+  }
+  if (gh && 8ull * hcap2 * HREC <= budget) {  // incarnation history: a larger table, every entry re-inserted
+    uint64_t* h2 = nullptr;
+    const uint64_t c2 = hcap2;
+    budget -= 8 * c2 * HREC;
+    if ((rc = dalloc(h, &h2, c2 * HREC))) return rc;
+    HIPCK(hipMemsetAsync(h2, 0, 8 * c2 * HREC, st));
+    launch_hist_rehash(d.hist, d.HCAP, h2, (uint32_t)c2, st);
+    HIPCK(hipStreamSynchronize(st));
+    dfree(h, d.hist, 8ull * d.HCAP * HREC);
+    d.hist = h2;
+    d.HCAP = (uint32_t)c2;
+  }
+  if (gr) {  // receipt rings: twice the entries, every held entry moved to its position's new index
+    const uint64_t b2 = 2ull * d.BCAP;
+    if (N * b2 * 4 <= budget) {
+      budget -= N * b2 * 4;
+      uint32_t* rg2 = nullptr;
+      if ((rc = dalloc(h, &rg2, N * b2))) return rc;
+      launch_ring_move(d.rg, rg2, d.rhead, d.rtail, d.N, d.BCAP, (uint32_t)b2, st);
+      HIPCK(hipStreamSynchronize(st));
+      dfree(h, d.rg, 4ull * N * d.BCAP);
+      d.rg = rg2;
+      d.BCAP = (uint32_t)b2;
+    }
+  }
+  if (gs) {  // slot table: twice the slots (whole 64-slot groups), or what the free HBM holds
+    const uint64_t per = 2 * N + N / 4 + 64;  // S + HB + WB per slot, plus the slot arrays
+    uint64_t s2 = std::min<uint64_t>(2ull * d.SPR, std::min<uint64_t>(1ull << 22, budget / per)) & ~63ull;
+    if (s2 > d.SPR) {
+      const uint64_t s1 = d.SPR, q1 = d.QW, q2 = s2 / 64;
+      uint16_t* S2 = nullptr;
+      unsigned long long *HB2 = nullptr, *WB2 = nullptr, *GU2 = nullptr, *DM2 = nullptr, *RX2 = nullptr;
+      uint64_t *gid2 = nullptr, *key2 = nullptr;
+      uint32_t *subj2 = nullptr, *ct2 = nullptr, *exp2 = nullptr, *used2 = nullptr, *fl2 = nullptr, *fexp2 = nullptr,
+               *ag2 = nullptr, *rxl2 = nullptr;
+      if ((rc = dalloc(h, &S2, N * s2)) || (rc = dalloc(h, &HB2, N * q2)) || (rc = dalloc(h, &WB2, N * q2)) ||
+          (rc = dalloc(h, &GU2, q2)) || (rc = dalloc(h, &DM2, q2)) || (rc = dalloc(h, &ag2, q2)) ||
+          (rc = dalloc(h, &gid2, s2)) || (rc = dalloc(h, &key2, s2)) || (rc = dalloc(h, &subj2, s2)) ||
+          (rc = dalloc(h, &ct2, s2)) || (rc = dalloc(h, &exp2, s2)) || (rc = dalloc(h, &used2, s2)) ||
+          (rc = dalloc(h, &fl2, s2)) || (rc = dalloc(h, &fexp2, s2)))
+        return rc;
+      // rows: the old columns, then zero (no holder of a new slot)
+      HIPCK(hipMemcpy2DAsync(S2, 2 * s2, d.S, 2 * s1, 2 * s1, N, hipMemcpyDeviceToDevice, st));
+      HIPCK(hipMemset2DAsync(S2 + s1, 2 * s2, 0, 2 * (s2 - s1), N, st));
+      HIPCK(hipMemcpy2DAsync(HB2, 8 * q2, d.HB, 8 * q1, 8 * q1, N, hipMemcpyDeviceToDevice, st));
+      HIPCK(hipMemset2DAsync(HB2 + q1, 8 * q2, 0, 8 * (q2 - q1), N, st));
+      HIPCK(hipMemcpy2DAsync(WB2, 8 * q2, d.WB, 8 * q1, 8 * q1, N, hipMemcpyDeviceToDevice, st));
+      HIPCK(hipMemset2DAsync(WB2 + q1, 8 * q2, 0, 8 * (q2 - q1), N, st));
+      HIPCK(hipMemsetAsync(GU2, 0, 8 * q2, st));
+      HIPCK(hipMemsetAsync(DM2, 0, 8 * q2, st));
+      HIPCK(hipMemcpyAsync(GU2, d.GU, 8 * q1, hipMemcpyDeviceToDevice, st));
+      HIPCK(hipMemcpyAsync(DM2, d.DM, 8 * q1, hipMemcpyDeviceToDevice, st));
+      HIPCK(hipMemcpyAsync(gid2, d.slot_gid, 8 * s1, hipMemcpyDeviceToDevice, st));
+      HIPCK(hipMemcpyAsync(key2, d.slot_key, 8 * s1, hipMemcpyDeviceToDevice, st));
+      HIPCK(hipMemcpyAsync(subj2, d.slot_subj, 4 * s1, hipMemcpyDeviceToDevice, st));
+      HIPCK(hipMemcpyAsync(ct2, d.slot_ctick, 4 * s1, hipMemcpyDeviceToDevice, st));
+      HIPCK(hipMemsetAsync(exp2, 0xFF, 4 * s2, st));  // new slots: unused, no expiry
+      HIPCK(hipMemcpyAsync(exp2, d.slot_exp, 4 * s1, hipMemcpyDeviceToDevice, st));
+      HIPCK(hipMemsetAsync(used2, 0, 4 * s2, st));
+      HIPCK(hipMemcpyAsync(used2, d.slot_used, 4 * s1, hipMemcpyDeviceToDevice, st));
+      // free list: the new ids below the old free entries (the old ones are taken first; ids are not observable)
+      int32_t top = 0;
+      HIPCK(hipMemcpyAsync(&top, d.free_top, 4, hipMemcpyDeviceToHost, st));
+      HIPCK(hipStreamSynchronize(st));
+      std::vector<uint32_t> ids(s2 - s1);
+      for (uint64_t i = 0; i < s2 - s1; ++i) ids[i] = (uint32_t)(s2 - 1 - i);
+      HIPCK(hipMemcpyAsync(fl2, ids.data(), 4 * ids.size(), hipMemcpyHostToDevice, st));
+      if (top > 0) HIPCK(hipMemcpyAsync(fl2 + ids.size(), d.free_list, 4ull * top, hipMemcpyDeviceToDevice, st));
+      const int32_t top2 = top + (int32_t)ids.size();
+      HIPCK(hipMemcpyAsync(d.free_top, &top2, 4, hipMemcpyHostToDevice, st));
+      // the per-tick contact rows follow the row width
+      const uint32_t crcap = (uint32_t)std::max<uint64_t>(64, std::min<uint64_t>(4096, (512ull << 20) / (8ull * q2)));
+      const uint32_t cr = getenv("SWIM_CAPS") && strstr(getenv("SWIM_CAPS"), "rx=") ? d.CRCAP : crcap;
+      if ((rc = dalloc(h, &RX2, (uint64_t)cr * q2)) || (rc = dalloc(h, &rxl2, 3ull * cr))) return rc;
+      HIPCK(hipStreamSynchronize(st));
+      dfree(h, d.S, 2 * N * s1), dfree(h, d.HB, 8 * N * q1), dfree(h, d.WB, 8 * N * q1), dfree(h, d.GU, 8 * q1);
+      dfree(h, d.DM, 8 * q1), dfree(h, d.agroup, 4 * q1), dfree(h, d.slot_gid, 8 * s1), dfree(h, d.slot_key, 8 * s1);
+      dfree(h, d.slot_subj, 4 * s1), dfree(h, d.slot_ctick, 4 * s1), dfree(h, d.slot_exp, 4 * s1);
+      dfree(h, d.slot_used, 4 * s1), dfree(h, d.free_list, 4 * s1), dfree(h, d.fexp, 4 * s1);
+      dfree(h, d.RX, 8ull * d.CRCAP * q1), dfree(h, d.rxl, 12ull * d.CRCAP);
+      d.S = S2, d.HB = HB2, d.WB = WB2, d.GU = GU2, d.DM = DM2, d.agroup = ag2, d.slot_gid = gid2, d.slot_key = key2;
+      d.slot_subj = subj2, d.slot_ctick = ct2, d.slot_exp = exp2, d.slot_used = used2, d.free_list = fl2, d.fexp = fexp2;
+      d.RX = RX2, d.rxl = rxl2, d.CRCAP = cr;
+      d.SPR = d.SLOTS = (uint32_t)s2;
+      d.QW = (uint32_t)q2;
+    }
+  }
+  HIPCK(h2d(st, (void*)d.self, &d, sizeof(Dev)));
+  h->growths++;
   return SWIM_OK;
 }
 
@@ -290,7 +446,7 @@ int build(swim_handle* h) {
   d.trk_cap = TRK, d.ulog_cap = ULOG, d.creq_cap = CREQ, d.cwmax_cap = CWMAX, d.cev_cap = CEV, d.mq_cap = MQ;
   d.XI = XINL;
   d.sort_cap = SORT_MAX;
-  uint32_t rx_cap = NEVER;
+  uint32_t rx_cap = NEVER, rp_cap = 0;
   const char* caps = getenv("SWIM_CAPS");
   if (caps) {
     std::string s(caps);
@@ -312,6 +468,7 @@ int build(swim_handle* h) {
       else if (k == "cev") d.cev_cap = clampv(0, CEV);
       else if (k == "mq") d.mq_cap = clampv(1, MQ);
       else if (k == "rx") rx_cap = v;
+      else if (k == "rp") rp_cap = std::max<uint32_t>(64, v);  // replay / slow-path send lists (grow_caps tests)
       else if (k == "xinl") d.XI = std::max<uint32_t>(64, std::min<uint32_t>(XINL, v)) & ~7u;  // send/recv group past it
       else if (k == "sort") {
         uint32_t r = 2;
@@ -372,6 +529,16 @@ int build(swim_handle* h) {
   // default: 64 slots per member, at most 32 GB of holder table (C2's SYNC re-spread storm keeps ~10^5 gossips alive)
   uint64_t slots = c.gossip_slot_cap ? c.gossip_slot_cap
                                      : std::min<uint64_t>(1ull << 22, std::max<uint64_t>(1024, std::min<uint64_t>(64 * N, (32ull << 30) / (4 * N))));
+  // RUMOR mode with churn (C5): the rumors alive together follow from the config. A rumor's receipts come within
+  // ~maxSpread rounds of its creation and its slot is recycled EXPB = 2 maxSpread + 4 rounds after the last one, so
+  // about churn x (3 maxSpread + 4) gossip intervals' worth are alive, split over the XW slot shards (+10 %); a member
+  // holds the ones of its last 2 maxSpread + 3 rounds (its receipt ring, below). Growth (grow_caps) covers the rest.
+  uint64_t rumor_ring = 0;
+  if (!c.gossip_slot_cap && c.mode == SWIM_MODE_RUMOR && c.churn_per_period) {
+    const uint64_t life = (3ull * maxSpread + 4) * d.gossip_t, held = (2ull * maxSpread + 3) * d.gossip_t;
+    slots = std::min<uint64_t>(1ull << 22, std::max<uint64_t>(1024, 11 * c.churn_per_period * life / (10 * d.ping_t * d.XW)));
+    rumor_ring = 21 * c.churn_per_period * held / (20 * d.ping_t * d.XW);
+  }
   // every shard allocates new gossips from its own slot range; the slot table itself is replicated, so the ranges
   // split the budget (twice over, for shards that create more than their share) instead of multiplying it by W: at
   // 100k members and W = 8 a full range per shard would be a 275 GB holder table on every GPU
@@ -400,11 +567,11 @@ int build(swim_handle* h) {
   // size, within about 16-24 GB in all (C2 holds ~3·10^5 gossips per member at 10k members), and
   // swim_config.gossip_ring_cap overrides (a full ring raises E_RING)
   {
-    const uint64_t want = c.gossip_ring_cap ? c.gossip_ring_cap
+    const uint64_t want = c.gossip_ring_cap ? c.gossip_ring_cap : rumor_ring ? std::max<uint64_t>(4096, rumor_ring)
                                             : std::min<uint64_t>(d.SLOTS, std::max<uint64_t>(4096, (16ull << 30) / (4 * N)));
     uint64_t bc = 64;
     while (bc < want && bc < (1ull << 31)) bc <<= 1;
-    if (!c.gossip_ring_cap && bc > 4096 && bc * N * 4 > (24ull << 30)) bc >>= 1;
+    if (!c.gossip_ring_cap && !rumor_ring && bc > 4096 && bc * N * 4 > (24ull << 30)) bc >>= 1;
     d.BCAP = (uint32_t)bc;
   }
   uint64_t mc = N / d.sync_t * 4 + N / d.ping_t + 1024;
@@ -423,6 +590,7 @@ int build(swim_handle* h) {
     d.DCAP = d.RCAP = (uint32_t)std::min<uint64_t>(1ull << 30, strtoull(dc, nullptr, 0));
     d.SLOWCAP = d.RPCAP = std::max(d.SLOWCAP, d.DCAP);
   }
+  if (rp_cap) d.SLOWCAP = d.RPCAP = rp_cap;
   if (d.implicit) {
     // C5: every period's rumors start at one tick, so their epidemics peak together: on one of 8 slot shards a tick
     // can deliver ~7·10^8 first receipts (8 B each). Their GOSSIP events skip the receipt routing (fastp4), and
@@ -478,6 +646,20 @@ int build(swim_handle* h) {
     if (d.W > 1) A(d.mlog, (uint64_t)d.MSGCAP * TL)
     HIPCK(hipMemsetAsync(d.tl_tick, 0xFF, 8 * NL, h->stream));
     HIPCK(hipMemsetAsync(d.ndl, 0, 4, h->stream));
+  }
+  // capacity growth between ticks (grow_caps): one GPU, without guard zones; SWIM_NO_GROW keeps the sizes fixed
+  if (d.W == 1 && !getenv("SWIM_NO_GROW") && !getenv("SWIM_GUARD")) {
+    A(d.rfill, 1) A(d.hist_n, 1)
+    HIPCK(hipMemsetAsync(d.rfill, 0, 4, h->stream));
+    HIPCK(hipMemsetAsync(d.hist_n, 0, 4, h->stream));
+  }
+  // the fused single-GPU tick of speculative batches (k_tick_front + k_member_c0); SWIM_NO_FUSED: the two-kernel tick
+  if (d.W == 1 && !d.implicit && !d.exp && !getenv("SWIM_NO_FUSED")) {
+    d.front_exp = getenv("SWIM_FRONT_EXP") ? (uint32_t)atoi(getenv("SWIM_FRONT_EXP")) : 0u;
+    A(d.stick, N) A(d.c0list, N) A(d.c0n, 1) A(d.dtk, 8 * 32)
+    HIPCK(hipMemsetAsync(d.stick, 0xFF, 4 * N, h->stream));
+    HIPCK(hipMemsetAsync(d.c0n, 0, 4, h->stream));
+    HIPCK(hipMemsetAsync(d.dtk, 0, 4 * 8 * 32, h->stream));
   }
   A(d.ev, (uint64_t)d.EVCAP * 8) A(d.ev_n, 1) A(d.ctr, C_NCTR) A(d.err, 8)
   if (c.flags & SWIM_FLAG_EMULATOR_COUNTERS) {
@@ -1166,6 +1348,10 @@ int swim_step(swim_handle* h, uint32_t n) {
       // that tick with the gossip plane.
       for (uint32_t j = i; j < nb; ++j) {
         const uint32_t kj = k + (j - i);
+        if (d.stick && need_diff) {  // the fused tick (k_tick_front + k_member_c0)
+          launch_fused(d, kj, h->stream, timed(kj) ? &h->prof[j] : nullptr, true);
+          continue;
+        }
         if (need_diff) launch_diff(d, kj, h->stream, timed(kj) ? &h->prof[j] : nullptr, true);
         launch_member(d, kj, h->stream, timed(kj) ? &h->prof[j] : nullptr, true);
         need_diff = j + 1 == nb;
@@ -1201,6 +1387,10 @@ int swim_step(swim_handle* h, uint32_t n) {
       need_diff = !pipe;
       if (!nosync) HIPCK(hipEventSynchronize(h->ev_member));  // (a spin wait measured the same here: diff(k+1) hides the wake-up)
       h->gossip_idle = !nosync && h->hflag[0] == 0;
+      if (!nosync && !h->gossip_idle) {  // slots, rings and receipt lists sized up before they can overflow
+        int gr;
+        if ((gr = grow_caps(h)) != SWIM_OK) return gr;
+      }
       if (nosync) {
       } else if (h->hflag[0] != 0 || h->no_skip) {
         launch_gossip(d, k, h->stream, te);
@@ -1846,6 +2036,14 @@ int swim_debug_fallbacks(swim_handle* h, uint64_t* out, size_t n) {
   if (!h->d.fb) return SWIM_EUNSUPPORTED;  // not counted (SWIM_CAPS / SWIM_FALLBACKS unset at create)
   HIPCK(hipStreamSynchronize(h->stream));
   HIPCK(hipMemcpy(out, h->d.fb, 8 * n, hipMemcpyDeviceToHost));
+  return SWIM_OK;
+}
+
+int swim_debug_caps(swim_handle* h, uint64_t* out, size_t n) {
+  if (!h || !out || n > 8) return SWIM_EINVAL;
+  if (h->grp) return SWIM_EUNSUPPORTED;
+  const uint64_t v[8] = {h->d.SPR, h->d.BCAP, h->d.RCAP, h->d.RPCAP, h->d.HCAP, h->growths, 0, 0};
+  for (size_t i = 0; i < n; ++i) out[i] = v[i];
   return SWIM_OK;
 }
 

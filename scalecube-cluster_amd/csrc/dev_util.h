@@ -256,6 +256,18 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* ctr) {
   return base + rank;
 }
 
+// wave_append for the lanes with pred (every lane of the wave calls it; the others get an unused index)
+__device__ __forceinline__ uint32_t wave_append_if(uint32_t* ctr, bool pred) {
+  const uint64_t mask = __ballot(pred);
+  if (!mask) return 0u;
+  const uint32_t lane = __lane_id();
+  const uint32_t leader = (uint32_t)__ffsll((unsigned long long)mask) - 1u;
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(ctr, (uint32_t)__popcll(mask));
+  base = __shfl(base, (int)leader);
+  return base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+}
+
 // reserve n entries per lane on a shared counter with ONE atomic per wave; every lane of the wave must call it
 // (inactive work passes n = 0). Returns the lane's first index.
 __device__ __forceinline__ uint32_t wave_reserve(uint32_t* ctr, uint32_t n) {
@@ -418,6 +430,14 @@ __device__ __forceinline__ void tick_flag(const Dev& d, uint32_t k, bool spec) {
   d.nmsg[nb] = 0;
   d.arena_used[nb] = 0;
   *d.pool_used = 0;
+  if (d.rfill) {  // the previous gossip plane's peaks, for the host's capacity growth (api.hip grow_caps)
+    d.hflag[2] = *d.rfill;
+    d.hflag[3] = *d.rc_n;
+    d.hflag[4] = *d.rp_n;
+    d.hflag[5] = *d.slow_n;
+    d.hflag[6] = *d.hist_n;
+    *d.rfill = 0;
+  }
   *d.rc_n = 0;
   if (d.ackres) *d.ndl = 0;
   const uint32_t used =

@@ -266,6 +266,7 @@ struct Dev {
   uint32_t* fexp;   // [SLOTS] slots recycled at the end of this tick (k_gossip_free)
   uint32_t* nfexp;
   uint64_t* hist;  // [HCAP][HREC] incarnation history: tag, gid, member | n << 32, HKEEP x u32 creation ticks
+  uint32_t* hist_n;  // [1] W == 1: entries in use (grow_caps)
 
   // ---- SYNC messages (double-buffered by tick parity) ----
   SyncMsg* msgs[2];
@@ -299,6 +300,10 @@ struct Dev {
   // W > 1: the sender's write-log prefix (SyncMsg.tln entries) of each message of the inbound list committed this tick,
   // by its index there: copied by k_sync_route for this shard's senders and shipped in exchange A for the peers'
   uint32_t* mlog;     // [MSGCAP][TL]
+  // fused single-GPU tick (k_tick_front + k_member_c0, speculative batches): the latest tick each member sent a SYNC /
+  // SYNC_ACK in, the class-0 list of the tick and its count, and the diff's work-item ticket
+  uint32_t *stick, *c0list, *c0n, *dtk;
+  uint32_t front_exp;  // timing experiments only (SWIM_FRONT_EXP, wrong results): 1 = k_tick_front skips its members, 2 = its diff
 
   // ---- outputs ----
   uint32_t* ev;  // [EVCAP][8] swim_event
@@ -308,6 +313,9 @@ struct Dev {
   uint32_t* err;            // [8] bits, info...
   const Dev* self;          // device-resident copy of this struct (kernels index it through a pointer)
   uint32_t* hflag;          // host-mapped: [0] gossip slots in use after this tick's member control (W == 1)
+                            // [1] halt tick (speculative batches); with rfill: the previous gossip plane's largest
+                            // receipt-ring fill [2], routed receipts [3], replay and slow-path sends [4], [5]
+  uint32_t* rfill;          // [1] W == 1: largest ring fill (rtail - rhead) after this tick's receipts (grow_caps)
   uint32_t* dbg_send;       // debugging aid (SWIM_SEND_LOG=cap): [cap][5] tick, sender, gid lo, gid hi, target
   uint32_t* dbg_send_n;
   uint32_t dbg_send_cap;
@@ -412,6 +420,8 @@ void launch_init(const Dev& d, void* stream);
 // spec: a launch of a speculative batch (it returns at once once d.halt is set)
 void launch_diff(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr, bool spec = false);
 void launch_member(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr, bool spec = false);
+// the fused tick (d.stick != null): launch_diff + launch_member of one tick in a speculative batch
+void launch_fused(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr, bool spec = false);
 void launch_gossip(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr);
 // sharded tick (W > 1): A = SYNC diff + member control + pack exchange A; B = unpack A, gossip sends, pack
 // exchange B; C = unpack B, apply receipts, routing, slot recycling. The host runs the exchanges in between and
@@ -432,5 +442,8 @@ void launch_join(const Dev& d, uint32_t m, uint32_t k, const uint32_t* seeds, ui
 void launch_hash(const Dev& d, uint64_t* out, uint32_t now, void* stream);
 void launch_held_add(const Dev& d, const int32_t* sum, void* stream);
 void launch_s_scrub(const Dev& d, uint32_t now, void* stream);  // every SCRUB ticks: stale S entries cleared
+void launch_ring_move(const uint32_t* rg, uint32_t* rg2, const uint32_t* rhead, const uint32_t* rtail, uint32_t N,
+                      uint32_t B, uint32_t B2, void* stream);  // capacity growth of the receipt rings
+void launch_hist_rehash(const uint64_t* h1, uint32_t cap1, uint64_t* h2, uint32_t cap2, void* stream);
 
 }  // namespace swim

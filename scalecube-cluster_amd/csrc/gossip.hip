@@ -47,6 +47,7 @@ __device__ void hist_push(const Dev& d, uint64_t gid, uint32_t member, uint32_t 
     if (old == 0ull) {
       e[1] = gid;
       e[2] = member;
+      if (d.hist_n) atomicAdd(d.hist_n, 1u);  // (grow_caps doubles the table past half full)
     }
     uint32_t n = (uint32_t)(e[2] >> 32);  // total rebirths so far; the ring keeps the latest HKEEP
     uint32_t* c = (uint32_t*)(e + 3);
@@ -1040,6 +1041,7 @@ __global__ void __launch_bounds__(256) k_gossip_apply(const Dev* __restrict__ dp
     }
     if (lane == 0) {
       const uint32_t nr = b - a;
+      if (d.rfill) atomicMax(d.rfill, b - d.rhead[t]);  // the host grows the rings before they can overflow
       if (nr) {
         if (d.XW > 1)
           atomicAdd(&d.held_delta[t], (int)nr);
@@ -1142,4 +1144,40 @@ void launch_unpack_b(const Dev& d, uint32_t k, hipStream_t st) {
   hipLaunchKernelGGL(k_unpack_b, dim3(64, d.W), dim3(256), 0, st, d, k);
 }
 
+}  // namespace swim
+
+namespace swim {
+// capacity growth (api.hip grow_caps): member m's held ring entries [rhead, rtail) at their positions in a ring of B2
+// entries (positions are absolute; a ring of B entries keeps position p at p & (B - 1))
+__global__ void __launch_bounds__(256) k_ring_move(const uint32_t* rg, uint32_t* rg2, const uint32_t* rhead,
+                                                   const uint32_t* rtail, uint32_t N, uint32_t B, uint32_t B2) {
+  for (uint32_t m = blockIdx.x; m < N; m += gridDim.x) {
+    const uint32_t h = rhead[m], t = rtail[m];
+    for (uint32_t p = h + threadIdx.x; p - h < t - h; p += blockDim.x)
+      rg2[(size_t)m * B2 + (p & (B2 - 1))] = rg[(size_t)m * B + (p & (B - 1))];
+  }
+}
+void launch_ring_move(const uint32_t* rg, uint32_t* rg2, const uint32_t* rhead, const uint32_t* rtail, uint32_t N,
+                      uint32_t B, uint32_t B2, void* stream) {
+  hipLaunchKernelGGL(k_ring_move, dim3(4096), dim3(256), 0, (hipStream_t)stream, rg, rg2, rhead, rtail, N, B, B2);
+}
+
+// capacity growth: every entry of the incarnation history re-inserted into a table of cap2 entries (same probing as
+// hist_push: linear from its tag)
+__global__ void __launch_bounds__(256) k_hist_rehash(const uint64_t* h1, uint32_t cap1, uint64_t* h2, uint32_t cap2) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cap1; i += gridDim.x * blockDim.x) {
+    const uint64_t* e = h1 + (size_t)i * HREC;
+    const uint64_t tag = e[0];
+    if (!tag) continue;
+    for (uint32_t p = 0; p < cap2; ++p) {
+      unsigned long long* o = (unsigned long long*)(h2 + (size_t)((tag + p) & (cap2 - 1)) * HREC);
+      if (atomicCAS(o, 0ull, (unsigned long long)tag) != 0ull) continue;
+      for (uint32_t j = 1; j < HREC; ++j) o[j] = e[j];
+      break;
+    }
+  }
+}
+void launch_hist_rehash(const uint64_t* h1, uint32_t cap1, uint64_t* h2, uint32_t cap2, void* stream) {
+  hipLaunchKernelGGL(k_hist_rehash, dim3(2048), dim3(256), 0, (hipStream_t)stream, h1, cap1, h2, cap2);
+}
 }  // namespace swim

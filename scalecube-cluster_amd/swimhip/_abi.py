@@ -205,7 +205,20 @@ def selftest_eval(lib, op, rows, device=0):
 FB_NAMES = ["trk_walk", "ulog", "creq", "cwmax", "cev_slow", "replay", "mq", "sort_merge", "rx_all"]
 DEBUG_SIGNATURES = {
     "swim_debug_fallbacks": (C.c_int, [_H, C.POINTER(C.c_uint64), C.c_size_t]),
+    "swim_debug_caps": (C.c_int, [_H, C.POINTER(C.c_uint64), C.c_size_t]),
 }
+CAP_NAMES = ["slots", "ring", "receipts", "replay", "history", "growths"]
+
+
+def debug_caps(lib, handle):
+    """{name: size} of the structures that grow between ticks (include/swimhip_debug.h swim_debug_caps)."""
+    fn = lib.swim_debug_caps
+    fn.restype, fn.argtypes = DEBUG_SIGNATURES["swim_debug_caps"]
+    out = (C.c_uint64 * len(CAP_NAMES))()
+    rc = fn(handle, out, len(CAP_NAMES))
+    if rc != 0:
+        raise RuntimeError(f"swim_debug_caps rc={rc}")
+    return dict(zip(CAP_NAMES, (int(x) for x in out)))
 
 
 def debug_fallbacks(lib, handle):

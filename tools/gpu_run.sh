@@ -6,6 +6,7 @@
 #   benchcpu          the default bench line with its CPU baseline (the driver's command)
 #   trace:W[:S[:WU]]  rocprofv3 kernel trace + stats of the same bench command, and its per-tick breakdown
 #   pmc:W:COUNTER[:S] one rocprofv3 --pmc pass (one counter) over a bench run of workload W with S steps (default 3)
+#   rehearse:R:N[:W]  bench.py --gpus R on this one GPU (R ranks over RCCL sockets), N members, workload W (default c3)
 # Example:  gpurun --timeout 1200 -- 'bash tools/gpu_run.sh r4a suite:fullsize smoke bench:c3'
 set -e
 cd $GRAFT_REPO_ROOT
@@ -43,6 +44,7 @@ for step in "$@"; do
       grep -o '"ms_per_step": [0-9.]*\|"frac": [0-9.]*' $O/bench.json
       ;;
     trace)
+      [ -n "$TRACE_ENV" ] && export $TRACE_ENV
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/t_$a -o run --output-format csv -- \
         python3 bench.py --workload $a --steps ${b:-5} --warmup ${c:-3} --no-cpu-baseline > $O/trace_$a.log 2>&1
       python3 tools/tick_breakdown.py $O/t_$a/run_kernel_trace.csv 10 | tail -3
@@ -50,6 +52,14 @@ for step in "$@"; do
     pmc)
       timeout -s KILL 300 rocprofv3 --pmc $b -d $O/pmc_${a}_${b}_${c:-3} -o run --output-format csv -- \
         python3 bench.py --workload $a --steps ${c:-3} --warmup 1 --no-cpu-baseline > $O/pmc_${a}_${b}_${c:-3}.log 2>&1
+      ;;
+    rehearse)
+      timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node $a --master-addr 127.0.0.1 \
+        --master-port $((29500 + a)) bench.py --workload ${c:-c3} --gpus $a --steps 5 --warmup 2 --members $b \
+        --rehearse-one-gpu > $O/rehearse_${c:-c3}_w${a}_$b.log 2>&1
+      grep metric $O/rehearse_${c:-c3}_w${a}_$b.log > $O/rehearse_${c:-c3}_w${a}_$b.json
+      grep -o '"ms_per_step": [0-9.]*\|"exchange_ms_per_step": [0-9.]*\|"diff_msgs_total": [0-9]*\|"ack_resolved_total": [0-9]*\|"sync_merges": [0-9]*' \
+        $O/rehearse_${c:-c3}_w${a}_$b.json | tr '\n' ' '; echo
       ;;
     *)
       echo "unknown step $step"
