@@ -653,14 +653,6 @@ int build(swim_handle* h) {
     HIPCK(hipMemsetAsync(d.rfill, 0, 4, h->stream));
     HIPCK(hipMemsetAsync(d.hist_n, 0, 4, h->stream));
   }
-  // the fused single-GPU tick of speculative batches (k_tick_front + k_member_c0); SWIM_NO_FUSED: the two-kernel tick
-  if (d.W == 1 && !d.implicit && !d.exp && !getenv("SWIM_NO_FUSED")) {
-    d.front_exp = getenv("SWIM_FRONT_EXP") ? (uint32_t)atoi(getenv("SWIM_FRONT_EXP")) : 0u;
-    A(d.stick, N) A(d.c0list, N) A(d.c0n, 1) A(d.dtk, 8 * 32)
-    HIPCK(hipMemsetAsync(d.stick, 0xFF, 4 * N, h->stream));
-    HIPCK(hipMemsetAsync(d.c0n, 0, 4, h->stream));
-    HIPCK(hipMemsetAsync(d.dtk, 0, 4 * 8 * 32, h->stream));
-  }
   A(d.ev, (uint64_t)d.EVCAP * 8) A(d.ev_n, 1) A(d.ctr, C_NCTR) A(d.err, 8)
   if (c.flags & SWIM_FLAG_EMULATOR_COUNTERS) {
     A(d.em, 2 * N)
@@ -1348,10 +1340,6 @@ int swim_step(swim_handle* h, uint32_t n) {
       // that tick with the gossip plane.
       for (uint32_t j = i; j < nb; ++j) {
         const uint32_t kj = k + (j - i);
-        if (d.stick && need_diff) {  // the fused tick (k_tick_front + k_member_c0)
-          launch_fused(d, kj, h->stream, timed(kj) ? &h->prof[j] : nullptr, true);
-          continue;
-        }
         if (need_diff) launch_diff(d, kj, h->stream, timed(kj) ? &h->prof[j] : nullptr, true);
         launch_member(d, kj, h->stream, timed(kj) ? &h->prof[j] : nullptr, true);
         need_diff = j + 1 == nb;

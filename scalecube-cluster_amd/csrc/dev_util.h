@@ -256,18 +256,6 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* ctr) {
   return base + rank;
 }
 
-// wave_append for the lanes with pred (every lane of the wave calls it; the others get an unused index)
-__device__ __forceinline__ uint32_t wave_append_if(uint32_t* ctr, bool pred) {
-  const uint64_t mask = __ballot(pred);
-  if (!mask) return 0u;
-  const uint32_t lane = __lane_id();
-  const uint32_t leader = (uint32_t)__ffsll((unsigned long long)mask) - 1u;
-  uint32_t base = 0;
-  if (lane == leader) base = atomicAdd(ctr, (uint32_t)__popcll(mask));
-  base = __shfl(base, (int)leader);
-  return base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
-}
-
 // reserve n entries per lane on a shared counter with ONE atomic per wave; every lane of the wave must call it
 // (inactive work passes n = 0). Returns the lane's first index.
 __device__ __forceinline__ uint32_t wave_reserve(uint32_t* ctr, uint32_t n) {

@@ -300,10 +300,6 @@ struct Dev {
   // W > 1: the sender's write-log prefix (SyncMsg.tln entries) of each message of the inbound list committed this tick,
   // by its index there: copied by k_sync_route for this shard's senders and shipped in exchange A for the peers'
   uint32_t* mlog;     // [MSGCAP][TL]
-  // fused single-GPU tick (k_tick_front + k_member_c0, speculative batches): the latest tick each member sent a SYNC /
-  // SYNC_ACK in, the class-0 list of the tick and its count, and the diff's work-item ticket
-  uint32_t *stick, *c0list, *c0n, *dtk;
-  uint32_t front_exp;  // timing experiments only (SWIM_FRONT_EXP, wrong results): 1 = k_tick_front skips its members, 2 = its diff
 
   // ---- outputs ----
   uint32_t* ev;  // [EVCAP][8] swim_event
@@ -420,8 +416,6 @@ void launch_init(const Dev& d, void* stream);
 // spec: a launch of a speculative batch (it returns at once once d.halt is set)
 void launch_diff(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr, bool spec = false);
 void launch_member(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr, bool spec = false);
-// the fused tick (d.stick != null): launch_diff + launch_member of one tick in a speculative batch
-void launch_fused(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr, bool spec = false);
 void launch_gossip(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr);
 // sharded tick (W > 1): A = SYNC diff + member control + pack exchange A; B = unpack A, gossip sends, pack
 // exchange B; C = unpack B, apply receipts, routing, slot recycling. The host runs the exchanges in between and

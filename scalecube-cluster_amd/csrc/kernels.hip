@@ -7,8 +7,6 @@
 namespace swim {
 
 __global__ void k_member_tick(const Dev* __restrict__ dp, uint32_t k, uint32_t flag);  // member.hip
-__global__ void k_tick_front(const Dev* __restrict__ dp, uint32_t k, uint32_t flag, uint32_t timed);
-__global__ void k_member_c0(const Dev* __restrict__ dp, uint32_t k, uint32_t flag);
 // shard.hip
 __global__ void k_sync_route(Dev d, uint32_t b, uint32_t spec);
 __global__ void k_pack_a(Dev d, uint32_t b, uint32_t spec);
@@ -803,19 +801,6 @@ __global__ void __launch_bounds__(256) k_sync_defer(Dev d, uint32_t k, uint32_t 
     }
     __syncthreads();
   }
-}
-
-// fused single-GPU tick (d.stick allocated; speculative batches): SYNC_ACK resolution, then k_tick_front (the SYNC
-// diff beside member classes 1-3, bracketed by the profiling events when timed), then class 0 and the tick's end
-void launch_fused(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool spec) {
-  hipStream_t st = (hipStream_t)stream;
-  const uint32_t sp = spec ? 2u : 0u;
-  launch_ack_resolve(d, k, st, spec, prof != nullptr);
-  if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
-  const uint32_t nbm = cdiv(d.NL, 256);
-  hipLaunchKernelGGL(k_tick_front, dim3(nbm > 512 ? nbm : 512), dim3(256), 0, st, d.self, k, sp, prof ? 1u : 0u);
-  if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
-  hipLaunchKernelGGL(k_member_c0, dim3(1024), dim3(64), 0, st, d.self, k, sp | 1u);
 }
 
 void launch_member(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool spec) {

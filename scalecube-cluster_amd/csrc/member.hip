@@ -208,7 +208,6 @@ __device__ __forceinline__ bool send_sync(ML& L, uint32_t kind, uint32_t dst, ui
   q->cid_cnt = mm.cid_cnt, q->payload = mm.payload, q->psize = mm.psize, q->ncand = mm.ncand, q->pad = mm.pad;
   q->due = L.k + d.lat + (uint32_t)e;
   q->tln = L.ntl;
-  if (d.stick) d.stick[L.m] = L.k;  // (k_tick_front: its row is read by the next tick's diff)
   L.pend = i;
   if (e > 0) return true;  // not linked to the receiver's inbound list before its delivery tick
   // the receiver's inbound list for the next tick (sharded handles build it when the exchange commits the list);
@@ -982,10 +981,6 @@ __device__ __forceinline__ void merge_payload(ML& L, uint32_t mi, uint32_t reaso
 // control path of k_member_tick this tick, and its work class: 1 = a ping is due and nothing else, 2 = only
 // request-state events (ping hops, ack arrivals, timeouts), 3 = both, 0 = anything else (SYNC receipt, gossip
 // receipts or round, timers, host requests, start).
-// FRONT (k_tick_front): the member runs beside the SYNC diff of its tick, so everything the diff or k_ack_resolve reads
-// stays with class 0: a dead member's inbound payloads (their pins are reset in k_member_c0) and the row of a member
-// that sent a SYNC / SYNC_ACK in tick k - 1 (the payload the diff streams, or copies into its pin, is that live row)
-template <bool FRONT>
 __device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t k, uint32_t& cls, uint32_t& drops,
                                               uint32_t& evs) {
   // A dead member does nothing itself, but the remote hops of its in-flight requests still run at the live
@@ -1017,7 +1012,6 @@ __device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t
   if (dead) {
     d.rc_cnt[m] = 0;
     d.rc_fill[m] = 0;
-    if (FRONT && k > 0 && mh != NEVER) return true;  // class 0: k_member_c0 resets the pins after the diff
     if (k > 0 && mh != NEVER) {  // dropped payloads: their pins go back to NEVER (send_sync)
       const uint32_t pb = (k - 1) & 1;
       for (uint32_t q = mh; q != NEVER; q = d.m_next[(size_t)pb * d.MSGCAP + q]) d.msgs[pb][q].pin = NEVER;
@@ -1029,7 +1023,6 @@ __device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t
     const bool other = (k > 0 && mh != NEVER) | (rc != 0) | (pi != 0) | (tm <= k) | (k == ns) |
                        ((inf & INIT_ACTIVE) != 0) | (k == st) | (k == ng && held != 0);
     cls = other ? 0u : (k == np ? 1u : 0u) | (ne <= k ? 2u : 0u);
-    if (FRONT && cls != 0 && d.stick[m] + 1u == k) cls = 0;  // its row is a payload the diff streams now
     if (!busy) {
       if (k != ng) {
         d.tround[m] = 0;
@@ -1666,7 +1659,7 @@ __global__ void __launch_bounds__(256, 2) k_member_tick(const Dev* __restrict__ 
   if (threadIdx.x < CWMAX) cw[threadIdx.x].x = NEVER;  // no member until written (cow scans by member)
   const uint32_t m = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t cls = 0, drops = 0, evs = 0;
-  const bool busy = m < d.hi && member_triage<false>(d, m, k, cls, drops, evs);
+  const bool busy = m < d.hi && member_triage(d, m, k, cls, drops, evs);
   {  // the triage's record compares and folded RUMOR events, one atomic each per wave
     uint32_t v = drops, e = evs;
 #pragma unroll
@@ -1747,304 +1740,6 @@ __global__ void __launch_bounds__(256, 2) k_member_tick(const Dev* __restrict__ 
   if (!(flag & 1u)) return;
   if (!last_block_ticket(d.mdone, gridDim.x) || threadIdx.x != 0) return;
   *d.mdone = 0;
-  tick_flag(d, k, (flag & 2u) != 0);
-}
-
-// ------------------------------------------------------------------------------------------------------------
-// Fused single-GPU tick (speculative batches, gossip plane idle): k_tick_front runs the SYNC diff of
-// tick k beside the member control of every member whose tick cannot touch what the diff reads (classes 1-3: pings,
-// FD hops and timeouts of members that neither receive a payload now nor sent one in tick k - 1), then
-// k_member_c0 runs class 0 (SYNC receivers and senders, gossip, timers, host requests) once the candidates exist.
-// The diff is split into wavefront work items (one 2048-subject chunk of one message each) taken by ticket, so the
-// waves of a member block that have no member to run stream from the moment the block's triage is done.
-
-// one wavefront's work item: message mi's payload against its receiver's row over chunk c, 4 steps of 512 subjects
-// (8 per lane, 2 x 16-B loads per side). pinw: the arena row a live-row payload is copied into (pin_msg), else NEVER
-__device__ __forceinline__ void dw_fetch(const Dev& d, uint32_t b, uint32_t mi, uint32_t c, uint32_t lane,
-                                         uint4 (&x)[16], uint32_t& pinw) {
-  const SyncMsg& mm = d.msgs[b][mi];
-  const uint32_t pay = mm.payload, kind = mm.kind;
-  pinw = pay == NEVER ? mm.pin : NEVER;
-  const uint32_t* pr = pay == NEVER ? d.rowk + (size_t)mm.src * d.NS : d.arena[b] + (size_t)pay * d.NS;
-  const uint32_t* rr = d.rowk + (size_t)mm.dst * d.NS;
-#pragma unroll
-  for (uint32_t q = 0; q < 4; ++q) {
-    const uint32_t s0 = c * CH + q * 512u + lane * 8u;
-    if (s0 >= d.NS || (kind & KF_DEFER)) {  // NS is a multiple of 8: a lane's 8 subjects are wholly in or out
-      x[4 * q] = x[4 * q + 1] = x[4 * q + 2] = x[4 * q + 3] = make_uint4(0, 0, 0, 0);
-    } else {
-      x[4 * q] = ld_c4(pr + s0);
-      x[4 * q + 1] = ld_c4(pr + s0 + 4);
-      x[4 * q + 2] = ld_c4(rr + s0);
-      x[4 * q + 3] = ld_c4(rr + s0 + 4);
-    }
-  }
-}
-
-// the differing records of the item, in subject order, into the candidate pool (k_sync_diff's output form)
-__device__ __forceinline__ void dw_process(const Dev& d, uint32_t b, uint32_t mi, uint32_t c, uint32_t lane,
-                                           const uint4 (&x)[16], uint32_t pinw) {
-  uint32_t msk[4], ab = 0, nc = 0;
-#pragma unroll
-  for (uint32_t q = 0; q < 4; ++q) {
-    const uint32_t p[8] = {x[4 * q].x, x[4 * q].y, x[4 * q].z, x[4 * q].w,
-                           x[4 * q + 1].x, x[4 * q + 1].y, x[4 * q + 1].z, x[4 * q + 1].w};
-    const uint32_t r[8] = {x[4 * q + 2].x, x[4 * q + 2].y, x[4 * q + 2].z, x[4 * q + 2].w,
-                           x[4 * q + 3].x, x[4 * q + 3].y, x[4 * q + 3].z, x[4 * q + 3].w};
-    uint32_t mk = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if ((p[j] & 3u) != ST_ABSENT && p[j] != r[j]) mk |= 1u << j;
-      ab |= (uint32_t)((p[j] & 3u) == ST_ABSENT && (r[j] & 3u) != ST_ABSENT);
-    }
-    msk[q] = mk;
-    nc += __popc(mk);
-  }
-  if (pinw != NEVER) {  // a live-row payload read again later in this tick (pin_msg): its copy, as streamed
-#pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) {
-      const uint32_t s0 = c * CH + q * 512u + lane * 8u;
-      if (s0 < d.NS) {
-        uint4* dst = (uint4*)(d.arena[b] + (size_t)pinw * d.NS + s0);
-        dst[0] = x[4 * q];
-        dst[1] = x[4 * q + 1];
-      }
-    }
-  }
-  const bool anyc = __ballot(nc != 0) != 0ull, anyab = __ballot(ab != 0) != 0ull;
-  uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NCHUNK + c) * 2;
-  if (!anyc) {  // steady state: the whole chunk matches
-    if (lane == 0) {
-      cm[0] = 0;
-      cm[1] = 0;
-      if (anyab && d.ackres) atomicOr(&d.msgs[b][mi].kind, KF_ABS);
-    }
-    return;
-  }
-  // place: step-major, then lane, then the lane's subjects (= subject order)
-  uint32_t base = 0, off[4], run = 0;
-#pragma unroll
-  for (uint32_t q = 0; q < 4; ++q) {
-    const uint32_t v = __popc(msk[q]);
-    uint32_t incl = v;
-#pragma unroll
-    for (uint32_t o = 1; o < 64; o <<= 1) {
-      const uint32_t t = __shfl_up(incl, o);
-      if (lane >= o) incl += t;
-    }
-    off[q] = run + incl - v;
-    run += __shfl(incl, 63);
-  }
-  if (lane == 0) {
-    base = atomicAdd(d.pool_used, run);
-    if (base + run > d.POOLCAP) {  // no room: nothing of this item is written (the error aborts the step)
-      atomicOr(d.err, E_POOL);
-      base = NEVER;
-    }
-    cm[0] = base;
-    cm[1] = base == NEVER ? 0u : run;
-    if (base != NEVER) atomicAdd(&d.msgs[b][mi].ncand, run);
-    if (anyab && d.ackres) atomicOr(&d.msgs[b][mi].kind, KF_ABS);
-  }
-  base = __shfl(base, 0);
-  if (base == NEVER) return;
-#pragma unroll
-  for (uint32_t q = 0; q < 4; ++q) {
-    const uint32_t s0 = c * CH + q * 512u + lane * 8u;
-    const uint32_t p[8] = {x[4 * q].x, x[4 * q].y, x[4 * q].z, x[4 * q].w,
-                           x[4 * q + 1].x, x[4 * q + 1].y, x[4 * q + 1].z, x[4 * q + 1].w};
-    uint32_t o = base + off[q];
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (msk[q] & (1u << j)) d.pool[o++] = ((uint64_t)(s0 + j) << 34) | key34(p[j]);
-  }
-}
-
-// Work items by ticket until none is left; the next item's loads are in flight while the current one is tested. One
-// counter for every wave serialises at its L2 channel (~13 ns per atomic: 16k items took ~250 us at C3), so the items
-// are split into DTK contiguous ranges with a counter each; a wave starts on the range of its block's XCD (blocks are
-// placed round robin) and moves on to the next range when its own is empty.
-constexpr uint32_t DTK = 8;
-__device__ __forceinline__ void dw_stream(const Dev& d, uint32_t b, uint32_t lane) {
-  const uint32_t nmsg = d.ackres ? *(volatile uint32_t*)d.ndl : min(d.nmsg[b], d.MSGCAP);
-  const uint32_t total = nmsg * d.NCHUNK, nch = d.NCHUNK;
-  uint32_t r = blockIdx.x % DTK;  // r counts up to r + DTK: every range once
-  const uint32_t r_end = r + DTK;
-  auto next = [&]() -> uint32_t {
-    for (; r < r_end; ++r) {
-      const uint32_t q = r % DTK;
-      uint32_t i = 0;
-      if (lane == 0) i = atomicAdd(d.dtk + q * 32, 1u);  // counters 128 B apart (one L2 line each)
-      i = __shfl(i, 0);
-      const uint32_t lo = (uint32_t)((uint64_t)total * q / DTK), hi = (uint32_t)((uint64_t)total * (q + 1) / DTK);
-      if (lo + i < hi) return lo + i;
-    }
-    return NEVER;
-  };
-  uint32_t it = next();
-  if (it == NEVER) return;
-  uint4 cur[16];
-  uint32_t mcur = d.ackres ? d.dlist[it / nch] : it / nch, ccur = it % nch, pcur;
-  dw_fetch(d, b, mcur, ccur, lane, cur, pcur);
-  for (;;) {
-    const uint32_t nx = next();
-    uint4 nxt[16];
-    uint32_t mn = 0, cn = 0, pn = NEVER;
-    if (nx != NEVER) {
-      mn = d.ackres ? d.dlist[nx / nch] : nx / nch;
-      cn = nx % nch;
-      dw_fetch(d, b, mn, cn, lane, nxt, pn);
-    }
-    dw_process(d, b, mcur, ccur, lane, cur, pcur);
-    if (nx == NEVER) return;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) cur[q] = nxt[q];
-    mcur = mn;
-    ccur = cn;
-    pcur = pn;
-  }
-}
-
-// the per-wave deferred copy-on-write snapshots of the members a wave ran (the wave's list in LDS; see k_member_tick)
-__device__ __forceinline__ void cow_wave(const Dev& d, uint32_t k, const uint4* cw, uint32_t ncw, uint32_t lane) {
-  for (uint32_t q = 0; q < ncw; ++q) {
-    const uint4 e = cw[q];
-    if (e.x == NEVER) continue;  // made by its lane already (cow_now)
-    const uint32_t b = k & 1;
-    const size_t li = lidx(d, e.x);
-    const uint4* src4 = (const uint4*)(d.rowk + li * d.NS);
-    uint4* dst4 = (uint4*)(d.arena[b] + (size_t)e.y * d.NS);
-    for (uint32_t s = lane; s < d.NS / 4; s += 64) dst4[s] = src4[s];
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) {
-      uint32_t* dst = d.arena[b] + (size_t)e.y * d.NS;
-      const uint32_t* lg = d.ulog + li * ULOG * 2;
-      for (uint32_t j = e.w; j-- > e.z;) dst[lg[2 * j]] = lg[2 * j + 1];
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-
-// the busy members of a wave (me != NEVER) through the control path; counters wave-reduced
-__device__ __forceinline__ void run_members(const Dev& d, uint32_t me, uint32_t k, uint4* cw, uint32_t* cw_n,
-                                            uint32_t lane) {
-  unsigned long long cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (me != NEVER) member_tick_body(d, me, k, cnt, cw, cw_n);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    unsigned long long v = cnt[i];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      uint32_t lo = __shfl_xor((uint32_t)v, o), hi = __shfl_xor((uint32_t)(v >> 32), o);
-      v += ((unsigned long long)hi << 32) | lo;
-    }
-    if (lane == 0 && v) atomicAdd(&d.ctr[i], v);
-  }
-  __builtin_amdgcn_wave_barrier();
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  cow_wave(d, k, cw, min(*cw_n, d.cwmax_cap), lane);
-}
-
-// Blocks [0, ceil(N / 256)): triage of 256 members; class 0 goes to the list of k_member_c0, classes 1-3 are
-// compacted onto the block's first waves and run there; every wave then streams diff items. The other blocks
-// stream from the start. flag & 2: a launch of a speculative batch.
-__global__ void __launch_bounds__(256, 2) k_tick_front(const Dev* __restrict__ dp, uint32_t k, uint32_t flag,
-                                                       uint32_t timed) {
-  const Dev& d = *dp;
-  if ((flag & 2u) && *(volatile uint32_t*)d.halt) return;  // a speculative batch halted at an earlier tick
-  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const uint32_t b = (k - 1) & 1;  // the messages of tick k - 1 (k > 0)
-  if (k > 0 && blockIdx.x == 0 && threadIdx.x == 0) {
-    const uint32_t nmsg = d.ackres ? *(volatile uint32_t*)d.ndl : min(d.nmsg[b], d.MSGCAP);
-    atomicAdd(&d.ctr[C_DIFFMSG_ALL], (unsigned long long)nmsg);
-    if (timed) atomicAdd(&d.ctr[C_DIFFMSG], (unsigned long long)nmsg);
-  }
-  const uint32_t nbm = (d.NL + 255) / 256;
-  if (blockIdx.x < nbm) {
-    __shared__ uint32_t wc[4][4];
-    __shared__ uint32_t list[256];
-    __shared__ uint4 cw[4][CWMAX];
-    __shared__ uint32_t cw_n[4];
-    if (lane == 0) cw_n[w] = 0;
-    if (lane < CWMAX) cw[w][lane].x = NEVER;
-    const uint32_t m = d.lo + blockIdx.x * 256 + threadIdx.x;
-    uint32_t cls = 0, drops = 0, evs = 0;
-    const bool busy = m < d.hi && member_triage<true>(d, m, k, cls, drops, evs);
-    {
-      uint32_t v = drops, e = evs;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o), e += __shfl_xor(e, o);
-      if (lane == 0 && v) atomicAdd(&d.ctr[C_R], (unsigned long long)v);
-      if (lane == 0 && e) atomicAdd(&d.ctr[C_E], (unsigned long long)e);
-    }
-    const bool c0 = busy && cls == 0;
-    const uint32_t ci = wave_append_if(d.c0n, c0);
-    if (c0) d.c0list[ci] = m;
-    const uint64_t b1 = __ballot(busy && cls == 1), b2 = __ballot(busy && cls == 2), b3 = __ballot(busy && cls == 3);
-    if (lane == 0) {
-      wc[w][1] = (uint32_t)__popcll(b1);
-      wc[w][2] = (uint32_t)__popcll(b2);
-      wc[w][3] = (uint32_t)__popcll(b3);
-    }
-    list[threadIdx.x] = NEVER;
-    __syncthreads();
-    uint32_t aligned = 0, dense = 0, all = 0, before = 0;
-    for (uint32_t c = 1; c < 4; ++c) {
-      const uint32_t t = wc[0][c] + wc[1][c] + wc[2][c] + wc[3][c];
-      all += (t + 63u) & ~63u;
-      if (c < cls) aligned += (t + 63u) & ~63u, dense += t;
-    }
-    if (busy && cls != 0) {
-      const uint32_t start = all <= 256 ? aligned : dense;  // classes on wave boundaries when they fit, else packed
-      for (uint32_t j = 0; j < w; ++j) before += wc[j][cls];
-      const uint64_t bal = cls == 1 ? b1 : cls == 2 ? b2 : b3;
-      list[start + before + __popcll(bal & ((1ull << lane) - 1ull))] = m;
-    }
-    __syncthreads();
-    const uint32_t me = list[threadIdx.x];
-    if (!(d.front_exp & 1u) && __ballot(me != NEVER)) run_members(d, me, k, cw[w], &cw_n[w], lane);
-  }
-  if (k > 0 && !(d.front_exp & 2u)) dw_stream(d, b, lane);
-}
-
-// class 0 of the tick, after the diff: one wavefront per 64 listed members (list order is not observable: every
-// member's work is its own, and the appends it makes are ordered by id where order matters). The block that
-// finishes last runs the end-of-tick resets (tick_flag).
-__global__ void __launch_bounds__(64) k_member_c0(const Dev* __restrict__ dp, uint32_t k, uint32_t flag) {
-  const Dev& d = *dp;
-  if ((flag & 2u) && *(volatile uint32_t*)d.halt) return;
-  __shared__ uint4 cw[CWMAX];
-  __shared__ uint32_t cw_n;
-  // a few members per wave: class 0 mixes work kinds (a SYNC receiver, a sender, a timer), and the lanes of a wave
-  // walk the union of their paths, so a full wave of them would chain every kind's latency (C0W per wave, as the
-  // two-kernel tick's blocks happened to hold)
-  constexpr uint32_t C0W = 4;
-  const uint32_t lane = threadIdx.x, n = *(volatile uint32_t*)d.c0n;
-  for (uint32_t base = blockIdx.x; base < n; base += gridDim.x * C0W) {
-    if (lane == 0) cw_n = 0;
-    if (lane < CWMAX) cw[lane].x = NEVER;
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t e = base + lane * gridDim.x;
-    uint32_t me = lane < C0W && e < n ? d.c0list[e] : NEVER;
-    if (me != NEVER && dead_at(d, me, k)) {  // the triage's dead path, deferred past the diff (member_triage)
-      const uint32_t pb = (k - 1) & 1, mh = d.m_head[(size_t)pb * d.N + me];
-      if (k > 0 && mh != NEVER) {
-        for (uint32_t q = mh; q != NEVER; q = d.m_next[(size_t)pb * d.MSGCAP + q]) d.msgs[pb][q].pin = NEVER;
-        d.m_head[(size_t)pb * d.N + me] = NEVER;
-      }
-      if (d.npath[me] == 0 && (d.nfetch[me] == 0 || d.fnext[me] > k)) {
-        d.tround[me] = 0;
-        me = NEVER;
-      }
-    }
-    run_members(d, me, k, cw, &cw_n, lane);
-  }
-  if (!(flag & 1u)) return;
-  if (!last_block_ticket(d.mdone, gridDim.x) || threadIdx.x != 0) return;
-  *d.mdone = 0;
-  *d.c0n = 0;
-  for (uint32_t q = 0; q < DTK; ++q) d.dtk[q * 32] = 0;
   tick_flag(d, k, (flag & 2u) != 0);
 }
 
