@@ -502,10 +502,6 @@ int build(swim_handle* h) {
     }
     d.EMAX = (uint32_t)t.size();
     d.PCAP = c.delay_cap_ms ? PATHCAP_DELAY : PATHCAP;
-    if (d.EMAX && d.W > 1) {
-      h->err = "link delays on a row-sharded handle";
-      return SWIM_EUNSUPPORTED;
-    }
   }
   d.LOGW = 8;
   // rounds kept for the infectedFrom replay (a delayed send arrives up to EMAX ticks after its round)
@@ -645,6 +641,14 @@ int build(swim_handle* h) {
     A(d.tlog, 2 * NL * TL) A(d.tl_n, 2 * NL) A(d.tl_tick, 2 * NL) A(d.dlist, d.MSGCAP) A(d.ndl, 1)
     if (d.W > 1) A(d.mlog, (uint64_t)d.MSGCAP * TL)
     HIPCK(hipMemsetAsync(d.tl_tick, 0xFF, 8 * NL, h->stream));
+    HIPCK(hipMemsetAsync(d.ndl, 0, 4, h->stream));
+  }
+  if (d.W == 1 && !d.implicit) {  // k_sync_diff1: the send-time message lists (dlist: what the resolvers leave)
+    if (!d.ackres) A(d.dlist, d.MSGCAP) A(d.ndl, 1)
+    A(d.slist, 2ull * d.MSGCAP) A(d.nslist, 2) A(d.rlist, 2ull * d.MSGCAP) A(d.nrlist, 2) A(d.rdone, 1)
+    HIPCK(hipMemsetAsync(d.nslist, 0, 8, h->stream));
+    HIPCK(hipMemsetAsync(d.nrlist, 0, 8, h->stream));
+    HIPCK(hipMemsetAsync(d.rdone, 0, 4, h->stream));
     HIPCK(hipMemsetAsync(d.ndl, 0, 4, h->stream));
   }
   // capacity growth between ticks (grow_caps): one GPU, without guard zones; SWIM_NO_GROW keeps the sizes fixed
@@ -1708,9 +1712,7 @@ static int delay_index(swim_handle* h, uint32_t delay_ms, uint32_t* idx) {
   if (!delay_table(delay_ms, h->cfg.tick_ms, &t)) return fail(h, SWIM_EINVAL, "mean delay above 11 x tick_ms");
   *idx = 0;
   if (t.empty()) return SWIM_OK;  // no message can be delayed past its tick
-  if (t.size() > h->d.EMAX || h->d.W > 1)
-    return fail(h, SWIM_EUNSUPPORTED, h->d.W > 1 ? "link delays on a row-sharded handle"
-                                                  : "mean delay above swim_config.delay_cap_ms");
+  if (t.size() > h->d.EMAX) return fail(h, SWIM_EUNSUPPORTED, "mean delay above swim_config.delay_cap_ms");
   for (uint32_t i = 1; i < (uint32_t)h->delays.size(); ++i)
     if (h->delays[i] == delay_ms) {
       *idx = i;
@@ -1751,7 +1753,15 @@ int swim_set_link_settings(swim_handle* h, uint32_t src, uint32_t dst, uint32_t 
 
 int swim_emulator_counters(swim_handle* h, uint64_t* out, size_t cap) {
   if (!h || !out || cap < 2ull * h->cfg.n_members) return SWIM_EINVAL;
-  if (h->grp) return fail(h, SWIM_EUNSUPPORTED, "emulator counters of a row-sharded handle");
+  if (h->grp) {  // each shard counted the sends it evaluated (its issuers' FD / SYNC / metadata, its targets' gossip)
+    std::vector<uint64_t> part(2ull * h->cfg.n_members);
+    std::fill(out, out + part.size(), 0ull);
+    return group_all(h, [&](swim_handle* s) {
+      const int rc = swim_emulator_counters(s, part.data(), part.size());
+      for (size_t i = 0; rc == SWIM_OK && i < part.size(); ++i) out[i] += part[i];
+      return rc;
+    });
+  }
   if (!h->d.em) return fail(h, SWIM_EUNSUPPORTED, "emulator counters need SWIM_FLAG_EMULATOR_COUNTERS");
   HIPCK(hipStreamSynchronize(h->stream));
   HIPCK(hipMemcpy(out, h->d.em, 16ull * h->d.N, hipMemcpyDeviceToHost));

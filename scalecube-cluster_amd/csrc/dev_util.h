@@ -197,6 +197,13 @@ __device__ __forceinline__ void delay_push(const Dev& d, uint32_t g, uint32_t t,
   else
     set_err(d, E_DELAYQ);
   atomicMax(&d.slot_exp[g], due + d.EXPB);
+  if (d.W > 1) {  // the other shards extend the slot's life the same way (exchange B: XD_EXT record, k_unpack_b)
+    const uint32_t xi = atomicAdd(d.xd_n, 1u);
+    if (xi < d.DCAP)
+      d.xd[xi] = ((uint64_t)g << 32) | XD_EXT | due;
+    else
+      set_err(d, E_DELIV);
+  }
 }
 
 // the same with the settings epoch of tick k already looked up (epoch_at once per thread, not per message)
@@ -427,7 +434,12 @@ __device__ __forceinline__ void tick_flag(const Dev& d, uint32_t k, bool spec) {
     *d.rfill = 0;
   }
   *d.rc_n = 0;
-  if (d.ackres) *d.ndl = 0;
+  if (d.ackres || d.slist) *d.ndl = 0;
+  if (d.slist) {  // the next tick's send lists; the resolvers of the next k_sync_diff1 count from zero
+    d.nslist[nb] = 0;
+    d.nrlist[nb] = 0;
+    *d.rdone = 0;
+  }
   const uint32_t used =
       (uint32_t)((int32_t)d.SPR - __hip_atomic_load(d.free_top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   d.hflag[0] = used;

@@ -77,6 +77,9 @@ constexpr uint32_t NSW = 8;               // words per new-gossip-slot record
 // exchange byte-count words: low 48 bits = bytes; bit 62 = the sender has gossip slots in use this tick
 // bit 61 = the sender has a region larger than the inline block for some peer (a send/recv group follows)
 constexpr unsigned long long XCNT_MASK = (1ull << 48) - 1, XFLAG_GOSSIP = 1ull << 62, XFLAG_OVER = 1ull << 61;
+// exchange B record (slot << 32 | low word): low = target id (< 2^31), or XD_EXT | tick: a delayed send queued on its
+// target's shard keeps the slot until tick + EXPB (delay_push), and every shard must recycle it at the same tick
+constexpr uint32_t XD_EXT = 0x80000000u;
 constexpr uint32_t XINL = 16384;  // RCCL: bytes per peer moved by the fixed-size all-to-all (count word + region head)
 
 // counters (swim_counters order after .tick)
@@ -300,6 +303,9 @@ struct Dev {
   // W > 1: the sender's write-log prefix (SyncMsg.tln entries) of each message of the inbound list committed this tick,
   // by its index there: copied by k_sync_route for this shard's senders and shipped in exchange A for the peers'
   uint32_t* mlog;     // [MSGCAP][TL]
+  // one GPU (k_sync_diff1): the messages of each tick parity as send_sync listed them, streamed (slist) or to be
+  // resolved (rlist), their counts, and the resolver blocks that have finished this launch
+  uint32_t *slist, *nslist, *rlist, *nrlist, *rdone;  // [2][MSGCAP], [2], [2][MSGCAP], [2], [1]
 
   // ---- outputs ----
   uint32_t* ev;  // [EVCAP][8] swim_event

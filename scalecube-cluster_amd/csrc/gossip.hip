@@ -959,6 +959,13 @@ __global__ void k_gossip_due(Dev d, uint32_t k) {
     if (atomicOr(hrow(d, t) + (g >> 6), bit) & bit) continue;  // held, or made a receipt by another delivery
     if (d.DM[g >> 6] & bit) d.dead_rx[t] = k + d.lat;
     receipt_mark(d, g, t, k, atomicAdd(&d.rtail[t], 1u));
+    if (d.W > 1) {  // replicated on the other shards from exchange B
+      const uint32_t xi = atomicAdd(d.xd_n, 1u);
+      if (xi < d.DCAP)
+        d.xd[xi] = ((uint64_t)g << 32) | t;
+      else
+        set_err(d, E_DELIV);
+    }
   }
 }
 __global__ void k_dq_reset(Dev d, uint32_t k) { d.dq_n[(k + d.lat) % (d.EMAX + 2u)] = 0; }
@@ -1093,6 +1100,10 @@ __global__ void k_unpack_b(Dev d, uint32_t k) {
   const uint64_t* V = (const uint64_t*)(R + 16);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nd; i += gridDim.x * blockDim.x) {
     const uint32_t g = (uint32_t)(V[i] >> 32), t = (uint32_t)V[i];
+    if (t & XD_EXT) {  // a peer's delayed send keeps the slot (delay_push)
+      atomicMax(&d.slot_exp[g], (t & ~XD_EXT) + d.EXPB);
+      continue;
+    }
     atomicOr(&hrow(d, t)[g >> 6], 1ull << (g & 63u));
     receipt_mark(d, g, t, k, atomicAdd(&d.rtail[t], 1u));
     receipt_create(d, g, t, k);

@@ -344,37 +344,26 @@ __device__ __forceinline__ void diff_fetch(const Dev& d, uint32_t b, uint32_t mi
 // walks its work items grid-strided with the next item's loads in flight while it tests the current one. SHARDED
 // adds payloads received from other shards (baseline row + shipped chunks); the single-GPU instance has only local
 // rows and snapshots.
+// the items of `nmsg` messages (list[j], or j itself without a list) over the blocks blk of nblk, grid-stride, with
+// the next item's loads in flight while the current one is tested
 template <bool SHARDED>
-__global__ void __launch_bounds__(256) k_sync_diff(const Dev* __restrict__ dp, uint32_t b, uint32_t timed, uint32_t spec) {
-  const Dev& d = *dp;  // global, not kernarg (as k_member_tick): a by-value Dev of this size was copied to scratch
-  if (spec && *(volatile uint32_t*)d.halt) return;  // a speculative batch halted at an earlier tick
-  __shared__ uint32_t scan[256];
-  __shared__ uint32_t base;
-  // (timed launches are bracketed by HIP events on the stream. A self-timing variant, first block start to last block
-  // end by wall clock and atomics, made every launch of this kernel 30 % slower by its mere presence in the code:
-  // 85 -> 112 us per launch at C3, profiles/r03_*)
-  // with SYNC_ACK resolution, only the messages k_ack_resolve left in dlist
+__device__ __forceinline__ void stream_list(const Dev& d, uint32_t b, const uint32_t* dlp, uint32_t nmsg, uint32_t blk,
+                                            uint32_t nblk, uint32_t* scan, uint32_t& base) {
   const bool dl = d.ackres != 0;
-  uint32_t nmsg = dl ? *(volatile uint32_t*)d.ndl : (d.nmsg[b] < d.MSGCAP ? d.nmsg[b] : d.MSGCAP);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    atomicAdd(&d.ctr[C_DIFFMSG_ALL], (unsigned long long)nmsg);
-    if (timed) atomicAdd(&d.ctr[C_DIFFMSG], (unsigned long long)nmsg);
-  }
-  uint32_t total = nmsg * d.NCHUNK;
-  const uint32_t* dlp = dl ? d.dlist : nullptr;
+  const uint32_t total = nmsg * d.NCHUNK;
   const uint32_t nch = d.NCHUNK;
   uint4 cur[4];
   uint32_t mcur = 0, pcur = NEVER;
-  if (blockIdx.x < total) {
-    mcur = dlp ? dlp[blockIdx.x / nch] : blockIdx.x / nch;
-    diff_fetch<SHARDED>(d, b, mcur, blockIdx.x % nch, cur, pcur);
+  if (blk < total) {
+    mcur = dlp ? dlp[blk / nch] : blk / nch;
+    diff_fetch<SHARDED>(d, b, mcur, blk % nch, cur, pcur);
   }
-  for (uint32_t w = blockIdx.x; w < total; w += gridDim.x) {
+  for (uint32_t w = blk; w < total; w += nblk) {
     uint4 nxt[4];
     uint32_t mnxt = 0, pnxt = NEVER;
-    if (w + gridDim.x < total) {
-      mnxt = dlp ? dlp[(w + gridDim.x) / nch] : (w + gridDim.x) / nch;
-      diff_fetch<SHARDED>(d, b, mnxt, (w + gridDim.x) % nch, nxt, pnxt);
+    if (w + nblk < total) {
+      mnxt = dlp ? dlp[(w + nblk) / nch] : (w + nblk) / nch;
+      diff_fetch<SHARDED>(d, b, mnxt, (w + nblk) % nch, nxt, pnxt);
     }
     const uint32_t mi = mcur, c = w % nch;
     const uint32_t s0 = c * CH + threadIdx.x * 8;
@@ -439,6 +428,31 @@ __global__ void __launch_bounds__(256) k_sync_diff(const Dev* __restrict__ dp, u
   }
 }
 
+// k_sync_diff: for every SYNC / SYNC_ACK sent in tick k-1, stream the payload's key plane (the sender's live row,
+// or its copy-on-write snapshot) against the receiver's key plane and extract, per 2048-subject chunk and in
+// subject order, the records that differ (the eager `!r1.equals(table.get(id))` filter of syncMembership,
+// :456-467). This is the HBM-bound hot loop: 2 x 4 B read per subject per merge (key32, swim_common.h). Each block
+// walks its work items grid-stride with the next item's loads in flight while it tests the current one. SHARDED
+// adds payloads received from other shards (baseline row + shipped chunks). The single-GPU tick uses k_sync_diff1.
+template <bool SHARDED>
+__global__ void __launch_bounds__(256) k_sync_diff(const Dev* __restrict__ dp, uint32_t b, uint32_t timed, uint32_t spec) {
+  const Dev& d = *dp;  // global, not kernarg (as k_member_tick): a by-value Dev of this size was copied to scratch
+  if (spec && *(volatile uint32_t*)d.halt) return;  // a speculative batch halted at an earlier tick
+  __shared__ uint32_t scan[256];
+  __shared__ uint32_t base;
+  // (timed launches are bracketed by HIP events on the stream. A self-timing variant, first block start to last block
+  // end by wall clock and atomics, made every launch of this kernel 30 % slower by its mere presence in the code:
+  // 85 -> 112 us per launch at C3, profiles/r03_*)
+  // with SYNC_ACK resolution, only the messages k_ack_resolve left in dlist
+  const bool dl = d.ackres != 0;
+  uint32_t nmsg = dl ? *(volatile uint32_t*)d.ndl : (d.nmsg[b] < d.MSGCAP ? d.nmsg[b] : d.MSGCAP);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    atomicAdd(&d.ctr[C_DIFFMSG_ALL], (unsigned long long)nmsg);
+    if (timed) atomicAdd(&d.ctr[C_DIFFMSG], (unsigned long long)nmsg);
+  }
+  stream_list<SHARDED>(d, b, dl ? d.dlist : nullptr, nmsg, blockIdx.x, gridDim.x, scan, base);
+}
+
 // ------------------------------------------------------------------------------------------------------------
 // k_ack_resolve (W == 1): the SYNC_ACKs of tick k-1 whose diff follows from logs instead of a stream.
 // Member A's SYNC of tick k-2 carried A's row as of its send; B's diff at tick k-1 extracted D = {s : payload[s] !=
@@ -477,6 +491,79 @@ __device__ __forceinline__ uint32_t res_payload_key(const ResArgs& d, uint32_t p
   for (uint32_t q = 0; q < (c >> 6); ++q) rank += __popcll(mk[q]);
   return ((const uint32_t*)(d.xa_recv + d.rx_off[ri]))[(size_t)rank * CH + v % CH];
 }
+// one SYNC_ACK (message i of buffer d.msgs) by one wave: true if it was resolved from the write logs (its candidates
+// written), false if k_sync_diff must stream it
+__device__ __forceinline__ bool res_wave(const ResArgs& d, uint32_t i, uint32_t k, uint32_t lane, volatile uint32_t* sv,
+                                         volatile uint32_t* sc) {
+  const SyncMsg& mm = d.msgs[i];
+  const uint32_t kind = mm.kind, src = mm.src, dst = mm.dst, tln = mm.tln, pay = mm.payload;
+  bool res = k >= 2 && (kind & KF_RES) && !(kind & KF_DEFER) && mm.pin == NEVER && tln <= TL;
+  uint32_t n0 = 0, n1 = 0;  // A's log entries of ticks k-2 and k-1
+  const uint32_t ld = dst - d.lo;  // the requester: an observer of this shard
+  if (res) {
+    const size_t a0 = (size_t)(k & 1) * d.NL + ld, a1 = (size_t)((k - 1) & 1) * d.NL + ld;
+    n0 = d.tl_tick[a0] == k - 2 ? d.tl_n[a0] : 0u;
+    n1 = d.tl_tick[a1] == k - 1 ? d.tl_n[a1] : 0u;
+    res = n0 <= TL && n1 <= TL;
+  }
+  const uint32_t nall = tln + n0 + n1;
+  if (!res) return false;
+  if (nall == 0) {  // nothing written on either side and nothing merged: nothing can differ
+    if (lane == 0) d.msgs[i].ncand = 0;
+    return true;
+  }
+  // gather: B's prefix, then A's two ticks (at most 3 TL <= 64 subjects, one per lane)
+  uint32_t v = NEVER;
+  if (lane < tln)  // W > 1: the prefix came with the message (the responder may live on another shard)
+    v = d.W > 1 ? d.mlog[(size_t)i * TL + lane] : d.tlog[((size_t)((k - 1) & 1) * d.NL + src) * TL + lane];
+  else if (lane < tln + n0) v = d.tlog[((size_t)(k & 1) * d.NL + ld) * TL + (lane - tln)];
+  else if (lane < tln + n0 + n1) v = d.tlog[((size_t)((k - 1) & 1) * d.NL + ld) * TL + (lane - tln - n0)];
+  sv[lane] = v;
+  __builtin_amdgcn_wave_barrier();
+  bool first = v != NEVER;
+  for (uint32_t j = 0; j < min(lane, nall); ++j) first &= sv[j] != v;
+  uint32_t key = 0;
+  bool cand = false;
+  if (first) {
+    key = res_payload_key(d, pay, src, v);
+    cand = (key & 3u) != ST_ABSENT && key != d.rowk[(size_t)ld * d.NS + v];
+  }
+  sc[lane] = cand ? v : NEVER;
+  __builtin_amdgcn_wave_barrier();
+  const uint64_t cb = __ballot(cand);
+  const uint32_t total = (uint32_t)__popcll(cb);
+  uint32_t off = 0;
+  if (total) {  // (wave-uniform; none in the C3 steady state)
+    uint32_t pos = 0;
+    for (uint32_t j = 0; j < nall; ++j) pos += sc[j] < v;
+    if (lane == 0) {
+      off = atomicAdd(d.pool_used, total);
+      if (off + total > d.POOLCAP) {
+        atomicOr(d.err, E_POOL);
+        off = NEVER;
+      }
+    }
+    off = __shfl(off, 0);
+    if (cand && off != NEVER) d.pool[(size_t)off + pos] = ((uint64_t)v << 34) | key34(key);
+  }
+  // per chunk: first candidate and count (the chunk walk of merge_payload, which reads none of it when ncand is 0)
+  if (total && off != NEVER)
+    for (uint32_t c = lane; c < d.NCHUNK; c += 64) {
+      uint32_t before = 0, in = 0;
+      for (uint32_t j = 0; j < nall; ++j) {
+        const uint32_t t = sc[j];
+        before += t < c * CH;
+        in += t != NEVER && t / CH == c;
+      }
+      uint32_t* cm = d.chunk_meta + ((size_t)i * d.NCHUNK + c) * 2;
+      cm[0] = off + before;
+      cm[1] = in;
+    }
+  if (lane == 0) d.msgs[i].ncand = off == NEVER ? 0u : total;
+  return true;
+}
+
+// sharded handles: every message of the tick, one wave each; the unresolved ones go to the list k_sync_diff streams
 __global__ void __launch_bounds__(512) k_ack_resolve(ResArgs d, uint32_t k, uint32_t spec, uint32_t timed) {
   if (spec && *(volatile uint32_t*)d.halt) return;
   __shared__ uint32_t sv_[8][64], sc_[8][64];
@@ -492,77 +579,10 @@ __global__ void __launch_bounds__(512) k_ack_resolve(ResArgs d, uint32_t k, uint
     __syncthreads();
     const uint32_t i = base + wv;
     if (i < nmsg) {  // wave-uniform
-      const SyncMsg& mm = d.msgs[i];
-      const uint32_t kind = mm.kind, src = mm.src, dst = mm.dst, tln = mm.tln, pay = mm.payload;
-      bool res = k >= 2 && (kind & KF_RES) && !(kind & KF_DEFER) && mm.pin == NEVER && tln <= TL;
-      uint32_t n0 = 0, n1 = 0;  // A's log entries of ticks k-2 and k-1
-      const uint32_t ld = dst - d.lo;  // the requester: an observer of this shard
-      if (res) {
-        const size_t a0 = (size_t)(k & 1) * d.NL + ld, a1 = (size_t)((k - 1) & 1) * d.NL + ld;
-        n0 = d.tl_tick[a0] == k - 2 ? d.tl_n[a0] : 0u;
-        n1 = d.tl_tick[a1] == k - 1 ? d.tl_n[a1] : 0u;
-        res = n0 <= TL && n1 <= TL;
-      }
-      const uint32_t nall = tln + n0 + n1;
-      if (!res) {
-        if (lane == 0) slist[atomicAdd(&nstream, 1u)] = i;
-      } else if (nall == 0) {  // nothing written on either side and nothing merged: nothing can differ
-        if (lane == 0) {
-          d.msgs[i].ncand = 0;
-          atomicAdd(&nres, 1u);
-        }
-      } else {
-        // gather: B's prefix, then A's two ticks (at most 3 TL <= 64 subjects, one per lane)
-        uint32_t v = NEVER;
-        if (lane < tln)  // W > 1: the prefix came with the message (the responder may live on another shard)
-          v = d.W > 1 ? d.mlog[(size_t)i * TL + lane] : d.tlog[((size_t)((k - 1) & 1) * d.NL + src) * TL + lane];
-        else if (lane < tln + n0) v = d.tlog[((size_t)(k & 1) * d.NL + ld) * TL + (lane - tln)];
-        else if (lane < tln + n0 + n1) v = d.tlog[((size_t)((k - 1) & 1) * d.NL + ld) * TL + (lane - tln - n0)];
-        sv[lane] = v;
-        __builtin_amdgcn_wave_barrier();
-        bool first = v != NEVER;
-        for (uint32_t j = 0; j < min(lane, nall); ++j) first &= sv[j] != v;
-        uint32_t key = 0;
-        bool cand = false;
-        if (first) {
-          key = res_payload_key(d, pay, src, v);
-          cand = (key & 3u) != ST_ABSENT && key != d.rowk[(size_t)ld * d.NS + v];
-        }
-        sc[lane] = cand ? v : NEVER;
-        __builtin_amdgcn_wave_barrier();
-        const uint64_t cb = __ballot(cand);
-        const uint32_t total = (uint32_t)__popcll(cb);
-        uint32_t off = 0;
-        if (total) {  // (wave-uniform; none in the C3 steady state)
-          uint32_t pos = 0;
-          for (uint32_t j = 0; j < nall; ++j) pos += sc[j] < v;
-          if (lane == 0) {
-            off = atomicAdd(d.pool_used, total);
-            if (off + total > d.POOLCAP) {
-              atomicOr(d.err, E_POOL);
-              off = NEVER;
-            }
-          }
-          off = __shfl(off, 0);
-          if (cand && off != NEVER) d.pool[(size_t)off + pos] = ((uint64_t)v << 34) | key34(key);
-        }
-        // per chunk: first candidate and count (the chunk walk of merge_payload, which reads none of it when ncand is 0)
-        if (total && off != NEVER)
-          for (uint32_t c = lane; c < d.NCHUNK; c += 64) {
-            uint32_t before = 0, in = 0;
-            for (uint32_t j = 0; j < nall; ++j) {
-              const uint32_t t = sc[j];
-              before += t < c * CH;
-              in += t != NEVER && t / CH == c;
-            }
-            uint32_t* cm = d.chunk_meta + ((size_t)i * d.NCHUNK + c) * 2;
-            cm[0] = off + before;
-            cm[1] = in;
-          }
-        if (lane == 0) {
-          d.msgs[i].ncand = off == NEVER ? 0u : total;
-          atomicAdd(&nres, 1u);
-        }
+      if (res_wave(d, i, k, lane, sv, sc)) {
+        if (lane == 0) atomicAdd(&nres, 1u);
+      } else if (lane == 0) {
+        slist[atomicAdd(&nstream, 1u)] = i;
       }
     }
     __syncthreads();
@@ -577,6 +597,68 @@ __global__ void __launch_bounds__(512) k_ack_resolve(ResArgs d, uint32_t k, uint
     if (threadIdx.x < nstream) d.dlist[sbase + threadIdx.x] = slist[threadIdx.x];
     __syncthreads();  // (slist and the counts are reused)
   }
+}
+
+// k_sync_diff1 (one GPU): SYNC_ACK resolution and the stream in one launch. The member kernel listed each message it
+// sent by what it is (send_sync): the ones that are streamed anyway (SYNCs, late and unresolvable SYNC_ACKs:
+// slist) and the SYNC_ACKs sent in the tick of their SYNC (rlist). Blocks [0, RESB) resolve rlist, a wave per message,
+// and list what they cannot resolve (dlist); the other blocks stream slist at once, then dlist once every resolver
+// block has arrived (they are the first blocks of the grid and wait for nothing, so they are resident; the wait is
+// bounded all the same and raises E_PIN if it ever ran out). The ~5 us resolve launch and its gap leave the tick.
+constexpr uint32_t RESB = 64;
+__global__ void __launch_bounds__(256) k_sync_diff1(const Dev* __restrict__ dp, ResArgs ra, uint32_t b, uint32_t k,
+                                                    uint32_t timed, uint32_t spec) {
+  const Dev& d = *dp;
+  if (spec && *(volatile uint32_t*)d.halt) return;
+  __shared__ uint32_t scan[256];
+  __shared__ uint32_t base, nres;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (blockIdx.x < RESB) {
+    __shared__ uint32_t sv_[4][64], sc_[4][64];
+    if (threadIdx.x == 0) nres = 0;
+    __syncthreads();
+    const uint32_t nr = min(d.nrlist[b], d.MSGCAP);
+    for (uint32_t j = blockIdx.x * 4 + wv; j < nr; j += RESB * 4) {  // wave-uniform
+      const uint32_t i = d.rlist[(size_t)b * d.MSGCAP + j];
+      if (res_wave(ra, i, k, lane, sv_[wv], sc_[wv])) {
+        if (lane == 0) atomicAdd(&nres, 1u);
+      } else if (lane == 0) {
+        d.dlist[atomicAdd(d.ndl, 1u)] = i;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      if (nres) {
+        atomicAdd(&d.ctr[C_ACKRES_ALL], (unsigned long long)nres);
+        if (timed) atomicAdd(&d.ctr[C_ACKRES], (unsigned long long)nres);
+      }
+      __threadfence();  // the dlist entries before the arrival
+      atomicAdd(d.rdone, 1u);
+    }
+    return;
+  }
+  const uint32_t blk = blockIdx.x - RESB, nblk = gridDim.x - RESB;
+  const uint32_t ns = min(d.nslist[b], d.MSGCAP);
+  stream_list<false>(d, b, d.slist + (size_t)b * d.MSGCAP, ns, blk, nblk, scan, base);
+  if (threadIdx.x == 0) {
+    uint32_t spins = 0;
+    while (__hip_atomic_load(d.rdone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < RESB) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins == (1u << 22)) {
+        set_err(d, E_PIN);
+        break;
+      }
+    }
+    base = *(volatile uint32_t*)d.ndl;
+  }
+  __syncthreads();
+  const uint32_t nd = base;
+  if (blk == 0 && threadIdx.x == 0) {
+    atomicAdd(&d.ctr[C_DIFFMSG_ALL], (unsigned long long)(ns + nd));
+    if (timed) atomicAdd(&d.ctr[C_DIFFMSG], (unsigned long long)(ns + nd));
+  }
+  __syncthreads();
+  if (nd) stream_list<false>(d, b, d.dlist, nd, blk, nblk, scan, base);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -689,13 +771,15 @@ void launch_init(const Dev& d, void* stream) {
 }
 
 // timed: this launch is bracketed by profiling events; it adds its message count to ctr[C_DIFFMSG]
+// 8 resident blocks per CU; SWIM_DIFF_GRID overrides it (measurements; a value that does not parse, or 0, keeps 2048)
+static uint32_t diff_grid() {
+  const char* e = getenv("SWIM_DIFF_GRID");
+  const unsigned long v = e ? strtoul(e, nullptr, 0) : 0ul;
+  return v >= 1 && v <= (1ul << 20) ? (uint32_t)v : 2048u;
+}
+
 static void launch_sync_diff(const Dev& d, uint32_t b, hipStream_t st, uint32_t timed, uint32_t spec = 0) {
-  // 8 resident blocks per CU; SWIM_DIFF_GRID overrides it (measurements; a value that does not parse, or 0, keeps 2048)
-  static const uint32_t grid = [] {
-    const char* e = getenv("SWIM_DIFF_GRID");
-    const unsigned long v = e ? strtoul(e, nullptr, 0) : 0ul;
-    return v >= 1 && v <= (1ul << 20) ? (uint32_t)v : 2048u;
-  }();
+  static const uint32_t grid = diff_grid();
   if (d.W > 1)
     hipLaunchKernelGGL(k_sync_diff<true>, dim3(grid), dim3(256), 0, st, d.self, b, timed, spec);
   else
@@ -716,6 +800,22 @@ static void launch_ack_resolve(const Dev& d, uint32_t k, hipStream_t st, bool sp
 
 void launch_diff(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool spec) {
   hipStream_t st = (hipStream_t)stream;
+  if (d.slist) {  // one GPU: resolution and stream in one launch
+    if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
+    if (k > 0) {
+      static const uint32_t grid = diff_grid();
+      const uint32_t b = (k - 1) & 1;
+      const ResArgs ra{d.halt, d.nmsg + b, d.tl_tick, d.tl_n, d.tlog, d.rowk, d.arena[b], d.msgs[b], d.dlist, d.ndl,
+                       d.chunk_meta, d.pool_used, d.err, d.pool, d.ctr, d.NL, d.NS, d.MSGCAP, d.NCHUNK, d.POOLCAP,
+                       d.lo, d.W, d.MW, d.mlog, d.base_row, d.rx_mask, d.rx_off, d.xa_recv};
+      // the whole grid resident at once (8 blocks per CU): a block that cannot start until another ends would
+      // stream its share after the others (~25 us longer per launch with RESB blocks on top of 2048)
+      hipLaunchKernelGGL(k_sync_diff1, dim3(grid > 2 * RESB ? grid : 2 * RESB), dim3(256), 0, st, d.self, ra, b, k,
+                         prof ? 1u : 0u, spec ? 1u : 0u);
+    }
+    if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
+    return;
+  }
   launch_ack_resolve(d, k, st, spec, prof != nullptr);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
   if (k > 0) launch_sync_diff(d, (k - 1) & 1, st, prof ? 1u : 0u, spec ? 1u : 0u);
@@ -756,6 +856,7 @@ __global__ void __launch_bounds__(256) k_sync_redeliver(Dev d, uint32_t k, uint3
         m.pad = NEVER;
         m.pin = NEVER;
         d.msgs[b][i] = m;
+        if (d.slist) d.slist[(size_t)b * d.MSGCAP + atomicAdd(&d.nslist[b], 1u)] = i;  // streamed (k_sync_diff1)
         const uint32_t old = atomicExch(&d.m_head[(size_t)b * d.N + m.dst], i);
         d.m_next[(size_t)b * d.MSGCAP + i] = old;
         if (old != NEVER) {
@@ -794,6 +895,94 @@ __global__ void __launch_bounds__(256) k_sync_defer(Dev d, uint32_t k, uint32_t 
       const uint32_t* src = mm.payload == NEVER ? d.rowk + lidx(d, mm.src) * d.NS : d.arena[b] + (size_t)mm.payload * d.NS;
       uint32_t* dst = d.ds_row + (size_t)e * d.NS;
       for (uint32_t s = threadIdx.x; s < d.NS; s += blockDim.x) dst[s] = src[s];
+      if (threadIdx.x == 0) {
+        d.ds_msg[e] = mm;
+        d.ds_used[e] = 1;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Row-sharded handles (W > 1): a delayed SYNC / SYNC_ACK travels to its receiver's shard in the tick it is sent (the
+// route and exchange A carry it like any other message, flagged KF_DEFER, and msgs_commit leaves it out of the inbound
+// lists); the receiver's shard stores it with its payload as sent at the end of that tick (k_sync_defer_x), and puts
+// it back into the inbound list of the tick before its delivery (k_sync_redeliver_x, before the list is committed).
+__global__ void __launch_bounds__(256) k_sync_redeliver_x(Dev d, uint32_t k, uint32_t spec) {
+  if (spec) {  // a speculative batch halted at an earlier tick
+    const uint32_t hk = *(volatile uint32_t*)d.halt;
+    if (hk != 0 && hk <= k) return;
+  }
+  __shared__ uint32_t slot[2];
+  const uint32_t b = k & 1;
+  for (uint32_t e = blockIdx.x; e < d.DSCAP; e += gridDim.x) {
+    if (!d.ds_used[e] || d.ds_msg[e].due != k + 1u) continue;
+    if (threadIdx.x == 0) {
+      slot[0] = atomicAdd(&d.xn[4], 1u);
+      slot[1] = atomicAdd(&d.arena_used[b], 1u);
+      if (slot[0] >= d.MSGCAP) set_err(d, E_MSGS);
+      if (slot[1] >= d.ARENA_ROWS) set_err(d, E_ARENA);
+    }
+    __syncthreads();
+    const uint32_t j = slot[0], r = slot[1];
+    if (j < d.MSGCAP && r < d.ARENA_ROWS) {
+      const uint32_t* src = d.ds_row + (size_t)e * d.NS;
+      uint32_t* dst = d.arena[b] + (size_t)r * d.NS;
+      for (uint32_t s = threadIdx.x; s < d.NS; s += blockDim.x) dst[s] = src[s];
+      if (threadIdx.x == 0) {
+        SyncMsg m = d.ds_msg[e];
+        m.kind = (m.kind & ~KF_DEFER) | KF_LATE;
+        m.payload = r;
+        m.ncand = 0;
+        m.pad = NEVER;
+        m.pin = NEVER;
+        d.mtmp[j] = m;
+      }
+    }
+    if (threadIdx.x == 0) {
+      d.ds_used[e] = 0;
+      d.ds_free[atomicAdd(d.ds_top, 1)] = e;
+    }
+    __syncthreads();
+  }
+}
+__global__ void __launch_bounds__(256) k_sync_defer_x(Dev d, uint32_t k, uint32_t spec) {
+  if (spec) {  // this tick's list was not committed (the batch halted at it or earlier)
+    const uint32_t hk = *(volatile uint32_t*)d.halt;
+    if (hk != 0 && hk <= k + 1u) return;
+  }
+  __shared__ int32_t slot;
+  const uint32_t b = k & 1, n = min(d.nmsg[b], d.MSGCAP);
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const SyncMsg mm = d.msgs[b][i];
+    if (!(mm.kind & KF_DEFER)) continue;
+    if (threadIdx.x == 0) {
+      const int32_t top = atomicSub(d.ds_top, 1) - 1;
+      slot = top >= 0 ? (int32_t)d.ds_free[top] : -1;
+      if (top < 0) set_err(d, E_SYNCQ);
+    }
+    __syncthreads();
+    const int32_t e = slot;
+    if (e >= 0) {  // the payload as sent: this shard's sender's row or snapshot, or the chunks a peer shipped
+      uint32_t* dst = d.ds_row + (size_t)e * d.NS;
+      if (mm.payload & PAY_RX && mm.payload != NEVER) {
+        const uint32_t ri = mm.payload & ~PAY_RX;
+        const uint64_t* mk = d.rx_mask + (size_t)ri * d.MW;
+        const uint32_t* data = (const uint32_t*)(d.xa_recv + d.rx_off[ri]);
+        for (uint32_t s = threadIdx.x; s < d.NS; s += blockDim.x) {
+          const uint32_t c = s / CH;
+          uint32_t v = d.base_row[s];
+          if ((mk[c >> 6] >> (c & 63)) & 1ull) {
+            uint32_t rank = __popcll(mk[c >> 6] & ((1ull << (c & 63)) - 1ull));
+            for (uint32_t q = 0; q < (c >> 6); ++q) rank += __popcll(mk[q]);
+            v = data[(size_t)rank * CH + s % CH];
+          }
+          dst[s] = v;
+        }
+      } else {
+        const uint32_t* src = mm.payload == NEVER ? d.rowk + lidx(d, mm.src) * d.NS : d.arena[b] + (size_t)mm.payload * d.NS;
+        for (uint32_t s = threadIdx.x; s < d.NS; s += blockDim.x) dst[s] = src[s];
+      }
       if (threadIdx.x == 0) {
         d.ds_msg[e] = mm;
         d.ds_used[e] = 1;
@@ -858,6 +1047,7 @@ void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k, spec ? 2u : 0u);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[3], st);
   hipLaunchKernelGGL(k_sync_route, dim3(cdiv(d.MSGCAP, 256)), dim3(256), 0, st, d, b, sp);
+  if (d.dly_on) hipLaunchKernelGGL(k_sync_redeliver_x, dim3(256), dim3(256), 0, st, d, k, sp);
   hipLaunchKernelGGL(k_pack_a, dim3(d.W), dim3(256), 0, st, d, b, sp);
   hipLaunchKernelGGL(k_pack_a_chunks, dim3(64, d.W), dim3(256), 0, st, d, b, sp);
 }
@@ -865,6 +1055,7 @@ void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
 void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool gossip, bool spec) {
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(k_unpack_a, dim3(32, d.W), dim3(256), 0, st, d, k, gossip ? 0u : 1u, spec ? 1u : 0u);
+  if (d.dly_on) hipLaunchKernelGGL(k_sync_defer_x, dim3(256), dim3(256), 0, st, d, k, spec ? 1u : 0u);
   if (!gossip) {  // no gossip slot in use on any shard: nothing to send, deliver or recycle; no exchange B
     if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[4], st);
     if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[5], st);

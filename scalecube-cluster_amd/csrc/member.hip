@@ -210,6 +210,12 @@ __device__ __forceinline__ bool send_sync(ML& L, uint32_t kind, uint32_t dst, ui
   q->tln = L.ntl;
   L.pend = i;
   if (e > 0) return true;  // not linked to the receiver's inbound list before its delivery tick
+  if (d.slist) {  // k_sync_diff1's lists: resolved from the write logs if it can be, else streamed
+    if (mm.kind & KF_RES)
+      d.rlist[(size_t)b * d.MSGCAP + wave_append(&d.nrlist[b])] = i;
+    else
+      d.slist[(size_t)b * d.MSGCAP + wave_append(&d.nslist[b])] = i;
+  }
   // the receiver's inbound list for the next tick (sharded handles build it when the exchange commits the list);
   // a receiver with several payloads gets them pinned (pin_msg)
   if (d.W == 1) {

@@ -182,6 +182,7 @@ __device__ void msgs_commit(const Dev& d, uint32_t b) {
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    if (d.mtmp[i].kind & KF_DEFER) continue;  // delivered later: stored by k_sync_defer_x at the end of this tick
     const uint32_t old = atomicExch(&d.m_head[(size_t)b * d.N + d.mtmp[i].dst], i);
     d.m_next[(size_t)b * d.MSGCAP + i] = old;
     if (old != NEVER) {

@@ -281,6 +281,22 @@ class ThreadShardGroup:
         for s in self.shards:
             s.set_link_loss(src, dst, pct)
 
+    def set_default_link_settings(self, loss, mean_delay_ms):
+        for s in self.shards:
+            s.set_default_link_settings(loss, mean_delay_ms)
+
+    def set_link_settings(self, src, dst, loss, mean_delay_ms):
+        for s in self.shards:
+            s.set_link_settings(src, dst, loss, mean_delay_ms)
+
+    def emulator_counters(self):
+        """Every member's (sent, lost) NetworkEmulator counters: each shard counted the sends it evaluated (its issuers'
+        FD / SYNC / metadata messages, the gossip sends to its targets), so the shards' arrays add up."""
+        out = self.shards[0].emulator_counters().copy()
+        for s in self.shards[1:]:
+            out += s.emulator_counters()
+        return out
+
     def block(self, src, *dsts):
         for s in self.shards:
             s.block(src, *dsts)

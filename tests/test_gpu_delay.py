@@ -121,3 +121,79 @@ def test_delay_cap_enforced(engine):
     with pytest.raises(Exception):
         c.emulator_counters()  # SWIM_FLAG_EMULATOR_COUNTERS not set
     c.close()
+
+
+# ---- the same on sharded handles: delayed SYNC / SYNC_ACK messages stored on the receiver's shard,
+# delayed gossip receipts queued on the target's shard and replicated through exchange B, emulator counters summed
+
+
+def sharded(oracle, engine, cfg, world):
+    from swimhip.shard import ThreadShardGroup
+    return SimulatedCluster(oracle, cfg), ThreadShardGroup(engine, cfg, world)
+
+
+@pytest.mark.parametrize("n,loss,delay", [g for g in GRID if g[0] >= 10])
+def test_gossip_protocol_grid_sharded(oracle, engine, n, loss, delay):
+    """RUMOR mode on 2 slot shards: each shard's own gossips' sends, delays and counters."""
+    cfg = SimConfig(n_members=n, mode=_abi.MODE_RUMOR, record_events=True, emulator_counters=True, delay_cap_ms=100)
+    o, e = sharded(oracle, engine, cfg, 2)
+    for c in (o, e):
+        c.set_default_link_settings(loss, delay)
+        c.spread_gossip(0, 0xC0FFEE)
+        c.spread_gossip(n - 1, 0xBEEF)
+    run_lockstep(o, e, sweep_ticks(cfg) + 30, 5, f"grid x2 N={n} loss={loss} delay={delay}")
+    same_emulators(o, e, "grid x2")
+    e.close()
+
+
+@pytest.mark.parametrize("delay,world", [(100, 2), (400, 3), (1100, 2)])
+def test_full_stack_delays_sharded(oracle, engine, delay, world):
+    """Row-sharded: every message kind late, kills, incarnation and metadata updates (the grid of the unsharded case)."""
+    cfg = SimConfig(n_members=40, cluster=ClusterConfig(syncInterval=3000, metadataTimeout=1000), record_events=True,
+                    emulator_counters=True, delay_cap_ms=1100, gossip_slot_cap=8192)
+    o, e = sharded(oracle, engine, cfg, world)
+    for c in (o, e):
+        c.set_default_link_settings(5, delay)
+    run_lockstep(o, e, 200, 20, f"x{world} delay {delay} warm")
+    for c in (o, e):
+        c.kill(7)
+        c.update_incarnation(3)
+        c.update_metadata(11)
+    run_lockstep(o, e, 400, 40, f"x{world} delay {delay} kill")
+    same_emulators(o, e, f"x{world} delay {delay}")
+    e.close()
+
+
+def test_per_link_delays_and_partition_sharded(oracle, engine):
+    n = 32
+    cfg = SimConfig(n_members=n, cluster=ClusterConfig(syncInterval=2000), record_events=True, emulator_counters=True,
+                    delay_cap_ms=800)
+    o, e = sharded(oracle, engine, cfg, 2)
+    g = np.array([0] * (n // 2) + [1] * (n // 2), dtype=np.uint32)
+    for c in (o, e):
+        c.set_default_link_settings(2, 200)
+        for s in range(0, n, 3):
+            c.set_link_settings(s, (s + 5) % n, 10, 800)
+            c.set_link_settings((s + 7) % n, s, 0, 50)
+        c.set_link_loss(4, 9, 20)
+    run_lockstep(o, e, 150, 25, "x2 per-link delays")
+    for c in (o, e):
+        c.partition(g)
+    run_lockstep(o, e, 250, 50, "x2 partitioned")
+    for c in (o, e):
+        c.unblock_all()
+        c.set_default_link_settings(0, 100)
+    run_lockstep(o, e, 300, 50, "x2 healed")
+    same_emulators(o, e, "x2 per-link")
+    e.close()
+
+
+def test_cold_join_with_delays_sharded(oracle, engine):
+    cfg = SimConfig(n_members=48, cluster=ClusterConfig(seedMembers=[0, 5]), init_mode=_abi.INIT_COLD_JOIN,
+                    record_events=True, emulator_counters=True, delay_cap_ms=300)
+    o, e = sharded(oracle, engine, cfg, 2)
+    for c in (o, e):
+        c.set_default_link_settings(0, 300)
+    run_lockstep(o, e, 300, 25, "x2 cold join, 300 ms delays")
+    same_emulators(o, e, "x2 cold join")
+    e.close()

@@ -7,6 +7,8 @@
 #   trace:W[:S[:WU]]  rocprofv3 kernel trace + stats of the same bench command, and its per-tick breakdown
 #   pmc:W:COUNTER[:S] one rocprofv3 --pmc pass (one counter) over a bench run of workload W with S steps (default 3)
 #   rehearse:R:N[:W]  bench.py --gpus R on this one GPU (R ranks over RCCL sockets), N members, workload W (default c3)
+#   c4:N              the C4 schedule at N members (tools/exp_c4.py: partition, unblockAll at period 200, run to 320)
+#   c5m               rank 0 of 8 C5 slot shards at 10^6 members alone (bench.py --rehearse-shard 8), default caps
 # Example:  gpurun --timeout 1200 -- 'bash tools/gpu_run.sh r4a suite:fullsize smoke bench:c3'
 set -e
 cd $GRAFT_REPO_ROOT
@@ -60,6 +62,16 @@ for step in "$@"; do
       grep metric $O/rehearse_${c:-c3}_w${a}_$b.log > $O/rehearse_${c:-c3}_w${a}_$b.json
       grep -o '"ms_per_step": [0-9.]*\|"exchange_ms_per_step": [0-9.]*\|"diff_msgs_total": [0-9]*\|"ack_resolved_total": [0-9]*\|"sync_merges": [0-9]*' \
         $O/rehearse_${c:-c3}_w${a}_$b.json | tr '\n' ' '; echo
+      ;;
+    c4)
+      timeout -k 10 900 python3 -u tools/exp_c4.py $a 200 320 > $O/c4_$a.log 2>&1 || { tail -3 $O/c4_$a.log; exit 1; }
+      tail -2 $O/c4_$a.log
+      ;;
+    c5m)
+      timeout -k 10 900 python3 -u bench.py --workload c5 --members 1000000 --rehearse-shard 8 --steps 3 --warmup 25 \
+        --no-cpu-baseline > $O/c5_1M_shard.log 2>&1 || { grep -v amdgpu $O/c5_1M_shard.log | tail -5; exit 1; }
+      grep metric $O/c5_1M_shard.log > $O/c5_1M_shard.json
+      grep -o '"ms_per_step": [0-9.]*\|"device_bytes": [0-9]*' $O/c5_1M_shard.json | tr '\n' ' '; echo
       ;;
     *)
       echo "unknown step $step"
