@@ -192,7 +192,9 @@ int swim_set_link_settings(swim_handle* h, uint32_t src, uint32_t dst, uint32_t 
 /* every member's NetworkEmulator counters (totalMessageSentCount / totalMessageLostCount, NetworkEmulator.java:200-222):
  * out[2m] = sent, out[2m + 1] = lost, cap >= 2 * n_members. tryFail and tryDelay each count a send, so a delivered
  * message counts 2 and a lost one 1 (+1 lost); sends to a dead member fail before the emulator and are not counted.
- * The engine needs SWIM_FLAG_EMULATOR_COUNTERS (else SWIM_EUNSUPPORTED). */
+ * The engine needs SWIM_FLAG_EMULATOR_COUNTERS (else SWIM_EUNSUPPORTED). On an n_gpus handle: the sum over its
+ * shards; on one shard of swim_create_sharded: the sends that shard evaluated (its observers' FD / SYNC / metadata
+ * messages, the gossip sends to its targets), so the shards' arrays add up to the cluster's. */
 int swim_emulator_counters(swim_handle* h, uint64_t* out, size_t cap);
 /* MembershipProtocolImpl.updateIncarnation (:178-190): the member bumps its own incarnation and spreads it, at the
  * start (P0) of the next tick; what ClusterImpl.updateMetadata does after storing new metadata */
