@@ -643,14 +643,6 @@ int build(swim_handle* h) {
     HIPCK(hipMemsetAsync(d.tl_tick, 0xFF, 8 * NL, h->stream));
     HIPCK(hipMemsetAsync(d.ndl, 0, 4, h->stream));
   }
-  if (d.W == 1 && !d.implicit) {  // k_sync_diff1: the send-time message lists (dlist: what the resolvers leave)
-    if (!d.ackres) A(d.dlist, d.MSGCAP) A(d.ndl, 1)
-    A(d.slist, 2ull * d.MSGCAP) A(d.nslist, 2) A(d.rlist, 2ull * d.MSGCAP) A(d.nrlist, 2) A(d.rdone, 1)
-    HIPCK(hipMemsetAsync(d.nslist, 0, 8, h->stream));
-    HIPCK(hipMemsetAsync(d.nrlist, 0, 8, h->stream));
-    HIPCK(hipMemsetAsync(d.rdone, 0, 4, h->stream));
-    HIPCK(hipMemsetAsync(d.ndl, 0, 4, h->stream));
-  }
   // capacity growth between ticks (grow_caps): one GPU, without guard zones; SWIM_NO_GROW keeps the sizes fixed
   if (d.W == 1 && !getenv("SWIM_NO_GROW") && !getenv("SWIM_GUARD")) {
     A(d.rfill, 1) A(d.hist_n, 1)

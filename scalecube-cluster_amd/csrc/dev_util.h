@@ -434,12 +434,7 @@ __device__ __forceinline__ void tick_flag(const Dev& d, uint32_t k, bool spec) {
     *d.rfill = 0;
   }
   *d.rc_n = 0;
-  if (d.ackres || d.slist) *d.ndl = 0;
-  if (d.slist) {  // the next tick's send lists; the resolvers of the next k_sync_diff1 count from zero
-    d.nslist[nb] = 0;
-    d.nrlist[nb] = 0;
-    *d.rdone = 0;
-  }
+  if (d.ackres) *d.ndl = 0;
   const uint32_t used =
       (uint32_t)((int32_t)d.SPR - __hip_atomic_load(d.free_top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   d.hflag[0] = used;

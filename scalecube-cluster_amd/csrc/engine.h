@@ -303,9 +303,6 @@ struct Dev {
   // W > 1: the sender's write-log prefix (SyncMsg.tln entries) of each message of the inbound list committed this tick,
   // by its index there: copied by k_sync_route for this shard's senders and shipped in exchange A for the peers'
   uint32_t* mlog;     // [MSGCAP][TL]
-  // one GPU (k_sync_diff1): the messages of each tick parity as send_sync listed them, streamed (slist) or to be
-  // resolved (rlist), their counts, and the resolver blocks that have finished this launch
-  uint32_t *slist, *nslist, *rlist, *nrlist, *rdone;  // [2][MSGCAP], [2], [2][MSGCAP], [2], [1]
 
   // ---- outputs ----
   uint32_t* ev;  // [EVCAP][8] swim_event

@@ -433,7 +433,8 @@ __device__ __forceinline__ void stream_list(const Dev& d, uint32_t b, const uint
 // subject order, the records that differ (the eager `!r1.equals(table.get(id))` filter of syncMembership,
 // :456-467). This is the HBM-bound hot loop: 2 x 4 B read per subject per merge (key32, swim_common.h). Each block
 // walks its work items grid-stride with the next item's loads in flight while it tests the current one. SHARDED
-// adds payloads received from other shards (baseline row + shipped chunks). The single-GPU tick uses k_sync_diff1.
+// adds payloads received from other shards (baseline row + shipped chunks); the single-GPU instance has only local
+// rows and snapshots.
 template <bool SHARDED>
 __global__ void __launch_bounds__(256) k_sync_diff(const Dev* __restrict__ dp, uint32_t b, uint32_t timed, uint32_t spec) {
   const Dev& d = *dp;  // global, not kernarg (as k_member_tick): a by-value Dev of this size was copied to scratch
@@ -599,68 +600,6 @@ __global__ void __launch_bounds__(512) k_ack_resolve(ResArgs d, uint32_t k, uint
   }
 }
 
-// k_sync_diff1 (one GPU): SYNC_ACK resolution and the stream in one launch. The member kernel listed each message it
-// sent by what it is (send_sync): the ones that are streamed anyway (SYNCs, late and unresolvable SYNC_ACKs:
-// slist) and the SYNC_ACKs sent in the tick of their SYNC (rlist). Blocks [0, RESB) resolve rlist, a wave per message,
-// and list what they cannot resolve (dlist); the other blocks stream slist at once, then dlist once every resolver
-// block has arrived (they are the first blocks of the grid and wait for nothing, so they are resident; the wait is
-// bounded all the same and raises E_PIN if it ever ran out). The ~5 us resolve launch and its gap leave the tick.
-constexpr uint32_t RESB = 64;
-__global__ void __launch_bounds__(256) k_sync_diff1(const Dev* __restrict__ dp, ResArgs ra, uint32_t b, uint32_t k,
-                                                    uint32_t timed, uint32_t spec) {
-  const Dev& d = *dp;
-  if (spec && *(volatile uint32_t*)d.halt) return;
-  __shared__ uint32_t scan[256];
-  __shared__ uint32_t base, nres;
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (blockIdx.x < RESB) {
-    __shared__ uint32_t sv_[4][64], sc_[4][64];
-    if (threadIdx.x == 0) nres = 0;
-    __syncthreads();
-    const uint32_t nr = min(d.nrlist[b], d.MSGCAP);
-    for (uint32_t j = blockIdx.x * 4 + wv; j < nr; j += RESB * 4) {  // wave-uniform
-      const uint32_t i = d.rlist[(size_t)b * d.MSGCAP + j];
-      if (res_wave(ra, i, k, lane, sv_[wv], sc_[wv])) {
-        if (lane == 0) atomicAdd(&nres, 1u);
-      } else if (lane == 0) {
-        d.dlist[atomicAdd(d.ndl, 1u)] = i;
-      }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      if (nres) {
-        atomicAdd(&d.ctr[C_ACKRES_ALL], (unsigned long long)nres);
-        if (timed) atomicAdd(&d.ctr[C_ACKRES], (unsigned long long)nres);
-      }
-      __threadfence();  // the dlist entries before the arrival
-      atomicAdd(d.rdone, 1u);
-    }
-    return;
-  }
-  const uint32_t blk = blockIdx.x - RESB, nblk = gridDim.x - RESB;
-  const uint32_t ns = min(d.nslist[b], d.MSGCAP);
-  stream_list<false>(d, b, d.slist + (size_t)b * d.MSGCAP, ns, blk, nblk, scan, base);
-  if (threadIdx.x == 0) {
-    uint32_t spins = 0;
-    while (__hip_atomic_load(d.rdone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < RESB) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins == (1u << 22)) {
-        set_err(d, E_PIN);
-        break;
-      }
-    }
-    base = *(volatile uint32_t*)d.ndl;
-  }
-  __syncthreads();
-  const uint32_t nd = base;
-  if (blk == 0 && threadIdx.x == 0) {
-    atomicAdd(&d.ctr[C_DIFFMSG_ALL], (unsigned long long)(ns + nd));
-    if (timed) atomicAdd(&d.ctr[C_DIFFMSG], (unsigned long long)(ns + nd));
-  }
-  __syncthreads();
-  if (nd) stream_list<false>(d, b, d.dlist, nd, blk, nblk, scan, base);
-}
-
 // ------------------------------------------------------------------------------------------------------------
 // state hashes (SEMANTICS.md §8), one block per member
 __global__ void __launch_bounds__(256) k_hash(Dev d, uint64_t* out, uint32_t now) {
@@ -800,22 +739,6 @@ static void launch_ack_resolve(const Dev& d, uint32_t k, hipStream_t st, bool sp
 
 void launch_diff(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool spec) {
   hipStream_t st = (hipStream_t)stream;
-  if (d.slist) {  // one GPU: resolution and stream in one launch
-    if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
-    if (k > 0) {
-      static const uint32_t grid = diff_grid();
-      const uint32_t b = (k - 1) & 1;
-      const ResArgs ra{d.halt, d.nmsg + b, d.tl_tick, d.tl_n, d.tlog, d.rowk, d.arena[b], d.msgs[b], d.dlist, d.ndl,
-                       d.chunk_meta, d.pool_used, d.err, d.pool, d.ctr, d.NL, d.NS, d.MSGCAP, d.NCHUNK, d.POOLCAP,
-                       d.lo, d.W, d.MW, d.mlog, d.base_row, d.rx_mask, d.rx_off, d.xa_recv};
-      // the whole grid resident at once (8 blocks per CU): a block that cannot start until another ends would
-      // stream its share after the others (~25 us longer per launch with RESB blocks on top of 2048)
-      hipLaunchKernelGGL(k_sync_diff1, dim3(grid > 2 * RESB ? grid : 2 * RESB), dim3(256), 0, st, d.self, ra, b, k,
-                         prof ? 1u : 0u, spec ? 1u : 0u);
-    }
-    if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
-    return;
-  }
   launch_ack_resolve(d, k, st, spec, prof != nullptr);
   if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
   if (k > 0) launch_sync_diff(d, (k - 1) & 1, st, prof ? 1u : 0u, spec ? 1u : 0u);
@@ -856,7 +779,6 @@ __global__ void __launch_bounds__(256) k_sync_redeliver(Dev d, uint32_t k, uint3
         m.pad = NEVER;
         m.pin = NEVER;
         d.msgs[b][i] = m;
-        if (d.slist) d.slist[(size_t)b * d.MSGCAP + atomicAdd(&d.nslist[b], 1u)] = i;  // streamed (k_sync_diff1)
         const uint32_t old = atomicExch(&d.m_head[(size_t)b * d.N + m.dst], i);
         d.m_next[(size_t)b * d.MSGCAP + i] = old;
         if (old != NEVER) {

@@ -210,12 +210,6 @@ __device__ __forceinline__ bool send_sync(ML& L, uint32_t kind, uint32_t dst, ui
   q->tln = L.ntl;
   L.pend = i;
   if (e > 0) return true;  // not linked to the receiver's inbound list before its delivery tick
-  if (d.slist) {  // k_sync_diff1's lists: resolved from the write logs if it can be, else streamed
-    if (mm.kind & KF_RES)
-      d.rlist[(size_t)b * d.MSGCAP + wave_append(&d.nrlist[b])] = i;
-    else
-      d.slist[(size_t)b * d.MSGCAP + wave_append(&d.nslist[b])] = i;
-  }
   // the receiver's inbound list for the next tick (sharded handles build it when the exchange commits the list);
   // a receiver with several payloads gets them pinned (pin_msg)
   if (d.W == 1) {
@@ -1693,7 +1687,8 @@ __global__ void __launch_bounds__(256, 2) k_member_tick(const Dev* __restrict__ 
   const uint32_t start = all <= 256 ? aligned : dense;  // classes on wave boundaries when they fit, else packed
   for (uint32_t j = 0; j < w; ++j) before += wc[j][cls];
   const uint64_t bal = cls == 0 ? b0 : cls == 1 ? b1 : cls == 2 ? b2 : b3;
-  if (busy) list[start + before + __popcll(bal & ((1ull << lane) - 1ull))] = m | (cls << 30);  // m < 2^30
+  uint32_t slot = start + before + __popcll(bal & ((1ull << lane) - 1ull));
+  if (busy) list[slot] = m | (cls << 30);  // m < 2^30
   __syncthreads();
   const uint32_t ent = list[threadIdx.x], me = ent == NEVER ? NEVER : (ent & 0x3FFFFFFFu), mcls = ent >> 30;
   if (wtime) {  // [1]: after triage, with the wave's class mix in the top byte
