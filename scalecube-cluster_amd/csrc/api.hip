@@ -72,6 +72,7 @@ struct swim_handle {
   bool no_spec = getenv("SWIM_NO_SPECULATION") != nullptr;  // debugging aid: a host wait after every member kernel
   bool gossip_idle = false;  // W == 1: no gossip slot was in use after the latest member kernel
   uint64_t growths = 0;      // capacity growth steps so far (grow_caps)
+  uint64_t grow_next = 0;    // grow_caps: no attempt before this tick (the last one found no room)
   // timing aid (bench.py --rehearse-shard): a slot shard alone, its peers' gossip-count deltas taken as zero without
   // any exchange (not the W-shard simulation's results)
   bool lone = getenv("SWIM_LONE_SHARD") != nullptr;
@@ -150,6 +151,10 @@ int grow_caps(swim_handle* h) {
   while (hcap2 < hwant && hcap2 < (1ull << 28)) hcap2 <<= 1;
   const bool gh = hcap2 > d.HCAP;
   if (!gs && !gr && !grc && !grp && !gh) return SWIM_OK;
+  // an attempt the free HBM could not serve is not repeated every tick (each one waits for the stream): the sizes
+  // that fit stay, and the next attempt is SCRUB ticks later
+  if (h->tick < h->grow_next) return SWIM_OK;
+  const uint64_t bytes0 = h->bytes, growths0 = h->growths;
   HIPCK(hipStreamSynchronize(h->stream));
   size_t fr = 0, tot = 0;
   HIPCK(hipMemGetInfo(&fr, &tot));
@@ -264,6 +269,10 @@ int grow_caps(swim_handle* h) {
       d.SPR = d.SLOTS = (uint32_t)s2;
       d.QW = (uint32_t)q2;
     }
+  }
+  if (h->bytes == bytes0 && h->growths == growths0) {  // nothing fitted
+    h->grow_next = h->tick + SCRUB;
+    return SWIM_OK;
   }
   HIPCK(h2d(st, (void*)d.self, &d, sizeof(Dev)));
   h->growths++;
@@ -525,13 +534,15 @@ int build(swim_handle* h) {
   // default: 64 slots per member, at most 32 GB of holder table (C2's SYNC re-spread storm keeps ~10^5 gossips alive)
   uint64_t slots = c.gossip_slot_cap ? c.gossip_slot_cap
                                      : std::min<uint64_t>(1ull << 22, std::max<uint64_t>(1024, std::min<uint64_t>(64 * N, (32ull << 30) / (4 * N))));
-  // RUMOR mode with churn (C5): the rumors alive together follow from the config. A rumor's receipts come within
-  // ~maxSpread rounds of its creation and its slot is recycled EXPB = 2 maxSpread + 4 rounds after the last one, so
-  // about churn x (3 maxSpread + 4) gossip intervals' worth are alive, split over the XW slot shards (+10 %); a member
-  // holds the ones of its last 2 maxSpread + 3 rounds (its receipt ring, below). Growth (grow_caps) covers the rest.
+  // RUMOR mode with churn (C5): the rumors alive together follow from the config. A rumor reaches every member in
+  // about 2 log2(N) rounds and its slot is recycled EXPB = 2 maxSpread + 4 rounds after its last receipt, so about
+  // churn x (2 maxSpread + 4 + 2 bitlen(N)) gossip intervals' worth are alive, split over the XW slot shards (+10 %);
+  // a member holds the ones of its last 2 maxSpread + 3 rounds (its receipt ring, below). Growth (grow_caps) covers
+  // what this misses.
   uint64_t rumor_ring = 0;
   if (!c.gossip_slot_cap && c.mode == SWIM_MODE_RUMOR && c.churn_per_period) {
-    const uint64_t life = (3ull * maxSpread + 4) * d.gossip_t, held = (2ull * maxSpread + 3) * d.gossip_t;
+    const uint64_t life = (2ull * maxSpread + 4 + 2ull * bitlen(d.N)) * d.gossip_t;
+    const uint64_t held = (2ull * maxSpread + 3) * d.gossip_t;
     slots = std::min<uint64_t>(1ull << 22, std::max<uint64_t>(1024, 11 * c.churn_per_period * life / (10 * d.ping_t * d.XW)));
     rumor_ring = 21 * c.churn_per_period * held / (20 * d.ping_t * d.XW);
   }
