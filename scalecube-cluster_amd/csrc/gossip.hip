@@ -47,7 +47,9 @@ __device__ void hist_push(const Dev& d, uint64_t gid, uint32_t member, uint32_t 
     if (old == 0ull) {
       e[1] = gid;
       e[2] = member;
-      if (d.hist_n) atomicAdd(d.hist_n, 1u);  // (grow_caps doubles the table past half full)
+      // entries in use, sampled: one entry in 8 counts 8 (grow_caps enlarges the table past half full; one counter
+      // taking an atomic per rebirth would serialise the heal of a C4 storm)
+      if (d.hist_n && (tag & 0x700ull) == 0) atomicAdd(d.hist_n, 8u);
     }
     uint32_t n = (uint32_t)(e[2] >> 32);  // total rebirths so far; the ring keeps the latest HKEEP
     uint32_t* c = (uint32_t*)(e + 3);
@@ -1048,7 +1050,10 @@ __global__ void __launch_bounds__(256) k_gossip_apply(const Dev* __restrict__ dp
     }
     if (lane == 0) {
       const uint32_t nr = b - a;
-      if (d.rfill) atomicMax(d.rfill, b - d.rhead[t]);  // the host grows the rings before they can overflow
+      // the host grows the rings before they can overflow (the atomic only when the fill beats the maximum so far:
+      // one address taking an atomic from every target wave serialises, ~13 ns each)
+      if (d.rfill && b - d.rhead[t] > __hip_atomic_load(d.rfill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMax(d.rfill, b - d.rhead[t]);
       if (nr) {
         if (d.XW > 1)
           atomicAdd(&d.held_delta[t], (int)nr);
