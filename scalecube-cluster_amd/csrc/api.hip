@@ -350,10 +350,16 @@ int push_epoch(swim_handle* h) {
   h->ep_loss[e] = h->loss;
   h->ep_part[e] = h->partitioned ? 1u : 0u;
   h->ep_delay[e] = h->delay_idx;
-  HIPCK(h2d(h->stream, h->d.ep_delay + e, &h->ep_delay[e], 4));
-  HIPCK(h2d(h->stream, h->d.ep_from + e, &h->ep_from[e], 4));
-  HIPCK(h2d(h->stream, h->d.ep_loss + e, &h->ep_loss[e], 4));
-  HIPCK(h2d(h->stream, h->d.ep_part + e, &h->ep_part[e], 4));
+  // the kernels that take Dev by value see h->d at launch; the others read the device copy (d.self)
+  Dev& d = h->d;
+  d.ep_delay[e] = h->ep_delay[e];
+  d.ep_from[e] = h->ep_from[e];
+  d.ep_loss[e] = h->ep_loss[e];
+  d.ep_part[e] = h->ep_part[e];
+  HIPCK(h2d(h->stream, (void*)(d.self->ep_delay + e), &d.ep_delay[e], 4));
+  HIPCK(h2d(h->stream, (void*)(d.self->ep_from + e), &d.ep_from[e], 4));
+  HIPCK(h2d(h->stream, (void*)(d.self->ep_loss + e), &d.ep_loss[e], 4));
+  HIPCK(h2d(h->stream, (void*)(d.self->ep_part + e), &d.ep_part[e], 4));
   HIPCK(h2d(h->stream, h->d.ep_group + (size_t)e * h->d.N, h->group.data(), 4ull * h->d.N));
   return SWIM_OK;
 }
@@ -390,7 +396,8 @@ int upload_links(swim_handle* h) {
   HIPCK(hipStreamSynchronize(h->stream));
   HIPCK(h2d(h->stream, h->d.link_key, keys.data(), 8ull * LKCAP));
   HIPCK(h2d(h->stream, h->d.link_hist, hist.data(), 4ull * hist.size()));
-  HIPCK(h2d(h->stream, h->d.link_n, &n, 4));
+  h->d.link_n = n;
+  HIPCK(h2d(h->stream, (void*)&h->d.self->link_n, &h->d.link_n, 4));
   return SWIM_OK;
 }
 
@@ -617,8 +624,8 @@ int build(swim_handle* h) {
   int rc;
 #define A(p, n)                                   \
   if ((rc = dalloc(h, &(p), (size_t)(n))) != 0) return rc;
-  A(d.link_n, 1) A(d.link_key, LKCAP) A(d.link_hist, (uint64_t)LKCAP * LKH * 2)
-  A(d.dead_tick, N) A(d.ep_from, MAX_EPOCHS) A(d.ep_loss, MAX_EPOCHS) A(d.ep_part, MAX_EPOCHS) A(d.ep_delay, MAX_EPOCHS)
+  A(d.link_key, LKCAP) A(d.link_hist, (uint64_t)LKCAP * LKH * 2)
+  A(d.dead_tick, N)
   A(d.dly_thr, DTAB * 256) A(d.dly_len, DTAB)
   A(d.ep_group, MAX_EPOCHS * N) A(d.md_version, N)
   A(d.tsize, N) A(d.fdLen, N) A(d.gLen, N) A(d.fdPeriod, N) A(d.gPeriod, N) A(d.gCounter, N) A(d.nextPing, N)
@@ -660,7 +667,7 @@ int build(swim_handle* h) {
     HIPCK(hipMemsetAsync(d.rfill, 0, 4, h->stream));
     HIPCK(hipMemsetAsync(d.hist_n, 0, 4, h->stream));
   }
-  A(d.ev, (uint64_t)d.EVCAP * 8) A(d.ev_n, 1) A(d.ctr, C_NCTR) A(d.err, 8)
+  A(d.ev, (uint64_t)d.EVCAP * 8) A(d.ev_n, 1) A(d.ctr, C_NCTR) A(d.ctr_sh, (uint64_t)CSH * CSTRIDE) A(d.err, 8)
   if (c.flags & SWIM_FLAG_EMULATOR_COUNTERS) {
     A(d.em, 2 * N)
     HIPCK(hipMemsetAsync(d.em, 0, 16 * N, h->stream));
@@ -743,6 +750,7 @@ int build(swim_handle* h) {
   HIPCK(hipMemsetAsync(d.DM, 0, (size_t)d.QW * 8, h->stream));
   HIPCK(hipMemsetAsync(d.nagroup, 0, 8, h->stream));
   HIPCK(hipMemsetAsync(d.ctr, 0, C_NCTR * 8, h->stream));
+  HIPCK(hipMemsetAsync(d.ctr_sh, 0, 8ull * CSH * CSTRIDE, h->stream));
   HIPCK(hipMemsetAsync(d.hist, 0, (size_t)d.HCAP * HREC * 8, h->stream));
   HIPCK(hipMemsetAsync(d.err, 0, 32, h->stream));
   HIPCK(hipMemsetAsync(d.ev_n, 0, 4, h->stream));
@@ -753,7 +761,7 @@ int build(swim_handle* h) {
   HIPCK(hipMemsetAsync(d.pool_used, 0, 4, h->stream));
   HIPCK(hipMemsetAsync(d.mdone, 0, 8, h->stream));
   d.halt = d.mdone + 1;
-  HIPCK(hipMemsetAsync(d.link_n, 0, 4, h->stream));
+  d.link_n = 0;
   HIPCK(hipMemsetAsync(d.link_key, 0, 8ull * LKCAP, h->stream));
   HIPCK(hipMemsetAsync(d.xd_n, 0, 4, h->stream));
   HIPCK(hipMemsetAsync(d.rc_n, 0, 4, h->stream));
@@ -770,8 +778,10 @@ int build(swim_handle* h) {
     HIPCK(hipMemsetAsync(d.xb_scnt, 0, 8ull * d.W, h->stream));
   }
   HIPCK(hipHostMalloc((void**)&h->hflag, 64, hipHostMallocMapped | hipHostMallocCoherent));
-  h->hflag[0] = 0;
+  for (int i = 0; i < 16; ++i) h->hflag[i] = 0;
   HIPCK(hipHostGetDevicePointer((void**)&d.hflag, (void*)h->hflag, 0));
+  if ((rc = dalloc(h, &d.hsh, 8)) != 0) return rc;
+  HIPCK(hipMemsetAsync(d.hsh, 0, 32, h->stream));  // (hflag above: all zero)
   HIPCK(hipEventCreateWithFlags(&h->ev_member, hipEventDisableTiming));
   HIPCK(hipMemsetAsync(d.subs, 0, NL * SUBCAP * 16, h->stream));
   int32_t top = (int32_t)d.SPR;
@@ -787,9 +797,8 @@ int build(swim_handle* h) {
     HIPCK(hipMemcpyAsync(d.mcfg, mc.data(), 16ull * N, hipMemcpyHostToDevice, h->stream));
     HIPCK(hipStreamSynchronize(h->stream));
   }
-  std::vector<uint32_t> never(MAX_EPOCHS, NEVER);
-  HIPCK(hipMemcpyAsync(d.ep_from, never.data(), 4 * MAX_EPOCHS, hipMemcpyHostToDevice, h->stream));
-  HIPCK(hipStreamSynchronize(h->stream));  // `top` and `never` live on this stack frame
+  for (uint32_t e = 0; e < MAX_EPOCHS; ++e) d.ep_from[e] = NEVER;  // (uploaded with Dev below)
+  HIPCK(hipStreamSynchronize(h->stream));  // `top` lives on this stack frame
   h->group.assign(d.N, 0);
   for (uint32_t e = 0; e < MAX_EPOCHS; ++e) h->ep_from[e] = NEVER;
   h->cur_ep = 0;
@@ -1479,17 +1488,30 @@ int swim_step(swim_handle* h, uint32_t n) {
             (tend - t0) / 100.0, sst / nw / 100.0, str / nw / 100.0, sbd / nw / 100.0, scw / nw / 100.0);
     for (size_t r = 0; r < 8 && r < nw; ++r) {
       const size_t i = ord[r];
+      if (r == 0) {  // when the waves of each class finish their bodies (us from the kernel's first wave): quartiles
+        for (int c = 0; c < 4; ++c) {
+          std::vector<double> e;
+          for (size_t j = 0; j < nw; ++j)
+            if ((w[4 * j + 1] >> 56) == (1ull << c)) e.push_back((w[4 * j + 2] - t0) / 100.0);
+          std::sort(e.begin(), e.end());
+          if (!e.empty())
+            fprintf(stderr, "exp512: class %d waves %zu body end min %.1f q1 %.1f med %.1f q3 %.1f max %.1f\n", c, e.size(),
+                    e[0], e[e.size() / 4], e[e.size() / 2], e[3 * e.size() / 4], e.back());
+        }
+      }
       fprintf(stderr, "exp512: wave %zu start %.2f triage %.2f body %.2f cow %.2f classes %llx busy %llu\n", i,
               (w[4 * i] - t0) / 100.0, ((w[4 * i + 1] & M) - w[4 * i]) / 100.0, (w[4 * i + 2] - (w[4 * i + 1] & M)) / 100.0,
               (w[4 * i + 3] - w[4 * i + 2]) / 100.0, w[4 * i + 1] >> 56, (w[4 * i + 1] >> 48) & 255);
-      if (w[4 * i + 1] >> 56) {  // phase groups of its busy lanes: P0+P1, P2+P3, P4, P5, P6
+      if (w[4 * i + 1] >> 56) {  // its lead lane's laps in time order, "slot:us since the previous lap"
+        // (slots 0-4: after P0+P1, P2+P3, P4, P5, P6; 5-11: finer laps inside them)
         unsigned long long prev = w[4 * i + 1] & M;
-        fprintf(stderr, "exp512:   phases");
-        for (int j = 0; j < 5; ++j) {
-          const unsigned long long t = w16[16 * i + 4 + j];
-          fprintf(stderr, " %.2f", t >= prev ? (t - prev) / 100.0 : -1.0);
-          if (t >= prev) prev = t;
-        }
+        std::vector<std::pair<unsigned long long, int>> laps;
+        for (int j = 0; j < 12; ++j)
+          if (w16[16 * i + 4 + j] >= prev && w16[16 * i + 4 + j] <= w[4 * i + 2]) laps.push_back({w16[16 * i + 4 + j], j});
+        std::sort(laps.begin(), laps.end());
+        fprintf(stderr, "exp512:   laps");
+        for (const auto& l : laps)
+          fprintf(stderr, " %d:%.2f@%.1f", l.second, (l.first - prev) / 100.0, (l.first - t0) / 100.0), prev = l.first;
         fprintf(stderr, "\n");
       }
     }
@@ -1998,6 +2020,12 @@ int swim_counters_get(swim_handle* h, swim_counters* out) {
   HIPCK(hipStreamSynchronize(h->stream));
   unsigned long long c[C_NCTR];
   HIPCK(hipMemcpy(c, h->d.ctr, sizeof(c), hipMemcpyDeviceToHost));
+  {  // the member kernel's rows of counters 0-7
+    std::vector<unsigned long long> sh((size_t)CSH * CSTRIDE);
+    HIPCK(hipMemcpy(sh.data(), h->d.ctr_sh, 8 * sh.size(), hipMemcpyDeviceToHost));
+    for (uint32_t r = 0; r < CSH; ++r)
+      for (uint32_t i = 0; i < 8; ++i) c[i] += sh[(size_t)r * CSTRIDE + i];
+  }
   std::memset(out, 0, sizeof(*out));
   out->tick = h->tick;
   out->record_compares = c[C_R];

@@ -103,7 +103,7 @@ __device__ __noinline__ int link_loss_at(const Dev& d, uint32_t src, uint32_t ds
 // 100 %), else the partition block (DEAD_LINK_SETTINGS, no delay) and the default settings. Returns loss % | delay
 // index << 8.
 __device__ __forceinline__ uint32_t link_set(const Dev& d, int ep, uint32_t src, uint32_t dst, uint32_t k) {
-  if (*d.link_n) {
+  if (d.link_n) {
     const int lp = link_loss_at(d, src, dst, k);
     if (lp >= 0) return (uint32_t)lp;
   }
@@ -422,22 +422,32 @@ __device__ __forceinline__ void tick_end(const Dev& d, uint32_t k) {
 // (no system-scope fence: that writes back the XCD's L2 at the end of every tick)
 __device__ __forceinline__ void tick_flag(const Dev& d, uint32_t k, bool spec) {
   uint32_t nb = (k + 1) & 1;
+  // every load first (in flight together), then the stores; the host-mapped words are written only when they change
+  // (a write to host memory holds the end of the kernel for a round trip over the host link)
+  const uint32_t used =
+      (uint32_t)((int32_t)d.SPR - __hip_atomic_load(d.free_top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  uint32_t v[6] = {used, 0, 0, 0, 0, 0}, sh[6];
+  if (d.rfill) {  // the previous gossip plane's peaks, for the host's capacity growth (api.hip grow_caps)
+    v[1] = *d.rfill;
+    v[2] = *d.rc_n;
+    v[3] = *d.rp_n;
+    v[4] = *d.slow_n;
+    v[5] = *d.hist_n;
+  }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) sh[i] = d.hsh[i];
   d.nmsg[nb] = 0;
   d.arena_used[nb] = 0;
   *d.pool_used = 0;
-  if (d.rfill) {  // the previous gossip plane's peaks, for the host's capacity growth (api.hip grow_caps)
-    d.hflag[2] = *d.rfill;
-    d.hflag[3] = *d.rc_n;
-    d.hflag[4] = *d.rp_n;
-    d.hflag[5] = *d.slow_n;
-    d.hflag[6] = *d.hist_n;
-    *d.rfill = 0;
-  }
+  if (d.rfill) *d.rfill = 0;
   *d.rc_n = 0;
   if (d.ackres) *d.ndl = 0;
-  const uint32_t used =
-      (uint32_t)((int32_t)d.SPR - __hip_atomic_load(d.free_top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  d.hflag[0] = used;
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+    if ((i == 0 || d.rfill) && v[i] != sh[i]) {
+      d.hflag[i == 0 ? 0 : i + 1] = v[i];  // [0] slots in use, [2..6] the peaks
+      d.hsh[i] = v[i];
+    }
   if (!spec) {
     __threadfence_system();
   } else if (used) {

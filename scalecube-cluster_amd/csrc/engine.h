@@ -84,6 +84,7 @@ constexpr uint32_t XINL = 16384;  // RCCL: bytes per peer moved by the fixed-siz
 
 // counters (swim_counters order after .tick)
 // 8..12: SWIM_EXP & 4 (and 16..19: the gossip plane's work units per tick, for algorithmic bytes; tools/pmc_gossip.py)
+constexpr uint32_t CSH = 64, CSTRIDE = 64;  // Dev::ctr_sh rows, 512 B apart
 enum Ctr { C_R = 0, C_W, C_M, C_G, C_E, C_LOST, C_GCREATED, C_SYNCMERGE, C_DIFFMSG = 13, C_XU = 16, C_ACKRES = 24, C_ACKRES_ALL = 25, C_DIFFMSG_ALL = 26, C_NCTR = 27 };
 
 // capacity fallbacks that fired (include/swimhip_debug.h; counted only when Dev::fb is allocated: SWIM_CAPS or
@@ -148,10 +149,12 @@ struct Dev {
 
   // ---- network / fault history (NetworkEmulator settings per epoch) ----
   uint32_t* dead_tick;  // [N] tick from which the member is dead, NEVER = alive
-  uint32_t* ep_from;    // [MAX_EPOCHS] first tick of each settings epoch (NEVER = unused)
-  uint32_t* ep_loss;    // [MAX_EPOCHS]
-  uint32_t* ep_part;    // [MAX_EPOCHS] partition active
-  uint32_t* ep_delay;   // [MAX_EPOCHS] default mean delay (its delay index)
+  // the epoch table and the link count are held in Dev itself: a kernel reads them with scalar loads at the tick's
+  // (uniform) epoch, not as a chain of dependent vector loads in every send (xmit_ep)
+  uint32_t ep_from[MAX_EPOCHS];   // first tick of each settings epoch (NEVER = unused)
+  uint32_t ep_loss[MAX_EPOCHS];
+  uint32_t ep_part[MAX_EPOCHS];   // partition active
+  uint32_t ep_delay[MAX_EPOCHS];  // default mean delay (its delay index)
   // NetworkLinkSettings.meanDelay (SEMANTICS.md §2): a link value is loss % | delay index << 8; each index has the
   // thresholds on the 32-bit delay draw whose count the draw reaches is the message's delay in ticks past lat
   uint32_t dly_on;      // a delay that reaches a tick was set (the gossip plane queues delayed first receipts)
@@ -173,7 +176,7 @@ struct Dev {
   int32_t* ds_top;      // [1]
   uint32_t* ep_group;   // [MAX_EPOCHS][N]
   uint32_t* md_version; // [N]
-  uint32_t* link_n;     // [1] keys in the link table (0: no per-link setting was ever made)
+  uint32_t link_n;      // keys in the link table (0: no per-link setting was ever made)
   uint64_t* link_key;   // [LKCAP] (src << 32 | dst) + 1, 0 = empty slot
   uint32_t* link_hist;  // [LKCAP][LKH][2] (from tick, loss % or LK_NONE), oldest first; [0][0] | LK_TRUNC if older ones dropped
 
@@ -308,10 +311,15 @@ struct Dev {
   uint32_t* ev;  // [EVCAP][8] swim_event
   uint32_t* ev_n;
   unsigned long long* ctr;  // [C_NCTR]
+  // counters 0-7 as the member kernel adds them: one row of CSTRIDE per block residue (blockIdx % CSH), summed by the
+  // host with ctr. ~1 400 waves adding to one word per tick serialise at its L2 channel (~13 ns each) and held every
+  // later memory access of the waves still running (k_member_tick 44 -> 31 us at C3)
+  unsigned long long* ctr_sh;  // [CSH][CSTRIDE]
   unsigned long long* wt;   // SWIM_EXP & 512: per-wave timestamps of the latest k_member_tick [waves][16]
   uint32_t* err;            // [8] bits, info...
   const Dev* self;          // device-resident copy of this struct (kernels index it through a pointer)
   uint32_t* hflag;          // host-mapped: [0] gossip slots in use after this tick's member control (W == 1)
+  uint32_t* hsh;            // [8] what hflag holds (device copy): tick_flag writes host memory only on a change
                             // [1] halt tick (speculative batches); with rfill: the previous gossip plane's largest
                             // receipt-ring fill [2], routed receipts [3], replay and slow-path sends [4], [5]
   uint32_t* rfill;          // [1] W == 1: largest ring fill (rtail - rhead) after this tick's receipts (grow_caps)

@@ -1107,15 +1107,18 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   L.ntl = 0;
   L.tlast = NEVER;
   L.rgrp = -1;
+  // P1's inbound list head, loaded with the state above (P0's sends link into the other buffer)
+  const uint32_t head0 = (!dead && k > 0) ? d.m_head[(size_t)((k - 1) & 1) * d.N + m] : NEVER;
   // SWIM_EXP & 16 (timing experiment): shader cycles per phase summed over members, ctr[8..12]
   // SWIM_EXP & 128: the largest per-member cycles of each phase instead (which phase makes the longest lane)
   const bool prof = (d.exp & (16 | 128)) != 0;
   unsigned long long tp = prof ? clock64() : 0;
   // SWIM_EXP & 512: the wave's first busy lane stamps the wall clock after each phase group (wt[4 + slot])
-  const bool wlead = (d.exp & 512) && (threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)__ballot(1)) - 1);
+  // (the first lane active at the lap stamps it: a lap inside a branch times the lanes that took it)
   auto lap = [&](int slot) {
-    if (wlead) d.wt[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + 4 + slot] = wall_clock64();
-    if (!prof) return;
+    if ((d.exp & 512) && (threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)__ballot(1)) - 1))
+      d.wt[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + 4 + slot] = wall_clock64();
+    if (!prof || slot > 4) return;  // (slots 5-10: finer wall-clock laps only)
     const unsigned long long t = clock64();
     if (d.exp & 16)
       atomicAdd(&d.ctr[8 + slot], t - tp);
@@ -1175,9 +1178,9 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   // ---- P1 SYNC / SYNC_ACK (onMessage :320-331, onSync :346-367, onSyncAck :337-343) ----
   // the senders linked this member's inbound messages into a list; they are handled in (src, syncSeq) order
   const uint32_t* mnext = d.m_next + (size_t)((k - 1) & 1) * d.MSGCAP;
-  if (!dead && k > 0 && d.m_head[(size_t)((k - 1) & 1) * d.N + m] != NEVER) {
+  if (head0 != NEVER) {
     const uint32_t pb = (k - 1) & 1;
-    const uint32_t head = d.m_head[(size_t)pb * d.N + m];
+    const uint32_t head = head0;
     d.m_head[(size_t)pb * d.N + m] = NEVER;
     uint64_t key[MQ];
     uint32_t idx[MQ], n = 0;
@@ -1199,6 +1202,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
       key[j] = kq;
       idx[j] = q;
     }
+    lap(5);
     uint64_t last = 0;
     L.trk_on = n > 1 || more;  // several payloads: later ones re-check the subjects earlier ones changed
     for (uint32_t r = 0;; ++r) {
@@ -1224,6 +1228,15 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
       const uint32_t mflags = mm.kind & KF_FLAGS;
       mm.kind &= ~KF_FLAGS;
       if (mc_group(d, mm.src) != mc_group(d, m)) continue;  // checkSyncGroup (:320-321,431-437): another group's data
+      if (mm.kind == K_SYNC && mm.ncand == 0 && L.ntrk == 0 && L.nfetch == 0) {
+        // onSync with nothing to merge (the steady state): merge_payload finds no record, and with no fetch pending
+        // every group is free, so the group alloc_group would take completes at once; its SYNC_ACK goes out without
+        // the group table's round trips (a free group's fields are never read before alloc_group rewrites them)
+        L.c[C_R] += mm.psize;
+        L.c[C_SYNCMERGE]++;
+        send_sync(L, K_SYNC_ACK, mm.src, mm.cid_iss, mm.cid_cnt, !(mflags & (KF_ABS | KF_LATE)));
+        continue;
+      }
       // one merge_payload / finish site for the three cases (each inlined copy is large)
       int g = -1;
       uint32_t reason = R_SYNC;
@@ -1247,6 +1260,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
         // its SYNC_ACK, if sent now, may be resolved unless the payload lacked records this row holds or came late
         L.rgrp = (mm.kind == K_SYNC && !(mflags & (KF_ABS | KF_LATE))) ? g : -1;
         finish(L, g, false);
+        lap(8);
         L.rgrp = -1;
       }
     }
@@ -1266,6 +1280,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
       uint32_t cnt = P[0], stage = P[1], tk = P[2], a = P[3], b = P[4];
       bool keep = true;
       if (tk == k) {
+        lap(9);
         uint32_t kind = stage & 0xF0, st = stage & 0xF;
         if (st == P_ARRIVE) {
           if (dead) keep = false;
@@ -1306,6 +1321,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
             }
           }
         }
+        lap(10);
       }
       if (keep) {
         uint32_t* Q = L.paths + (size_t)w * 5;
@@ -1318,6 +1334,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
       }
     }
     L.npath = w;
+    lap(6);
     // arrivals: every pending subscription on the cid takes the first PING_ACK (TransportImpl.java:205-232), in cid
     // order; then the arrived entries leave the list
     const uint32_t narr = __popc(arrmask);
@@ -1344,8 +1361,10 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
         }
       }
       L.nsub = w2;
+      lap(11);
       for (uint32_t q = 0; q < nh; ++q) on_fd_event(L, hit[q], ST_ALIVE);  // publishPingResult(ALIVE)
     }
+    lap(7);
     if (arrmask) {
       uint32_t w3 = 0;
       for (uint32_t p = 0; p < w; ++p)
@@ -1593,10 +1612,20 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
 
   lap(4);  // P6
   flush_spreads(L);
-  uint32_t nev = NEVER;
-  for (uint32_t q = 0; q < L.npath; ++q) nev = min(nev, L.paths[(size_t)q * 5 + 2]);
-  for (uint32_t q = 0; q < L.nsub; ++q) nev = min(nev, L.subs[(size_t)q * 4 + 3]);
-  nev = min(nev, L.fnext);
+  // the next due event: the first four paths and subscriptions are loaded together (one round trip, not one per entry)
+  uint32_t nev = L.fnext;
+  {
+    uint32_t t[8];
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+      t[q] = q < L.npath ? L.paths[(size_t)q * 5 + 2] : NEVER;
+      t[4 + q] = q < L.nsub ? L.subs[(size_t)q * 4 + 3] : NEVER;
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < 8; ++q) nev = min(nev, t[q]);
+  }
+  for (uint32_t q = 4; q < L.npath; ++q) nev = min(nev, L.paths[(size_t)q * 5 + 2]);
+  for (uint32_t q = 4; q < L.nsub; ++q) nev = min(nev, L.subs[(size_t)q * 4 + 3]);
   if (L.ncreq)  // the log length the block epilogue undoes from
     for (uint32_t q = 0, n = min(*L.cw_n, d.cwmax_cap); q < n; ++q)
       if (L.cw[q].x == m) L.cw[q].w = L.nlog;
@@ -1664,8 +1693,9 @@ __global__ void __launch_bounds__(256, 2) k_member_tick(const Dev* __restrict__ 
     uint32_t v = drops, e = evs;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o), e += __shfl_xor(e, o);
-    if ((threadIdx.x & 63) == 0 && v) atomicAdd(&d.ctr[C_R], (unsigned long long)v);
-    if ((threadIdx.x & 63) == 0 && e) atomicAdd(&d.ctr[C_E], (unsigned long long)e);
+    unsigned long long* cs = d.ctr_sh + (size_t)(blockIdx.x % CSH) * CSTRIDE;
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(&cs[C_R], (unsigned long long)v);
+    if ((threadIdx.x & 63) == 0 && e) atomicAdd(&cs[C_E], (unsigned long long)e);
   }
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t b0 = __ballot(busy && cls == 0), b1 = __ballot(busy && cls == 1), b2 = __ballot(busy && cls == 2),
@@ -1710,7 +1740,7 @@ __global__ void __launch_bounds__(256, 2) k_member_tick(const Dev* __restrict__ 
         uint32_t lo = __shfl_xor((uint32_t)v, o), hi = __shfl_xor((uint32_t)(v >> 32), o);
         v += ((unsigned long long)hi << 32) | lo;
       }
-      if (lane == 0 && v) atomicAdd(&d.ctr[i], v);
+      if (lane == 0 && v) atomicAdd(&d.ctr_sh[(size_t)(blockIdx.x % CSH) * CSTRIDE + i], v);
     }
   }
   if (wtime && (threadIdx.x & 63) == 0) wt[2] = wall_clock64();
