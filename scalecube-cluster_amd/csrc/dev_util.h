@@ -415,6 +415,17 @@ __device__ __forceinline__ void tick_end(const Dev& d, uint32_t k) {
   }
 }
 
+// start of a speculative k_member_tick (W == 1, block 0, one thread): the per-tick counters the SYNC diff and the
+// member control of the next tick append to; this tick's member kernel uses only the other buffer's. (In a speculative
+// batch no gossip slot is in use and no gossip plane runs, so the receipt lists and peaks stay as they are.)
+__device__ __forceinline__ void tick_reset(const Dev& d, uint32_t k) {
+  const uint32_t nb = (k + 1) & 1;
+  d.nmsg[nb] = 0;
+  d.arena_used[nb] = 0;
+  *d.pool_used = 0;
+  if (d.ackres) *d.ndl = 0;
+}
+
 // end of k_member_tick (W == 1, the last block, one thread): reset the per-tick counters the gossip plane of this tick and the SYNC diff and
 // member control of the next tick append to, and tell the host whether any gossip slot is in use (if none, the
 // gossip data plane of this tick has nothing to send, deliver, route or recycle and is not launched)

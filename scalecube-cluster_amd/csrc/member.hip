@@ -51,6 +51,7 @@ struct ML {
   uint32_t* tl;
   uint32_t ntl, tlast;
   int rgrp;
+  bool spec;  // a launch of a one-GPU speculative batch: a member that takes a gossip slot raises d.halt (k_member_tick)
 };
 
 // a subject whose key this member's row changed in this tick, or a candidate of a payload it merged (k_ack_resolve)
@@ -368,6 +369,7 @@ __device__ __forceinline__ void flush_spreads(ML& L) {
   if (n == 0) return;
   L.nsp = 0;
   const Dev& d = *L.d;
+  if (L.spec) *(volatile uint32_t*)d.halt = L.k + 1u;  // a slot in use: the batch stops after this tick
   const int base = atomicSub(d.free_top, (int)n) - (int)n;
   uint32_t rt = d.rtail[L.m];  // only this lane appends to the member's ring in this kernel
   for (uint32_t i = 0; i < n; ++i) {
@@ -1044,7 +1046,7 @@ __device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t
 }
 
 __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint32_t k, unsigned long long (&cnt)[8],
-                                                 uint4* cw, uint32_t* cw_n) {
+                                                 uint4* cw, uint32_t* cw_n, bool spec) {
   const bool dead = dead_at(d, m, k);
   ML L;
   L.d = &d;
@@ -1098,6 +1100,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   L.trk_on = false;
   L.cw = cw;
   L.cw_n = cw_n;
+  L.spec = spec;
   L.ulog = d.ulog + li * ULOG * 2;
   L.ncreq = 0;
   L.nlog = 0;
@@ -1675,7 +1678,13 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
 // speculative batch.
 __global__ void __launch_bounds__(256, 2) k_member_tick(const Dev* __restrict__ dp, uint32_t k, uint32_t flag) {
   const Dev& d = *dp;  // global, not kernarg: taking its address must not copy ~1 KB into per-lane scratch
-  if ((flag & 2u) && *(volatile uint32_t*)d.halt) return;  // a speculative batch halted at an earlier tick
+  if (flag & 2u) {  // a speculative batch halted at an earlier tick (this tick's own halt is raised while it runs)
+    const uint32_t hv = *(volatile uint32_t*)d.halt;
+    if (hv != 0u && hv - 1u < k) return;
+  }
+  // a speculative launch resets the next tick's counters at its start (nothing in this kernel uses them), so no block
+  // waits for the last one at its end: the halt that tick_flag would raise is raised by the member taking a slot
+  if ((flag & 3u) == 3u && blockIdx.x == 0 && threadIdx.x == 0) tick_reset(d, k);
   // SWIM_EXP & 512 (timing experiment): wall clock of each wave at entry, after triage, after its bodies, at exit
   const bool wtime = (d.exp & 512) != 0;
   unsigned long long* wt = wtime ? d.wt + ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 : nullptr;
@@ -1731,7 +1740,7 @@ __global__ void __launch_bounds__(256, 2) k_member_tick(const Dev* __restrict__ 
   if (__ballot(me != NEVER)) {  // waves with no busy member skip to the end
     unsigned long long cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const bool skip = ((d.exp & 32) && mcls == 0) || ((d.exp & 64) && mcls != 0);
-    if (me != NEVER && !skip) member_tick_body(d, me, k, cnt, cw, &cw_n);
+    if (me != NEVER && !skip) member_tick_body(d, me, k, cnt, cw, &cw_n, (flag & 3u) == 3u);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       unsigned long long v = cnt[i];
@@ -1768,10 +1777,10 @@ __global__ void __launch_bounds__(256, 2) k_member_tick(const Dev* __restrict__ 
     __syncthreads();
   }
   if (wtime && (threadIdx.x & 63) == 0) wt[3] = wall_clock64();
-  if (!(flag & 1u)) return;
+  if ((flag & 3u) != 1u) return;
   if (!last_block_ticket(d.mdone, gridDim.x) || threadIdx.x != 0) return;
   *d.mdone = 0;
-  tick_flag(d, k, (flag & 2u) != 0);
+  tick_flag(d, k, false);
 }
 
 }  // namespace swim
