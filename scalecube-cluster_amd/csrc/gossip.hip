@@ -335,9 +335,9 @@ __global__ void k_tin_scatter(Dev d) {
     if (t < d.lo || t >= d.hi) continue;
     const uint32_t j = atomicAdd(&d.tin_fill[t], 1u);
     d.tin[d.tin_off[t] + j] = ms;
-    if (j == 0) {
+    if (j == 0) {  // one atomic per wave on the list counter (10^4 targets a tick adding one by one serialise on it)
       d.rt0[t] = d.rtail[t];
-      d.tlist[atomicAdd(d.ntl, 1u)] = t;
+      d.tlist[wave_append(d.ntl)] = t;
     }
   }
 }
@@ -565,7 +565,7 @@ __device__ void contact_cache(const Dev& d, uint32_t i, uint32_t m, uint32_t t, 
     if (lo == 0) {
       ci = NEVER;  // every window gossip arrived after the contact: no replay at all
     } else if (lo < tl - w0) {
-      const uint32_t r = atomicAdd(d.nrx, 1u);
+      const uint32_t r = wave_append(d.nrx);
       if (r < d.CRCAP) {
         d.crow[i] = r;
         d.rxl[3 * r] = i;
