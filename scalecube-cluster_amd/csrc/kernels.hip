@@ -1,6 +1,7 @@
 // kernels.hip — initialisation, receipt routing, the SYNC-payload diff, state hashes and the tick launchers (the
 // gossip data plane is in gossip.hip).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include "dev_util.h"
 
@@ -717,12 +718,22 @@ static uint32_t diff_grid() {
   return v >= 1 && v <= (1ul << 20) ? (uint32_t)v : 2048u;
 }
 
-static void launch_sync_diff(const Dev& d, uint32_t b, hipStream_t st, uint32_t timed, uint32_t spec = 0) {
+// a timed launch carries its start / stop events in its own dispatch (hipExtLaunchKernelGGL): the interval is the
+// kernel's, not that of two marker packets around it (those read ~4 us per launch longer than rocprofv3)
+static void launch_sync_diff(const Dev& d, uint32_t b, hipStream_t st, uint32_t timed, uint32_t spec = 0,
+                             const TickEvents* prof = nullptr) {
   static const uint32_t grid = diff_grid();
-  if (d.W > 1)
+  if (prof) {
+    hipEvent_t e0 = (hipEvent_t)prof->ev[0], e1 = (hipEvent_t)prof->ev[1];
+    if (d.W > 1)
+      hipExtLaunchKernelGGL(k_sync_diff<true>, dim3(grid), dim3(256), 0, st, e0, e1, 0, d.self, b, timed, spec);
+    else
+      hipExtLaunchKernelGGL(k_sync_diff<false>, dim3(grid), dim3(256), 0, st, e0, e1, 0, d.self, b, timed, spec);
+  } else if (d.W > 1) {
     hipLaunchKernelGGL(k_sync_diff<true>, dim3(grid), dim3(256), 0, st, d.self, b, timed, spec);
-  else
+  } else {
     hipLaunchKernelGGL(k_sync_diff<false>, dim3(grid), dim3(256), 0, st, d.self, b, timed, spec);
+  }
 }
 
 // single GPU: the tick is cut in three so that the host can hold back the gossip data plane when no slot is in
@@ -740,9 +751,7 @@ static void launch_ack_resolve(const Dev& d, uint32_t k, hipStream_t st, bool sp
 void launch_diff(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool spec) {
   hipStream_t st = (hipStream_t)stream;
   launch_ack_resolve(d, k, st, spec, prof != nullptr);
-  if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
-  if (k > 0) launch_sync_diff(d, (k - 1) & 1, st, prof ? 1u : 0u, spec ? 1u : 0u);
-  if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
+  if (k > 0) launch_sync_diff(d, (k - 1) & 1, st, prof ? 1u : 0u, spec ? 1u : 0u, prof);
 }
 
 // link delays: SYNC / SYNC_ACK messages due in the next tick back into this tick's buffer, then the delayed messages
@@ -962,9 +971,7 @@ void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   uint32_t b = k & 1;
   const uint32_t sp = spec ? 1u : 0u;
   launch_ack_resolve(d, k, st, spec, prof != nullptr);
-  if (prof) hipEventRecord((hipEvent_t)prof->ev[0], st);
-  if (k > 0) launch_sync_diff(d, (k - 1) & 1, st, prof ? 1u : 0u, sp);
-  if (prof) hipEventRecord((hipEvent_t)prof->ev[1], st);
+  if (k > 0) launch_sync_diff(d, (k - 1) & 1, st, prof ? 1u : 0u, sp, prof);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[2], st);
   hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k, spec ? 2u : 0u);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[3], st);
