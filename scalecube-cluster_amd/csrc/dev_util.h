@@ -418,12 +418,16 @@ __device__ __forceinline__ void tick_end(const Dev& d, uint32_t k) {
 // start of a speculative k_member_tick (W == 1, block 0, one thread): the per-tick counters the SYNC diff and the
 // member control of the next tick append to; this tick's member kernel uses only the other buffer's. (In a speculative
 // batch no gossip slot is in use and no gossip plane runs, so the receipt lists and peaks stay as they are.)
+// Slots already in use when the launch starts (the host's user gossips of this tick, k_ug_create) stop the batch after
+// this tick like the ones its members take (flush_spreads).
 __device__ __forceinline__ void tick_reset(const Dev& d, uint32_t k) {
   const uint32_t nb = (k + 1) & 1;
   d.nmsg[nb] = 0;
   d.arena_used[nb] = 0;
   *d.pool_used = 0;
   if (d.ackres) *d.ndl = 0;
+  if (__hip_atomic_load(d.free_top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (int32_t)d.SPR)
+    *(volatile uint32_t*)d.halt = k + 1u;
 }
 
 // end of k_member_tick (W == 1, the last block, one thread): reset the per-tick counters the gossip plane of this tick and the SYNC diff and
