@@ -261,8 +261,9 @@ def main():
         merges = d["sync_merges"]
         diff_s = d["diff_ns"] * 1e-9
         launches = max(1, d["diff_launches"])
-        # one GPU: the engine times every 5th tick's k_sync_diff and counts the payloads those launches streamed
-        timed_msgs = d["diff_msgs"] if world == 1 else merges
+        # the engine counts the payloads its timed k_sync_diff launches streamed (every 5th tick on one GPU, every tick
+        # on a row shard); SYNC_ACKs resolved from write logs are not streamed, so they are not priced here
+        timed_msgs = d["diff_msgs"]
         bytes_per_launch = 8.0 * n * timed_msgs / launches  # payload keys + receiver keys, 4 B each per subject
         achieved = (8.0 * n * timed_msgs) / diff_s / 1e9 if diff_s > 0 else 0.0
         # whole-step algorithmic bytes, SURVEY.md §8d with 4-B record keys (B = 8R + 8W + 32M + 0.375G + 24E), with R's

@@ -63,6 +63,18 @@ int swim_debug_fallbacks(swim_handle* h, uint64_t* out, size_t n);
 #define SWIM_CAP_GROWTHS 5u
 int swim_debug_caps(swim_handle* h, uint64_t* out, size_t n);
 
+/* the holder bookkeeping of members [first, first + n), out[5 * i + j] for member first + i: j = 0 its gossip count
+ * (GossipProtocolImpl.gossips.size(), what doSpreadGossip's early return reads, :141-146), 1 / 2 the receipt-ring
+ * positions of its first held entry and of the ring end (absolute: every creation and first receipt appends one entry,
+ * every sweep advances the first), 3 the popcount of its held-bit row, 4 first receipts of the last tick whose GOSSIP
+ * events the next P4 folds (RUMOR mode without recorded events; 0 otherwise). One GPU or one shard of a slot-sharded
+ * RUMOR cluster (a row-sharded or multi-device handle: SWIM_EUNSUPPORTED). */
+int swim_debug_holders(swim_handle* h, uint32_t first, uint32_t n, uint32_t* out);
+
+/* sets member m's own record in its own table to incarnation inc, status unchanged, between steps (one GPU): the
+ * boundary test of the 30-bit incarnation field of the key plane (SEMANTICS.md §8). inc >= 2^30: SWIM_ECAPACITY. */
+int swim_debug_set_incarnation(swim_handle* h, uint32_t m, uint32_t inc);
+
 #ifdef __cplusplus
 }
 #endif

@@ -134,7 +134,15 @@ void dfree(swim_handle* h, void* p, size_t bytes) {
 // list lengths (Dev::hflag). A structure past half (slots, rings) or a quarter (per-tick lists) of its capacity is
 // reallocated larger, within the free HBM, its contents moved: slot ids, ring positions and every held bit keep their
 // meaning, so the simulation is unchanged (slot ids are not observable). SWIM_NO_GROW: fixed sizes.
+static int grow_caps_(swim_handle* h);
 int grow_caps(swim_handle* h) {
+  const int rc = grow_caps_(h);
+  // a structure replaced before a later allocation failed: the device copy of Dev must name the new buffers (the old
+  // ones are freed), so it is uploaded on that path too
+  if (rc != SWIM_OK) (void)h2d(h->stream, (void*)h->d.self, &h->d, sizeof(Dev));
+  return rc;
+}
+static int grow_caps_(swim_handle* h) {
   Dev& d = h->d;
   if (!d.rfill) return SWIM_OK;
   const volatile uint32_t* f = h->hflag;
@@ -168,18 +176,30 @@ int grow_caps(swim_handle* h) {
     const uint64_t need = (rcap - d.RCAP) * 32 + (pcap - d.RPCAP) * 16;
     if (need <= budget) {
       budget -= need;
+      // every replacement is allocated before an old buffer is given back: a failed allocation leaves the handle on
+      // its old (valid) buffers
       if (rcap != d.RCAP) {
+        uint64_t *raw2 = nullptr, *key2 = nullptr, *keyb = nullptr;
+        uint32_t *slot2 = nullptr, *slotb = nullptr;
+        if ((rc = dalloc(h, &raw2, rcap)) || (rc = dalloc(h, &slot2, rcap)) || (rc = dalloc(h, &key2, rcap)) ||
+            (rc = dalloc(h, &slotb, rcap)) || (rc = dalloc(h, &keyb, rcap))) {
+          dfree(h, raw2, 8 * rcap), dfree(h, slot2, 4 * rcap), dfree(h, key2, 8 * rcap), dfree(h, slotb, 4 * rcap);
+          return rc;
+        }
         dfree(h, d.rc_raw, 8ull * d.RCAP), dfree(h, d.rc_slot, 4ull * d.RCAP), dfree(h, d.rc_key, 8ull * d.RCAP);
         dfree(h, d.rc_slot2, 4ull * d.RCAP), dfree(h, d.rc_key2, 8ull * d.RCAP);
+        d.rc_raw = raw2, d.rc_slot = slot2, d.rc_key = key2, d.rc_slot2 = slotb, d.rc_key2 = keyb;
         d.RCAP = d.DCAP = (uint32_t)rcap;
-        if ((rc = dalloc(h, &d.rc_raw, rcap)) || (rc = dalloc(h, &d.rc_slot, rcap)) || (rc = dalloc(h, &d.rc_key, rcap)) ||
-            (rc = dalloc(h, &d.rc_slot2, rcap)) || (rc = dalloc(h, &d.rc_key2, rcap)))
-          return rc;
       }
       if (pcap != d.RPCAP) {
+        uint64_t *rp2 = nullptr, *slow2 = nullptr;
+        if ((rc = dalloc(h, &rp2, pcap)) || (rc = dalloc(h, &slow2, pcap))) {
+          dfree(h, rp2, 8 * pcap);
+          return rc;
+        }
         dfree(h, d.rp, 8ull * d.RPCAP), dfree(h, d.slow, 8ull * d.SLOWCAP);
+        d.rp = rp2, d.slow = slow2;
         d.RPCAP = d.SLOWCAP = (uint32_t)pcap;
-        if ((rc = dalloc(h, &d.rp, pcap)) || (rc = dalloc(h, &d.slow, pcap))) return rc;
       }
     }
   }
@@ -222,8 +242,13 @@ int grow_caps(swim_handle* h) {
           (rc = dalloc(h, &GU2, q2)) || (rc = dalloc(h, &DM2, q2)) || (rc = dalloc(h, &ag2, q2)) ||
           (rc = dalloc(h, &gid2, s2)) || (rc = dalloc(h, &key2, s2)) || (rc = dalloc(h, &subj2, s2)) ||
           (rc = dalloc(h, &ct2, s2)) || (rc = dalloc(h, &exp2, s2)) || (rc = dalloc(h, &used2, s2)) ||
-          (rc = dalloc(h, &fl2, s2)) || (rc = dalloc(h, &fexp2, s2)))
-        return rc;
+          (rc = dalloc(h, &fl2, s2)) || (rc = dalloc(h, &fexp2, s2))) {
+        dfree(h, S2, 2 * N * s2), dfree(h, HB2, 8 * N * q2), dfree(h, WB2, 8 * N * q2), dfree(h, GU2, 8 * q2);
+        dfree(h, DM2, 8 * q2), dfree(h, ag2, 4 * q2), dfree(h, gid2, 8 * s2), dfree(h, key2, 8 * s2);
+        dfree(h, subj2, 4 * s2), dfree(h, ct2, 4 * s2), dfree(h, exp2, 4 * s2), dfree(h, used2, 4 * s2);
+        dfree(h, fl2, 4 * s2);
+        return rc;  // the old table stays in use
+      }
       // rows: the old columns, then zero (no holder of a new slot)
       HIPCK(hipMemcpy2DAsync(S2, 2 * s2, d.S, 2 * s1, 2 * s1, N, hipMemcpyDeviceToDevice, st));
       HIPCK(hipMemset2DAsync(S2 + s1, 2 * s2, 0, 2 * (s2 - s1), N, st));
@@ -1373,6 +1398,19 @@ int swim_step(swim_handle* h, uint32_t n) {
       if (kh < k || kh >= k + (nb - i)) return fail(h, SWIM_EDEVICE, "speculative batch: bad halt tick");
       HIPCK(hipMemsetAsync(d.halt, 0, 4, h->stream));
       const uint32_t ih = i + (kh - k);
+      // a speculative member launch publishes no flag (tick_flag): the slots in use after member(kh) are read here, so
+      // the first gossip plane after an idle stretch gets the same capacity check as every other one (grow_caps); the
+      // device copy of the flag word follows, so tick_flag keeps writing it only on a change
+      {
+        int32_t top = 0;
+        HIPCK(hipMemcpyAsync(&top, d.free_top, 4, hipMemcpyDeviceToHost, h->stream));
+        HIPCK(hipStreamSynchronize(h->stream));
+        const uint32_t used = (uint32_t)((int32_t)d.SPR - top);
+        h->hflag[0] = used;
+        HIPCK(hipMemcpyAsync(d.hsh, &used, 4, hipMemcpyHostToDevice, h->stream));
+        int gr;
+        if ((gr = grow_caps(h)) != SWIM_OK) return gr;
+      }
       launch_gossip(d, kh, h->stream, timed(kh) ? &h->prof[ih] : nullptr);
       h->gossip_idle = false;
       need_diff = true;  // diff(kh + 1) returned at once
@@ -2073,6 +2111,37 @@ int swim_debug_caps(swim_handle* h, uint64_t* out, size_t n) {
   if (h->grp) return SWIM_EUNSUPPORTED;
   const uint64_t v[8] = {h->d.SPR, h->d.BCAP, h->d.RCAP, h->d.RPCAP, h->d.HCAP, h->growths, 0, 0};
   for (size_t i = 0; i < n; ++i) out[i] = v[i];
+  return SWIM_OK;
+}
+
+int swim_debug_holders(swim_handle* h, uint32_t first, uint32_t n, uint32_t* out) {
+  if (!h || !out) return SWIM_EINVAL;
+  if (h->grp) return SWIM_EUNSUPPORTED;
+  const Dev& d = h->d;
+  if (d.W > 1 || (uint64_t)first + n > d.N) return d.W > 1 ? SWIM_EUNSUPPORTED : SWIM_EINVAL;
+  if (n == 0) return SWIM_OK;
+  uint32_t* buf = nullptr;
+  HIPCK(hipMalloc(&buf, 20ull * n));
+  launch_dbg_holders(d, first, n, buf, h->stream);
+  HIPCK(hipStreamSynchronize(h->stream));
+  const hipError_t e = hipMemcpy(out, buf, 20ull * n, hipMemcpyDeviceToHost);
+  hipFree(buf);
+  HIPCK(e);
+  return SWIM_OK;
+}
+
+int swim_debug_set_incarnation(swim_handle* h, uint32_t m, uint32_t inc) {
+  if (!h) return SWIM_EINVAL;
+  if (h->grp || h->d.W > 1) return SWIM_EUNSUPPORTED;
+  const Dev& d = h->d;
+  if (m >= d.N || d.implicit) return SWIM_EINVAL;
+  if (inc >= INC_LIMIT) return SWIM_ECAPACITY;
+  HIPCK(hipStreamSynchronize(h->stream));
+  uint32_t* w = d.rowk + lidx(d, m) * d.NS + m;
+  uint32_t k = 0;
+  HIPCK(hipMemcpy(&k, w, 4, hipMemcpyDeviceToHost));
+  k = (inc << 2) | (k & 3u);
+  HIPCK(hipMemcpy(w, &k, 4, hipMemcpyHostToDevice));
   return SWIM_OK;
 }
 

@@ -433,9 +433,9 @@ __device__ __forceinline__ void tick_reset(const Dev& d, uint32_t k) {
 // end of k_member_tick (W == 1, the last block, one thread): reset the per-tick counters the gossip plane of this tick and the SYNC diff and
 // member control of the next tick append to, and tell the host whether any gossip slot is in use (if none, the
 // gossip data plane of this tick has nothing to send, deliver, route or recycle and is not launched)
-// In a speculative batch the host reads nothing until the batch ends: a gossip plane needed raises d.halt instead
-// (no system-scope fence: that writes back the XCD's L2 at the end of every tick)
-__device__ __forceinline__ void tick_flag(const Dev& d, uint32_t k, bool spec) {
+// (A speculative launch never runs this: it resets the counters at its start, tick_reset, and the member taking a slot
+// raises d.halt.)
+__device__ __forceinline__ void tick_flag(const Dev& d, uint32_t k) {
   uint32_t nb = (k + 1) & 1;
   // every load first (in flight together), then the stores; the host-mapped words are written only when they change
   // (a write to host memory holds the end of the kernel for a round trip over the host link)
@@ -463,11 +463,7 @@ __device__ __forceinline__ void tick_flag(const Dev& d, uint32_t k, bool spec) {
       d.hflag[i == 0 ? 0 : i + 1] = v[i];  // [0] slots in use, [2..6] the peaks
       d.hsh[i] = v[i];
     }
-  if (!spec) {
-    __threadfence_system();
-  } else if (used) {
-    *d.halt = k + 1u;
-  }
+  __threadfence_system();
 }
 
 }  // namespace swim

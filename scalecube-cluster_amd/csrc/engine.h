@@ -318,10 +318,12 @@ struct Dev {
   unsigned long long* wt;   // SWIM_EXP & 512: per-wave timestamps of the latest k_member_tick [waves][16]
   uint32_t* err;            // [8] bits, info...
   const Dev* self;          // device-resident copy of this struct (kernels index it through a pointer)
-  uint32_t* hflag;          // host-mapped: [0] gossip slots in use after this tick's member control (W == 1)
-  uint32_t* hsh;            // [8] what hflag holds (device copy): tick_flag writes host memory only on a change
-                            // [1] halt tick (speculative batches); with rfill: the previous gossip plane's largest
-                            // receipt-ring fill [2], routed receipts [3], replay and slow-path sends [4], [5]
+  uint32_t* hflag;          // host-mapped: [0] gossip slots in use after this tick's member control (W == 1);
+                            // [1] the halt tick read back after a speculative batch; with rfill: the previous gossip
+                            // plane's largest receipt-ring fill [2], routed receipts [3], replay and slow-path sends
+                            // [4], [5], history entries in use [6]
+  uint32_t* hsh;            // [8] device copy of what hflag holds (tick_flag writes host memory only on a change):
+                            // hsh[0] mirrors hflag[0], hsh[1..5] mirror hflag[2..6]
   uint32_t* rfill;          // [1] W == 1: largest ring fill (rtail - rhead) after this tick's receipts (grow_caps)
   uint32_t* dbg_send;       // debugging aid (SWIM_SEND_LOG=cap): [cap][5] tick, sender, gid lo, gid hi, target
   uint32_t* dbg_send_n;
@@ -450,5 +452,6 @@ void launch_s_scrub(const Dev& d, uint32_t now, void* stream);  // every SCRUB t
 void launch_ring_move(const uint32_t* rg, uint32_t* rg2, const uint32_t* rhead, const uint32_t* rtail, uint32_t N,
                       uint32_t B, uint32_t B2, void* stream);  // capacity growth of the receipt rings
 void launch_hist_rehash(const uint64_t* h1, uint32_t cap1, uint64_t* h2, uint32_t cap2, void* stream);
+void launch_dbg_holders(const Dev& d, uint32_t first, uint32_t n, uint32_t* out, void* stream);  // swim_debug_holders
 
 }  // namespace swim

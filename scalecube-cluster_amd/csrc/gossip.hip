@@ -1196,4 +1196,27 @@ __global__ void __launch_bounds__(256) k_hist_rehash(const uint64_t* h1, uint32_
 void launch_hist_rehash(const uint64_t* h1, uint32_t cap1, uint64_t* h2, uint32_t cap2, void* stream) {
   hipLaunchKernelGGL(k_hist_rehash, dim3(2048), dim3(256), 0, (hipStream_t)stream, h1, cap1, h2, cap2);
 }
+
+// test surface (swim_debug_holders): per member of [first, first + n): its gossip count, the receipt-ring positions of
+// the first held entry and of the end, the popcount of its held-bit row, and the first receipts whose GOSSIP events the
+// next P4 folds (RUMOR mode without recorded events)
+__global__ void __launch_bounds__(256) k_dbg_holders(const Dev* __restrict__ dp, uint32_t first, uint32_t n, uint32_t* out) {
+  const Dev& d = *dp;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t m = first + i;
+    const unsigned long long* hb = d.HB + (size_t)m * d.QW;
+    uint32_t pop = 0;
+    for (uint32_t w = 0; w < d.QW; ++w) pop += (uint32_t)__popcll(hb[w]);
+    uint32_t* o = out + 5ull * i;
+    o[0] = d.held[m];
+    o[1] = d.rhead[m];
+    o[2] = d.rtail[m];
+    o[3] = pop;
+    o[4] = d.evp_n ? d.evp_n[m] : 0u;
+  }
+}
+void launch_dbg_holders(const Dev& d, uint32_t first, uint32_t n, uint32_t* out, void* stream) {
+  hipLaunchKernelGGL(k_dbg_holders, dim3(std::min<uint32_t>(4096, (n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     d.self, first, n, out);
+}
 }  // namespace swim

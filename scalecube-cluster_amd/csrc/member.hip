@@ -1780,7 +1780,7 @@ __global__ void __launch_bounds__(256, 2) k_member_tick(const Dev* __restrict__ 
   if ((flag & 3u) != 1u) return;
   if (!last_block_ticket(d.mdone, gridDim.x) || threadIdx.x != 0) return;
   *d.mdone = 0;
-  tick_flag(d, k, false);
+  tick_flag(d, k);
 }
 
 }  // namespace swim

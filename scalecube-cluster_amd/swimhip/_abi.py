@@ -206,6 +206,8 @@ FB_NAMES = ["trk_walk", "ulog", "creq", "cwmax", "cev_slow", "replay", "mq", "so
 DEBUG_SIGNATURES = {
     "swim_debug_fallbacks": (C.c_int, [_H, C.POINTER(C.c_uint64), C.c_size_t]),
     "swim_debug_caps": (C.c_int, [_H, C.POINTER(C.c_uint64), C.c_size_t]),
+    "swim_debug_holders": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "swim_debug_set_incarnation": (C.c_int, [_H, C.c_uint32, C.c_uint32]),
 }
 CAP_NAMES = ["slots", "ring", "receipts", "replay", "history", "growths"]
 
@@ -219,6 +221,26 @@ def debug_caps(lib, handle):
     if rc != 0:
         raise RuntimeError(f"swim_debug_caps rc={rc}")
     return dict(zip(CAP_NAMES, (int(x) for x in out)))
+
+
+def debug_holders(lib, handle, first, n):
+    """[n][5] uint32 array: per member of [first, first + n) its gossip count, receipt-ring head and end positions,
+    held-bit popcount and pending folded GOSSIP events (include/swimhip_debug.h swim_debug_holders)."""
+    import numpy as np
+    fn = lib.swim_debug_holders
+    fn.restype, fn.argtypes = DEBUG_SIGNATURES["swim_debug_holders"]
+    out = np.zeros((n, 5), dtype=np.uint32)
+    rc = fn(handle, first, n, out.ctypes.data_as(C.POINTER(C.c_uint32)))
+    if rc != 0:
+        raise RuntimeError(f"swim_debug_holders rc={rc}")
+    return out
+
+
+def debug_set_incarnation(lib, handle, m, inc):
+    """Member m's own record at incarnation inc (include/swimhip_debug.h swim_debug_set_incarnation); the return code."""
+    fn = lib.swim_debug_set_incarnation
+    fn.restype, fn.argtypes = DEBUG_SIGNATURES["swim_debug_set_incarnation"]
+    return fn(handle, m, inc)
 
 
 def debug_fallbacks(lib, handle):

@@ -66,6 +66,15 @@ def _c4_large():  # C4's full schedule (BASELINE configs[3]) at 1 000 members: p
         ("partition", g), ("periods", 200), ("unblock", None), ("periods", 120)]
 
 
+def _c2_full():  # C2 at its configured size (BASELINE configs[1]: 10 000 members, 5 % loss, preconverged) for as many
+    # periods as the oracle can hold in this container's 64 GB: it keeps GossipState.infectedFrom as explicit per-holder
+    # sets, so its memory grows with the re-spread storm (measured: period 2 4.4 s / 3.4 GB, period 3 152 s / 32 GB with
+    # 2.2e4 gossips created and 3.7e8 gossip messages; period 4 creates ~3.5x the gossips and does not fit). Periods 1-3
+    # already run the SYNC re-spreads (SYNCs are staggered over the first 300 ticks) and the suspicion refutations.
+    # Recorded once (SWIMREF_THREADS=8 python tests/golden/make_golden.py c2_full, ~3 min); replayed on 1 and 2 shards
+    return SimConfig(n_members=10_000, record_events=True), [("loss", 5), ("periods", 3)]
+
+
 def _c3_small():  # C3-shaped: steady state SYNC / SYNC_ACK anti-entropy, no loss
     return SimConfig(n_members=1000), [("periods", 35)]
 
@@ -75,8 +84,8 @@ def _c5_small():  # C5-shaped: rumor-only dissemination with 1 % churn per perio
 
 
 SCENARIOS = {"c1": _c1, "c2_small": _c2_small, "c4_small": _c4_small, "c3_small": _c3_small, "c5_small": _c5_small,
-             "c4_mid": _c4_mid, "c2_mid": _c2_mid, "c4_long": _c4_long, "c4_large": _c4_large}
-SLOW_ON_ORACLE = {"c4_mid", "c2_mid", "c4_long", "c4_large"}  # recorded once; replaying it on the oracle takes minutes
+             "c4_mid": _c4_mid, "c2_mid": _c2_mid, "c4_long": _c4_long, "c4_large": _c4_large, "c2_full": _c2_full}
+SLOW_ON_ORACLE = {"c4_mid", "c2_mid", "c4_long", "c4_large", "c2_full"}  # recorded once; replaying it on the oracle takes minutes
 FULL_EVENTS = {"c1"}
 
 

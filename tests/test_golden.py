@@ -50,7 +50,7 @@ def test_engine_matches_golden(engine, name):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,world", [("c1", 2), ("c2_small", 3), ("c4_small", 2), ("c3_small", 4), ("c5_small", 3),
                                         ("c4_mid", 2), ("c2_mid", 2), ("c4_long", 2),
-                                        ("c4_large", 2)])
+                                        ("c4_large", 2), ("c2_full", 2)])
 def test_sharded_engine_matches_golden(engine, name, world):
     from swimhip.shard import ThreadShardGroup
     cfg, _ = SCENARIOS[name]()

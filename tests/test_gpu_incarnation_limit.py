@@ -1,0 +1,37 @@
+"""The 30-bit incarnation field of the key plane (SEMANTICS.md §8).
+
+MembershipRecord.incarnation is a Java `int` (MembershipRecord.java:12-84): it starts at 0 and grows by one per
+refutation or updateIncarnation call (MembershipProtocolImpl.java:178-190,488-509), so 2^31 - 1 is its largest value.
+The engine stores a record as the 4-B key `inc << 2 | status` (what k_sync_diff streams), so it holds incarnations up
+to 2^30 - 1 and raises SWIM_ECAPACITY (E_INC) instead of truncating above that. These tests put one member's own record
+just below the limit (swim_debug_set_incarnation) and check both sides of it: 2^30 - 1 is stored, gossiped and merged
+everywhere like any other incarnation; the bump past it fails loudly."""
+import pytest
+
+from swimhip import SimConfig, _abi
+from swimhip.cluster import SimulatedCluster, SwimError
+
+pytestmark = pytest.mark.gpu
+
+LIMIT = 1 << 30
+
+
+def test_incarnation_at_the_limit(engine):
+    n, m = 40, 11
+    c = SimulatedCluster(engine, SimConfig(n_members=n, record_events=True))
+    try:
+        c.step(3)
+        assert _abi.debug_set_incarnation(engine, c._h, m, LIMIT) == -4  # SWIM_ECAPACITY: not representable
+        assert _abi.debug_set_incarnation(engine, c._h, m, LIMIT - 2) == 0
+        c.update_incarnation(m)  # -> 2^30 - 1, spread as a gossip to every member (UPDATED events after metadata)
+        c.step(200)
+        for obs in range(n):
+            key = int(c.row(obs)[m])
+            assert key & 0xFFFFFFFF == LIMIT - 1 and (key >> 32) & 3 == 1, (obs, hex(key))
+        upd = {e.observer for e in c.events() if e.isUpdated() and e.member == m}
+        assert upd == set(range(n)) - {m}
+        c.update_incarnation(m)  # -> 2^30: past the key plane's field
+        with pytest.raises(SwimError, match="error bits 0x100000"):
+            c.step(2)
+    finally:
+        c.close()
