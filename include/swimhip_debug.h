@@ -5,7 +5,8 @@
  * when one is full. Those fallbacks must give the same bits as the fast path, so tests force them:
  * the environment variable SWIM_CAPS, read by swim_create, lowers the capacities, e.g.
  *   SWIM_CAPS="trk=1,ulog=2,creq=1,cwmax=1,cev=1,mq=1,sort=2"
- *   trk    subjects tracked per receiver and tick for later SYNC payloads (more: whole-row walk),
+ *   trk    subjects tracked per receiver and tick in a sorted list for later SYNC payloads (more: the written-subject
+ *          bitmap is walked in subject order),
  *          MembershipProtocolImpl.syncMembership (:456-467) with several payloads in one tick
  *   ulog   row writes logged after a SYNC send of the same tick (more: the lane copies its open snapshots),
  *          prepareSyncDataMsg (:446-454) snapshot semantics
@@ -36,7 +37,7 @@ extern "C" {
 #endif
 
 /* indices into swim_debug_fallbacks' output */
-#define SWIM_FB_TRK_WALK 0u    /* whole-row SYNC walks (trk) */
+#define SWIM_FB_TRK_WALK 0u    /* later SYNC payloads merged with the written-subject bitmap (trk) */
 #define SWIM_FB_ULOG 1u        /* snapshot copies forced by a full undo log (ulog) */
 #define SWIM_FB_CREQ 2u        /* snapshot copies forced by too many open snapshots (creq) */
 #define SWIM_FB_CWMAX 3u       /* lane row copies, block list full (cwmax) */

@@ -71,11 +71,15 @@ struct swim_handle {
   bool no_pipe = getenv("SWIM_NO_PIPELINE") != nullptr;    // debugging aid: no early SYNC diff of the next tick
   bool no_spec = getenv("SWIM_NO_SPECULATION") != nullptr;  // debugging aid: a host wait after every member kernel
   bool gossip_idle = false;  // W == 1: no gossip slot was in use after the latest member kernel
+  bool gossip_ran = false;   // W == 1: the latest tick ran the gossip plane (the next P4 may have routed receipts)
   uint64_t growths = 0;      // capacity growth steps so far (grow_caps)
   uint64_t grow_next = 0;    // grow_caps: no attempt before this tick (the last one found no room)
   // timing aid (bench.py --rehearse-shard): a slot shard alone, its peers' gossip-count deltas taken as zero without
   // any exchange (not the W-shard simulation's results)
   bool lone = getenv("SWIM_LONE_SHARD") != nullptr;
+  // timing aid (SWIM_STATS): the gossip plane's work per tick on stderr (routed receipts, targets, active groups,
+  // replay / slow-path sends, contact pairs, RX rows); one stream wait per tick
+  bool stats = getenv("SWIM_STATS") != nullptr;
   Group* grp = nullptr;  // n_gpus > 1: every call is forwarded to the shards (d holds shard 0's constants only)
 };
 
@@ -484,7 +488,11 @@ int build(swim_handle* h) {
   d.exp = getenv("SWIM_EXP") ? (uint32_t)atoi(getenv("SWIM_EXP")) : 0u;  // timing experiments: wrong results
   // fast-structure capacities (include/swimhip_debug.h): SWIM_CAPS="trk=1,ulog=2,creq=1,cwmax=1,cev=1,mq=1,sort=2"
   // lowers them so that the exact fallbacks run; results stay bit-exact, only slower
-  d.trk_cap = TRK, d.ulog_cap = ULOG, d.creq_cap = CREQ, d.cwmax_cap = CWMAX, d.cev_cap = CEV, d.mq_cap = MQ;
+  // undo log per member: a receiver merging thousands of records after a SYNC_ACK send (C2) would otherwise copy its
+  // row on its own lane (cow_now); 1024 entries up to 65 536 members (8 KB each), 256 above
+  d.ULOGC = c.n_members <= 65536 ? ULOG : 256;
+  d.trk_cap = TRK, d.ulog_cap = d.ULOGC, d.creq_cap = CREQ, d.cwmax_cap = CWMAX, d.cev_cap = CEV, d.mq_cap = MQ;
+  d.hv = 24;  // routed receipts from which a member's P4 runs on a wave of its own (k_inbox_apply)
   d.XI = XINL;
   d.sort_cap = SORT_MAX;
   uint32_t rx_cap = NEVER, rp_cap = 0;
@@ -503,11 +511,12 @@ int build(swim_handle* h) {
       const uint32_t v = (uint32_t)strtoul(kv.c_str() + eq + 1, nullptr, 0);
       auto clampv = [&](uint32_t lo, uint32_t hi) { return std::max(lo, std::min(hi, v)); };
       if (k == "trk") d.trk_cap = clampv(0, TRK);
-      else if (k == "ulog") d.ulog_cap = clampv(0, ULOG);
+      else if (k == "ulog") d.ulog_cap = clampv(0, d.ULOGC);
       else if (k == "creq") d.creq_cap = clampv(1, CREQ);
       else if (k == "cwmax") d.cwmax_cap = clampv(0, CWMAX);
       else if (k == "cev") d.cev_cap = clampv(0, CEV);
       else if (k == "mq") d.mq_cap = clampv(1, MQ);
+      else if (k == "hv") d.hv = std::max<uint32_t>(1, v);  // k_inbox_apply from this many receipts
       else if (k == "rx") rx_cap = v;
       else if (k == "rp") rp_cap = std::max<uint32_t>(64, v);  // replay / slow-path send lists (grow_caps tests)
       else if (k == "xinl") d.XI = std::max<uint32_t>(64, std::min<uint32_t>(XINL, v)) & ~7u;  // send/recv group past it
@@ -548,6 +557,7 @@ int build(swim_handle* h) {
   // rounds kept for the infectedFrom replay (a delayed send arrives up to EMAX ticks after its round)
   while (d.LOGW < 4 * (maxSpread + 2) + 2 * ((d.EMAX + d.gossip_t - 1) / d.gossip_t + 1)) d.LOGW <<= 1;
   d.LOOKBACK = d.LOGW * d.gossip_t;
+  d.gt_mul = d.gossip_t == 1 ? 0xFFFFFFFFu : (uint32_t)((1ull << 32) / d.gossip_t);
   // incarnation history of reborn (gossip, member) pairs (88 B per entry). 2^20 entries (92 MB) by default; a run
   // that asks for a large slot table (a storm: C4's heal rebirths a large share of the holder states) gets one
   // entry per 8 holder states, up to 2^24; SWIM_HIST_CAP overrides (a full table raises E_REBORN, info 1)
@@ -676,8 +686,13 @@ int build(swim_handle* h) {
   A(d.rc_slot, d.RCAP) A(d.rc_ndrop, N) A(d.dead_rx, N) A(d.leaving, N) A(d.rc_key, d.RCAP) A(d.rc_slot2, d.RCAP) A(d.rc_key2, d.RCAP) A(d.fexp, d.SLOTS) A(d.nfexp, 1) A(d.hist, (uint64_t)d.HCAP * HREC)
   A(d.msgs[0], d.MSGCAP) A(d.msgs[1], d.MSGCAP) A(d.nmsg, 2) A(d.arena[0], (uint64_t)d.ARENA_ROWS * d.NS)
   A(d.arena[1], (uint64_t)d.ARENA_ROWS * d.NS) A(d.arena_used, 2)
-  A(d.m_next, 2ull * d.MSGCAP) A(d.m_head, 2 * N) A(d.next_evt, N) A(d.mdone, 2) A(d.trk, NL * TRK) A(d.ulog, NL * ULOG * 2) A(d.spq, NL * SPQ * 8) A(d.fpend, NL * KP * 2) A(d.pending_inc, N) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
+  A(d.m_next, 2ull * d.MSGCAP) A(d.m_head, 2 * N) A(d.next_evt, N) A(d.mdone, 2) A(d.trk, NL * TRKL) A(d.ulog, NL * d.ULOGC * 2) A(d.spq, NL * SPQ * 8) A(d.fpend, NL * KP * 2) A(d.pending_inc, N) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
   A(d.pool, d.POOLCAP) A(d.pool_used, 1)
+  d.NW = d.implicit ? 0u : (d.N + 63u) / 64u;  // (RUMOR mode with implicit views has no SYNC)
+  A(d.hv_list, NL) A(d.nhv, 1) A(d.hv_pend, NL) A(d.hv_tlast, NL)
+  HIPCK(hipMemsetAsync(d.nhv, 0, 4, h->stream));
+  A(d.tbm, std::max<uint64_t>(1, NL * d.NW))
+  HIPCK(hipMemsetAsync(d.tbm, 0, 8 * std::max<uint64_t>(1, NL * d.NW), h->stream));
   // SYNC_ACK resolution (k_ack_resolve); SWIM_NO_ACKRES streams every payload (measurements)
   d.ackres = !d.implicit && !getenv("SWIM_NO_ACKRES") ? 1u : 0u;
   if (d.ackres) {
@@ -1392,6 +1407,7 @@ int swim_step(swim_handle* h, uint32_t n) {
       if (hk == 0) {  // the whole batch ran
         h->tick += nb - i;
         i = nb;
+        h->gossip_ran = false;
         continue;
       }
       const uint32_t kh = hk - 1u;  // member(kh) ran; the launches after it returned at once
@@ -1413,6 +1429,7 @@ int swim_step(swim_handle* h, uint32_t n) {
       }
       launch_gossip(d, kh, h->stream, timed(kh) ? &h->prof[ih] : nullptr);
       h->gossip_idle = false;
+      h->gossip_ran = true;
       need_diff = true;  // diff(kh + 1) returned at once
       h->tick = kh + 1ull;
       i = ih + 1;
@@ -1421,7 +1438,7 @@ int swim_step(swim_handle* h, uint32_t n) {
     if (d.W == 1) {
       // SYNC diff(k) was queued in the previous iteration, except for the first tick of this call
       if (need_diff) launch_diff(d, k, h->stream, te);
-      launch_member(d, k, h->stream, te);
+      launch_member(d, k, h->stream, te, false, h->gossip_ran && !d.fastp4);
       const bool nosync = (d.exp & 256) != 0;  // timing experiment: no per-tick event (gossip plane never launched)
       if (!nosync) HIPCK(hipEventRecord(h->ev_member, h->stream));
       const bool pipe = i + 1 < n && !h->no_pipe;
@@ -1433,9 +1450,25 @@ int swim_step(swim_handle* h, uint32_t n) {
         int gr;
         if ((gr = grow_caps(h)) != SWIM_OK) return gr;
       }
+      h->gossip_ran = !nosync && (h->hflag[0] != 0 || h->no_skip);
       if (nosync) {
       } else if (h->hflag[0] != 0 || h->no_skip) {
         launch_gossip(d, k, h->stream, te);
+        if (h->stats) {
+          uint32_t v[8];
+          HIPCK(hipStreamSynchronize(h->stream));
+          const uint32_t* src[8] = {d.rc_n, d.ntl, d.nagroup, d.rp_n, d.slow_n, d.ncfl, d.nrx, d.nrwl};
+          for (int q = 0; q < 8; ++q) HIPCK(hipMemcpy(&v[q], src[q], 4, hipMemcpyDeviceToHost));
+          std::vector<uint32_t> rc(d.N), nf(d.N);
+          HIPCK(hipMemcpy(rc.data(), d.rc_cnt, 4ull * d.N, hipMemcpyDeviceToHost));
+          HIPCK(hipMemcpy(nf.data(), d.nfetch, 4ull * d.N, hipMemcpyDeviceToHost));
+          std::sort(rc.begin(), rc.end());
+          std::sort(nf.begin(), nf.end());
+          fprintf(stderr, "stats tick %u: routed %u targets %u groups %u replay %u slow %u contacts %u rx %u rounds %u; "
+                  "receipts per member median %u p99 %u max %u; pending fetches median %u p99 %u max %u\n",
+                  k, v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], rc[d.N / 2], rc[d.N * 99 / 100], rc[d.N - 1],
+                  nf[d.N / 2], nf[d.N * 99 / 100], nf[d.N - 1]);
+        }
       } else if (te && te->all) {
         HIPCK(hipEventRecord((hipEvent_t)te->ev[4], h->stream));
         HIPCK(hipEventRecord((hipEvent_t)te->ev[5], h->stream));

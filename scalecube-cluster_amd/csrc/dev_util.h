@@ -148,14 +148,15 @@ __device__ __noinline__ int xmit_delay(const Dev& d, uint32_t di, uint32_t kind,
   return (int)delay_ticks(d, di, delay_draw(d.seed_lo, d.seed_hi, kind, src, dst, k, aux, id));
 }
 
-// tryFail + tryDelay of one non-gossip message: -1 if the send fails, else its delay in ticks past lat
+// tryFail + tryDelay of one non-gossip message: -1 if the send fails, else its delay in ticks past lat. dd: whether
+// dst is dead at k when the caller loaded it already (-1: look it up)
 __device__ __forceinline__ int xmit_ep(const Dev& d, int ep, uint32_t kind, uint32_t src, uint32_t dst, uint32_t k,
-                                       uint32_t aux, uint32_t id) {
+                                       uint32_t aux, uint32_t id, int dd = -1) {
   if (ep < 0) {
     set_err(d, E_EPOCH);
     return -1;
   }
-  if (dead_at(d, dst, k)) return -1;  // connection refused: fails before the emulator, not counted
+  if (dd < 0 ? dead_at(d, dst, k) : dd != 0) return -1;  // connection refused: fails before the emulator, not counted
   const uint32_t ls = link_set(d, ep, src, dst, k), loss = ls & 0xFFu, di = ls >> 8;
   const bool lost = loss >= 100 || (loss > 0 && loss_roll(d.seed_lo, d.seed_hi, kind, src, dst, k, aux, id) < loss);
   em_count(d, src, 1u, lost ? 1u : 0u);
@@ -314,10 +315,17 @@ __device__ __forceinline__ uint32_t payload_key_at(const Dev& d, const SyncMsg& 
   return d.arena[b][(size_t)mm.payload * d.NS + s];
 }
 
+// (c - f + gossip_t - 1) / gossip_t without an integer division (~35 instructions for a runtime divisor; the infectedFrom
+// replay evaluates this several times per replayed gossip): q = umulhi(x, floor(2^32 / gt)) is floor(x / gt) or one less
+__device__ __forceinline__ uint32_t div_gt(const Dev& d, uint32_t x) {
+  uint32_t q = __umulhi(x, d.gt_mul);
+  q += x - q * d.gossip_t >= d.gossip_t ? 1u : 0u;
+  return q;
+}
 __device__ __forceinline__ uint32_t rounds_before(const Dev& d, uint32_t x, uint32_t c) {
   uint32_t f = d.firstGossip[x];
   if (f == NEVER || c <= f) return 0;
-  return (c - f + d.gossip_t - 1) / d.gossip_t;
+  return div_gt(d, c - f + d.gossip_t - 1);
 }
 
 // ClusterMath (ClusterMath.java:99-125): gossipPeriodsToSpread, gossipPeriodsToSweep (from the spread), and

@@ -24,10 +24,11 @@ constexpr uint32_t SUBCAP = 8, PATHCAP = 8, FREC = 8, GREC = 8;
 // open for up to 4 x (lat + EMAX) ticks, several FD periods, so more of them overlap (Dev::PCAP <= 32)
 constexpr uint32_t PATHCAP_DELAY = 32;
 constexpr uint32_t CH = 2048;  // subjects per SYNC-diff work item (256 threads x 8)
-constexpr uint32_t TRK = 16;   // subjects written in one tick's P1 that are re-checked against later payloads
+constexpr uint32_t TRK = 16;   // subjects written in one tick's P1 that are re-checked against later payloads (sorted list)
+constexpr uint32_t TRKL = 64;  // of them listed per member for clearing its written-subject bitmap (more: the whole row)
 // deferred copy-on-write (member.hip cow): row writes logged per member and tick while a snapshot is open, open
 // snapshots per member, deferred snapshots per k_member_tick block
-constexpr uint32_t ULOG = 64, CREQ = 4, CWMAX = 32;
+constexpr uint32_t ULOG = 1024, CREQ = 4, CWMAX = 32;  // ULOG: the largest undo log (Dev::ULOGC is the stride in use)
 constexpr uint32_t SPQ = 32;  // gossips a member creates in one tick before their slots are taken together
 constexpr uint32_t KP = 64;   // FD-list inserts of one member's tick applied together (member.hip fd_flush)
 constexpr uint32_t MQ = 16;   // inbound SYNC messages of one tick sorted in registers (more: selected by list walks)
@@ -64,7 +65,9 @@ constexpr uint32_t LKCAP = 4096, LKH = 8;  // keys, history entries per key
 constexpr uint32_t CIN_SLOW = 0xFFFFFFFEu;
 constexpr uint32_t RX_ALL = 0xFFFFFFFFu;
 constexpr uint32_t MDU = 64;  // members with updated metadata per handle
-constexpr uint32_t CEV = 6, CEVW = 4 + 2 * CEV;  // cached contact events per (sender, target): n, oldest[2], events
+// cached contact events per (sender, target): n, oldest[2], last inbound, then per event tick, slot | dir | loss % |
+// spread, and the sender's rounds before the event's tick
+constexpr uint32_t CEV = 6, CEVW = 4 + 3 * CEV;
 // gossip incarnation history entry: 3 header words + HKEEP creation ticks of swept incarnations (small clusters
 // under loss re-infect a member with the same gossip many times: each late sender restarts the chain)
 constexpr uint32_t HREC = 11, HKEEP = 16;
@@ -90,7 +93,7 @@ enum Ctr { C_R = 0, C_W, C_M, C_G, C_E, C_LOST, C_GCREATED, C_SYNCMERGE, C_DIFFM
 // capacity fallbacks that fired (include/swimhip_debug.h; counted only when Dev::fb is allocated: SWIM_CAPS or
 // SWIM_FALLBACKS set at create). Each one is an exact slow path taken when a fixed-capacity fast structure is full.
 enum Fb {
-  FB_TRK_WALK = 0,  // merge_payload compared a later payload against the whole row (more than trk_cap tracked subjects)
+  FB_TRK_WALK = 0,  // merge_payload merged a later payload with the written-subject bitmap (more than trk_cap tracked)
   FB_ULOG,          // cow_now: a member's undo log was full (ulog_cap), its open snapshots copied by its lane
   FB_CREQ,          // cow_now: a member had creq_cap snapshots open
   FB_CWMAX,         // copy_row_to: the block's deferred snapshot list was full (cwmax_cap), the lane copied the row
@@ -146,6 +149,7 @@ struct Dev {
   uint32_t* ucnt;        // [N] scratch of the user-gossip queue: its entries per member (zero between launches)
   uint32_t seeds[16];
   uint32_t LCAP, FCAP, GRCAP, LOGW, SLOTS, MSGCAP, NCHUNK, POOLCAP, EVCAP, DCAP, RCAP, ARENA_ROWS, LOOKBACK, HCAP;
+  uint32_t gt_mul;  // floor(2^32 / gossip_t) (2^32 - 1 for 1): rounds_before divides by multiply-high + one correction
 
   // ---- network / fault history (NetworkEmulator settings per epoch) ----
   uint32_t* dead_tick;  // [N] tick from which the member is dead, NEVER = alive
@@ -287,8 +291,11 @@ struct Dev {
   // speculative batches (W == 1, gossip plane idle): tick + 1 of the member kernel after which the gossip plane was
   // needed (0: none); every later k_sync_diff / k_member_tick launch of the batch returns at once
   uint32_t* halt;
-  uint32_t* trk;    // [NL][TRK] per receiver: subjects its row changed earlier in this tick's P1 (member.hip)
-  uint32_t* ulog;   // [NL][ULOG][2] per member: (subject, old key) of its row writes this tick after a SYNC send
+  uint32_t* trk;    // [NL][TRKL] per receiver: subjects its row changed earlier in this tick's P1 (member.hip)
+  unsigned long long* tbm;  // [NL][NW] the same subjects as a bitmap (zero between ticks): merged in subject order
+  uint32_t NW;       // u64 words per bitmap row ((N + 63) / 64; no SYNC with implicit views: 0)
+  uint32_t* ulog;   // [NL][ULOGC][2] per member: (subject, old key) of its row writes this tick after a SYNC send
+  uint32_t ULOGC;   // undo-log entries per member (1024 up to 65 536 members, 256 above; ulog_cap <= ULOGC)
   uint32_t* spq;    // [NL][SPQ][8] per member: gossips created this tick, waiting for their slots (member.hip)
   uint32_t* fpend;  // [NL][KP][2] per member: this tick's pending FD-list inserts (subject, final position)
   uint32_t* chunk_meta;                      // [MSGCAP][NCHUNK][2] (pool offset, count)
@@ -306,6 +313,11 @@ struct Dev {
   // W > 1: the sender's write-log prefix (SyncMsg.tln entries) of each message of the inbound list committed this tick,
   // by its index there: copied by k_sync_route for this shard's senders and shipped in exchange A for the peers'
   uint32_t* mlog;     // [MSGCAP][TL]
+  // P4 of the members with many routed gossip receipts (W == 1, ticks after a gossip plane): k_member_tick parks a
+  // member with at least hv receipts before P4 (its pending live-row payload chain and write-log tail kept here),
+  // k_inbox_apply runs its P4 a wave per member, and a second k_member_tick launch runs its P5 and P6
+  uint32_t hv;
+  uint32_t *hv_list, *nhv, *hv_pend, *hv_tlast;  // [NL], [1], [NL], [NL]
 
   // ---- outputs ----
   uint32_t* ev;  // [EVCAP][8] swim_event
@@ -428,7 +440,10 @@ void launch_init(const Dev& d, void* stream);
 // says a gossip slot is in use; launch_diff(k+1) may be queued before launch_gossip(k)
 // spec: a launch of a speculative batch (it returns at once once d.halt is set)
 void launch_diff(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr, bool spec = false);
-void launch_member(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr, bool spec = false);
+// split: the previous tick ran the gossip plane (routed receipts for P4: k_member_tick parks the members with many,
+// k_inbox_apply runs their P4, a second k_member_tick launch their P5 and P6)
+void launch_member(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr, bool spec = false,
+                   bool split = false);
 void launch_gossip(const Dev& d, uint32_t k, void* stream, const TickEvents* prof = nullptr);
 // sharded tick (W > 1): A = SYNC diff + member control + pack exchange A; B = unpack A, gossip sends, pack
 // exchange B; C = unpack B, apply receipts, routing, slot recycling. The host runs the exchanges in between and

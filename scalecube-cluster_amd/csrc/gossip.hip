@@ -28,9 +28,35 @@ namespace swim {
 // state for g. Whether such a send was delivered depends, one level down, on whether x had delivered g to y earlier
 // (then y skips x), and so on. The dependency only runs over the contact events between the pair (x's rounds that
 // targeted y, y's rounds that targeted x). Those are replayed in tick order as a small dynamic program.
+// pct: NetworkEmulator's loss percent of the send (link_loss at its tick: 100 for a dead receiver or a blocked link),
+// rb: the sender's gossip rounds before its tick (rounds_before); both independent of the gossip, so they are evaluated
+// once per pair (k_contact_cache) instead of once per replayed gossip
 struct Contact {
   uint32_t tick, slot, spread, dir;  // dir 0: y -> x, 1: x -> y
+  uint32_t pct, rb;
 };
+
+// the pair-level parts of a contact event: sender snd -> receiver rcv at tick t2
+__device__ __forceinline__ Contact make_contact(const Dev& d, uint32_t t2, uint32_t s2, uint32_t spread, uint32_t dir,
+                                                uint32_t snd, uint32_t rcv) {
+  const int ep = epoch_at(d, t2);
+  uint32_t pct = 100;
+  if (ep < 0)
+    set_err(d, E_EPOCH);  // (lost_gossip_ep's answer: the send fails)
+  else
+    pct = link_loss(d, ep, snd, rcv, t2);
+  return Contact{t2, s2, spread, dir, pct, rounds_before(d, snd, t2)};
+}
+
+// lost_gossip_ep with the link's loss percent already known (Contact.pct)
+__device__ __forceinline__ bool lost_gossip_pct(const Dev& d, uint32_t pct, uint32_t src, uint32_t k, uint32_t slot,
+                                                uint64_t gid) {
+  if (pct == 0) return false;
+  if (pct >= 100) return true;
+  const u32x4 r = philox(src, k ^ ((slot >> 2) << 31), (uint32_t)(gid >> 32), (uint32_t)gid, d.seed_lo ^ SALT_LOSS_GOSSIP,
+                         d.seed_hi);
+  return next_int(pick(r, slot & 3), 100) < pct;
+}
 
 // incarnation history of (gid, member): creation ticks of swept incarnations (rebirths are rare)
 __device__ __forceinline__ uint64_t hist_tag(uint64_t gid, uint32_t member) {
@@ -132,7 +158,7 @@ __device__ __forceinline__ bool replay_pair(const Dev& d, uint32_t x, uint32_t y
       if (cinc[i] == NEVER - 1) cinc[i] = inc_at(d, c.dir == 0 ? y : x, g, gid, c.tick, tau + lat);
       uint32_t cs = cinc[i];
       uint32_t snd = c.dir == 0 ? y : x;
-      if (cs == NEVER || rounds_before(d, snd, cs) + c.spread < rounds_before(d, snd, c.tick)) continue;
+      if (cs == NEVER || rounds_before(d, snd, cs) + c.spread < c.rb) continue;
       if (swept_before(d, snd, cs, c.tick)) continue;
       uint32_t sin = 1 - rin;
       if (lo_in[sin] == NEVER || cs < lo_in[sin]) {
@@ -163,7 +189,7 @@ __device__ __forceinline__ bool replay_pair(const Dev& d, uint32_t x, uint32_t y
     // the sender held g at that round (its incarnation then), inside its spread window (selectGossipsToSend :246)
     uint32_t cs = cinc[i] != NEVER - 1 ? cinc[i] : inc_at(d, snd, g, gid, c.tick, tau + lat);
     if (cs == NEVER) continue;
-    if (rounds_before(d, snd, cs) + c.spread < rounds_before(d, snd, c.tick)) continue;
+    if (rounds_before(d, snd, cs) + c.spread < c.rb) continue;
     if (swept_before(d, snd, cs, c.tick)) continue;  // x no longer held it
     // the receiver delivered g to the sender during that incarnation: infectedFrom (isInfected :247)
     uint32_t od = 1 - c.dir;  // opposite direction
@@ -171,7 +197,7 @@ __device__ __forceinline__ bool replay_pair(const Dev& d, uint32_t x, uint32_t y
     for (uint32_t q = 0; q < nd[od] && !blocked; ++q) blocked = del[od][q] >= cs && del[od][q] <= c.tick;
     if (blocked) continue;
     const uint32_t rcv = c.dir == 0 ? x : y;
-    if (lost_gossip(d, snd, rcv, c.tick, c.slot, gid)) continue;
+    if (lost_gossip_pct(d, c.pct, snd, c.tick, c.slot, gid)) continue;
     del[c.dir][nd[c.dir]++] = d.dly_on ? gossip_arrival(d, snd, rcv, c.tick, c.slot, gid) : c.tick + lat;
   }
   for (uint32_t q = 0; q < nd[0]; ++q)
@@ -203,7 +229,7 @@ __device__ __forceinline__ uint32_t collect_contacts(const Dev& d, uint32_t x, u
             ev[j] = ev[j - 1];
             --j;
           }
-          ev[j] = Contact{t2, s2, d.log_spread[li], (uint32_t)side};
+          ev[j] = make_contact(d, t2, s2, d.log_spread[li], (uint32_t)side, from, to);
         }
     }
     oldest[side] = wrapped ? old : 0;
@@ -235,16 +261,16 @@ __device__ __forceinline__ bool blocked_pair_cached(const Dev& d, uint32_t x, ui
   // are older than the gossip)
   bool relevant = false;
   for (uint32_t i = 0; i < nall; ++i) {
-    const uint32_t t2 = rec[4 + 2 * i];
-    relevant |= ((rec[5 + 2 * i] >> 8) & 1u) == 0 && t2 >= born && t2 + d.lat + dmax(d) >= cx;
+    const uint32_t t2 = rec[4 + 3 * i];
+    relevant |= ((rec[5 + 3 * i] >> 8) & 1u) == 0 && t2 >= born && t2 + d.lat + dmax(d) >= cx;
   }
   if (!relevant) return false;
   Contact ev[CEV];
   uint32_t n = 0;
   for (uint32_t i = 0; i < nall; ++i) {
-    const uint32_t t2 = rec[4 + 2 * i], w = rec[5 + 2 * i];
+    const uint32_t t2 = rec[4 + 3 * i], w = rec[5 + 3 * i];
     if (t2 < born) continue;
-    ev[n++] = Contact{t2, w & 0xFFu, w >> 16, (w >> 8) & 1u};
+    ev[n++] = Contact{t2, w & 0xFFu, w >> 16, (w >> 8) & 1u, (w >> 9) & 0x7Fu, rec[6 + 3 * i]};
   }
   const uint32_t oldest[2] = {rec[1], rec[2]};
   return replay_pair<CEV>(d, x, y, g, gid, tau, cx, ev, n, oldest);
@@ -501,7 +527,8 @@ __device__ uint32_t collect_contacts_wave(const Dev& d, uint32_t m, uint32_t t, 
       }
       const uint32_t tot = __shfl(incl, 63);
       if (n <= CEV && n + tot <= CEV)
-        for (uint32_t j = n + incl - c; hits; hits &= hits - 1, ++j) ev[j] = Contact{t2, (uint32_t)(__ffs(hits) - 1), sp, side};
+        for (uint32_t j = n + incl - c; hits; hits &= hits - 1, ++j)
+          ev[j] = make_contact(d, t2, (uint32_t)(__ffs(hits) - 1), sp, side, from, to);
       n = min(n + tot, CEV + 1u);
     }
 #pragma unroll
@@ -532,8 +559,9 @@ __device__ void contact_cache(const Dev& d, uint32_t i, uint32_t m, uint32_t t, 
   uint32_t last_in = NEVER;  // latest t -> m contact (NEVER: none); overflow is flagged by n alone
   if (n <= CEV)
     for (uint32_t j = 0; j < n; ++j) {
-      rec[4 + 2 * j] = ev[j].tick;
-      rec[5 + 2 * j] = ev[j].slot | (ev[j].dir << 8) | (ev[j].spread << 16);
+      rec[4 + 3 * j] = ev[j].tick;
+      rec[5 + 3 * j] = ev[j].slot | (ev[j].dir << 8) | (ev[j].pct << 9) | (ev[j].spread << 16);
+      rec[6 + 3 * j] = ev[j].rb;
       if (ev[j].dir == 0) last_in = ev[j].tick;  // events are in tick order
     }
   rec[3] = last_in;

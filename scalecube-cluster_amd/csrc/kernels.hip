@@ -923,10 +923,17 @@ __global__ void __launch_bounds__(256) k_sync_defer_x(Dev d, uint32_t k, uint32_
   }
 }
 
-void launch_member(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool spec) {
+__global__ void k_inbox_apply(const Dev* __restrict__ dp, uint32_t k);  // member.hip
+void launch_member(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool spec, bool split) {
   hipStream_t st = (hipStream_t)stream;
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[2], st);
-  hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k, spec ? 3u : 1u);  // + tick_flag
+  if (split) {  // a gossip plane ran last tick: members with many routed receipts run P4 a wave each (k_inbox_apply)
+    hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k, 4u);
+    hipLaunchKernelGGL(k_inbox_apply, dim3(2048), dim3(256), 0, st, d.self, k);
+    hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k, 9u);  // + tick_flag
+  } else {
+    hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k, spec ? 3u : 1u);  // + tick_flag
+  }
   if (d.dly_on) {
     hipLaunchKernelGGL(k_sync_redeliver, dim3(256), dim3(256), 0, st, d, k, spec ? 1u : 0u);
     hipLaunchKernelGGL(k_sync_defer, dim3(256), dim3(256), 0, st, d, k, spec ? 1u : 0u);

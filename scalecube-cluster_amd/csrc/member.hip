@@ -32,7 +32,10 @@ struct ML {
   unsigned long long c[8];
   uint32_t pend;  // this tick's SYNC messages that carry the live row: a chain through SyncMsg.pad (NEVER = none)
   uint32_t tround;
-  uint32_t* trk;  // subjects whose key changed in this tick's P1 (several payloads only); ntrk > TRK: overflowed
+  // subjects whose key changed in this tick's P1 (several payloads only): the first TRKL listed, all of them in the
+  // bitmap tb (one bit per subject); ntrk counts them
+  uint32_t* trk;
+  unsigned long long* tb;
   uint32_t ntrk;
   bool trk_on;
   // deferred copy-on-write (cow): open snapshots of this member (indices into the block's list cw) and its undo log
@@ -139,34 +142,36 @@ __device__ __forceinline__ void cow(ML& L) {
 __device__ __forceinline__ uint64_t row_ld(const ML& L, uint32_t s) { return rec_join(L.rk[s], L.ra[s]); }
 __device__ __forceinline__ uint32_t row_status(const ML& L, uint32_t s) { return L.rk[s] & 3u; }
 
-__device__ __forceinline__ void row_put(ML& L, uint32_t s, uint64_t v) {
+// old: the key the row holds for s now (callers that loaded it already pass it: no load after this lane's stores)
+__device__ __forceinline__ void row_put(ML& L, uint32_t s, uint64_t v, uint32_t old) {
   const uint32_t k = key32(v);
   if (rec_inc(v) >= INC_LIMIT) set_err(*L.d, E_INC);
-  if (L.pend != NEVER && L.rk[s] != k) cow(L);
-  if (L.ncreq && L.rk[s] != k) {  // an open snapshot: log the key this write replaces
+  if (L.pend != NEVER && old != k) cow(L);
+  if (L.ncreq && old != k) {  // an open snapshot: log the key this write replaces
     if (L.nlog == L.d->ulog_cap) {
       fb_add(*L.d, FB_ULOG);
       cow_now(L);
     } else {
       L.ulog[2 * L.nlog] = s;
-      L.ulog[2 * L.nlog + 1] = L.rk[s];
+      L.ulog[2 * L.nlog + 1] = old;
       L.nlog++;
     }
   }
-  const uint32_t tcap = L.d->trk_cap;
-  if (L.trk_on && L.rk[s] != k && L.ntrk <= tcap) {  // merge_payload re-checks it against the later payloads
-    bool seen = false;
-    for (uint32_t i = 0; i < L.ntrk; ++i) seen |= L.trk[i] == s;
-    if (!seen) {
-      if (L.ntrk < tcap) L.trk[L.ntrk] = s;
+  if (L.trk_on && old != k) {  // merge_payload re-checks it against the later payloads
+    unsigned long long* tw = L.tb + (s >> 6);
+    const unsigned long long bit = 1ull << (s & 63u), old = *tw;
+    if (!(old & bit)) {
+      *tw = old | bit;
+      if (L.ntrk < TRKL) L.trk[L.ntrk] = s;
       L.ntrk++;
     }
   }
-  if (L.d->ackres && L.rk[s] != k) tl_add(L, s);
+  if (L.d->ackres && old != k) tl_add(L, s);
   L.rk[s] = k;
   if (L.rd && k != L.d->base_row[s]) L.rd[(s / CH) >> 6] |= 1ull << ((s / CH) & 63);
   L.ra[s] = aux32(v);
 }
+__device__ __forceinline__ void row_put(ML& L, uint32_t s, uint64_t v) { row_put(L, s, v, L.rk[s]); }
 
 // prepareSyncDataMsg (MembershipProtocolImpl.java:446-454) + transport.send; false if the send failed
 // res: a SYNC_ACK sent in the tick its SYNC was merged (k_ack_resolve may derive its diff from the write logs)
@@ -554,11 +559,13 @@ __device__ __forceinline__ void do_finally(ML& L, uint32_t subj, uint32_t st, ui
 }
 
 // MetadataStoreImpl.fetchMetadata (:149-186); the response hop is evaluated in P3 at k + lat
-__device__ __forceinline__ void fetch_md(ML& L, uint32_t subj, uint32_t st, uint32_t inc, uint32_t reason, uint32_t added, int g) {
+// dd: whether subj is dead at this tick, when the caller loaded it already (-1: look it up)
+__device__ __forceinline__ void fetch_md(ML& L, uint32_t subj, uint32_t st, uint32_t inc, uint32_t reason, uint32_t added, int g,
+                                         int dd = -1) {
   const Dev& d = *L.d;
   uint32_t cnt = L.cidCnt++;
   L.c[C_M]++;
-  const int e = xmit_ep(d, L.ep, K_GMD_REQ, L.m, subj, L.k, L.m, cnt);
+  const int e = xmit_ep(d, L.ep, K_GMD_REQ, L.m, subj, L.k, L.m, cnt, dd);
   if (e < 0) {
     L.c[C_LOST]++;
     if (g >= 0) grp(L, g)[5] |= GF_ERROR;
@@ -630,6 +637,31 @@ __device__ __forceinline__ void update_membership(ML& L, uint32_t subj, uint32_t
   }
   finish(L, g, false);
   do_finally(L, subj, s1, i1, reason);
+}
+
+// updateMembership of a gossip record (P4, reason MEMBERSHIP_GOSSIP) in its common case, with the row entry and the
+// subject's liveness loaded by the caller: another member's present row, a record that is not DEAD. No row entry is
+// added or removed, so no event is emitted here and the table size stays (the UPDATED event waits for the metadata
+// fetch); nothing is re-spread for this reason (:526-539). Returns the row entry after the update (key | aux << 32).
+__device__ __forceinline__ uint64_t update_gossip_fast(ML& L, uint32_t subj, uint32_t s1, uint32_t i1, uint32_t k0,
+                                                       uint32_t a0, bool dead) {
+  const Dev& d = *L.d;
+  const uint32_t s0 = k0 & 3u, i0 = k0 >> 2;
+  if (!overrides(s1, i1, s0, i0)) return (uint64_t)k0 | ((uint64_t)a0 << 32);
+  uint64_t v = (rec_join(k0, a0) & ~KEY_MASK) | rec_key(s1, i1);
+  if (s1 == ST_SUSPECT) {  // scheduleSuspicionTimeoutTask (:597-606): computeIfAbsent
+    if (rec_timer(v) == 0) {
+      const uint32_t dl = L.k + suspicion_ticks(d, L.tsize, mc_ping_t(d, L.m));
+      v = rec_with_timer(v, dl);
+      if (dl < L.timerMin) L.timerMin = dl;
+    }
+  } else {
+    v = rec_with_timer(v, 0);  // cancelSuspicionTimeoutTask (:590-595)
+  }
+  row_put(L, subj, v, k0);
+  L.c[C_W]++;
+  if (i0 < i1) fetch_md(L, subj, s1, i1, R_GOSSIP, 0, -1, dead ? 1 : 0);  // UPDATED once the metadata arrives
+  return (uint64_t)key32(v) | ((uint64_t)aux32(v) << 32);
 }
 
 // onFailureDetectorEvent (:370-398)
@@ -882,8 +914,10 @@ __device__ __forceinline__ void merge_record(ML& L, uint32_t s, uint32_t k1, uin
 // the start of the tick, in subject order; that is exact for the first payload of the tick. A later payload can
 // also hold, for a subject an earlier payload changed, a record equal to the start row but not to the live one (a
 // leaver's own DEAD record removes it, then another member's ALIVE record of the old incarnation re-adds it,
-// MembershipRecord.java:67-69). Those subjects (L.trk) are read from the payload itself and merged into the
-// candidate walk in subject order; past TRK of them, the whole payload is compared against the live row.
+// MembershipRecord.java:67-69). Those subjects are read from the payload itself and merged into the candidate walk
+// in subject order: up to trk_cap of them from the sorted list L.trk, more from the bitmap L.tb, word by word with the
+// next word's load in flight (C2's receivers change hundreds of subjects in one P1: comparing every later payload with
+// the whole row on one lane held the member kernel).
 __device__ __forceinline__ void merge_payload(ML& L, uint32_t mi, uint32_t reason, int g) {
   const Dev& d = *L.d;
   const uint32_t b = (L.k - 1) & 1;
@@ -891,14 +925,14 @@ __device__ __forceinline__ void merge_payload(ML& L, uint32_t mi, uint32_t reaso
   L.c[C_R] += mm.psize;
   L.c[C_SYNCMERGE]++;
   const uint32_t nt = L.ntrk;
-  const bool full = nt > d.trk_cap;  // rare: many subjects changed earlier in this tick; exact full walk
-  if (full) fb_add(d, FB_TRK_WALK);
+  const bool bmap = nt > d.trk_cap;  // many subjects changed earlier in this tick: walk the bitmap
+  if (bmap) fb_add(d, FB_TRK_WALK);
   if (d.exp & 128) {  // timing experiments: full walks, largest candidate count
-    if (full) atomicAdd(&d.ctr[14], 1ull);
+    if (bmap) atomicAdd(&d.ctr[14], 1ull);
     atomicMax(&d.ctr[15], (unsigned long long)mm.ncand);
   }
-  if (!full && mm.ncand == 0 && nt == 0) return;  // steady state: nothing differs, skip the chunk walk
-  if (!full)
+  if (mm.ncand == 0 && nt == 0) return;  // steady state: nothing differs, skip the chunk walk
+  if (!bmap)
     for (uint32_t i = 1; i < nt; ++i)  // the tracked subjects in ascending order (insertion sort, at most TRK)
       for (uint32_t j = i; j > 0 && L.trk[j - 1] > L.trk[j]; --j) {
         const uint32_t t = L.trk[j];
@@ -906,44 +940,33 @@ __device__ __forceinline__ void merge_payload(ML& L, uint32_t mi, uint32_t reaso
         L.trk[j - 1] = t;
       }
   // One walk with a single merge site: update_membership is large, and each inlined copy of it costs instruction
-  // cache in every wave of this kernel. The next record comes from the full payload, or else from the candidate pool
-  // and the tracked subjects merged in subject order (a tracked candidate takes the pool's record).
-  uint32_t ti = 0, c = 0, e = 0, n = 0, off = 0, s = 0;
-  bool pool = !full && mm.ncand != 0;
-  // the full walk skips runs where the payload equals the live row, 4 subjects per 16-B compare, when the payload is
-  // an arena row (its snapshot or pinned copy); a lane walking N subjects one by one held C2's member kernel
-  const uint32_t* prow = nullptr;
-  if (full && !(mm.payload != NEVER && (mm.payload & PAY_RX))) {
-    const uint32_t r = mm.payload == NEVER ? mm.pin : mm.payload;
-    if (r != NEVER) prow = d.arena[b] + (size_t)r * d.NS;
+  // cache in every wave of this kernel. The next record comes from the candidate pool and the tracked subjects merged
+  // in subject order (a tracked candidate takes the pool's record).
+  uint32_t ti = 0, c = 0, e = 0, n = 0, off = 0;
+  bool pool = mm.ncand != 0;
+  // the bitmap cursor: word wi - 1 is being consumed (bits left: wcur), word wi is loading (wnxt)
+  uint32_t wi = 0;
+  unsigned long long wcur = 0, wnxt = 0;
+  if (bmap && d.NW) {
+    wcur = L.tb[0];
+    wnxt = d.NW > 1 ? L.tb[1] : 0ull;
+    wi = 1;
   }
+  auto tnext = [&]() -> uint32_t {  // the next tracked subject in ascending order (bitmap mode), NEVER at the end
+    while (wcur == 0ull) {
+      if (wi >= d.NW) return NEVER;
+      wcur = wnxt;
+      ++wi;
+      wnxt = wi < d.NW ? L.tb[wi] : 0ull;
+    }
+    const uint32_t v = (wi - 1u) * 64u + (uint32_t)(__ffsll((long long)wcur) - 1);
+    wcur &= wcur - 1ull;
+    return v;
+  };
+  uint32_t tsb = bmap ? tnext() : NEVER;
   for (;;) {
     uint32_t subj, k1;
-    if (full) {
-      if (prow) {
-        // 16 subjects per step with all eight loads in flight, then 4 at a time near the next difference
-        while (s + 16 <= L.N && (s & 3u) == 0u) {
-          uint32_t diff = 0;
-#pragma unroll
-          for (uint32_t q = 0; q < 4; ++q) {
-            const uint4 p4 = *(const uint4*)(prow + s + 4 * q), r4 = *(const uint4*)(L.rk + s + 4 * q);
-            diff |= (p4.x ^ r4.x) | (p4.y ^ r4.y) | (p4.z ^ r4.z) | (p4.w ^ r4.w);
-          }
-          if (diff) break;
-          s += 16;
-        }
-      }
-      if (prow)
-        while (s + 4 <= L.N && (s & 3u) == 0u) {
-          const uint4 p4 = *(const uint4*)(prow + s), r4 = *(const uint4*)(L.rk + s);
-          if (p4.x != r4.x || p4.y != r4.y || p4.z != r4.z || p4.w != r4.w) break;
-          s += 4;
-        }
-      if (s >= L.N) break;
-      subj = s;
-      k1 = payload_key_at(d, mm, b, s);
-      ++s;
-    } else {
+    {
       while (pool && e == n) {
         if (c == d.NCHUNK) {
           pool = false;
@@ -961,17 +984,19 @@ __device__ __forceinline__ void merge_payload(ML& L, uint32_t mi, uint32_t reaso
         prec = d.pool[(size_t)off + e];
         ps = (uint32_t)(prec >> 34);
       }
-      const uint32_t ts = ti < nt ? L.trk[ti] : NEVER;
+      const uint32_t ts = bmap ? tsb : ti < nt ? L.trk[ti] : NEVER;
       if (ps == NEVER && ts == NEVER) break;
       if (ts < ps) {
         subj = ts;
         k1 = payload_key_at(d, mm, b, ts);
-        ++ti;
+        if (bmap) tsb = tnext(); else ++ti;
       } else {
         subj = ps;
         k1 = key32(prec & KEY_MASK);
         ++e;
-        if (ts == ps) ++ti;
+        if (ts == ps) {
+          if (bmap) tsb = tnext(); else ++ti;
+        }
       }
     }
     merge_record(L, subj, k1, reason, g);
@@ -1045,10 +1070,8 @@ __device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t
   return true;
 }
 
-__device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint32_t k, unsigned long long (&cnt)[8],
-                                                 uint4* cw, uint32_t* cw_n, bool spec) {
-  const bool dead = dead_at(d, m, k);
-  ML L;
+// the member's state as member_tick_body holds it (one lane per member; k_inbox_apply: every lane of the member's wave)
+__device__ __forceinline__ void ml_init(ML& L, const Dev& d, uint32_t m, uint32_t k, uint4* cw, uint32_t* cw_n, bool spec) {
   L.d = &d;
   L.m = m;
   L.k = k;
@@ -1095,13 +1118,14 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   for (int i = 0; i < 8; ++i) L.c[i] = 0;
   L.pend = NEVER;
   L.tround = 0;
-  L.trk = d.trk + li * TRK;
+  L.trk = d.trk + li * TRKL;
+  L.tb = d.tbm + li * d.NW;
   L.ntrk = 0;
   L.trk_on = false;
   L.cw = cw;
   L.cw_n = cw_n;
   L.spec = spec;
-  L.ulog = d.ulog + li * ULOG * 2;
+  L.ulog = d.ulog + li * d.ULOGC * 2;
   L.ncreq = 0;
   L.nlog = 0;
   L.spq = d.spq + li * SPQ * 8;
@@ -1110,8 +1134,62 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   L.ntl = 0;
   L.tlast = NEVER;
   L.rgrp = -1;
+}
+
+// member_tick_body's state back (everything but next_evt and tround, which only a finished tick stores)
+__device__ __forceinline__ void ml_store(const ML& L) {
+  const Dev& d = *L.d;
+  const uint32_t m = L.m, k = L.k;
+  const size_t li = lidx(d, m);
+  d.tsize[m] = L.tsize;
+  d.fdLen[m] = L.fdLen;
+  d.gLen[m] = L.gLen;
+  d.fdPeriod[m] = L.fdPeriod;
+  d.gPeriod[m] = L.gPeriod;
+  d.gCounter[m] = L.gCounter;
+  d.nextPing[m] = L.nextPing;
+  d.nextGossip[m] = L.nextGossip;
+  d.nextSync[m] = L.nextSync;
+  d.cidCnt[m] = L.cidCnt;
+  d.syncSeq[m] = L.syncSeq;
+  d.evSeq[m] = L.evSeq;
+  d.held[m] = L.held;
+  d.timerMin[m] = L.timerMin;
+  d.initFlags[m] = L.initFlags;
+  d.initDeadline[m] = L.initDeadline;
+  d.initCidBase[m] = L.initCidBase;
+  d.initN[m] = L.initN;
+  d.nsub[m] = L.nsub;
+  d.npath[m] = L.npath;
+  d.nfetch[m] = L.nfetch;
+  d.fnext[m] = L.fnext;
+  d.pingIdx[m] = L.pingIdx;
+  d.remoteIdx[m] = L.remoteIdx;
+  for (int i = 0; i < 8; ++i) d.sel[(size_t)m * 8 + i] = L.sel[i];
+  d.evHash[m] = L.evHash;
+  if (L.ntl) {  // (no entry this tick: the stale tick stamp reads as an empty log)
+    d.tl_n[(size_t)(k & 1) * d.NL + li] = L.ntl;
+    d.tl_tick[(size_t)(k & 1) * d.NL + li] = k;
+  }
+}
+
+// mode: BODY_FULL = the whole tick; BODY_SPLIT = the whole tick, except that a member with at least Dev::hv routed
+// gossip receipts stops before P4 and is listed for k_inbox_apply (P4, a wave per member) and the resumed launch;
+// BODY_RESUME = P5 and P6 of a listed member (its P0-P4 ran in the two launches before)
+enum : uint32_t { BODY_FULL = 0, BODY_SPLIT = 1, BODY_RESUME = 2 };
+__device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint32_t k, unsigned long long (&cnt)[8],
+                                                 uint4* cw, uint32_t* cw_n, bool spec, uint32_t mode = BODY_FULL) {
+  const bool dead = dead_at(d, m, k);
+  ML L;
+  ml_init(L, d, m, k, cw, cw_n, spec);
+  const size_t li = lidx(d, m);
+  if (mode == BODY_RESUME) {  // what the parked member kept between the launches (k_inbox_apply updated it)
+    L.pend = d.hv_pend[li];
+    L.tlast = d.hv_tlast[li];
+    if (d.ackres && d.tl_tick[(size_t)(k & 1) * d.NL + li] == k) L.ntl = d.tl_n[(size_t)(k & 1) * d.NL + li];
+  }
   // P1's inbound list head, loaded with the state above (P0's sends link into the other buffer)
-  const uint32_t head0 = (!dead && k > 0) ? d.m_head[(size_t)((k - 1) & 1) * d.N + m] : NEVER;
+  const uint32_t head0 = (mode != BODY_RESUME && !dead && k > 0) ? d.m_head[(size_t)((k - 1) & 1) * d.N + m] : NEVER;
   // SWIM_EXP & 16 (timing experiment): shader cycles per phase summed over members, ctr[8..12]
   // SWIM_EXP & 128: the largest per-member cycles of each phase instead (which phase makes the longest lane)
   const bool prof = (d.exp & (16 | 128)) != 0;
@@ -1130,6 +1208,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
     tp = t;
   };
 
+  if (mode != BODY_RESUME) {  // P0 - P4
   // ---- P0 host requests: updateIncarnation (MembershipProtocolImpl.java:178-190), then leaveCluster (:197-206) ----
   const uint32_t preq = dead ? 0u : d.pending_inc[m];
   if (preq) {
@@ -1268,6 +1347,13 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
       }
     }
     L.trk_on = false;
+    if (L.ntrk) {  // the written-subject bitmap back to zero: the listed subjects' words, or the whole row
+      if (L.ntrk <= TRKL)
+        for (uint32_t q = 0; q < L.ntrk; ++q) L.tb[L.trk[q] >> 6] = 0ull;
+      else
+        for (uint32_t q = 0; q < d.NW; ++q) L.tb[q] = 0ull;
+      L.ntrk = 0;
+    }
     if (n > 1 || more)  // the pins of this tick's payloads go back to NEVER for the slots' next use (send_sync)
       for (uint32_t q = head; q != NEVER; q = mnext[q]) d.msgs[pb][q].pin = NEVER;
   }
@@ -1469,17 +1555,33 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   // as record compares by the triage
   {
     uint32_t off = d.rc_off[m], n = d.rc_cnt[m];
+    if (mode == BODY_SPLIT && n >= d.hv) {  // many receipts: P4 in k_inbox_apply, P5 and P6 in the resumed launch
+      d.hv_list[wave_append(d.nhv)] = m;
+      d.hv_pend[li] = L.pend;
+      d.hv_tlast[li] = L.tlast;
+      flush_spreads(L);
+      fd_ready(L);
+      if (L.ncreq)  // this launch's epilogue completes the open snapshots, undoing the writes logged so far
+        for (uint32_t q = 0, nq = min(*L.cw_n, d.cwmax_cap); q < nq; ++q)
+          if (L.cw[q].x == m) L.cw[q].w = L.nlog;
+      ml_store(L);
+      for (int i = 0; i < 8; ++i) cnt[i] += L.c[i];
+      return;
+    }
     if (n) {
       d.rc_cnt[m] = 0;  // the next receipt routing counts from zero
       d.rc_fill[m] = 0;
     }
-    // batches of PB receipts: their slot words and the rows they touch are loaded together (independent loads in
-    // flight at once), then the updates run in order; update_membership re-reads the row (cache-hot), so a batch
-    // that touches one subject twice still sees its own earlier write
+    // batches of PB receipts: everything the common update reads (slot words, the row entries, the subjects'
+    // liveness) is loaded first, with the loads of one batch in flight together; the updates then run in order with
+    // no load between them (on gfx950 a load issued after this lane's stores waits for them: one round trip per
+    // receipt otherwise). A later receipt of the same subject in the batch sees the earlier one's write through the
+    // registers; the rare cases (the own record, a DEAD record, an absent row, user gossips) take update_membership,
+    // which reads the row itself.
     constexpr uint32_t PB = 8;
     for (uint32_t q0 = 0; q0 < n; q0 += PB) {
       const uint32_t nb = min(PB, n - q0);
-      uint32_t gs[PB], subj[PB];
+      uint32_t gs[PB], subj[PB], rk0[PB], ra0[PB], dtk[PB];
       uint64_t key[PB];
 #pragma unroll
       for (uint32_t i = 0; i < PB; ++i) gs[i] = i < nb ? d.rc_slot[off + q0 + i] : 0u;
@@ -1488,24 +1590,40 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
         subj[i] = i < nb ? d.slot_subj[gs[i]] : USER_SUBJ;
         key[i] = i < nb ? d.slot_key[gs[i]] : 0ull;
       }
-      uint32_t warm = 0;
 #pragma unroll
-      for (uint32_t i = 0; i < PB; ++i)
-        if (subj[i] != USER_SUBJ) warm += L.rk[subj[i]] + L.ra[subj[i]];
-      asm volatile("" ::"v"(warm));  // keep the warming loads
+      for (uint32_t i = 0; i < PB; ++i) {
+        const bool ms = subj[i] != USER_SUBJ;
+        rk0[i] = ms ? L.rk[subj[i]] : 0u;
+        ra0[i] = ms ? L.ra[subj[i]] : 0u;
+        dtk[i] = ms ? d.dead_tick[subj[i]] : NEVER;
+      }
       for (uint32_t i = 0; i < nb; ++i) {
-        if (subj[i] == USER_SUBJ) {  // sink.next -> ClusterImpl.listenGossips (:213-216), not membership
+        const uint32_t s = subj[i];
+        if (s == USER_SUBJ) {  // sink.next -> ClusterImpl.listenGossips (:213-216), not membership
           const uint64_t gid = d.slot_gid[gs[i]];
           emit_event(L, 3, (uint32_t)(gid >> 32), (uint32_t)key[i], (uint32_t)(key[i] >> 32), (uint32_t)gid);
           continue;
         }
         L.c[C_R]++;
-        update_membership(L, subj[i], rec_status(key[i]), rec_inc(key[i]), R_GOSSIP, -1);
+        const uint32_t s1 = rec_status(key[i]);
+        uint64_t now;
+        if (s != m && (rk0[i] & 3u) != ST_ABSENT && s1 != ST_DEAD) {
+          now = update_gossip_fast(L, s, s1, rec_inc(key[i]), rk0[i], ra0[i], k >= dtk[i]);
+        } else {
+          update_membership(L, s, s1, rec_inc(key[i]), R_GOSSIP, -1);
+          now = (uint64_t)L.rk[s] | ((uint64_t)L.ra[s] << 32);
+        }
+        for (uint32_t j = i + 1; j < nb; ++j)
+          if (subj[j] == s) {
+            rk0[j] = (uint32_t)now;
+            ra0[j] = (uint32_t)(now >> 32);
+          }
       }
     }
   }
 
   lap(2);  // P4
+  }  // P0 - P4
   // ---- P5 timers ----
   if (L.nsub) {  // FD subscription timeouts in (cid, subscription) order
     uint32_t dcnt[SUBCAP], dkind[SUBCAP], dtgt[SUBCAP], nd = 0, w = 0;
@@ -1635,37 +1753,203 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   fd_ready(L);
   d.next_evt[m] = nev;
   d.tround[m] = L.tround;
-  d.tsize[m] = L.tsize;
-  d.fdLen[m] = L.fdLen;
-  d.gLen[m] = L.gLen;
-  d.fdPeriod[m] = L.fdPeriod;
-  d.gPeriod[m] = L.gPeriod;
-  d.gCounter[m] = L.gCounter;
-  d.nextPing[m] = L.nextPing;
-  d.nextGossip[m] = L.nextGossip;
-  d.nextSync[m] = L.nextSync;
-  d.cidCnt[m] = L.cidCnt;
-  d.syncSeq[m] = L.syncSeq;
-  d.evSeq[m] = L.evSeq;
-  d.held[m] = L.held;
-  d.timerMin[m] = L.timerMin;
-  d.initFlags[m] = L.initFlags;
-  d.initDeadline[m] = L.initDeadline;
-  d.initCidBase[m] = L.initCidBase;
-  d.initN[m] = L.initN;
-  d.nsub[m] = L.nsub;
-  d.npath[m] = L.npath;
-  d.nfetch[m] = L.nfetch;
-  d.fnext[m] = L.fnext;
-  d.pingIdx[m] = L.pingIdx;
-  d.remoteIdx[m] = L.remoteIdx;
-  for (int i = 0; i < 8; ++i) d.sel[(size_t)m * 8 + i] = L.sel[i];
-  d.evHash[m] = L.evHash;
-  if (L.ntl) {  // (no entry this tick: the stale tick stamp reads as an empty log)
-    d.tl_n[(size_t)(k & 1) * d.NL + li] = L.ntl;
-    d.tl_tick[(size_t)(k & 1) * d.NL + li] = k;
-  }
+  ml_store(L);
   for (int i = 0; i < 8; ++i) cnt[i] += L.c[i];
+}
+
+// ---- P4 of a parked member on one wave (k_inbox_apply) ----
+// A member with many routed gossip receipts (C2: a few hundred in a tick) ran them one after another on its lane,
+// each a chain of dependent loads, while 63 lanes of another member's wave waited. Here the member's receipts are taken
+// 64 at a time in gossip-id order. A receipt of the common case (another member's present row, a record that is not
+// DEAD) touches only its subject's row entry, the metadata-fetch list, the correlation counter and the write log, and
+// on a present row isOverrides (MembershipRecord.java:66-84) is the order of the packed keys: a receipt is accepted iff
+// its key is above the largest of the row's and every earlier same-subject key of the batch (a segmented prefix
+// maximum). Its correlation id, fetch-list place and write-log place are prefix sums in gossip-id order, so every
+// per-member sequence is the one the lane-serial P4 produces. Any other receipt (the member's own record, a DEAD
+// record, an absent row, a user gossip) runs the full update on lane 0 between batches.
+
+// one batch: lanes [0, cnt) hold common-case receipts (subject s, record s1 / i1, row entry k0 / a0 before the batch)
+__device__ __forceinline__ void inbox_batch(ML& L, uint32_t lane, uint32_t cnt, uint32_t s, uint32_t s1, uint32_t i1,
+                                            uint32_t k0, uint32_t a0, bool dead) {
+  const Dev& d = *L.d;
+  const bool act = lane < cnt;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  const uint32_t kk = (i1 << 2) | s1;
+  uint32_t pm = 0;  // the largest earlier key of this subject in the batch
+  for (uint32_t o = 0; o < cnt; ++o) {
+    const uint32_t so = __shfl(s, (int)o), ko = __shfl(kk, (int)o);
+    if (o < lane && so == s) pm = max(pm, ko);
+  }
+  const uint32_t run = max(k0, pm);  // the subject's key just before this receipt
+  const bool acc = act && kk > run;
+  const unsigned long long am = __ballot(acc);
+  // the accepted receipts before this one: of any subject (write log) and of this subject (suspicion timer)
+  uint32_t pacc = 0, prev = L.tlast;
+  bool alive_before = false, acc_before = false, acc_later = false;
+  for (uint32_t o = 0; o < cnt; ++o) {
+    if (!((am >> o) & 1ull)) continue;
+    const uint32_t so = __shfl(s, (int)o), sto = __shfl(s1, (int)o);
+    if (o < lane) {
+      acc_before = true;
+      prev = so;
+      if (so == s) {
+        pacc = sto;
+        alive_before |= sto == ST_ALIVE;
+      }
+    } else if (o > lane && so == s) {
+      acc_later = true;
+    }
+  }
+  // scheduleSuspicionTimeoutTask (:597-606, computeIfAbsent) / cancelSuspicionTimeoutTask (:590-595) along the chain:
+  // every deadline set in this tick is the same
+  const uint32_t dl = L.k + suspicion_ticks(d, L.tsize, mc_ping_t(d, L.m));
+  const uint64_t v0 = rec_join(k0, a0);
+  const uint32_t T0 = rec_timer(v0);
+  if (__ballot(acc && s1 == ST_SUSPECT && (pacc == ST_ALIVE || (pacc == 0 && T0 == 0)))) L.timerMin = min(L.timerMin, dl);
+  if (acc && !acc_later) {  // the subject's last accepted record is what the row holds after the batch
+    uint64_t v = (v0 & ~KEY_MASK) | rec_key(s1, i1);
+    v = rec_with_timer(v, s1 == ST_SUSPECT ? ((alive_before || T0 == 0) ? dl : T0) : 0u);
+    L.rk[s] = key32(v);
+    L.ra[s] = aux32(v);
+  }
+  if (act) L.c[C_R]++;
+  if (acc) L.c[C_W]++;
+  if (d.ackres) {  // tl_add of each accepted write, in order
+    const bool flag = acc && !((L.ntl > 0 || acc_before) && prev == s);
+    const unsigned long long fm = __ballot(flag);
+    const uint32_t p = L.ntl + (uint32_t)__popcll(fm & lt);
+    if (flag && p < TL) L.tl[p] = s;
+    L.ntl = min(TL + 1u, L.ntl + (uint32_t)__popcll(fm));
+    if (am) L.tlast = __shfl(s, 63 - (int)__clzll(am));
+  }
+  // fetchMetadata for an incarnation increase (:572-584): ids and fetch-list places in gossip-id order
+  const bool fet = acc && (run >> 2) < i1;
+  const unsigned long long fm = __ballot(fet);
+  int e = -1;
+  if (fet) {
+    L.c[C_M]++;
+    e = xmit_ep(d, L.ep, K_GMD_REQ, L.m, s, L.k, L.m, L.cidCnt + (uint32_t)__popcll(fm & lt), dead ? 1 : 0);
+    if (e < 0) L.c[C_LOST]++;
+  }
+  L.cidCnt += (uint32_t)__popcll(fm);
+  const bool kept = fet && e >= 0;
+  const unsigned long long km = __ballot(kept);
+  uint32_t fn = NEVER;
+  if (kept) {
+    const uint32_t q = L.nfetch + (uint32_t)__popcll(km & lt);
+    if (q >= d.FCAP) {
+      set_err(d, E_FETCH);
+    } else {
+      uint32_t* f = L.fetch + (size_t)q * FREC;
+      const uint32_t cid = L.cidCnt - (uint32_t)__popcll(fm) + (uint32_t)__popcll(fm & lt);
+      *(uint4*)f = make_uint4(cid, s, i1, s1 | (R_GOSSIP << 8) | (1u << 24));
+      *(uint4*)(f + 4) = make_uint4(0xFFFFFFFFu, L.k + d.md_t, L.k + d.lat + (uint32_t)e, NONE32);
+      fn = min(L.k + d.md_t, L.k + d.lat + (uint32_t)e);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) fn = min(fn, (uint32_t)__shfl_xor(fn, o));
+  L.nfetch = min(d.FCAP, L.nfetch + (uint32_t)__popcll(km));
+  L.fnext = min(L.fnext, fn);
+}
+
+// lane 0's member state to every lane of the wave (after a receipt lane 0 ran alone)
+__device__ __forceinline__ void ml_bcast(ML& L) {
+  L.tsize = __shfl(L.tsize, 0), L.fdLen = __shfl(L.fdLen, 0), L.gLen = __shfl(L.gLen, 0);
+  L.cidCnt = __shfl(L.cidCnt, 0), L.evSeq = __shfl(L.evSeq, 0), L.held = __shfl(L.held, 0);
+  L.gCounter = __shfl(L.gCounter, 0), L.timerMin = __shfl(L.timerMin, 0), L.nfetch = __shfl(L.nfetch, 0);
+  L.fnext = __shfl(L.fnext, 0), L.ntl = __shfl(L.ntl, 0), L.tlast = __shfl(L.tlast, 0), L.nsp = __shfl(L.nsp, 0);
+  L.npend = __shfl(L.npend, 0), L.pend = __shfl(L.pend, 0);
+  const uint32_t hl = __shfl((uint32_t)L.evHash, 0), hh = __shfl((uint32_t)(L.evHash >> 32), 0);
+  L.evHash = ((uint64_t)hh << 32) | hl;
+  for (int i = 0; i < 8; ++i) L.sel[i] = __shfl(L.sel[i], 0);
+}
+
+__device__ void inbox_member(const Dev& d, uint32_t m, uint32_t k, uint32_t lane) {
+  ML L;
+  ml_init(L, d, m, k, nullptr, nullptr, false);  // every lane holds the member's state
+  const size_t li = lidx(d, m);
+  L.pend = d.hv_pend[li];
+  L.tlast = d.hv_tlast[li];
+  if (d.ackres && d.tl_tick[(size_t)(k & 1) * d.NL + li] == k) L.ntl = d.tl_n[(size_t)(k & 1) * d.NL + li];
+  const uint32_t off = d.rc_off[m], n = d.rc_cnt[m];
+  if (L.pend != NEVER) {  // a SYNC / SYNC_ACK of this tick still carries the live row: its snapshot, copied by the wave
+    const uint32_t b = k & 1;
+    uint32_t r = 0;
+    if (lane == 0) r = atomicAdd(&d.arena_used[b], 1u);
+    r = __shfl(r, 0);
+    if (r >= d.ARENA_ROWS) {
+      if (lane == 0) set_err(d, E_ARENA);
+    } else {
+      const uint4* src4 = (const uint4*)L.rk;
+      uint4* dst4 = (uint4*)(d.arena[b] + (size_t)r * d.NS);
+      for (uint32_t q = lane; q < d.NS / 4; q += 64) dst4[q] = src4[q];
+      if (lane == 0)
+        for (uint32_t i = L.pend; i != NEVER; i = d.msgs[b][i].pad) d.msgs[b][i].payload = r;
+    }
+    L.pend = NEVER;
+    __threadfence_block();
+  }
+  for (uint32_t pos = 0; pos < n;) {
+    const uint32_t j = pos + lane;
+    const bool act = j < n;
+    const uint32_t g = act ? d.rc_slot[off + j] : 0u;
+    const uint32_t s = act ? d.slot_subj[g] : USER_SUBJ;
+    const uint64_t key = act ? d.slot_key[g] : 0ull;
+    const bool mem = act && s != USER_SUBJ;
+    const uint32_t k0 = mem ? L.rk[s] : 0u, a0 = mem ? L.ra[s] : 0u, dt = mem ? d.dead_tick[s] : NEVER;
+    const uint32_t s1 = rec_status(key), i1 = rec_inc(key);
+    const bool fast = mem && s != m && (k0 & 3u) != ST_ABSENT && s1 != ST_DEAD && i1 < INC_LIMIT;
+    const unsigned long long slow = __ballot(act && !fast);
+    const uint32_t f = slow ? (uint32_t)__ffsll((long long)slow) - 1u : 64u;
+    const uint32_t cnt = min(f, n - pos);
+    if (cnt) inbox_batch(L, lane, cnt, s, s1, i1, k0, a0, k >= dt);
+    __threadfence_block();  // the batch's row writes, before any lane reads the row again
+    if (f == 64u) {
+      pos += cnt;
+      continue;
+    }
+    const uint32_t gs = __shfl(g, (int)f), ss = __shfl(s, (int)f);
+    const uint32_t klo = __shfl((uint32_t)key, (int)f), khi = __shfl((uint32_t)(key >> 32), (int)f);
+    const uint64_t kf = ((uint64_t)khi << 32) | klo;
+    if (lane == 0) {
+      if (ss == USER_SUBJ) {  // sink.next -> ClusterImpl.listenGossips (:213-216)
+        const uint64_t gid = d.slot_gid[gs];
+        emit_event(L, 3, (uint32_t)(gid >> 32), (uint32_t)kf, (uint32_t)(kf >> 32), (uint32_t)gid);
+      } else {
+        L.c[C_R]++;
+        update_membership(L, ss, rec_status(kf), rec_inc(kf), R_GOSSIP, -1);
+      }
+    }
+    ml_bcast(L);
+    __threadfence_block();
+    pos += f + 1;
+  }
+  unsigned long long* cs = d.ctr_sh + (size_t)(blockIdx.x % CSH) * CSTRIDE;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    unsigned long long v = L.c[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint32_t lo = __shfl_xor((uint32_t)v, o), hi = __shfl_xor((uint32_t)(v >> 32), o);
+      v += ((unsigned long long)hi << 32) | lo;
+    }
+    if (lane == 0 && v) atomicAdd(&cs[i], v);
+  }
+  if (lane != 0) return;
+  flush_spreads(L);
+  fd_ready(L);
+  ml_store(L);
+  d.hv_pend[li] = L.pend;
+  d.hv_tlast[li] = L.tlast;
+  d.rc_cnt[m] = 0;  // the next receipt routing counts from zero
+  d.rc_fill[m] = 0;
+}
+
+__global__ void __launch_bounds__(256) k_inbox_apply(const Dev* __restrict__ dp, uint32_t k) {
+  const Dev& d = *dp;
+  const uint32_t nh = *d.nhv, lane = threadIdx.x & 63u;
+  for (uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6); i < nh; i += gridDim.x * 4) inbox_member(d, d.hv_list[i], k, lane);
 }
 
 // One launch per tick for member control. Each block triages its 256 members (the idle fast path, one thread per
@@ -1695,9 +1979,10 @@ __global__ void __launch_bounds__(256, 2) k_member_tick(const Dev* __restrict__ 
   __shared__ uint32_t cw_n;
   if (threadIdx.x == 0) cw_n = 0;
   if (threadIdx.x < CWMAX) cw[threadIdx.x].x = NEVER;  // no member until written (cow scans by member)
+  const bool resume = (flag & 8u) != 0;  // the parked members' P5 and P6 (one lane each, from the list)
   const uint32_t m = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t cls = 0, drops = 0, evs = 0;
-  const bool busy = m < d.hi && member_triage(d, m, k, cls, drops, evs);
+  const bool busy = !resume && m < d.hi && member_triage(d, m, k, cls, drops, evs);
   {  // the triage's record compares and folded RUMOR events, one atomic each per wave
     uint32_t v = drops, e = evs;
 #pragma unroll
@@ -1729,7 +2014,12 @@ __global__ void __launch_bounds__(256, 2) k_member_tick(const Dev* __restrict__ 
   uint32_t slot = start + before + __popcll(bal & ((1ull << lane) - 1ull));
   if (busy) list[slot] = m | (cls << 30);  // m < 2^30
   __syncthreads();
-  const uint32_t ent = list[threadIdx.x], me = ent == NEVER ? NEVER : (ent & 0x3FFFFFFFu), mcls = ent >> 30;
+  uint32_t ent = list[threadIdx.x];
+  if (resume) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    ent = i < *d.nhv ? d.hv_list[i] : NEVER;  // class 0
+  }
+  const uint32_t me = ent == NEVER ? NEVER : (ent & 0x3FFFFFFFu), mcls = ent >> 30;
   if (wtime) {  // [1]: after triage, with the wave's class mix in the top byte
     const uint64_t cm = (__ballot(me != NEVER && mcls == 0) ? 1ull : 0ull) | (__ballot(me != NEVER && mcls == 1) ? 2ull : 0ull) |
                         (__ballot(me != NEVER && mcls == 2) ? 4ull : 0ull) | (__ballot(me != NEVER && mcls == 3) ? 8ull : 0ull);
@@ -1740,7 +2030,9 @@ __global__ void __launch_bounds__(256, 2) k_member_tick(const Dev* __restrict__ 
   if (__ballot(me != NEVER)) {  // waves with no busy member skip to the end
     unsigned long long cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const bool skip = ((d.exp & 32) && mcls == 0) || ((d.exp & 64) && mcls != 0);
-    if (me != NEVER && !skip) member_tick_body(d, me, k, cnt, cw, &cw_n, (flag & 3u) == 3u);
+    if (me != NEVER && !skip)
+      member_tick_body(d, me, k, cnt, cw, &cw_n, (flag & 3u) == 3u,
+                       resume ? BODY_RESUME : (flag & 4u) ? BODY_SPLIT : BODY_FULL);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       unsigned long long v = cnt[i];
@@ -1771,7 +2063,7 @@ __global__ void __launch_bounds__(256, 2) k_member_tick(const Dev* __restrict__ 
     __syncthreads();
     if (threadIdx.x == 0) {
       uint32_t* dst = d.arena[b] + (size_t)e.y * d.NS;
-      const uint32_t* lg = d.ulog + li * ULOG * 2;
+      const uint32_t* lg = d.ulog + li * d.ULOGC * 2;
       for (uint32_t j = e.w; j-- > e.z;) dst[lg[2 * j]] = lg[2 * j + 1];
     }
     __syncthreads();
@@ -1780,6 +2072,7 @@ __global__ void __launch_bounds__(256, 2) k_member_tick(const Dev* __restrict__ 
   if ((flag & 3u) != 1u) return;
   if (!last_block_ticket(d.mdone, gridDim.x) || threadIdx.x != 0) return;
   *d.mdone = 0;
+  if (resume) *d.nhv = 0;  // every block has read the list
   tick_flag(d, k);
 }
 

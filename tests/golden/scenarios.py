@@ -72,7 +72,7 @@ def _c2_full():  # C2 at its configured size (BASELINE configs[1]: 10 000 member
     # 2.2e4 gossips created and 3.7e8 gossip messages; period 4 creates ~3.5x the gossips and does not fit). Periods 1-3
     # already run the SYNC re-spreads (SYNCs are staggered over the first 300 ticks) and the suspicion refutations.
     # Recorded once (SWIMREF_THREADS=8 python tests/golden/make_golden.py c2_full, ~3 min); replayed on 1 and 2 shards
-    return SimConfig(n_members=10_000, record_events=True), [("loss", 5), ("periods", 3)]
+    return SimConfig(n_members=10_000, record_events=True, event_cap=1 << 22), [("loss", 5), ("periods", 3)]
 
 
 def _c3_small():  # C3-shaped: steady state SYNC / SYNC_ACK anti-entropy, no loss

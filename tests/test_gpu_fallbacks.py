@@ -17,7 +17,7 @@ from test_gpu_fuzz import play, schedule
 
 pytestmark = pytest.mark.gpu
 
-TINY = "trk=1,ulog=1,creq=1,cwmax=1,cev=1,mq=1,sort=2,rx=1"
+TINY = "trk=1,ulog=1,creq=1,cwmax=1,cev=1,mq=1,sort=2,rx=1,hv=1"  # hv=1: every P4 with a receipt on a wave (k_inbox_apply)
 
 
 def _engine(engine, cfg, monkeypatch, caps=TINY, shards=1):
