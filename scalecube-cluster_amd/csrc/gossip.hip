@@ -662,7 +662,10 @@ __global__ void __launch_bounds__(256) k_gossip_contacts(Dev d, uint32_t k) {
 }
 
 // the flagged pairs' contact caches, one wave each: its lanes scan the two round logs 64 entries at a time
-__global__ void __launch_bounds__(256) k_contact_cache(Dev d, uint32_t k) {
+// (Dev through a pointer: the contacts' loss percents index its epoch table by a per-lane epoch, which a by-value Dev
+// would copy to scratch, 2.3 KB per lane)
+__global__ void __launch_bounds__(256) k_contact_cache(const Dev* __restrict__ dp, uint32_t k) {
+  const Dev& d = *dp;
   __shared__ Contact sev[4][CEV];
   const uint32_t n = *d.ncfl, lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   for (uint32_t j = blockIdx.x * 4 + wave; j < n; j += gridDim.x * 4) {
@@ -1162,7 +1165,7 @@ void launch_gossip_send(const Dev& d, uint32_t k, hipStream_t st, const TickEven
   hipLaunchKernelGGL(k_round_apply_w, dim3(4096), dim3(256), 0, st, d.self, k);
   hipLaunchKernelGGL(k_round_apply_b, dim3(2048), dim3(256), 0, st, d.self, k);
   hipLaunchKernelGGL(k_gossip_contacts, dim3(2048), dim3(256), 0, st, d, k);
-  hipLaunchKernelGGL(k_contact_cache, dim3(1024), dim3(256), 0, st, d, k);
+  hipLaunchKernelGGL(k_contact_cache, dim3(1024), dim3(256), 0, st, d.self, k);
   hipLaunchKernelGGL(k_rx_build, dim3(512), dim3(256), 0, st, d.self);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[4], st);
   hipLaunchKernelGGL(k_gossip_send, dim3(SEND_GRID), dim3(256), 0, st, d.self, k);

@@ -7,7 +7,9 @@
 
 namespace swim {
 
-__global__ void k_member_tick(const Dev* __restrict__ dp, uint32_t k, uint32_t flag);  // member.hip
+enum : uint32_t { BODY_FULL = 0, BODY_SPLIT = 1, BODY_RESUME = 2 };  // member.hip
+template <uint32_t MODE>
+__global__ void k_member_tick_t(const Dev* __restrict__ dp, uint32_t k, uint32_t flag);  // member.hip
 // shard.hip
 __global__ void k_sync_route(Dev d, uint32_t b, uint32_t spec);
 __global__ void k_pack_a(Dev d, uint32_t b, uint32_t spec);
@@ -928,11 +930,11 @@ void launch_member(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   hipStream_t st = (hipStream_t)stream;
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[2], st);
   if (split) {  // a gossip plane ran last tick: members with many routed receipts run P4 a wave each (k_inbox_apply)
-    hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k, 4u);
+    hipLaunchKernelGGL(k_member_tick_t<BODY_SPLIT>, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k, 0u);
     hipLaunchKernelGGL(k_inbox_apply, dim3(2048), dim3(256), 0, st, d.self, k);
-    hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k, 9u);  // + tick_flag
+    hipLaunchKernelGGL(k_member_tick_t<BODY_RESUME>, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k, 1u);  // + tick_flag
   } else {
-    hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k, spec ? 3u : 1u);  // + tick_flag
+    hipLaunchKernelGGL(k_member_tick_t<BODY_FULL>, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k, spec ? 3u : 1u);  // + tick_flag
   }
   if (d.dly_on) {
     hipLaunchKernelGGL(k_sync_redeliver, dim3(256), dim3(256), 0, st, d, k, spec ? 1u : 0u);
@@ -980,7 +982,7 @@ void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   launch_ack_resolve(d, k, st, spec, prof != nullptr);
   if (k > 0) launch_sync_diff(d, (k - 1) & 1, st, prof ? 1u : 0u, sp, prof);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[2], st);
-  hipLaunchKernelGGL(k_member_tick, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k, spec ? 2u : 0u);
+  hipLaunchKernelGGL(k_member_tick_t<BODY_FULL>, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k, spec ? 2u : 0u);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[3], st);
   hipLaunchKernelGGL(k_sync_route, dim3(cdiv(d.MSGCAP, 256)), dim3(256), 0, st, d, b, sp);
   if (d.dly_on) hipLaunchKernelGGL(k_sync_redeliver_x, dim3(256), dim3(256), 0, st, d, k, sp);

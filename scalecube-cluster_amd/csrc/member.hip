@@ -24,18 +24,16 @@ struct ML {
   int ep;          // NetworkEmulator settings epoch of tick k (epoch_at, looked up once)
   uint32_t fnext;  // earliest tick at which a pending fetch needs the member (hop, arrival or timeout); NEVER: none
   int32_t pingIdx, remoteIdx;
-  uint32_t sel[8];
   uint64_t evHash;
   uint32_t *rk, *ra;  // this observer's row: key plane and aux plane (swim_common.h)
   uint64_t* rd;       // W > 1: its dirty-chunk mask against base_row (Dev::rdirty), else null
   uint32_t *fdl, *gl, *subs, *paths, *fetch, *groups;
-  unsigned long long c[8];
+  uint32_t c[8];  // this tick's op counters (one member, one tick: u32; summed per wave in u64)
   uint32_t pend;  // this tick's SYNC messages that carry the live row: a chain through SyncMsg.pad (NEVER = none)
   uint32_t tround;
   // subjects whose key changed in this tick's P1 (several payloads only): the first TRKL listed, all of them in the
   // bitmap tb (one bit per subject); ntrk counts them
   uint32_t* trk;
-  unsigned long long* tb;
   uint32_t ntrk;
   bool trk_on;
   // deferred copy-on-write (cow): open snapshots of this member (indices into the block's list cw) and its undo log
@@ -65,15 +63,25 @@ __device__ __forceinline__ void tl_add(ML& L, uint32_t s) {
   L.tlast = s;
 }
 
-__device__ __forceinline__ uint32_t draw(ML& L, uint32_t stream) {
-  uint32_t c = L.sel[stream]++;
+// the selector counters live in memory (Dev::sel), not in the member's registers: draws are rare next to the
+// registers every member-kernel wave would hold for them
+__device__ __forceinline__ uint32_t draw_at(const ML& L, uint32_t stream, uint32_t c) {
   return philox(L.m, stream, c, 0, L.d->seed_lo ^ SALT_SEL, L.d->seed_hi).x;
+}
+__device__ __forceinline__ uint32_t draw(ML& L, uint32_t stream) {
+  uint32_t* p = L.d->sel + (size_t)L.m * 8 + stream;
+  const uint32_t c = *p;
+  *p = c + 1u;
+  return draw_at(L, stream, c);
 }
 
 // Collections.shuffle: for i = size..2: swap(i-1, nextInt(i))
 __device__ __forceinline__ void shuffle_list(ML& L, uint32_t* v, uint32_t n, uint32_t stream) {
+  uint32_t* p = L.d->sel + (size_t)L.m * 8 + stream;
+  uint32_t c = *p;
+  if (n > 1) *p = c + (n - 1u);
   for (uint32_t i = n; i > 1; --i) {
-    uint32_t j = next_int(draw(L, stream), i);
+    uint32_t j = next_int(draw_at(L, stream, c++), i);
     uint32_t t = v[i - 1];
     v[i - 1] = v[j];
     v[j] = t;
@@ -158,7 +166,7 @@ __device__ __forceinline__ void row_put(ML& L, uint32_t s, uint64_t v, uint32_t 
     }
   }
   if (L.trk_on && old != k) {  // merge_payload re-checks it against the later payloads
-    unsigned long long* tw = L.tb + (s >> 6);
+    unsigned long long* tw = L.d->tbm + lidx(*L.d, L.m) * L.d->NW + (s >> 6);
     const unsigned long long bit = 1ull << (s & 63u), old = *tw;
     if (!(old & bit)) {
       *tw = old | bit;
@@ -639,31 +647,6 @@ __device__ __forceinline__ void update_membership(ML& L, uint32_t subj, uint32_t
   do_finally(L, subj, s1, i1, reason);
 }
 
-// updateMembership of a gossip record (P4, reason MEMBERSHIP_GOSSIP) in its common case, with the row entry and the
-// subject's liveness loaded by the caller: another member's present row, a record that is not DEAD. No row entry is
-// added or removed, so no event is emitted here and the table size stays (the UPDATED event waits for the metadata
-// fetch); nothing is re-spread for this reason (:526-539). Returns the row entry after the update (key | aux << 32).
-__device__ __forceinline__ uint64_t update_gossip_fast(ML& L, uint32_t subj, uint32_t s1, uint32_t i1, uint32_t k0,
-                                                       uint32_t a0, bool dead) {
-  const Dev& d = *L.d;
-  const uint32_t s0 = k0 & 3u, i0 = k0 >> 2;
-  if (!overrides(s1, i1, s0, i0)) return (uint64_t)k0 | ((uint64_t)a0 << 32);
-  uint64_t v = (rec_join(k0, a0) & ~KEY_MASK) | rec_key(s1, i1);
-  if (s1 == ST_SUSPECT) {  // scheduleSuspicionTimeoutTask (:597-606): computeIfAbsent
-    if (rec_timer(v) == 0) {
-      const uint32_t dl = L.k + suspicion_ticks(d, L.tsize, mc_ping_t(d, L.m));
-      v = rec_with_timer(v, dl);
-      if (dl < L.timerMin) L.timerMin = dl;
-    }
-  } else {
-    v = rec_with_timer(v, 0);  // cancelSuspicionTimeoutTask (:590-595)
-  }
-  row_put(L, subj, v, k0);
-  L.c[C_W]++;
-  if (i0 < i1) fetch_md(L, subj, s1, i1, R_GOSSIP, 0, -1, dead ? 1 : 0);  // UPDATED once the metadata arrives
-  return (uint64_t)key32(v) | ((uint64_t)aux32(v) << 32);
-}
-
 // onFailureDetectorEvent (:370-398)
 __device__ __forceinline__ void on_fd_event(ML& L, uint32_t target, uint32_t status) {
   uint64_t v0 = row_ld(L, target);
@@ -915,7 +898,7 @@ __device__ __forceinline__ void merge_record(ML& L, uint32_t s, uint32_t k1, uin
 // also hold, for a subject an earlier payload changed, a record equal to the start row but not to the live one (a
 // leaver's own DEAD record removes it, then another member's ALIVE record of the old incarnation re-adds it,
 // MembershipRecord.java:67-69). Those subjects are read from the payload itself and merged into the candidate walk
-// in subject order: up to trk_cap of them from the sorted list L.trk, more from the bitmap L.tb, word by word with the
+// in subject order: up to trk_cap of them from the sorted list L.trk, more from the bitmap Dev::tbm, word by word with the
 // next word's load in flight (C2's receivers change hundreds of subjects in one P1: comparing every later payload with
 // the whole row on one lane held the member kernel).
 __device__ __forceinline__ void merge_payload(ML& L, uint32_t mi, uint32_t reason, int g) {
@@ -947,9 +930,10 @@ __device__ __forceinline__ void merge_payload(ML& L, uint32_t mi, uint32_t reaso
   // the bitmap cursor: word wi - 1 is being consumed (bits left: wcur), word wi is loading (wnxt)
   uint32_t wi = 0;
   unsigned long long wcur = 0, wnxt = 0;
+  const unsigned long long* tb = d.tbm + lidx(d, L.m) * d.NW;
   if (bmap && d.NW) {
-    wcur = L.tb[0];
-    wnxt = d.NW > 1 ? L.tb[1] : 0ull;
+    wcur = tb[0];
+    wnxt = d.NW > 1 ? tb[1] : 0ull;
     wi = 1;
   }
   auto tnext = [&]() -> uint32_t {  // the next tracked subject in ascending order (bitmap mode), NEVER at the end
@@ -957,7 +941,7 @@ __device__ __forceinline__ void merge_payload(ML& L, uint32_t mi, uint32_t reaso
       if (wi >= d.NW) return NEVER;
       wcur = wnxt;
       ++wi;
-      wnxt = wi < d.NW ? L.tb[wi] : 0ull;
+      wnxt = wi < d.NW ? tb[wi] : 0ull;
     }
     const uint32_t v = (wi - 1u) * 64u + (uint32_t)(__ffsll((long long)wcur) - 1);
     wcur &= wcur - 1ull;
@@ -1101,7 +1085,6 @@ __device__ __forceinline__ void ml_init(ML& L, const Dev& d, uint32_t m, uint32_
   L.ep = epoch_at(d, k);
   L.pingIdx = d.pingIdx[m];
   L.remoteIdx = d.remoteIdx[m];
-  for (int i = 0; i < 8; ++i) L.sel[i] = d.sel[(size_t)m * 8 + i];
   L.evHash = d.evHash[m];
   const size_t li = lidx(d, m);  // per-observer arrays hold only this shard's rows
   L.rk = d.rowk + li * d.NS;
@@ -1119,7 +1102,6 @@ __device__ __forceinline__ void ml_init(ML& L, const Dev& d, uint32_t m, uint32_
   L.pend = NEVER;
   L.tround = 0;
   L.trk = d.trk + li * TRKL;
-  L.tb = d.tbm + li * d.NW;
   L.ntrk = 0;
   L.trk_on = false;
   L.cw = cw;
@@ -1165,7 +1147,6 @@ __device__ __forceinline__ void ml_store(const ML& L) {
   d.fnext[m] = L.fnext;
   d.pingIdx[m] = L.pingIdx;
   d.remoteIdx[m] = L.remoteIdx;
-  for (int i = 0; i < 8; ++i) d.sel[(size_t)m * 8 + i] = L.sel[i];
   d.evHash[m] = L.evHash;
   if (L.ntl) {  // (no entry this tick: the stale tick stamp reads as an empty log)
     d.tl_n[(size_t)(k & 1) * d.NL + li] = L.ntl;
@@ -1177,8 +1158,9 @@ __device__ __forceinline__ void ml_store(const ML& L) {
 // gossip receipts stops before P4 and is listed for k_inbox_apply (P4, a wave per member) and the resumed launch;
 // BODY_RESUME = P5 and P6 of a listed member (its P0-P4 ran in the two launches before)
 enum : uint32_t { BODY_FULL = 0, BODY_SPLIT = 1, BODY_RESUME = 2 };
+template <uint32_t mode>
 __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint32_t k, unsigned long long (&cnt)[8],
-                                                 uint4* cw, uint32_t* cw_n, bool spec, uint32_t mode = BODY_FULL) {
+                                                 uint4* cw, uint32_t* cw_n, bool spec) {
   const bool dead = dead_at(d, m, k);
   ML L;
   ml_init(L, d, m, k, cw, cw_n, spec);
@@ -1348,10 +1330,11 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
     }
     L.trk_on = false;
     if (L.ntrk) {  // the written-subject bitmap back to zero: the listed subjects' words, or the whole row
+      unsigned long long* tb = d.tbm + li * d.NW;
       if (L.ntrk <= TRKL)
-        for (uint32_t q = 0; q < L.ntrk; ++q) L.tb[L.trk[q] >> 6] = 0ull;
+        for (uint32_t q = 0; q < L.ntrk; ++q) tb[L.trk[q] >> 6] = 0ull;
       else
-        for (uint32_t q = 0; q < d.NW; ++q) L.tb[q] = 0ull;
+        for (uint32_t q = 0; q < d.NW; ++q) tb[q] = 0ull;
       L.ntrk = 0;
     }
     if (n > 1 || more)  // the pins of this tick's payloads go back to NEVER for the slots' next use (send_sync)
@@ -1572,16 +1555,14 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
       d.rc_cnt[m] = 0;  // the next receipt routing counts from zero
       d.rc_fill[m] = 0;
     }
-    // batches of PB receipts: everything the common update reads (slot words, the row entries, the subjects'
-    // liveness) is loaded first, with the loads of one batch in flight together; the updates then run in order with
-    // no load between them (on gfx950 a load issued after this lane's stores waits for them: one round trip per
-    // receipt otherwise). A later receipt of the same subject in the batch sees the earlier one's write through the
-    // registers; the rare cases (the own record, a DEAD record, an absent row, user gossips) take update_membership,
-    // which reads the row itself.
+    // batches of PB receipts: their slot words and the rows they touch are loaded together (independent loads in
+    // flight at once), then the updates run in order; update_membership re-reads the row (cache-hot), so a batch
+    // that touches one subject twice still sees its own earlier write. (A member with many receipts in a tick after a
+    // gossip plane runs them on a wave of its own instead: k_inbox_apply.)
     constexpr uint32_t PB = 8;
     for (uint32_t q0 = 0; q0 < n; q0 += PB) {
       const uint32_t nb = min(PB, n - q0);
-      uint32_t gs[PB], subj[PB], rk0[PB], ra0[PB], dtk[PB];
+      uint32_t gs[PB], subj[PB];
       uint64_t key[PB];
 #pragma unroll
       for (uint32_t i = 0; i < PB; ++i) gs[i] = i < nb ? d.rc_slot[off + q0 + i] : 0u;
@@ -1590,34 +1571,19 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
         subj[i] = i < nb ? d.slot_subj[gs[i]] : USER_SUBJ;
         key[i] = i < nb ? d.slot_key[gs[i]] : 0ull;
       }
+      uint32_t warm = 0;
 #pragma unroll
-      for (uint32_t i = 0; i < PB; ++i) {
-        const bool ms = subj[i] != USER_SUBJ;
-        rk0[i] = ms ? L.rk[subj[i]] : 0u;
-        ra0[i] = ms ? L.ra[subj[i]] : 0u;
-        dtk[i] = ms ? d.dead_tick[subj[i]] : NEVER;
-      }
+      for (uint32_t i = 0; i < PB; ++i)
+        if (subj[i] != USER_SUBJ) warm += L.rk[subj[i]] + L.ra[subj[i]];
+      asm volatile("" ::"v"(warm));  // keep the warming loads
       for (uint32_t i = 0; i < nb; ++i) {
-        const uint32_t s = subj[i];
-        if (s == USER_SUBJ) {  // sink.next -> ClusterImpl.listenGossips (:213-216), not membership
+        if (subj[i] == USER_SUBJ) {  // sink.next -> ClusterImpl.listenGossips (:213-216), not membership
           const uint64_t gid = d.slot_gid[gs[i]];
           emit_event(L, 3, (uint32_t)(gid >> 32), (uint32_t)key[i], (uint32_t)(key[i] >> 32), (uint32_t)gid);
           continue;
         }
         L.c[C_R]++;
-        const uint32_t s1 = rec_status(key[i]);
-        uint64_t now;
-        if (s != m && (rk0[i] & 3u) != ST_ABSENT && s1 != ST_DEAD) {
-          now = update_gossip_fast(L, s, s1, rec_inc(key[i]), rk0[i], ra0[i], k >= dtk[i]);
-        } else {
-          update_membership(L, s, s1, rec_inc(key[i]), R_GOSSIP, -1);
-          now = (uint64_t)L.rk[s] | ((uint64_t)L.ra[s] << 32);
-        }
-        for (uint32_t j = i + 1; j < nb; ++j)
-          if (subj[j] == s) {
-            rk0[j] = (uint32_t)now;
-            ra0[j] = (uint32_t)(now >> 32);
-          }
+        update_membership(L, subj[i], rec_status(key[i]), rec_inc(key[i]), R_GOSSIP, -1);
       }
     }
   }
@@ -1862,7 +1828,6 @@ __device__ __forceinline__ void ml_bcast(ML& L) {
   L.npend = __shfl(L.npend, 0), L.pend = __shfl(L.pend, 0);
   const uint32_t hl = __shfl((uint32_t)L.evHash, 0), hh = __shfl((uint32_t)(L.evHash >> 32), 0);
   L.evHash = ((uint64_t)hh << 32) | hl;
-  for (int i = 0; i < 8; ++i) L.sel[i] = __shfl(L.sel[i], 0);
 }
 
 __device__ void inbox_member(const Dev& d, uint32_t m, uint32_t k, uint32_t lane) {
@@ -1925,6 +1890,10 @@ __device__ void inbox_member(const Dev& d, uint32_t m, uint32_t k, uint32_t lane
     __threadfence_block();
     pos += f + 1;
   }
+  if (lane == 0) {  // the gossips lane 0 created (refutations) take their slots; the FD list inserts land
+    flush_spreads(L);
+    fd_ready(L);
+  }
   unsigned long long* cs = d.ctr_sh + (size_t)(blockIdx.x % CSH) * CSTRIDE;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -1937,8 +1906,6 @@ __device__ void inbox_member(const Dev& d, uint32_t m, uint32_t k, uint32_t lane
     if (lane == 0 && v) atomicAdd(&cs[i], v);
   }
   if (lane != 0) return;
-  flush_spreads(L);
-  fd_ready(L);
   ml_store(L);
   d.hv_pend[li] = L.pend;
   d.hv_tlast[li] = L.tlast;
@@ -1960,7 +1927,10 @@ __global__ void __launch_bounds__(256) k_inbox_apply(const Dev* __restrict__ dp,
 // pingers per tick adding to one word would serialise on that address. With `flag` (W == 1) the block that finishes
 // last runs the end-of-tick resets and raises the host flag. flag: 1 = W == 1 (end-of-tick work), 2 = a launch of a
 // speculative batch.
-__global__ void __launch_bounds__(256, 2) k_member_tick(const Dev* __restrict__ dp, uint32_t k, uint32_t flag) {
+// (MODE: BODY_FULL, or the two launches around k_inbox_apply, BODY_SPLIT and BODY_RESUME: three kernels, each with its
+// own register allocation, so the steady-state one keeps the code it had before the split)
+template <uint32_t MODE>
+__global__ void __launch_bounds__(256, 2) k_member_tick_t(const Dev* __restrict__ dp, uint32_t k, uint32_t flag) {
   const Dev& d = *dp;  // global, not kernarg: taking its address must not copy ~1 KB into per-lane scratch
   if (flag & 2u) {  // a speculative batch halted at an earlier tick (this tick's own halt is raised while it runs)
     const uint32_t hv = *(volatile uint32_t*)d.halt;
@@ -1979,7 +1949,7 @@ __global__ void __launch_bounds__(256, 2) k_member_tick(const Dev* __restrict__ 
   __shared__ uint32_t cw_n;
   if (threadIdx.x == 0) cw_n = 0;
   if (threadIdx.x < CWMAX) cw[threadIdx.x].x = NEVER;  // no member until written (cow scans by member)
-  const bool resume = (flag & 8u) != 0;  // the parked members' P5 and P6 (one lane each, from the list)
+  constexpr bool resume = MODE == BODY_RESUME;  // the parked members' P5 and P6 (one lane each, from the list)
   const uint32_t m = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t cls = 0, drops = 0, evs = 0;
   const bool busy = !resume && m < d.hi && member_triage(d, m, k, cls, drops, evs);
@@ -2031,8 +2001,7 @@ __global__ void __launch_bounds__(256, 2) k_member_tick(const Dev* __restrict__ 
     unsigned long long cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const bool skip = ((d.exp & 32) && mcls == 0) || ((d.exp & 64) && mcls != 0);
     if (me != NEVER && !skip)
-      member_tick_body(d, me, k, cnt, cw, &cw_n, (flag & 3u) == 3u,
-                       resume ? BODY_RESUME : (flag & 4u) ? BODY_SPLIT : BODY_FULL);
+      member_tick_body<MODE>(d, me, k, cnt, cw, &cw_n, (flag & 3u) == 3u);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       unsigned long long v = cnt[i];
@@ -2075,5 +2044,9 @@ __global__ void __launch_bounds__(256, 2) k_member_tick(const Dev* __restrict__ 
   if (resume) *d.nhv = 0;  // every block has read the list
   tick_flag(d, k);
 }
+
+template __global__ void k_member_tick_t<BODY_FULL>(const Dev* __restrict__, uint32_t, uint32_t);
+template __global__ void k_member_tick_t<BODY_SPLIT>(const Dev* __restrict__, uint32_t, uint32_t);
+template __global__ void k_member_tick_t<BODY_RESUME>(const Dev* __restrict__, uint32_t, uint32_t);
 
 }  // namespace swim
