@@ -51,6 +51,10 @@ struct ML {
   // the group of the SYNC merged just now whose SYNC_ACK may be resolved (-1: none)
   uint32_t* tl;
   uint32_t ntl, tlast;
+  // the FD list entry the P6 ping takes and its dead_tick, loaded with the member state when the ping is due and the
+  // cursor needs no reshuffle (compared only at the ping, so nothing waits for them before); pre = NEVER when not
+  // loaded or once the list changes in this tick
+  uint32_t pre, pre_dt;
   int rgrp;
   bool spec;  // a launch of a one-GPU speculative batch: a member that takes a gossip slot raises d.halt (k_member_tick)
 };
@@ -294,6 +298,7 @@ __device__ __forceinline__ void fd_ready(ML& L) {
 
 __device__ __forceinline__ void on_member_event(ML& L, uint32_t type, uint32_t subj) {
   const Dev& d = *L.d;
+  L.pre = NEVER;
   if (type == 1) {  // REMOVED: FailureDetectorImpl.onMemberEvent (:321-325), GossipProtocolImpl (:187-189)
     fd_ready(L);
     if (list_remove(L.fdl, L.fdLen, subj)) L.fdLen--;
@@ -756,10 +761,18 @@ __device__ __forceinline__ void do_ping(ML& L) {
     L.pingIdx = 0;
     shuffle_list(L, L.fdl, L.fdLen, S_FD_SHUFFLE);
   }
-  uint32_t target = L.fdl[L.pingIdx++];
+  uint32_t target;
+  int dd = -1;  // the target's liveness, when loaded with the member state (L.pre)
+  if (L.pre != NEVER) {
+    target = L.pre;
+    dd = L.k >= L.pre_dt ? 1 : 0;
+    L.pingIdx++;
+  } else {
+    target = L.fdl[L.pingIdx++];
+  }
   uint32_t cnt = L.cidCnt++;
   L.c[C_M]++;
-  const int e = xmit_ep(d, L.ep, K_PING, L.m, target, L.k, L.m, cnt);
+  const int e = xmit_ep(d, L.ep, K_PING, L.m, target, L.k, L.m, cnt, dd);
   if (e < 0) {
     L.c[C_LOST]++;
     ping_req_step(L, target, cnt);
@@ -1116,6 +1129,7 @@ __device__ __forceinline__ void ml_init(ML& L, const Dev& d, uint32_t m, uint32_
   L.ntl = 0;
   L.tlast = NEVER;
   L.rgrp = -1;
+  L.pre = NEVER;
 }
 
 // member_tick_body's state back (everything but next_evt and tround, which only a finished tick stores)
@@ -1172,6 +1186,11 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   }
   // P1's inbound list head, loaded with the state above (P0's sends link into the other buffer)
   const uint32_t head0 = (mode != BODY_RESUME && !dead && k > 0) ? d.m_head[(size_t)((k - 1) & 1) * d.N + m] : NEVER;
+  // the P6 ping's target and its liveness, loaded now (do_ping's loads would wait for this tick's stores)
+  if (!dead && k == L.nextPing && L.fdLen > 0 && L.pingIdx >= 0 && L.pingIdx < (int32_t)L.fdLen) {
+    L.pre = L.fdl[L.pingIdx];
+    L.pre_dt = d.dead_tick[L.pre];
+  }
   // SWIM_EXP & 16 (timing experiment): shader cycles per phase summed over members, ctr[8..12]
   // SWIM_EXP & 128: the largest per-member cycles of each phase instead (which phase makes the longest lane)
   const bool prof = (d.exp & (16 | 128)) != 0;
@@ -1245,7 +1264,6 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   if (head0 != NEVER) {
     const uint32_t pb = (k - 1) & 1;
     const uint32_t head = head0;
-    d.m_head[(size_t)pb * d.N + m] = NEVER;
     uint64_t key[MQ];
     uint32_t idx[MQ], n = 0;
     bool more = false;
@@ -1266,6 +1284,8 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
       key[j] = kq;
       idx[j] = q;
     }
+    // (reset after the walk's loads: on gfx950 a load issued after this lane's store waits for the store)
+    d.m_head[(size_t)pb * d.N + m] = NEVER;
     lap(5);
     uint64_t last = 0;
     L.trk_on = n > 1 || more;  // several payloads: later ones re-check the subjects earlier ones changed
