@@ -763,8 +763,6 @@ int build(swim_handle* h) {
     A(d.rdirty, (uint64_t)NL * d.MW) A(d.arena_dirty[0], (uint64_t)d.ARENA_ROWS * d.MW)
     A(d.arena_dirty[1], (uint64_t)d.ARENA_ROWS * d.MW)
     A(d.base_row, d.NS) A(d.xn, 8) A(d.ns_rec, (uint64_t)d.NSCAP * NSW) A(d.rr_rec, (uint64_t)d.RRCAP * RRW)
-    A(d.rq_n, d.W) A(d.rq_list, (uint64_t)d.W * d.RQCAP)
-    A(d.rq_mask, (uint64_t)d.W * d.RQCAP * d.MW) A(d.rq_cnt, (uint64_t)d.W * d.RQCAP) A(d.rq_base, (uint64_t)d.W * d.RQCAP)
     A(d.mtmp, d.MSGCAP) A(d.rx_mask, (uint64_t)d.RXCAP * d.MW) A(d.rx_off, d.RXCAP)
     A(d.xa_send, d.W * d.XA_PEER) A(d.xa_recv, d.W * d.XA_PEER) A(d.xb_send, d.W * d.XB_PEER)
     A(d.xb_recv, d.W * d.XB_PEER) A(d.xa_scnt, d.W) A(d.xa_rcnt, d.W) A(d.xb_scnt, d.W) A(d.xb_rcnt, d.W)
@@ -813,7 +811,6 @@ int build(swim_handle* h) {
   HIPCK(hipMemsetAsync(d.msgs[1], 0xFF, (size_t)d.MSGCAP * sizeof(SyncMsg), h->stream));
   if (d.W > 1) {
     HIPCK(hipMemsetAsync(d.xn, 0, 32, h->stream));
-    HIPCK(hipMemsetAsync(d.rq_n, 0, 4ull * d.W, h->stream));
     HIPCK(hipMemsetAsync(d.xa_scnt, 0, 8ull * d.W, h->stream));
     HIPCK(hipMemsetAsync(d.xb_scnt, 0, 8ull * d.W, h->stream));
   }

@@ -408,7 +408,6 @@ __device__ __forceinline__ void tick_end(const Dev& d, uint32_t k) {
   uint32_t t = threadIdx.x;
   if (t < 8) d.xn[t] = 0;
   if (t < d.W) {
-    d.rq_n[t] = 0;
     d.xa_scnt[t] = 0;
     d.xb_scnt[t] = 0;
     d.xdone[t] = 0;

@@ -360,11 +360,6 @@ struct Dev {
   uint32_t* xn;        // [8] 0 new slots, 1 round records, 2 sweeps, 4 inbound msgs (mtmp), 5 rx payloads
   uint32_t* ns_rec;    // [NSCAP][NSW] gossips created on this shard this tick
   uint32_t* rr_rec;    // [RRCAP][RRW] gossip rounds of this shard's members this tick
-  uint32_t* rq_n;      // [W] SYNC messages to each shard this tick
-  uint32_t* rq_list;   // [W][RQCAP] their indices in msgs[b]
-  uint64_t* rq_mask;   // [W * RQCAP][MW] chunks of the payload that differ from base_row
-  uint32_t* rq_cnt;    // [W * RQCAP] popcount of the mask
-  uint32_t* rq_base;   // [W * RQCAP] first chunk slot in the peer region
   SyncMsg* mtmp;       // [MSGCAP] inbound list of the next tick while it is assembled
   uint64_t* rx_mask;   // [RXCAP][MW]
   uint64_t* rx_off;    // [RXCAP] byte offset (in xa_recv) of the first shipped chunk of a received payload

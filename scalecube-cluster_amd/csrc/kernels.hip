@@ -11,9 +11,7 @@ enum : uint32_t { BODY_FULL = 0, BODY_SPLIT = 1, BODY_RESUME = 2 };  // member.h
 template <uint32_t MODE>
 __global__ void k_member_tick_t(const Dev* __restrict__ dp, uint32_t k, uint32_t flag);  // member.hip
 // shard.hip
-__global__ void k_sync_route(Dev d, uint32_t b, uint32_t spec);
-__global__ void k_pack_a(Dev d, uint32_t b, uint32_t spec);
-__global__ void k_pack_a_chunks(Dev d, uint32_t b, uint32_t spec);
+__global__ void k_pack_all(Dev d, uint32_t b, uint32_t spec);  // shard.hip
 __global__ void k_unpack_a(Dev d, uint32_t k, uint32_t end, uint32_t spec);
 __global__ void k_pack_b(Dev d);
 __global__ void k_round_reset(Dev d);
@@ -984,10 +982,8 @@ void launch_tick_a(const Dev& d, uint32_t k, void* stream, const TickEvents* pro
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[2], st);
   hipLaunchKernelGGL(k_member_tick_t<BODY_FULL>, dim3(cdiv(d.NL, 256)), dim3(256), 0, st, d.self, k, spec ? 2u : 0u);
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[3], st);
-  hipLaunchKernelGGL(k_sync_route, dim3(cdiv(d.MSGCAP, 256)), dim3(256), 0, st, d, b, sp);
   if (d.dly_on) hipLaunchKernelGGL(k_sync_redeliver_x, dim3(256), dim3(256), 0, st, d, k, sp);
-  hipLaunchKernelGGL(k_pack_a, dim3(d.W), dim3(256), 0, st, d, b, sp);
-  hipLaunchKernelGGL(k_pack_a_chunks, dim3(64, d.W), dim3(256), 0, st, d, b, sp);
+  hipLaunchKernelGGL(k_pack_all, dim3(16, d.W), dim3(256), 0, st, d, b, sp);  // route + exchange-A regions
 }
 
 void launch_tick_b(const Dev& d, uint32_t k, void* stream, const TickEvents* prof, bool gossip, bool spec) {

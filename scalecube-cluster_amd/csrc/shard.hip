@@ -37,139 +37,184 @@ __device__ __forceinline__ const uint32_t* payload_row(const Dev& d, const SyncM
   return mm.payload == NEVER ? d.rowk + lidx(d, mm.src) * d.NS : d.arena[b] + (size_t)mm.payload * d.NS;
 }
 
-// this tick's sends: local destinations go straight to the next tick's inbound list, the rest are queued per shard
-// with their payload's dirty-chunk mask (maintained at every key write, member.hip row_put; no scan of the payload)
-__global__ void k_sync_route(Dev d, uint32_t b, uint32_t spec) {
-  if (spec_halted(d, spec)) return;
-  uint32_t n = d.nmsg[b] < d.MSGCAP ? d.nmsg[b] : d.MSGCAP;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const SyncMsg& mm = d.msgs[b][i];
-    uint32_t q = shard_of(d.N, d.W, mm.dst);
-    if (q == d.rank) {
-      uint32_t j = atomicAdd(&d.xn[4], 1u);
-      if (j < d.MSGCAP) {
-        d.mtmp[j] = mm;
-        if (d.ackres) copy_log_prefix(d, mm, b, d.mlog + (size_t)j * TL);
-      }
-      continue;
-    }
-    uint32_t j = atomicAdd(&d.rq_n[q], 1u);
-    if (j >= d.RQCAP) {
-      atomicOr(d.err, E_XCAP);
-      continue;
-    }
-    // the payload's chunk mask against base_row: the sender's dirty chunks, as of its copy-on-write if it made one
-    const uint64_t* dm = mm.payload == NEVER ? d.rdirty + lidx(d, mm.src) * d.MW : d.arena_dirty[b] + (size_t)mm.payload * d.MW;
-    size_t e = (size_t)q * d.RQCAP + j;
-    d.rq_list[e] = i;
-    uint32_t nc = 0;
-    for (uint32_t w = 0; w < d.MW; ++w) {
-      const uint64_t x = dm[w];
-      d.rq_mask[e * d.MW + w] = x;
-      nc += __popcll(x);
-    }
-    d.rq_cnt[e] = nc;
+// block-wide exclusive prefix sum of v over the 256 threads (sh: 8 words of LDS); *tot = the block's sum
+__device__ __forceinline__ uint32_t block_excl_256(uint32_t v, uint32_t* sh, uint32_t* tot) {
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  uint32_t incl = v;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_up(incl, o);
+    if (lane >= o) incl += u;
   }
+  __syncthreads();
+  if (lane == 63) sh[wv] = incl;
+  __syncthreads();
+  uint32_t before = 0;
+  for (uint32_t w = 0; w < wv; ++w) before += sh[w];
+  *tot = sh[0] + sh[1] + sh[2] + sh[3];
+  return before + incl - v;
 }
 
-// region layout, records and SYNC headers for peer q (one block per peer)
-__global__ void __launch_bounds__(256) k_pack_a(Dev d, uint32_t b, uint32_t spec) {
-  const uint32_t q = blockIdx.x;
-  if (q == d.rank || spec_halted(d, spec)) return;
-  __shared__ uint32_t sh[8];
+// k_sync_route + k_pack_a + k_pack_a_chunks in one launch (grid 16 x W): every block of peer column q walks this
+// tick's messages in index order and finds the ones to shard q (the same list in every block of the column, so no
+// block waits for another); block 0 writes the region's header, records and SYNC entries, every block copies its share
+// of the payloads' differing chunks, and the last block of the column writes q's inline all-to-all block. Column
+// `rank` queues the local messages for the next tick's inbound list. (A steady-state sharded tick was member kernel,
+// route, pack, chunk launches back to back: two launches and their drains fewer.)
+__global__ void __launch_bounds__(256) k_pack_all(Dev d, uint32_t b, uint32_t spec) {
+  if (spec_halted(d, spec)) return;
+  const uint32_t q = blockIdx.y, x = blockIdx.x, t = threadIdx.x;
+  __shared__ uint32_t sh[8], tot_sh[2];
+  const uint32_t n = min(d.nmsg[b], d.MSGCAP);
+  if (q == d.rank) {  // local destinations: straight to the next tick's inbound list
+    if (d.inl && x == 0 && t == 0) *(uint64_t*)(d.xi_send + (size_t)q * d.XI) = 0ull;  // the block to itself: empty
+    for (uint32_t base = 0; x == 0 && base < n; base += 256) {
+      const uint32_t i = base + t;
+      const bool sel = i < n && shard_of(d.N, d.W, d.msgs[b][i].dst) == q;
+      uint32_t tot;
+      const uint32_t ex = block_excl_256(sel ? 1u : 0u, sh, &tot);
+      if (t == 0 && tot) tot_sh[0] = atomicAdd(&d.xn[4], tot);
+      __syncthreads();
+      if (sel) {
+        const uint32_t j = tot_sh[0] + ex;
+        if (j < d.MSGCAP) {
+          const SyncMsg& mm = d.msgs[b][i];
+          d.mtmp[j] = mm;
+          if (d.ackres) copy_log_prefix(d, mm, b, d.mlog + (size_t)j * TL);
+        } else if (j == d.MSGCAP) {
+          set_err(d, E_MSGS);
+        }
+      }
+      __syncthreads();
+    }
+  } else {
   uint8_t* R = d.xa_send + (size_t)q * d.XA_PEER;
   const uint64_t SE = sync_entry_bytes(d);
-  if (threadIdx.x == 0) {
-    uint32_t nslot = min(d.xn[0], d.NSCAP), nround = min(d.xn[1], d.RRCAP), nsync = min(d.rq_n[q], d.RQCAP);
-    uint32_t nchunk = 0;
-    for (uint32_t j = 0; j < nsync; ++j) {
-      size_t e = (size_t)q * d.RQCAP + j;
-      d.rq_base[e] = nchunk;
-      nchunk += d.rq_cnt[e];
+  // pass 1: how many messages go to q and how many payload chunks they ship
+  uint32_t nsync = 0, nchunk = 0;
+  for (uint32_t base = 0; base < n; base += 256) {
+    const uint32_t i = base + t;
+    uint32_t sel = 0, nc = 0;
+    if (i < n) {
+      const SyncMsg& mm = d.msgs[b][i];
+      if (shard_of(d.N, d.W, mm.dst) == q) {
+        sel = 1;
+        const uint64_t* dm = mm.payload == NEVER ? d.rdirty + lidx(d, mm.src) * d.MW : d.arena_dirty[b] + (size_t)mm.payload * d.MW;
+        for (uint32_t w = 0; w < d.MW; ++w) nc += (uint32_t)__popcll(dm[w]);
+      }
     }
-    uint64_t off_sync = 32 + 4ull * NSW * nslot + 4ull * RRW * nround;
-    uint64_t data_off = (off_sync + SE * nsync + 255) & ~255ull;
+    uint32_t ts, tc;
+    block_excl_256(sel, sh, &ts);
+    __syncthreads();
+    block_excl_256(nc, sh, &tc);
+    nsync += ts;
+    nchunk += tc;
+  }
+  const uint32_t nslot = min(d.xn[0], d.NSCAP), nround = min(d.xn[1], d.RRCAP);
+  const uint64_t off_sync = 32 + 4ull * NSW * nslot + 4ull * RRW * nround;
+  uint64_t data_off = (off_sync + SE * nsync + 255) & ~255ull;
+  const bool fits = nsync <= d.RQCAP && data_off + (uint64_t)nchunk * CH * 4 <= d.XA_PEER && nchunk <= d.CHCAP;
+  if (x == 0 && t == 0) {
+    uint32_t* H = (uint32_t*)R;
     uint64_t total = data_off + (uint64_t)nchunk * CH * 4;
-    if (total > d.XA_PEER || nchunk > d.CHCAP) {
+    if (!fits) {
       atomicOr(d.err, E_XCAP);
-      nslot = nround = nsync = nchunk = 0;
       data_off = 256;
       total = 32;
     }
-    uint32_t* H = (uint32_t*)R;
-    H[0] = nslot;
-    H[1] = nround;
-    H[2] = nsync;
-    H[3] = nchunk;
+    H[0] = fits ? nslot : 0u;
+    H[1] = fits ? nround : 0u;
+    H[2] = fits ? nsync : 0u;
+    H[3] = fits ? nchunk : 0u;
     H[4] = (uint32_t)data_off;
     H[5] = H[6] = H[7] = 0;
     // the flag rides on the byte count: every shard learns whether any shard has a gossip slot in use
     d.xa_scnt[q] = total | ((int32_t)d.SPR - *d.free_top > 0 ? XFLAG_GOSSIP : 0ull);
-    sh[0] = nslot;
-    sh[1] = nround;
-    sh[2] = nsync;
   }
-  __syncthreads();
-  const uint32_t nslot = sh[0], nround = sh[1], nsync = sh[2];
-  uint32_t* S = (uint32_t*)(R + 32);
-  for (uint32_t i = threadIdx.x; i < nslot * NSW; i += blockDim.x) S[i] = d.ns_rec[i];
-  uint32_t* RR = S + (size_t)nslot * NSW;
-  for (uint32_t i = threadIdx.x; i < nround * RRW; i += blockDim.x) RR[i] = d.rr_rec[i];
-  uint8_t* E = (uint8_t*)(RR + (size_t)nround * RRW);
-  for (uint32_t j = threadIdx.x; j < nsync; j += blockDim.x) {
-    size_t e = (size_t)q * d.RQCAP + j;
-    uint8_t* p = E + SE * j;
-    *(SyncMsg*)p = d.msgs[b][d.rq_list[e]];
-    ((uint32_t*)(p + sizeof(SyncMsg)))[0] = d.rq_base[e];
-    ((uint32_t*)(p + sizeof(SyncMsg)))[1] = 0;
-    uint64_t* mk = (uint64_t*)(p + sizeof(SyncMsg) + 8);
-    for (uint32_t w = 0; w < d.MW; ++w) mk[w] = d.rq_mask[e * d.MW + w];
-    if (d.ackres) copy_log_prefix(d, d.msgs[b][d.rq_list[e]], b, (uint32_t*)(mk + d.MW));
-  }
-}
-
-// copy the differing payload chunks (key plane) into peer q's region (16-B loads and stores, 8 keys per lane). With
-// RCCL, the last block of peer q's column then writes q's inline all-to-all block (count word + region head), so
-// exchange A needs no separate copy kernel.
-__global__ void __launch_bounds__(256) k_pack_a_chunks(Dev d, uint32_t b, uint32_t spec) {
-  if (spec_halted(d, spec)) return;
-  const uint32_t q = blockIdx.y;
-  if (q == d.rank) {  // the block to itself carries an empty region
-    if (d.inl && blockIdx.x == 0 && threadIdx.x == 0) *(uint64_t*)(d.xi_send + (size_t)q * d.XI) = 0ull;
-    return;
-  }
-  uint8_t* R = d.xa_send + (size_t)q * d.XA_PEER;
-  const uint32_t* H = (const uint32_t*)R;
-  const uint32_t nsync = H[2], data_off = H[4];
-  if (H[3] != 0) {
+  if (fits) {
+    if (x == 0) {  // gossip records (replicated on every shard)
+      uint32_t* S = (uint32_t*)(R + 32);
+      for (uint32_t i = t; i < nslot * NSW; i += blockDim.x) S[i] = d.ns_rec[i];
+      uint32_t* RR = S + (size_t)nslot * NSW;
+      for (uint32_t i = t; i < nround * RRW; i += blockDim.x) RR[i] = d.rr_rec[i];
+    }
+    uint8_t* E = R + off_sync;
     uint32_t* dst0 = (uint32_t*)(R + data_off);
-    for (uint32_t w = blockIdx.x; w < nsync * d.NCHUNK; w += gridDim.x) {
-      const uint32_t j = w / d.NCHUNK, c = w % d.NCHUNK;
-      const size_t e = (size_t)q * d.RQCAP + j;
-      const uint64_t* mk = d.rq_mask + e * d.MW;
-      if (!((mk[c >> 6] >> (c & 63)) & 1ull)) continue;
-      uint32_t rank = __popcll(mk[c >> 6] & ((1ull << (c & 63)) - 1ull));
-      for (uint32_t x = 0; x < (c >> 6); ++x) rank += __popcll(mk[x]);
-      const uint32_t s0 = c * CH + threadIdx.x * 8;
-      if (s0 >= d.NS) continue;
-      const SyncMsg& mm = d.msgs[b][d.rq_list[e]];
-      const uint4* src = (const uint4*)(payload_row(d, mm, b) + s0);
-      uint4* dst = (uint4*)(dst0 + (size_t)(d.rq_base[e] + rank) * CH + threadIdx.x * 8);
-      dst[0] = src[0];
-      dst[1] = src[1];
+    // pass 2: the entries (block 0) and the chunks (chunk r of the column's payloads by block r % gridDim.x)
+    uint32_t j0 = 0, c0 = 0;
+    for (uint32_t base = 0; base < n; base += 256) {
+      const uint32_t i = base + t;
+      uint32_t sel = 0, nc = 0;
+      const uint64_t* dm = nullptr;
+      if (i < n) {
+        const SyncMsg& mm = d.msgs[b][i];
+        if (shard_of(d.N, d.W, mm.dst) == q) {
+          sel = 1;
+          dm = mm.payload == NEVER ? d.rdirty + lidx(d, mm.src) * d.MW : d.arena_dirty[b] + (size_t)mm.payload * d.MW;
+          for (uint32_t w = 0; w < d.MW; ++w) nc += (uint32_t)__popcll(dm[w]);
+        }
+      }
+      uint32_t ts, tc;
+      const uint32_t ej = block_excl_256(sel, sh, &ts);
+      __syncthreads();
+      const uint32_t ec = block_excl_256(nc, sh, &tc);
+      if (sel && x == 0) {
+        uint8_t* p = E + SE * (j0 + ej);
+        *(SyncMsg*)p = d.msgs[b][i];
+        ((uint32_t*)(p + sizeof(SyncMsg)))[0] = c0 + ec;
+        ((uint32_t*)(p + sizeof(SyncMsg)))[1] = 0;
+        uint64_t* mk = (uint64_t*)(p + sizeof(SyncMsg) + 8);
+        for (uint32_t w = 0; w < d.MW; ++w) mk[w] = dm[w];
+        if (d.ackres) copy_log_prefix(d, d.msgs[b][i], b, (uint32_t*)(mk + d.MW));
+      }
+      if (tc) {  // this batch's payload chunks: the block's share, 8 keys per thread with 16-B loads and stores
+        __shared__ uint32_t cmsg[256], cbase[256];
+        __syncthreads();
+        cmsg[t] = nc ? i : NEVER;
+        cbase[t] = c0 + ec;
+        __syncthreads();
+        for (uint32_t l = 0; l < 256; ++l) {
+          const uint32_t mi = cmsg[l];
+          if (mi == NEVER) continue;
+          const SyncMsg& mm = d.msgs[b][mi];
+          const uint64_t* mk = mm.payload == NEVER ? d.rdirty + lidx(d, mm.src) * d.MW : d.arena_dirty[b] + (size_t)mm.payload * d.MW;
+          uint32_t r = cbase[l];
+          for (uint32_t c = 0; c < d.NCHUNK; ++c) {
+            if (!((mk[c >> 6] >> (c & 63)) & 1ull)) continue;
+            if (r % gridDim.x == x) {
+              const uint32_t s0 = c * CH + t * 8;
+              if (s0 < d.NS) {
+                const uint4* src = (const uint4*)(payload_row(d, mm, b) + s0);
+                uint4* dst = (uint4*)(dst0 + (size_t)r * CH + t * 8);
+                dst[0] = src[0];
+                dst[1] = src[1];
+              }
+            }
+            ++r;
+          }
+        }
+      }
+      j0 += ts;
+      c0 += tc;
+      __syncthreads();
     }
   }
-  if (!d.inl || !last_block(&d.xdone[q], gridDim.x)) return;
-  // every peer learns whether this shard needs a send/recv group past the inline blocks this tick (k_pack_a wrote
-  // all the counts in an earlier launch), so a speculative batch halts at the same tick on every shard
+  }  // q != rank
+  // the block that finishes last in the whole grid writes every peer's inline all-to-all block: each count word says
+  // whether any of this shard's regions is past its inline block (then a send/recv group follows), so every peer of
+  // a speculative batch halts at the same tick; every column's count is written by then
+  if (!d.inl || !last_block(&d.xdone[0], gridDim.x * gridDim.y)) return;
   bool over = false;
-  for (uint32_t r = 0; r < d.W; ++r) over |= (d.xa_scnt[r] & XCNT_MASK) > d.XI - 8;
-  const unsigned long long w = d.xa_scnt[q] | (over ? XFLAG_OVER : 0ull);
-  uint64_t* idst = (uint64_t*)(d.xi_send + (size_t)q * d.XI);
-  if (threadIdx.x == 0) idst[0] = w;
-  const uint64_t n = min((uint64_t)(w & XCNT_MASK), (uint64_t)d.XI - 8) / 8;  // regions are multiples of 8 B
-  const uint64_t* isrc = (const uint64_t*)R;
-  for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) idst[1 + i] = isrc[i];
+  for (uint32_t r = 0; r < d.W; ++r) over |= r != d.rank && (d.xa_scnt[r] & XCNT_MASK) > d.XI - 8;
+  for (uint32_t p = 0; p < d.W; ++p) {
+    if (p == d.rank) continue;
+    const unsigned long long w = d.xa_scnt[p] | (over ? XFLAG_OVER : 0ull);
+    uint64_t* idst = (uint64_t*)(d.xi_send + (size_t)p * d.XI);
+    if (t == 0) idst[0] = w;
+    const uint64_t nw = min((uint64_t)(w & XCNT_MASK), (uint64_t)d.XI - 8) / 8;  // regions are multiples of 8 B
+    const uint64_t* isrc = (const uint64_t*)(d.xa_send + (size_t)p * d.XA_PEER);
+    for (uint64_t i = t; i < nw; i += blockDim.x) idst[1 + i] = isrc[i];
+  }
 }
 
 // the assembled inbound list becomes msgs[b], which the next tick sorts and merges (one block)
