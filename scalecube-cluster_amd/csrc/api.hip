@@ -689,7 +689,7 @@ int build(swim_handle* h) {
   A(d.m_next, 2ull * d.MSGCAP) A(d.m_head, 2 * N) A(d.next_evt, N) A(d.mdone, 2) A(d.trk, NL * TRKL) A(d.ulog, NL * d.ULOGC * 2) A(d.spq, NL * SPQ * 8) A(d.fpend, NL * KP * 2) A(d.pending_inc, N) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
   A(d.pool, d.POOLCAP) A(d.pool_used, 1)
   d.NW = d.implicit ? 0u : (d.N + 63u) / 64u;  // (RUMOR mode with implicit views has no SYNC)
-  A(d.hv_list, NL) A(d.nhv, 1) A(d.hv_pend, NL) A(d.hv_tlast, NL)
+  A(d.hv_list, NL) A(d.nhv, 1) A(d.hv_pend, NL) A(d.hv_tlast, NL) A(d.sg_list, N) A(d.nsg, 1) A(d.ap_list, N) A(d.nap, 1)
   HIPCK(hipMemsetAsync(d.nhv, 0, 4, h->stream));
   A(d.tbm, std::max<uint64_t>(1, NL * d.NW))
   HIPCK(hipMemsetAsync(d.tbm, 0, 8 * std::max<uint64_t>(1, NL * d.NW), h->stream));
@@ -918,7 +918,7 @@ int exchange(swim_handle* h, uint8_t* send, uint8_t* recv, uint64_t cap, unsigne
   if (h->spec.transport == SWIM_TRANSPORT_RCCL) {
     // one fixed-size all-to-all (count word + the first XINL - 8 bytes of each region), one host read of the
     // count words through mapped memory, and a send/recv group only for regions that did not fit
-    if (!inline_packed) launch_inline_out(h->d, send, cap, scnt, st);  // exchange A: k_pack_a_chunks wrote them
+    if (!inline_packed) launch_inline_out(h->d, send, cap, scnt, st);  // exchange A: k_pack_all wrote them
     int rc;
     if ((rc = exchange_inline(h, recv, cap, scnt, rcnt, false)) != SWIM_OK) return rc;
     HIPCK(hipEventRecord(h->ev_member, st));
@@ -1461,10 +1461,28 @@ int swim_step(swim_handle* h, uint32_t n) {
           HIPCK(hipMemcpy(nf.data(), d.nfetch, 4ull * d.N, hipMemcpyDeviceToHost));
           std::sort(rc.begin(), rc.end());
           std::sort(nf.begin(), nf.end());
+          // first receipts per target with senders this tick (rtail - rt0), and senders per target
+          std::vector<uint32_t> tl(v[1]), r0(d.N), r1(d.N), tc(d.N), fr, sn;
+          HIPCK(hipMemcpy(tl.data(), d.tlist, 4ull * v[1], hipMemcpyDeviceToHost));
+          HIPCK(hipMemcpy(r0.data(), d.rt0, 4ull * d.N, hipMemcpyDeviceToHost));
+          HIPCK(hipMemcpy(r1.data(), d.rtail, 4ull * d.N, hipMemcpyDeviceToHost));
+          HIPCK(hipMemcpy(tc.data(), d.tin_off, 4ull * d.N, hipMemcpyDeviceToHost));  // (tin_cnt is reset by then)
+          uint64_t tot = 0;
+          for (uint32_t t : tl) {
+            fr.push_back(r1[t] - r0[t]);
+            if (t + 1 < d.N) sn.push_back(tc[t + 1] - tc[t]);
+            tot += r1[t] - r0[t];
+          }
+          std::sort(fr.begin(), fr.end());
+          std::sort(sn.begin(), sn.end());
+          const size_t nt = fr.size();
           fprintf(stderr, "stats tick %u: routed %u targets %u groups %u replay %u slow %u contacts %u rx %u rounds %u; "
-                  "receipts per member median %u p99 %u max %u; pending fetches median %u p99 %u max %u\n",
+                  "receipts per member median %u p99 %u max %u; pending fetches median %u p99 %u max %u; "
+                  "first receipts %llu, per target median %u p90 %u p99 %u max %u; senders per target median %u max %u\n",
                   k, v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], rc[d.N / 2], rc[d.N * 99 / 100], rc[d.N - 1],
-                  nf[d.N / 2], nf[d.N * 99 / 100], nf[d.N - 1]);
+                  nf[d.N / 2], nf[d.N * 99 / 100], nf[d.N - 1], (unsigned long long)tot, nt ? fr[nt / 2] : 0,
+                  nt ? fr[nt * 9 / 10] : 0, nt ? fr[nt * 99 / 100] : 0, nt ? fr[nt - 1] : 0, sn.empty() ? 0 : sn[sn.size() / 2],
+                  sn.empty() ? 0 : sn.back());
         }
       } else if (te && te->all) {
         HIPCK(hipEventRecord((hipEvent_t)te->ev[4], h->stream));

@@ -272,6 +272,8 @@ struct Dev {
   uint32_t* leaving;   // [N] 1 once the member's leave was requested (its own DEAD record may travel in SYNC data)
   uint64_t* rc_key;   // [RCAP] gossip id sort key
   uint32_t* rc_slot2;  // [RCAP] merge scratch of k_seg_sort (segments above SORT_MAX)
+  uint32_t *ap_list, *nap;  // [N], [1] targets with more than APPLY_LANE first receipts this tick (k_gossip_apply_big)
+  uint32_t *sg_list, *nsg;  // [N], [1] members with two routed receipts or more this tick (the segments to sort)
   uint64_t* rc_key2;
   uint32_t* fexp;   // [SLOTS] slots recycled at the end of this tick (k_gossip_free)
   uint32_t* nfexp;
@@ -311,7 +313,7 @@ struct Dev {
   uint32_t* dlist;    // [MSGCAP]
   uint32_t* ndl;
   // W > 1: the sender's write-log prefix (SyncMsg.tln entries) of each message of the inbound list committed this tick,
-  // by its index there: copied by k_sync_route for this shard's senders and shipped in exchange A for the peers'
+  // by its index there: copied by k_pack_all for this shard's senders and shipped in exchange A for the peers'
   uint32_t* mlog;     // [MSGCAP][TL]
   // P4 of the members with many routed gossip receipts (W == 1, ticks after a gossip plane): k_member_tick parks a
   // member with at least hv receipts before P4 (its pending live-row payload chain and write-log tail kept here),
@@ -368,8 +370,8 @@ struct Dev {
   uint8_t *xi_send, *xi_recv;    // [W][XINL] inline all-to-all blocks
   uint32_t XI;                   // bytes per peer the inline all-to-all moves (XINL; SWIM_CAPS xinl= lowers it)
   unsigned long long* xi_host;   // host-mapped [2W]: send and receive count words of the last exchange
-  uint32_t* xdone;  // [W] finished k_pack_a_chunks blocks per peer column (the last one writes the inline block)
-  uint32_t inl;     // RCCL transport: exchange A's inline blocks are written by k_pack_a_chunks
+  uint32_t* xdone;  // [W] finished k_pack_all blocks per peer column (the last one writes the inline block)
+  uint32_t inl;     // RCCL transport: exchange A's inline blocks are written by k_pack_all
 
   // ---- slot sharding (RUMOR mode with W > 1) ----
   // Every shard runs all N members (their scalar state is replicated and evolves identically) but holds only the

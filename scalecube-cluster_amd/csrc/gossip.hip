@@ -284,7 +284,7 @@ __global__ void __launch_bounds__(1024) k_gossip_groups(Dev d) {
   __shared__ uint32_t base;
   if (threadIdx.x == 0) {
     base = 0;
-    *d.slow_n = *d.rp_n = *d.nrwl = *d.ntl = *d.xd_n = *d.nfexp = *d.nrx = *d.ncfl = 0;
+    *d.slow_n = *d.rp_n = *d.nrwl = *d.ntl = *d.xd_n = *d.nfexp = *d.nrx = *d.ncfl = *d.nsg = *d.nap = 0;
   }
   __syncthreads();
   for (uint32_t q0 = 0; q0 < d.QW; q0 += 1024) {
@@ -1033,72 +1033,127 @@ __device__ __forceinline__ void receipt_create(const Dev& d, uint32_t g, uint32_
     d.slot_exp[g] = k + d.lat + d.EXPB;  // every holder sweeps it by then (all receipts of a tick store the same value)
 }
 
-// 8. first receipts of this shard's targets, one wave per target: the entries its ring gained this tick. Holder
-// table, expiry, gossip count, then membership: records that can change the row are queued for P4 of k + lat in
-// gossip-id order (receipt routing), the others are counted as record compares; RUMOR mode hashes the GOSSIP events
-// here (fastp4). The senders' lists are reset for the next tick.
+// 8. first receipts of this shard's targets: the entries each target's ring gained this tick. Holder table, expiry,
+// gossip count, then membership: records that can change the row are queued for P4 of k + lat in gossip-id order
+// (receipt routing), the others are counted as record compares; RUMOR mode hashes the GOSSIP events here (fastp4).
+// The senders' lists are reset for the next tick. A wave takes 64 targets: those with at most APPLY_LANE new entries
+// (C3 with membership evolution: one to three) on a lane each; the others (C2: a few hundred) are listed for
+// k_gossip_apply_big, a wave each, so neither 63 idle lanes per target nor one lane walking hundreds of entries hold
+// the launch.
+constexpr uint32_t APPLY_LANE = 8;
+
+// the target's bookkeeping once its entries are applied (one lane)
+__device__ __forceinline__ void apply_target_end(const Dev& d, uint32_t t, uint32_t a, uint32_t b, uint32_t drops,
+                                                 unsigned long long eh) {
+  const uint32_t nr = b - a;
+  // the host grows the rings before they can overflow (the atomic only when the fill beats the maximum so far:
+  // one address taking an atomic from every target serialises, ~13 ns each)
+  if (d.rfill && b - d.rhead[t] > __hip_atomic_load(d.rfill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    atomicMax(d.rfill, b - d.rhead[t]);
+  if (nr) {
+    if (d.XW > 1)
+      atomicAdd(&d.held_delta[t], (int)nr);
+    else
+      atomicAdd(&d.held[t], nr);
+  }
+  if (drops) atomicAdd(&d.rc_ndrop[t], drops);
+  if (d.fastp4 && nr) {
+    atomicAdd(&d.evp_hash[t], eh);
+    atomicAdd(&d.evp_n[t], nr);
+  }
+  d.tin_cnt[t] = 0;
+  d.tin_fill[t] = 0;
+}
+
+// one entry at ring position p of target t: holder table and expiry; true if its record is routed to P4
+__device__ __forceinline__ bool apply_entry(const Dev& d, uint32_t t, uint32_t g, uint32_t k, uint32_t& drops,
+                                            unsigned long long& eh) {
+  receipt_create(d, g, t, k);
+  if (d.fastp4 && d.slot_subj[g] == USER_SUBJ) {  // RUMOR mode: the GOSSIP event of P4 (k + lat), hashed now
+    const uint64_t gid = d.slot_gid[g], key = d.slot_key[g];
+    const uint64_t ev = ((uint64_t)(k + d.lat) << 32) | (3ull << 30) | (uint32_t)(gid >> 32);
+    const uint64_t meta = ((uint64_t)(uint32_t)key << 32) | (key >> 32);  // (oldMeta, newMeta) = payload (lo, hi)
+    eh += hpair(hpair(ev, meta), (uint32_t)gid);
+    return false;
+  }
+  if (!receipt_matters(d, t, g, k + d.lat)) {  // counted as a record compare in P4, nothing else
+    drops++;
+    return false;
+  }
+  return true;
+}
+
 __global__ void __launch_bounds__(256) k_gossip_apply(const Dev* __restrict__ dp, uint32_t k) {
   const Dev& d = *dp;
-  const uint32_t lane = threadIdx.x & 63u, ntl = *d.ntl;
-  for (uint32_t ti = blockIdx.x * 4 + (threadIdx.x >> 6); ti < ntl; ti += gridDim.x * 4) {
-    const uint32_t t = d.tlist[ti], a = d.rt0[t], b = d.rtail[t];
-    const uint32_t* R = ring(d, t);
-    uint32_t drops = 0;
-    unsigned long long eh = 0;
-    // batches of 64 entries per lane: which ones are routed to P4 is kept as a bit per entry, then the wave reserves
+  const uint32_t lane = threadIdx.x & 63u, ntl = *d.ntl, mask = d.BCAP - 1;
+  const uint32_t nw = gridDim.x * 4;
+  for (uint32_t t0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 64; t0 < ntl; t0 += nw * 64) {
+    const uint32_t ti = t0 + lane;
+    uint32_t t = 0, a = 0, b = 0;
+    if (ti < ntl) {
+      t = d.tlist[ti];
+      a = d.rt0[t];
+      b = d.rtail[t];
+    }
+    const bool small = ti < ntl && b - a <= APPLY_LANE;
+    // the small targets, a lane each: which entries are routed is kept as a bit per entry, then the wave reserves
     // their places in the routing list with one atomic (a per-entry append would serialise on rc_n)
-    for (uint32_t p0 = a; p0 - a < b - a; p0 += 64u * 64u) {
-      unsigned long long routed = 0;
+    uint32_t routed = 0, drops = 0;
+    unsigned long long eh = 0;
+    if (small) {
+      const uint32_t* R = ring(d, t);
+      for (uint32_t i = 0; i < b - a; ++i)
+        if (apply_entry(d, t, R[(a + i) & mask] & RG_SLOT, k, drops, eh)) routed |= 1u << i;
+    }
+    uint32_t ri = wave_reserve(d.rc_n, (uint32_t)__popc(routed));
+    if (small) {
+      const uint32_t* R = ring(d, t);
+      for (uint32_t r = routed; r; r &= r - 1, ++ri) {
+        const uint32_t p = a + (uint32_t)(__ffs(r) - 1);
+        if (ri < d.RCAP)
+          d.rc_raw[ri] = ((uint64_t)t << 32) | (R[p & mask] & RG_SLOT);
+        else
+          set_err(d, E_RECEIPTS);
+      }
+      apply_target_end(d, t, a, b, drops, eh);
+    }
+    // the large targets go to a list for k_gossip_apply_big (a wave each, all of them in parallel)
+    const bool big = ti < ntl && !small;
+    const uint32_t bi = wave_reserve(d.nap, big ? 1u : 0u);
+    if (big) d.ap_list[bi] = t;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_gossip_apply_big(const Dev* __restrict__ dp, uint32_t k) {
+  const Dev& d = *dp;
+  const uint32_t lane = threadIdx.x & 63u, n = *d.nap, mask = d.BCAP - 1;
+  for (uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6); w < n; w += gridDim.x * 4) {
+    const uint32_t t = d.ap_list[w], a = d.rt0[t], b = d.rtail[t];
+    const uint32_t* R = ring(d, t);
+    uint32_t dr = 0;
+    unsigned long long h = 0;
+    for (uint32_t p0 = a; p0 - a < b - a; p0 += 64u * 64u) {  // 64 entries per lane per batch
+      unsigned long long rt = 0;
       for (uint32_t it = 0; it < 64; ++it) {
         const uint32_t p = p0 + it * 64u + lane;
         if (p - a >= b - a) break;
-        const uint32_t g = R[p & (d.BCAP - 1)] & RG_SLOT;
-        receipt_create(d, g, t, k);
-        if (d.fastp4 && d.slot_subj[g] == USER_SUBJ) {  // RUMOR mode: the GOSSIP event of P4 (k + lat), hashed now
-          const uint64_t gid = d.slot_gid[g], key = d.slot_key[g];
-          const uint64_t ev = ((uint64_t)(k + d.lat) << 32) | (3ull << 30) | (uint32_t)(gid >> 32);
-          const uint64_t meta = ((uint64_t)(uint32_t)key << 32) | (key >> 32);  // (oldMeta, newMeta) = payload (lo, hi)
-          eh += hpair(hpair(ev, meta), (uint32_t)gid);
-        } else if (!receipt_matters(d, t, g, k + d.lat)) {  // counted as a record compare in P4, nothing else
-          drops++;
-        } else {
-          routed |= 1ull << it;
-        }
+        if (apply_entry(d, t, R[p & mask] & RG_SLOT, k, dr, h)) rt |= 1ull << it;
       }
-      uint32_t ri = wave_reserve(d.rc_n, (uint32_t)__popcll(routed));
-      for (; routed; routed &= routed - 1, ++ri) {
-        const uint32_t p = p0 + (uint32_t)(__ffsll((long long)routed) - 1) * 64u + lane;
-        if (ri < d.RCAP)
-          d.rc_raw[ri] = ((uint64_t)t << 32) | (R[p & (d.BCAP - 1)] & RG_SLOT);
+      uint32_t rj = wave_reserve(d.rc_n, (uint32_t)__popcll(rt));
+      for (; rt; rt &= rt - 1, ++rj) {
+        const uint32_t p = p0 + (uint32_t)(__ffsll((long long)rt) - 1) * 64u + lane;
+        if (rj < d.RCAP)
+          d.rc_raw[rj] = ((uint64_t)t << 32) | (R[p & mask] & RG_SLOT);
         else
           set_err(d, E_RECEIPTS);
       }
     }
     for (uint32_t o = 32; o > 0; o >>= 1) {
-      drops += __shfl_xor(drops, o);
-      const uint32_t lo = __shfl_xor((uint32_t)eh, o), hi = __shfl_xor((uint32_t)(eh >> 32), o);
-      eh += ((unsigned long long)hi << 32) | lo;
+      dr += __shfl_xor(dr, o);
+      const uint32_t lo = __shfl_xor((uint32_t)h, o), hi = __shfl_xor((uint32_t)(h >> 32), o);
+      h += ((unsigned long long)hi << 32) | lo;
     }
-    if (lane == 0) {
-      const uint32_t nr = b - a;
-      // the host grows the rings before they can overflow (the atomic only when the fill beats the maximum so far:
-      // one address taking an atomic from every target wave serialises, ~13 ns each)
-      if (d.rfill && b - d.rhead[t] > __hip_atomic_load(d.rfill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-        atomicMax(d.rfill, b - d.rhead[t]);
-      if (nr) {
-        if (d.XW > 1)
-          atomicAdd(&d.held_delta[t], (int)nr);
-        else
-          atomicAdd(&d.held[t], nr);
-      }
-      if (drops) atomicAdd(&d.rc_ndrop[t], drops);
-      if (d.fastp4 && nr) {
-        atomicAdd(&d.evp_hash[t], eh);
-        atomicAdd(&d.evp_n[t], nr);
-      }
-      d.tin_cnt[t] = 0;
-      d.tin_fill[t] = 0;
-    }
+    if (lane == 0) apply_target_end(d, t, a, b, dr, h);
   }
 }
 
@@ -1182,6 +1237,7 @@ void launch_gossip_send(const Dev& d, uint32_t k, hipStream_t st, const TickEven
 // the receivers' side of this tick's first receipts, P4 routing and slot recycling
 void launch_gossip_apply(const Dev& d, uint32_t k, hipStream_t st) {
   hipLaunchKernelGGL(k_gossip_apply, dim3(2048), dim3(256), 0, st, d.self, k);
+  hipLaunchKernelGGL(k_gossip_apply_big, dim3(2048), dim3(256), 0, st, d.self, k);
   launch_receipt_routing(d, st);
   hipLaunchKernelGGL(k_gossip_expire, dim3(cdiv((uint64_t)d.QW * 64, 256)), dim3(256), 0, st, d, k);
   hipLaunchKernelGGL(k_gossip_free, dim3(1024), dim3(256), 0, st, d);

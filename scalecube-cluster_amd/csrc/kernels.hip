@@ -130,7 +130,9 @@ __global__ void k_scatter_rc(const Dev d, const uint64_t* raw, const uint32_t* n
   uint32_t n = *n_ < cap ? *n_ : cap;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     uint32_t t = (uint32_t)(raw[i] >> 32), g = (uint32_t)raw[i];
-    uint32_t p = off[t] + atomicAdd(&fill[t], 1u);
+    const uint32_t f = atomicAdd(&fill[t], 1u);
+    if (f == 1u) d.sg_list[atomicAdd(d.nsg, 1u)] = t;  // a segment with two receipts or more: k_seg_sort sorts it
+    uint32_t p = off[t] + f;
     idx[p] = g;
     key[p] = d.slot_gid[g];
   }
@@ -240,13 +242,15 @@ __device__ __forceinline__ uint32_t lower_rank(const uint64_t* r, uint32_t n, ui
   return lo;
 }
 
+// the segments listed in sg (nsg of them: members with two receipts or more, k_scatter_rc), not all N
 __global__ void __launch_bounds__(256) k_seg_sort(uint64_t* key, uint32_t* val, uint64_t* tkey, uint32_t* tval,
-                                                  const uint32_t* off, const uint32_t* cnt, uint32_t nseg,
-                                                  const uint32_t* nitems, uint32_t run, unsigned long long* fb) {
+                                                  const uint32_t* off, const uint32_t* cnt, const uint32_t* sg,
+                                                  const uint32_t* nsg, uint32_t run, unsigned long long* fb) {
   __shared__ uint64_t K[SORT_MAX];
   __shared__ uint32_t V[SORT_MAX];
-  if (*nitems == 0) return;  // nothing was routed this tick
-  for (uint32_t sgi = blockIdx.x; sgi < nseg; sgi += gridDim.x) {
+  const uint32_t nseg = *nsg;
+  for (uint32_t li = blockIdx.x; li < nseg; li += gridDim.x) {
+    const uint32_t sgi = sg[li];
     const uint32_t n = cnt[sgi];
     if (n <= 1) continue;
     const uint32_t o = off[sgi];
@@ -967,7 +971,7 @@ void launch_receipt_routing(const Dev& d, hipStream_t st) {
   hipLaunchKernelGGL(k_scatter_rc, dim3(256), dim3(256), 0, st, d, d.rc_raw, d.rc_n, d.RCAP, d.rc_off, d.rc_fill,
                      d.rc_slot, d.rc_key);
   hipLaunchKernelGGL(k_seg_sort, dim3(1024), dim3(256), 0, st, d.rc_key, d.rc_slot, d.rc_key2, d.rc_slot2, d.rc_off,
-                     d.rc_cnt, d.N, d.rc_n, d.sort_cap, d.fb);
+                     d.rc_cnt, d.sg_list, d.nsg, d.sort_cap, d.fb);
 }
 
 // sharded tick (W > 1): A = SYNC diff + member control + pack exchange A; B = unpack A, the rounds' holder-state

@@ -55,7 +55,7 @@ __device__ __forceinline__ uint32_t block_excl_256(uint32_t v, uint32_t* sh, uin
   return before + incl - v;
 }
 
-// k_sync_route + k_pack_a + k_pack_a_chunks in one launch (grid 16 x W): every block of peer column q walks this
+// k_pack_all: routing, packing and chunk copy of exchange A in one launch (grid 16 x W): every block of peer column q walks this
 // tick's messages in index order and finds the ones to shard q (the same list in every block of the column, so no
 // block waits for another); block 0 writes the region's header, records and SYNC entries, every block copies its share
 // of the payloads' differing chunks, and the last block of the column writes q's inline all-to-all block. Column

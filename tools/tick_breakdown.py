@@ -10,7 +10,7 @@ rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]
 ticks, cur = [], None
 for r in rows:
     name = r["Kernel_Name"].split("(")[0].replace("swim::", "").replace("void ", "")
-    if name.startswith("k_member_tick"):
+    if name.startswith("k_member_tick") and not name.endswith("<2u>"):  # <2u>: the resume launch of a split tick
         cur = collections.OrderedDict(_start=int(r["Start_Timestamp"]))
         ticks.append(cur)
     if cur is None:
@@ -26,4 +26,10 @@ for t in ticks[-n:]:
     for k, v in t.items():
         if not k.startswith("_"):
             tot[k] += v
-print("mean over the last", min(n, len(ticks)), "ticks:", ", ".join(f"{k} {v / min(n, len(ticks)):.0f}" for k, v in tot.most_common(10)))
+nt = min(n, len(ticks))
+spans = [(t["_end"] - t["_start"]) / 1e3 for t in ticks[-n:]]
+print("mean over the last", nt, "ticks:", ", ".join(f"{k} {v / nt:.0f}" for k, v in tot.most_common(10)))
+if len(sys.argv) > 3:  # every kernel, and the mean span / busy time
+    print(f"mean span {sum(spans) / nt:.1f} us, busy {sum(tot.values()) / nt:.1f} us")
+    for k, v in tot.most_common():
+        print(f"  {k:40s} {v / nt:8.1f}")
