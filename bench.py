@@ -6,9 +6,10 @@ members with full membership views, PRECONVERGED (every row ALIVE inc 0, shuffle
 ClusterConfig (ping 1 s / 500 ms, ping-req 3, gossip 200 ms x fanout 3 x repeat 3, SYNC every 30 s), no loss. One
 "step" = one FD period (pingInterval = 10 ticks of 100 ms) for every member. In this steady state every member pings
 one peer per period, and periodic SYNC / SYNC_ACK anti-entropy streams whole 100k-record payloads against whole
-receiver rows (N/30 syncs per period in each direction), so the dominant kernel is k_sync_diff. It is HBM-bound
-(8 B of algorithmic traffic per record compare: the 4-B record keys of payload and receiver; SURVEY.md
-§8d priced it at 16 B for 8-B keys) with no dense math, so no MFMA.
+receiver rows (N/30 syncs per period in each direction), so the dominant kernel is k_sync_diff. It is HBM-bound with
+no dense math, so no MFMA: on one GPU it compares the 16-bit shadows of the record keys (4 B of algorithmic traffic
+per record compare, payload + receiver; an escaped key past incarnation 16 382 is compared on its 4-B key), on a row
+shard the 4-B keys (8 B per compare; SURVEY.md §8d priced it at 16 B for 8-B keys).
 
 With N=1, all 100k members run on one MI355X (about 206 GB of HBM). With --gpus N under torch.distributed.run, the
 SAME 100k-member cluster is row-sharded: rank r owns observers [r N/W, (r+1) N/W) and its rows (about 206/W GB), the
@@ -18,8 +19,9 @@ scaling is "strong" and `value` is the whole cluster's member·periods/s. torch.
 it broadcasts the RCCL unique id, runs the barriers and takes the max time over ranks.
 
 The JSON line also carries:
-  roofline      k_sync_diff algorithmic bytes (8 B x N per merged payload) / its HIP-event time, against 8 TB/s;
-                traffic = measured HBM bytes per launch from rocprofv3 PMC when available (profiles/), else null.
+  roofline      k_sync_diff algorithmic bytes (the key bytes the engine counts per streamed payload: 4 B or 8 B x N,
+                swim_counters.diff_key_bytes) / its HIP-event time, against 8 TB/s; traffic = measured HBM bytes per
+                launch from a committed rocprofv3 PMC summary when available (profiles/), else null.
   cpu_baseline  the CPU oracle (oracle/swimref.cpp, a port) on a bounded sample: same workload shape at 10k members,
                 timed here on the host on all its cores (worker threads over observer ranges, at most 16) and on one.
 """
@@ -68,7 +70,7 @@ def parse():
 
 def traffic_from_profiles(n_members):
     """HBM bytes per k_sync_diff launch from a committed rocprofv3 PMC summary for this member count, if present."""
-    f = ROOT / "profiles" / "pmc_sync_diff_k32.json"  # measured with the 4-B key plane
+    f = ROOT / "profiles" / "pmc_sync_diff_k16.json"  # measured with the 16-bit shadow key plane
     if not f.exists():
         return None
     try:
@@ -261,18 +263,19 @@ def main():
         merges = d["sync_merges"]
         diff_s = d["diff_ns"] * 1e-9
         launches = max(1, d["diff_launches"])
-        # the engine counts the payloads its timed k_sync_diff launches streamed (every 5th tick on one GPU, every tick
-        # on a row shard); SYNC_ACKs resolved from write logs are not streamed, so they are not priced here
-        timed_msgs = d["diff_msgs"]
-        bytes_per_launch = 8.0 * n * timed_msgs / launches  # payload keys + receiver keys, 4 B each per subject
-        achieved = (8.0 * n * timed_msgs) / diff_s / 1e9 if diff_s > 0 else 0.0
+        # the engine counts the key bytes its timed k_sync_diff launches compared (every 5th tick on one GPU, every
+        # tick on a row shard): 2 x 2 B per subject for a payload streamed from the 16-bit shadow plane, 2 x 4 B for
+        # the others; SYNC_ACKs resolved from write logs are not streamed, so they are not priced here
+        timed_bytes = d["diff_key_bytes"]
+        bytes_per_launch = timed_bytes / launches
+        achieved = timed_bytes / diff_s / 1e9 if diff_s > 0 else 0.0
         # whole-step algorithmic bytes, SURVEY.md §8d with 4-B record keys (B = 8R + 8W + 32M + 0.375G + 24E), with R's
-        # SYNC part priced as the engine reads it: 8 B x N per payload k_sync_diff streamed, and for a SYNC_ACK
-        # resolved from write logs (k_ack_resolve) at most 3 x 16 subjects x 8 B; every other record compare at 8 B.
-        # (R counts the sender's table size per merged payload, N in these preconverged workloads.)
-        streamed, resolved = d["diff_msgs_total"], d["ack_resolved_total"]
+        # SYNC part priced as the engine reads it: the key bytes k_sync_diff compared per streamed payload (above), and
+        # for a SYNC_ACK resolved from write logs (k_ack_resolve) at most 3 x 16 subjects x 8 B; every other record
+        # compare at 8 B. (R counts the sender's table size per merged payload, N in these preconverged workloads.)
+        resolved = d["ack_resolved_total"]
         r_other = max(0, d["record_compares"] - n * merges)
-        B = (8 * n * streamed + 8 * 48 * resolved + 8 * r_other + 8 * d["row_writes"] + 32 * d["messages"]
+        B = (d["diff_key_bytes_total"] + 8 * 48 * resolved + 8 * r_other + 8 * d["row_writes"] + 32 * d["messages"]
              + 0.375 * d["gossip_messages"] + 24 * d["events"])
         line = {
             "metric": "member·periods/sec at 100k members (whole node); achieved HBM GB/s",
@@ -286,8 +289,10 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             # record keys are u32 `inc << 2 | status`: incarnations are capped at 2^30 - 1 (Java int: 2^31 - 1), past
-            # which the engine raises SWIM_ECAPACITY (SEMANTICS.md §8); list entries are u32 member ids
-            "dtype": "u32 (record key inc<<2|status: 30-bit incarnation cap)",
+            # which the engine raises SWIM_ECAPACITY (SEMANTICS.md §8); the diff compares their exact 16-bit shadows
+            # (a key past 0xFFFE escapes to its u32 compare); list entries are u32 member ids
+            "dtype": ("u16 key shadows, exact (u32 record key inc<<2|status: 30-bit incarnation cap)" if world == 1
+                      else "u32 (record key inc<<2|status: 30-bit incarnation cap)"),
             "data": "synthetic (PRECONVERGED full views, seeded Philox selector)",
             "config": {"workload": workload_name(a, n),
                        "members": n, "periods_per_step": 1, "ticks_per_period": ticks_per_period,
@@ -298,7 +303,7 @@ def main():
                          "algorithmic_bytes_per_launch": bytes_per_launch,
                          "avg_launch_us": diff_s * 1e6 / launches,
                          "traffic": traffic_from_profiles(n) if world == 1 else None,
-                         "traffic_source": "committed rocprofv3 PMC summary profiles/pmc_sync_diff_k32.json (FETCH_SIZE x 2 "
+                         "traffic_source": "committed rocprofv3 PMC summary profiles/pmc_sync_diff_k16.json (FETCH_SIZE x 2 "
                                            "+ WRITE_SIZE per launch), not measured in this run"},
             # the engine times a sample of the launches (every 5th tick on one GPU): average x launches per period
             "kernel_time_share": {"k_sync_diff": diff_s / launches * ticks_per_period * a.steps / dt},  # others: profiles/*kernel_stats*
@@ -308,12 +313,13 @@ def main():
             # the difference of two runs of different lengths): read from the committed profiles/, not this run
             "whole_step_pmc_bytes_per_period_committed": whole_step_pmc(a.workload, n) if world == 1 else None,
             "counters": {k: d[k] for k in ("record_compares", "row_writes", "messages", "gossip_messages", "events",
-                                           "sync_merges", "diff_msgs_total", "ack_resolved_total")},
+                                           "sync_merges", "diff_msgs_total", "ack_resolved_total",
+                                           "diff_key_bytes_total")},
             "device_bytes": ctr["device_bytes"],
             # since the handle was created (warm-up included): a profiler pass over the whole process prices its
-            # k_sync_diff traffic against 8 B x N x these merges (tools/make_profiles.py)
+            # k_sync_diff traffic against these key bytes (tools/make_profiles.py)
             "run_totals": {"sync_merges": ctr["sync_merges"], "ack_resolved": ctr.get("ack_resolved_total", 0),
-                           "ticks": ctr["tick"]},
+                           "diff_key_bytes": ctr["diff_key_bytes_total"], "ticks": ctr["tick"]},
             "exchange_ms_per_step": d["exchange_ns"] * 1e-6 / a.steps,
         }
         if a.workload not in ("c3",):  # the gossip plane dominates: whole-step algorithmic bytes against HBM

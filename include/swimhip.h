@@ -155,6 +155,9 @@ typedef struct swim_counters {
   uint64_t ack_resolved; /* SYNC_ACK payloads of those ticks resolved from write logs instead (one GPU; k_ack_resolve) */
   uint64_t ack_resolved_total; /* the same over every tick (payloads streamed = those merged minus these) */
   uint64_t diff_msgs_total;    /* SYNC / SYNC_ACK payloads streamed by every k_sync_diff launch (timed or not) */
+  uint64_t diff_key_bytes;     /* key bytes the timed k_sync_diff launches compared: 2 x 2 B per subject for a payload
+                                  read from the 16-bit key shadow plane (one GPU, live-row payloads), 2 x 4 B otherwise */
+  uint64_t diff_key_bytes_total; /* the same over every k_sync_diff launch */
 } swim_counters;
 
 typedef struct swim_handle swim_handle;

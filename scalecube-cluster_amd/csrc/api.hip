@@ -670,6 +670,8 @@ int build(swim_handle* h) {
   const uint64_t NL = d.NL;  // per-observer arrays: this shard's rows only
   const uint64_t NV = d.implicit ? 1 : NL;  // implicit views: no table or list is stored
   A(d.rowk, NV * d.NS) A(d.rowa, NV * d.NS) A(d.fdl, NV * d.LCAP) A(d.gl, NV * d.LCAP)
+  d.rowk16 = nullptr;  // one GPU, stored tables: the diff's 16-bit shadow plane (SWIM_NO_K16: the diff reads u32 keys)
+  if (d.W == 1 && !d.implicit && !getenv("SWIM_NO_K16")) A(d.rowk16, NV * d.NS)
   A(d.subs, NL * SUBCAP * 4) A(d.paths, NL * d.PCAP * 5) A(d.fetch, NL * d.FCAP * FREC) A(d.groups, NL * d.GRCAP * GREC)
   A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.slow, d.SLOWCAP) A(d.slow_n, 1) A(d.rp, d.RPCAP) A(d.rp_n, 1) A(d.start_tick, N) A(d.jseed_n, N) A(d.jseeds, 16 * N) A(d.md_uidx, N) A(d.mcfg, 4 * N) A(d.md_ver, NL * MDU) A(d.churn_q, 2ull * d.churn) A(d.ucnt, N) A(d.cin, N * d.F) A(d.HB, (uint64_t)d.QW * N) A(d.WB, (uint64_t)d.QW * N) A(d.cev, N * d.F * CEVW)
   A(d.rg, (uint64_t)d.BCAP * N) A(d.rhead, N) A(d.rwin, N) A(d.rseen, N) A(d.rtail, N) A(d.rwl, N) A(d.nrwl, 1)
@@ -2131,6 +2133,11 @@ int swim_counters_get(swim_handle* h, swim_counters* out) {
   out->ack_resolved = c[C_ACKRES];
   out->ack_resolved_total = c[C_ACKRES_ALL];
   out->diff_msgs_total = c[C_DIFFMSG_ALL];
+  // the payloads streamed from the 16-bit shadow plane compared 4 B per subject, the others (C_DIFFWIDE) 8 B
+  const uint64_t nsub = h->d.N;
+  out->diff_key_bytes = nsub * (4 * (c[C_DIFFMSG] - std::min(c[C_DIFFMSG], c[C_DIFFWIDE])) + 8 * c[C_DIFFWIDE]);
+  out->diff_key_bytes_total =
+      nsub * (4 * (c[C_DIFFMSG_ALL] - std::min(c[C_DIFFMSG_ALL], c[C_DIFFWIDE_ALL])) + 8 * c[C_DIFFWIDE_ALL]);
   out->exchange_ns = (uint64_t)(h->xchg_ms * 1e6);
   return SWIM_OK;
 }
@@ -2190,6 +2197,10 @@ int swim_debug_set_incarnation(swim_handle* h, uint32_t m, uint32_t inc) {
   HIPCK(hipMemcpy(&k, w, 4, hipMemcpyDeviceToHost));
   k = (inc << 2) | (k & 3u);
   HIPCK(hipMemcpy(w, &k, 4, hipMemcpyHostToDevice));
+  if (d.rowk16) {
+    const uint16_t k16 = key16(k);
+    HIPCK(hipMemcpy(d.rowk16 + lidx(d, m) * d.NS + m, &k16, 2, hipMemcpyHostToDevice));
+  }
   return SWIM_OK;
 }
 

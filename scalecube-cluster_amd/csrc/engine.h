@@ -88,7 +88,7 @@ constexpr uint32_t XINL = 16384;  // RCCL: bytes per peer moved by the fixed-siz
 // counters (swim_counters order after .tick)
 // 8..12: SWIM_EXP & 4 (and 16..19: the gossip plane's work units per tick, for algorithmic bytes; tools/pmc_gossip.py)
 constexpr uint32_t CSH = 64, CSTRIDE = 64;  // Dev::ctr_sh rows, 512 B apart
-enum Ctr { C_R = 0, C_W, C_M, C_G, C_E, C_LOST, C_GCREATED, C_SYNCMERGE, C_DIFFMSG = 13, C_XU = 16, C_ACKRES = 24, C_ACKRES_ALL = 25, C_DIFFMSG_ALL = 26, C_NCTR = 27 };
+enum Ctr { C_R = 0, C_W, C_M, C_G, C_E, C_LOST, C_GCREATED, C_SYNCMERGE, C_DIFFMSG = 13, C_XU = 16, C_ACKRES = 24, C_ACKRES_ALL = 25, C_DIFFMSG_ALL = 26, C_DIFFWIDE = 27, C_DIFFWIDE_ALL = 28, C_NCTR = 29 };
 
 // capacity fallbacks that fired (include/swimhip_debug.h; counted only when Dev::fb is allocated: SWIM_CAPS or
 // SWIM_FALLBACKS set at create). Each one is an exact slow path taken when a fixed-capacity fast structure is full.
@@ -193,6 +193,8 @@ struct Dev {
   uint64_t* evHash;
 
   uint32_t* rowk;  // [N][NS] key plane: row stride NS = N rounded up to 8 (32-B aligned rows for 16-B loads)
+  uint16_t* rowk16;  // [N][NS] or null: the key plane's 16-bit shadow (key16) that k_sync_diff streams for live-row
+                     // payloads on one GPU (2 B + 2 B per record compare instead of 4 B + 4 B); written with every key
   uint32_t* rowa;  // [N][NS] aux plane
   uint32_t *fdl, *gl;  // [N][LCAP]
 

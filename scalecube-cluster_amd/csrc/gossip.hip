@@ -183,7 +183,12 @@ __device__ __forceinline__ bool replay_pair(const Dev& d, uint32_t x, uint32_t y
   }
   uint32_t del[2][CM];  // arrival ticks of the delivered sends, per direction
   uint32_t nd[2] = {0, 0};
-  for (uint32_t i = 0; i < n; ++i) {
+  // the answer reads only the deliveries y -> x; an x -> y delivery matters only by blocking a later y -> x send, so
+  // the events after the last y -> x one change nothing
+  uint32_t nlast = 0;
+  for (uint32_t i = 0; i < n; ++i)
+    if (ev[i].dir == 0) nlast = i + 1;
+  for (uint32_t i = 0; i < nlast; ++i) {
     const Contact& c = ev[i];
     uint32_t snd = c.dir == 0 ? y : x;
     // the sender held g at that round (its incarnation then), inside its spread window (selectGossipsToSend :246)
@@ -265,6 +270,8 @@ __device__ __forceinline__ bool blocked_pair_cached(const Dev& d, uint32_t x, ui
     relevant |= ((rec[5 + 3 * i] >> 8) & 1u) == 0 && t2 >= born && t2 + d.lat + dmax(d) >= cx;
   }
   if (!relevant) return false;
+  // y never held g up to now: no send y -> x carried it (inc_at of every y -> x event is NEVER)
+  if (!s_ever(s_get(d, g, y, tau + d.lat))) return false;
   Contact ev[CEV];
   uint32_t n = 0;
   for (uint32_t i = 0; i < nall; ++i) {
@@ -312,60 +319,70 @@ __global__ void __launch_bounds__(1024) k_gossip_groups(Dev d) {
 // 2. per member with a gossip round this tick (every member on every shard: the holder state is replicated): where
 // its sweep ends and its window starts in the ring (binary searches: the infection periods are sorted), and whether
 // the round changes anything; the (sender, target) pairs of this shard's targets are counted per target
-__global__ void k_round_plan(Dev d, uint32_t k) {
+__global__ void __launch_bounds__(256) k_round_plan(Dev d, uint32_t k) {
+  __shared__ uint32_t sh[5];
   const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= d.N || !d.tround[m]) return;
-  const uint32_t cnt = d.tcnt[m];
-  for (uint32_t s = 0; s < cnt; ++s) {
-    const uint32_t t = d.T[(size_t)m * d.F + s];
-    if (t >= d.lo && t < d.hi) atomicAdd(&d.tin_cnt[t], 1u);
+  bool listed = false;
+  if (m < d.N && d.tround[m]) {
+    const uint32_t cnt = d.tcnt[m];
+    for (uint32_t s = 0; s < cnt; ++s) {
+      const uint32_t t = d.T[(size_t)m * d.F + s];
+      if (t >= d.lo && t < d.hi) atomicAdd(&d.tin_cnt[t], 1u);
+    }
+    const uint32_t P = d.tperiod[m], sp = d.tspread[m];
+    const int64_t slo = (int64_t)P - (int64_t)sweep_after(sp), wlo = (int64_t)P - (int64_t)sp;
+    const uint32_t h = d.rhead[m], tl = d.rtail[m];
+    const uint32_t* R = ring(d, m);
+    const uint32_t mask = d.BCAP - 1;
+    uint32_t lo = 0, hi = tl - h;  // offsets from h
+    while (lo < hi) {  // first entry not swept: sweepGossips (:283-308) removes infP < P - 2 (spread + 1)
+      const uint32_t mid = lo + (hi - lo) / 2;
+      if (rg_period(R[(h + mid) & mask], P) < slo)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    const uint32_t send = h + lo;
+    hi = tl - h;
+    while (lo < hi) {  // first entry inside the window: selectGossipsToSend (:246) keeps infP + spread >= P
+      const uint32_t mid = lo + (hi - lo) / 2;
+      if (rg_period(R[(h + mid) & mask], P) < wlo)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    const uint32_t wnew = h + lo;
+    listed = send != h || wnew != d.rwin[m] || d.rseen[m] != tl;
+    if (listed) {
+      d.rsend[m] = send;
+      d.rwnew[m] = wnew;
+    }
   }
-  const uint32_t P = d.tperiod[m], sp = d.tspread[m];
-  const int64_t slo = (int64_t)P - (int64_t)sweep_after(sp), wlo = (int64_t)P - (int64_t)sp;
-  const uint32_t h = d.rhead[m], tl = d.rtail[m];
-  const uint32_t* R = ring(d, m);
-  const uint32_t mask = d.BCAP - 1;
-  uint32_t lo = 0, hi = tl - h;  // offsets from h
-  while (lo < hi) {  // first entry not swept: sweepGossips (:283-308) removes infP < P - 2 (spread + 1)
-    const uint32_t mid = lo + (hi - lo) / 2;
-    if (rg_period(R[(h + mid) & mask], P) < slo)
-      lo = mid + 1;
-    else
-      hi = mid;
-  }
-  const uint32_t send = h + lo;
-  hi = tl - h;
-  while (lo < hi) {  // first entry inside the window: selectGossipsToSend (:246) keeps infP + spread >= P
-    const uint32_t mid = lo + (hi - lo) / 2;
-    if (rg_period(R[(h + mid) & mask], P) < wlo)
-      lo = mid + 1;
-    else
-      hi = mid;
-  }
-  const uint32_t wnew = h + lo;
-  if (send != h || wnew != d.rwin[m] || d.rseen[m] != tl) {
-    d.rsend[m] = send;
-    d.rwnew[m] = wnew;
-    d.rwl[wave_append(d.nrwl)] = m;
-  }
+  const uint32_t i = block_reserve(d.nrwl, listed ? 1u : 0u, sh);
+  if (listed) d.rwl[i] = m;
 }
 
 // 3. senders of each target in one contiguous list (counting sort over this tick's pairs); the targets with senders;
 // each target's ring end before this tick's receipts
-__global__ void k_tin_scatter(Dev d) {
+__global__ void __launch_bounds__(256) k_tin_scatter(Dev d) {
+  __shared__ uint32_t sh[5];
   const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= d.N || !d.tround[m]) return;
-  const uint32_t cnt = d.tcnt[m];
-  for (uint32_t s = 0; s < cnt; ++s) {
-    const uint32_t ms = m * d.F + s, t = d.T[ms];
-    if (t < d.lo || t >= d.hi) continue;
-    const uint32_t j = atomicAdd(&d.tin_fill[t], 1u);
-    d.tin[d.tin_off[t] + j] = ms;
-    if (j == 0) {  // one atomic per wave on the list counter (10^4 targets a tick adding one by one serialise on it)
-      d.rt0[t] = d.rtail[t];
-      d.tlist[wave_append(d.ntl)] = t;
+  uint32_t firsts = 0;  // bit s: this member's send s is its target's first this tick (the target is listed)
+  if (m < d.N && d.tround[m]) {
+    const uint32_t cnt = d.tcnt[m];
+    for (uint32_t s = 0; s < cnt; ++s) {
+      const uint32_t ms = m * d.F + s, t = d.T[ms];
+      if (t < d.lo || t >= d.hi) continue;
+      const uint32_t j = atomicAdd(&d.tin_fill[t], 1u);
+      d.tin[d.tin_off[t] + j] = ms;
+      if (j == 0) {
+        d.rt0[t] = d.rtail[t];
+        firsts |= 1u << s;  // gossip_fanout <= 8
+      }
     }
   }
+  uint32_t i = block_reserve(d.ntl, (uint32_t)__popc(firsts), sh);
+  for (; firsts; firsts &= firsts - 1, ++i) d.tlist[i] = d.T[m * d.F + (uint32_t)(__ffs(firsts) - 1)];
 }
 
 // 4. the rounds' holder-state changes (sweepGossips :283-308 and the window of selectGossipsToSend :239-250), a
@@ -492,8 +509,10 @@ __global__ void __launch_bounds__(256) k_round_apply_b(const Dev* __restrict__ d
 }
 
 // 5. contact lists: did target t = T[m][s] choose m in a logged round inside the look-back window? If so, cache the
-// pair's contact events in both directions (independent of the gossip) for blocked_pair_cached. One wave per target
-// of this shard: its lanes read the target's round log once (coalesced) and test every sender of the target against it.
+// pair's contact events in both directions (independent of the gossip) for blocked_pair_cached. Eight lanes per
+// (sender, target) pair of this shard's targets, eight pairs per wave: the lanes read consecutive entries of the
+// target's round log for the sender (a wave per target walked its senders one after another, ~12 targets per wave at
+// C3 with membership evolution; a lane per pair made every load touch 64 lines).
 // The pair's contact events (collect_contacts for x = m, y = t), gathered by one wave: lanes test 64 log entries of
 // one side at a time, a wave prefix sum places the hits, and lane 0 orders them by (tick, side, target slot) as the
 // serial insertion does. n = CEV + 1 on overflow.
@@ -634,30 +653,41 @@ __global__ void __launch_bounds__(256) k_rx_build(const Dev* __restrict__ dp) {
 }
 
 __global__ void __launch_bounds__(256) k_gossip_contacts(Dev d, uint32_t k) {
-  const uint32_t lane = threadIdx.x & 63u, ntl = *d.ntl;
-  for (uint32_t ti = blockIdx.x * 4 + (threadIdx.x >> 6); ti < ntl; ti += gridDim.x * 4) {
-    const uint32_t t = d.tlist[ti], o = d.tin_off[t], ns = d.tin_cnt[t];
-    const uint32_t pos = d.log_pos[t], nlog = min(pos, d.LOGW);
-    for (uint32_t p = 0; p < ns; ++p) {
-      const uint32_t i = d.tin[o + p], m = i / d.F;
+  __shared__ uint32_t sh[5];
+  const uint32_t np = d.tin_off[d.N - 1] + d.tin_cnt[d.N - 1];  // this tick's (sender, target) pairs, by target
+  const uint32_t sub = threadIdx.x & 7u;
+  for (uint32_t j0 = blockIdx.x * 32; j0 < np; j0 += gridDim.x * 32) {  // block-uniform trip count (block_reserve)
+    const uint32_t j = j0 + (threadIdx.x >> 3);
+    uint32_t i = 0;
+    bool hit = false;
+    if (j < np) {
+      i = d.tin[j];
+      const uint32_t m = i / d.F, t = d.T[i];
+      const uint32_t pos = d.log_pos[t], nlog = min(pos, d.LOGW);
       // Only a contact t -> m that arrived after m's window horizon can put t in infectedFrom_m (contact_cache): t's
       // rounds since then, newest first. t logs at most one round per gossip interval, so they are its last R entries.
       const int64_t cut = (int64_t)k - (int64_t)(d.tspread[m] + 1u) * d.gossip_t - d.lat - dmax(d);
       const uint32_t R = min(nlog, d.tspread[m] + 2u + (d.lat + dmax(d) + d.gossip_t - 1u) / d.gossip_t);
-      bool hit = false;
-      for (uint32_t e = lane; e < R && !hit; e += 64) {
+      for (uint32_t e = sub; e < R; e += 8) {
         const size_t lo = (size_t)t * d.LOGW + (pos - 1u - e) % d.LOGW;
         const uint32_t t2 = d.log_tick[lo];
         if (t2 == NEVER || t2 >= k || (int64_t)t2 <= cut) continue;
         const uint32_t n = d.log_cnt[lo];
         for (uint32_t s2 = 0; s2 < n; ++s2) hit |= d.log_tg[lo * d.F + s2] == m;
       }
-      const bool flag = __ballot(hit) != 0ull;
-      if (lane != 0) continue;
-      d.tcontact[i] = flag ? 1u : 0u;
-      d.cin[i] = NEVER;
-      if (flag) d.cfl[atomicAdd(d.ncfl, 1u)] = i;  // its contact events are cached by k_contact_cache
     }
+    // the pair's eight lanes
+    uint32_t h = hit ? 1u : 0u;
+    h |= __shfl_xor(h, 1);
+    h |= __shfl_xor(h, 2);
+    h |= __shfl_xor(h, 4);
+    const bool lead = j < np && sub == 0;
+    if (lead) {
+      d.tcontact[i] = h;
+      d.cin[i] = NEVER;
+    }
+    const uint32_t c = block_reserve(d.ncfl, lead && h ? 1u : 0u, sh);
+    if (lead && h) d.cfl[c] = i;  // its contact events are cached by k_contact_cache
   }
 }
 

@@ -79,6 +79,7 @@ __global__ void k_init_rows(Dev d) {
       const uint64_t v = s >= d.N ? 0ull : (d.init_mode == 1 || m == s) ? full : 0ull;
       rk[s] = key32(v);
       ra[s] = aux32(v);
+      if (d.rowk16) d.rowk16[(size_t)li * d.NS + s] = key16(key32(v));
     }
     if (d.W > 1)  // dirty chunks against base_row: none for a PRECONVERGED row, the own chunk for a cold join
       for (uint32_t w = threadIdx.x; w < d.MW; w += blockDim.x)
@@ -131,7 +132,7 @@ __global__ void k_scatter_rc(const Dev d, const uint64_t* raw, const uint32_t* n
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     uint32_t t = (uint32_t)(raw[i] >> 32), g = (uint32_t)raw[i];
     const uint32_t f = atomicAdd(&fill[t], 1u);
-    if (f == 1u) d.sg_list[atomicAdd(d.nsg, 1u)] = t;  // a segment with two receipts or more: k_seg_sort sorts it
+    if (f == 1u) d.sg_list[wave_append(d.nsg)] = t;  // a segment with two receipts or more: k_seg_sort sorts it
     uint32_t p = off[t] + f;
     idx[p] = g;
     key[p] = d.slot_gid[g];
@@ -297,24 +298,43 @@ __global__ void __launch_bounds__(256) k_seg_sort(uint64_t* key, uint32_t* val, 
 // k_sync_diff: for every SYNC / SYNC_ACK sent in tick k-1, stream the payload's key plane (the sender's live row,
 // or its copy-on-write snapshot) against the receiver's key plane and extract, per 2048-subject chunk and in
 // subject order, the records that differ (the eager `!r1.equals(table.get(id))` filter of syncMembership,
-// :456-467). This is the HBM-bound hot loop: 2 x 4 B read per subject per merge (key32, swim_common.h). SHARDED adds
-// payloads received from other shards (baseline row + shipped chunks); the single-GPU instance has only local rows
-// and snapshots.
-// this lane's 8 payload keys and 8 receiver keys of work item w (message w / NCHUNK, chunk w % NCHUNK): the payload
+// :456-467). This is the HBM-bound hot loop: 2 x 2 B read per subject per merge on one GPU (the keys' 16-bit
+// shadows, key16; an escaped key is compared on its 4-B key32), 2 x 4 B on a row shard. SHARDED adds payloads
+// received from other shards (baseline row + shipped chunks); the single-GPU instance has only local rows and
+// snapshots.
+// this lane's 8 payload keys and 8 receiver keys of chunk c of message mi: the payload
 // is the sender's live row or its copy-on-write snapshot; for a payload received from another shard, the shipped
 // chunk if it differs from the baseline, else the baseline
 // pinw: the arena row a live-row payload is copied into while it streams (pin_msg), else NEVER; loaded here with the
 // item's data so that no dependent load of the message waits at the top of the item's iteration
+// narrow (one GPU, a live-row payload that is not pinned): the item is chunks c and c + 1 of the message, and x holds
+// the 16-bit shadow keys (key16) of payload and receiver for both, x[2 h] / x[2 h + 1] for chunk c + h: the same 64 B
+// per lane in flight as one chunk of 4-B keys. Every lane of the block takes the same item, so the mode is uniform.
 template <bool SHARDED>
 __device__ __forceinline__ void diff_fetch(const Dev& d, uint32_t b, uint32_t mi, uint32_t c, uint4 (&x)[4],
-                                           uint32_t& pinw) {
+                                           uint32_t& pinw, bool& narrow) {
   const SyncMsg& mm = d.msgs[b][mi];
   const uint32_t s0 = c * CH + threadIdx.x * 8;
   pinw = NEVER;
+  narrow = false;
   // NS is a multiple of 8: a 32-B group is wholly in or out; padding entries are 0 (absent). A delayed message
   // (KF_DEFER) is merged in a later tick: nothing to compare now
   if (s0 >= d.NS || (mm.kind & KF_DEFER)) {
     x[0] = x[1] = x[2] = x[3] = make_uint4(0, 0, 0, 0);
+    return;
+  }
+  if (!SHARDED && d.rowk16 && mm.payload == NEVER && mm.pin == NEVER) {
+    narrow = true;
+    const uint16_t* p16 = d.rowk16 + lidx(d, mm.src) * d.NS + s0;
+    const uint16_t* r16 = d.rowk16 + lidx(d, mm.dst) * d.NS + s0;
+    x[0] = ld_c4((const uint32_t*)p16);
+    x[1] = ld_c4((const uint32_t*)r16);
+    if (s0 + CH < d.NS) {
+      x[2] = ld_c4((const uint32_t*)(p16 + CH));
+      x[3] = ld_c4((const uint32_t*)(r16 + CH));
+    } else {
+      x[2] = x[3] = make_uint4(0, 0, 0, 0);
+    }
     return;
   }
   const uint32_t* p8;
@@ -342,106 +362,152 @@ __device__ __forceinline__ void diff_fetch(const Dev& d, uint32_t b, uint32_t mi
   x[3] = ld_c4(r8 + 4);
 }
 
-// k_sync_diff: for every SYNC / SYNC_ACK sent in tick k-1, stream the payload's key plane (the sender's live row,
-// or its copy-on-write snapshot) against the receiver's key plane and extract, per 2048-subject chunk and in
-// subject order, the records that differ (the eager `!r1.equals(table.get(id))` filter of syncMembership,
-// :456-467). This is the HBM-bound hot loop: 2 x 4 B read per subject per merge (key32, swim_common.h). Each block
-// walks its work items grid-strided with the next item's loads in flight while it tests the current one. SHARDED
-// adds payloads received from other shards (baseline row + shipped chunks); the single-GPU instance has only local
-// rows and snapshots.
-// the items of `nmsg` messages (list[j], or j itself without a list) over the blocks blk of nblk, grid-stride, with
-// the next item's loads in flight while the current one is tested
+// chunk c of message mi against this lane's 8 payload keys p and receiver keys r (s0: its first subject): the
+// differing records in subject order into the candidate pool, the chunk's (offset, count) into chunk_meta
+__device__ __forceinline__ void diff_chunk(const Dev& d, uint32_t b, uint32_t mi, uint32_t c, uint32_t s0,
+                                           const uint32_t (&p)[8], const uint32_t (&r)[8], uint32_t* scan,
+                                           uint32_t& base) {
+  const bool dl = d.ackres != 0;
+  uint32_t mask = 0, ab = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if ((p[j] & 3u) != ST_ABSENT && p[j] != r[j]) mask |= 1u << j;
+    ab |= (uint32_t)((p[j] & 3u) == ST_ABSENT && (r[j] & 3u) != ST_ABSENT);
+  }
+  uint32_t nc = __popc(mask);
+  if (!__syncthreads_or(nc | ab)) {  // steady state: the whole 2048-subject chunk matches
+    if (threadIdx.x == 0) {
+      uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NCHUNK + c) * 2;
+      cm[0] = 0;
+      cm[1] = 0;
+    }
+    return;
+  }
+  if (dl && ab) atomicOr(&d.msgs[b][mi].kind, KF_ABS);  // (rare: a record the payload lacks)
+  scan[threadIdx.x] = nc;
+  __syncthreads();
+  for (uint32_t o = 1; o < 256; o <<= 1) {
+    uint32_t v = threadIdx.x >= o ? scan[threadIdx.x - o] : 0;
+    __syncthreads();
+    scan[threadIdx.x] += v;
+    __syncthreads();
+  }
+  uint32_t incl = scan[threadIdx.x];
+  uint32_t totc = scan[255];
+  if (threadIdx.x == 0) {
+    uint32_t bo = atomicAdd(d.pool_used, totc);
+    if (bo + totc > d.POOLCAP) {  // no room: nothing of this chunk is written (the error aborts the step)
+      atomicOr(d.err, E_POOL);
+      totc = 0;
+      bo = NEVER;
+    }
+    base = bo;
+    uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NCHUNK + c) * 2;
+    cm[0] = bo;
+    cm[1] = totc;
+    if (totc) atomicAdd(&d.msgs[b][mi].ncand, totc);
+  }
+  __syncthreads();
+  uint32_t o = base + incl - nc;
+  if (base != NEVER)  // (an overflowed chunk must not overwrite other chunks' candidates)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (mask & (1u << j)) d.pool[o++] = ((uint64_t)(s0 + j) << 34) | key34(p[j]);
+  __syncthreads();
+}
+
+// this lane's 8 keys of chunk c + h from a narrow item (16-bit shadows in x[2h], x[2h + 1]); an escaped shadow makes
+// the lane read its 8 full keys of both rows (an incarnation past 16 382 among them)
+__device__ __forceinline__ void narrow_keys(const Dev& d, uint32_t b, uint32_t mi, uint32_t s0, const uint4& xp,
+                                            const uint4& xr, uint32_t (&p)[8], uint32_t (&r)[8]) {
+  const uint32_t pw[4] = {xp.x, xp.y, xp.z, xp.w}, rw[4] = {xr.x, xr.y, xr.z, xr.w};
+  bool esc = false;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    p[j] = (pw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+    r[j] = (rw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+    esc |= p[j] == 0xFFFFu || r[j] == 0xFFFFu;
+  }
+  if (esc && s0 < d.NS) {
+    const SyncMsg& mm = d.msgs[b][mi];
+    const uint32_t* p8 = d.rowk + lidx(d, mm.src) * d.NS + s0;
+    const uint32_t* r8 = d.rowk + lidx(d, mm.dst) * d.NS + s0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      p[j] = p8[j];
+      r[j] = r8[j];
+    }
+  }
+}
+
+// k_sync_diff's work: the items of `nmsg` messages (list[j], or j itself without a list) over the blocks blk of nblk,
+// grid-stride, with the next item's loads in flight while the current one is tested. An item is PER chunks of a
+// message (2 on one GPU: a narrow item's 16-bit keys; a wide item's second chunk is loaded when the first is done)
 template <bool SHARDED>
 __device__ __forceinline__ void stream_list(const Dev& d, uint32_t b, const uint32_t* dlp, uint32_t nmsg, uint32_t blk,
-                                            uint32_t nblk, uint32_t* scan, uint32_t& base) {
-  const bool dl = d.ackres != 0;
-  const uint32_t total = nmsg * d.NCHUNK;
-  const uint32_t nch = d.NCHUNK;
+                                            uint32_t nblk, uint32_t* scan, uint32_t& base, uint32_t timed) {
+  constexpr uint32_t PER = SHARDED ? 1u : 2u;
+  const uint32_t nch = d.NCHUNK, nit = (nch + PER - 1) / PER;
+  const uint32_t total = nmsg * nit;
   uint4 cur[4];
   uint32_t mcur = 0, pcur = NEVER;
+  bool ncur = false;
   if (blk < total) {
-    mcur = dlp ? dlp[blk / nch] : blk / nch;
-    diff_fetch<SHARDED>(d, b, mcur, blk % nch, cur, pcur);
+    mcur = dlp ? dlp[blk / nit] : blk / nit;
+    diff_fetch<SHARDED>(d, b, mcur, (blk % nit) * PER, cur, pcur, ncur);
   }
   for (uint32_t w = blk; w < total; w += nblk) {
     uint4 nxt[4];
     uint32_t mnxt = 0, pnxt = NEVER;
+    bool nnxt = false;
     if (w + nblk < total) {
-      mnxt = dlp ? dlp[(w + nblk) / nch] : (w + nblk) / nch;
-      diff_fetch<SHARDED>(d, b, mnxt, (w + nblk) % nch, nxt, pnxt);
+      mnxt = dlp ? dlp[(w + nblk) / nit] : (w + nblk) / nit;
+      diff_fetch<SHARDED>(d, b, mnxt, ((w + nblk) % nit) * PER, nxt, pnxt, nnxt);
     }
-    const uint32_t mi = mcur, c = w % nch;
-    const uint32_t s0 = c * CH + threadIdx.x * 8;
-    const uint32_t pin = pcur;
-    if (pin != NEVER && s0 < d.NS) {  // a live-row payload read again later (pin_msg)
-      uint4* dst = (uint4*)(d.arena[b] + (size_t)pin * d.NS + s0);
-      dst[0] = cur[0];
-      dst[1] = cur[1];
+    const uint32_t mi = mcur, c0 = (w % nit) * PER;
+    if (!SHARDED && !ncur && c0 == 0 && threadIdx.x == 0 && d.rowk16) {  // priced at 8 B per subject (swim_counters)
+      atomicAdd(&d.ctr[C_DIFFWIDE_ALL], 1ull);
+      if (timed) atomicAdd(&d.ctr[C_DIFFWIDE], 1ull);
     }
-    const uint32_t p[8] = {cur[0].x, cur[0].y, cur[0].z, cur[0].w, cur[1].x, cur[1].y, cur[1].z, cur[1].w};
-    const uint32_t r[8] = {cur[2].x, cur[2].y, cur[2].z, cur[2].w, cur[3].x, cur[3].y, cur[3].z, cur[3].w};
-    uint32_t mask = 0, ab = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if ((p[j] & 3u) != ST_ABSENT && p[j] != r[j]) mask |= 1u << j;
-      ab |= (uint32_t)((p[j] & 3u) == ST_ABSENT && (r[j] & 3u) != ST_ABSENT);
-    }
-    uint32_t nc = __popc(mask);
-    if (!__syncthreads_or(nc | ab)) {  // steady state: the whole 2048-subject item matches
-      if (threadIdx.x == 0) {
-        uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NCHUNK + c) * 2;
-        cm[0] = 0;
-        cm[1] = 0;
-      }
-    } else {
-      if (dl && ab) atomicOr(&d.msgs[b][mi].kind, KF_ABS);  // (rare: a record the payload lacks)
-      scan[threadIdx.x] = nc;
-      __syncthreads();
-      for (uint32_t o = 1; o < 256; o <<= 1) {
-        uint32_t v = threadIdx.x >= o ? scan[threadIdx.x - o] : 0;
-        __syncthreads();
-        scan[threadIdx.x] += v;
-        __syncthreads();
-      }
-      uint32_t incl = scan[threadIdx.x];
-      uint32_t totc = scan[255];
-      if (threadIdx.x == 0) {
-        uint32_t bo = atomicAdd(d.pool_used, totc);
-        if (bo + totc > d.POOLCAP) {  // no room: nothing of this item is written (the error aborts the step)
-          atomicOr(d.err, E_POOL);
-          totc = 0;
-          bo = NEVER;
+    for (uint32_t h = 0; h < PER; ++h) {
+      const uint32_t c = c0 + h;
+      if (c >= nch) break;  // (block-uniform)
+      const uint32_t s0 = c * CH + threadIdx.x * 8;
+      uint32_t p[8], r[8];
+      if (ncur) {
+        narrow_keys(d, b, mi, s0, cur[2 * h], cur[2 * h + 1], p, r);
+      } else {
+        if (h > 0) {  // a wide item's later chunk
+          bool nw;
+          diff_fetch<SHARDED>(d, b, mi, c, cur, pcur, nw);
         }
-        base = bo;
-        uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NCHUNK + c) * 2;
-        cm[0] = bo;
-        cm[1] = totc;
-        if (totc) atomicAdd(&d.msgs[b][mi].ncand, totc);
-      }
-      __syncthreads();
-      uint32_t o = base + incl - nc;
-      if (base != NEVER)  // (an overflowed item must not overwrite other items' candidates)
+        if (pcur != NEVER && s0 < d.NS) {  // a live-row payload read again later (pin_msg)
+          uint4* dst = (uint4*)(d.arena[b] + (size_t)pcur * d.NS + s0);
+          dst[0] = cur[0];
+          dst[1] = cur[1];
+        }
+        const uint32_t pv[8] = {cur[0].x, cur[0].y, cur[0].z, cur[0].w, cur[1].x, cur[1].y, cur[1].z, cur[1].w};
+        const uint32_t rv[8] = {cur[2].x, cur[2].y, cur[2].z, cur[2].w, cur[3].x, cur[3].y, cur[3].z, cur[3].w};
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (mask & (1u << j)) d.pool[o++] = ((uint64_t)(s0 + j) << 34) | key34(p[j]);
-      __syncthreads();
+        for (int j = 0; j < 8; ++j) {
+          p[j] = pv[j];
+          r[j] = rv[j];
+        }
+      }
+      diff_chunk(d, b, mi, c, s0, p, r, scan, base);
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
     mcur = mnxt;
     pcur = pnxt;
+    ncur = nnxt;
   }
 }
 
-// k_sync_diff: for every SYNC / SYNC_ACK sent in tick k-1, stream the payload's key plane (the sender's live row,
-// or its copy-on-write snapshot) against the receiver's key plane and extract, per 2048-subject chunk and in
-// subject order, the records that differ (the eager `!r1.equals(table.get(id))` filter of syncMembership,
-// :456-467). This is the HBM-bound hot loop: 2 x 4 B read per subject per merge (key32, swim_common.h). Each block
-// walks its work items grid-stride with the next item's loads in flight while it tests the current one. SHARDED
-// adds payloads received from other shards (baseline row + shipped chunks); the single-GPU instance has only local
-// rows and snapshots.
+// k_sync_diff: the diff of every payload streamed this tick (see diff_fetch and stream_list above)
 template <bool SHARDED>
-__global__ void __launch_bounds__(256) k_sync_diff(const Dev* __restrict__ dp, uint32_t b, uint32_t timed, uint32_t spec) {
+__global__ void __launch_bounds__(256, 8) k_sync_diff(const Dev* __restrict__ dp, uint32_t b, uint32_t timed, uint32_t spec) {
   const Dev& d = *dp;  // global, not kernarg (as k_member_tick): a by-value Dev of this size was copied to scratch
   if (spec && *(volatile uint32_t*)d.halt) return;  // a speculative batch halted at an earlier tick
   __shared__ uint32_t scan[256];
@@ -455,8 +521,12 @@ __global__ void __launch_bounds__(256) k_sync_diff(const Dev* __restrict__ dp, u
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     atomicAdd(&d.ctr[C_DIFFMSG_ALL], (unsigned long long)nmsg);
     if (timed) atomicAdd(&d.ctr[C_DIFFMSG], (unsigned long long)nmsg);
+    if (SHARDED || !d.rowk16) {  // every payload compared on 4-B keys
+      atomicAdd(&d.ctr[C_DIFFWIDE_ALL], (unsigned long long)nmsg);
+      if (timed) atomicAdd(&d.ctr[C_DIFFWIDE], (unsigned long long)nmsg);
+    }
   }
-  stream_list<SHARDED>(d, b, dl ? d.dlist : nullptr, nmsg, blockIdx.x, gridDim.x, scan, base);
+  stream_list<SHARDED>(d, b, dl ? d.dlist : nullptr, nmsg, blockIdx.x, gridDim.x, scan, base, timed);
 }
 
 // ------------------------------------------------------------------------------------------------------------

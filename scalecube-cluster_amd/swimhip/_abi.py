@@ -106,6 +106,8 @@ class SwimCounters(C.Structure):
         ("ack_resolved", C.c_uint64),
         ("ack_resolved_total", C.c_uint64),
         ("diff_msgs_total", C.c_uint64),
+        ("diff_key_bytes", C.c_uint64),
+        ("diff_key_bytes_total", C.c_uint64),
     ]
 
     def as_dict(self):

@@ -6,6 +6,9 @@
 #   benchcpu          the default bench line with its CPU baseline (the driver's command)
 #   trace:W[:S[:WU]]  rocprofv3 kernel trace + stats of the same bench command, and its per-tick breakdown
 #   pmc:W:COUNTER[:S] one rocprofv3 --pmc pass (one counter) over a bench run of workload W with S steps (default 3)
+#   pmcg:W[:S[:WU]]   the gossip plane's HBM bytes and L2 atomics per kernel and tick: FETCH_SIZE, WRITE_SIZE and
+#                     TCC_ATOMIC_sum passes + a SWIM_EXP=4 work-unit run of the same command (tools/pmc_gossip.py);
+#                     run a trace:W step with the same S / WU first for the kernel times
 #   rehearse:R:N[:W]  bench.py --gpus R on this one GPU (R ranks over RCCL sockets), N members, workload W (default c3)
 #   c4:N              the C4 schedule at N members (tools/exp_c4.py: partition, unblockAll at period 200, run to 320)
 #   c5m               rank 0 of 8 C5 slot shards at 10^6 members alone (bench.py --rehearse-shard 8), default caps
@@ -54,6 +57,16 @@ for step in "$@"; do
     pmc)
       timeout -s KILL 300 rocprofv3 --pmc $b -d $O/pmc_${a}_${b}_${c:-3} -o run --output-format csv -- \
         python3 bench.py --workload $a --steps ${c:-3} --warmup 1 --no-cpu-baseline > $O/pmc_${a}_${b}_${c:-3}.log 2>&1
+      ;;
+    pmcg)
+      for ctr in FETCH_SIZE WRITE_SIZE TCC_ATOMIC_sum; do
+        timeout -s KILL 300 rocprofv3 --pmc $ctr -d $O/pmc_${a}_$ctr -o run --output-format csv -- \
+          python3 bench.py --workload $a --steps ${b:-2} --warmup ${c:-12} --no-cpu-baseline > $O/pmc_${a}_$ctr.log 2>&1
+      done
+      SWIM_EXP=4 timeout -k 10 300 python3 bench.py --workload $a --steps ${b:-2} --warmup ${c:-12} --no-cpu-baseline \
+        > $O/exp4_$a.log 2>&1
+      python3 tools/pmc_gossip.py $O $a $((${b:-2} * 10)) $O/pmc_gossip_$a.json > /dev/null
+      python3 -c "import json; d = json.load(open('$O/pmc_gossip_$a.json')); print({k: d.get(k) for k in ('gossip_plane_hbm_bytes_per_tick', 'algorithmic_bytes_per_tick', 'wasted_traffic_ratio')})"
       ;;
     rehearse)
       timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node $a --master-addr 127.0.0.1 \

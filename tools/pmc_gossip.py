@@ -1,7 +1,9 @@
 """Per-tick HBM bytes and L2 atomics of the gossip data plane from three rocprofv3 --pmc passes (FETCH_SIZE with the
 gfx950 x2 correction, WRITE_SIZE, TCC_ATOMIC_sum; MI355X_MICROARCH.md HBM section), averaged over the last <timed ticks>
 member-kernel dispatches (= ticks) and the dispatches after the first of them. Usage: python tools/pmc_gossip.py <dir> <workload> <timed ticks> [out.json]
-<dir> holds pmc_<workload>_<counter>/run_counter_collection.csv"""
+<dir> holds pmc_<workload>_<counter>/run_counter_collection.csv (tools/gpu_run.sh step pmcg), exp4_<workload>.log and
+t_<workload>/run_kernel_stats.csv. A tick starts at each k_member_tick dispatch that is not the resume launch of a split
+tick (k_member_tick_t<2u>)."""
 import csv
 import json
 import sys
@@ -12,8 +14,10 @@ def per_kernel(path, last):
     """counter sums per kernel over the dispatches of the last `last` ticks (the timed periods of the bench run)"""
     rows = list(csv.DictReader(open(path)))
     for r in rows:
-        r["name"] = r["Kernel_Name"].split("(")[0].replace("swim::", "").replace("void ", "").split("<")[0]
-    ticks = sorted({int(r["Dispatch_Id"]) for r in rows if r["name"] == "k_member_tick"})
+        full = r["Kernel_Name"].split("(")[0].replace("swim::", "").replace("void ", "")
+        r["name"] = full.split("<")[0]
+        r["tick"] = full.startswith("k_member_tick") and not full.endswith("<2u>")
+    ticks = sorted({int(r["Dispatch_Id"]) for r in rows if r["tick"]})
     first = ticks[-last] if last and len(ticks) >= last else 0
     tot, disp = defaultdict(float), defaultdict(set)
     for r in rows:
@@ -21,7 +25,9 @@ def per_kernel(path, last):
             continue
         tot[r["name"]] += float(r["Counter_Value"])
         disp[r["name"]].add(r["Dispatch_Id"])
-    return tot, {k: len(v) for k, v in disp.items()}
+    nd = {k: len(v) for k, v in disp.items()}
+    nd["_ticks"] = len([t for t in ticks if t >= first])
+    return tot, nd
 
 
 def main():
@@ -32,14 +38,14 @@ def main():
         at, _ = per_kernel(f"{d}/pmc_{w}_TCC_ATOMIC_sum/run_counter_collection.csv", last)
     except FileNotFoundError:
         at = {}
-    ticks = nd.get("k_member_tick", 1)
+    ticks = max(1, nd.pop("_ticks"))
     out = {"ticks": ticks, "kernels": {}}
     for k in sorted(f, key=lambda k: -(2 * f[k] + wr.get(k, 0))):
         out["kernels"][k] = {"dispatches": nd[k], "hbm_bytes_per_tick": (2 * f[k] + wr.get(k, 0)) * 1024 / ticks,
                              "fetch_bytes_per_tick_x2": 2 * f[k] * 1024 / ticks,
                              "write_bytes_per_tick": wr.get(k, 0) * 1024 / ticks,
                              "l2_atomics_per_tick": at.get(k, 0) / ticks}
-    gk = [k for k in out["kernels"] if k != "k_member_tick"]
+    gk = [k for k in out["kernels"] if not k.startswith("k_member_tick") and k != "k_inbox_apply"]
     out["gossip_plane_hbm_bytes_per_tick"] = sum(out["kernels"][k]["hbm_bytes_per_tick"] for k in gk)
     out["gossip_plane_l2_atomics_per_tick"] = sum(out["kernels"][k]["l2_atomics_per_tick"] for k in gk)
     # the same ticks' op counters from the bench line of the FETCH_SIZE pass: SURVEY.md §8d algorithmic bytes
@@ -71,7 +77,7 @@ def main():
     except FileNotFoundError:
         pass
     try:
-        for r in csv.DictReader(open(f"{d}/trace_{w}/run_kernel_stats.csv")):
+        for r in csv.DictReader(open(f"{d}/t_{w}/run_kernel_stats.csv")):
             k = r["Name"].split("(")[0].replace("swim::", "").replace("void ", "").split("<")[0]
             if k in out["kernels"]:
                 us = float(r["AverageNs"]) / 1e3
