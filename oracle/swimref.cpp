@@ -1295,6 +1295,13 @@ __attribute__((visibility("default"))) int swim_update_incarnation(swim_handle* 
   h->sim.members[m].pendingInc++;
   return SWIM_OK;
 }
+// include/swimhip_debug.h: member m's own record at incarnation inc (the engine's limit: 2^30)
+__attribute__((visibility("default"))) int swim_debug_set_incarnation(swim_handle* h, uint32_t m, uint32_t inc) {
+  if (!h || m >= h->sim.N) return SWIM_EINVAL;
+  if (inc >= (1u << 30)) return SWIM_ECAPACITY;
+  h->sim.members[m].table[m].inc = inc;
+  return SWIM_OK;
+}
 __attribute__((visibility("default"))) int swim_update_metadata(swim_handle* h, uint32_t m) {
   if (!h || m >= h->sim.N || !h->sim.members[m].alive) return SWIM_EINVAL;
   h->sim.md_version[m]++;  // MetadataStoreImpl.updateMetadata (:111-132), effective for the next response

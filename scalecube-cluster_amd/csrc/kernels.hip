@@ -307,34 +307,33 @@ __global__ void __launch_bounds__(256) k_seg_sort(uint64_t* key, uint32_t* val, 
 // chunk if it differs from the baseline, else the baseline
 // pinw: the arena row a live-row payload is copied into while it streams (pin_msg), else NEVER; loaded here with the
 // item's data so that no dependent load of the message waits at the top of the item's iteration
-// narrow (one GPU, a live-row payload that is not pinned): the item is chunks c and c + 1 of the message, and x holds
-// the 16-bit shadow keys (key16) of payload and receiver for both, x[2 h] / x[2 h + 1] for chunk c + h: the same 64 B
-// per lane in flight as one chunk of 4-B keys. Every lane of the block takes the same item, so the mode is uniform.
+// narrow (one GPU, a live-row payload that is not pinned): the item is chunks c and c + 1 of the message, lane i
+// the 16 subjects c CH + 16 i ..., and x holds their 16-bit shadow keys (key16): payload x[0..1], receiver x[2..3],
+// the same 64 B per lane in flight as one chunk of 4-B keys. Every lane of the block takes the same item, so the mode
+// is uniform.
 template <bool SHARDED>
 __device__ __forceinline__ void diff_fetch(const Dev& d, uint32_t b, uint32_t mi, uint32_t c, uint4 (&x)[4],
                                            uint32_t& pinw, bool& narrow) {
   const SyncMsg& mm = d.msgs[b][mi];
-  const uint32_t s0 = c * CH + threadIdx.x * 8;
   pinw = NEVER;
   narrow = false;
+  if (!SHARDED && d.rowk16 && mm.payload == NEVER && mm.pin == NEVER && !(mm.kind & KF_DEFER)) {
+    narrow = true;
+    const uint32_t n0 = c * CH + threadIdx.x * 16;  // NS is a multiple of 8: 8-subject groups are wholly in or out
+    const uint16_t* p16 = d.rowk16 + lidx(d, mm.src) * d.NS + n0;
+    const uint16_t* r16 = d.rowk16 + lidx(d, mm.dst) * d.NS + n0;
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    x[0] = n0 < d.NS ? ld_c4((const uint32_t*)p16) : z;
+    x[1] = n0 + 8 < d.NS ? ld_c4((const uint32_t*)(p16 + 8)) : z;
+    x[2] = n0 < d.NS ? ld_c4((const uint32_t*)r16) : z;
+    x[3] = n0 + 8 < d.NS ? ld_c4((const uint32_t*)(r16 + 8)) : z;
+    return;
+  }
+  const uint32_t s0 = c * CH + threadIdx.x * 8;
   // NS is a multiple of 8: a 32-B group is wholly in or out; padding entries are 0 (absent). A delayed message
   // (KF_DEFER) is merged in a later tick: nothing to compare now
   if (s0 >= d.NS || (mm.kind & KF_DEFER)) {
     x[0] = x[1] = x[2] = x[3] = make_uint4(0, 0, 0, 0);
-    return;
-  }
-  if (!SHARDED && d.rowk16 && mm.payload == NEVER && mm.pin == NEVER) {
-    narrow = true;
-    const uint16_t* p16 = d.rowk16 + lidx(d, mm.src) * d.NS + s0;
-    const uint16_t* r16 = d.rowk16 + lidx(d, mm.dst) * d.NS + s0;
-    x[0] = ld_c4((const uint32_t*)p16);
-    x[1] = ld_c4((const uint32_t*)r16);
-    if (s0 + CH < d.NS) {
-      x[2] = ld_c4((const uint32_t*)(p16 + CH));
-      x[3] = ld_c4((const uint32_t*)(r16 + CH));
-    } else {
-      x[2] = x[3] = make_uint4(0, 0, 0, 0);
-    }
     return;
   }
   const uint32_t* p8;
@@ -416,28 +415,89 @@ __device__ __forceinline__ void diff_chunk(const Dev& d, uint32_t b, uint32_t mi
   __syncthreads();
 }
 
-// this lane's 8 keys of chunk c + h from a narrow item (16-bit shadows in x[2h], x[2h + 1]); an escaped shadow makes
-// the lane read its 8 full keys of both rows (an incarnation past 16 382 among them)
-__device__ __forceinline__ void narrow_keys(const Dev& d, uint32_t b, uint32_t mi, uint32_t s0, const uint4& xp,
-                                            const uint4& xr, uint32_t (&p)[8], uint32_t (&r)[8]) {
-  const uint32_t pw[4] = {xp.x, xp.y, xp.z, xp.w}, rw[4] = {xr.x, xr.y, xr.z, xr.w};
+// a narrow item: chunks c and c + 1 of message mi in one pass (lanes 0-127 chunk c, 128-255 chunk c + 1, 16
+// subjects each from x), one block barrier for both; the candidates of both chunks in subject order from one pool
+// reservation. A lane with an escaped shadow (0xFFFF: an incarnation past 16 382 among its subjects) compares its 16
+// full keys of both rows instead.
+__device__ __forceinline__ void diff_pair16(const Dev& d, uint32_t b, uint32_t mi, uint32_t c, const uint4 (&x)[4],
+                                            uint32_t* scan, uint32_t& base) {
+  const bool dl = d.ackres != 0;
+  const uint32_t n0 = c * CH + threadIdx.x * 16, nch = d.NCHUNK;
+  const uint32_t pw[8] = {x[0].x, x[0].y, x[0].z, x[0].w, x[1].x, x[1].y, x[1].z, x[1].w};
+  const uint32_t rw[8] = {x[2].x, x[2].y, x[2].z, x[2].w, x[3].x, x[3].y, x[3].z, x[3].w};
+  uint32_t mask = 0, ab = 0;
   bool esc = false;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    p[j] = (pw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-    r[j] = (rw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-    esc |= p[j] == 0xFFFFu || r[j] == 0xFFFFu;
-  }
-  if (esc && s0 < d.NS) {
+  for (int q = 0; q < 8; ++q)
+    esc |= (pw[q] & 0xFFFFu) == 0xFFFFu || (pw[q] >> 16) == 0xFFFFu || (rw[q] & 0xFFFFu) == 0xFFFFu ||
+           (rw[q] >> 16) == 0xFFFFu;
+  const uint32_t *pk = nullptr, *rk = nullptr;
+  if (esc) {
     const SyncMsg& mm = d.msgs[b][mi];
-    const uint32_t* p8 = d.rowk + lidx(d, mm.src) * d.NS + s0;
-    const uint32_t* r8 = d.rowk + lidx(d, mm.dst) * d.NS + s0;
+    pk = d.rowk + lidx(d, mm.src) * d.NS + n0;
+    rk = d.rowk + lidx(d, mm.dst) * d.NS + n0;
+#pragma unroll 1
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t p = n0 + j < d.NS ? pk[j] : 0u, r = n0 + j < d.NS ? rk[j] : 0u;
+      if ((p & 3u) != ST_ABSENT && p != r) mask |= 1u << j;
+      ab |= (uint32_t)((p & 3u) == ST_ABSENT && (r & 3u) != ST_ABSENT);
+    }
+  } else {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      p[j] = p8[j];
-      r[j] = r8[j];
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t p = (pw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu, r = (rw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+      if ((p & 3u) != ST_ABSENT && p != r) mask |= 1u << j;
+      ab |= (uint32_t)((p & 3u) == ST_ABSENT && (r & 3u) != ST_ABSENT);
     }
   }
+  const uint32_t nc = __popc(mask);
+  const bool two = c + 1 < nch;
+  if (!__syncthreads_or(nc | ab)) {  // steady state: all 4096 subjects match
+    if (threadIdx.x == 0) {
+      uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NCHUNK + c) * 2;
+      cm[0] = cm[1] = 0;
+      if (two) cm[2] = cm[3] = 0;
+    }
+    return;
+  }
+  if (dl && ab) atomicOr(&d.msgs[b][mi].kind, KF_ABS);  // (rare: a record the payload lacks)
+  scan[threadIdx.x] = nc;
+  __syncthreads();
+  for (uint32_t o = 1; o < 256; o <<= 1) {
+    uint32_t v = threadIdx.x >= o ? scan[threadIdx.x - o] : 0;
+    __syncthreads();
+    scan[threadIdx.x] += v;
+    __syncthreads();
+  }
+  const uint32_t incl = scan[threadIdx.x];
+  if (threadIdx.x == 0) {
+    uint32_t totc = scan[255];
+    const uint32_t first = scan[127];  // chunk c's candidates (lanes 0-127)
+    uint32_t bo = atomicAdd(d.pool_used, totc);
+    if (bo + totc > d.POOLCAP) {  // no room: nothing of this item is written (the error aborts the step)
+      atomicOr(d.err, E_POOL);
+      totc = 0;
+      bo = NEVER;
+    }
+    base = bo;
+    uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NCHUNK + c) * 2;
+    cm[0] = bo;
+    cm[1] = bo == NEVER ? 0u : first;
+    if (two) {
+      cm[2] = bo == NEVER ? NEVER : bo + first;
+      cm[3] = bo == NEVER ? 0u : totc - first;
+    }
+    if (totc) atomicAdd(&d.msgs[b][mi].ncand, totc);
+  }
+  __syncthreads();
+  uint32_t o = base + incl - nc;
+  if (base != NEVER)  // (an overflowed item must not overwrite other items' candidates)
+    for (uint32_t m = mask; m; m &= m - 1) {
+      const uint32_t j = (uint32_t)(__ffs(m) - 1);
+      const uint32_t p = esc ? pk[j] : (pw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+      d.pool[o++] = ((uint64_t)(n0 + j) << 34) | key34(p);
+    }
+  __syncthreads();
 }
 
 // k_sync_diff's work: the items of `nmsg` messages (list[j], or j itself without a list) over the blocks blk of nblk,
@@ -469,15 +529,15 @@ __device__ __forceinline__ void stream_list(const Dev& d, uint32_t b, const uint
       atomicAdd(&d.ctr[C_DIFFWIDE_ALL], 1ull);
       if (timed) atomicAdd(&d.ctr[C_DIFFWIDE], 1ull);
     }
+    if (ncur) {
+      diff_pair16(d, b, mi, c0, cur, scan, base);
+    } else {
 #pragma unroll
-    for (uint32_t h = 0; h < PER; ++h) {
-      const uint32_t c = c0 + h;
-      if (c >= nch) break;  // (block-uniform)
-      const uint32_t s0 = c * CH + threadIdx.x * 8;
-      uint32_t p[8], r[8];
-      if (ncur) {
-        narrow_keys(d, b, mi, s0, cur[2 * h], cur[2 * h + 1], p, r);
-      } else {
+      for (uint32_t h = 0; h < PER; ++h) {
+        const uint32_t c = c0 + h;
+        if (c >= nch) break;  // (block-uniform)
+        const uint32_t s0 = c * CH + threadIdx.x * 8;
+        uint32_t p[8], r[8];
         if (h > 0) {  // a wide item's later chunk
           bool nw;
           diff_fetch<SHARDED>(d, b, mi, c, cur, pcur, nw);
@@ -494,8 +554,8 @@ __device__ __forceinline__ void stream_list(const Dev& d, uint32_t b, const uint
           p[j] = pv[j];
           r[j] = rv[j];
         }
+        diff_chunk(d, b, mi, c, s0, p, r, scan, base);
       }
-      diff_chunk(d, b, mi, c, s0, p, r, scan, base);
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) cur[q] = nxt[q];

@@ -8,8 +8,10 @@ just below the limit (swim_debug_set_incarnation) and check both sides of it: 2^
 everywhere like any other incarnation; the bump past it fails loudly."""
 import pytest
 
-from swimhip import SimConfig, _abi
+from swimhip import ClusterConfig, SimConfig, _abi
 from swimhip.cluster import SimulatedCluster, SwimError
+
+from parity_util import pair, run_lockstep
 
 pytestmark = pytest.mark.gpu
 
@@ -35,3 +37,23 @@ def test_incarnation_at_the_limit(engine):
             c.step(2)
     finally:
         c.close()
+
+
+def test_key16_escape_boundary(oracle, engine):
+    n = 64
+    cfg = SimConfig(n_members=n, cluster=ClusterConfig(syncInterval=1000), record_events=True, seed=0x16B)
+    o, e = pair(oracle, engine, cfg)
+    lib = {id(o): oracle, id(e): engine}
+    movers = (3, 17, 29, 40)
+    for c in (o, e):
+        c.set_default_loss(10)
+        for j, m in enumerate(movers):  # keys 16 379 << 2 | ALIVE .. : every bump below crosses or nears 0xFFFF
+            assert _abi.debug_set_incarnation(lib[id(c)], c._h, m, 16379 + j) == 0
+    run_lockstep(o, e, 40, 10, "incarnations below the 16-bit escape")
+    for step in range(4):
+        for c in (o, e):
+            for m in movers:
+                c.update_incarnation(m)
+        run_lockstep(o, e, 40, 10, f"bump {step + 1} across the escape")
+    o.close()
+    e.close()
