@@ -147,7 +147,15 @@ __device__ __forceinline__ bool replay_pair(const Dev& d, uint32_t x, uint32_t y
   // those ranges.
   uint32_t lo_in[2] = {cx, NEVER};  // [0]: deliveries into x, [1]: deliveries into y
   uint32_t cinc[CM];
-  for (uint32_t i = 0; i < n; ++i) cinc[i] = NEVER - 1;  // not computed yet
+  uint8_t swc[CM];  // swept_before of event i's sender: 0 not computed yet, 1 no, 2 yes (both loops ask)
+  for (uint32_t i = 0; i < n; ++i) {
+    cinc[i] = NEVER - 1;  // not computed yet
+    swc[i] = 0;
+  }
+  auto swept = [&](uint32_t i, uint32_t snd, uint32_t cs) {
+    if (!swc[i]) swc[i] = swept_before(d, snd, cs, ev[i].tick) ? 2 : 1;
+    return swc[i] == 2;
+  };
   for (int pass = 0; pass < 8; ++pass) {
     bool changed = false;
     for (int i = (int)n - 1; i >= 0; --i) {
@@ -159,7 +167,7 @@ __device__ __forceinline__ bool replay_pair(const Dev& d, uint32_t x, uint32_t y
       uint32_t cs = cinc[i];
       uint32_t snd = c.dir == 0 ? y : x;
       if (cs == NEVER || rounds_before(d, snd, cs) + c.spread < c.rb) continue;
-      if (swept_before(d, snd, cs, c.tick)) continue;
+      if (swept((uint32_t)i, snd, cs)) continue;
       uint32_t sin = 1 - rin;
       if (lo_in[sin] == NEVER || cs < lo_in[sin]) {
         lo_in[sin] = cs;
@@ -195,7 +203,7 @@ __device__ __forceinline__ bool replay_pair(const Dev& d, uint32_t x, uint32_t y
     uint32_t cs = cinc[i] != NEVER - 1 ? cinc[i] : inc_at(d, snd, g, gid, c.tick, tau + lat);
     if (cs == NEVER) continue;
     if (rounds_before(d, snd, cs) + c.spread < c.rb) continue;
-    if (swept_before(d, snd, cs, c.tick)) continue;  // x no longer held it
+    if (swept(i, snd, cs)) continue;  // x no longer held it
     // the receiver delivered g to the sender during that incarnation: infectedFrom (isInfected :247)
     uint32_t od = 1 - c.dir;  // opposite direction
     bool blocked = false;
@@ -203,7 +211,10 @@ __device__ __forceinline__ bool replay_pair(const Dev& d, uint32_t x, uint32_t y
     if (blocked) continue;
     const uint32_t rcv = c.dir == 0 ? x : y;
     if (lost_gossip_pct(d, c.pct, snd, c.tick, c.slot, gid)) continue;
-    del[c.dir][nd[c.dir]++] = d.dly_on ? gossip_arrival(d, snd, rcv, c.tick, c.slot, gid) : c.tick + lat;
+    const uint32_t at = d.dly_on ? gossip_arrival(d, snd, rcv, c.tick, c.slot, gid) : c.tick + lat;
+    // a delivery depends only on earlier events: the first y -> x one inside [cx, tau] is the answer
+    if (c.dir == 0 && at >= cx && at <= tau) return true;
+    del[c.dir][nd[c.dir]++] = at;
   }
   for (uint32_t q = 0; q < nd[0]; ++q)
     if (del[0][q] >= cx && del[0][q] <= tau) return true;
