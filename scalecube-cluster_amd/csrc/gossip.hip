@@ -419,16 +419,32 @@ __device__ __forceinline__ void grp_sync() {
   }
 }
 
+// f(slot) for the ring entries at positions [a, b) of ring R, a group of nth threads (tid) taking every nth: four
+// loads in flight per thread before their uses (a plain loop waited out each load: C2 walks ~10^4 entries per member)
+template <typename F>
+__device__ __forceinline__ void ring_walk(const uint32_t* R, uint32_t mask, uint32_t a, uint32_t b, uint32_t tid,
+                                          uint32_t nth, F f) {
+  const uint32_t n = b - a;
+  uint32_t o = tid;
+  for (; o + 3 * nth < n; o += 4 * nth) {
+    const uint32_t g0 = R[(a + o) & mask], g1 = R[(a + o + nth) & mask], g2 = R[(a + o + 2 * nth) & mask],
+                   g3 = R[(a + o + 3 * nth) & mask];
+    f(g0 & RG_SLOT);
+    f(g1 & RG_SLOT);
+    f(g2 & RG_SLOT);
+    f(g3 & RG_SLOT);
+  }
+  for (; o < n; o += nth) f(R[(a + o) & mask] & RG_SLOT);
+}
+
 __device__ __forceinline__ void rr_bits(const Dev& d, uint32_t m, uint32_t a, uint32_t b, uint32_t op,
                                         unsigned long long* lh, unsigned long long* lw, uint32_t c0, uint32_t c1,
                                         uint32_t tid, uint32_t nth) {
-  const uint32_t* R = ring(d, m);
-  const uint32_t mask = d.BCAP - 1;
-  for (uint32_t p = a + tid; p - a < b - a; p += nth) {
-    const uint32_t g = R[p & mask] & RG_SLOT, q = g >> 6;
+  ring_walk(ring(d, m), d.BCAP - 1, a, b, tid, nth, [&](uint32_t g) {
+    const uint32_t q = g >> 6;
     const unsigned long long bit = 1ull << (g & 63u);
     if (lh) {  // LDS chunk [c0, c1) of the rows
-      if (q < c0 || q >= c1) continue;
+      if (q < c0 || q >= c1) return;
       if (op == 0) atomicAnd(&lh[q - c0], ~bit);
       else if (op == 1) atomicAnd(&lw[q - c0], ~bit);
       else atomicOr(&lw[q - c0], bit);
@@ -437,7 +453,7 @@ __device__ __forceinline__ void rr_bits(const Dev& d, uint32_t m, uint32_t a, ui
       else if (op == 1) atomicAnd(&wrow(d, m)[q], ~bit);
       else atomicOr(&wrow(d, m)[q], bit);
     }
-  }
+  });
 }
 
 // one round member's ring ranges (see above) by a group of nth threads; lh / lw: LDS rows of cw words
@@ -450,12 +466,10 @@ __device__ void round_member(const Dev& d, uint32_t m, uint32_t k, unsigned long
   const uint32_t r4 = (int32_t)(seen - wnew) > 0 ? seen : wnew;  // max(seen, wnew)
   const uint32_t r3 = (int32_t)(w0 - wnew) > 0 ? w0 : wnew;      // end of the re-entry range
   // side effects of the sweeps (sweepGossips :283-308; on_sweep: a completed leave)
-  const uint32_t* R = ring(d, m);
-  for (uint32_t p = h + tid; p - h < send - h; p += nth) {
-    const uint32_t g = R[p & (d.BCAP - 1)] & RG_SLOT;
+  ring_walk(ring(d, m), d.BCAP - 1, h, send, tid, nth, [&](uint32_t g) {
     d.S[s_idx(d, g, m)] |= S16_SWEPT;
     on_sweep(d, g, m, k);
-  }
+  });
   const uint32_t nch = (send - h) + ((int32_t)(r2 - w0) > 0 ? r2 - w0 : 0u) + (r3 - wnew) + (tl - r4);
   if (nch <= 64 || span == 0) {  // few changes: atomics on the rows
     rr_bits(d, m, h, send, 0, nullptr, nullptr, 0, 0, tid, nth);
@@ -652,10 +666,10 @@ __global__ void __launch_bounds__(256) k_rx_build(const Dev* __restrict__ dp) {
       const uint32_t c1 = min(span, c0 + RXW);
       for (uint32_t j = threadIdx.x; j < c1 - c0; j += blockDim.x) lr[j] = 0ull;
       __syncthreads();
-      for (uint32_t p = a + threadIdx.x; p - a < b - a; p += blockDim.x) {
-        const uint32_t g = R[p & (d.BCAP - 1)] & RG_SLOT, q = g >> 6;
+      ring_walk(R, d.BCAP - 1, a, b, threadIdx.x, blockDim.x, [&](uint32_t g) {
+        const uint32_t q = g >> 6;
         if (q >= c0 && q < c1) atomicOr(&lr[q - c0], 1ull << (g & 63u));
-      }
+      });
       __syncthreads();
       for (uint32_t j = threadIdx.x; j < c1 - c0; j += blockDim.x) row[c0 + j] = lr[j];
       __syncthreads();
@@ -1175,10 +1189,16 @@ __global__ void __launch_bounds__(256) k_gossip_apply_big(const Dev* __restrict_
     unsigned long long h = 0;
     for (uint32_t p0 = a; p0 - a < b - a; p0 += 64u * 64u) {  // 64 entries per lane per batch
       unsigned long long rt = 0;
+      // the next entry's ring load is issued before this one's holder-table and row accesses (their stores would
+      // otherwise keep the compiler from hoisting it)
+      uint32_t g = p0 + lane - a < b - a ? R[(p0 + lane) & mask] & RG_SLOT : 0u;
       for (uint32_t it = 0; it < 64; ++it) {
         const uint32_t p = p0 + it * 64u + lane;
         if (p - a >= b - a) break;
-        if (apply_entry(d, t, R[p & mask] & RG_SLOT, k, dr, h)) rt |= 1ull << it;
+        const uint32_t pn = p + 64u;
+        const uint32_t gn = it + 1 < 64 && pn - a < b - a ? R[pn & mask] & RG_SLOT : 0u;
+        if (apply_entry(d, t, g, k, dr, h)) rt |= 1ull << it;
+        g = gn;
       }
       uint32_t rj = wave_reserve(d.rc_n, (uint32_t)__popcll(rt));
       for (; rt; rt &= rt - 1, ++rj) {

@@ -1,5 +1,6 @@
 # round profile: the default bench line (with the CPU baseline), its kernel-trace summary, and the HBM PMC passes
-# for k_sync_diff (FETCH_SIZE and WRITE_SIZE in separate runs, MI355X_MICROARCH.md HBM/rocprofv3 section)
+# for k_sync_diff (FETCH_SIZE and WRITE_SIZE in separate runs, MI355X_MICROARCH.md HBM/rocprofv3 section); then
+# tools/make_profiles.py <tag> copies the summaries into profiles/
 set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
