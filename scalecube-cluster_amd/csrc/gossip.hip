@@ -125,7 +125,7 @@ __device__ bool swept_before(const Dev& d, uint32_t x, uint32_t cs, uint32_t t) 
   const uint32_t pos = d.log_pos[x], n = min(pos, d.LOGW);
   const bool steady = d.spchg[x] <= cs;
   for (uint32_t e = 1; e <= n; ++e) {
-    const size_t li = (size_t)x * d.LOGW + (pos - e) % d.LOGW;
+    const size_t li = (size_t)x * d.LOGW + ((pos - e) & (d.LOGW - 1u));  // LOGW is a power of two
     const uint32_t tr = d.log_tick[li];
     if (tr == NEVER || tr >= t) continue;
     if (tr < cs) break;
@@ -694,7 +694,7 @@ __global__ void __launch_bounds__(256) k_gossip_contacts(Dev d, uint32_t k) {
       const int64_t cut = (int64_t)k - (int64_t)(d.tspread[m] + 1u) * d.gossip_t - d.lat - dmax(d);
       const uint32_t R = min(nlog, d.tspread[m] + 2u + (d.lat + dmax(d) + d.gossip_t - 1u) / d.gossip_t);
       for (uint32_t e = sub; e < R; e += 8) {
-        const size_t lo = (size_t)t * d.LOGW + (pos - 1u - e) % d.LOGW;
+        const size_t lo = (size_t)t * d.LOGW + ((pos - 1u - e) & (d.LOGW - 1u));
         const uint32_t t2 = d.log_tick[lo];
         if (t2 == NEVER || t2 >= k || (int64_t)t2 <= cut) continue;
         const uint32_t n = d.log_cnt[lo];
