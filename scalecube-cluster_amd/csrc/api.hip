@@ -149,6 +149,7 @@ int grow_caps(swim_handle* h) {
 static int grow_caps_(swim_handle* h) {
   Dev& d = h->d;
   if (!d.rfill) return SWIM_OK;
+  // (a row shard publishes only the ring fill and the history entries, grow_caps_shard: [0], [3..5] stay 0)
   const volatile uint32_t* f = h->hflag;
   const uint64_t used = f[0], fill = f[2], nrc = f[3], nrp = f[4], nsl = f[5], nhist = f[6];
   const uint64_t N = d.N;
@@ -306,6 +307,28 @@ static int grow_caps_(swim_handle* h) {
   HIPCK(h2d(st, (void*)d.self, &d, sizeof(Dev)));
   h->growths++;
   return SWIM_OK;
+}
+
+// Capacity growth on a row shard (W > 1), after a tick whose gossip plane ran: the receipt rings and the incarnation
+// history hold the replicated holder state, indexed by absolute ring positions and (gid, member) tags, so each shard
+// sizes them for itself. The largest ring fill (this shard's targets in k_gossip_apply, the peers' first receipts in
+// k_unpack_b) and the history entries are read back here (the speculative sharded batches never run the gossip
+// plane, so this costs a stream sync only on gossip ticks). Slot ids are global (owner = id / SPR) and the per-tick
+// lists feed fixed-size exchange regions, so those keep the sizes the config gives them.
+static int grow_caps_shard(swim_handle* h) {
+  Dev& d = h->d;
+  if (!d.rfill) return SWIM_OK;
+  uint32_t v[2] = {0, 0};
+  HIPCK(hipMemcpyAsync(&v[0], d.rfill, 4, hipMemcpyDeviceToHost, h->stream));
+  HIPCK(hipMemcpyAsync(&v[1], d.hist_n, 4, hipMemcpyDeviceToHost, h->stream));
+  HIPCK(hipMemsetAsync(d.rfill, 0, 4, h->stream));
+  HIPCK(hipStreamSynchronize(h->stream));
+  volatile uint32_t* f = h->hflag;
+  f[0] = 0;  // slots: not grown on a shard
+  f[2] = v[0];
+  f[3] = f[4] = f[5] = 0;
+  f[6] = v[1];
+  return grow_caps(h);
 }
 
 // NetworkLinkSettings.evaluateDelay (:64-74) quantised to ticks (SEMANTICS.md §2): thresholds on the 32-bit delay draw
@@ -492,6 +515,7 @@ int build(swim_handle* h) {
   // row on its own lane (cow_now); 1024 entries up to 65 536 members (8 KB each), 256 above
   d.ULOGC = c.n_members <= 65536 ? ULOG : 256;
   d.trk_cap = TRK, d.ulog_cap = d.ULOGC, d.creq_cap = CREQ, d.cwmax_cap = CWMAX, d.cev_cap = CEV, d.mq_cap = MQ;
+  d.rr_atomic = getenv("SWIM_RR_ATOMIC") ? (uint32_t)atoi(getenv("SWIM_RR_ATOMIC")) : 64u;  // (measurements)
   d.hv = 24;  // routed receipts from which a member's P4 runs on a wave of its own (k_inbox_apply)
   d.XI = XINL;
   d.sort_cap = SORT_MAX;
@@ -703,8 +727,9 @@ int build(swim_handle* h) {
     HIPCK(hipMemsetAsync(d.tl_tick, 0xFF, 8 * NL, h->stream));
     HIPCK(hipMemsetAsync(d.ndl, 0, 4, h->stream));
   }
-  // capacity growth between ticks (grow_caps): one GPU, without guard zones; SWIM_NO_GROW keeps the sizes fixed
-  if (d.W == 1 && !getenv("SWIM_NO_GROW") && !getenv("SWIM_GUARD")) {
+  // capacity growth between ticks (grow_caps), without guard zones; SWIM_NO_GROW keeps the sizes fixed. A row shard
+  // grows its receipt rings and incarnation history (grow_caps_shard); its slot ids and exchange capacities are global
+  if (!getenv("SWIM_NO_GROW") && !getenv("SWIM_GUARD")) {
     A(d.rfill, 1) A(d.hist_n, 1)
     HIPCK(hipMemsetAsync(d.rfill, 0, 4, h->stream));
     HIPCK(hipMemsetAsync(d.hist_n, 0, 4, h->stream));
@@ -1527,6 +1552,7 @@ int swim_step(swim_handle* h, uint32_t n) {
       launch_tick_b(d, kh, h->stream, th, gossip);
       if (gossip && (xr = exchange(h, d.xb_send, d.xb_recv, d.XB_PEER, d.xb_scnt, d.xb_rcnt, false)) != SWIM_OK) return xr;
       launch_tick_c(d, kh, h->stream, gossip);
+      if (gossip && (xr = grow_caps_shard(h)) != SWIM_OK) return xr;
       h->tick = kh + 1ull;
       i = ih + 1;
       continue;
@@ -1538,6 +1564,7 @@ int swim_step(swim_handle* h, uint32_t n) {
       launch_tick_b(d, k, h->stream, te, gossip);
       if (gossip && (xr = exchange(h, d.xb_send, d.xb_recv, d.XB_PEER, d.xb_scnt, d.xb_rcnt, false)) != SWIM_OK) return xr;
       launch_tick_c(d, k, h->stream, gossip);
+      if (gossip && (xr = grow_caps_shard(h)) != SWIM_OK) return xr;
     }
     h->tick++;
     ++i;

@@ -321,6 +321,7 @@ struct Dev {
   // member with at least hv receipts before P4 (its pending live-row payload chain and write-log tail kept here),
   // k_inbox_apply runs its P4 a wave per member, and a second k_member_tick launch runs its P5 and P6
   uint32_t hv;
+  uint32_t rr_atomic;  // a round's holder-row changes up to this many go to the rows by global atomics (k_round_apply)
   uint32_t *hv_list, *nhv, *hv_pend, *hv_tlast;  // [NL], [1], [NL], [NL]
 
   // ---- outputs ----

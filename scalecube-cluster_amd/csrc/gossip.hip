@@ -471,7 +471,7 @@ __device__ void round_member(const Dev& d, uint32_t m, uint32_t k, unsigned long
     on_sweep(d, g, m, k);
   });
   const uint32_t nch = (send - h) + ((int32_t)(r2 - w0) > 0 ? r2 - w0 : 0u) + (r3 - wnew) + (tl - r4);
-  if (nch <= 64 || span == 0) {  // few changes: atomics on the rows
+  if (nch <= d.rr_atomic || span == 0) {  // few changes: atomics on the rows
     rr_bits(d, m, h, send, 0, nullptr, nullptr, 0, 0, tid, nth);
     if ((int32_t)(r2 - w0) > 0) rr_bits(d, m, w0, r2, 1, nullptr, nullptr, 0, 0, tid, nth);
     rr_bits(d, m, wnew, r3, 2, nullptr, nullptr, 0, 0, tid, nth);
@@ -1257,9 +1257,13 @@ __global__ void k_unpack_b(Dev d, uint32_t k) {
       continue;
     }
     atomicOr(&hrow(d, t)[g >> 6], 1ull << (g & 63u));
-    receipt_mark(d, g, t, k, atomicAdd(&d.rtail[t], 1u));
+    const uint32_t pos = atomicAdd(&d.rtail[t], 1u);
+    receipt_mark(d, g, t, k, pos);
     receipt_create(d, g, t, k);
     atomicAdd(&d.held[t], 1u);
+    // the ring fill for grow_caps_shard (an atomic only on a new maximum)
+    if (d.rfill && pos + 1u - d.rhead[t] > __hip_atomic_load(d.rfill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      atomicMax(d.rfill, pos + 1u - d.rhead[t]);
   }
 }
 

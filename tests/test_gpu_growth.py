@@ -61,3 +61,25 @@ def test_rumor_defaults_from_churn(engine):
     c.run_periods(40)
     assert _abi.debug_caps(c.lib, c._h)["growths"] <= 1
     c.close()
+
+
+@pytest.mark.parametrize("name", ["c2_mid", "c4_long"])
+def test_sharded_golden_with_growing_rings(engine, name):
+    """Row-sharded handles (2 shards) grow their receipt rings and incarnation history between gossip ticks
+    (api.hip grow_caps_shard): the rings start at 256 entries, the peers' first receipts count towards the fill
+    (k_unpack_b), and the golden replays bit for bit with more device memory at the end."""
+    import sys
+    sys.path.insert(0, str(GOLDEN))
+    from scenarios import SCENARIOS, record
+    from swimhip.shard import ThreadShardGroup
+    cfg, _ = SCENARIOS[name]()
+    c = ThreadShardGroup(engine, dataclasses.replace(cfg, gossip_ring_cap=256), 2)
+    b0 = c.counters()["device_bytes"]
+    rec = record(c, name)
+    b1 = c.counters()["device_bytes"]
+    c.close()
+    want = json.loads((GOLDEN / f"{name}.json").read_text())
+    assert len(rec["periods"]) == len(want["periods"])
+    for got, exp in zip(rec["periods"], want["periods"]):
+        assert got == exp, f"{name} (2 shards) period {exp['period']}: {got} != {exp}"
+    assert b1 > b0, "no ring grew"
