@@ -651,6 +651,7 @@ int build(swim_handle* h) {
   if (c.init_mode == SWIM_INIT_COLD_JOIN) mc = std::max<uint64_t>(mc, N + 1024);
   d.MSGCAP = (uint32_t)mc;
   d.NCHUNK = (uint32_t)((d.NS + CH - 1) / CH);
+  d.NMETA = (uint32_t)((d.NS + MCH - 1) / MCH);
   d.POOLCAP = (uint32_t)std::min<uint64_t>(1ull << 26, std::max<uint64_t>(1ull << 20, N * 64));
   d.EVCAP = c.event_cap ? c.event_cap : (1u << 20);
   // first receipts per tick: routed to P4 (RCAP), shipped to the other row shards (DCAP)
@@ -712,7 +713,7 @@ int build(swim_handle* h) {
   A(d.rc_slot, d.RCAP) A(d.rc_ndrop, N) A(d.dead_rx, N) A(d.leaving, N) A(d.rc_key, d.RCAP) A(d.rc_slot2, d.RCAP) A(d.rc_key2, d.RCAP) A(d.fexp, d.SLOTS) A(d.nfexp, 1) A(d.hist, (uint64_t)d.HCAP * HREC)
   A(d.msgs[0], d.MSGCAP) A(d.msgs[1], d.MSGCAP) A(d.nmsg, 2) A(d.arena[0], (uint64_t)d.ARENA_ROWS * d.NS)
   A(d.arena[1], (uint64_t)d.ARENA_ROWS * d.NS) A(d.arena_used, 2)
-  A(d.m_next, 2ull * d.MSGCAP) A(d.m_head, 2 * N) A(d.next_evt, N) A(d.mdone, 2) A(d.trk, NL * TRKL) A(d.ulog, NL * d.ULOGC * 2) A(d.spq, NL * SPQ * 8) A(d.fpend, NL * KP * 2) A(d.pending_inc, N) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NCHUNK * 2)
+  A(d.m_next, 2ull * d.MSGCAP) A(d.m_head, 2 * N) A(d.next_evt, N) A(d.mdone, 2) A(d.trk, NL * TRKL) A(d.ulog, NL * d.ULOGC * 2) A(d.spq, NL * SPQ * 8) A(d.fpend, NL * KP * 2) A(d.pending_inc, N) A(d.chunk_meta, (uint64_t)d.MSGCAP * d.NMETA * 2)
   A(d.pool, d.POOLCAP) A(d.pool_used, 1)
   d.NW = d.implicit ? 0u : (d.N + 63u) / 64u;  // (RUMOR mode with implicit views has no SYNC)
   A(d.hv_list, NL) A(d.nhv, 1) A(d.hv_pend, NL) A(d.hv_tlast, NL) A(d.sg_list, N) A(d.nsg, 1) A(d.ap_list, N) A(d.nap, 1)

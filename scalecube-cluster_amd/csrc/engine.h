@@ -23,7 +23,8 @@ constexpr uint32_t SUBCAP = 8, PATHCAP = 8, FREC = 8, GREC = 8;
 // pending virtual hops per member with link delays (swim_config.delay_cap_ms > 0): a delayed ping-req chain stays
 // open for up to 4 x (lat + EMAX) ticks, several FD periods, so more of them overlap (Dev::PCAP <= 32)
 constexpr uint32_t PATHCAP_DELAY = 32;
-constexpr uint32_t CH = 2048;  // subjects per SYNC-diff work item (256 threads x 8)
+constexpr uint32_t CH = 2048;  // subjects per SYNC-diff work item (256 threads x 8) and per shipped payload chunk
+constexpr uint32_t MCH = 1024;  // subjects per candidate-list segment (chunk_meta): one wave of 16-bit keys
 constexpr uint32_t TRK = 16;   // subjects written in one tick's P1 that are re-checked against later payloads (sorted list)
 constexpr uint32_t TRKL = 64;  // of them listed per member for clearing its written-subject bitmap (more: the whole row)
 // deferred copy-on-write (member.hip cow): row writes logged per member and tick while a snapshot is open, open
@@ -148,6 +149,7 @@ struct Dev {
   uint64_t* churn_q;     // [churn][2] (origin, payload) of this period's rumors
   uint32_t* ucnt;        // [N] scratch of the user-gossip queue: its entries per member (zero between launches)
   uint32_t seeds[16];
+  uint32_t NMETA;  // candidate-list segments per payload: NS / MCH rounded up
   uint32_t LCAP, FCAP, GRCAP, LOGW, SLOTS, MSGCAP, NCHUNK, POOLCAP, EVCAP, DCAP, RCAP, ARENA_ROWS, LOOKBACK, HCAP;
   uint32_t gt_mul;  // floor(2^32 / gossip_t) (2^32 - 1 for 1): rounds_before divides by multiply-high + one correction
 
@@ -302,7 +304,7 @@ struct Dev {
   uint32_t ULOGC;   // undo-log entries per member (1024 up to 65 536 members, 256 above; ulog_cap <= ULOGC)
   uint32_t* spq;    // [NL][SPQ][8] per member: gossips created this tick, waiting for their slots (member.hip)
   uint32_t* fpend;  // [NL][KP][2] per member: this tick's pending FD-list inserts (subject, final position)
-  uint32_t* chunk_meta;                      // [MSGCAP][NCHUNK][2] (pool offset, count)
+  uint32_t* chunk_meta;                      // [MSGCAP][NMETA][2] (pool offset, count) per MCH subjects
   uint64_t* pool;                            // candidate (subject << 34 | key)
   uint32_t* pool_used;
   // SYNC_ACK resolution (W == 1): per member and tick parity, the subjects whose key its row changed in

@@ -374,11 +374,12 @@ __device__ __forceinline__ void diff_chunk(const Dev& d, uint32_t b, uint32_t mi
     ab |= (uint32_t)((p[j] & 3u) == ST_ABSENT && (r[j] & 3u) != ST_ABSENT);
   }
   uint32_t nc = __popc(mask);
+  const bool two = 2 * c + 1 < d.NMETA;  // the chunk's second candidate segment (lanes 128-255)
   if (!__syncthreads_or(nc | ab)) {  // steady state: the whole 2048-subject chunk matches
     if (threadIdx.x == 0) {
-      uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NCHUNK + c) * 2;
-      cm[0] = 0;
-      cm[1] = 0;
+      uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NMETA + 2 * c) * 2;
+      cm[0] = cm[1] = 0;
+      if (two) cm[2] = cm[3] = 0;
     }
     return;
   }
@@ -394,6 +395,7 @@ __device__ __forceinline__ void diff_chunk(const Dev& d, uint32_t b, uint32_t mi
   uint32_t incl = scan[threadIdx.x];
   uint32_t totc = scan[255];
   if (threadIdx.x == 0) {
+    const uint32_t first = scan[127];  // the first segment's candidates (lanes 0-127)
     uint32_t bo = atomicAdd(d.pool_used, totc);
     if (bo + totc > d.POOLCAP) {  // no room: nothing of this chunk is written (the error aborts the step)
       atomicOr(d.err, E_POOL);
@@ -401,9 +403,13 @@ __device__ __forceinline__ void diff_chunk(const Dev& d, uint32_t b, uint32_t mi
       bo = NEVER;
     }
     base = bo;
-    uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NCHUNK + c) * 2;
+    uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NMETA + 2 * c) * 2;
     cm[0] = bo;
-    cm[1] = totc;
+    cm[1] = bo == NEVER ? 0u : first;
+    if (two) {
+      cm[2] = bo == NEVER ? NEVER : bo + first;
+      cm[3] = bo == NEVER ? 0u : totc - first;
+    }
     if (totc) atomicAdd(&d.msgs[b][mi].ncand, totc);
   }
   __syncthreads();
@@ -415,14 +421,13 @@ __device__ __forceinline__ void diff_chunk(const Dev& d, uint32_t b, uint32_t mi
   __syncthreads();
 }
 
-// a narrow item: chunks c and c + 1 of message mi in one pass (lanes 0-127 chunk c, 128-255 chunk c + 1, 16
-// subjects each from x), one block barrier for both; the candidates of both chunks in subject order from one pool
-// reservation. A lane with an escaped shadow (0xFFFF: an incarnation past 16 382 among its subjects) compares its 16
-// full keys of both rows instead.
-__device__ __forceinline__ void diff_pair16(const Dev& d, uint32_t b, uint32_t mi, uint32_t c, const uint4 (&x)[4],
-                                            uint32_t* scan, uint32_t& base) {
+// a narrow item: chunks c and c + 1 of message mi, each wave one 1024-subject candidate segment (wave w: segment
+// 2c + w, 16 subjects per lane from x), tested, scanned and written by the wave alone: no block barrier. A lane with
+// an escaped shadow (0xFFFF: an incarnation past 16 382 among its subjects) compares its 16 full keys of both rows.
+__device__ __forceinline__ void diff_wave16(const Dev& d, uint32_t b, uint32_t mi, uint32_t c, const uint4 (&x)[4]) {
   const bool dl = d.ackres != 0;
-  const uint32_t n0 = c * CH + threadIdx.x * 16, nch = d.NCHUNK;
+  const uint32_t lane = threadIdx.x & 63u, seg = 2 * c + (threadIdx.x >> 6);
+  const uint32_t n0 = c * CH + threadIdx.x * 16;  // = seg * MCH + lane * 16
   const uint32_t pw[8] = {x[0].x, x[0].y, x[0].z, x[0].w, x[1].x, x[1].y, x[1].z, x[1].w};
   const uint32_t rw[8] = {x[2].x, x[2].y, x[2].z, x[2].w, x[3].x, x[3].y, x[3].z, x[3].w};
   uint32_t mask = 0, ab = 0;
@@ -451,53 +456,40 @@ __device__ __forceinline__ void diff_pair16(const Dev& d, uint32_t b, uint32_t m
     }
   }
   const uint32_t nc = __popc(mask);
-  const bool two = c + 1 < nch;
-  if (!__syncthreads_or(nc | ab)) {  // steady state: all 4096 subjects match
-    if (threadIdx.x == 0) {
-      uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NCHUNK + c) * 2;
-      cm[0] = cm[1] = 0;
-      if (two) cm[2] = cm[3] = 0;
-    }
+  uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NMETA + seg) * 2;
+  const bool live = seg < d.NMETA;
+  if (!__ballot(nc | ab)) {  // steady state: the segment's 1024 subjects match
+    if (lane == 0 && live) cm[0] = cm[1] = 0;
     return;
   }
-  if (dl && ab) atomicOr(&d.msgs[b][mi].kind, KF_ABS);  // (rare: a record the payload lacks)
-  scan[threadIdx.x] = nc;
-  __syncthreads();
-  for (uint32_t o = 1; o < 256; o <<= 1) {
-    uint32_t v = threadIdx.x >= o ? scan[threadIdx.x - o] : 0;
-    __syncthreads();
-    scan[threadIdx.x] += v;
-    __syncthreads();
+  if (dl && __ballot(ab) && lane == 0) atomicOr(&d.msgs[b][mi].kind, KF_ABS);  // (rare: a record the payload lacks)
+  uint32_t incl = nc;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
   }
-  const uint32_t incl = scan[threadIdx.x];
-  if (threadIdx.x == 0) {
-    uint32_t totc = scan[255];
-    const uint32_t first = scan[127];  // chunk c's candidates (lanes 0-127)
-    uint32_t bo = atomicAdd(d.pool_used, totc);
-    if (bo + totc > d.POOLCAP) {  // no room: nothing of this item is written (the error aborts the step)
+  uint32_t totc = __shfl(incl, 63), bo = 0;
+  if (lane == 0 && totc) {
+    bo = atomicAdd(d.pool_used, totc);
+    if (bo + totc > d.POOLCAP) {  // no room: nothing of this segment is written (the error aborts the step)
       atomicOr(d.err, E_POOL);
-      totc = 0;
       bo = NEVER;
     }
-    base = bo;
-    uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NCHUNK + c) * 2;
-    cm[0] = bo;
-    cm[1] = bo == NEVER ? 0u : first;
-    if (two) {
-      cm[2] = bo == NEVER ? NEVER : bo + first;
-      cm[3] = bo == NEVER ? 0u : totc - first;
-    }
-    if (totc) atomicAdd(&d.msgs[b][mi].ncand, totc);
+    if (bo != NEVER) atomicAdd(&d.msgs[b][mi].ncand, totc);
   }
-  __syncthreads();
-  uint32_t o = base + incl - nc;
-  if (base != NEVER)  // (an overflowed item must not overwrite other items' candidates)
-    for (uint32_t m = mask; m; m &= m - 1) {
-      const uint32_t j = (uint32_t)(__ffs(m) - 1);
-      const uint32_t p = esc ? pk[j] : (pw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-      d.pool[o++] = ((uint64_t)(n0 + j) << 34) | key34(p);
-    }
-  __syncthreads();
+  bo = __shfl(bo, 0);
+  if (lane == 0 && live) {
+    cm[0] = bo;
+    cm[1] = bo == NEVER ? 0u : totc;
+  }
+  if (bo == NEVER) return;  // (an overflowed segment must not overwrite other segments' candidates)
+  uint32_t o = bo + incl - nc;
+  for (uint32_t m = mask; m; m &= m - 1, ++o) {
+    const uint32_t j = (uint32_t)(__ffs(m) - 1);
+    const uint32_t p = esc ? pk[j] : (pw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+    d.pool[o] = ((uint64_t)(n0 + j) << 34) | key34(p);
+  }
 }
 
 // k_sync_diff's work: the items of `nmsg` messages (list[j], or j itself without a list) over the blocks blk of nblk,
@@ -530,7 +522,7 @@ __device__ __forceinline__ void stream_list(const Dev& d, uint32_t b, const uint
       if (timed) atomicAdd(&d.ctr[C_DIFFWIDE], 1ull);
     }
     if (ncur) {
-      diff_pair16(d, b, mi, c0, cur, scan, base);
+      diff_wave16(d, b, mi, c0, cur);
     } else {
 #pragma unroll
       for (uint32_t h = 0; h < PER; ++h) {
@@ -606,7 +598,7 @@ struct ResArgs {
   uint32_t *dlist, *ndl, *chunk_meta, *pool_used, *err;
   uint64_t* pool;
   unsigned long long* ctr;
-  uint32_t NL, NS, MSGCAP, NCHUNK, POOLCAP;
+  uint32_t NL, NS, MSGCAP, NCHUNK, POOLCAP, NMETA;
   // W > 1: this shard's first observer, the senders' log prefixes by message (Dev::mlog), and the received payloads
   // (baseline row + shipped chunks, as diff_fetch reads them)
   uint32_t lo, W, MW;
@@ -684,14 +676,14 @@ __device__ __forceinline__ bool res_wave(const ResArgs& d, uint32_t i, uint32_t 
   }
   // per chunk: first candidate and count (the chunk walk of merge_payload, which reads none of it when ncand is 0)
   if (total && off != NEVER)
-    for (uint32_t c = lane; c < d.NCHUNK; c += 64) {
+    for (uint32_t c = lane; c < d.NMETA; c += 64) {
       uint32_t before = 0, in = 0;
       for (uint32_t j = 0; j < nall; ++j) {
         const uint32_t t = sc[j];
-        before += t < c * CH;
-        in += t != NEVER && t / CH == c;
+        before += t < c * MCH;
+        in += t != NEVER && t / MCH == c;
       }
-      uint32_t* cm = d.chunk_meta + ((size_t)i * d.NCHUNK + c) * 2;
+      uint32_t* cm = d.chunk_meta + ((size_t)i * d.NMETA + c) * 2;
       cm[0] = off + before;
       cm[1] = in;
     }
@@ -877,7 +869,7 @@ static void launch_ack_resolve(const Dev& d, uint32_t k, hipStream_t st, bool sp
   if (k == 0 || !d.ackres) return;
   const uint32_t b = (k - 1) & 1;
   const ResArgs ra{d.halt, d.nmsg + b, d.tl_tick, d.tl_n, d.tlog, d.rowk, d.arena[b], d.msgs[b], d.dlist, d.ndl,
-                   d.chunk_meta, d.pool_used, d.err, d.pool, d.ctr, d.NL, d.NS, d.MSGCAP, d.NCHUNK, d.POOLCAP,
+                   d.chunk_meta, d.pool_used, d.err, d.pool, d.ctr, d.NL, d.NS, d.MSGCAP, d.NCHUNK, d.POOLCAP, d.NMETA,
                    d.lo, d.W, d.MW, d.mlog, d.base_row, d.rx_mask, d.rx_off, d.xa_recv};
   hipLaunchKernelGGL(k_ack_resolve, dim3(128), dim3(512), 0, st, ra, k, spec ? 1u : 0u, timed ? 1u : 0u);
 }

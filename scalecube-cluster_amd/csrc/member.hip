@@ -966,11 +966,11 @@ __device__ __forceinline__ void merge_payload(ML& L, uint32_t mi, uint32_t reaso
     uint32_t subj, k1;
     {
       while (pool && e == n) {
-        if (c == d.NCHUNK) {
+        if (c == d.NMETA) {
           pool = false;
           break;
         }
-        const uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NCHUNK + c) * 2;
+        const uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NMETA + c) * 2;
         off = cm[0];
         n = cm[1];
         e = 0;
