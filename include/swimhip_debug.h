@@ -73,7 +73,9 @@ int swim_debug_caps(swim_handle* h, uint64_t* out, size_t n);
 int swim_debug_holders(swim_handle* h, uint32_t first, uint32_t n, uint32_t* out);
 
 /* sets member m's own record in its own table to incarnation inc, status unchanged, between steps (one GPU): the
- * boundary test of the 30-bit incarnation field of the key plane (SEMANTICS.md §8). inc >= 2^30: SWIM_ECAPACITY. */
+ * boundary test of the 30-bit incarnation field of the key plane (SEMANTICS.md §8). inc >= 2^30: SWIM_ECAPACITY.
+ * The write bypasses the row's copy-on-write and write-log bookkeeping, so it is refused (SWIM_EINVAL) while a SYNC /
+ * SYNC_ACK that m sent in the last tick still carries m's live row as its payload. */
 int swim_debug_set_incarnation(swim_handle* h, uint32_t m, uint32_t inc);
 
 #ifdef __cplusplus

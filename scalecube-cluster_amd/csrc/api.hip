@@ -695,8 +695,7 @@ int build(swim_handle* h) {
   const uint64_t NL = d.NL;  // per-observer arrays: this shard's rows only
   const uint64_t NV = d.implicit ? 1 : NL;  // implicit views: no table or list is stored
   A(d.rowk, NV * d.NS) A(d.rowa, NV * d.NS) A(d.fdl, NV * d.LCAP) A(d.gl, NV * d.LCAP)
-  d.rowk16 = nullptr;  // one GPU, stored tables: the diff's 16-bit shadow plane (SWIM_NO_K16: the diff reads u32 keys)
-  if (d.W == 1 && !d.implicit && !getenv("SWIM_NO_K16")) A(d.rowk16, NV * d.NS)
+  d.rowk16 = nullptr;  // allocated last, if it fits (below)
   A(d.subs, NL * SUBCAP * 4) A(d.paths, NL * d.PCAP * 5) A(d.fetch, NL * d.FCAP * FREC) A(d.groups, NL * d.GRCAP * GREC)
   A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.slow, d.SLOWCAP) A(d.slow_n, 1) A(d.rp, d.RPCAP) A(d.rp_n, 1) A(d.start_tick, N) A(d.jseed_n, N) A(d.jseeds, 16 * N) A(d.md_uidx, N) A(d.mcfg, 4 * N) A(d.md_ver, NL * MDU) A(d.churn_q, 2ull * d.churn) A(d.ucnt, N) A(d.cin, N * d.F) A(d.HB, (uint64_t)d.QW * N) A(d.WB, (uint64_t)d.QW * N) A(d.cev, N * d.F * CEVW)
   A(d.rg, (uint64_t)d.BCAP * N) A(d.rhead, N) A(d.rwin, N) A(d.rseen, N) A(d.rtail, N) A(d.rwl, N) A(d.nrwl, 1)
@@ -807,6 +806,13 @@ int build(swim_handle* h) {
       h->hsend.resize(d.W * std::max(d.XA_PEER, d.XB_PEER));
       h->hrecv.resize(d.W * std::max(d.XA_PEER, d.XB_PEER));
     }
+  }
+  // one GPU, stored tables: the diff's 16-bit shadow plane, only when it fits beside everything else with the usual
+  // growth reserve (an optimisation: without it k_sync_diff and row_put use the u32 keys; SWIM_NO_K16 forces that)
+  if (d.W == 1 && !d.implicit && !getenv("SWIM_NO_K16")) {
+    size_t fr = 0, tot = 0;
+    HIPCK(hipMemGetInfo(&fr, &tot));
+    if ((uint64_t)fr > 2ull * NV * d.NS + (4ull << 30)) A(d.rowk16, NV * d.NS)
   }
 #undef A
   HIPCK(hipMemsetAsync(d.S, 0, (size_t)d.SLOTS * N * 2, h->stream));
@@ -2220,6 +2226,19 @@ int swim_debug_set_incarnation(swim_handle* h, uint32_t m, uint32_t inc) {
   if (m >= d.N || d.implicit) return SWIM_EINVAL;
   if (inc >= INC_LIMIT) return SWIM_ECAPACITY;
   HIPCK(hipStreamSynchronize(h->stream));
+  if (h->tick > 0) {  // a SYNC / SYNC_ACK of m still in flight carries m's live row: the host write would reach it
+    const uint32_t b = (uint32_t)((h->tick - 1) & 1);
+    uint32_t nm = 0;
+    HIPCK(hipMemcpy(&nm, d.nmsg + b, 4, hipMemcpyDeviceToHost));
+    nm = std::min(nm, d.MSGCAP);
+    std::vector<SyncMsg> v(nm);
+    if (nm) HIPCK(hipMemcpy(v.data(), d.msgs[b], nm * sizeof(SyncMsg), hipMemcpyDeviceToHost));
+    for (const SyncMsg& q : v)
+      if (q.src == m && q.payload == NEVER && !(q.kind & KF_DEFER)) {
+        h->err = "swim_debug_set_incarnation: member " + std::to_string(m) + " has a live-row payload in flight";
+        return SWIM_EINVAL;
+      }
+  }
   uint32_t* w = d.rowk + lidx(d, m) * d.NS + m;
   uint32_t k = 0;
   HIPCK(hipMemcpy(&k, w, 4, hipMemcpyDeviceToHost));

@@ -16,6 +16,7 @@ ORACLE_LIB = ORACLE_DIR / "liboracle_swimref.so"
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libswimhip.so)")
     config.addinivalue_line("markers", "slow: long CPU oracle runs")
+    config.addinivalue_line("markers", "tape: the oracle side runs from a recorded tape when one exists (tests/tape.py)")
 
 
 def _build_oracle():
@@ -23,15 +24,67 @@ def _build_oracle():
         subprocess.check_call(["make", "-s", "-C", str(ORACLE_DIR)])
 
 
+_ORACLE = {}
+
+
 @pytest.fixture(scope="session")
 def oracle():
     """The CPU oracle (test infrastructure only): same C ABI as libswimhip."""
     from swimhip import _abi
     _build_oracle()
-    return _abi.load(ORACLE_LIB)
+    _ORACLE["lib"] = _abi.load(ORACLE_LIB)
+    return _ORACLE["lib"]
+
+
+def _install_tapes():
+    """SimulatedCluster(oracle, cfg) inside a @pytest.mark.tape test becomes a tests/tape.py TapeCluster."""
+    import tape
+    from swimhip.cluster import SimulatedCluster
+
+    def _new(cls, lib=None, cfg=None, *a, **k):
+        if cls is SimulatedCluster and tape.mode() != "live" and lib is not None and lib is _ORACLE.get("lib"):
+            return tape.TapeCluster(lib, cfg)
+        return object.__new__(cls)
+
+    SimulatedCluster.__new__ = staticmethod(_new)
+
+
+_install_tapes()
+
+
+@pytest.hookimpl(hookwrapper=True)
+def pytest_runtest_makereport(item, call):
+    out = yield
+    rep = out.get_result()
+    if rep.when == "call":
+        item._tape_passed = rep.passed
+
+
+@pytest.fixture(autouse=True)
+def _oracle_tape(request):
+    import tape
+    tape.begin(request.node.nodeid, request.node.get_closest_marker("tape") is not None)
+    yield
+    tape.end(getattr(request.node, "_tape_passed", False))
 
 
 @pytest.fixture(scope="session")
 def engine():
     import swimhip
     return swimhip.engine()
+
+
+@pytest.fixture(autouse=True)
+def _lockstep_timing(request):
+    """SWIM_TEST_TIMING=1: print how a test's lockstep time splits between the oracle and the engine."""
+    if not os.environ.get("SWIM_TEST_TIMING"):
+        yield
+        return
+    import parity_util
+    for k in parity_util.TIMES:
+        parity_util.TIMES[k] = 0.0
+    yield
+    t = parity_util.TIMES
+    if t["wall"] > 0:
+        print(f"\nLOCKSTEP {request.node.nodeid}: oracle {t['oracle']:.1f}s engine {t['engine']:.1f}s "
+              f"wall {t['wall']:.1f}s", flush=True)

@@ -83,8 +83,33 @@ def _c5_small():  # C5-shaped: rumor-only dissemination with 1 % churn per perio
     return SimConfig(n_members=400, mode=_abi.MODE_RUMOR, churn_per_period=4, record_events=True), [("periods", 30)]
 
 
+def _c3_full():  # C3 at the headline size (BASELINE configs[2], 100 000 members, the bench's own config with
+    # profile=True): the 25 steady periods the default bench line runs (warm-up 5 + 20 timed), then two periods each
+    # after one updateIncarnation (the c3dyn line's evolution: gossip, SYNC re-spread, UPDATED events, metadata
+    # fetches). Recorded on the GPU box (~210 GB of host RAM: tools/record_golden_box.py c3_full)
+    return SimConfig(n_members=100_000, profile=True, record_events=True), [
+        ("periods", 25), ("inc", 17), ("periods", 1), ("inc", 50_021), ("periods", 1)]
+
+
+def _c2_long():  # C2 at its configured 10 000 members past c2_full's 3 periods: as many periods as the GPU box's RAM
+    # holds the oracle's explicit infectedFrom sets (tools/record_golden_box.py c2_long stops before its memory cap)
+    return SimConfig(n_members=10_000, record_events=True, event_cap=1 << 22), [("loss", 5), ("periods", 12)]
+
+
+def _c4_50k():  # C4 at its configured 50 000 members (BASELINE configs[3]): groups A = [0, 25 000) and B blocked both
+    # ways from period 0, seeds = {0}. The oracle runs on the GPU box through the first SUSPECT wave (pings across the
+    # partition time out from period 1, ping-req timeouts suspect, the SUSPECT gossips fill each side) for as many
+    # periods as its RAM holds (tools/record_golden_box.py c4_50k)
+    n = 50_000
+    g = [0] * (n // 2) + [1] * (n // 2)
+    return SimConfig(n_members=n, cluster=ClusterConfig(seedMembers=[0]), record_events=True, pending_fetch_cap=4096,
+                     list_slack=4096), [("partition", g), ("periods", 80)]
+
+
 SCENARIOS = {"c1": _c1, "c2_small": _c2_small, "c4_small": _c4_small, "c3_small": _c3_small, "c5_small": _c5_small,
              "c4_mid": _c4_mid, "c2_mid": _c2_mid, "c4_long": _c4_long, "c4_large": _c4_large, "c2_full": _c2_full}
+# recorded on the GPU box (its host RAM and 16 cores): replayed by their own -m gpu tests, not by test_golden.py
+BOX_SCENARIOS = {"c3_full": _c3_full, "c2_long": _c2_long, "c4_50k": _c4_50k}
 SLOW_ON_ORACLE = {"c4_mid", "c2_mid", "c4_long", "c4_large", "c2_full"}  # recorded once; replaying it on the oracle takes minutes
 FULL_EVENTS = {"c1"}
 
@@ -98,14 +123,17 @@ def event_rows(evs):
              -1 if e.oldMetadata is None else e.oldMetadata, -1 if e.newMetadata is None else e.newMetadata] for e in evs]
 
 
-def record(c, name):
-    """Run scenario `name` on cluster c (already created from the scenario's SimConfig); return the record."""
-    cfg, actions = SCENARIOS[name]()
+def record(c, name, limit=None, on_period=None):
+    """Run scenario `name` on cluster c (already created from the scenario's SimConfig); return the record.
+    limit: stop after that many periods; on_period(out): called after every recorded period."""
+    cfg, actions = {**SCENARIOS, **BOX_SCENARIOS}[name]()
     out = {"periods": [], "events": [] if name in FULL_EVENTS else None}
     period = 0
     for what, arg in actions:
         if what == "periods":
             for _ in range(arg):
+                if limit is not None and period >= limit:
+                    return out
                 c.run_periods(1)
                 period += 1
                 ctr = c.counters()
@@ -115,6 +143,8 @@ def record(c, name):
                 out["periods"].append({"period": period, "state": digest(c.state_hash()),
                                        "counters": [int(ctr[k]) for k in COUNTERS],
                                        "events": digest(np.array(rows, dtype=np.int64).reshape(-1, 7))})
+                if on_period is not None:
+                    on_period(out)
         elif what == "kill":
             c.kill(arg)
         elif what == "loss":
@@ -123,4 +153,6 @@ def record(c, name):
             c.partition(np.array(arg, dtype=np.uint32))
         elif what == "unblock":
             c.unblock_all()
+        elif what == "inc":
+            c.update_incarnation(arg)
     return out

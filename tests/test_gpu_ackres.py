@@ -32,6 +32,7 @@ def faults(c, phase):
         c.set_default_link_settings(5, 150)  # delays from now on: late SYNCs and SYNC_ACKs are streamed
 
 
+@pytest.mark.tape
 def test_ack_resolution_parity_under_faults(oracle, engine):
     cfg = SimConfig(n_members=160, cluster=FAST_SYNC, delay_cap_ms=400, gossip_slot_cap=1 << 16)
     o, e = SimulatedCluster(oracle, cfg), SimulatedCluster(engine, dataclasses.replace(cfg, profile_all=True))
@@ -73,6 +74,7 @@ def test_ack_resolution_equals_streaming(engine):
         assert ca[k] == cb[k], k
 
 
+@pytest.mark.tape
 @pytest.mark.parametrize("world", [2, 3])
 def test_ack_resolution_sharded_parity(oracle, engine, world):
     """Row-sharded handles resolve SYNC_ACKs too: the responder's write-log prefix travels with the SYNC_ACK in exchange

@@ -37,6 +37,7 @@ def test_gossip_protocol_grid(oracle, engine, n, loss, delay):
     same_emulators(o, e, "grid")
 
 
+@pytest.mark.tape
 @pytest.mark.parametrize("delay", [100, 400, 1100])
 def test_full_stack_delays(oracle, engine, delay):
     """Every message kind late: pings and acks past the ping timeout (ping-req then resolves on the late direct ack),
@@ -146,6 +147,7 @@ def test_gossip_protocol_grid_sharded(oracle, engine, n, loss, delay):
     e.close()
 
 
+@pytest.mark.tape
 @pytest.mark.parametrize("delay,world", [(100, 2), (400, 3), (1100, 2)])
 def test_full_stack_delays_sharded(oracle, engine, delay, world):
     """Row-sharded: every message kind late, kills, incarnation and metadata updates (the grid of the unsharded case)."""

@@ -55,6 +55,7 @@ def test_tiny_caps_fast_sync_fuzz(oracle, engine, seed, monkeypatch):
     e.close()
 
 
+@pytest.mark.tape
 def test_tiny_caps_fallbacks_all_fire(oracle, engine, monkeypatch):
     """Across a few schedules every counted fallback fires at least once, each run bit-exact."""
     total = {}

@@ -4,10 +4,11 @@ updateIncarnation per period, MembershipProtocolImpl.java:178-190, so gossip, SY
 metadata fetches run at full size).
 
 The engine runs first in the bench's own configuration (SWIM_FLAG_PROFILE, speculative batches, SYNC_ACK resolution)
-and keeps only the per-member state hashes, counters and events; it is closed before the oracle (~20 B of host RAM
-per member pair, about 200 GB at 10^5 members) is built on 16 worker threads. Skipped, with the reason printed, when
+and keeps only the per-member state hashes, counters and events; the oracle (~20 B of host RAM per member pair, about
+200 GB at 10^5 members, 16 worker threads) runs the same periods beside it on a helper thread. Skipped, with the reason printed, when
 the host does not have that much memory available."""
 import os
+import threading
 
 import numpy as np
 import pytest
@@ -54,20 +55,36 @@ def test_c3_headline_size_parity(oracle, engine, monkeypatch):
         print("SKIP:", msg, flush=True)
         pytest.skip(msg)
     cfg = SimConfig(n_members=N, profile=True, record_events=True)
-    e = SimulatedCluster(engine, cfg)
-    er, ee = run(e)
-    ce = e.counters()
-    e.close()
+    # the oracle (16 worker threads) runs beside the engine on a helper thread: ctypes calls release the GIL
+    monkeypatch.setenv("SWIMREF_THREADS", "16")
+    got = {}
+
+    def run_oracle():
+        try:
+            o = SimulatedCluster(oracle, cfg)
+            got["o"] = run(o)
+            o.close()
+        except BaseException as x:  # noqa: BLE001 - re-raised below
+            got["err"] = x
+
+    th = threading.Thread(target=run_oracle)
+    th.start()
+    try:
+        e = SimulatedCluster(engine, cfg)
+        er, ee = run(e)
+        ce = e.counters()
+        e.close()
+    finally:
+        th.join()
+    if "err" in got:
+        raise got["err"]
+    orr, oe = got["o"]
     # every merged payload was either streamed by k_sync_diff or resolved from write logs (k_ack_resolve)
     assert ce["ack_resolved_total"] > 0
     assert ce["ack_resolved_total"] + ce["diff_msgs_total"] == ce["sync_merges"], ce
     steady = er[STEADY - 1][1]
     assert steady["row_writes"] == 0 and steady["events"] == 0  # the headline's steady state
 
-    monkeypatch.setenv("SWIMREF_THREADS", "16")
-    o = SimulatedCluster(oracle, cfg)
-    orr, oe = run(o)
-    o.close()
     for p, ((he, ce_), (ho, co)) in enumerate(zip(er, orr)):
         d = first_diff(ho, he)
         assert d is None, f"period {p + 1}: state hash differs at member {d[0]} word {d[1]} ({d[2]} words)"

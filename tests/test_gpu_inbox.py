@@ -42,6 +42,7 @@ def test_golden_with_inbox_waves(engine, monkeypatch, name, hv):
         assert rec["events"] == want["events"]
 
 
+@pytest.mark.tape
 @pytest.mark.parametrize("seed", [0, 1])
 def test_inbox_waves_refutations_and_leaves(oracle, engine, monkeypatch, seed):
     """The receipts k_inbox_apply hands to lane 0 (the member's own record, DEAD records, absent rows, user gossips)

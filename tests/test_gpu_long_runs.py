@@ -11,6 +11,7 @@ from parity_util import pair, run_lockstep
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.tape
 def test_rumor_long_run_slot_reuse(oracle, engine):
     cfg = SimConfig(n_members=200, mode=_abi.MODE_RUMOR, churn_per_period=8, gossip_slot_cap=1024)
     o, e = pair(oracle, engine, cfg)
@@ -22,6 +23,7 @@ def test_rumor_long_run_slot_reuse(oracle, engine):
     o.close()
 
 
+@pytest.mark.tape
 def test_full_long_run_slot_reuse(oracle, engine):
     cfg = SimConfig(n_members=120, cluster=ClusterConfig(seedMembers=[0]), gossip_slot_cap=1024)
     o, e = pair(oracle, engine, cfg)
@@ -36,6 +38,7 @@ def test_full_long_run_slot_reuse(oracle, engine):
     o.close()
 
 
+@pytest.mark.tape
 def test_fine_tick_long_run(oracle, engine):
     """A 10 ms tick (gossip interval = 20 ticks, so a slot's lifetime is ~2 000 ticks of the 4 096 its 16-bit holder
     entries allow): slots recycled over 24 000 ticks, bit-exact."""

@@ -444,6 +444,7 @@ def test_sampled_diff_accounting(oracle, engine, profile_all):
     e.close()
 
 
+@pytest.mark.tape
 @pytest.mark.parametrize("world", [1, 3])
 def test_rumor_mode_at_scale_paths(oracle, engine, world):
     """The C5 code paths at test size: implicit views (the PRECONVERGED row and Feistel lists computed, not stored;

@@ -61,6 +61,7 @@ def test_sharded_partition_heal(oracle, engine):
     e.close()
 
 
+@pytest.mark.tape
 def test_sharded_sync_multichunk(oracle, engine):
     """5000 members: 3 payload chunks per row, so clean and dirty chunks of one SYNC payload mix after the kill."""
     cfg = SimConfig(n_members=5000, record_events=True)

@@ -42,8 +42,9 @@ def test_two_process_shards(transport, mode, tmp_path):
             if time.time() - t0 > 240:
                 timed_out = True
                 break
-            time.sleep(5)
-            print(f"[{transport}] {time.time() - t0:.0f}s", flush=True)
+            time.sleep(0.25)
+            if int(time.time() - t0) % 10 == 0:
+                print(f"[{transport}] {time.time() - t0:.0f}s", flush=True)
     finally:
         for p in procs:
             if p.poll() is None:

@@ -29,12 +29,31 @@ while p < end:
         c.unblock_all()
     step = min(int(os.environ.get("C4_CHUNK", "10")), (heal if p < heal else end) - p)
     t0 = time.perf_counter()
-    c.run_periods(step)
-    c.sync()
+    try:
+        c.run_periods(step)
+        c.sync()
+    except Exception as x:  # capacity / memory: report how far it got
+        print(f"N={n} stopped in periods {p}-{p + step}: {x}; device bytes "
+              f"{c.counters()['device_bytes'] / 2**30:.1f} GiB", flush=True)
+        raise SystemExit(2)
     dt = time.perf_counter() - t0
     p += step
     ctr = c.counters()
     print(f"N={n} periods {p - step}-{p}: {dt / step * 1e3:.1f} ms/period, created {ctr['gossips_created']}, "
-          f"events {ctr['events']}, G {ctr['gossip_messages']}", flush=True)
+          f"events {ctr['events']}, G {ctr['gossip_messages']}, device {ctr['device_bytes'] / 2**30:.1f} GiB",
+          flush=True)
+    if os.environ.get("C4_SUSPECT"):  # sampled observers: how much of the other side each one holds SUSPECT
+        import numpy as np
+        half = n // 2
+        obs = list(range(0, half, max(1, half // 16))) + list(range(half, n, max(1, half // 16)))
+        fr = []
+        for o in obs:
+            st = (c.row(o) >> np.uint64(32)) & np.uint64(3)
+            other = st[half:] if o < half else st[:half]
+            own = st[:half] if o < half else st[half:]
+            fr.append(((other == 2).mean(), (own == 1).mean()))  # SUSPECT on the other side, ALIVE on its own
+        fr = np.array(fr)
+        print(f"   SUSPECT share of the other side: min {fr[:, 0].min():.4f} mean {fr[:, 0].mean():.4f}; "
+              f"own side ALIVE min {fr[:, 1].min():.4f}", flush=True)
 print(f"N={n} total {time.perf_counter() - t_all:.1f} s for {end} periods", flush=True)
 c.close()

@@ -11,6 +11,8 @@
 #                     run a trace:W step with the same S / WU first for the kernel times
 #   rehearse:R:N[:W]  bench.py --gpus R on this one GPU (R ranks over RCCL sockets), N members, workload W (default c3)
 #   c4:N              the C4 schedule at N members (tools/exp_c4.py: partition, unblockAll at period 200, run to 320)
+#   tapes             record the oracle tapes of the @pytest.mark.tape tests into $O/tapes
+#   golden:NAME[:P[:T]] record box-sized golden NAME (P periods at most, T seconds) into $O/golden
 #   c5m               rank 0 of 8 C5 slot shards at 10^6 members alone (bench.py --rehearse-shard 8), default caps
 # Example:  gpurun --timeout 1200 -- 'bash tools/gpu_run.sh r4a suite:fullsize smoke bench:c3'
 set -e
@@ -27,11 +29,28 @@ for step in "$@"; do
       k=()
       [ -n "$a" ] && k=(-k "$a")
       rc=0
-      timeout -k 10 1100 python -u -m pytest tests -m gpu -v --durations=25 --timeout 600 --timeout-method thread -p no:cacheprovider \
+      timeout -k 10 1100 python -u -m pytest tests -m gpu -v --durations=${DURATIONS:-25} --timeout 600 --timeout-method thread -p no:cacheprovider \
         "${k[@]}" > $O/tests.log 2>&1 || rc=$?
       tail -n 1 $O/tests.log
       grep -E "^FAILED|^ERROR" $O/tests.log | head -30 || true
       [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc  # 1 = test failures (listed above); anything else ends the call
+      ;;
+    tapes)
+      # record the oracle tapes of the @pytest.mark.tape tests (tests/tape.py): the tests run against the live oracle
+      rc=0
+      SWIM_ORACLE_TAPE=record SWIM_TAPE_OUT=$O/tapes timeout -k 10 1000 python -u -m pytest tests -m "gpu and tape" -v \
+        --durations=0 --timeout 600 --timeout-method thread -p no:cacheprovider > $O/tapes.log 2>&1 || rc=$?
+      tail -n 1 $O/tapes.log
+      grep -E "^FAILED|^ERROR" $O/tapes.log | head -30 || true
+      [ $rc -eq 0 ] || exit $rc
+      ;;
+    golden)
+      # a box-sized golden fixture from the oracle on this host (tools/record_golden_box.py); b = max periods
+      rc=0
+      timeout -k 10 ${c:-1000} python3 -u tools/record_golden_box.py $a ${b:+--max-periods $b} --out $O/golden \
+        > $O/golden_$a.log 2>&1 || rc=$?
+      tail -n 3 $O/golden_$a.log
+      [ $rc -eq 0 ] || [ $rc -eq 3 ] || exit $rc  # 3: the memory guard stopped it (finished periods are saved)
       ;;
     smoke)
       timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
@@ -79,6 +98,14 @@ for step in "$@"; do
     c4)
       timeout -k 10 900 python3 -u tools/exp_c4.py $a 200 320 > $O/c4_$a.log 2>&1 || { tail -3 $O/c4_$a.log; exit 1; }
       tail -2 $O/c4_$a.log
+      ;;
+    c4s)
+      # the C4 partition phase at a members, one line per period to period b, with sampled SUSPECT coverage (exit 2: a
+      # capacity or allocation error ended it, reported in the log)
+      rc=0
+      C4_CHUNK=1 C4_SUSPECT=1 timeout -k 10 ${c:-900} python3 -u tools/exp_c4.py $a 200 $b > $O/c4s_$a.log 2>&1 || rc=$?
+      tail -n 4 $O/c4s_$a.log
+      [ $rc -eq 0 ] || [ $rc -eq 2 ] || exit $rc
       ;;
     c5m)
       timeout -k 10 900 python3 -u bench.py --workload c5 --members 1000000 --rehearse-shard 8 --steps 3 --warmup 25 \
