@@ -1860,7 +1860,9 @@ __device__ void inbox_member(const Dev& d, uint32_t m, uint32_t k, uint32_t lane
   L.tlast = d.hv_tlast[li];
   if (d.ackres && d.tl_tick[(size_t)(k & 1) * d.NL + li] == k) L.ntl = d.tl_n[(size_t)(k & 1) * d.NL + li];
   const uint32_t off = d.rc_off[m], n = d.rc_cnt[m];
-  if (L.pend != NEVER) {  // a SYNC / SYNC_ACK of this tick still carries the live row: its snapshot, copied by the wave
+  // a SYNC / SYNC_ACK of this tick still carries the live row: its snapshot, copied by the wave before the first batch
+  // that may write the row (an accepted receipt's key is above the row's; lane 0's receipts may write), not before
+  auto snapshot = [&]() {
     const uint32_t b = k & 1;
     uint32_t r = 0;
     if (lane == 0) r = atomicAdd(&d.arena_used[b], 1u);
@@ -1876,7 +1878,7 @@ __device__ void inbox_member(const Dev& d, uint32_t m, uint32_t k, uint32_t lane
     }
     L.pend = NEVER;
     __threadfence_block();
-  }
+  };
   for (uint32_t pos = 0; pos < n;) {
     const uint32_t j = pos + lane;
     const bool act = j < n;
@@ -1890,6 +1892,7 @@ __device__ void inbox_member(const Dev& d, uint32_t m, uint32_t k, uint32_t lane
     const unsigned long long slow = __ballot(act && !fast);
     const uint32_t f = slow ? (uint32_t)__ffsll((long long)slow) - 1u : 64u;
     const uint32_t cnt = min(f, n - pos);
+    if (L.pend != NEVER && __ballot((lane < cnt && key32(key) > k0) || (f < 64u && lane == f))) snapshot();
     if (cnt) inbox_batch(L, lane, cnt, s, s1, i1, k0, a0, k >= dt);
     __threadfence_block();  // the batch's row writes, before any lane reads the row again
     if (f == 64u) {
