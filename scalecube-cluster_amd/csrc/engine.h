@@ -314,9 +314,7 @@ struct Dev {
   uint32_t* tlog;     // [2][NL][TL]
   uint32_t* tl_n;     // [2][NL]
   uint32_t* tl_tick;  // [2][NL]
-  // [MSGCAP] the messages k_sync_diff streams (k_ack_resolve): {message, sender row, receiver row, DL_*}, so that a
-  // diff item's first load is its data (no dependent load of the message record before it)
-  uint4* dlist;
+  uint32_t* dlist;    // [MSGCAP]
   uint32_t* ndl;
   // W > 1: the sender's write-log prefix (SyncMsg.tln entries) of each message of the inbound list committed this tick,
   // by its index there: copied by k_pack_all for this shard's senders and shipped in exchange A for the peers'

@@ -307,32 +307,21 @@ __global__ void __launch_bounds__(256) k_seg_sort(uint64_t* key, uint32_t* val, 
 // chunk if it differs from the baseline, else the baseline
 // pinw: the arena row a live-row payload is copied into while it streams (pin_msg), else NEVER; loaded here with the
 // item's data so that no dependent load of the message waits at the top of the item's iteration
-// a streamed message's descriptor (Dev::dlist): .x = the message index | DL_* flags, .y / .z the sender's and
-// receiver's rows. DL_NARROW = a live-row payload on one GPU with the 16-bit shadow plane, not pinned and not delayed
-// (the narrow item below); DL_DESC = .y / .z are valid (else diff_fetch reads the message itself)
-constexpr uint32_t DL_NARROW = 1u << 31, DL_DESC = 1u << 30, DL_MSG = DL_DESC - 1u;
 // narrow (one GPU, a live-row payload that is not pinned): the item is chunks c and c + 1 of the message, lane i
 // the 16 subjects c CH + 16 i ..., and x holds their 16-bit shadow keys (key16): payload x[0..1], receiver x[2..3],
 // the same 64 B per lane in flight as one chunk of 4-B keys. Every lane of the block takes the same item, so the mode
 // is uniform.
 template <bool SHARDED>
-__device__ __forceinline__ void diff_fetch(const Dev& d, uint32_t b, const uint4& ds, uint32_t c, uint4 (&x)[4],
+__device__ __forceinline__ void diff_fetch(const Dev& d, uint32_t b, uint32_t mi, uint32_t c, uint4 (&x)[4],
                                            uint32_t& pinw, bool& narrow) {
+  const SyncMsg& mm = d.msgs[b][mi];
   pinw = NEVER;
   narrow = false;
-  const uint32_t mi = ds.x & DL_MSG;
-  const SyncMsg* mp = (ds.x & DL_DESC) ? nullptr : &d.msgs[b][mi];  // no descriptor: the message itself
-  uint32_t srow = ds.y, drow = ds.z;
-  if (!SHARDED && mp && d.rowk16 && mp->payload == NEVER && mp->pin == NEVER && !(mp->kind & KF_DEFER)) {
-    narrow = true;
-    srow = (uint32_t)lidx(d, mp->src);
-    drow = (uint32_t)lidx(d, mp->dst);
-  }
-  if (!SHARDED && (narrow || (ds.x & DL_NARROW))) {
+  if (!SHARDED && d.rowk16 && mm.payload == NEVER && mm.pin == NEVER && !(mm.kind & KF_DEFER)) {
     narrow = true;
     const uint32_t n0 = c * CH + threadIdx.x * 16;  // NS is a multiple of 8: 8-subject groups are wholly in or out
-    const uint16_t* p16 = d.rowk16 + (size_t)srow * d.NS + n0;
-    const uint16_t* r16 = d.rowk16 + (size_t)drow * d.NS + n0;
+    const uint16_t* p16 = d.rowk16 + lidx(d, mm.src) * d.NS + n0;
+    const uint16_t* r16 = d.rowk16 + lidx(d, mm.dst) * d.NS + n0;
     const uint4 z = make_uint4(0, 0, 0, 0);
     x[0] = n0 < d.NS ? ld_c4((const uint32_t*)p16) : z;
     x[1] = n0 + 8 < d.NS ? ld_c4((const uint32_t*)(p16 + 8)) : z;
@@ -340,7 +329,6 @@ __device__ __forceinline__ void diff_fetch(const Dev& d, uint32_t b, const uint4
     x[3] = n0 + 8 < d.NS ? ld_c4((const uint32_t*)(r16 + 8)) : z;
     return;
   }
-  const SyncMsg& mm = d.msgs[b][mi];
   const uint32_t s0 = c * CH + threadIdx.x * 8;
   // NS is a multiple of 8: a 32-B group is wholly in or out; padding entries are 0 (absent). A delayed message
   // (KF_DEFER) is merged in a later tick: nothing to compare now
@@ -508,33 +496,27 @@ __device__ __forceinline__ void diff_wave16(const Dev& d, uint32_t b, uint32_t m
 // grid-stride, with the next item's loads in flight while the current one is tested. An item is PER chunks of a
 // message (2 on one GPU: a narrow item's 16-bit keys; a wide item's second chunk is loaded when the first is done)
 template <bool SHARDED>
-__device__ __forceinline__ void stream_list(const Dev& d, uint32_t b, const uint4* dlp, uint32_t nmsg, uint32_t blk,
+__device__ __forceinline__ void stream_list(const Dev& d, uint32_t b, const uint32_t* dlp, uint32_t nmsg, uint32_t blk,
                                             uint32_t nblk, uint32_t* scan, uint32_t& base, uint32_t timed) {
   constexpr uint32_t PER = SHARDED ? 1u : 2u;
   const uint32_t nch = d.NCHUNK, nit = (nch + PER - 1) / PER;
   const uint32_t total = nmsg * nit;
-  // item w's descriptor: the stream list's entry (k_ack_resolve), else just the message index (diff_fetch reads it)
-  auto desc = [&](uint32_t w) {
-    if (!dlp) return make_uint4(w / nit, 0u, 0u, 0u);
-    const uint4 e = dlp[w / nit];
-    return make_uint4(e.x, e.y, e.z, 0u);  // (.w unused: three registers per descriptor in flight)
-  };
   uint4 cur[4];
-  uint32_t pcur = NEVER;
+  uint32_t mcur = 0, pcur = NEVER;
   bool ncur = false;
-  uint4 dcur = make_uint4(0, 0, 0, 0), dnxt = dcur;
   if (blk < total) {
-    dcur = desc(blk);
-    if (blk + nblk < total) dnxt = desc(blk + nblk);  // (one item ahead of its data: its load is off the data's chain)
-    diff_fetch<SHARDED>(d, b, dcur, (blk % nit) * PER, cur, pcur, ncur);
+    mcur = dlp ? dlp[blk / nit] : blk / nit;
+    diff_fetch<SHARDED>(d, b, mcur, (blk % nit) * PER, cur, pcur, ncur);
   }
   for (uint32_t w = blk; w < total; w += nblk) {
     uint4 nxt[4];
-    uint32_t pnxt = NEVER;
+    uint32_t mnxt = 0, pnxt = NEVER;
     bool nnxt = false;
-    const uint4 dnn = w + 2 * nblk < total ? desc(w + 2 * nblk) : make_uint4(0, 0, 0, 0);
-    if (w + nblk < total) diff_fetch<SHARDED>(d, b, dnxt, ((w + nblk) % nit) * PER, nxt, pnxt, nnxt);
-    const uint32_t mi = dcur.x & DL_MSG, c0 = (w % nit) * PER;
+    if (w + nblk < total) {
+      mnxt = dlp ? dlp[(w + nblk) / nit] : (w + nblk) / nit;
+      diff_fetch<SHARDED>(d, b, mnxt, ((w + nblk) % nit) * PER, nxt, pnxt, nnxt);
+    }
+    const uint32_t mi = mcur, c0 = (w % nit) * PER;
     if (!SHARDED && !ncur && c0 == 0 && threadIdx.x == 0 && d.rowk16) {  // priced at 8 B per subject (swim_counters)
       atomicAdd(&d.ctr[C_DIFFWIDE_ALL], 1ull);
       if (timed) atomicAdd(&d.ctr[C_DIFFWIDE], 1ull);
@@ -550,7 +532,7 @@ __device__ __forceinline__ void stream_list(const Dev& d, uint32_t b, const uint
         uint32_t p[8], r[8];
         if (h > 0) {  // a wide item's later chunk
           bool nw;
-          diff_fetch<SHARDED>(d, b, dcur, c, cur, pcur, nw);
+          diff_fetch<SHARDED>(d, b, mi, c, cur, pcur, nw);
         }
         if (pcur != NEVER && s0 < d.NS) {  // a live-row payload read again later (pin_msg)
           uint4* dst = (uint4*)(d.arena[b] + (size_t)pcur * d.NS + s0);
@@ -569,16 +551,15 @@ __device__ __forceinline__ void stream_list(const Dev& d, uint32_t b, const uint
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
+    mcur = mnxt;
     pcur = pnxt;
     ncur = nnxt;
-    dcur = dnxt;
-    dnxt = dnn;
   }
 }
 
 // k_sync_diff: the diff of every payload streamed this tick (see diff_fetch and stream_list above)
 template <bool SHARDED>
-__global__ void __launch_bounds__(256, 7) k_sync_diff(const Dev* __restrict__ dp, uint32_t b, uint32_t timed, uint32_t spec) {
+__global__ void __launch_bounds__(256, 8) k_sync_diff(const Dev* __restrict__ dp, uint32_t b, uint32_t timed, uint32_t spec) {
   const Dev& d = *dp;  // global, not kernarg (as k_member_tick): a by-value Dev of this size was copied to scratch
   if (spec && *(volatile uint32_t*)d.halt) return;  // a speculative batch halted at an earlier tick
   __shared__ uint32_t scan[256];
@@ -614,15 +595,13 @@ __global__ void __launch_bounds__(256, 7) k_sync_diff(const Dev* __restrict__ dp
 struct ResArgs {
   const uint32_t *halt, *nmsg, *tl_tick, *tl_n, *tlog, *rowk, *arena;
   SyncMsg* msgs;
-  uint4* dlist;
-  uint32_t *ndl, *chunk_meta, *pool_used, *err;
+  uint32_t *dlist, *ndl, *chunk_meta, *pool_used, *err;
   uint64_t* pool;
   unsigned long long* ctr;
   uint32_t NL, NS, MSGCAP, NCHUNK, POOLCAP, NMETA;
   // W > 1: this shard's first observer, the senders' log prefixes by message (Dev::mlog), and the received payloads
   // (baseline row + shipped chunks, as diff_fetch reads them)
   uint32_t lo, W, MW;
-  uint32_t narrow;  // W == 1 with the 16-bit shadow plane: live-row payloads stream as narrow items (DL_NARROW)
   const uint32_t *mlog, *base_row;
   const uint64_t *rx_mask, *rx_off;
   const uint8_t* xa_recv;
@@ -642,14 +621,11 @@ __device__ __forceinline__ uint32_t res_payload_key(const ResArgs& d, uint32_t p
 }
 // one SYNC_ACK (message i of buffer d.msgs) by one wave: true if it was resolved from the write logs (its candidates
 // written), false if k_sync_diff must stream it
-// (ds: the message's k_sync_diff descriptor, for the stream list when it is not resolved here)
 __device__ __forceinline__ bool res_wave(const ResArgs& d, uint32_t i, uint32_t k, uint32_t lane, volatile uint32_t* sv,
-                                         volatile uint32_t* sc, uint4& ds) {
+                                         volatile uint32_t* sc) {
   const SyncMsg& mm = d.msgs[i];
-  const uint32_t kind = mm.kind, src = mm.src, dst = mm.dst, tln = mm.tln, pay = mm.payload, pin = mm.pin;
-  ds = make_uint4(i | DL_DESC | (d.narrow && pay == NEVER && pin == NEVER && !(kind & KF_DEFER) ? DL_NARROW : 0u),
-                  src - d.lo, dst - d.lo, 0u);
-  bool res = k >= 2 && (kind & KF_RES) && !(kind & KF_DEFER) && pin == NEVER && tln <= TL;
+  const uint32_t kind = mm.kind, src = mm.src, dst = mm.dst, tln = mm.tln, pay = mm.payload;
+  bool res = k >= 2 && (kind & KF_RES) && !(kind & KF_DEFER) && mm.pin == NEVER && tln <= TL;
   uint32_t n0 = 0, n1 = 0;  // A's log entries of ticks k-2 and k-1
   const uint32_t ld = dst - d.lo;  // the requester: an observer of this shard
   if (res) {
@@ -719,8 +695,7 @@ __device__ __forceinline__ bool res_wave(const ResArgs& d, uint32_t i, uint32_t 
 __global__ void __launch_bounds__(512) k_ack_resolve(ResArgs d, uint32_t k, uint32_t spec, uint32_t timed) {
   if (spec && *(volatile uint32_t*)d.halt) return;
   __shared__ uint32_t sv_[8][64], sc_[8][64];
-  __shared__ uint4 slist[8];
-  __shared__ uint32_t nstream, nres, sbase;
+  __shared__ uint32_t slist[8], nstream, nres, sbase;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   volatile uint32_t* sv = sv_[wv];  // this wave's lists (volatile: read across lanes)
   volatile uint32_t* sc = sc_[wv];
@@ -732,11 +707,10 @@ __global__ void __launch_bounds__(512) k_ack_resolve(ResArgs d, uint32_t k, uint
     __syncthreads();
     const uint32_t i = base + wv;
     if (i < nmsg) {  // wave-uniform
-      uint4 ds;
-      if (res_wave(d, i, k, lane, sv, sc, ds)) {
+      if (res_wave(d, i, k, lane, sv, sc)) {
         if (lane == 0) atomicAdd(&nres, 1u);
       } else if (lane == 0) {
-        slist[atomicAdd(&nstream, 1u)] = ds;
+        slist[atomicAdd(&nstream, 1u)] = i;
       }
     }
     __syncthreads();
@@ -863,11 +837,11 @@ void launch_init(const Dev& d, void* stream) {
 }
 
 // timed: this launch is bracketed by profiling events; it adds its message count to ctr[C_DIFFMSG]
-// 7 resident blocks per CU on 256 CUs; SWIM_DIFF_GRID overrides it (measurements; a value that does not parse, or 0, keeps 2048)
+// 8 resident blocks per CU; SWIM_DIFF_GRID overrides it (measurements; a value that does not parse, or 0, keeps 2048)
 static uint32_t diff_grid() {
   const char* e = getenv("SWIM_DIFF_GRID");
   const unsigned long v = e ? strtoul(e, nullptr, 0) : 0ul;
-  return v >= 1 && v <= (1ul << 20) ? (uint32_t)v : 7u * 256u;  // every block resident at once (launch bounds)
+  return v >= 1 && v <= (1ul << 20) ? (uint32_t)v : 2048u;
 }
 
 // a timed launch carries its start / stop events in its own dispatch (hipExtLaunchKernelGGL): the interval is the
@@ -896,8 +870,7 @@ static void launch_ack_resolve(const Dev& d, uint32_t k, hipStream_t st, bool sp
   const uint32_t b = (k - 1) & 1;
   const ResArgs ra{d.halt, d.nmsg + b, d.tl_tick, d.tl_n, d.tlog, d.rowk, d.arena[b], d.msgs[b], d.dlist, d.ndl,
                    d.chunk_meta, d.pool_used, d.err, d.pool, d.ctr, d.NL, d.NS, d.MSGCAP, d.NCHUNK, d.POOLCAP, d.NMETA,
-                   d.lo, d.W, d.MW, d.W == 1 && d.rowk16 ? 1u : 0u, d.mlog, d.base_row, d.rx_mask, d.rx_off,
-                   d.xa_recv};
+                   d.lo, d.W, d.MW, d.mlog, d.base_row, d.rx_mask, d.rx_off, d.xa_recv};
   hipLaunchKernelGGL(k_ack_resolve, dim3(128), dim3(512), 0, st, ra, k, spec ? 1u : 0u, timed ? 1u : 0u);
 }
 

@@ -75,12 +75,69 @@ def test_c2_configured_size_golden(engine, shards):
     assert len(want["periods"]) > 3
 
 
-def c4_side_status(c, n, observers):
-    """For each observer: the share of the other side it holds SUSPECT, and of its own side ALIVE."""
+def c4_sides(c, n):
+    """Every observer's table against the two sides of the partition (A = [0, n/2), B = the rest): per observer, the
+    members of its own side it holds ALIVE, of the other side SUSPECT, and of the other side absent (removed)."""
     half = n // 2
-    out = []
-    for o in observers:
+    out = np.zeros((n, 3), dtype=np.int64)
+    for o in range(n):
         st = (c.row(o) >> np.uint64(32)) & np.uint64(3)
-        other, own = (st[half:], st[:half]) if o < half else (st[:half], st[half:])
-        out.append(((other == 2).mean(), (own == 1).mean(), int((st == 0).sum())))
+        own, other = (st[:half], st[half:]) if o < half else (st[half:], st[:half])
+        out[o] = ((own == 1).sum(), (other == 2).sum(), (other == 0).sum())
     return out
+
+
+def test_c4_configured_size_golden(engine):
+    """C4 at its configured 50 000 members through the periods the oracle's memory held on the GPU box: the partition
+    from period 0, the first ping and ping-req timeouts across it (SUSPECT records and their gossips)."""
+    c, want = replay(engine, "c4_50k")
+    sides = [c.row(o) for o in (0, 24_999, 25_000, 49_999)]
+    c.close()
+    last = dict(zip(COUNTERS, want["periods"][-1]["counters"]))
+    assert last["gossips_created"] > 10_000 and last["events"] == 0, last  # the SUSPECT wave has started
+    for o, row in zip((0, 24_999, 25_000, 49_999), sides):
+        st = (row >> np.uint64(32)) & np.uint64(3)
+        own = st[:25_000] if o < 25_000 else st[25_000:]
+        assert (own == 1).all(), o  # no member suspects its own side
+
+
+def test_c4_long_partition_no_recovery_2000(engine):
+    """MembershipProtocolTest.testLongNetworkPartitionNoRecovery (MembershipProtocolTest.java:313-366) on the C4 shape
+    at 2 000 members, engine only: two halves blocked both ways from period 0. After the SUSPECT wave every member
+    trusts its own side and suspects the whole other side; after the suspicion timeout (5 x ceilLog2(2000) = 55
+    periods, ClusterMath.suspicionTimeout) and the DEAD-gossip storm it trusts its own side and the other side is
+    gone: N x N/2 REMOVED events, nobody suspected."""
+    from swimhip import ClusterConfig, SimConfig
+    n = 2000
+    c = SimulatedCluster(engine, SimConfig(n_members=n, cluster=ClusterConfig(seedMembers=[0]), record_events=True,
+                                           event_cap=1 << 22, pending_fetch_cap=4096, list_slack=4096))
+    c.partition([0] * (n // 2) + [1] * (n // 2))
+    c.run_periods(30)
+    s = c4_sides(c, n)
+    assert (s[:, 0] == n // 2).all() and (s[:, 1] == n // 2).all(), s.min(axis=0)
+    c.run_periods(50)  # period 80: every suspicion timer has fired
+    s = c4_sides(c, n)
+    ev = c.events()
+    c.close()
+    assert (s[:, 0] == n // 2).all() and (s[:, 1] == 0).all() and (s[:, 2] == n // 2).all(), s.min(axis=0)
+    removed = [e for e in ev if e.isRemoved()]
+    assert len(removed) == n * (n // 2) and len(ev) == len(removed)
+    half = n // 2
+    assert all((e.observer < half) != (e.member < half) for e in removed)  # only the other side is removed
+
+
+def test_c4_suspect_wave_8000(engine):
+    """The C4 partition phase at 8 000 members (16 % of the configured size), engine only, to period 64, the last
+    period before the first suspicion timer (5 x ceilLog2(8000) = 65 periods) can fire: every member holds its own side
+    ALIVE and the whole other side SUSPECT (testLongNetworkPartitionNoRecovery's middle assertion), no event yet."""
+    from swimhip import ClusterConfig, SimConfig
+    n = 8000
+    c = SimulatedCluster(engine, SimConfig(n_members=n, cluster=ClusterConfig(seedMembers=[0]), record_events=True,
+                                           pending_fetch_cap=4096, list_slack=4096))
+    c.partition([0] * (n // 2) + [1] * (n // 2))
+    c.run_periods(64)
+    s = c4_sides(c, n)
+    ctr = c.counters()
+    c.close()
+    assert (s[:, 0] == n // 2).all() and (s[:, 1] == n // 2).all(), s.min(axis=0)
+    assert ctr["events"] == 0 and ctr["gossips_created"] > 100_000, ctr
