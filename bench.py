@@ -302,6 +302,14 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                          "algorithmic_bytes_per_launch": bytes_per_launch,
                          "avg_launch_us": diff_s * 1e6 / launches,
+                         # the same launches priced by SURVEY.md §8d's model (16 B per record compare: 8-B keys read
+                         # on both sides), which predates the 4-B key plane and its 2-B shadow: above 1 means the
+                         # engine reads fewer bytes per compare than that model assumes, not that it skips compares
+                         "survey_8d_model": {
+                             "bytes_per_compare": 16,
+                             "bytes_per_launch": 16 * n * d["diff_msgs"] / launches,
+                             "achieved": 16 * n * d["diff_msgs"] / diff_s / 1e9 if diff_s > 0 else 0.0,
+                             "frac": (16 * n * d["diff_msgs"] / diff_s / 1e9 / HBM_PEAK_GBPS) if diff_s > 0 else 0.0},
                          "traffic": traffic_from_profiles(n) if world == 1 else None,
                          "traffic_source": "committed rocprofv3 PMC summary profiles/pmc_sync_diff_k16.json (FETCH_SIZE x 2 "
                                            "+ WRITE_SIZE per launch), not measured in this run"},

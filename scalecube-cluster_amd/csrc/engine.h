@@ -126,7 +126,10 @@ constexpr uint32_t KF_ABS = 0x200u;
 // k_sync_diff streaming it (cleared there when it cannot)
 constexpr uint32_t KF_RES = 0x400u;
 constexpr uint32_t KF_LATE = 0x800u;  // a delayed message put back by k_sync_redeliver
-constexpr uint32_t KF_FLAGS = KF_DEFER | KF_ABS | KF_RES | KF_LATE;
+// k_ack_resolve (W == 1 or a shard, with SYNC_ACK resolution) has looked up whether the sender is dead at the
+// delivery tick (dead_tick is fixed within a tick): the receiver's answer skips that dependent load (xmit_ep's `dd`)
+constexpr uint32_t KF_SRCLIVE = 0x1000u, KF_SRCDEAD = 0x2000u;
+constexpr uint32_t KF_FLAGS = KF_DEFER | KF_ABS | KF_RES | KF_LATE | KF_SRCLIVE | KF_SRCDEAD;
 constexpr uint32_t TL = 16;  // per-member tick write log (ack resolution); past it the member's ACKs are streamed
 // exchange A's SYNC entry: the message, its first chunk slot + pad, the chunk mask, the sender's write-log prefix
 __host__ __device__ __forceinline__ uint64_t sync_entry_size(uint32_t MW) { return sizeof(SyncMsg) + 8 + 8ull * MW + 4ull * TL; }

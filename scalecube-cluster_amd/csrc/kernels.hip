@@ -593,7 +593,7 @@ __global__ void __launch_bounds__(256, 8) k_sync_diff(const Dev* __restrict__ dp
 // the fields k_ack_resolve reads, passed as kernel arguments: through Dev* every one of them was a dependent load of
 // its own before the loads that use it (the kernel is a chain of short dependent loads)
 struct ResArgs {
-  const uint32_t *halt, *nmsg, *tl_tick, *tl_n, *tlog, *rowk, *arena;
+  const uint32_t *halt, *nmsg, *tl_tick, *tl_n, *tlog, *rowk, *arena, *dead_tick;
   SyncMsg* msgs;
   uint32_t *dlist, *ndl, *chunk_meta, *pool_used, *err;
   uint64_t* pool;
@@ -625,6 +625,8 @@ __device__ __forceinline__ bool res_wave(const ResArgs& d, uint32_t i, uint32_t 
                                          volatile uint32_t* sc) {
   const SyncMsg& mm = d.msgs[i];
   const uint32_t kind = mm.kind, src = mm.src, dst = mm.dst, tln = mm.tln, pay = mm.payload;
+  if (lane == 0 && !(kind & KF_DEFER))  // the sender's liveness at this tick, for the receiver's answer (KF_SRCLIVE)
+    d.msgs[i].kind = (kind & ~(KF_SRCLIVE | KF_SRCDEAD)) | (k >= d.dead_tick[src] ? KF_SRCDEAD : KF_SRCLIVE);
   bool res = k >= 2 && (kind & KF_RES) && !(kind & KF_DEFER) && mm.pin == NEVER && tln <= TL;
   uint32_t n0 = 0, n1 = 0;  // A's log entries of ticks k-2 and k-1
   const uint32_t ld = dst - d.lo;  // the requester: an observer of this shard
@@ -868,7 +870,7 @@ static void launch_sync_diff(const Dev& d, uint32_t b, hipStream_t st, uint32_t 
 static void launch_ack_resolve(const Dev& d, uint32_t k, hipStream_t st, bool spec, bool timed) {
   if (k == 0 || !d.ackres) return;
   const uint32_t b = (k - 1) & 1;
-  const ResArgs ra{d.halt, d.nmsg + b, d.tl_tick, d.tl_n, d.tlog, d.rowk, d.arena[b], d.msgs[b], d.dlist, d.ndl,
+  const ResArgs ra{d.halt, d.nmsg + b, d.tl_tick, d.tl_n, d.tlog, d.rowk, d.arena[b], d.dead_tick, d.msgs[b], d.dlist, d.ndl,
                    d.chunk_meta, d.pool_used, d.err, d.pool, d.ctr, d.NL, d.NS, d.MSGCAP, d.NCHUNK, d.POOLCAP, d.NMETA,
                    d.lo, d.W, d.MW, d.mlog, d.base_row, d.rx_mask, d.rx_off, d.xa_recv};
   hipLaunchKernelGGL(k_ack_resolve, dim3(128), dim3(512), 0, st, ra, k, spec ? 1u : 0u, timed ? 1u : 0u);

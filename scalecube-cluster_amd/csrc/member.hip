@@ -188,12 +188,13 @@ __device__ __forceinline__ void row_put(ML& L, uint32_t s, uint64_t v) { row_put
 
 // prepareSyncDataMsg (MembershipProtocolImpl.java:446-454) + transport.send; false if the send failed
 // res: a SYNC_ACK sent in the tick its SYNC was merged (k_ack_resolve may derive its diff from the write logs)
+// dd: whether dst is dead at this tick when the caller knows it (KF_SRCLIVE / KF_SRCDEAD), -1: look it up
 __device__ __forceinline__ bool send_sync(ML& L, uint32_t kind, uint32_t dst, uint32_t ciss, uint32_t ccnt,
-                                          bool res = false) {
+                                          bool res = false, int dd = -1) {
   const Dev& d = *L.d;
   uint32_t seq = L.syncSeq++;
   L.c[C_M]++;
-  const int e = xmit_ep(d, L.ep, kind, L.m, dst, L.k, L.m, seq);
+  const int e = xmit_ep(d, L.ep, kind, L.m, dst, L.k, L.m, seq, dd);
   if (e < 0) {
     L.c[C_LOST]++;
     return false;
@@ -1006,8 +1007,10 @@ __device__ __forceinline__ void merge_payload(ML& L, uint32_t mi, uint32_t reaso
 // control path of k_member_tick this tick, and its work class: 1 = a ping is due and nothing else, 2 = only
 // request-state events (ping hops, ack arrivals, timeouts), 3 = both, 0 = anything else (SYNC receipt, gossip
 // receipts or round, timers, host requests, start).
+// head: the member's inbound SYNC / SYNC_ACK list (P1), NEVER for a dead member: passed to its body through LDS, so
+// that the body's first message loads go out with its state loads
 __device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t k, uint32_t& cls, uint32_t& drops,
-                                              uint32_t& evs) {
+                                              uint32_t& evs, uint32_t& head) {
   // A dead member does nothing itself, but the remote hops of its in-flight requests still run at the live
   // responders (their sends fail against the dead issuer), so those hops are still evaluated for the counters.
   // every word is loaded up front (no short-circuit chain of dependent loads); the SoA loads coalesce per wave
@@ -1018,6 +1021,7 @@ __device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t
   const bool dead = k >= dt;
   cls = 0;
   drops = 0;
+  head = (!dead && k > 0) ? mh : NEVER;
   if (d.fastp4) {  // RUMOR mode: P4's GOSSIP events of this tick, hashed and counted when they were applied
     const uint32_t pn = d.evp_n[m];
     if (pn) {
@@ -1173,9 +1177,10 @@ __device__ __forceinline__ void ml_store(const ML& L) {
 // gossip receipts stops before P4 and is listed for k_inbox_apply (P4, a wave per member) and the resumed launch;
 // BODY_RESUME = P5 and P6 of a listed member (its P0-P4 ran in the two launches before)
 enum : uint32_t { BODY_FULL = 0, BODY_SPLIT = 1, BODY_RESUME = 2 };
+// head: the inbound list head the triage read (BODY_RESUME: none)
 template <uint32_t mode>
 __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint32_t k, unsigned long long (&cnt)[8],
-                                                 uint4* cw, uint32_t* cw_n, bool spec) {
+                                                 uint4* cw, uint32_t* cw_n, bool spec, uint32_t head) {
   const bool dead = dead_at(d, m, k);
   ML L;
   ml_init(L, d, m, k, cw, cw_n, spec);
@@ -1185,8 +1190,16 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
     L.tlast = d.hv_tlast[li];
     if (d.ackres && d.tl_tick[(size_t)(k & 1) * d.NL + li] == k) L.ntl = d.tl_n[(size_t)(k & 1) * d.NL + li];
   }
-  // P1's inbound list head, loaded with the state above (P0's sends link into the other buffer)
-  const uint32_t head0 = (mode != BODY_RESUME && !dead && k > 0) ? d.m_head[(size_t)((k - 1) & 1) * d.N + m] : NEVER;
+  // P1's inbound list head from the triage, and its first message's sort key and link loaded with the state above
+  // (P0's sends link into the other buffer)
+  const uint32_t head0 = (mode != BODY_RESUME && !dead && k > 0) ? head : NEVER;
+  uint64_t key0 = 0;
+  uint32_t next0 = NEVER;
+  if (head0 != NEVER) {
+    const SyncMsg& m0 = d.msgs[(k - 1) & 1][head0];
+    key0 = ((uint64_t)m0.src << 32) | m0.seq;
+    next0 = d.m_next[(size_t)((k - 1) & 1) * d.MSGCAP + head0];
+  }
   // the P6 ping's target and its liveness, loaded now (do_ping's loads would wait for this tick's stores)
   if (!dead && k == L.nextPing && L.fdLen > 0 && L.pingIdx >= 0 && L.pingIdx < (int32_t)L.fdLen) {
     L.pre = L.fdl[L.pingIdx];
@@ -1268,14 +1281,14 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
     uint64_t key[MQ];
     uint32_t idx[MQ], n = 0;
     bool more = false;
-    for (uint32_t q = head; q != NEVER; q = mnext[q]) {
+    for (uint32_t q = head; q != NEVER; q = q == head ? next0 : mnext[q]) {
       if (n == d.mq_cap) {
         more = true;
         fb_add(d, FB_MQ);
         break;
       }
       const SyncMsg& mq = d.msgs[pb][q];
-      uint64_t kq = ((uint64_t)mq.src << 32) | mq.seq;
+      uint64_t kq = q == head ? key0 : ((uint64_t)mq.src << 32) | mq.seq;
       uint32_t j = n++;
       while (j > 0 && key[j - 1] > kq) {
         key[j] = key[j - 1];
@@ -1319,7 +1332,8 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
         // the group table's round trips (a free group's fields are never read before alloc_group rewrites them)
         L.c[C_R] += mm.psize;
         L.c[C_SYNCMERGE]++;
-        send_sync(L, K_SYNC_ACK, mm.src, mm.cid_iss, mm.cid_cnt, !(mflags & (KF_ABS | KF_LATE)));
+        send_sync(L, K_SYNC_ACK, mm.src, mm.cid_iss, mm.cid_cnt, !(mflags & (KF_ABS | KF_LATE)),
+                  (mflags & KF_SRCDEAD) ? 1 : (mflags & KF_SRCLIVE) ? 0 : -1);
         continue;
       }
       // one merge_payload / finish site for the three cases (each inlined copy is large)
@@ -1969,7 +1983,7 @@ __global__ void __launch_bounds__(256, 2) k_member_tick_t(const Dev* __restrict_
   unsigned long long* wt = wtime ? d.wt + ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 : nullptr;
   if (wtime && (threadIdx.x & 63) == 0) wt[0] = wall_clock64();
   __shared__ uint32_t wc[4][4];  // [wave][class] busy members
-  __shared__ uint32_t list[256];
+  __shared__ uint32_t list[256], lhead[256];
   __shared__ uint4 cw[CWMAX];  // deferred copy-on-write snapshots of this block's members (cow)
   __shared__ uint32_t cw_n;
   if (threadIdx.x == 0) cw_n = 0;
@@ -1977,7 +1991,8 @@ __global__ void __launch_bounds__(256, 2) k_member_tick_t(const Dev* __restrict_
   constexpr bool resume = MODE == BODY_RESUME;  // the parked members' P5 and P6 (one lane each, from the list)
   const uint32_t m = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t cls = 0, drops = 0, evs = 0;
-  const bool busy = !resume && m < d.hi && member_triage(d, m, k, cls, drops, evs);
+  uint32_t head = NEVER;
+  const bool busy = !resume && m < d.hi && member_triage(d, m, k, cls, drops, evs, head);
   {  // the triage's record compares and folded RUMOR events, one atomic each per wave
     uint32_t v = drops, e = evs;
 #pragma unroll
@@ -2007,9 +2022,13 @@ __global__ void __launch_bounds__(256, 2) k_member_tick_t(const Dev* __restrict_
   for (uint32_t j = 0; j < w; ++j) before += wc[j][cls];
   const uint64_t bal = cls == 0 ? b0 : cls == 1 ? b1 : cls == 2 ? b2 : b3;
   uint32_t slot = start + before + __popcll(bal & ((1ull << lane) - 1ull));
-  if (busy) list[slot] = m | (cls << 30);  // m < 2^30
+  if (busy) {
+    list[slot] = m | (cls << 30);  // m < 2^30
+    lhead[slot] = head;
+  }
   __syncthreads();
   uint32_t ent = list[threadIdx.x];
+  const uint32_t ehead = resume ? NEVER : lhead[threadIdx.x];
   if (resume) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     ent = i < *d.nhv ? d.hv_list[i] : NEVER;  // class 0
@@ -2026,7 +2045,7 @@ __global__ void __launch_bounds__(256, 2) k_member_tick_t(const Dev* __restrict_
     unsigned long long cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const bool skip = ((d.exp & 32) && mcls == 0) || ((d.exp & 64) && mcls != 0);
     if (me != NEVER && !skip)
-      member_tick_body<MODE>(d, me, k, cnt, cw, &cw_n, (flag & 3u) == 3u);
+      member_tick_body<MODE>(d, me, k, cnt, cw, &cw_n, (flag & 3u) == 3u, ehead);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       unsigned long long v = cnt[i];

@@ -4,6 +4,7 @@
 #   smoke             __graft_entry__.smoke()
 #   bench:W[:S[:WU]]  bench.py --workload W (c3 | c3dyn | c2 | c5), S steps, WU warm-up, no CPU baseline
 #   benchcpu          the default bench line with its CPU baseline (the driver's command)
+#   benchc:W[:S[:WU]] bench.py --workload W with its CPU baseline leg
 #   trace:W[:S[:WU]]  rocprofv3 kernel trace + stats of the same bench command, and its per-tick breakdown
 #   pmc:W:COUNTER[:S] one rocprofv3 --pmc pass (one counter) over a bench run of workload W with S steps (default 3)
 #   pmcg:W[:S[:WU]]   the gossip plane's HBM bytes and L2 atomics per kernel and tick: FETCH_SIZE, WRITE_SIZE and
@@ -61,6 +62,12 @@ for step in "$@"; do
         > $O/bench_$a.log 2>&1
       grep metric $O/bench_$a.log > $O/bench_$a.json
       grep -o '"ms_per_step": [0-9.]*' $O/bench_$a.json
+      ;;
+    benchc)
+      # a secondary line (c3dyn / c2 / c5) with its CPU baseline leg
+      timeout -k 10 900 python -u bench.py --workload $a --steps ${b:-20} --warmup ${c:-3} > $O/benchc_$a.log 2>&1
+      grep metric $O/benchc_$a.log > $O/benchc_$a.json
+      grep -o '"ms_per_step": [0-9.]*\|"cpu_baseline": {"value": [0-9.e+]*' $O/benchc_$a.json
       ;;
     benchcpu)
       timeout -k 10 600 python -u bench.py > $O/bench.log 2>&1
