@@ -688,10 +688,8 @@ int build(swim_handle* h) {
   A(d.dead_tick, N)
   A(d.dly_thr, DTAB * 256) A(d.dly_len, DTAB)
   A(d.ep_group, MAX_EPOCHS * N) A(d.md_version, N)
-  A(d.tsize, N) A(d.fdLen, N) A(d.gLen, N) A(d.fdPeriod, N) A(d.gPeriod, N) A(d.gCounter, N) A(d.nextPing, N)
-  A(d.nextGossip, N) A(d.nextSync, N) A(d.cidCnt, N) A(d.syncSeq, N) A(d.evSeq, N) A(d.held, N) A(d.timerMin, N)
-  A(d.initFlags, N) A(d.initDeadline, N) A(d.initCidBase, N) A(d.initN, N) A(d.firstGossip, N) A(d.nsub, N)
-  A(d.npath, N) A(d.nfetch, N) A(d.fnext, N) A(d.pingIdx, N) A(d.remoteIdx, N) A(d.sel, N * 8) A(d.evHash, N)
+  A(d.nextPing, N) A(d.nextGossip, N) A(d.nextSync, N) A(d.held, N) A(d.timerMin, N) A(d.initFlags, N)
+  A(d.firstGossip, N) A(d.ms, N) A(d.sel, N * 8)
   const uint64_t NL = d.NL;  // per-observer arrays: this shard's rows only
   const uint64_t NV = d.implicit ? 1 : NL;  // implicit views: no table or list is stored
   A(d.rowk, NV * d.NS) A(d.rowa, NV * d.NS) A(d.fdl, NV * d.LCAP) A(d.gl, NV * d.LCAP)
@@ -1492,7 +1490,7 @@ int swim_step(swim_handle* h, uint32_t n) {
           for (int q = 0; q < 8; ++q) HIPCK(hipMemcpy(&v[q], src[q], 4, hipMemcpyDeviceToHost));
           std::vector<uint32_t> rc(d.N), nf(d.N);
           HIPCK(hipMemcpy(rc.data(), d.rc_cnt, 4ull * d.N, hipMemcpyDeviceToHost));
-          HIPCK(hipMemcpy(nf.data(), d.nfetch, 4ull * d.N, hipMemcpyDeviceToHost));
+          HIPCK(hipMemcpy2D(nf.data(), 4, &d.ms[0].nfetch, sizeof(MS), 4, d.N, hipMemcpyDeviceToHost));
           std::sort(rc.begin(), rc.end());
           std::sort(nf.begin(), nf.end());
           // first receipts per target with senders this tick (rtail - rt0), and senders per target
@@ -1988,8 +1986,10 @@ int swim_read_lists(swim_handle* h, uint32_t obs, uint32_t* fd, uint32_t* fd_len
   if (!h || obs >= h->d.N || !owns(h, obs)) return SWIM_EINVAL;
   HIPCK(hipStreamSynchronize(h->stream));
   uint32_t fl = 0, glen = 0;
-  HIPCK(hipMemcpy(&fl, h->d.fdLen + obs, 4, hipMemcpyDeviceToHost));
-  HIPCK(hipMemcpy(&glen, h->d.gLen + obs, 4, hipMemcpyDeviceToHost));
+  MS ms;
+  HIPCK(hipMemcpy(&ms, h->d.ms + obs, sizeof(MS), hipMemcpyDeviceToHost));
+  fl = ms.fdLen;
+  glen = ms.gLen;
   if (fl > cap || glen > cap) return SWIM_EINVAL;
   if (h->d.implicit) {  // RUMOR mode: the PRECONVERGED permutations (list_at)
     const FeistelPerm P0 = list_perm(h->d, obs, 0), P1 = list_perm(h->d, obs, 1);
@@ -1999,8 +1999,8 @@ int swim_read_lists(swim_handle* h, uint32_t obs, uint32_t* fd, uint32_t* fd_len
     HIPCK(hipMemcpy(fd, h->d.fdl + lidx(h->d, obs) * h->d.LCAP, 4ull * fl, hipMemcpyDeviceToHost));
     HIPCK(hipMemcpy(gl, h->d.gl + lidx(h->d, obs) * h->d.LCAP, 4ull * glen, hipMemcpyDeviceToHost));
   }
-  HIPCK(hipMemcpy(&cursors[0], h->d.pingIdx + obs, 4, hipMemcpyDeviceToHost));
-  HIPCK(hipMemcpy(&cursors[1], h->d.remoteIdx + obs, 4, hipMemcpyDeviceToHost));
+  cursors[0] = ms.pingIdx;
+  cursors[1] = ms.remoteIdx;
   *fd_len = fl;
   *g_len = glen;
   return SWIM_OK;
@@ -2268,12 +2268,12 @@ int swimdbg_send_log(swim_handle* h, uint32_t* out, size_t cap, size_t* n) {
 int swimdbg_scalars(swim_handle* h, uint32_t m, uint64_t* out) {
   if (!h || !owns(h, m)) return SWIM_EINVAL;
   HIPCK(hipStreamSynchronize(h->stream));
-  uint32_t* src[6] = {h->d.cidCnt, h->d.syncSeq, h->d.gCounter, h->d.nextSync, h->d.fdPeriod, h->d.gPeriod};
-  for (int i = 0; i < 6; ++i) {
-    uint32_t v = 0;
-    HIPCK(hipMemcpy(&v, src[i] + m, 4, hipMemcpyDeviceToHost));
-    out[i] = (i == 3 && v == NEVER) ? ~0ull : v;
-  }
+  MS ms;
+  uint32_t ns = 0;
+  HIPCK(hipMemcpy(&ms, h->d.ms + m, sizeof(MS), hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(&ns, h->d.nextSync + m, 4, hipMemcpyDeviceToHost));
+  const uint32_t v[6] = {ms.cidCnt, ms.syncSeq, ms.gCounter, ns, ms.fdPeriod, ms.gPeriod};
+  for (int i = 0; i < 6; ++i) out[i] = (i == 3 && v[i] == NEVER) ? ~0ull : v[i];
   return SWIM_OK;
 }
 

@@ -126,13 +126,22 @@ constexpr uint32_t KF_ABS = 0x200u;
 // k_sync_diff streaming it (cleared there when it cannot)
 constexpr uint32_t KF_RES = 0x400u;
 constexpr uint32_t KF_LATE = 0x800u;  // a delayed message put back by k_sync_redeliver
-// k_ack_resolve (W == 1 or a shard, with SYNC_ACK resolution) has looked up whether the sender is dead at the
-// delivery tick (dead_tick is fixed within a tick): the receiver's answer skips that dependent load (xmit_ep's `dd`)
-constexpr uint32_t KF_SRCLIVE = 0x1000u, KF_SRCDEAD = 0x2000u;
-constexpr uint32_t KF_FLAGS = KF_DEFER | KF_ABS | KF_RES | KF_LATE | KF_SRCLIVE | KF_SRCDEAD;
+constexpr uint32_t KF_FLAGS = KF_DEFER | KF_ABS | KF_RES | KF_LATE;
 constexpr uint32_t TL = 16;  // per-member tick write log (ack resolution); past it the member's ACKs are streamed
 // exchange A's SYNC entry: the message, its first chunk slot + pad, the chunk mask, the sender's write-log prefix
 __host__ __device__ __forceinline__ uint64_t sync_entry_size(uint32_t MW) { return sizeof(SyncMsg) + 8 + 8ull * MW + 4ull * TL; }
+
+// a member's body-only state (member_tick_body's ML fields): one 128-B line per member
+struct alignas(16) MS {
+  uint32_t tsize, fdLen, gLen, fdPeriod;
+  uint32_t gPeriod, gCounter, cidCnt, syncSeq;
+  uint32_t evSeq, initDeadline, initCidBase, initN;
+  uint32_t nsub, npath, nfetch, fnext;  // fnext: earliest tick at which a pending metadata fetch needs the member
+  int32_t pingIdx, remoteIdx;
+  uint64_t evHash;
+  uint32_t pad[12];
+};
+static_assert(sizeof(MS) == 128, "one cache line per member");
 
 struct Dev {
   // ---- configuration ----
@@ -190,12 +199,13 @@ struct Dev {
   uint32_t* link_hist;  // [LKCAP][LKH][2] (from tick, loss % or LK_NONE), oldest first; [0][0] | LK_TRUNC if older ones dropped
 
   // ---- per member scalars ----
-  uint32_t *tsize, *fdLen, *gLen, *fdPeriod, *gPeriod, *gCounter, *nextPing, *nextGossip, *nextSync, *cidCnt, *syncSeq,
-      *evSeq, *held, *timerMin, *initFlags, *initDeadline, *initCidBase, *initN, *firstGossip, *nsub, *npath, *nfetch,
-      *fnext;  // [N] earliest tick at which a pending metadata fetch needs the member (NEVER: none)
-  int32_t *pingIdx, *remoteIdx;
+  // the triage's words, one array each ([N], coalesced loads over every member of a wave)
+  uint32_t *nextPing, *nextGossip, *nextSync, *held, *timerMin, *initFlags, *firstGossip;
+  // the rest of a member's state, read and written only by its own lane's body: one 128-B record per member (MS),
+  // loaded and stored as five 16-B words, so that the busy members a block compacts into its first waves touch one
+  // cache line each instead of a line per field
+  MS* ms;  // [N]
   uint32_t* sel;  // [N][8]
-  uint64_t* evHash;
 
   uint32_t* rowk;  // [N][NS] key plane: row stride NS = N rounded up to 8 (32-B aligned rows for 16-B loads)
   uint16_t* rowk16;  // [N][NS] or null: the key plane's 16-bit shadow (key16) that k_sync_diff streams for live-row

@@ -26,10 +26,10 @@ __global__ void k_init_members(Dev d) {
   uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= d.N) return;
   bool pre = d.init_mode == 1;
-  d.tsize[m] = pre ? d.N : 1;
-  d.fdLen[m] = pre ? d.N - 1 : 0;
-  d.gLen[m] = pre ? d.N - 1 : 0;
-  d.fdPeriod[m] = d.gPeriod[m] = d.gCounter[m] = 0;
+  d.ms[m].tsize = pre ? d.N : 1;
+  d.ms[m].fdLen = pre ? d.N - 1 : 0;
+  d.ms[m].gLen = pre ? d.N - 1 : 0;
+  d.ms[m].fdPeriod = d.ms[m].gPeriod = d.ms[m].gCounter = 0;
   d.nextPing[m] = pre ? 1 + init_draw(d, m, 1, 0) % d.ping_t : d.ping_t;
   uint32_t ng = pre ? 1 + init_draw(d, m, 2, 0) % d.gossip_t : d.gossip_t;
   d.nextGossip[m] = ng;
@@ -40,15 +40,15 @@ __global__ void k_init_members(Dev d) {
   d.start_tick[m] = (pre || dormant) ? NEVER : 0u;
   d.jseed_n[m] = NONE32;
   d.md_uidx[m] = NONE32;
-  d.cidCnt[m] = d.syncSeq[m] = d.evSeq[m] = d.held[m] = 0;
+  d.ms[m].cidCnt = d.ms[m].syncSeq = d.ms[m].evSeq = d.held[m] = 0;
   d.timerMin[m] = NEVER;
-  d.initFlags[m] = d.initDeadline[m] = d.initCidBase[m] = d.initN[m] = 0;
-  d.nsub[m] = d.npath[m] = d.nfetch[m] = 0;
-  d.fnext[m] = NEVER;
-  d.pingIdx[m] = 0;
-  d.remoteIdx[m] = pre ? 0 : -1;
+  d.initFlags[m] = d.ms[m].initDeadline = d.ms[m].initCidBase = d.ms[m].initN = 0;
+  d.ms[m].nsub = d.ms[m].npath = d.ms[m].nfetch = 0;
+  d.ms[m].fnext = NEVER;
+  d.ms[m].pingIdx = 0;
+  d.ms[m].remoteIdx = pre ? 0 : -1;
   for (int i = 0; i < 8; ++i) d.sel[(size_t)m * 8 + i] = 0;
-  d.evHash[m] = 0;
+  d.ms[m].evHash = 0;
   d.tround[m] = 0;
   d.log_pos[m] = 0;
   d.spchg[m] = 0;
@@ -593,7 +593,7 @@ __global__ void __launch_bounds__(256, 8) k_sync_diff(const Dev* __restrict__ dp
 // the fields k_ack_resolve reads, passed as kernel arguments: through Dev* every one of them was a dependent load of
 // its own before the loads that use it (the kernel is a chain of short dependent loads)
 struct ResArgs {
-  const uint32_t *halt, *nmsg, *tl_tick, *tl_n, *tlog, *rowk, *arena, *dead_tick;
+  const uint32_t *halt, *nmsg, *tl_tick, *tl_n, *tlog, *rowk, *arena;
   SyncMsg* msgs;
   uint32_t *dlist, *ndl, *chunk_meta, *pool_used, *err;
   uint64_t* pool;
@@ -625,8 +625,6 @@ __device__ __forceinline__ bool res_wave(const ResArgs& d, uint32_t i, uint32_t 
                                          volatile uint32_t* sc) {
   const SyncMsg& mm = d.msgs[i];
   const uint32_t kind = mm.kind, src = mm.src, dst = mm.dst, tln = mm.tln, pay = mm.payload;
-  if (lane == 0 && !(kind & KF_DEFER))  // the sender's liveness at this tick, for the receiver's answer (KF_SRCLIVE)
-    d.msgs[i].kind = (kind & ~(KF_SRCLIVE | KF_SRCDEAD)) | (k >= d.dead_tick[src] ? KF_SRCDEAD : KF_SRCLIVE);
   bool res = k >= 2 && (kind & KF_RES) && !(kind & KF_DEFER) && mm.pin == NEVER && tln <= TL;
   uint32_t n0 = 0, n1 = 0;  // A's log entries of ticks k-2 and k-1
   const uint32_t ld = dst - d.lo;  // the requester: an observer of this shard
@@ -738,7 +736,7 @@ __global__ void __launch_bounds__(256) k_hash(Dev d, uint64_t* out, uint32_t now
   unsigned long long hr = 0, hf = 0, hg = 0, hgs = 0;
   const uint32_t* rk = d.rowk + lidx(d, m) * d.NS;
   const uint32_t* ra = d.rowa + lidx(d, m) * d.NS;
-  uint32_t fl = d.fdLen[m], gl = d.gLen[m];
+  uint32_t fl = d.ms[m].fdLen, gl = d.ms[m].gLen;
   if (d.implicit) {  // the PRECONVERGED row and lists, computed (engine.h list_at)
     const FeistelPerm P0 = list_perm(d, m, 0), P1 = list_perm(d, m, 1);
     for (uint32_t s = threadIdx.x; s < d.N; s += blockDim.x) hr += hpair(s, PRE_REC);
@@ -772,13 +770,13 @@ __global__ void __launch_bounds__(256) k_hash(Dev d, uint64_t* out, uint32_t now
   if (threadIdx.x == 0) {
     uint64_t* o6 = out + (size_t)m * 6;
     o6[0] = red[0][0];
-    o6[1] = red[1][0] + mix64((uint64_t)(int64_t)d.pingIdx[m] ^ 0xF00Dull) + fl;
-    o6[2] = red[2][0] + mix64((uint64_t)(int64_t)d.remoteIdx[m] ^ 0xBEEFull) + gl;
-    o6[3] = d.evHash[m];
+    o6[1] = red[1][0] + mix64((uint64_t)(int64_t)d.ms[m].pingIdx ^ 0xF00Dull) + fl;
+    o6[2] = red[2][0] + mix64((uint64_t)(int64_t)d.ms[m].remoteIdx ^ 0xBEEFull) + gl;
+    o6[3] = d.ms[m].evHash;
     o6[4] = red[3][0];
     uint64_t ns = d.nextSync[m] == NEVER ? ~0ull : (uint64_t)d.nextSync[m];
-    o6[5] = hpair(hpair(hpair(d.cidCnt[m], d.syncSeq[m]), d.gCounter[m]), ns) +
-            mix64((uint64_t)d.fdPeriod[m] * 3 + (uint64_t)d.gPeriod[m] * 7);
+    o6[5] = hpair(hpair(hpair(d.ms[m].cidCnt, d.ms[m].syncSeq), d.ms[m].gCounter), ns) +
+            mix64((uint64_t)d.ms[m].fdPeriod * 3 + (uint64_t)d.ms[m].gPeriod * 7);
   }
 }
 
@@ -870,7 +868,7 @@ static void launch_sync_diff(const Dev& d, uint32_t b, hipStream_t st, uint32_t 
 static void launch_ack_resolve(const Dev& d, uint32_t k, hipStream_t st, bool spec, bool timed) {
   if (k == 0 || !d.ackres) return;
   const uint32_t b = (k - 1) & 1;
-  const ResArgs ra{d.halt, d.nmsg + b, d.tl_tick, d.tl_n, d.tlog, d.rowk, d.arena[b], d.dead_tick, d.msgs[b], d.dlist, d.ndl,
+  const ResArgs ra{d.halt, d.nmsg + b, d.tl_tick, d.tl_n, d.tlog, d.rowk, d.arena[b], d.msgs[b], d.dlist, d.ndl,
                    d.chunk_meta, d.pool_used, d.err, d.pool, d.ctr, d.NL, d.NS, d.MSGCAP, d.NCHUNK, d.POOLCAP, d.NMETA,
                    d.lo, d.W, d.MW, d.mlog, d.base_row, d.rx_mask, d.rx_off, d.xa_recv};
   hipLaunchKernelGGL(k_ack_resolve, dim3(128), dim3(512), 0, st, ra, k, spec ? 1u : 0u, timed ? 1u : 0u);

@@ -55,6 +55,10 @@ struct ML {
   // cursor needs no reshuffle (compared only at the ping, so nothing waits for them before); pre = NEVER when not
   // loaded or once the list changes in this tick
   uint32_t pre, pre_dt;
+  // the last SYNC / SYNC_ACK this lane linked into its receiver's inbound list (W == 1): the list-link exchange's old
+  // head, written to m_next with the pins at the next send or at the end of the body (link_flush), so that the
+  // exchange's round trip overlaps the lane's next loads instead of holding them (NEVER: none pending)
+  uint32_t lk_i, lk_o;
   int rgrp;
   bool spec;  // a launch of a one-GPU speculative batch: a member that takes a gossip slot raises d.halt (k_member_tick)
 };
@@ -186,15 +190,26 @@ __device__ __forceinline__ void row_put(ML& L, uint32_t s, uint64_t v, uint32_t 
 }
 __device__ __forceinline__ void row_put(ML& L, uint32_t s, uint64_t v) { row_put(L, s, v, L.rk[s]); }
 
+__device__ __forceinline__ void link_flush(ML& L) {
+  if (L.lk_i == NEVER) return;
+  const Dev& d = *L.d;
+  const uint32_t b = L.k & 1, i = L.lk_i, old = L.lk_o;
+  d.m_next[(size_t)b * d.MSGCAP + i] = old;
+  if (old != NEVER) {  // a receiver with several payloads this tick: both pinned (pin_msg)
+    pin_msg(d, b, i);
+    pin_msg(d, b, old);
+  }
+  L.lk_i = NEVER;
+}
+
 // prepareSyncDataMsg (MembershipProtocolImpl.java:446-454) + transport.send; false if the send failed
 // res: a SYNC_ACK sent in the tick its SYNC was merged (k_ack_resolve may derive its diff from the write logs)
-// dd: whether dst is dead at this tick when the caller knows it (KF_SRCLIVE / KF_SRCDEAD), -1: look it up
 __device__ __forceinline__ bool send_sync(ML& L, uint32_t kind, uint32_t dst, uint32_t ciss, uint32_t ccnt,
-                                          bool res = false, int dd = -1) {
+                                          bool res = false) {
   const Dev& d = *L.d;
   uint32_t seq = L.syncSeq++;
   L.c[C_M]++;
-  const int e = xmit_ep(d, L.ep, kind, L.m, dst, L.k, L.m, seq, dd);
+  const int e = xmit_ep(d, L.ep, kind, L.m, dst, L.k, L.m, seq);
   if (e < 0) {
     L.c[C_LOST]++;
     return false;
@@ -233,12 +248,9 @@ __device__ __forceinline__ bool send_sync(ML& L, uint32_t kind, uint32_t dst, ui
   // the receiver's inbound list for the next tick (sharded handles build it when the exchange commits the list);
   // a receiver with several payloads gets them pinned (pin_msg)
   if (d.W == 1) {
-    const uint32_t old = atomicExch(&d.m_head[(size_t)b * d.N + dst], i);
-    d.m_next[(size_t)b * d.MSGCAP + i] = old;
-    if (old != NEVER) {
-      pin_msg(d, b, i);
-      pin_msg(d, b, old);
-    }
+    link_flush(L);
+    L.lk_o = atomicExch(&d.m_head[(size_t)b * d.N + dst], i);
+    L.lk_i = i;
   }
   return true;
 }
@@ -454,8 +466,8 @@ __global__ void __launch_bounds__(256) k_ug_create(Dev d, uint32_t k, const uint
   uint64_t gid = 0;
   UgRank rk{0, 0};
   if (i < n && ug_live(d, m, k)) {
-    rk = ug_rank(d, q, i, m, ucnt[m], d.gCounter[m]);
-    gid = ((uint64_t)m << 32) | (d.gCounter[m] + rk.all);
+    rk = ug_rank(d, q, i, m, ucnt[m], d.ms[m].gCounter);
+    gid = ((uint64_t)m << 32) | (d.ms[m].gCounter + rk.all);
     mine = slot_mine(d, gid);  // slot sharding: only the owning shard stores it; every shard counts it as held
   }
   const uint64_t bm = __ballot(mine);
@@ -477,11 +489,11 @@ __global__ void k_ug_finish(Dev d, uint32_t k, const uint64_t* q, uint32_t n, ui
   if (i >= n) return;
   const uint32_t m = (uint32_t)q[2 * i];
   if (!ug_live(d, m, k)) return;
-  const uint32_t c = ucnt[m], gc0 = d.gCounter[m];
+  const uint32_t c = ucnt[m], gc0 = d.ms[m].gCounter;
   if (c > 1 && ug_rank(d, q, i, m, c, gc0).all != 0) return;  // the member's first entry advances it once
   uint32_t mine = 0;  // ring entries this shard appended for the member
   for (uint32_t r = 0; r < c; ++r) mine += slot_mine(d, ((uint64_t)m << 32) | (gc0 + r)) ? 1u : 0u;
-  d.gCounter[m] = gc0 + c;
+  d.ms[m].gCounter = gc0 + c;
   d.held[m] += c;
   d.rtail[m] += mine;
   ucnt[m] = 0;
@@ -1007,10 +1019,8 @@ __device__ __forceinline__ void merge_payload(ML& L, uint32_t mi, uint32_t reaso
 // control path of k_member_tick this tick, and its work class: 1 = a ping is due and nothing else, 2 = only
 // request-state events (ping hops, ack arrivals, timeouts), 3 = both, 0 = anything else (SYNC receipt, gossip
 // receipts or round, timers, host requests, start).
-// head: the member's inbound SYNC / SYNC_ACK list (P1), NEVER for a dead member: passed to its body through LDS, so
-// that the body's first message loads go out with its state loads
 __device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t k, uint32_t& cls, uint32_t& drops,
-                                              uint32_t& evs, uint32_t& head) {
+                                              uint32_t& evs) {
   // A dead member does nothing itself, but the remote hops of its in-flight requests still run at the live
   // responders (their sends fail against the dead issuer), so those hops are still evaluated for the counters.
   // every word is loaded up front (no short-circuit chain of dependent loads); the SoA loads coalesce per wave
@@ -1021,13 +1031,12 @@ __device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t
   const bool dead = k >= dt;
   cls = 0;
   drops = 0;
-  head = (!dead && k > 0) ? mh : NEVER;
   if (d.fastp4) {  // RUMOR mode: P4's GOSSIP events of this tick, hashed and counted when they were applied
     const uint32_t pn = d.evp_n[m];
     if (pn) {
       if (!dead) {  // a member crashed since holds no P4 (its receipts are dropped, as rc_cnt below)
-        d.evHash[m] += d.evp_hash[m];
-        d.evSeq[m] += pn;
+        d.ms[m].evHash += d.evp_hash[m];
+        d.ms[m].evSeq += pn;
         evs = pn;
       }
       d.evp_hash[m] = 0;
@@ -1058,14 +1067,14 @@ __device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t
         return false;
       }
       if (held == 0) {  // doSpreadGossip with no gossips: period++ only (GossipProtocolImpl.java:141-146)
-        d.gPeriod[m]++;
+        d.ms[m].gPeriod++;
         d.nextGossip[m] = ng + d.gossip_t;
         d.tround[m] = 0;
         return false;
       }
     }
   }
-  if (dead && d.npath[m] == 0 && (d.nfetch[m] == 0 || d.fnext[m] > k)) {
+  if (dead && d.ms[m].npath == 0 && (d.ms[m].nfetch == 0 || d.ms[m].fnext > k)) {
     d.tround[m] = 0;
     return false;
   }
@@ -1078,32 +1087,22 @@ __device__ __forceinline__ void ml_init(ML& L, const Dev& d, uint32_t m, uint32_
   L.m = m;
   L.k = k;
   L.N = d.N;
-  L.tsize = d.tsize[m];
-  L.fdLen = d.fdLen[m];
-  L.gLen = d.gLen[m];
-  L.fdPeriod = d.fdPeriod[m];
-  L.gPeriod = d.gPeriod[m];
-  L.gCounter = d.gCounter[m];
+  {  // the body-only state: one 128-B record, five 16-B loads
+    const uint4* mp = (const uint4*)(d.ms + m);
+    const uint4 w0 = mp[0], w1 = mp[1], w2 = mp[2], w3 = mp[3], w4 = mp[4];
+    L.tsize = w0.x, L.fdLen = w0.y, L.gLen = w0.z, L.fdPeriod = w0.w;
+    L.gPeriod = w1.x, L.gCounter = w1.y, L.cidCnt = w1.z, L.syncSeq = w1.w;
+    L.evSeq = w2.x, L.initDeadline = w2.y, L.initCidBase = w2.z, L.initN = w2.w;
+    L.nsub = w3.x, L.npath = w3.y, L.nfetch = w3.z, L.fnext = w3.w;
+    L.pingIdx = (int32_t)w4.x, L.remoteIdx = (int32_t)w4.y, L.evHash = ((uint64_t)w4.w << 32) | w4.z;
+  }
   L.nextPing = d.nextPing[m];
   L.nextGossip = d.nextGossip[m];
   L.nextSync = d.nextSync[m];
-  L.cidCnt = d.cidCnt[m];
-  L.syncSeq = d.syncSeq[m];
-  L.evSeq = d.evSeq[m];
   L.held = d.held[m];
   L.timerMin = d.timerMin[m];
   L.initFlags = d.initFlags[m];
-  L.initDeadline = d.initDeadline[m];
-  L.initCidBase = d.initCidBase[m];
-  L.initN = d.initN[m];
-  L.nsub = d.nsub[m];
-  L.npath = d.npath[m];
-  L.nfetch = d.nfetch[m];
-  L.fnext = d.fnext[m];
   L.ep = epoch_at(d, k);
-  L.pingIdx = d.pingIdx[m];
-  L.remoteIdx = d.remoteIdx[m];
-  L.evHash = d.evHash[m];
   const size_t li = lidx(d, m);  // per-observer arrays hold only this shard's rows
   L.rk = d.rowk + li * d.NS;
   L.ra = d.rowa + li * d.NS;
@@ -1135,38 +1134,29 @@ __device__ __forceinline__ void ml_init(ML& L, const Dev& d, uint32_t m, uint32_
   L.tlast = NEVER;
   L.rgrp = -1;
   L.pre = NEVER;
+  L.lk_i = NEVER;
 }
 
 // member_tick_body's state back (everything but next_evt and tround, which only a finished tick stores)
-__device__ __forceinline__ void ml_store(const ML& L) {
+__device__ __forceinline__ void ml_store(ML& L) {
+  link_flush(L);
   const Dev& d = *L.d;
   const uint32_t m = L.m, k = L.k;
   const size_t li = lidx(d, m);
-  d.tsize[m] = L.tsize;
-  d.fdLen[m] = L.fdLen;
-  d.gLen[m] = L.gLen;
-  d.fdPeriod[m] = L.fdPeriod;
-  d.gPeriod[m] = L.gPeriod;
-  d.gCounter[m] = L.gCounter;
+  {  // the body-only state: five 16-B stores into the member's record
+    uint4* mp = (uint4*)(d.ms + m);
+    mp[0] = make_uint4(L.tsize, L.fdLen, L.gLen, L.fdPeriod);
+    mp[1] = make_uint4(L.gPeriod, L.gCounter, L.cidCnt, L.syncSeq);
+    mp[2] = make_uint4(L.evSeq, L.initDeadline, L.initCidBase, L.initN);
+    mp[3] = make_uint4(L.nsub, L.npath, L.nfetch, L.fnext);
+    mp[4] = make_uint4((uint32_t)L.pingIdx, (uint32_t)L.remoteIdx, (uint32_t)L.evHash, (uint32_t)(L.evHash >> 32));
+  }
   d.nextPing[m] = L.nextPing;
   d.nextGossip[m] = L.nextGossip;
   d.nextSync[m] = L.nextSync;
-  d.cidCnt[m] = L.cidCnt;
-  d.syncSeq[m] = L.syncSeq;
-  d.evSeq[m] = L.evSeq;
   d.held[m] = L.held;
   d.timerMin[m] = L.timerMin;
   d.initFlags[m] = L.initFlags;
-  d.initDeadline[m] = L.initDeadline;
-  d.initCidBase[m] = L.initCidBase;
-  d.initN[m] = L.initN;
-  d.nsub[m] = L.nsub;
-  d.npath[m] = L.npath;
-  d.nfetch[m] = L.nfetch;
-  d.fnext[m] = L.fnext;
-  d.pingIdx[m] = L.pingIdx;
-  d.remoteIdx[m] = L.remoteIdx;
-  d.evHash[m] = L.evHash;
   if (L.ntl) {  // (no entry this tick: the stale tick stamp reads as an empty log)
     d.tl_n[(size_t)(k & 1) * d.NL + li] = L.ntl;
     d.tl_tick[(size_t)(k & 1) * d.NL + li] = k;
@@ -1177,10 +1167,9 @@ __device__ __forceinline__ void ml_store(const ML& L) {
 // gossip receipts stops before P4 and is listed for k_inbox_apply (P4, a wave per member) and the resumed launch;
 // BODY_RESUME = P5 and P6 of a listed member (its P0-P4 ran in the two launches before)
 enum : uint32_t { BODY_FULL = 0, BODY_SPLIT = 1, BODY_RESUME = 2 };
-// head: the inbound list head the triage read (BODY_RESUME: none)
 template <uint32_t mode>
 __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint32_t k, unsigned long long (&cnt)[8],
-                                                 uint4* cw, uint32_t* cw_n, bool spec, uint32_t head) {
+                                                 uint4* cw, uint32_t* cw_n, bool spec) {
   const bool dead = dead_at(d, m, k);
   ML L;
   ml_init(L, d, m, k, cw, cw_n, spec);
@@ -1190,16 +1179,8 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
     L.tlast = d.hv_tlast[li];
     if (d.ackres && d.tl_tick[(size_t)(k & 1) * d.NL + li] == k) L.ntl = d.tl_n[(size_t)(k & 1) * d.NL + li];
   }
-  // P1's inbound list head from the triage, and its first message's sort key and link loaded with the state above
-  // (P0's sends link into the other buffer)
-  const uint32_t head0 = (mode != BODY_RESUME && !dead && k > 0) ? head : NEVER;
-  uint64_t key0 = 0;
-  uint32_t next0 = NEVER;
-  if (head0 != NEVER) {
-    const SyncMsg& m0 = d.msgs[(k - 1) & 1][head0];
-    key0 = ((uint64_t)m0.src << 32) | m0.seq;
-    next0 = d.m_next[(size_t)((k - 1) & 1) * d.MSGCAP + head0];
-  }
+  // P1's inbound list head, loaded with the state above (P0's sends link into the other buffer)
+  const uint32_t head0 = (mode != BODY_RESUME && !dead && k > 0) ? d.m_head[(size_t)((k - 1) & 1) * d.N + m] : NEVER;
   // the P6 ping's target and its liveness, loaded now (do_ping's loads would wait for this tick's stores)
   if (!dead && k == L.nextPing && L.fdLen > 0 && L.pingIdx >= 0 && L.pingIdx < (int32_t)L.fdLen) {
     L.pre = L.fdl[L.pingIdx];
@@ -1281,14 +1262,14 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
     uint64_t key[MQ];
     uint32_t idx[MQ], n = 0;
     bool more = false;
-    for (uint32_t q = head; q != NEVER; q = q == head ? next0 : mnext[q]) {
+    for (uint32_t q = head; q != NEVER; q = mnext[q]) {
       if (n == d.mq_cap) {
         more = true;
         fb_add(d, FB_MQ);
         break;
       }
       const SyncMsg& mq = d.msgs[pb][q];
-      uint64_t kq = q == head ? key0 : ((uint64_t)mq.src << 32) | mq.seq;
+      uint64_t kq = ((uint64_t)mq.src << 32) | mq.seq;
       uint32_t j = n++;
       while (j > 0 && key[j - 1] > kq) {
         key[j] = key[j - 1];
@@ -1332,8 +1313,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
         // the group table's round trips (a free group's fields are never read before alloc_group rewrites them)
         L.c[C_R] += mm.psize;
         L.c[C_SYNCMERGE]++;
-        send_sync(L, K_SYNC_ACK, mm.src, mm.cid_iss, mm.cid_cnt, !(mflags & (KF_ABS | KF_LATE)),
-                  (mflags & KF_SRCDEAD) ? 1 : (mflags & KF_SRCLIVE) ? 0 : -1);
+        send_sync(L, K_SYNC_ACK, mm.src, mm.cid_iss, mm.cid_cnt, !(mflags & (KF_ABS | KF_LATE)));
         continue;
       }
       // one merge_payload / finish site for the three cases (each inlined copy is large)
@@ -1555,10 +1535,11 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   lap(1);  // P2 + P3
   if (dead) {
     fd_ready(L);
+    link_flush(L);
     d.tround[m] = 0;
-    d.npath[m] = L.npath;
-    d.nfetch[m] = L.nfetch;
-    d.fnext[m] = L.fnext;
+    d.ms[m].npath = L.npath;
+    d.ms[m].nfetch = L.nfetch;
+    d.ms[m].fnext = L.fnext;
     d.next_evt[m] = NEVER;
     if (L.ntl) {
       d.tl_n[(size_t)(k & 1) * d.NL + li] = L.ntl;
@@ -1983,7 +1964,7 @@ __global__ void __launch_bounds__(256, 2) k_member_tick_t(const Dev* __restrict_
   unsigned long long* wt = wtime ? d.wt + ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 : nullptr;
   if (wtime && (threadIdx.x & 63) == 0) wt[0] = wall_clock64();
   __shared__ uint32_t wc[4][4];  // [wave][class] busy members
-  __shared__ uint32_t list[256], lhead[256];
+  __shared__ uint32_t list[256];
   __shared__ uint4 cw[CWMAX];  // deferred copy-on-write snapshots of this block's members (cow)
   __shared__ uint32_t cw_n;
   if (threadIdx.x == 0) cw_n = 0;
@@ -1991,8 +1972,7 @@ __global__ void __launch_bounds__(256, 2) k_member_tick_t(const Dev* __restrict_
   constexpr bool resume = MODE == BODY_RESUME;  // the parked members' P5 and P6 (one lane each, from the list)
   const uint32_t m = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t cls = 0, drops = 0, evs = 0;
-  uint32_t head = NEVER;
-  const bool busy = !resume && m < d.hi && member_triage(d, m, k, cls, drops, evs, head);
+  const bool busy = !resume && m < d.hi && member_triage(d, m, k, cls, drops, evs);
   {  // the triage's record compares and folded RUMOR events, one atomic each per wave
     uint32_t v = drops, e = evs;
 #pragma unroll
@@ -2022,13 +2002,9 @@ __global__ void __launch_bounds__(256, 2) k_member_tick_t(const Dev* __restrict_
   for (uint32_t j = 0; j < w; ++j) before += wc[j][cls];
   const uint64_t bal = cls == 0 ? b0 : cls == 1 ? b1 : cls == 2 ? b2 : b3;
   uint32_t slot = start + before + __popcll(bal & ((1ull << lane) - 1ull));
-  if (busy) {
-    list[slot] = m | (cls << 30);  // m < 2^30
-    lhead[slot] = head;
-  }
+  if (busy) list[slot] = m | (cls << 30);  // m < 2^30
   __syncthreads();
   uint32_t ent = list[threadIdx.x];
-  const uint32_t ehead = resume ? NEVER : lhead[threadIdx.x];
   if (resume) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     ent = i < *d.nhv ? d.hv_list[i] : NEVER;  // class 0
@@ -2045,7 +2021,7 @@ __global__ void __launch_bounds__(256, 2) k_member_tick_t(const Dev* __restrict_
     unsigned long long cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const bool skip = ((d.exp & 32) && mcls == 0) || ((d.exp & 64) && mcls != 0);
     if (me != NEVER && !skip)
-      member_tick_body<MODE>(d, me, k, cnt, cw, &cw_n, (flag & 3u) == 3u, ehead);
+      member_tick_body<MODE>(d, me, k, cnt, cw, &cw_n, (flag & 3u) == 3u);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       unsigned long long v = cnt[i];

@@ -74,6 +74,12 @@ for step in "$@"; do
       grep metric $O/bench.log > $O/bench.json
       grep -o '"ms_per_step": [0-9.]*\|"frac": [0-9.]*' $O/bench.json
       ;;
+    exp512)
+      # per-wave wall-clock trace of the member kernel (SWIM_EXP=512, a timing experiment: not a result)
+      SWIM_EXP=512 timeout -k 10 300 python3 bench.py --workload ${a:-c3} --steps 2 --warmup 3 --no-cpu-baseline \
+        > $O/exp512_${a:-c3}.log 2>&1
+      grep "exp512" $O/exp512_${a:-c3}.log | tail -14
+      ;;
     trace)
       [ -n "$TRACE_ENV" ] && export $TRACE_ENV
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/t_$a -o run --output-format csv -- \
