@@ -1016,9 +1016,9 @@ __device__ __forceinline__ void merge_payload(ML& L, uint32_t mi, uint32_t reaso
 
 // Triage (k_member_triage): the idle fast path. Most members have nothing due in most ticks (a ping every 10 ticks,
 // a SYNC every 300); they only advance an empty gossip round here. Returns whether the member needs the full
-// control path of k_member_tick this tick, and its work class: 1 = a ping is due and nothing else, 2 = only
-// request-state events (ping hops, ack arrivals, timeouts), 3 = both, 0 = anything else (SYNC receipt, gossip
-// receipts or round, timers, host requests, start).
+// control path of k_member_tick this tick, and its work class: 1 = a ping and / or a periodic SYNC is due (P6) and
+// nothing else, 2 = only request-state events (ping hops, ack arrivals, timeouts), 3 = both, 0 = anything else (SYNC
+// receipt, gossip receipts or round, timers, host requests, start).
 __device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t k, uint32_t& cls, uint32_t& drops,
                                               uint32_t& evs) {
   // A dead member does nothing itself, but the remote hops of its in-flight requests still run at the live
@@ -1058,9 +1058,11 @@ __device__ __forceinline__ bool member_triage(const Dev& d, uint32_t m, uint32_t
   } else {
     const bool busy = (k > 0 && mh != NEVER) | (rc != 0) | (pi != 0) | (ne <= k) | (tm <= k) | (k == np) | (k == ns) |
                       ((inf & INIT_ACTIVE) != 0) | (k == st);
-    const bool other = (k > 0 && mh != NEVER) | (rc != 0) | (pi != 0) | (tm <= k) | (k == ns) |
-                       ((inf & INIT_ACTIVE) != 0) | (k == st) | (k == ng && held != 0);
-    cls = other ? 0u : (k == np ? 1u : 0u) | (ne <= k ? 2u : 0u);
+    // a periodic SYNC send (doSync, P6) is scheduled with the pings (P6 too), not with the SYNC receivers: in one wave
+    // their chains would run one after the other
+    const bool other = (k > 0 && mh != NEVER) | (rc != 0) | (pi != 0) | (tm <= k) | ((inf & INIT_ACTIVE) != 0) |
+                       (k == st) | (k == ng && held != 0);
+    cls = other ? 0u : (k == np || k == ns ? 1u : 0u) | (ne <= k ? 2u : 0u);
     if (!busy) {
       if (k != ng) {
         d.tround[m] = 0;
