@@ -36,6 +36,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "scalecube-cluster_amd"))
 
 HBM_PEAK_GBPS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
+HBM_STREAM_GBPS = 6290.0  # measured streaming ceiling (MI355X_MICROARCH.md: float4 copy, 79 % of spec)
 BASELINE_WORKLOAD = "C3: 100k members, full views, preconverged, default ClusterConfig, no loss"
 
 
@@ -300,6 +301,7 @@ def main():
                                        if world > 1 else "single-gpu")},
             "roofline": {"bound": "hbm", "kernel": "k_sync_diff", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
+                         "frac_of_measured_stream_ceiling": achieved / HBM_STREAM_GBPS,
                          "algorithmic_bytes_per_launch": bytes_per_launch,
                          "avg_launch_us": diff_s * 1e6 / launches,
                          # the same launches priced by SURVEY.md §8d's model (16 B per record compare: 8-B keys read
