@@ -59,6 +59,11 @@ struct ML {
   // head, written to m_next with the pins at the next send or at the end of the body (link_flush), so that the
   // exchange's round trip overlaps the lane's next loads instead of holding them (NEVER: none pending)
   uint32_t lk_i, lk_o;
+  // the earliest pending path tick and subscription deadline, kept in registers once P2 and P5 have walked the lists
+  // (NEVER: none), so the next-event minimum at the end of the body needs no loads of entries just stored; ev_ok says
+  // whether they are known (not in a resumed launch, whose P2 ran in the launch before)
+  uint32_t pmin, smin;
+  bool ev_ok;
   int rgrp;
   bool spec;  // a launch of a one-GPU speculative batch: a member that takes a gossip slot raises d.halt (k_member_tick)
 };
@@ -689,6 +694,7 @@ __device__ __forceinline__ void add_sub(ML& L, uint32_t cnt, uint32_t kind, uint
   s[1] = kind;
   s[2] = target;
   s[3] = deadline;
+  L.smin = min(L.smin, deadline);
 }
 __device__ __forceinline__ void add_path(ML& L, uint32_t cnt, uint32_t stage, uint32_t tick, uint32_t a, uint32_t b) {
   if (L.npath >= L.d->PCAP) {
@@ -701,6 +707,7 @@ __device__ __forceinline__ void add_path(ML& L, uint32_t cnt, uint32_t stage, ui
   p[2] = tick;
   p[3] = a;
   p[4] = b;
+  L.pmin = min(L.pmin, tick);
 }
 
 // doPing error branch (FailureDetectorImpl.java:159-175), selectPingReqMembers (:349-361), doPingReq (:178-213)
@@ -1137,6 +1144,8 @@ __device__ __forceinline__ void ml_init(ML& L, const Dev& d, uint32_t m, uint32_
   L.rgrp = -1;
   L.pre = NEVER;
   L.lk_i = NEVER;
+  L.pmin = L.smin = NEVER;
+  L.ev_ok = false;
 }
 
 // member_tick_body's state back (everything but next_evt and tround, which only a finished tick stores)
@@ -1360,20 +1369,21 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
 
   lap(0);  // P0 + P1
   // ---- P2 FD: remote hops of pending pings, then PING_ACK arrivals in cid order ----
+  L.ev_ok = mode != BODY_RESUME;  // this launch walks the path list (P2) and the subscriptions (P5)
   if (L.npath) {
     // arrivals stay in the compacted list this pass, marked by their new index (at most PATHCAP_DELAY = 32 entries)
     uint32_t arrmask = 0;
-    uint32_t w = 0;
+    uint32_t w = 0, pm = NEVER;
     for (uint32_t p = 0; p < L.npath; ++p) {
       uint32_t* P = L.paths + (size_t)p * 5;
       uint32_t cnt = P[0], stage = P[1], tk = P[2], a = P[3], b = P[4];
-      bool keep = true;
+      bool keep = true, arr = false;
       if (tk == k) {
         lap(9);
         uint32_t kind = stage & 0xF0, st = stage & 0xF;
         if (st == P_ARRIVE) {
           if (dead) keep = false;
-          else arrmask |= 1u << w;
+          else arrmask |= 1u << w, arr = true;
         } else if (kind == P_DIRECT) {  // onPing at the target (:230-255): PING_ACK back to the issuer
           if (dead_at(d, a, k)) {
             keep = false;
@@ -1420,9 +1430,11 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
         Q[3] = a;
         Q[4] = b;
         w++;
+        if (!arr) pm = min(pm, tk);  // (an arrival leaves the list below)
       }
     }
     L.npath = w;
+    L.pmin = min(L.pmin, pm);
     lap(6);
     // arrivals: every pending subscription on the cid takes the first PING_ACK (TransportImpl.java:205-232), in cid
     // order; then the arrived entries leave the list
@@ -1610,7 +1622,7 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
   }  // P0 - P4
   // ---- P5 timers ----
   if (L.nsub) {  // FD subscription timeouts in (cid, subscription) order
-    uint32_t dcnt[SUBCAP], dkind[SUBCAP], dtgt[SUBCAP], nd = 0, w = 0;
+    uint32_t dcnt[SUBCAP], dkind[SUBCAP], dtgt[SUBCAP], nd = 0, w = 0, sm = NEVER;
     for (uint32_t s = 0; s < L.nsub; ++s) {
       uint32_t* S4 = L.subs + (size_t)s * 4;
       if (S4[3] == k) {
@@ -1631,9 +1643,11 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
         D4[2] = S4[2];
         D4[3] = S4[3];
         w++;
+        sm = min(sm, S4[3]);
       }
     }
     L.nsub = w;
+    L.smin = sm;  // (no subscription was added in this body before this pass)
     for (uint32_t q = 0; q < nd; ++q) {
       if (dkind[q] == 0)
         ping_req_step(L, dtgt[q], dcnt[q]);  // ping timeout (:159-175)
@@ -1717,9 +1731,11 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
 
   lap(4);  // P6
   flush_spreads(L);
-  // the next due event: the first four paths and subscriptions are loaded together (one round trip, not one per entry)
+  // the next due event
   uint32_t nev = L.fnext;
-  {
+  if (L.ev_ok) {  // from registers (P2, P5 and every add since)
+    nev = min(nev, min(L.pmin, L.smin));
+  } else {  // a resumed launch: the first four paths and subscriptions loaded together (one round trip)
     uint32_t t[8];
 #pragma unroll
     for (uint32_t q = 0; q < 4; ++q) {
@@ -1728,9 +1744,9 @@ __device__ __forceinline__ void member_tick_body(const Dev& d, uint32_t m, uint3
     }
 #pragma unroll
     for (uint32_t q = 0; q < 8; ++q) nev = min(nev, t[q]);
+    for (uint32_t q = 4; q < L.npath; ++q) nev = min(nev, L.paths[(size_t)q * 5 + 2]);
+    for (uint32_t q = 4; q < L.nsub; ++q) nev = min(nev, L.subs[(size_t)q * 4 + 3]);
   }
-  for (uint32_t q = 4; q < L.npath; ++q) nev = min(nev, L.paths[(size_t)q * 5 + 2]);
-  for (uint32_t q = 4; q < L.nsub; ++q) nev = min(nev, L.subs[(size_t)q * 4 + 3]);
   if (L.ncreq)  // the log length the block epilogue undoes from
     for (uint32_t q = 0, n = min(*L.cw_n, d.cwmax_cap); q < n; ++q)
       if (L.cw[q].x == m) L.cw[q].w = L.nlog;
