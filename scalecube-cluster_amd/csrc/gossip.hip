@@ -511,24 +511,28 @@ __device__ void round_member(const Dev& d, uint32_t m, uint32_t k, unsigned long
   }
 }
 
-// rows of up to RCS words: one wavefront per round member (16 KB of LDS each, four per workgroup)
-__global__ void __launch_bounds__(256) k_round_apply_w(const Dev* __restrict__ dp, uint32_t k) {
+// rows of up to cw = min(RCS, QW) words: one wavefront per round member (2 cw words of LDS each, four per workgroup,
+// sized at launch: a slot table of 45 056 slots takes 11 KB per wave, so three workgroups fit a CU instead of two)
+__global__ void __launch_bounds__(256) k_round_apply_w(const Dev* __restrict__ dp, uint32_t k, uint32_t cw) {
   const Dev& d = *dp;
-  __shared__ unsigned long long lh[4][RCS], lw[4][RCS];
+  extern __shared__ unsigned long long lds_rows[];
   const uint32_t n = *d.nrwl, span = d.nagroup[1], wave = threadIdx.x >> 6;
-  if (span > RCS) return;  // k_round_apply_b
+  if (span > cw) return;  // k_round_apply_b
+  unsigned long long* lh = lds_rows + (size_t)wave * 2 * cw;
   for (uint32_t i = blockIdx.x * 4 + wave; i < n; i += gridDim.x * 4)
-    round_member<false>(d, d.rwl[i], k, lh[wave], lw[wave], RCS, span, threadIdx.x & 63u, 64u);
+    round_member<false>(d, d.rwl[i], k, lh, lh + cw, cw, span, threadIdx.x & 63u, 64u);
 }
 
 // larger rows: one workgroup per round member, the rows staged in chunks of RCW words
-__global__ void __launch_bounds__(256) k_round_apply_b(const Dev* __restrict__ dp, uint32_t k) {
+// (cb = min(RCW, QW): the chunk in LDS; cw: k_round_apply_w's row limit)
+__global__ void __launch_bounds__(256) k_round_apply_b(const Dev* __restrict__ dp, uint32_t k, uint32_t cb, uint32_t cw) {
   const Dev& d = *dp;
-  __shared__ unsigned long long lh[RCW], lw[RCW];
+  extern __shared__ unsigned long long lds_rows[];
+  unsigned long long *lh = lds_rows, *lw = lds_rows + cb;
   const uint32_t n = *d.nrwl, span = d.nagroup[1];
-  if (span <= RCS) return;  // k_round_apply_w
+  if (span <= cw) return;  // k_round_apply_w
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-    round_member<true>(d, d.rwl[i], k, lh, lw, RCW, span, threadIdx.x, blockDim.x);
+    round_member<true>(d, d.rwl[i], k, lh, lw, cb, span, threadIdx.x, blockDim.x);
     __syncthreads();
   }
 }
@@ -652,18 +656,19 @@ __device__ void contact_cache(const Dev& d, uint32_t i, uint32_t m, uint32_t t, 
 }
 
 // the RX rows of this tick's contact pairs: bit g set for the window gossips received no later than the contact (one
-// workgroup per row, staged through LDS in chunks of RCW words)
+// workgroup per row, staged through LDS in chunks of at most RXW words)
 constexpr uint32_t RXW = 8192;
-__global__ void __launch_bounds__(256) k_rx_build(const Dev* __restrict__ dp) {
+// (cx = min(RXW, QW) words of LDS, sized at launch)
+__global__ void __launch_bounds__(256) k_rx_build(const Dev* __restrict__ dp, uint32_t cx) {
   const Dev& d = *dp;
-  __shared__ unsigned long long lr[RXW];
+  extern __shared__ unsigned long long lr[];
   const uint32_t n = min(*d.nrx, d.CRCAP), span = d.nagroup[1];
   for (uint32_t r = blockIdx.x; r < n; r += gridDim.x) {
     const uint32_t m = d.rxl[3 * r] / d.F, a = d.rxl[3 * r + 1], b = d.rxl[3 * r + 2];
     const uint32_t* R = ring(d, m);
     unsigned long long* row = d.RX + (size_t)r * d.QW;
-    for (uint32_t c0 = 0; c0 < span; c0 += RXW) {
-      const uint32_t c1 = min(span, c0 + RXW);
+    for (uint32_t c0 = 0; c0 < span; c0 += cx) {
+      const uint32_t c1 = min(span, c0 + cx);
       for (uint32_t j = threadIdx.x; j < c1 - c0; j += blockDim.x) lr[j] = 0ull;
       __syncthreads();
       ring_walk(R, d.BCAP - 1, a, b, threadIdx.x, blockDim.x, [&](uint32_t g) {
@@ -719,7 +724,7 @@ __global__ void __launch_bounds__(256) k_gossip_contacts(Dev d, uint32_t k) {
 // the flagged pairs' contact caches, one wave each: its lanes scan the two round logs 64 entries at a time
 // (Dev through a pointer: the contacts' loss percents index its epoch table by a per-lane epoch, which a by-value Dev
 // would copy to scratch, 2.3 KB per lane)
-__global__ void __launch_bounds__(256) k_contact_cache(const Dev* __restrict__ dp, uint32_t k) {
+__global__ void __launch_bounds__(256, 8) k_contact_cache(const Dev* __restrict__ dp, uint32_t k) {
   const Dev& d = *dp;
   __shared__ Contact sev[4][CEV];
   const uint32_t n = *d.ncfl, lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -746,7 +751,7 @@ __device__ __forceinline__ void receipt_mark(const Dev& d, uint32_t g, uint32_t 
 // .evaluateLoss: SEMANTICS.md §2). A receipt needs one surviving send from any sender; draws of candidates another
 // sender already delivered are skipped (they change nothing). Pairs with a cached contact go to k_gossip_replay and
 // pairs whose contact list overflowed to k_gossip_send_slow (isInfected, :247).
-__global__ void __launch_bounds__(256) k_gossip_send(const Dev* __restrict__ dp, uint32_t k) {
+__global__ void __launch_bounds__(256, 8) k_gossip_send(const Dev* __restrict__ dp, uint32_t k) {
   const Dev& d = *dp;
   __shared__ unsigned long long red[4];
   const uint32_t nag = d.nagroup[0], ntl = *d.ntl;
@@ -973,7 +978,7 @@ __device__ __forceinline__ void deliver_one(const Dev& d, uint32_t g, uint32_t m
 
 // 7a. sends of pairs with a cached contact, one thread per (slot, sender, target): the isInfected replay runs only
 // where the contact can matter (t -> m at or after m's incarnation start and after the gossip existed), then the send
-__global__ void __launch_bounds__(256) k_gossip_replay(const Dev* __restrict__ dp, uint32_t k) {
+__global__ void __launch_bounds__(256, 8) k_gossip_replay(const Dev* __restrict__ dp, uint32_t k) {
   const Dev& d = *dp;
   __shared__ unsigned long long red[4];
   const uint32_t n = min(*d.rp_n, d.RPCAP);
@@ -1282,11 +1287,17 @@ void launch_gossip_send(const Dev& d, uint32_t k, hipStream_t st, const TickEven
   hipLaunchKernelGGL(k_round_plan, dim3(cdiv(d.N, 256)), dim3(256), 0, st, d, k);
   launch_scan(d.tin_cnt, d.tin_off, d.scan_part, d.N, st);
   hipLaunchKernelGGL(k_tin_scatter, dim3(cdiv(d.N, 256)), dim3(256), 0, st, d);
-  hipLaunchKernelGGL(k_round_apply_w, dim3(4096), dim3(256), 0, st, d.self, k);
-  hipLaunchKernelGGL(k_round_apply_b, dim3(2048), dim3(256), 0, st, d.self, k);
+  {  // LDS rows sized by the slot table (the active span never exceeds QW words)
+    const uint32_t cw = std::min<uint32_t>(RCS, d.QW), cb = std::min<uint32_t>(RCW, d.QW);
+    hipLaunchKernelGGL(k_round_apply_w, dim3(4096), dim3(256), 4 * 2 * 8 * cw, st, d.self, k, cw);
+    hipLaunchKernelGGL(k_round_apply_b, dim3(2048), dim3(256), 2 * 8 * cb, st, d.self, k, cb, cw);
+  }
   hipLaunchKernelGGL(k_gossip_contacts, dim3(2048), dim3(256), 0, st, d, k);
   hipLaunchKernelGGL(k_contact_cache, dim3(1024), dim3(256), 0, st, d.self, k);
-  hipLaunchKernelGGL(k_rx_build, dim3(512), dim3(256), 0, st, d.self);
+  {
+    const uint32_t cx = std::min<uint32_t>(RXW, d.QW);
+    hipLaunchKernelGGL(k_rx_build, dim3(512), dim3(256), 8 * cx, st, d.self, cx);
+  }
   if (prof && prof->all) hipEventRecord((hipEvent_t)prof->ev[4], st);
   hipLaunchKernelGGL(k_gossip_send, dim3(SEND_GRID), dim3(256), 0, st, d.self, k);
   hipLaunchKernelGGL(k_gossip_send_slow, dim3(64), dim3(64), 0, st, d.self, k);  // rare; ~14 KB of stack per lane
