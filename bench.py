@@ -7,8 +7,8 @@ ClusterConfig (ping 1 s / 500 ms, ping-req 3, gossip 200 ms x fanout 3 x repeat 
 "step" = one FD period (pingInterval = 10 ticks of 100 ms) for every member. In this steady state every member pings
 one peer per period, and periodic SYNC / SYNC_ACK anti-entropy streams whole 100k-record payloads against whole
 receiver rows (N/30 syncs per period in each direction), so the dominant kernel is k_sync_diff. It is HBM-bound with
-no dense math, so no MFMA: on one GPU it compares the 16-bit shadows of the record keys (4 B of algorithmic traffic
-per record compare, payload + receiver; an escaped key past incarnation 16 382 is compared on its 4-B key), on a row
+no dense math, so no MFMA: on one GPU it compares the 8-bit shadows of the record keys (2 B of algorithmic traffic
+per record compare, payload + receiver; an escaped key past incarnation 62 is compared on its 4-B key), on a row
 shard the 4-B keys (8 B per compare; SURVEY.md §8d priced it at 16 B for 8-B keys).
 
 With N=1, all 100k members run on one MI355X (about 206 GB of HBM). With --gpus N under torch.distributed.run, the
@@ -19,7 +19,7 @@ scaling is "strong" and `value` is the whole cluster's member·periods/s. torch.
 it broadcasts the RCCL unique id, runs the barriers and takes the max time over ranks.
 
 The JSON line also carries:
-  roofline      k_sync_diff algorithmic bytes (the key bytes the engine counts per streamed payload: 4 B or 8 B x N,
+  roofline      k_sync_diff algorithmic bytes (the key bytes the engine counts per streamed payload: 2 B or 8 B x N,
                 swim_counters.diff_key_bytes) / its HIP-event time, against 8 TB/s; traffic = measured HBM bytes per
                 launch from a committed rocprofv3 PMC summary when available (profiles/), else null.
   cpu_baseline  the CPU oracle (oracle/swimref.cpp, a port) on a bounded sample: same workload shape at 10k members,
@@ -71,7 +71,7 @@ def parse():
 
 def traffic_from_profiles(n_members):
     """HBM bytes per k_sync_diff launch from a committed rocprofv3 PMC summary for this member count, if present."""
-    f = ROOT / "profiles" / "pmc_sync_diff_k16.json"  # measured with the 16-bit shadow key plane
+    f = ROOT / "profiles" / "pmc_sync_diff_k8.json"  # measured with the 8-bit shadow key plane
     if not f.exists():
         return None
     try:
@@ -265,7 +265,7 @@ def main():
         diff_s = d["diff_ns"] * 1e-9
         launches = max(1, d["diff_launches"])
         # the engine counts the key bytes its timed k_sync_diff launches compared (every 5th tick on one GPU, every
-        # tick on a row shard): 2 x 2 B per subject for a payload streamed from the 16-bit shadow plane, 2 x 4 B for
+        # tick on a row shard): 2 x 1 B per subject for a payload streamed from the 8-bit shadow plane, 2 x 4 B for
         # the others; SYNC_ACKs resolved from write logs are not streamed, so they are not priced here
         timed_bytes = d["diff_key_bytes"]
         bytes_per_launch = timed_bytes / launches
@@ -290,9 +290,9 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             # record keys are u32 `inc << 2 | status`: incarnations are capped at 2^30 - 1 (Java int: 2^31 - 1), past
-            # which the engine raises SWIM_ECAPACITY (SEMANTICS.md §8); the diff compares their exact 16-bit shadows
-            # (a key past 0xFFFE escapes to its u32 compare); list entries are u32 member ids
-            "dtype": ("u16 key shadows, exact (u32 record key inc<<2|status: 30-bit incarnation cap)" if world == 1
+            # which the engine raises SWIM_ECAPACITY (SEMANTICS.md §8); the diff compares their exact 8-bit shadows
+            # (a key past 0xFE escapes to its u32 compare); list entries are u32 member ids
+            "dtype": ("u8 key shadows, exact (u32 record key inc<<2|status: 30-bit incarnation cap)" if world == 1
                       else "u32 (record key inc<<2|status: 30-bit incarnation cap)"),
             "data": "synthetic (PRECONVERGED full views, seeded Philox selector)",
             "config": {"workload": workload_name(a, n),
@@ -313,7 +313,7 @@ def main():
                              "achieved": 16 * n * d["diff_msgs"] / diff_s / 1e9 if diff_s > 0 else 0.0,
                              "frac": (16 * n * d["diff_msgs"] / diff_s / 1e9 / HBM_PEAK_GBPS) if diff_s > 0 else 0.0},
                          "traffic": traffic_from_profiles(n) if world == 1 else None,
-                         "traffic_source": "committed rocprofv3 PMC summary profiles/pmc_sync_diff_k16.json (FETCH_SIZE x 2 "
+                         "traffic_source": "committed rocprofv3 PMC summary profiles/pmc_sync_diff_k8.json (FETCH_SIZE x 2 "
                                            "+ WRITE_SIZE per launch), not measured in this run"},
             # the engine times a sample of the launches (every 5th tick on one GPU): average x launches per period
             "kernel_time_share": {"k_sync_diff": diff_s / launches * ticks_per_period * a.steps / dt},  # others: profiles/*kernel_stats*

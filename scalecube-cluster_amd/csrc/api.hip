@@ -693,7 +693,8 @@ int build(swim_handle* h) {
   const uint64_t NL = d.NL;  // per-observer arrays: this shard's rows only
   const uint64_t NV = d.implicit ? 1 : NL;  // implicit views: no table or list is stored
   A(d.rowk, NV * d.NS) A(d.rowa, NV * d.NS) A(d.fdl, NV * d.LCAP) A(d.gl, NV * d.LCAP)
-  d.rowk16 = nullptr;  // allocated last, if it fits (below)
+  d.rowk8 = nullptr;  // allocated last, if it fits (below)
+  d.NS8 = (c.n_members + 15u) & ~15u;
   A(d.subs, NL * SUBCAP * 4) A(d.paths, NL * d.PCAP * 5) A(d.fetch, NL * d.FCAP * FREC) A(d.groups, NL * d.GRCAP * GREC)
   A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.slow, d.SLOWCAP) A(d.slow_n, 1) A(d.rp, d.RPCAP) A(d.rp_n, 1) A(d.start_tick, N) A(d.jseed_n, N) A(d.jseeds, 16 * N) A(d.md_uidx, N) A(d.mcfg, 4 * N) A(d.md_ver, NL * MDU) A(d.churn_q, 2ull * d.churn) A(d.ucnt, N) A(d.cin, N * d.F) A(d.HB, (uint64_t)d.QW * N) A(d.WB, (uint64_t)d.QW * N) A(d.cev, N * d.F * CEVW)
   A(d.rg, (uint64_t)d.BCAP * N) A(d.rhead, N) A(d.rwin, N) A(d.rseen, N) A(d.rtail, N) A(d.rwl, N) A(d.nrwl, 1)
@@ -720,10 +721,11 @@ int build(swim_handle* h) {
   // SYNC_ACK resolution (k_ack_resolve); SWIM_NO_ACKRES streams every payload (measurements)
   d.ackres = !d.implicit && !getenv("SWIM_NO_ACKRES") ? 1u : 0u;
   if (d.ackres) {
-    A(d.tlog, 2 * NL * TL) A(d.tl_n, 2 * NL) A(d.tl_tick, 2 * NL) A(d.dlist, d.MSGCAP) A(d.ndl, 1)
+    A(d.tlog, 2 * NL * TL) A(d.tl_n, 2 * NL) A(d.tl_tick, 2 * NL) A(d.dlist, 4ull * d.MSGCAP) A(d.ndl, 1) A(d.dlist_w, 4ull * d.MSGCAP) A(d.ndlw, 1)
     if (d.W > 1) A(d.mlog, (uint64_t)d.MSGCAP * TL)
     HIPCK(hipMemsetAsync(d.tl_tick, 0xFF, 8 * NL, h->stream));
     HIPCK(hipMemsetAsync(d.ndl, 0, 4, h->stream));
+    HIPCK(hipMemsetAsync(d.ndlw, 0, 4, h->stream));
   }
   // capacity growth between ticks (grow_caps), without guard zones; SWIM_NO_GROW keeps the sizes fixed. A row shard
   // grows its receipt rings and incarnation history (grow_caps_shard); its slot ids and exchange capacities are global
@@ -805,12 +807,12 @@ int build(swim_handle* h) {
       h->hrecv.resize(d.W * std::max(d.XA_PEER, d.XB_PEER));
     }
   }
-  // one GPU, stored tables: the diff's 16-bit shadow plane, only when it fits beside everything else with the usual
-  // growth reserve (an optimisation: without it k_sync_diff and row_put use the u32 keys; SWIM_NO_K16 forces that)
-  if (d.W == 1 && !d.implicit && !getenv("SWIM_NO_K16")) {
+  // one GPU, stored tables: the diff's 8-bit shadow plane, only when it fits beside everything else with the usual
+  // growth reserve (an optimisation: without it k_sync_diff and row_put use the u32 keys; SWIM_NO_K8 forces that)
+  if (d.W == 1 && !d.implicit && !getenv("SWIM_NO_K8")) {
     size_t fr = 0, tot = 0;
     HIPCK(hipMemGetInfo(&fr, &tot));
-    if ((uint64_t)fr > 2ull * NV * d.NS + (4ull << 30)) A(d.rowk16, NV * d.NS)
+    if ((uint64_t)fr > NV * d.NS8 + (4ull << 30)) A(d.rowk8, NV * d.NS8)
   }
 #undef A
   HIPCK(hipMemsetAsync(d.S, 0, (size_t)d.SLOTS * N * 2, h->stream));
@@ -2167,11 +2169,11 @@ int swim_counters_get(swim_handle* h, swim_counters* out) {
   out->ack_resolved = c[C_ACKRES];
   out->ack_resolved_total = c[C_ACKRES_ALL];
   out->diff_msgs_total = c[C_DIFFMSG_ALL];
-  // the payloads streamed from the 16-bit shadow plane compared 4 B per subject, the others (C_DIFFWIDE) 8 B
+  // the payloads streamed from the 8-bit shadow plane compared 2 B per subject, the others (C_DIFFWIDE) 8 B
   const uint64_t nsub = h->d.N;
-  out->diff_key_bytes = nsub * (4 * (c[C_DIFFMSG] - std::min(c[C_DIFFMSG], c[C_DIFFWIDE])) + 8 * c[C_DIFFWIDE]);
+  out->diff_key_bytes = nsub * (2 * (c[C_DIFFMSG] - std::min(c[C_DIFFMSG], c[C_DIFFWIDE])) + 8 * c[C_DIFFWIDE]);
   out->diff_key_bytes_total =
-      nsub * (4 * (c[C_DIFFMSG_ALL] - std::min(c[C_DIFFMSG_ALL], c[C_DIFFWIDE_ALL])) + 8 * c[C_DIFFWIDE_ALL]);
+      nsub * (2 * (c[C_DIFFMSG_ALL] - std::min(c[C_DIFFMSG_ALL], c[C_DIFFWIDE_ALL])) + 8 * c[C_DIFFWIDE_ALL]);
   out->exchange_ns = (uint64_t)(h->xchg_ms * 1e6);
   return SWIM_OK;
 }
@@ -2244,9 +2246,9 @@ int swim_debug_set_incarnation(swim_handle* h, uint32_t m, uint32_t inc) {
   HIPCK(hipMemcpy(&k, w, 4, hipMemcpyDeviceToHost));
   k = (inc << 2) | (k & 3u);
   HIPCK(hipMemcpy(w, &k, 4, hipMemcpyHostToDevice));
-  if (d.rowk16) {
-    const uint16_t k16 = key16(k);
-    HIPCK(hipMemcpy(d.rowk16 + lidx(d, m) * d.NS + m, &k16, 2, hipMemcpyHostToDevice));
+  if (d.rowk8) {
+    const uint8_t k8 = key8(k);
+    HIPCK(hipMemcpy(d.rowk8 + lidx(d, m) * d.NS8 + m, &k8, 1, hipMemcpyHostToDevice));
   }
   return SWIM_OK;
 }

@@ -441,7 +441,7 @@ __device__ __forceinline__ void tick_end(const Dev& d, uint32_t k) {
     d.arena_used[nb] = 0;
     *d.pool_used = 0;
     *d.rc_n = 0;
-    if (d.ackres) *d.ndl = 0;
+    if (d.ackres) *d.ndl = *d.ndlw = 0;
   }
 }
 
@@ -455,7 +455,7 @@ __device__ __forceinline__ void tick_reset(const Dev& d, uint32_t k) {
   d.nmsg[nb] = 0;
   d.arena_used[nb] = 0;
   *d.pool_used = 0;
-  if (d.ackres) *d.ndl = 0;
+  if (d.ackres) *d.ndl = *d.ndlw = 0;
   if (__hip_atomic_load(d.free_top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (int32_t)d.SPR)
     *(volatile uint32_t*)d.halt = k + 1u;
 }
@@ -486,7 +486,7 @@ __device__ __forceinline__ void tick_flag(const Dev& d, uint32_t k) {
   *d.pool_used = 0;
   if (d.rfill) *d.rfill = 0;
   *d.rc_n = 0;
-  if (d.ackres) *d.ndl = 0;
+  if (d.ackres) *d.ndl = *d.ndlw = 0;
 #pragma unroll
   for (int i = 0; i < 6; ++i)
     if ((i == 0 || d.rfill) && v[i] != sh[i]) {

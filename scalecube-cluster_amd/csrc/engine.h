@@ -125,6 +125,10 @@ constexpr uint32_t KF_ABS = 0x200u;
 // a SYNC_ACK sent in the tick its SYNC was merged: k_ack_resolve derives its diff from the two write logs instead of
 // k_sync_diff streaming it (cleared there when it cannot)
 constexpr uint32_t KF_RES = 0x400u;
+// k_sync_diff's list entries (Dev::dlist, dlist_w: 16 B = message, sender, receiver, payload place): the payload place
+// is the message's payload (arena row or PAY_RX | rx index), NEVER for the live row, DESC_PIN | arena row for a pinned
+// live row, DESC_DEFER for a delayed message (kernels.hip desc_pay)
+constexpr uint32_t DESC_PIN = 0x80000000u, DESC_DEFER = 0xFFFFFFFEu;
 constexpr uint32_t KF_LATE = 0x800u;  // a delayed message put back by k_sync_redeliver
 constexpr uint32_t KF_FLAGS = KF_DEFER | KF_ABS | KF_RES | KF_LATE;
 constexpr uint32_t TL = 16;  // per-member tick write log (ack resolution); past it the member's ACKs are streamed
@@ -208,8 +212,9 @@ struct Dev {
   uint32_t* sel;  // [N][8]
 
   uint32_t* rowk;  // [N][NS] key plane: row stride NS = N rounded up to 8 (32-B aligned rows for 16-B loads)
-  uint16_t* rowk16;  // [N][NS] or null: the key plane's 16-bit shadow (key16) that k_sync_diff streams for live-row
-                     // payloads on one GPU (2 B + 2 B per record compare instead of 4 B + 4 B); written with every key
+  uint8_t* rowk8;  // [N][NS8] or null: the key plane's 8-bit shadow (key8) that k_sync_diff streams for live-row
+                   // payloads on one GPU (1 B + 1 B per record compare instead of 4 B + 4 B); written with every key
+  uint32_t NS8;    // its row stride: N rounded up to 16 (16-B aligned rows for 16-B loads)
   uint32_t* rowa;  // [N][NS] aux plane
   uint32_t *fdl, *gl;  // [N][LCAP]
 
@@ -327,7 +332,9 @@ struct Dev {
   uint32_t* tlog;     // [2][NL][TL]
   uint32_t* tl_n;     // [2][NL]
   uint32_t* tl_tick;  // [2][NL]
-  uint32_t* dlist;    // [MSGCAP]
+  uint32_t* dlist;    // [MSGCAP] 16-B entries: payloads k_sync_diff streams from the 8-bit plane (k_ack_resolve)
+  uint32_t* dlist_w;  // [MSGCAP] 16-B entries: payloads it streams on 4-B keys
+  uint32_t* ndlw;
   uint32_t* ndl;
   // W > 1: the sender's write-log prefix (SyncMsg.tln entries) of each message of the inbound list committed this tick,
   // by its index there: copied by k_pack_all for this shard's senders and shipped in exchange A for the peers'

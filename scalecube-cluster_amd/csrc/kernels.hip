@@ -79,8 +79,10 @@ __global__ void k_init_rows(Dev d) {
       const uint64_t v = s >= d.N ? 0ull : (d.init_mode == 1 || m == s) ? full : 0ull;
       rk[s] = key32(v);
       ra[s] = aux32(v);
-      if (d.rowk16) d.rowk16[(size_t)li * d.NS + s] = key16(key32(v));
+      if (d.rowk8) d.rowk8[(size_t)li * d.NS8 + s] = key8(key32(v));
     }
+    if (d.rowk8)  // (the 8-bit plane's wider padding: zero, absent)
+      for (uint32_t s = d.NS + threadIdx.x; s < d.NS8; s += blockDim.x) d.rowk8[(size_t)li * d.NS8 + s] = 0;
     if (d.W > 1)  // dirty chunks against base_row: none for a PRECONVERGED row, the own chunk for a cold join
       for (uint32_t w = threadIdx.x; w < d.MW; w += blockDim.x)
         d.rdirty[(size_t)li * d.MW + w] = (d.init_mode != 1 && (m / CH) >> 6 == w) ? 1ull << ((m / CH) & 63) : 0ull;
@@ -298,8 +300,8 @@ __global__ void __launch_bounds__(256) k_seg_sort(uint64_t* key, uint32_t* val, 
 // k_sync_diff: for every SYNC / SYNC_ACK sent in tick k-1, stream the payload's key plane (the sender's live row,
 // or its copy-on-write snapshot) against the receiver's key plane and extract, per 2048-subject chunk and in
 // subject order, the records that differ (the eager `!r1.equals(table.get(id))` filter of syncMembership,
-// :456-467). This is the HBM-bound hot loop: 2 x 2 B read per subject per merge on one GPU (the keys' 16-bit
-// shadows, key16; an escaped key is compared on its 4-B key32), 2 x 4 B on a row shard. SHARDED adds payloads
+// :456-467). This is the HBM-bound hot loop: 2 x 1 B read per subject per merge on one GPU (the keys' 8-bit
+// shadows, key8; an escaped key is compared on its 4-B key32), 2 x 4 B on a row shard. SHARDED adds payloads
 // received from other shards (baseline row + shipped chunks); the single-GPU instance has only local rows and
 // snapshots.
 // this lane's 8 payload keys and 8 receiver keys of chunk c of message mi: the payload
@@ -307,41 +309,55 @@ __global__ void __launch_bounds__(256) k_seg_sort(uint64_t* key, uint32_t* val, 
 // chunk if it differs from the baseline, else the baseline
 // pinw: the arena row a live-row payload is copied into while it streams (pin_msg), else NEVER; loaded here with the
 // item's data so that no dependent load of the message waits at the top of the item's iteration
-// narrow (one GPU, a live-row payload that is not pinned): the item is chunks c and c + 1 of the message, lane i
-// the 16 subjects c CH + 16 i ..., and x holds their 16-bit shadow keys (key16): payload x[0..1], receiver x[2..3],
+// narrow (one GPU, a live-row payload that is not pinned): the item is chunks c .. c + 3 of the message, lane i
+// the 32 subjects c CH + 32 i ..., and x holds their 8-bit shadow keys (key8): payload x[0..1], receiver x[2..3],
 // the same 64 B per lane in flight as one chunk of 4-B keys. Every lane of the block takes the same item, so the mode
 // is uniform.
+// an item's message as k_sync_diff reads it (the 16-B entries of Dev::dlist / dlist_w, written by k_ack_resolve;
+// without a list, read from the message): x = the message index, y = sender, z = receiver, w = where the payload is
+// (desc_pay)
+__device__ __forceinline__ uint32_t desc_pay(const SyncMsg& mm) {
+  if (mm.kind & KF_DEFER) return DESC_DEFER;  // merged in a later tick: nothing to compare now
+  if (mm.payload != NEVER) return mm.payload;  // an arena snapshot, or (W > 1) PAY_RX | rx index
+  return mm.pin == NEVER ? NEVER : DESC_PIN | mm.pin;  // the live row (pinned: copied into the arena as it streams)
+}
+
+// this lane's keys of the item's chunk c: narrow (an entry of the narrow list: one GPU, an unpinned live-row payload):
+// the item is chunks c .. c + 3 of the message, lane i the 32 subjects c CH + 32 i ..., and x holds their 8-bit
+// shadow keys (key8): payload x[0..1], receiver x[2..3], the same 64 B per lane in flight as one chunk of 4-B keys.
+// Otherwise 8 payload keys and 8 receiver keys of chunk c: the payload is the sender's live row or its copy-on-write
+// snapshot; for a payload received from another shard, the shipped chunk if it differs from the baseline, else the
+// baseline. pinw: the arena row a live-row payload is copied into while it streams (pin_msg), else NEVER. Every lane
+// of the block takes the same item, so the mode is uniform.
 template <bool SHARDED>
-__device__ __forceinline__ void diff_fetch(const Dev& d, uint32_t b, uint32_t mi, uint32_t c, uint4 (&x)[4],
-                                           uint32_t& pinw, bool& narrow) {
-  const SyncMsg& mm = d.msgs[b][mi];
+__device__ __forceinline__ void diff_fetch(const Dev& d, uint32_t b, const uint4& D, uint32_t c, uint4 (&x)[4],
+                                           uint32_t& pinw, bool& narrow, bool narrow_item) {
   pinw = NEVER;
   narrow = false;
-  if (!SHARDED && d.rowk16 && mm.payload == NEVER && mm.pin == NEVER && !(mm.kind & KF_DEFER)) {
+  if (!SHARDED && narrow_item) {
     narrow = true;
-    const uint32_t n0 = c * CH + threadIdx.x * 16;  // NS is a multiple of 8: 8-subject groups are wholly in or out
-    const uint16_t* p16 = d.rowk16 + lidx(d, mm.src) * d.NS + n0;
-    const uint16_t* r16 = d.rowk16 + lidx(d, mm.dst) * d.NS + n0;
+    const uint32_t n0 = c * CH + threadIdx.x * 32;  // NS8 is a multiple of 16: 16-subject groups wholly in or out
+    const uint8_t* p8 = d.rowk8 + lidx(d, D.y) * d.NS8 + n0;
+    const uint8_t* r8 = d.rowk8 + lidx(d, D.z) * d.NS8 + n0;
     const uint4 z = make_uint4(0, 0, 0, 0);
-    x[0] = n0 < d.NS ? ld_c4((const uint32_t*)p16) : z;
-    x[1] = n0 + 8 < d.NS ? ld_c4((const uint32_t*)(p16 + 8)) : z;
-    x[2] = n0 < d.NS ? ld_c4((const uint32_t*)r16) : z;
-    x[3] = n0 + 8 < d.NS ? ld_c4((const uint32_t*)(r16 + 8)) : z;
+    x[0] = n0 < d.NS8 ? ld_c4((const uint32_t*)p8) : z;
+    x[1] = n0 + 16 < d.NS8 ? ld_c4((const uint32_t*)(p8 + 16)) : z;
+    x[2] = n0 < d.NS8 ? ld_c4((const uint32_t*)r8) : z;
+    x[3] = n0 + 16 < d.NS8 ? ld_c4((const uint32_t*)(r8 + 16)) : z;
     return;
   }
   const uint32_t s0 = c * CH + threadIdx.x * 8;
-  // NS is a multiple of 8: a 32-B group is wholly in or out; padding entries are 0 (absent). A delayed message
-  // (KF_DEFER) is merged in a later tick: nothing to compare now
-  if (s0 >= d.NS || (mm.kind & KF_DEFER)) {
+  // NS is a multiple of 8: a 32-B group is wholly in or out; padding entries are 0 (absent)
+  if (s0 >= d.NS || D.w == DESC_DEFER) {
     x[0] = x[1] = x[2] = x[3] = make_uint4(0, 0, 0, 0);
     return;
   }
   const uint32_t* p8;
-  if (mm.payload == NEVER) {
-    pinw = mm.pin;
-    p8 = d.rowk + lidx(d, mm.src) * d.NS + s0;
-  } else if (SHARDED && (mm.payload & PAY_RX)) {
-    const uint32_t ri = mm.payload & ~PAY_RX;
+  if (D.w == NEVER || (D.w & DESC_PIN)) {
+    pinw = D.w == NEVER ? NEVER : D.w & ~DESC_PIN;
+    p8 = d.rowk + lidx(d, D.y) * d.NS + s0;
+  } else if (SHARDED && (D.w & PAY_RX)) {
+    const uint32_t ri = D.w & ~PAY_RX;
     const uint64_t* mk = d.rx_mask + (size_t)ri * d.MW;
     if ((mk[c >> 6] >> (c & 63)) & 1ull) {
       uint32_t rank = __popcll(mk[c >> 6] & ((1ull << (c & 63)) - 1ull));
@@ -351,9 +367,9 @@ __device__ __forceinline__ void diff_fetch(const Dev& d, uint32_t b, uint32_t mi
       p8 = d.base_row + s0;
     }
   } else {
-    p8 = d.arena[b] + (size_t)mm.payload * d.NS + s0;
+    p8 = d.arena[b] + (size_t)D.w * d.NS + s0;
   }
-  const uint32_t* r8 = d.rowk + lidx(d, mm.dst) * d.NS + s0;
+  const uint32_t* r8 = d.rowk + lidx(d, D.z) * d.NS + s0;
   // (non-temporal loads measured 1.5x slower here on gfx950)
   x[0] = ld_c4(p8);
   x[1] = ld_c4(p8 + 4);
@@ -421,45 +437,45 @@ __device__ __forceinline__ void diff_chunk(const Dev& d, uint32_t b, uint32_t mi
   __syncthreads();
 }
 
-// a narrow item: chunks c and c + 1 of message mi, each wave one 1024-subject candidate segment (wave w: segment
-// 2c + w, 16 subjects per lane from x), tested, scanned and written by the wave alone: no block barrier. A lane with
-// an escaped shadow (0xFFFF: an incarnation past 16 382 among its subjects) compares its 16 full keys of both rows.
-__device__ __forceinline__ void diff_wave16(const Dev& d, uint32_t b, uint32_t mi, uint32_t c, const uint4 (&x)[4]) {
+// a narrow item: chunks c .. c + 3 of message mi, each wave two 1024-subject candidate segments (wave w: segments
+// 2c + 2w (lanes 0-31) and 2c + 2w + 1 (lanes 32-63), 32 subjects per lane from x), tested, scanned and written by the
+// wave alone: no block barrier. A lane with an escaped shadow (0xFF: an incarnation past 62 among its subjects)
+// compares its 32 full keys of both rows.
+__device__ __forceinline__ void diff_wave8(const Dev& d, uint32_t b, uint32_t mi, uint32_t src, uint32_t dst, uint32_t c,
+                                           const uint4 (&x)[4]) {
   const bool dl = d.ackres != 0;
-  const uint32_t lane = threadIdx.x & 63u, seg = 2 * c + (threadIdx.x >> 6);
-  const uint32_t n0 = c * CH + threadIdx.x * 16;  // = seg * MCH + lane * 16
+  const uint32_t lane = threadIdx.x & 63u, seg = 2 * c + 2 * (threadIdx.x >> 6) + (lane >> 5);
+  const uint32_t n0 = c * CH + threadIdx.x * 32;  // = seg * MCH + (lane & 31) * 32
   const uint32_t pw[8] = {x[0].x, x[0].y, x[0].z, x[0].w, x[1].x, x[1].y, x[1].z, x[1].w};
   const uint32_t rw[8] = {x[2].x, x[2].y, x[2].z, x[2].w, x[3].x, x[3].y, x[3].z, x[3].w};
-  uint32_t mask = 0, ab = 0;
-  bool esc = false;
+  uint32_t esc = 0;
 #pragma unroll
-  for (int q = 0; q < 8; ++q)
-    esc |= (pw[q] & 0xFFFFu) == 0xFFFFu || (pw[q] >> 16) == 0xFFFFu || (rw[q] & 0xFFFFu) == 0xFFFFu ||
-           (rw[q] >> 16) == 0xFFFFu;
+  for (int q = 0; q < 8; ++q)  // a 0xFF byte in either word (a zero byte of the complement)
+    esc |= ((~pw[q] - 0x01010101u) & pw[q] & 0x80808080u) | ((~rw[q] - 0x01010101u) & rw[q] & 0x80808080u);
+  uint32_t mask = 0, ab = 0;
   const uint32_t *pk = nullptr, *rk = nullptr;
-  if (esc) {
-    const SyncMsg& mm = d.msgs[b][mi];
-    pk = d.rowk + lidx(d, mm.src) * d.NS + n0;
-    rk = d.rowk + lidx(d, mm.dst) * d.NS + n0;
+  if (esc) {  // (rare) the 32 subjects' 4-B keys, one at a time
+    pk = d.rowk + lidx(d, src) * d.NS + n0;
+    rk = d.rowk + lidx(d, dst) * d.NS + n0;
 #pragma unroll 1
-    for (int j = 0; j < 16; ++j) {
+    for (uint32_t j = 0; j < 32; ++j) {
       const uint32_t p = n0 + j < d.NS ? pk[j] : 0u, r = n0 + j < d.NS ? rk[j] : 0u;
       if ((p & 3u) != ST_ABSENT && p != r) mask |= 1u << j;
       ab |= (uint32_t)((p & 3u) == ST_ABSENT && (r & 3u) != ST_ABSENT);
     }
   } else {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const uint32_t p = (pw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu, r = (rw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+    for (int j = 0; j < 32; ++j) {
+      const uint32_t p = (pw[j >> 2] >> (8 * (j & 3))) & 0xFFu, r = (rw[j >> 2] >> (8 * (j & 3))) & 0xFFu;
       if ((p & 3u) != ST_ABSENT && p != r) mask |= 1u << j;
       ab |= (uint32_t)((p & 3u) == ST_ABSENT && (r & 3u) != ST_ABSENT);
     }
   }
   const uint32_t nc = __popc(mask);
   uint32_t* cm = d.chunk_meta + ((size_t)mi * d.NMETA + seg) * 2;
-  const bool live = seg < d.NMETA;
-  if (!__ballot(nc | ab)) {  // steady state: the segment's 1024 subjects match
-    if (lane == 0 && live) cm[0] = cm[1] = 0;
+  const bool live = seg < d.NMETA, head = (lane & 31u) == 0;
+  if (!__ballot(nc | ab)) {  // steady state: the wave's 2048 subjects match
+    if (head && live) cm[0] = cm[1] = 0;
     return;
   }
   if (dl && __ballot(ab) && lane == 0) atomicOr(&d.msgs[b][mi].kind, KF_ABS);  // (rare: a record the payload lacks)
@@ -469,97 +485,128 @@ __device__ __forceinline__ void diff_wave16(const Dev& d, uint32_t b, uint32_t m
     const uint32_t v = __shfl_up(incl, o);
     if (lane >= o) incl += v;
   }
-  uint32_t totc = __shfl(incl, 63), bo = 0;
+  const uint32_t totc = __shfl(incl, 63), first = __shfl(incl, 31);  // both segments, the first one
+  uint32_t bo = 0;
   if (lane == 0 && totc) {
     bo = atomicAdd(d.pool_used, totc);
-    if (bo + totc > d.POOLCAP) {  // no room: nothing of this segment is written (the error aborts the step)
+    if (bo + totc > d.POOLCAP) {  // no room: nothing of these segments is written (the error aborts the step)
       atomicOr(d.err, E_POOL);
       bo = NEVER;
     }
     if (bo != NEVER) atomicAdd(&d.msgs[b][mi].ncand, totc);
   }
   bo = __shfl(bo, 0);
-  if (lane == 0 && live) {
-    cm[0] = bo;
-    cm[1] = bo == NEVER ? 0u : totc;
+  if (head && live) {
+    const uint32_t off = lane ? first : 0u, cnt = lane ? totc - first : first;
+    cm[0] = bo == NEVER ? NEVER : bo + off;
+    cm[1] = bo == NEVER ? 0u : cnt;
   }
   if (bo == NEVER) return;  // (an overflowed segment must not overwrite other segments' candidates)
   uint32_t o = bo + incl - nc;
-  for (uint32_t m = mask; m; m &= m - 1, ++o) {
-    const uint32_t j = (uint32_t)(__ffs(m) - 1);
-    const uint32_t p = esc ? pk[j] : (pw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-    d.pool[o] = ((uint64_t)(n0 + j) << 34) | key34(p);
+  if (esc) {
+    for (uint32_t m = mask; m; m &= m - 1, ++o) {
+      const uint32_t j = (uint32_t)(__ffs(m) - 1);
+      d.pool[o] = ((uint64_t)(n0 + j) << 34) | key34(pk[j]);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 32; ++j)
+      if (mask & (1u << j)) d.pool[o++] = ((uint64_t)(n0 + j) << 34) | key34((pw[j >> 2] >> (8 * (j & 3))) & 0xFFu);
   }
 }
 
-// k_sync_diff's work: the items of `nmsg` messages (list[j], or j itself without a list) over the blocks blk of nblk,
-// grid-stride, with the next item's loads in flight while the current one is tested. An item is PER chunks of a
-// message (2 on one GPU: a narrow item's 16-bit keys; a wide item's second chunk is loaded when the first is done)
+// k_sync_diff's work, two lists of 16-B entries (message, sender, receiver, payload place; desc_pay) over the blocks
+// blk of nblk, grid-stride, each with the next item's keys in flight while the current one is tested and the entry of
+// the item after that in flight too, so that an item's key loads never wait for its message:
+// * stream_wide: payloads compared on 4-B keys (snapshots, pinned live rows, row shards, or no 8-bit plane), one
+//   2048-subject chunk per item, block barriers per chunk (diff_chunk);
+// * stream_narrow (one GPU): unpinned live-row payloads on the 8-bit plane, four chunks per item, one wave per two
+//   1024-subject candidate segments and no block barrier (diff_wave8).
+// Two loops rather than one with both kinds of item: the narrow loop's registers are then not sized by the wide
+// path's (with both in one loop it spilled, and a scratch reload made every iteration wait for the prefetched keys).
+// A list entry is block-uniform: held in scalar registers once loaded (uni), so that the addresses, modes and
+// branches derived from it are scalar.
+__device__ __forceinline__ uint4 uni(const uint4& v) {
+  return make_uint4(__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y),
+                    __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w));
+}
+// list entry j (without a list: message j itself, read from the message buffer)
+__device__ __forceinline__ uint4 diff_entry(const Dev& d, uint32_t b, const uint4* lst, uint32_t j) {
+  if (lst) return lst[j];
+  const SyncMsg& mm = d.msgs[b][j];
+  return make_uint4(j, mm.src, mm.dst, desc_pay(mm));
+}
+
 template <bool SHARDED>
-__device__ __forceinline__ void stream_list(const Dev& d, uint32_t b, const uint32_t* dlp, uint32_t nmsg, uint32_t blk,
+__device__ __forceinline__ void stream_wide(const Dev& d, uint32_t b, const uint4* lst, uint32_t n, uint32_t blk,
                                             uint32_t nblk, uint32_t* scan, uint32_t& base, uint32_t timed) {
-  constexpr uint32_t PER = SHARDED ? 1u : 2u;
-  const uint32_t nch = d.NCHUNK, nit = (nch + PER - 1) / PER;
-  const uint32_t total = nmsg * nit;
-  uint4 cur[4];
-  uint32_t mcur = 0, pcur = NEVER;
-  bool ncur = false;
+  const uint32_t nch = d.NCHUNK, total = n * nch;
+  uint4 cur[4], dc = make_uint4(0, 0, 0, 0), dn = dc;
+  uint32_t pcur = NEVER;
+  bool nw;
   if (blk < total) {
-    mcur = dlp ? dlp[blk / nit] : blk / nit;
-    diff_fetch<SHARDED>(d, b, mcur, (blk % nit) * PER, cur, pcur, ncur);
+    dc = uni(diff_entry(d, b, lst, blk / nch));
+    diff_fetch<SHARDED>(d, b, dc, blk % nch, cur, pcur, nw, false);
   }
+  if (blk + nblk < total) dn = diff_entry(d, b, lst, (blk + nblk) / nch);
   for (uint32_t w = blk; w < total; w += nblk) {
-    uint4 nxt[4];
-    uint32_t mnxt = 0, pnxt = NEVER;
-    bool nnxt = false;
-    if (w + nblk < total) {
-      mnxt = dlp ? dlp[(w + nblk) / nit] : (w + nblk) / nit;
-      diff_fetch<SHARDED>(d, b, mnxt, ((w + nblk) % nit) * PER, nxt, pnxt, nnxt);
-    }
-    const uint32_t mi = mcur, c0 = (w % nit) * PER;
-    if (!SHARDED && !ncur && c0 == 0 && threadIdx.x == 0 && d.rowk16) {  // priced at 8 B per subject (swim_counters)
+    uint4 nxt[4], dnn = make_uint4(0, 0, 0, 0);
+    uint32_t pnxt = NEVER;
+    const uint4 du = uni(dn);
+    if (w + nblk < total) diff_fetch<SHARDED>(d, b, du, (w + nblk) % nch, nxt, pnxt, nw, false);
+    if (w + 2 * nblk < total) dnn = diff_entry(d, b, lst, (w + 2 * nblk) / nch);
+    const uint32_t mi = dc.x, c = w % nch, s0 = c * CH + threadIdx.x * 8;
+    if (!SHARDED && c == 0 && threadIdx.x == 0) {  // priced at 8 B per subject (swim_counters)
       atomicAdd(&d.ctr[C_DIFFWIDE_ALL], 1ull);
       if (timed) atomicAdd(&d.ctr[C_DIFFWIDE], 1ull);
     }
-    if (ncur) {
-      diff_wave16(d, b, mi, c0, cur);
-    } else {
-#pragma unroll
-      for (uint32_t h = 0; h < PER; ++h) {
-        const uint32_t c = c0 + h;
-        if (c >= nch) break;  // (block-uniform)
-        const uint32_t s0 = c * CH + threadIdx.x * 8;
-        uint32_t p[8], r[8];
-        if (h > 0) {  // a wide item's later chunk
-          bool nw;
-          diff_fetch<SHARDED>(d, b, mi, c, cur, pcur, nw);
-        }
-        if (pcur != NEVER && s0 < d.NS) {  // a live-row payload read again later (pin_msg)
-          uint4* dst = (uint4*)(d.arena[b] + (size_t)pcur * d.NS + s0);
-          dst[0] = cur[0];
-          dst[1] = cur[1];
-        }
-        const uint32_t pv[8] = {cur[0].x, cur[0].y, cur[0].z, cur[0].w, cur[1].x, cur[1].y, cur[1].z, cur[1].w};
-        const uint32_t rv[8] = {cur[2].x, cur[2].y, cur[2].z, cur[2].w, cur[3].x, cur[3].y, cur[3].z, cur[3].w};
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          p[j] = pv[j];
-          r[j] = rv[j];
-        }
-        diff_chunk(d, b, mi, c, s0, p, r, scan, base);
-      }
+    if (pcur != NEVER && s0 < d.NS) {  // a live-row payload read again later (pin_msg)
+      uint4* dst = (uint4*)(d.arena[b] + (size_t)pcur * d.NS + s0);
+      dst[0] = cur[0];
+      dst[1] = cur[1];
     }
+    const uint32_t p[8] = {cur[0].x, cur[0].y, cur[0].z, cur[0].w, cur[1].x, cur[1].y, cur[1].z, cur[1].w};
+    const uint32_t r[8] = {cur[2].x, cur[2].y, cur[2].z, cur[2].w, cur[3].x, cur[3].y, cur[3].z, cur[3].w};
+    diff_chunk(d, b, mi, c, s0, p, r, scan, base);
 #pragma unroll
     for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
-    mcur = mnxt;
+    dc = du;
+    dn = dnn;
     pcur = pnxt;
-    ncur = nnxt;
   }
 }
 
-// k_sync_diff: the diff of every payload streamed this tick (see diff_fetch and stream_list above)
+__device__ __forceinline__ void stream_narrow(const Dev& d, uint32_t b, const uint4* lst, uint32_t n, uint32_t blk,
+                                              uint32_t nblk) {
+  constexpr uint32_t PER = 4;
+  const uint32_t nit = (d.NCHUNK + PER - 1) / PER, total = n * nit;
+  uint4 cur[4], dc = make_uint4(0, 0, 0, 0), dn = dc;
+  uint32_t pw;
+  bool nr;
+  if (blk < total) {
+    dc = uni(lst[blk / nit]);
+    diff_fetch<false>(d, b, dc, (blk % nit) * PER, cur, pw, nr, true);
+  }
+  if (blk + nblk < total) dn = lst[(blk + nblk) / nit];
+  for (uint32_t w = blk; w < total; w += nblk) {
+    uint4 nxt[4], dnn = make_uint4(0, 0, 0, 0);
+    const uint4 du = uni(dn);
+    if (w + nblk < total) diff_fetch<false>(d, b, du, ((w + nblk) % nit) * PER, nxt, pw, nr, true);
+    if (w + 2 * nblk < total) dnn = lst[(w + 2 * nblk) / nit];
+    diff_wave8(d, b, dc.x, dc.y, dc.z, (w % nit) * PER, cur);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
+    dc = du;
+    dn = dnn;
+  }
+}
+
+// k_sync_diff: the diff of every payload streamed this tick (see diff_fetch and the stream loops above). The wide
+// items go first, on blocks 0, 1, ...; the narrow ones continue from the block after the last wide one.
+// DIFF_WAVES waves per SIMD; the grid is DIFF_WAVES blocks per CU, all resident (diff_grid)
+constexpr uint32_t DIFF_WAVES = 7;
 template <bool SHARDED>
-__global__ void __launch_bounds__(256, 8) k_sync_diff(const Dev* __restrict__ dp, uint32_t b, uint32_t timed, uint32_t spec) {
+__global__ void __launch_bounds__(256, DIFF_WAVES) k_sync_diff(const Dev* __restrict__ dp, uint32_t b, uint32_t timed, uint32_t spec) {
   const Dev& d = *dp;  // global, not kernarg (as k_member_tick): a by-value Dev of this size was copied to scratch
   if (spec && *(volatile uint32_t*)d.halt) return;  // a speculative batch halted at an earlier tick
   __shared__ uint32_t scan[256];
@@ -567,18 +614,23 @@ __global__ void __launch_bounds__(256, 8) k_sync_diff(const Dev* __restrict__ dp
   // (timed launches are bracketed by HIP events on the stream. A self-timing variant, first block start to last block
   // end by wall clock and atomics, made every launch of this kernel 30 % slower by its mere presence in the code:
   // 85 -> 112 us per launch at C3, profiles/r03_*)
-  // with SYNC_ACK resolution, only the messages k_ack_resolve left in dlist
+  // with SYNC_ACK resolution, only the messages k_ack_resolve listed (and counted); without it every message, on
+  // 4-B keys
   const bool dl = d.ackres != 0;
-  uint32_t nmsg = dl ? *(volatile uint32_t*)d.ndl : (d.nmsg[b] < d.MSGCAP ? d.nmsg[b] : d.MSGCAP);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  const uint32_t nmsg = d.nmsg[b] < d.MSGCAP ? d.nmsg[b] : d.MSGCAP;
+  const uint32_t nwide = dl ? *(volatile uint32_t*)d.ndlw : nmsg;
+  const uint32_t nnar = !SHARDED && dl ? *(volatile uint32_t*)d.ndl : 0u;
+  if (!dl && blockIdx.x == 0 && threadIdx.x == 0) {
     atomicAdd(&d.ctr[C_DIFFMSG_ALL], (unsigned long long)nmsg);
     if (timed) atomicAdd(&d.ctr[C_DIFFMSG], (unsigned long long)nmsg);
-    if (SHARDED || !d.rowk16) {  // every payload compared on 4-B keys
+    if (SHARDED) {  // (one GPU: stream_wide counts its messages)
       atomicAdd(&d.ctr[C_DIFFWIDE_ALL], (unsigned long long)nmsg);
       if (timed) atomicAdd(&d.ctr[C_DIFFWIDE], (unsigned long long)nmsg);
     }
   }
-  stream_list<SHARDED>(d, b, dl ? d.dlist : nullptr, nmsg, blockIdx.x, gridDim.x, scan, base, timed);
+  const uint32_t nblk = gridDim.x, wtot = nwide * d.NCHUNK;
+  stream_wide<SHARDED>(d, b, dl ? (const uint4*)d.dlist_w : nullptr, nwide, blockIdx.x, nblk, scan, base, timed);
+  if (!SHARDED && nnar) stream_narrow(d, b, (const uint4*)d.dlist, nnar, (blockIdx.x + nblk - wtot % nblk) % nblk, nblk);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -595,10 +647,11 @@ __global__ void __launch_bounds__(256, 8) k_sync_diff(const Dev* __restrict__ dp
 struct ResArgs {
   const uint32_t *halt, *nmsg, *tl_tick, *tl_n, *tlog, *rowk, *arena;
   SyncMsg* msgs;
-  uint32_t *dlist, *ndl, *chunk_meta, *pool_used, *err;
+  uint32_t *dlist, *ndl, *dlist_w, *ndlw, *chunk_meta, *pool_used, *err;
   uint64_t* pool;
   unsigned long long* ctr;
   uint32_t NL, NS, MSGCAP, NCHUNK, POOLCAP, NMETA;
+  uint32_t k8;  // the 8-bit key plane exists (k_sync_diff streams live-row payloads narrow)
   // W > 1: this shard's first observer, the senders' log prefixes by message (Dev::mlog), and the received payloads
   // (baseline row + shipped chunks, as diff_fetch reads them)
   uint32_t lo, W, MW;
@@ -695,7 +748,8 @@ __device__ __forceinline__ bool res_wave(const ResArgs& d, uint32_t i, uint32_t 
 __global__ void __launch_bounds__(512) k_ack_resolve(ResArgs d, uint32_t k, uint32_t spec, uint32_t timed) {
   if (spec && *(volatile uint32_t*)d.halt) return;
   __shared__ uint32_t sv_[8][64], sc_[8][64];
-  __shared__ uint32_t slist[8], nstream, nres, sbase;
+  __shared__ uint4 slist[8], wlist[8];
+  __shared__ uint32_t nstream, nwide, nres, sbase, wbase;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   volatile uint32_t* sv = sv_[wv];  // this wave's lists (volatile: read across lanes)
   volatile uint32_t* sc = sc_[wv];
@@ -703,26 +757,42 @@ __global__ void __launch_bounds__(512) k_ack_resolve(ResArgs d, uint32_t k, uint
   // block-uniform loop, one message per wave; the stream list and the counters take one atomic per block (a few
   // hundred waves adding to one address one by one took ~17 us per tick at C3)
   for (uint32_t base = blockIdx.x * 8; base < nmsg; base += gridDim.x * 8) {
-    if (threadIdx.x == 0) nstream = nres = 0;
+    if (threadIdx.x == 0) nstream = nwide = nres = 0;
     __syncthreads();
     const uint32_t i = base + wv;
     if (i < nmsg) {  // wave-uniform
       if (res_wave(d, i, k, lane, sv, sc)) {
         if (lane == 0) atomicAdd(&nres, 1u);
-      } else if (lane == 0) {
-        slist[atomicAdd(&nstream, 1u)] = i;
+      } else if (lane == 0) {  // its entry in the narrow list (one GPU, unpinned live row) or the wide one
+        const SyncMsg& mm = d.msgs[i];
+        const uint32_t pw = desc_pay(mm);
+        const uint4 e = make_uint4(i, mm.src, mm.dst, pw);
+        if (d.W == 1 && d.k8 && pw == NEVER)
+          slist[atomicAdd(&nstream, 1u)] = e;
+        else
+          wlist[atomicAdd(&nwide, 1u)] = e;
       }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
       if (nstream) sbase = atomicAdd(d.ndl, nstream);
+      if (nwide) wbase = atomicAdd(d.ndlw, nwide);
+      if (nstream + nwide) {  // the messages k_sync_diff streams (the wide ones: 8 B per subject)
+        atomicAdd(&d.ctr[C_DIFFMSG_ALL], (unsigned long long)(nstream + nwide));
+        if (timed) atomicAdd(&d.ctr[C_DIFFMSG], (unsigned long long)(nstream + nwide));
+      }
+      if (nwide && d.W > 1) {  // (one GPU: k_sync_diff counts its wide messages)
+        atomicAdd(&d.ctr[C_DIFFWIDE_ALL], (unsigned long long)nwide);
+        if (timed) atomicAdd(&d.ctr[C_DIFFWIDE], (unsigned long long)nwide);
+      }
       if (nres) {
         atomicAdd(&d.ctr[C_ACKRES_ALL], (unsigned long long)nres);
         if (timed) atomicAdd(&d.ctr[C_ACKRES], (unsigned long long)nres);
       }
     }
     __syncthreads();
-    if (threadIdx.x < nstream) d.dlist[sbase + threadIdx.x] = slist[threadIdx.x];
+    if (threadIdx.x < nstream) ((uint4*)d.dlist)[sbase + threadIdx.x] = slist[threadIdx.x];
+    if (threadIdx.x >= 64 && threadIdx.x - 64 < nwide) ((uint4*)d.dlist_w)[wbase + threadIdx.x - 64] = wlist[threadIdx.x - 64];
     __syncthreads();  // (slist and the counts are reused)
   }
 }
@@ -837,11 +907,16 @@ void launch_init(const Dev& d, void* stream) {
 }
 
 // timed: this launch is bracketed by profiling events; it adds its message count to ctr[C_DIFFMSG]
-// 8 resident blocks per CU; SWIM_DIFF_GRID overrides it (measurements; a value that does not parse, or 0, keeps 2048)
+// DIFF_WAVES resident blocks per CU (the launch bounds), all of them resident; SWIM_DIFF_GRID overrides it
+// (measurements; a value that does not parse, or 0, keeps the default)
 static uint32_t diff_grid() {
   const char* e = getenv("SWIM_DIFF_GRID");
   const unsigned long v = e ? strtoul(e, nullptr, 0) : 0ul;
-  return v >= 1 && v <= (1ul << 20) ? (uint32_t)v : 2048u;
+  if (v >= 1 && v <= (1ul << 20)) return (uint32_t)v;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  return DIFF_WAVES * (uint32_t)cus;
 }
 
 // a timed launch carries its start / stop events in its own dispatch (hipExtLaunchKernelGGL): the interval is the
@@ -869,8 +944,8 @@ static void launch_ack_resolve(const Dev& d, uint32_t k, hipStream_t st, bool sp
   if (k == 0 || !d.ackres) return;
   const uint32_t b = (k - 1) & 1;
   const ResArgs ra{d.halt, d.nmsg + b, d.tl_tick, d.tl_n, d.tlog, d.rowk, d.arena[b], d.msgs[b], d.dlist, d.ndl,
-                   d.chunk_meta, d.pool_used, d.err, d.pool, d.ctr, d.NL, d.NS, d.MSGCAP, d.NCHUNK, d.POOLCAP, d.NMETA,
-                   d.lo, d.W, d.MW, d.mlog, d.base_row, d.rx_mask, d.rx_off, d.xa_recv};
+                   d.dlist_w, d.ndlw, d.chunk_meta, d.pool_used, d.err, d.pool, d.ctr, d.NL, d.NS, d.MSGCAP, d.NCHUNK, d.POOLCAP, d.NMETA,
+                   d.rowk8 ? 1u : 0u, d.lo, d.W, d.MW, d.mlog, d.base_row, d.rx_mask, d.rx_off, d.xa_recv};
   hipLaunchKernelGGL(k_ack_resolve, dim3(128), dim3(512), 0, st, ra, k, spec ? 1u : 0u, timed ? 1u : 0u);
 }
 

@@ -189,7 +189,7 @@ __device__ __forceinline__ void row_put(ML& L, uint32_t s, uint64_t v, uint32_t 
   }
   if (L.d->ackres && old != k) tl_add(L, s);
   L.rk[s] = k;
-  if (L.d->rowk16) L.d->rowk16[(L.rk - L.d->rowk) + s] = key16(k);
+  if (L.d->rowk8) L.d->rowk8[lidx(*L.d, L.m) * L.d->NS8 + s] = key8(k);
   if (L.rd && k != L.d->base_row[s]) L.rd[(s / CH) >> 6] |= 1ull << ((s / CH) & 63);
   L.ra[s] = aux32(v);
 }
@@ -1811,7 +1811,7 @@ __device__ __forceinline__ void inbox_batch(ML& L, uint32_t lane, uint32_t cnt, 
     v = rec_with_timer(v, s1 == ST_SUSPECT ? ((alive_before || T0 == 0) ? dl : T0) : 0u);
     L.rk[s] = key32(v);
     L.ra[s] = aux32(v);
-    if (d.rowk16) d.rowk16[(L.rk - d.rowk) + s] = key16(key32(v));
+    if (d.rowk8) d.rowk8[lidx(d, L.m) * d.NS8 + s] = key8(key32(v));
   }
   if (act) L.c[C_R]++;
   if (acc) L.c[C_W]++;

@@ -36,9 +36,10 @@ SW_HD uint32_t rec_inc(uint64_t v) { return (uint32_t)v; }
 SW_HD uint64_t rec_key(uint32_t st, uint32_t inc) { return (uint64_t)inc | ((uint64_t)st << 32); }
 constexpr uint32_t INC_LIMIT = 1u << 30;
 SW_HD uint32_t key32(uint64_t v) { return ((uint32_t)v << 2) | rec_status(v); }
-// the 16-bit shadow of a key (Dev::rowk16, k_sync_diff): the key itself below 0xFFFF (incarnations up to 16 382),
-// else the escape 0xFFFF, whose subjects the diff compares on the full keys
-SW_HD uint16_t key16(uint32_t k) { return k < 0xFFFFu ? (uint16_t)k : (uint16_t)0xFFFFu; }
+// the 8-bit shadow of a key (Dev::rowk8, k_sync_diff): the key itself below 0xFF (incarnations up to 62, or 63 for a
+// record that is not DEAD), else the escape 0xFF, whose subjects the diff compares on the full keys. Two keys below
+// 0xFF are equal iff their shadows are, so the shadow compare is exact wherever neither side escapes
+SW_HD uint8_t key8(uint32_t k) { return k < 0xFFu ? (uint8_t)k : (uint8_t)0xFFu; }
 SW_HD uint64_t key34(uint32_t k) { return (uint64_t)(k >> 2) | ((uint64_t)(k & 3u) << 32); }
 SW_HD uint32_t aux32(uint64_t v) { return (uint32_t)(v >> 34); }
 SW_HD uint64_t rec_join(uint32_t k, uint32_t a) { return key34(k) | ((uint64_t)a << 34); }

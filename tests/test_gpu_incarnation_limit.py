@@ -40,6 +40,8 @@ def test_incarnation_at_the_limit(engine):
 
 
 def test_key16_escape_boundary(oracle, engine):
+    """Incarnations around 16 382 (the 16-bit shadow's escape in round 5): far past the 8-bit shadow's, so every
+    payload lane holding a mover compares its subjects on the full keys, under loss and SYNCs."""
     n = 64
     cfg = SimConfig(n_members=n, cluster=ClusterConfig(syncInterval=1000), record_events=True, seed=0x16B)
     o, e = pair(oracle, engine, cfg)
@@ -55,5 +57,29 @@ def test_key16_escape_boundary(oracle, engine):
             for m in movers:
                 c.update_incarnation(m)
         run_lockstep(o, e, 40, 10, f"bump {step + 1} across the escape")
+    o.close()
+    e.close()
+
+
+def test_key8_escape_boundary(oracle, engine):
+    """The 8-bit shadow the SYNC diff streams on one GPU (key8: the key itself below 0xFF, else the escape 0xFF): movers
+    start at incarnations 60-63 and are bumped across 62 / 63 (keys 249-255, DEAD at 63 is the first escaped key) and
+    past 64, in different 32-subject lanes of the diff and at a lane boundary (31 / 32), under loss and SYNCs every
+    tick; every merged record against the oracle."""
+    n = 200
+    cfg = SimConfig(n_members=n, cluster=ClusterConfig(syncInterval=1000), record_events=True, seed=0x8B)
+    o, e = pair(oracle, engine, cfg)
+    lib = {id(o): oracle, id(e): engine}
+    movers = (3, 31, 32, 95, 150, 199)
+    for c in (o, e):
+        c.set_default_loss(10)
+        for j, m in enumerate(movers):
+            assert _abi.debug_set_incarnation(lib[id(c)], c._h, m, 60 + j % 4) == 0
+    run_lockstep(o, e, 30, 10, "incarnations below the 8-bit escape")
+    for step in range(4):
+        for c in (o, e):
+            for m in movers[step % 2::2]:
+                c.update_incarnation(m)
+        run_lockstep(o, e, 30, 10, f"bump {step + 1} across the 8-bit escape")
     o.close()
     e.close()
