@@ -117,3 +117,40 @@ def test_ack_resolution_sharded_steady_accounting(engine, world):
         ref.run_periods(6)
         assert np.array_equal(ref.state_hash(), h)
         ref.close()
+
+
+def test_diff_modes_agree(engine):
+    """The SYNC diff's three ways of reading payloads give the same run: the 8-bit shadow plane (narrow list) with wide
+    payloads in their own list (default), every payload on 4-B keys through the wide list (SWIM_NO_K8), and every
+    payload streamed from the message buffer without SYNC_ACK resolution (SWIM_NO_ACKRES). Some members start at
+    incarnation 60 and are bumped past the 8-bit escape while SYNCs run every tick, under loss, kills and a leave."""
+    from swimhip import _abi
+    cfg = SimConfig(n_members=400, cluster=FAST_SYNC, gossip_slot_cap=1 << 16)
+    runs = []
+    for env in (None, "SWIM_NO_K8", "SWIM_NO_ACKRES"):
+        if env:
+            os.environ[env] = "1"
+        try:
+            c = SimulatedCluster(engine, cfg)
+        finally:
+            if env:
+                os.environ.pop(env, None)
+        for m in (7, 31, 32, 200, 399):
+            assert _abi.debug_set_incarnation(engine, c._h, m, 60) == 0
+        hs = []
+        for phase in range(3):
+            faults(c, phase) if phase < 2 else c.leave(90)
+            for m in (7, 32, 200):
+                c.update_incarnation(m)
+            c.step(60)
+            hs.append(c.state_hash())
+        runs.append((env, hs, c.events(), c.counters()))
+        c.close()
+    ref = runs[0]
+    assert ref[3]["diff_msgs_total"] > 0
+    for env, hs, ev, ctr in runs[1:]:
+        for x, y in zip(ref[1], hs):
+            assert np.array_equal(x, y), env
+        assert ev == ref[2], env
+        for k in ("record_compares", "row_writes", "messages", "events", "sync_merges", "messages_lost"):
+            assert ctr[k] == ref[3][k], (env, k)
