@@ -807,9 +807,10 @@ int build(swim_handle* h) {
       h->hrecv.resize(d.W * std::max(d.XA_PEER, d.XB_PEER));
     }
   }
-  // one GPU, stored tables: the diff's 8-bit shadow plane, only when it fits beside everything else with the usual
-  // growth reserve (an optimisation: without it k_sync_diff and row_put use the u32 keys; SWIM_NO_K8 forces that)
-  if (d.W == 1 && !d.implicit && !getenv("SWIM_NO_K8")) {
+  // stored tables: the diff's 8-bit shadow plane of this shard's rows, only when it fits beside everything else with
+  // the usual growth reserve (an optimisation: without it k_sync_diff and row_put use the u32 keys; SWIM_NO_K8 forces
+  // that). On a row shard it serves the payloads of local senders; peers' payloads arrive as u32 chunks
+  if (!d.implicit && !getenv("SWIM_NO_K8")) {
     size_t fr = 0, tot = 0;
     HIPCK(hipMemGetInfo(&fr, &tot));
     if ((uint64_t)fr > NV * d.NS8 + (4ull << 30)) A(d.rowk8, NV * d.NS8)

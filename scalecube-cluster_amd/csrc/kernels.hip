@@ -301,7 +301,7 @@ __global__ void __launch_bounds__(256) k_seg_sort(uint64_t* key, uint32_t* val, 
 // or its copy-on-write snapshot) against the receiver's key plane and extract, per 2048-subject chunk and in
 // subject order, the records that differ (the eager `!r1.equals(table.get(id))` filter of syncMembership,
 // :456-467). This is the HBM-bound hot loop: 2 x 1 B read per subject per merge on one GPU (the keys' 8-bit
-// shadows, key8; an escaped key is compared on its 4-B key32), 2 x 4 B on a row shard. SHARDED adds payloads
+// shadows, key8; an escaped key is compared on its 4-B key32), 2 x 4 B for the rest. SHARDED adds payloads
 // received from other shards (baseline row + shipped chunks); the single-GPU instance has only local rows and
 // snapshots.
 // this lane's 8 payload keys and 8 receiver keys of chunk c of message mi: the payload
@@ -322,7 +322,8 @@ __device__ __forceinline__ uint32_t desc_pay(const SyncMsg& mm) {
   return mm.pin == NEVER ? NEVER : DESC_PIN | mm.pin;  // the live row (pinned: copied into the arena as it streams)
 }
 
-// this lane's keys of the item's chunk c: narrow (an entry of the narrow list: one GPU, an unpinned live-row payload):
+// this lane's keys of the item's chunk c: narrow (an entry of the narrow list: an unpinned live-row payload of a local
+// sender):
 // the item is chunks c .. c + 3 of the message, lane i the 32 subjects c CH + 32 i ..., and x holds their 8-bit
 // shadow keys (key8): payload x[0..1], receiver x[2..3], the same 64 B per lane in flight as one chunk of 4-B keys.
 // Otherwise 8 payload keys and 8 receiver keys of chunk c: the payload is the sender's live row or its copy-on-write
@@ -518,10 +519,10 @@ __device__ __forceinline__ void diff_wave8(const Dev& d, uint32_t b, uint32_t mi
 // k_sync_diff's work, two lists of 16-B entries (message, sender, receiver, payload place; desc_pay) over the blocks
 // blk of nblk, grid-stride, each with the next item's keys in flight while the current one is tested and the entry of
 // the item after that in flight too, so that an item's key loads never wait for its message:
-// * stream_wide: payloads compared on 4-B keys (snapshots, pinned live rows, row shards, or no 8-bit plane), one
-//   2048-subject chunk per item, block barriers per chunk (diff_chunk);
-// * stream_narrow (one GPU): unpinned live-row payloads on the 8-bit plane, four chunks per item, one wave per two
-//   1024-subject candidate segments and no block barrier (diff_wave8).
+// * stream_wide: payloads compared on 4-B keys (snapshots, pinned live rows, payloads from other shards, or no 8-bit
+//   plane), one 2048-subject chunk per item, block barriers per chunk (diff_chunk);
+// * stream_narrow: unpinned live-row payloads (on a row shard: of local senders) on the 8-bit plane, four chunks per
+//   item, one wave per two 1024-subject candidate segments and no block barrier (diff_wave8).
 // Two loops rather than one with both kinds of item: the narrow loop's registers are then not sized by the wide
 // path's (with both in one loop it spilled, and a scratch reload made every iteration wait for the prefetched keys).
 // A list entry is block-uniform: held in scalar registers once loaded (uni), so that the addresses, modes and
@@ -619,7 +620,7 @@ __global__ void __launch_bounds__(256, DIFF_WAVES) k_sync_diff(const Dev* __rest
   const bool dl = d.ackres != 0;
   const uint32_t nmsg = d.nmsg[b] < d.MSGCAP ? d.nmsg[b] : d.MSGCAP;
   const uint32_t nwide = dl ? *(volatile uint32_t*)d.ndlw : nmsg;
-  const uint32_t nnar = !SHARDED && dl ? *(volatile uint32_t*)d.ndl : 0u;
+  const uint32_t nnar = dl ? *(volatile uint32_t*)d.ndl : 0u;
   if (!dl && blockIdx.x == 0 && threadIdx.x == 0) {
     atomicAdd(&d.ctr[C_DIFFMSG_ALL], (unsigned long long)nmsg);
     if (timed) atomicAdd(&d.ctr[C_DIFFMSG], (unsigned long long)nmsg);
@@ -630,7 +631,7 @@ __global__ void __launch_bounds__(256, DIFF_WAVES) k_sync_diff(const Dev* __rest
   }
   const uint32_t nblk = gridDim.x, wtot = nwide * d.NCHUNK;
   stream_wide<SHARDED>(d, b, dl ? (const uint4*)d.dlist_w : nullptr, nwide, blockIdx.x, nblk, scan, base, timed);
-  if (!SHARDED && nnar) stream_narrow(d, b, (const uint4*)d.dlist, nnar, (blockIdx.x + nblk - wtot % nblk) % nblk, nblk);
+  if (nnar) stream_narrow(d, b, (const uint4*)d.dlist, nnar, (blockIdx.x + nblk - wtot % nblk) % nblk, nblk);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -767,7 +768,7 @@ __global__ void __launch_bounds__(512) k_ack_resolve(ResArgs d, uint32_t k, uint
         const SyncMsg& mm = d.msgs[i];
         const uint32_t pw = desc_pay(mm);
         const uint4 e = make_uint4(i, mm.src, mm.dst, pw);
-        if (d.W == 1 && d.k8 && pw == NEVER)
+        if (d.k8 && pw == NEVER)  // (on a row shard: a local sender's row)
           slist[atomicAdd(&nstream, 1u)] = e;
         else
           wlist[atomicAdd(&nwide, 1u)] = e;
