@@ -694,6 +694,7 @@ int build(swim_handle* h) {
   const uint64_t NV = d.implicit ? 1 : NL;  // implicit views: no table or list is stored
   A(d.rowk, NV * d.NS) A(d.rowa, NV * d.NS) A(d.fdl, NV * d.LCAP) A(d.gl, NV * d.LCAP)
   d.rowk8 = nullptr;  // allocated last, if it fits (below)
+  d.base_row8 = nullptr;
   d.NS8 = (c.n_members + 15u) & ~15u;
   A(d.subs, NL * SUBCAP * 4) A(d.paths, NL * d.PCAP * 5) A(d.fetch, NL * d.FCAP * FREC) A(d.groups, NL * d.GRCAP * GREC)
   A(d.tround, N) A(d.tcnt, N) A(d.tspread, N) A(d.tperiod, N) A(d.T, N * d.F) A(d.tcontact, N * d.F) A(d.slow, d.SLOWCAP) A(d.slow_n, 1) A(d.rp, d.RPCAP) A(d.rp_n, 1) A(d.start_tick, N) A(d.jseed_n, N) A(d.jseeds, 16 * N) A(d.md_uidx, N) A(d.mcfg, 4 * N) A(d.md_ver, NL * MDU) A(d.churn_q, 2ull * d.churn) A(d.ucnt, N) A(d.cin, N * d.F) A(d.HB, (uint64_t)d.QW * N) A(d.WB, (uint64_t)d.QW * N) A(d.cev, N * d.F * CEVW)
@@ -813,7 +814,10 @@ int build(swim_handle* h) {
   if (!d.implicit && !getenv("SWIM_NO_K8")) {
     size_t fr = 0, tot = 0;
     HIPCK(hipMemGetInfo(&fr, &tot));
-    if ((uint64_t)fr > NV * d.NS8 + (4ull << 30)) A(d.rowk8, NV * d.NS8)
+    if ((uint64_t)fr > NV * d.NS8 + (4ull << 30)) {
+      A(d.rowk8, NV * d.NS8)
+      if (d.W > 1) A(d.base_row8, d.NS8)
+    }
   }
 #undef A
   HIPCK(hipMemsetAsync(d.S, 0, (size_t)d.SLOTS * N * 2, h->stream));

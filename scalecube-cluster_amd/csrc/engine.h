@@ -384,6 +384,7 @@ struct Dev {
                        // that differs from base_row (conservative: never cleared); a payload ships exactly these
   uint64_t* arena_dirty[2];  // [ARENA_ROWS][MW] the sender's rdirty at copy-on-write time
   uint32_t* base_row;  // [NS] baseline key plane: a remote SYNC payload ships only its chunks that differ
+  uint8_t* base_row8;  // [NS8] with rowk8: base_row's 8-bit shadow (narrow items of peers' payloads)
   uint32_t* xn;        // [8] 0 new slots, 1 round records, 2 sweeps, 4 inbound msgs (mtmp), 5 rx payloads
   uint32_t* ns_rec;    // [NSCAP][NSW] gossips created on this shard this tick
   uint32_t* rr_rec;    // [RRCAP][RRW] gossip rounds of this shard's members this tick

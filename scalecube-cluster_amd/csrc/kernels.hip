@@ -116,9 +116,12 @@ __global__ void k_init_slots(Dev d) {
 }
 
 // the SYNC baseline row (record keys): what a PRECONVERGED row starts as, an empty row for a cold join
+// (and its 8-bit shadow, what a narrow item reads for a peer's payload chunk that was not shipped)
 __global__ void k_init_base(Dev d) {
   uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s < d.NS) d.base_row[s] = (s < d.N && d.init_mode == 1) ? key32(rec_key(ST_ALIVE, 0)) : 0u;
+  const uint32_t v = (s < d.N && d.init_mode == 1) ? key32(rec_key(ST_ALIVE, 0)) : 0u;
+  if (s < d.NS) d.base_row[s] = v;
+  if (d.base_row8 && s < d.NS8) d.base_row8[s] = key8(v);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -322,6 +325,24 @@ __device__ __forceinline__ uint32_t desc_pay(const SyncMsg& mm) {
   return mm.pin == NEVER ? NEVER : DESC_PIN | mm.pin;  // the live row (pinned: copied into the arena as it streams)
 }
 
+// a peer's payload (PAY_RX | rx index): was chunk c shipped (it differs from the baseline row)?
+__device__ __forceinline__ bool rx_shipped(const Dev& d, uint32_t pay, uint32_t c) {
+  const uint64_t* mk = d.rx_mask + (size_t)(pay & ~PAY_RX) * d.MW;
+  return (mk[c >> 6] >> (c & 63)) & 1ull;
+}
+// the 4-B payload keys from subject s on (within one chunk) of the entry's payload: the local sender's row, or a peer's
+// shipped chunk, or the baseline row
+template <bool SHARDED>
+__device__ __forceinline__ const uint32_t* pay_keys(const Dev& d, const uint4& D, uint32_t s) {
+  if (!SHARDED || D.w == NEVER) return d.rowk + lidx(d, D.y) * d.NS + s;
+  const uint32_t ri = D.w & ~PAY_RX, c = s / CH;
+  const uint64_t* mk = d.rx_mask + (size_t)ri * d.MW;
+  if (!((mk[c >> 6] >> (c & 63)) & 1ull)) return d.base_row + s;
+  uint32_t rank = __popcll(mk[c >> 6] & ((1ull << (c & 63)) - 1ull));
+  for (uint32_t q = 0; q < (c >> 6); ++q) rank += __popcll(mk[q]);
+  return (const uint32_t*)(d.xa_recv + d.rx_off[ri]) + (size_t)rank * CH + s % CH;
+}
+
 // this lane's keys of the item's chunk c: narrow (an entry of the narrow list: an unpinned live-row payload of a local
 // sender):
 // the item is chunks c .. c + 3 of the message, lane i the 32 subjects c CH + 32 i ..., and x holds their 8-bit
@@ -335,14 +356,21 @@ __device__ __forceinline__ void diff_fetch(const Dev& d, uint32_t b, const uint4
                                            uint32_t& pinw, bool& narrow, bool narrow_item) {
   pinw = NEVER;
   narrow = false;
-  if (!SHARDED && narrow_item) {
+  if (narrow_item) {
     narrow = true;
     const uint32_t n0 = c * CH + threadIdx.x * 32;  // NS8 is a multiple of 16: 16-subject groups wholly in or out
-    const uint8_t* p8 = d.rowk8 + lidx(d, D.y) * d.NS8 + n0;
+    // the payload: the local sender's row, or (a peer's payload) the baseline row's shadow for a chunk that was not
+    // shipped; a shipped chunk has no shadow: its lanes read as escaped (0xFF) and diff_wave8 compares its u32 keys
+    const uint8_t* p8 = nullptr;
+    if (!SHARDED || D.w == NEVER) {
+      p8 = d.rowk8 + lidx(d, D.y) * d.NS8 + n0;
+    } else if (n0 < d.NS8 && !rx_shipped(d, D.w, n0 / CH)) {
+      p8 = d.base_row8 + n0;
+    }
     const uint8_t* r8 = d.rowk8 + lidx(d, D.z) * d.NS8 + n0;
-    const uint4 z = make_uint4(0, 0, 0, 0);
-    x[0] = n0 < d.NS8 ? ld_c4((const uint32_t*)p8) : z;
-    x[1] = n0 + 16 < d.NS8 ? ld_c4((const uint32_t*)(p8 + 16)) : z;
+    const uint4 z = make_uint4(0, 0, 0, 0), e = make_uint4(~0u, ~0u, ~0u, ~0u);
+    x[0] = n0 < d.NS8 ? (p8 ? ld_c4((const uint32_t*)p8) : e) : z;
+    x[1] = n0 + 16 < d.NS8 ? (p8 ? ld_c4((const uint32_t*)(p8 + 16)) : e) : z;
     x[2] = n0 < d.NS8 ? ld_c4((const uint32_t*)r8) : z;
     x[3] = n0 + 16 < d.NS8 ? ld_c4((const uint32_t*)(r8 + 16)) : z;
     return;
@@ -442,8 +470,9 @@ __device__ __forceinline__ void diff_chunk(const Dev& d, uint32_t b, uint32_t mi
 // 2c + 2w (lanes 0-31) and 2c + 2w + 1 (lanes 32-63), 32 subjects per lane from x), tested, scanned and written by the
 // wave alone: no block barrier. A lane with an escaped shadow (0xFF: an incarnation past 62 among its subjects)
 // compares its 32 full keys of both rows.
-__device__ __forceinline__ void diff_wave8(const Dev& d, uint32_t b, uint32_t mi, uint32_t src, uint32_t dst, uint32_t c,
-                                           const uint4 (&x)[4]) {
+template <bool SHARDED>
+__device__ __forceinline__ void diff_wave8(const Dev& d, uint32_t b, const uint4& D, uint32_t c, const uint4 (&x)[4]) {
+  const uint32_t mi = D.x;
   const bool dl = d.ackres != 0;
   const uint32_t lane = threadIdx.x & 63u, seg = 2 * c + 2 * (threadIdx.x >> 6) + (lane >> 5);
   const uint32_t n0 = c * CH + threadIdx.x * 32;  // = seg * MCH + (lane & 31) * 32
@@ -456,8 +485,8 @@ __device__ __forceinline__ void diff_wave8(const Dev& d, uint32_t b, uint32_t mi
   uint32_t mask = 0, ab = 0;
   const uint32_t *pk = nullptr, *rk = nullptr;
   if (esc) {  // (rare) the 32 subjects' 4-B keys, one at a time
-    pk = d.rowk + lidx(d, src) * d.NS + n0;
-    rk = d.rowk + lidx(d, dst) * d.NS + n0;
+    pk = pay_keys<SHARDED>(d, D, n0);  // (32 subjects: within one chunk)
+    rk = d.rowk + lidx(d, D.z) * d.NS + n0;
 #pragma unroll 1
     for (uint32_t j = 0; j < 32; ++j) {
       const uint32_t p = n0 + j < d.NS ? pk[j] : 0u, r = n0 + j < d.NS ? rk[j] : 0u;
@@ -577,6 +606,7 @@ __device__ __forceinline__ void stream_wide(const Dev& d, uint32_t b, const uint
   }
 }
 
+template <bool SHARDED>
 __device__ __forceinline__ void stream_narrow(const Dev& d, uint32_t b, const uint4* lst, uint32_t n, uint32_t blk,
                                               uint32_t nblk) {
   constexpr uint32_t PER = 4;
@@ -586,15 +616,15 @@ __device__ __forceinline__ void stream_narrow(const Dev& d, uint32_t b, const ui
   bool nr;
   if (blk < total) {
     dc = uni(lst[blk / nit]);
-    diff_fetch<false>(d, b, dc, (blk % nit) * PER, cur, pw, nr, true);
+    diff_fetch<SHARDED>(d, b, dc, (blk % nit) * PER, cur, pw, nr, true);
   }
   if (blk + nblk < total) dn = lst[(blk + nblk) / nit];
   for (uint32_t w = blk; w < total; w += nblk) {
     uint4 nxt[4], dnn = make_uint4(0, 0, 0, 0);
     const uint4 du = uni(dn);
-    if (w + nblk < total) diff_fetch<false>(d, b, du, ((w + nblk) % nit) * PER, nxt, pw, nr, true);
+    if (w + nblk < total) diff_fetch<SHARDED>(d, b, du, ((w + nblk) % nit) * PER, nxt, pw, nr, true);
     if (w + 2 * nblk < total) dnn = lst[(w + 2 * nblk) / nit];
-    diff_wave8(d, b, dc.x, dc.y, dc.z, (w % nit) * PER, cur);
+    diff_wave8<SHARDED>(d, b, dc, (w % nit) * PER, cur);
 #pragma unroll
     for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
     dc = du;
@@ -631,7 +661,7 @@ __global__ void __launch_bounds__(256, DIFF_WAVES) k_sync_diff(const Dev* __rest
   }
   const uint32_t nblk = gridDim.x, wtot = nwide * d.NCHUNK;
   stream_wide<SHARDED>(d, b, dl ? (const uint4*)d.dlist_w : nullptr, nwide, blockIdx.x, nblk, scan, base, timed);
-  if (nnar) stream_narrow(d, b, (const uint4*)d.dlist, nnar, (blockIdx.x + nblk - wtot % nblk) % nblk, nblk);
+  if (nnar) stream_narrow<SHARDED>(d, b, (const uint4*)d.dlist, nnar, (blockIdx.x + nblk - wtot % nblk) % nblk, nblk);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -768,7 +798,7 @@ __global__ void __launch_bounds__(512) k_ack_resolve(ResArgs d, uint32_t k, uint
         const SyncMsg& mm = d.msgs[i];
         const uint32_t pw = desc_pay(mm);
         const uint4 e = make_uint4(i, mm.src, mm.dst, pw);
-        if (d.k8 && pw == NEVER)  // (on a row shard: a local sender's row)
+        if (d.k8 && (pw == NEVER || (d.W > 1 && pw != DESC_DEFER && (pw & PAY_RX) && !(pw & DESC_PIN))))
           slist[atomicAdd(&nstream, 1u)] = e;
         else
           wlist[atomicAdd(&nwide, 1u)] = e;
@@ -904,7 +934,7 @@ void launch_init(const Dev& d, void* stream) {
   hipLaunchKernelGGL(k_init_rows, dim3(4096), dim3(256), 0, st, d);
   hipLaunchKernelGGL(k_init_lists, dim3(4096), dim3(256), 0, st, d);
   hipLaunchKernelGGL(k_init_slots, dim3(cdiv(d.SLOTS, 256)), dim3(256), 0, st, d);
-  if (d.W > 1) hipLaunchKernelGGL(k_init_base, dim3(cdiv(d.NS, 256)), dim3(256), 0, st, d);
+  if (d.W > 1) hipLaunchKernelGGL(k_init_base, dim3(cdiv(d.NS8, 256)), dim3(256), 0, st, d);
 }
 
 // timed: this launch is bracketed by profiling events; it adds its message count to ctr[C_DIFFMSG]
