@@ -1605,7 +1605,8 @@ int swim_step(swim_handle* h, uint32_t n) {
     for (size_t i = 0; i < nw; ++i) t0 = std::min(t0, w[4 * i]), tend = std::max(tend, w[4 * i + 3]);
     std::vector<size_t> ord(nw);
     for (size_t i = 0; i < nw; ++i) ord[i] = i;
-    std::sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return w[4 * a + 3] > w[4 * b + 3]; });
+    // the waves whose bodies end last (a block's waves also wait for each other at the deferred copy-on-write)
+    std::sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return w[4 * a + 2] > w[4 * b + 2]; });
     double sst = 0, str = 0, sbd = 0, scw = 0;
     for (size_t i = 0; i < nw; ++i) {
       sst += (double)(w[4 * i] - t0), str += (double)((w[4 * i + 1] & M) - w[4 * i]);
