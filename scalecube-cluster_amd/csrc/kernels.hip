@@ -606,19 +606,20 @@ __device__ __forceinline__ void stream_wide(const Dev& d, uint32_t b, const uint
   }
 }
 
+// e0 (uniform), e1: the entries of items blk and blk + nblk, loaded by the caller before the list's length was known
+// (indices clamped to the list's capacity: an entry past the length is never used)
 template <bool SHARDED>
 __device__ __forceinline__ void stream_narrow(const Dev& d, uint32_t b, const uint4* lst, uint32_t n, uint32_t blk,
-                                              uint32_t nblk) {
+                                              uint32_t nblk, const uint4& e0, const uint4& e1) {
   constexpr uint32_t PER = 4;
   const uint32_t nit = (d.NCHUNK + PER - 1) / PER, total = n * nit;
-  uint4 cur[4], dc = make_uint4(0, 0, 0, 0), dn = dc;
+  uint4 cur[4], dc = make_uint4(0, 0, 0, 0), dn = e1;
   uint32_t pw;
   bool nr;
   if (blk < total) {
-    dc = uni(lst[blk / nit]);
+    dc = e0;
     diff_fetch<SHARDED>(d, b, dc, (blk % nit) * PER, cur, pw, nr, true);
   }
-  if (blk + nblk < total) dn = lst[(blk + nblk) / nit];
   for (uint32_t w = blk; w < total; w += nblk) {
     uint4 nxt[4], dnn = make_uint4(0, 0, 0, 0);
     const uint4 du = uni(dn);
@@ -632,8 +633,9 @@ __device__ __forceinline__ void stream_narrow(const Dev& d, uint32_t b, const ui
   }
 }
 
-// k_sync_diff: the diff of every payload streamed this tick (see diff_fetch and the stream loops above). The wide
-// items go first, on blocks 0, 1, ...; the narrow ones continue from the block after the last wide one.
+// k_sync_diff: the diff of every payload streamed this tick (see diff_fetch and the stream loops above). The narrow
+// items go first, on blocks 0, 1, ... (so a block's first entries are loaded together with the lists' lengths, not
+// after them); the wide ones continue from the block after the last narrow one.
 // DIFF_WAVES waves per SIMD; the grid is DIFF_WAVES blocks per CU, all resident (diff_grid)
 constexpr uint32_t DIFF_WAVES = 7;
 template <bool SHARDED>
@@ -648,6 +650,13 @@ __global__ void __launch_bounds__(256, DIFF_WAVES) k_sync_diff(const Dev* __rest
   // with SYNC_ACK resolution, only the messages k_ack_resolve listed (and counted); without it every message, on
   // 4-B keys
   const bool dl = d.ackres != 0;
+  // this block's first two narrow entries, issued before the lengths arrive
+  uint4 e0 = make_uint4(0, 0, 0, 0), e1 = e0;
+  if (dl) {
+    const uint32_t nit = (d.NCHUNK + 3) / 4, cap = d.MSGCAP - 1;
+    e0 = ((const uint4*)d.dlist)[min(blockIdx.x / nit, cap)];
+    e1 = ((const uint4*)d.dlist)[min((blockIdx.x + gridDim.x) / nit, cap)];
+  }
   const uint32_t nmsg = d.nmsg[b] < d.MSGCAP ? d.nmsg[b] : d.MSGCAP;
   const uint32_t nwide = dl ? *(volatile uint32_t*)d.ndlw : nmsg;
   const uint32_t nnar = dl ? *(volatile uint32_t*)d.ndl : 0u;
@@ -659,9 +668,10 @@ __global__ void __launch_bounds__(256, DIFF_WAVES) k_sync_diff(const Dev* __rest
       if (timed) atomicAdd(&d.ctr[C_DIFFWIDE], (unsigned long long)nmsg);
     }
   }
-  const uint32_t nblk = gridDim.x, wtot = nwide * d.NCHUNK;
-  stream_wide<SHARDED>(d, b, dl ? (const uint4*)d.dlist_w : nullptr, nwide, blockIdx.x, nblk, scan, base, timed);
-  if (nnar) stream_narrow<SHARDED>(d, b, (const uint4*)d.dlist, nnar, (blockIdx.x + nblk - wtot % nblk) % nblk, nblk);
+  const uint32_t nblk = gridDim.x, ntot = nnar * ((d.NCHUNK + 3) / 4);
+  if (nnar) stream_narrow<SHARDED>(d, b, (const uint4*)d.dlist, nnar, blockIdx.x, nblk, uni(e0), e1);
+  stream_wide<SHARDED>(d, b, dl ? (const uint4*)d.dlist_w : nullptr, nwide, (blockIdx.x + nblk - ntot % nblk) % nblk,
+                       nblk, scan, base, timed);
 }
 
 // ------------------------------------------------------------------------------------------------------------
