@@ -264,7 +264,7 @@ def main():
         merges = d["sync_merges"]
         diff_s = d["diff_ns"] * 1e-9
         launches = max(1, d["diff_launches"])
-        # the engine counts the key bytes its timed k_sync_diff launches compared (every 5th tick on one GPU, every
+        # the engine counts the key bytes its timed k_sync_diff launches compared (every 10th tick on one GPU, every
         # tick on a row shard): 2 x 1 B per subject for a payload streamed from the 8-bit shadow plane, 2 x 4 B for
         # the others; SYNC_ACKs resolved from write logs are not streamed, so they are not priced here
         timed_bytes = d["diff_key_bytes"]
@@ -315,7 +315,7 @@ def main():
                          "traffic": traffic_from_profiles(n) if world == 1 else None,
                          "traffic_source": "committed rocprofv3 PMC summary profiles/pmc_sync_diff_k8.json (FETCH_SIZE x 2 "
                                            "+ WRITE_SIZE per launch), not measured in this run"},
-            # the engine times a sample of the launches (every 5th tick on one GPU): average x launches per period
+            # the engine times a sample of the launches (every 10th tick on one GPU): average x launches per period
             "kernel_time_share": {"k_sync_diff": diff_s / launches * ticks_per_period * a.steps / dt},  # others: profiles/*kernel_stats*
             "whole_step_algorithmic_GBps": B / dt / 1e9,
             "whole_step_algorithmic_bytes_per_period": B / a.steps,

@@ -60,7 +60,7 @@ extern "C" {
 /* flags */
 #define SWIM_FLAG_RECORD_EVENTS 1u /* keep full event records for swim_drain_events (hashes are always kept) */
 #define SWIM_FLAG_PROFILE 2u       /* time a SAMPLE of the k_sync_diff launches with HIP events on the engine stream:
-                                      one GPU: the launches of ticks k % 5 == 0; sharded or with PROFILE_ALL: every
+                                      one GPU: the launches of ticks k % 10 == 0; sharded or with PROFILE_ALL: every
                                       launch (swim_counters diff_ns / diff_launches / diff_msgs cover the same set) */
 #define SWIM_FLAG_IMPLICIT_VIEWS 8u /* RUMOR mode: the (unchanging) tables and lists are computed, not stored; always
                                       on above 65536 members (C5: 10^6 members would need 8 TB of tables) */

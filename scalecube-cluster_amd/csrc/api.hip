@@ -1361,7 +1361,16 @@ int swim_destroy(swim_handle* h) {
   return SWIM_OK;
 }
 
-constexpr uint64_t DIFF_SAMPLE = 5;
+// W == 1 with SWIM_FLAG_PROFILE: every DIFF_SAMPLE-th tick's k_sync_diff is bracketed by events (the roofline's
+// sample); SWIM_DIFF_SAMPLE overrides it (measurements of the sampling's own cost)
+static uint64_t diff_sample() {
+  static const uint64_t v = [] {
+    const char* e = getenv("SWIM_DIFF_SAMPLE");
+    const unsigned long x = e ? strtoul(e, nullptr, 0) : 0ul;
+    return x >= 1 && x <= 1000 ? (uint64_t)x : (uint64_t)10;
+  }();
+  return v;
+}
 
 int swim_step(swim_handle* h, uint32_t n) {
   if (!h) return SWIM_EINVAL;
@@ -1395,10 +1404,11 @@ int swim_step(swim_handle* h, uint32_t n) {
     }
   uint64_t first = h->tick;
   const Dev& d = h->d;
-  // W == 1 with SWIM_FLAG_PROFILE: only every DIFF_SAMPLE-th tick's k_sync_diff is bracketed by events (each event
-  // pair costs ~6.7 us of GPU time per tick); the timed launches count their own messages (diff_msgs)
+  // W == 1 with SWIM_FLAG_PROFILE: only every diff_sample()-th tick's k_sync_diff is bracketed by events (an event
+  // pair costs GPU time of its own); the timed launches count their own messages (diff_msgs)
+  const uint64_t ds = diff_sample();
   auto timed = [&](uint64_t kk) {
-    return profile && ((h->cfg.flags & SWIM_FLAG_PROFILE_ALL) || d.W > 1 || kk % DIFF_SAMPLE == 0);
+    return profile && ((h->cfg.flags & SWIM_FLAG_PROFILE_ALL) || d.W > 1 || kk % ds == 0);
   };
   bool need_diff = true;  // W == 1: SYNC diff(k) not queued yet (it is queued with the previous tick when it can be)
   for (uint32_t i = 0; i < n;) {
