@@ -798,8 +798,8 @@ int build(swim_handle* h) {
     HIPCK(hipMemsetAsync(d.xb_rcnt, 0, 8ull * d.W, h->stream));
     HIPCK(hipHostMalloc((void**)&h->hcnt, 16ull * d.W, hipHostMallocDefault));
     A(d.xi_send, (uint64_t)d.W * XINL) A(d.xi_recv, (uint64_t)d.W * XINL)
-    A(d.xdone, d.W)
-    HIPCK(hipMemsetAsync(d.xdone, 0, 4ull * d.W, h->stream));
+    A(d.xdone, 2ull * d.W)  // [0]: peer columns done (k_pack_all), [1 + q]: blocks of column q done
+    HIPCK(hipMemsetAsync(d.xdone, 0, 8ull * d.W, h->stream));
     d.inl = h->spec.transport == SWIM_TRANSPORT_RCCL ? 1u : 0u;
     HIPCK(hipHostMalloc((void**)&h->xi_host_h, 16ull * d.W, hipHostMallocMapped | hipHostMallocCoherent));
     HIPCK(hipHostGetDevicePointer((void**)&d.xi_host, (void*)h->xi_host_h, 0));

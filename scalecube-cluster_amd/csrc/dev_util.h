@@ -433,8 +433,8 @@ __device__ __forceinline__ void tick_end(const Dev& d, uint32_t k) {
   if (t < d.W) {
     d.xa_scnt[t] = 0;
     d.xb_scnt[t] = 0;
-    d.xdone[t] = 0;
   }
+  for (uint32_t i = t; i < 2 * d.W; i += blockDim.x) d.xdone[i] = 0;
   if (t == 0) {
     uint32_t nb = (k + 1) & 1;
     d.nmsg[nb] = 0;

@@ -396,7 +396,7 @@ struct Dev {
   uint8_t *xi_send, *xi_recv;    // [W][XINL] inline all-to-all blocks
   uint32_t XI;                   // bytes per peer the inline all-to-all moves (XINL; SWIM_CAPS xinl= lowers it)
   unsigned long long* xi_host;   // host-mapped [2W]: send and receive count words of the last exchange
-  uint32_t* xdone;  // [W] finished k_pack_all blocks per peer column (the last one writes the inline block)
+  uint32_t* xdone;  // [2 W] k_pack_all: [0] peer columns done, [1 + q] blocks of column q done (the last writes q's inline block)
   uint32_t inl;     // RCCL transport: exchange A's inline blocks are written by k_pack_all
 
   // ---- slot sharding (RUMOR mode with W > 1) ----

@@ -200,21 +200,36 @@ __global__ void __launch_bounds__(256) k_pack_all(Dev d, uint32_t b, uint32_t sp
     }
   }
   }  // q != rank
-  // the block that finishes last in the whole grid writes every peer's inline all-to-all block: each count word says
-  // whether any of this shard's regions is past its inline block (then a send/recv group follows), so every peer of
-  // a speculative batch halts at the same tick; every column's count is written by then
-  if (!d.inl || !last_block(&d.xdone[0], gridDim.x * gridDim.y)) return;
+  // the last block of each peer column writes that peer's inline all-to-all block (count word, then the region's first
+  // XI - 8 bytes: every lane's loads before its stores); the last peer column to finish then marks every count word
+  // if any of this shard's regions is past its inline block (a send/recv group follows), so every peer of a
+  // speculative batch halts at the same tick. (One block of the whole grid writing every peer's block one after the
+  // other grew with W.)
+  if (!d.inl || q == d.rank || !last_block(&d.xdone[1 + q], gridDim.x)) return;
+  {
+    const unsigned long long w = d.xa_scnt[q];
+    uint64_t* idst = (uint64_t*)(d.xi_send + (size_t)q * d.XI);
+    const uint64_t nw = min((uint64_t)(w & XCNT_MASK), (uint64_t)d.XI - 8) / 8;  // regions are multiples of 8 B
+    const uint64_t* isrc = (const uint64_t*)(d.xa_send + (size_t)q * d.XA_PEER);
+    for (uint64_t i0 = 0; i0 < nw; i0 += 8 * blockDim.x) {
+      uint64_t v[8];
+#pragma unroll
+      for (uint32_t j = 0; j < 8; ++j) {
+        const uint64_t i = i0 + t + (uint64_t)j * blockDim.x;
+        v[j] = i < nw ? isrc[i] : 0ull;
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < 8; ++j) {
+        const uint64_t i = i0 + t + (uint64_t)j * blockDim.x;
+        if (i < nw) idst[1 + i] = v[j];
+      }
+    }
+    if (t == 0) idst[0] = w;
+  }
+  if (!last_block(&d.xdone[0], d.W - 1)) return;
   bool over = false;
   for (uint32_t r = 0; r < d.W; ++r) over |= r != d.rank && (d.xa_scnt[r] & XCNT_MASK) > d.XI - 8;
-  for (uint32_t p = 0; p < d.W; ++p) {
-    if (p == d.rank) continue;
-    const unsigned long long w = d.xa_scnt[p] | (over ? XFLAG_OVER : 0ull);
-    uint64_t* idst = (uint64_t*)(d.xi_send + (size_t)p * d.XI);
-    if (t == 0) idst[0] = w;
-    const uint64_t nw = min((uint64_t)(w & XCNT_MASK), (uint64_t)d.XI - 8) / 8;  // regions are multiples of 8 B
-    const uint64_t* isrc = (const uint64_t*)(d.xa_send + (size_t)p * d.XA_PEER);
-    for (uint64_t i = t; i < nw; i += blockDim.x) idst[1 + i] = isrc[i];
-  }
+  if (over && t < d.W && t != d.rank) *(uint64_t*)(d.xi_send + (size_t)t * d.XI) |= XFLAG_OVER;
 }
 
 // the assembled inbound list becomes msgs[b], which the next tick sorts and merges (one block)
