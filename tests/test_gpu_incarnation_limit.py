@@ -83,3 +83,30 @@ def test_key8_escape_boundary(oracle, engine):
         run_lockstep(o, e, 30, 10, f"bump {step + 1} across the 8-bit escape")
     o.close()
     e.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_key8_escape_sharded(oracle, engine, world):
+    """Row shards stream SYNC payloads from the 8-bit plane too: a local sender's row, and a peer's payload through the
+    baseline row's shadow, its shipped chunks (rows that differ from the baseline) as escaped lanes compared on the
+    shipped u32 keys. Movers are bumped to incarnation 61 in one tick (one gossip per call) and then across the 8-bit
+    escape, under 10 % loss and SYNCs every tick, against the oracle."""
+    from swimhip.shard import ThreadShardGroup
+    n = 96
+    cfg = SimConfig(n_members=n, cluster=ClusterConfig(syncInterval=1000), record_events=True, seed=0x8C,
+                    gossip_slot_cap=1 << 12)
+    o, e = SimulatedCluster(oracle, cfg), ThreadShardGroup(engine, cfg, world)
+    movers = (3, 32, 64, 95)
+    for c in (o, e):
+        c.set_default_loss(10)
+        for m in movers:
+            for _ in range(61):
+                c.update_incarnation(m)
+    run_lockstep(o, e, 40, 10, f"W={world}: incarnations 61")
+    for step in range(3):
+        for c in (o, e):
+            for m in movers:
+                c.update_incarnation(m)
+        run_lockstep(o, e, 30, 10, f"W={world}: bump {step + 1} across the 8-bit escape")
+    e.close()
+    o.close()
