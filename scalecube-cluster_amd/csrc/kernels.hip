@@ -307,15 +307,7 @@ __global__ void __launch_bounds__(256) k_seg_sort(uint64_t* key, uint32_t* val, 
 // shadows, key8; an escaped key is compared on its 4-B key32), 2 x 4 B for the rest. SHARDED adds payloads
 // received from other shards (baseline row + shipped chunks); the single-GPU instance has only local rows and
 // snapshots.
-// this lane's 8 payload keys and 8 receiver keys of chunk c of message mi: the payload
-// is the sender's live row or its copy-on-write snapshot; for a payload received from another shard, the shipped
-// chunk if it differs from the baseline, else the baseline
-// pinw: the arena row a live-row payload is copied into while it streams (pin_msg), else NEVER; loaded here with the
-// item's data so that no dependent load of the message waits at the top of the item's iteration
-// narrow (one GPU, a live-row payload that is not pinned): the item is chunks c .. c + 3 of the message, lane i
-// the 32 subjects c CH + 32 i ..., and x holds their 8-bit shadow keys (key8): payload x[0..1], receiver x[2..3],
-// the same 64 B per lane in flight as one chunk of 4-B keys. Every lane of the block takes the same item, so the mode
-// is uniform.
+//
 // an item's message as k_sync_diff reads it (the 16-B entries of Dev::dlist / dlist_w, written by k_ack_resolve;
 // without a list, read from the message): x = the message index, y = sender, z = receiver, w = where the payload is
 // (desc_pay)
@@ -343,10 +335,10 @@ __device__ __forceinline__ const uint32_t* pay_keys(const Dev& d, const uint4& D
   return (const uint32_t*)(d.xa_recv + d.rx_off[ri]) + (size_t)rank * CH + s % CH;
 }
 
-// this lane's keys of the item's chunk c: narrow (an entry of the narrow list: an unpinned live-row payload of a local
-// sender):
-// the item is chunks c .. c + 3 of the message, lane i the 32 subjects c CH + 32 i ..., and x holds their 8-bit
-// shadow keys (key8): payload x[0..1], receiver x[2..3], the same 64 B per lane in flight as one chunk of 4-B keys.
+// this lane's keys of the item's chunk c: narrow (an entry of the narrow list: a local sender's unpinned live row, or
+// on a row shard a peer's payload): the item is chunks c .. c + 3 of the message, lane i the 32 subjects c CH + 32 i
+// ..., and x holds their 8-bit shadow keys (key8): payload x[0..1], receiver x[2..3], the same 64 B per lane in
+// flight as one chunk of 4-B keys.
 // Otherwise 8 payload keys and 8 receiver keys of chunk c: the payload is the sender's live row or its copy-on-write
 // snapshot; for a payload received from another shard, the shipped chunk if it differs from the baseline, else the
 // baseline. pinw: the arena row a live-row payload is copied into while it streams (pin_msg), else NEVER. Every lane
@@ -385,16 +377,8 @@ __device__ __forceinline__ void diff_fetch(const Dev& d, uint32_t b, const uint4
   if (D.w == NEVER || (D.w & DESC_PIN)) {
     pinw = D.w == NEVER ? NEVER : D.w & ~DESC_PIN;
     p8 = d.rowk + lidx(d, D.y) * d.NS + s0;
-  } else if (SHARDED && (D.w & PAY_RX)) {
-    const uint32_t ri = D.w & ~PAY_RX;
-    const uint64_t* mk = d.rx_mask + (size_t)ri * d.MW;
-    if ((mk[c >> 6] >> (c & 63)) & 1ull) {
-      uint32_t rank = __popcll(mk[c >> 6] & ((1ull << (c & 63)) - 1ull));
-      for (uint32_t q = 0; q < (c >> 6); ++q) rank += __popcll(mk[q]);
-      p8 = (const uint32_t*)(d.xa_recv + d.rx_off[ri]) + (size_t)rank * CH + threadIdx.x * 8;
-    } else {
-      p8 = d.base_row + s0;
-    }
+  } else if (SHARDED && (D.w & PAY_RX)) {  // the shipped chunk, or the baseline row
+    p8 = pay_keys<SHARDED>(d, D, s0);
   } else {
     p8 = d.arena[b] + (size_t)D.w * d.NS + s0;
   }
